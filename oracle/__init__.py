@@ -1,0 +1,257 @@
+"""ctypes binding of the CPU oracle -- TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import this
+module.  It is the checker, never the product: aeon_amd/ does not import it.
+See aeon_oracle.h for what is restated and which reference lines each part follows.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liboracle.so")
+
+
+class AugConfig(ctypes.Structure):
+    _fields_ = [
+        ("scale_min", ctypes.c_float), ("scale_max", ctypes.c_float),
+        ("angle_min", ctypes.c_int), ("angle_max", ctypes.c_int),
+        ("lighting_mean", ctypes.c_float), ("lighting_stddev", ctypes.c_float),
+        ("hdist_min", ctypes.c_float), ("hdist_max", ctypes.c_float),
+        ("contrast_min", ctypes.c_float), ("contrast_max", ctypes.c_float),
+        ("brightness_min", ctypes.c_float), ("brightness_max", ctypes.c_float),
+        ("saturation_min", ctypes.c_float), ("saturation_max", ctypes.c_float),
+        ("hue_min", ctypes.c_int), ("hue_max", ctypes.c_int),
+        ("flip_enable", ctypes.c_int), ("center", ctypes.c_int),
+        ("crop_enable", ctypes.c_int), ("do_area_scale", ctypes.c_int),
+        ("resize_short_size", ctypes.c_int), ("padding", ctypes.c_int),
+        ("fixed_scaling_factor", ctypes.c_float),
+        ("interp", ctypes.c_int),
+    ]
+
+
+class Params(ctypes.Structure):
+    _fields_ = [
+        ("crop_x", ctypes.c_int), ("crop_y", ctypes.c_int),
+        ("crop_w", ctypes.c_int), ("crop_h", ctypes.c_int),
+        ("resize_short_size", ctypes.c_int),
+        ("out_w", ctypes.c_int), ("out_h", ctypes.c_int),
+        ("angle", ctypes.c_int), ("flip", ctypes.c_int), ("padding", ctypes.c_int),
+        ("pad_off_x", ctypes.c_int), ("pad_off_y", ctypes.c_int),
+        ("n_lighting", ctypes.c_int), ("lighting", ctypes.c_float * 3),
+        ("color_noise_std", ctypes.c_float),
+        ("contrast", ctypes.c_float), ("brightness", ctypes.c_float),
+        ("saturation", ctypes.c_float), ("hue", ctypes.c_int),
+        ("interp", ctypes.c_int),
+    ]
+
+    def as_dict(self):
+        d = {f: getattr(self, f) for f, _ in self._fields_}
+        d["lighting"] = list(self.lighting)
+        return d
+
+
+class LoadConfig(ctypes.Structure):
+    _fields_ = [
+        ("channels", ctypes.c_int), ("channel_major", ctypes.c_int),
+        ("bgr_to_rgb", ctypes.c_int), ("out_dtype", ctypes.c_int),
+        ("has_mean", ctypes.c_int),
+        ("mean", ctypes.c_double * 3), ("stddev", ctypes.c_double * 3),
+    ]
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", HERE])
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        P = ctypes.POINTER
+        L.orc_factory_create.restype = ctypes.c_void_p
+        L.orc_factory_create.argtypes = [P(AugConfig)]
+        L.orc_factory_destroy.argtypes = [ctypes.c_void_p]
+        L.orc_make_params.argtypes = [ctypes.c_void_p, P(ctypes.c_uint32), ctypes.c_int, ctypes.c_int,
+                                      ctypes.c_int, ctypes.c_int, P(Params)]
+        L.orc_seed_slots.argtypes = [ctypes.c_uint32, ctypes.c_int, P(ctypes.c_uint32)]
+        L.orc_transform_image.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                          ctypes.c_int, P(Params), ctypes.c_void_p]
+        L.orc_load_image.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, P(LoadConfig),
+                                     ctypes.c_void_p]
+        L.orc_transform_mask.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                         P(Params), ctypes.c_void_p]
+        for fn in (L.orc_resize_linear, L.orc_resize_nearest):
+            fn.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                           ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+        L.orc_cbsjitter.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_float,
+                                    ctypes.c_float, ctypes.c_float, ctypes.c_int]
+        L.orc_lighting.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, P(ctypes.c_float),
+                                   ctypes.c_int, ctypes.c_float]
+        L.orc_standardize_value.restype = ctypes.c_float
+        L.orc_standardize_value.argtypes = [ctypes.c_int, ctypes.c_double, ctypes.c_double]
+        L.orc_batch_augment.restype = ctypes.c_double
+        L.orc_batch_augment.argtypes = [ctypes.c_int, P(ctypes.c_void_p), P(ctypes.c_int),
+                                        P(ctypes.c_int), P(Params), P(LoadConfig), ctypes.c_void_p,
+                                        ctypes.c_size_t, ctypes.c_int]
+        L.orc_last_error.restype = ctypes.c_char_p
+        _lib = L
+    return _lib
+
+
+def _check(rc):
+    if rc != 0:
+        raise RuntimeError("oracle: " + lib().orc_last_error().decode())
+
+
+def aug_config(**kw):
+    """AugConfig with aeon's param_factory defaults (augment_image.hpp:141-204)."""
+    c = AugConfig(scale_min=1.0, scale_max=1.0, angle_min=0, angle_max=0,
+                  lighting_mean=0.0, lighting_stddev=0.0, hdist_min=1.0, hdist_max=1.0,
+                  contrast_min=1.0, contrast_max=1.0, brightness_min=1.0, brightness_max=1.0,
+                  saturation_min=1.0, saturation_max=1.0, hue_min=0, hue_max=0,
+                  flip_enable=0, center=1, crop_enable=1, do_area_scale=0,
+                  resize_short_size=0, padding=0, fixed_scaling_factor=-1.0, interp=0)
+    for k, v in kw.items():
+        setattr(c, k, v)
+    return c
+
+
+class Factory:
+    def __init__(self, cfg):
+        self._f = lib().orc_factory_create(ctypes.byref(cfg))
+
+    def __del__(self):
+        if getattr(self, "_f", None):
+            lib().orc_factory_destroy(self._f)
+            self._f = None
+
+    def make_params(self, state, in_w, in_h, out_w, out_h):
+        """state: 1-element np.uint32 array (the slot's engine state, updated in place)."""
+        p = Params()
+        st = ctypes.c_uint32(int(state[0]))
+        _check(lib().orc_make_params(self._f, ctypes.byref(st), in_w, in_h, out_w, out_h,
+                                     ctypes.byref(p)))
+        state[0] = st.value
+        return p
+
+
+def seed_slots(seed, n):
+    out = np.zeros(n, np.uint32)
+    lib().orc_seed_slots(seed, n, out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)))
+    return out
+
+
+def params(**kw):
+    p = Params(interp=0, contrast=1.0, brightness=1.0, saturation=1.0)
+    for k, v in kw.items():
+        if k == "lighting":
+            p.n_lighting = len(v)
+            for i, x in enumerate(v):
+                p.lighting[i] = x
+        else:
+            setattr(p, k, v)
+    return p
+
+
+def transform_image(src, p):
+    src = np.ascontiguousarray(src, dtype=np.uint8)
+    h, w = src.shape[:2]
+    cn = 1 if src.ndim == 2 else src.shape[2]
+    out = np.zeros((p.out_h, p.out_w, cn), np.uint8)
+    _check(lib().orc_transform_image(src.ctypes.data, w, h, cn, w * cn, ctypes.byref(p),
+                                     out.ctypes.data))
+    return out
+
+
+def load_config(channels=3, channel_major=True, bgr_to_rgb=False, out_dtype="float32",
+                mean=None, stddev=None):
+    lc = LoadConfig(channels=channels, channel_major=int(channel_major), bgr_to_rgb=int(bgr_to_rgb),
+                    out_dtype=0 if out_dtype == "uint8" else 1, has_mean=0)
+    if mean is not None:
+        lc.has_mean = 1
+        for i in range(channels):
+            lc.mean[i] = mean[i]
+            lc.stddev[i] = stddev[i]
+    return lc
+
+
+def load_image(img, lc):
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    h, w = img.shape[:2]
+    dt = np.uint8 if lc.out_dtype == 0 else np.float32
+    shape = (lc.channels, h, w) if lc.channel_major else (h, w, lc.channels)
+    out = np.zeros(shape, dt)
+    _check(lib().orc_load_image(img.ctypes.data, w, h, ctypes.byref(lc), out.ctypes.data))
+    return out
+
+
+def transform_mask(src, p):
+    src = np.ascontiguousarray(src, dtype=np.uint8)
+    h, w = src.shape[:2]
+    out = np.zeros((p.out_h, p.out_w), np.uint8)
+    _check(lib().orc_transform_mask(src.ctypes.data, w, h, w, ctypes.byref(p), out.ctypes.data))
+    return out
+
+
+def resize_linear(src, dw, dh):
+    src = np.ascontiguousarray(src, dtype=np.uint8)
+    h, w = src.shape[:2]
+    cn = 1 if src.ndim == 2 else src.shape[2]
+    out = np.zeros((dh, dw, cn), np.uint8)
+    _check(lib().orc_resize_linear(src.ctypes.data, w, h, w * cn, cn, out.ctypes.data, dw, dh))
+    return out
+
+
+def resize_nearest(src, dw, dh):
+    src = np.ascontiguousarray(src, dtype=np.uint8)
+    h, w = src.shape[:2]
+    cn = 1 if src.ndim == 2 else src.shape[2]
+    out = np.zeros((dh, dw, cn), np.uint8)
+    _check(lib().orc_resize_nearest(src.ctypes.data, w, h, w * cn, cn, out.ctypes.data, dw, dh))
+    return out
+
+
+def cbsjitter(img, contrast=1.0, brightness=1.0, saturation=1.0, hue=0):
+    img = np.ascontiguousarray(img, dtype=np.uint8).copy()
+    h, w = img.shape[:2]
+    lib().orc_cbsjitter(img.ctypes.data, w, h, contrast, brightness, saturation, hue)
+    return img
+
+
+def lighting(img, alphas, sigma):
+    img = np.ascontiguousarray(img, dtype=np.uint8).copy()
+    h, w = img.shape[:2]
+    a = (ctypes.c_float * 3)(*alphas)
+    lib().orc_lighting(img.ctypes.data, w, h, a, len(alphas), sigma)
+    return img
+
+
+def augment_record(src, p, lc):
+    """transform_single_image + loader::load for one record."""
+    return load_image(transform_image(src, p), lc)
+
+
+def batch_augment(srcs, params_list, lc, item_shape, threads):
+    """CPU-baseline batch on `threads` pool workers; returns (outputs, seconds)."""
+    n = len(srcs)
+    srcs = [np.ascontiguousarray(s, dtype=np.uint8) for s in srcs]
+    ptrs = (ctypes.c_void_p * n)(*[s.ctypes.data for s in srcs])
+    ws = (ctypes.c_int * n)(*[s.shape[1] for s in srcs])
+    hs = (ctypes.c_int * n)(*[s.shape[0] for s in srcs])
+    ps = (Params * n)(*params_list)
+    dt = np.uint8 if lc.out_dtype == 0 else np.float32
+    out = np.zeros((n,) + tuple(item_shape), dt)
+    item_bytes = out[0].nbytes
+    secs = lib().orc_batch_augment(n, ptrs, ws, hs, ps, ctypes.byref(lc), out.ctypes.data,
+                                   item_bytes, threads)
+    if secs < 0:
+        raise RuntimeError("oracle: " + lib().orc_last_error().decode())
+    return out, secs

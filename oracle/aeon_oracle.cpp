@@ -1,0 +1,772 @@
+// aeon_oracle.cpp -- TEST INFRASTRUCTURE ONLY (see aeon_oracle.h).
+//
+// A from-scratch CPU restatement of aeon's image path with the OpenCV-2.4 (SSE2 build)
+// arithmetic it inherits.  Every function names the reference code it restates.
+// Built with -ffp-contract=off so float expressions round exactly like the x86 SSE2
+// reference build (no FMA contraction).
+#include "aeon_oracle.h"
+
+#include <algorithm>
+#include <atomic>
+#include <cfloat>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <random>
+#include <stdexcept>
+#include <string>
+#include <thread>
+#include <vector>
+
+namespace {
+
+thread_local std::string g_err;
+
+// ---- OpenCV scalar helpers (x86-64 SSE2: cvRound = cvtsd2si, round-half-even) ----------
+inline int cv_round(double v) { return (int)std::nearbyint(v); }
+inline int cv_roundf(float v) { return (int)std::nearbyintf(v); }
+inline int cv_floor(double v) { return (int)std::floor(v); }
+inline uint8_t sat_u8(int v) { return (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v)); }
+inline int sat_s16(int v) { return v < -32768 ? -32768 : (v > 32767 ? 32767 : v); }
+inline uint8_t sat_u8f(float v) { return sat_u8(cv_roundf(v)); }
+
+// A minstd_rand0 wrapper whose state word can be read back (the LCG state == last output).
+struct Engine {
+    using result_type = std::minstd_rand0::result_type;
+    std::minstd_rand0 e;
+    result_type       last;
+    static constexpr result_type min() { return std::minstd_rand0::min(); }
+    static constexpr result_type max() { return std::minstd_rand0::max(); }
+    explicit Engine(uint32_t s) : e(s), last(s) {}
+    result_type operator()() { return last = e(); }
+};
+
+// ---- augment::image::param_factory (src/augment_image.cpp:28-89, .hpp:141-204) --------------
+struct Factory {
+    orc_aug_config                        c;
+    std::uniform_real_distribution<float> scale, hdist, contrast, brightness, saturation;
+    std::uniform_real_distribution<float> crop_offset{0.5f, 0.5f};
+    std::uniform_int_distribution<int>    angle, hue;
+    std::uniform_int_distribution<int>    pad_offset{0, 0};
+    std::normal_distribution<float>       lighting;
+    std::bernoulli_distribution           flip{0};
+
+    explicit Factory(const orc_aug_config& cfg)
+        : c(cfg)
+        , scale{cfg.scale_min, cfg.scale_max}
+        , hdist{cfg.hdist_min, cfg.hdist_max}
+        , contrast{cfg.contrast_min, cfg.contrast_max}
+        , brightness{cfg.brightness_min, cfg.brightness_max}
+        , saturation{cfg.saturation_min, cfg.saturation_max}
+        , angle{cfg.angle_min, cfg.angle_max}
+        , hue{cfg.hue_min, cfg.hue_max}
+        , lighting{cfg.lighting_mean, cfg.lighting_stddev}
+    {
+        if (cfg.flip_enable) flip = std::bernoulli_distribution{0.5};
+        if (!cfg.center) crop_offset = std::uniform_real_distribution<float>{0.0f, 1.0f};
+        if (cfg.padding > 0) pad_offset = std::uniform_int_distribution<int>(0, cfg.padding * 2);
+    }
+};
+
+// src/util.cpp:212-239
+int unbiased_round(float x)
+{
+    float i;
+    float frac = std::modf(x, &i);
+    int   ip   = int(i);
+    int   rc;
+    if (std::fabs(frac) == 0.5f) {
+        if (ip % 2 == 0) rc = ip;
+        else {
+            rc = std::fabs(x) + 0.5;
+            rc = x < 0.0 ? -rc : rc;
+        }
+    } else {
+        rc = std::floor(std::fabs(x) + 0.5);
+        rc = x < 0.0 ? -rc : rc;
+    }
+    return rc;
+}
+
+// image.cpp:108-116 get_resized_short_size
+void resized_short_size(int in_w, int in_h, int target, int* ow, int* oh)
+{
+    float pct = static_cast<float>(target) / (float)std::min(in_h, in_w);
+    *ow = static_cast<int>(std::round((float)in_w * pct));
+    *oh = static_cast<int>(std::round((float)in_h * pct));
+}
+
+// image.cpp:214-224 calculate_scale (cv::Size int input)
+float calculate_scale(int w, int h, int ow, int oh)
+{
+    float im_scale = (float)ow / (float)w;
+    float rh       = (float)h * im_scale;
+    if (rh > oh) im_scale = (float)oh / (float)h;
+    return im_scale;
+}
+
+// image.cpp:226-237 cropbox_max_proportional
+void cropbox_max_proportional(float in_w, float in_h, float out_w, float out_h, float* rw, float* rh)
+{
+    float w = out_w, h = out_h;
+    float s = in_w / w;
+    w *= s;
+    h *= s;
+    if (h > in_h) {
+        s = in_h / h;
+        w *= s;
+        h *= s;
+    }
+    *rw = w;
+    *rh = h;
+}
+
+// param_factory::make_params (src/augment_image.cpp:107-230)
+void make_params(const Factory& fc, Engine& eng, int in_w, int in_h, int out_w, int out_h,
+                 orc_params* p)
+{
+    Factory&              f = const_cast<Factory&>(fc); // distributions are `mutable` in aeon
+    const orc_aug_config& c = f.c;
+    std::memset(p, 0, sizeof(*p));
+    p->out_w      = out_w;
+    p->out_h      = out_h;
+    p->angle      = f.angle(eng);
+    p->flip       = f.flip(eng) ? 1 : 0;
+    p->hue        = f.hue(eng);
+    p->contrast   = f.contrast(eng);
+    p->brightness = f.brightness(eng);
+    p->saturation = f.saturation(eng);
+    p->padding    = c.padding;
+    p->resize_short_size = c.resize_short_size;
+    p->interp            = c.interp;
+
+    float in_sw = (float)in_w, in_sh = (float)in_h; // cv::Size2f input_size
+
+    if (!c.crop_enable) {
+        int ox       = f.pad_offset(eng);
+        int oy       = f.pad_offset(eng);
+        p->pad_off_x = ox;
+        p->pad_off_y = oy;
+        p->crop_x = 0;
+        p->crop_y = 0;
+        p->crop_w = cv_roundf(in_sw);
+        p->crop_h = cv_roundf(in_sh);
+        float s   = c.fixed_scaling_factor > 0 ? c.fixed_scaling_factor
+                                               : calculate_scale(in_w, in_h, out_w, out_h);
+        in_sw *= s;
+        in_sh *= s;
+        p->out_w = unbiased_round(in_sw);
+        p->out_h = unbiased_round(in_sh);
+    } else if (c.do_area_scale) {
+        float hd = f.hdist(eng);
+        hd       = std::sqrt(hd);
+        float sw = hd, sh = 1 / hd;
+        float bound = std::min((float)in_w / (float)in_h / (sw * sw),
+                               (float)in_h / (float)in_w / (sh * sh));
+        float smax = std::min(f.scale.max(), bound);
+        float smin = std::min(f.scale.min(), bound);
+        std::uniform_real_distribution<float> scale2{smin, smax};
+        float target_area = std::sqrt((float)((size_t)in_h * (size_t)in_w) * scale2(eng));
+        sw *= target_area;
+        sh *= target_area;
+        float offx = f.crop_offset(eng);
+        float offy = f.crop_offset(eng);
+        p->crop_x  = (int)((in_sw - sw) * offx);
+        p->crop_y  = (int)((in_sh - sh) * offy);
+        p->crop_w  = cv_roundf(sw);
+        p->crop_h  = cv_roundf(sh);
+    } else {
+        if (c.padding > 0) {
+            throw std::invalid_argument("crop_enable should not be true: when padding is defined");
+        }
+        float image_scale = f.scale(eng);
+        float hd          = f.hdist(eng);
+        float osw = (float)out_w * hd, osh = (float)out_h;
+        if (c.resize_short_size > 0) {
+            int rw, rh;
+            resized_short_size(in_w, in_h, c.resize_short_size, &rw, &rh);
+            in_sw = (float)rw;
+            in_sh = (float)rh;
+        }
+        float cw, ch;
+        cropbox_max_proportional(in_sw, in_sh, osw, osh, &cw, &ch);
+        cw *= image_scale; // cropbox_linear_scale (image.cpp:239-242)
+        ch *= image_scale;
+        float offx = f.crop_offset(eng);
+        float offy = f.crop_offset(eng);
+        p->crop_x  = (int)((in_sw - cw) * offx); // cropbox_shift truncates (image.cpp:263-273)
+        p->crop_y  = (int)((in_sh - ch) * offy);
+        p->crop_w  = cv_roundf(cw);             // cv::Rect(Point2i, Size2f): saturate_cast
+        p->crop_h  = cv_roundf(ch);
+    }
+
+    if (f.lighting.stddev() != 0) {
+        for (int i = 0; i < 3; i++) p->lighting[i] = f.lighting(eng);
+        p->n_lighting      = 3;
+        p->color_noise_std = f.lighting.stddev();
+    }
+}
+
+// ---- a light u8 image view ------------------------------------------------------------------
+struct Img {
+    int                  w = 0, h = 0, cn = 0, stride = 0;
+    const uint8_t*       data = nullptr;
+    std::vector<uint8_t> own;
+    uint8_t*       row(int y) { return const_cast<uint8_t*>(data) + (size_t)y * stride; }
+    const uint8_t* row(int y) const { return data + (size_t)y * stride; }
+    static Img alloc(int w, int h, int cn)
+    {
+        Img r;
+        r.w = w, r.h = h, r.cn = cn, r.stride = w * cn;
+        r.own.assign((size_t)w * h * cn, 0);
+        r.data = r.own.data();
+        return r;
+    }
+    static Img view(const uint8_t* d, int w, int h, int cn, int stride)
+    {
+        Img r;
+        r.w = w, r.h = h, r.cn = cn, r.stride = stride, r.data = d;
+        return r;
+    }
+    Img clone() const
+    {
+        Img r = alloc(w, h, cn);
+        for (int y = 0; y < h; y++) std::memcpy(r.row(y), row(y), (size_t)w * cn);
+        return r;
+    }
+};
+
+// ---- cv::resize INTER_LINEAR, 8U (OpenCV 2.4 imgwarp.cpp resize / resizeGeneric_ /
+//      HResizeLinear / VResizeLinear + VResizeLinearVec_32s8u, ResizeAreaFastVec) ----------------
+void resize_linear(const Img& s, Img& d)
+{
+    const int sw = s.w, sh = s.h, cn = s.cn, dw = d.w, dh = d.h;
+    if (sw == dw && sh == dh) {
+        for (int y = 0; y < sh; y++) std::memcpy(d.row(y), s.row(y), (size_t)sw * cn);
+        return;
+    }
+    double inv_sx = (double)dw / sw, inv_sy = (double)dh / sh;
+    double scale_x = 1. / inv_sx, scale_y = 1. / inv_sy;
+    int    isx = cv_round(scale_x), isy = cv_round(scale_y);
+    bool   area_fast = std::abs(scale_x - isx) < DBL_EPSILON && std::abs(scale_y - isy) < DBL_EPSILON;
+    if (area_fast && isx == 2 && isy == 2 && (cn == 1 || cn == 3 || cn == 4)) {
+        // INTER_LINEAR at exactly 2x is routed to INTER_AREA's fast path (resizeAreaFast_).
+        for (int dy = 0; dy < dh; dy++) {
+            const uint8_t* S0 = s.row(2 * dy);
+            const uint8_t* S1 = s.row(2 * dy + 1);
+            uint8_t*       D  = d.row(dy);
+            for (int dx = 0; dx < dw * cn; dx++) {
+                int px = dx / cn, k = dx % cn, i = px * 2 * cn + k;
+                D[dx]  = (uint8_t)((S0[i] + S0[i + cn] + S1[i] + S1[i + cn] + 2) >> 2);
+            }
+        }
+        return;
+    }
+
+    const int        W = dw * cn;
+    std::vector<int> xofs(W), a0(W), a1(W);
+    int              xmax = dw;
+    for (int dx = 0; dx < dw; dx++) {
+        float fx = (float)((dx + 0.5) * scale_x - 0.5);
+        int   sx = cv_floor(fx);
+        fx -= sx;
+        if (sx < 0) fx = 0, sx = 0;
+        if (sx + 1 >= sw) {
+            xmax = std::min(xmax, dx);
+            if (sx >= sw - 1) fx = 0, sx = sw - 1;
+        }
+        int c0 = sat_s16(cv_roundf((1.f - fx) * 2048)), c1 = sat_s16(cv_roundf(fx * 2048));
+        for (int k = 0; k < cn; k++) {
+            xofs[dx * cn + k] = sx * cn + k;
+            a0[dx * cn + k]   = c0;
+            a1[dx * cn + k]   = c1;
+        }
+    }
+    const int xmax_e = xmax * cn;
+    // SIMD / scalar split of VResizeLinearVec_32s8u: 16-wide while x <= W-16, then 4-wide
+    // while x < W-4; the remaining elements use the scalar FixedPtCast formula.
+    int xv = 0;
+    if (W >= 16) xv = (W / 16) * 16;
+    while (xv < W - 4) xv += 4;
+
+    std::vector<int> H0(W), H1(W);
+    auto hrow = [&](const uint8_t* S, std::vector<int>& H) {
+        for (int x = 0; x < W; x++) {
+            int sx = xofs[x];
+            H[x]   = x < xmax_e ? S[sx] * a0[x] + S[sx + cn] * a1[x] : S[sx] * 2048;
+        }
+    };
+    for (int dy = 0; dy < dh; dy++) {
+        float fy = (float)((dy + 0.5) * scale_y - 0.5);
+        int   sy = cv_floor(fy);
+        fy -= sy;
+        int b0 = sat_s16(cv_roundf((1.f - fy) * 2048)), b1 = sat_s16(cv_roundf(fy * 2048));
+        int r0 = std::min(std::max(sy, 0), sh - 1), r1 = std::min(std::max(sy + 1, 0), sh - 1);
+        hrow(s.row(r0), H0);
+        hrow(s.row(r1), H1);
+        uint8_t* D = d.row(dy);
+        for (int x = 0; x < W; x++) {
+            if (x < xv) {
+                int h0 = sat_s16(H0[x] >> 4), h1 = sat_s16(H1[x] >> 4);
+                int m  = sat_s16(((h0 * (int)(short)b0) >> 16) + ((h1 * (int)(short)b1) >> 16));
+                int v  = sat_s16(m + 2) >> 2;
+                D[x]   = sat_u8(v);
+            } else {
+                D[x] = sat_u8((H0[x] * b0 + H1[x] * b1 + (1 << 21)) >> 22);
+            }
+        }
+    }
+}
+
+// cv::resize INTER_NEAREST (resizeNN)
+void resize_nearest(const Img& s, Img& d)
+{
+    double fx = (double)d.w / s.w, fy = (double)d.h / s.h;
+    double ifx = 1. / fx, ify = 1. / fy;
+    for (int y = 0; y < d.h; y++) {
+        int            sy = std::min(cv_floor(y * ify), s.h - 1);
+        const uint8_t* S  = s.row(sy);
+        uint8_t*       D  = d.row(y);
+        for (int x = 0; x < d.w; x++) {
+            int sx = std::min(cv_floor(x * ifx), s.w - 1);
+            for (int k = 0; k < s.cn; k++) D[x * s.cn + k] = S[sx * s.cn + k];
+        }
+    }
+}
+
+// image::resize (image.cpp:93-106): identity when the size already matches.
+void resize_any(const Img& s, Img& d, int interp)
+{
+    if (s.w == d.w && s.h == d.h) {
+        for (int y = 0; y < s.h; y++) std::memcpy(d.row(y), s.row(y), (size_t)s.w * s.cn);
+        return;
+    }
+    if (interp == 1) resize_nearest(s, d);
+    else resize_linear(s, d);
+}
+
+// ---- photometric::cbsjitter (src/image.cpp:358-406) -----------------------------------------
+void bs_transform(Img& m, float brightness, float saturation)
+{
+    // satmtx = brightness * (saturation*I + (1-saturation)*ones(3,1)*GSCL^T)   (MatExpr, float)
+    const float g[3] = {0.0820f, 0.6094f, 0.3086f};
+    float       A[3][3], B[3][3], M[3][3];
+    float       oms = 1 - saturation;
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) {
+            A[i][j] = i == j ? saturation : 0.f;
+            B[i][j] = (float)((double)oms * (double)g[j]);
+        }
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) {
+            if (brightness == 1.0f) M[i][j] = A[i][j] + B[i][j];            // cv::add
+            else M[i][j] = (float)((double)A[i][j] * brightness + (double)B[i][j] * brightness + 0.0);
+        }                                                                    // cv::addWeighted
+    bool diag = true;
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++)
+            if (i != j && std::fabs((double)M[i][j]) > FLT_EPSILON) diag = false;
+    const int n = m.w * m.h;
+    if (diag) { // diagtransform_8u: saturate_cast<uchar>(m*src + 0) in float
+        for (int y = 0; y < m.h; y++) {
+            uint8_t* p = m.row(y);
+            for (int x = 0; x < m.w; x++, p += 3) {
+                uint8_t t0 = sat_u8f(M[0][0] * p[0] + 0.f);
+                uint8_t t1 = sat_u8f(M[1][1] * p[1] + 0.f);
+                uint8_t t2 = sat_u8f(M[2][2] * p[2] + 0.f);
+                p[0] = t0, p[1] = t1, p[2] = t2;
+            }
+        }
+        (void)n;
+        return;
+    }
+    const float MAX_M = 32.f;
+    bool        fixpt = true;
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++)
+            if (!(std::fabs(M[i][j]) < MAX_M)) fixpt = false;
+    if (fixpt) { // transform_8u, 10-bit fixed point (SSE2 path and its scalar tail agree)
+        int q[3][3];
+        for (int i = 0; i < 3; i++)
+            for (int j = 0; j < 3; j++) q[i][j] = sat_s16(cv_roundf(M[i][j] * 1024));
+        const int r = cv_roundf((0.f + 0.5f) * 1024);
+        for (int y = 0; y < m.h; y++) {
+            uint8_t* p = m.row(y);
+            for (int x = 0; x < m.w; x++, p += 3) {
+                int v0 = p[0], v1 = p[1], v2 = p[2];
+                p[0] = sat_u8((q[0][0] * v0 + q[0][1] * v1 + q[0][2] * v2 + r) >> 10);
+                p[1] = sat_u8((q[1][0] * v0 + q[1][1] * v1 + q[1][2] * v2 + r) >> 10);
+                p[2] = sat_u8((q[2][0] * v0 + q[2][1] * v1 + q[2][2] * v2 + r) >> 10);
+            }
+        }
+    } else { // transform_<uchar,float>
+        for (int y = 0; y < m.h; y++) {
+            uint8_t* p = m.row(y);
+            for (int x = 0; x < m.w; x++, p += 3) {
+                float v0 = p[0], v1 = p[1], v2 = p[2];
+                uint8_t t0 = sat_u8f(M[0][0] * v0 + M[0][1] * v1 + M[0][2] * v2 + 0.f);
+                uint8_t t1 = sat_u8f(M[1][0] * v0 + M[1][1] * v1 + M[1][2] * v2 + 0.f);
+                uint8_t t2 = sat_u8f(M[2][0] * v0 + M[2][1] * v1 + M[2][2] * v2 + 0.f);
+                p[0] = t0, p[1] = t1, p[2] = t2;
+            }
+        }
+    }
+}
+
+// cvtColor BGR2HSV (RGB2HSV_b, hrange 180) -> hue shift -> HSV2BGR (HSV2RGB_b over HSV2RGB_f)
+struct HsvTables {
+    int sdiv[256], hdiv180[256];
+    HsvTables()
+    {
+        sdiv[0] = hdiv180[0] = 0;
+        for (int i = 1; i < 256; i++) {
+            sdiv[i]    = cv_round((255 << 12) / (1. * i));
+            hdiv180[i] = cv_round((180 << 12) / (6. * i));
+        }
+    }
+};
+const HsvTables& hsv_tables()
+{
+    static HsvTables t;
+    return t;
+}
+
+void hue_shift_pixel(uint8_t* px, int hue)
+{
+    const HsvTables& T = hsv_tables();
+    // RGB2HSV_b, bidx = 0 (BGR)
+    int b = px[0], g = px[1], r = px[2];
+    int v = std::max(b, std::max(g, r)), vmin = std::min(b, std::min(g, r));
+    int diff = v - vmin;
+    int vr = v == r ? -1 : 0, vg = v == g ? -1 : 0;
+    int s = (diff * T.sdiv[v] + (1 << 11)) >> 12;
+    int h = (vr & (g - b)) + (~vr & ((vg & (b - r + 2 * diff)) + ((~vg) & (r - g + 4 * diff))));
+    h = (h * T.hdiv180[diff] + (1 << 11)) >> 12;
+    h += h < 0 ? 180 : 0;
+    uint8_t H = sat_u8(h), S = (uint8_t)s, V = (uint8_t)v;
+    // image.cpp:386-390  *p = (*p + hue) % 180  (C remainder, stored as uchar)
+    H = (uint8_t)((H + hue) % 180);
+    // HSV2RGB_b: h stays 0..255, s and v scaled by 1/255; HSV2RGB_f with hscale = 6/180
+    float hf = H, sf = S * (1.f / 255), vf = V * (1.f / 255);
+    float bb, gg, rr;
+    if (sf == 0) bb = gg = rr = vf;
+    else {
+        static const int sector_data[][3] = {{1, 3, 0}, {1, 0, 2}, {3, 0, 1},
+                                             {0, 2, 1}, {0, 1, 3}, {2, 1, 0}};
+        float tab[4];
+        hf *= 6.f / 180.f;
+        if (hf < 0) do hf += 6; while (hf < 0);
+        else if (hf >= 6) do hf -= 6; while (hf >= 6);
+        int sector = cv_floor(hf);
+        hf -= sector;
+        if ((unsigned)sector >= 6u) sector = 0, hf = 0.f;
+        tab[0] = vf;
+        tab[1] = vf * (1.f - sf);
+        tab[2] = vf * (1.f - sf * hf);
+        tab[3] = vf * (1.f - sf * (1.f - hf));
+        bb = tab[sector_data[sector][0]];
+        gg = tab[sector_data[sector][1]];
+        rr = tab[sector_data[sector][2]];
+    }
+    px[0] = sat_u8f(bb * 255.f);
+    px[1] = sat_u8f(gg * 255.f);
+    px[2] = sat_u8f(rr * 255.f);
+}
+
+void cbsjitter(Img& m, float contrast, float brightness, float saturation, int hue)
+{
+    if (brightness != 1.0 || saturation != 1.0) bs_transform(m, brightness, saturation);
+    if (hue != 0) {
+        for (int y = 0; y < m.h; y++) {
+            uint8_t* p = m.row(y);
+            for (int x = 0; x < m.w; x++) hue_shift_pixel(p + 3 * x, hue);
+        }
+    }
+    if (contrast != 1.0) {
+        // cv::mean: exact per-channel sum times 1./N; dst = f32(x*c) (convertTo, f32 work type);
+        // dst += (1.0-c)*mean runs with an f64 work type (same arithm_op rule that the
+        // standardize goldens pin) and rounds to f32; convertTo(CV_8UC3) rounds half-even.
+        long long sum[3] = {0, 0, 0};
+        for (int y = 0; y < m.h; y++) {
+            const uint8_t* p = m.row(y);
+            for (int x = 0; x < m.w; x++)
+                for (int k = 0; k < 3; k++) sum[k] += p[3 * x + k];
+        }
+        const double inv_n = 1. / (double)(m.w * m.h);
+        double       shift[3];
+        for (int k = 0; k < 3; k++) shift[k] = (1.0 - contrast) * ((double)sum[k] * inv_n);
+        for (int y = 0; y < m.h; y++) {
+            uint8_t* p = m.row(y);
+            for (int x = 0; x < 3 * m.w; x++) {
+                float t = (float)p[x] * contrast + 0.f;
+                p[x]    = sat_u8f((float)((double)t + shift[x % 3]));
+            }
+        }
+    }
+}
+
+// ---- photometric::lighting (src/image.cpp:320-346) ------------------------------------------
+const float CPCA[3][3] = {{0.39731118f, 0.70119634f, -0.59200296f},
+                          {-0.81698062f, -0.02354167f, -0.57618440f},
+                          {0.41795513f, -0.71257945f, -0.56351045f}};
+const float CSTD[3]    = {19.72083305f, 37.09388853f, 121.78006099f};
+
+void lighting(Img& m, const float* al, int n, float sigma)
+{
+    if (n <= 0) return;
+    float v[3], px[3];
+    for (int k = 0; k < 3; k++) v[k] = CSTD[k] * al[k];                     // CSTD.mul(alphas)
+    for (int i = 0; i < 3; i++) px[i] = CPCA[i][0] * v[0] + CPCA[i][1] * v[1] + CPCA[i][2] * v[2];
+    // (inout + pixel) / (1 + sigma) -> convertTo(u8, a) then add(Scalar(pixel*a)) in CV_32S
+    const double a  = 1. / (1.0 + (double)sigma);
+    const float  af = (float)a;
+    int          li[3];
+    for (int k = 0; k < 3; k++) li[k] = cv_round((double)px[k] * a);
+    for (int y = 0; y < m.h; y++) {
+        uint8_t* p = m.row(y);
+        for (int x = 0; x < 3 * m.w; x++) {
+            int t = sat_u8f((float)p[x] * af + 0.f);
+            p[x]  = sat_u8(t + li[x % 3]);
+        }
+    }
+}
+
+void flip_h(Img& m)
+{
+    for (int y = 0; y < m.h; y++) {
+        uint8_t* p = m.row(y);
+        for (int x = 0; x < m.w / 2; x++)
+            for (int k = 0; k < m.cn; k++) std::swap(p[x * m.cn + k], p[(m.w - 1 - x) * m.cn + k]);
+    }
+}
+
+// image::transformer::transform_single_image (src/etl_image.cpp:146-202)
+Img transform_single_image(const Img& src, const orc_params& p)
+{
+    if (p.angle != 0) throw std::invalid_argument("oracle: rotation not restated yet");
+    Img base = Img::view(src.data, src.w, src.h, src.cn, src.stride);
+    Img rs;
+    if (p.resize_short_size != 0) {
+        int rw, rh;
+        resized_short_size(src.w, src.h, p.resize_short_size, &rw, &rh);
+        rs = Img::alloc(rw, rh, src.cn);
+        if (p.interp == 1) resize_nearest(base, rs);
+        else resize_linear(base, rs);
+        base = Img::view(rs.data, rs.w, rs.h, rs.cn, rs.stride);
+    }
+    if (p.crop_x < 0 || p.crop_y < 0 || p.crop_w <= 0 || p.crop_h <= 0 ||
+        p.crop_x + p.crop_w > base.w || p.crop_y + p.crop_h > base.h)
+        throw std::invalid_argument("cropbox outside image");
+    Img crop = Img::view(base.row(p.crop_y) + (size_t)p.crop_x * base.cn, p.crop_w, p.crop_h,
+                         base.cn, base.stride);
+    Img padded;
+    if (!(p.padding == 0 || (p.pad_off_x == p.padding && p.pad_off_y == p.padding))) {
+        // image::add_padding (image.cpp:77-91): zero border, then crop back to the input size
+        padded = Img::alloc(crop.w, crop.h, crop.cn);
+        for (int y = 0; y < crop.h; y++)
+            for (int x = 0; x < crop.w; x++) {
+                int sx = x + p.pad_off_x - p.padding, sy = y + p.pad_off_y - p.padding;
+                if (sx < 0 || sy < 0 || sx >= crop.w || sy >= crop.h) continue;
+                std::memcpy(padded.row(y) + x * crop.cn, crop.row(sy) + sx * crop.cn, crop.cn);
+            }
+        crop = Img::view(padded.data, padded.w, padded.h, padded.cn, padded.stride);
+    }
+    Img out = Img::alloc(p.out_w, p.out_h, src.cn);
+    resize_any(crop, out, p.interp);
+    if (src.cn == 3) {
+        cbsjitter(out, p.contrast, p.brightness, p.saturation, p.hue);
+        lighting(out, p.lighting, p.n_lighting, p.color_noise_std);
+    }
+    if (p.flip) flip_h(out);
+    return out;
+}
+
+// image::standardize arithmetic (image.cpp:129-174 + OpenCV 2.4 arithm_op): every
+// Mat(f32) op Scalar(f64) runs with an f64 work type and rounds back to f32 after each op.
+// Pinned bit-exact by augment_output_linear_{train,eval}.bin (all 765 channel/value pairs).
+float standardize_value(int x, double mean, double stddev)
+{
+    float t1 = (float)((double)(float)x * (1. / 255.));
+    float t2 = (float)((double)t1 - mean);
+    if (stddev == 0) return t2;
+    return (float)((double)t2 * (1. / stddev));
+}
+
+// image::loader::load (src/etl_image.cpp:246-341), non-fixed-aspect-ratio branch
+void load_image(const Img& img, const orc_load_config& lc, void* out)
+{
+    const int cn = lc.channels, w = img.w, h = img.h;
+    if (img.cn != cn) throw std::invalid_argument("channel mismatch");
+    const size_t plane = (size_t)w * h;
+    for (int y = 0; y < h; y++) {
+        const uint8_t* p = img.row(y);
+        for (int x = 0; x < w; x++) {
+            for (int oc = 0; oc < cn; oc++) {
+                int    sc  = lc.bgr_to_rgb ? (cn - 1 - oc) : oc; // from_to {0,2,1,1,2,0}
+                int    v   = p[x * cn + sc];
+                size_t idx = lc.channel_major ? (size_t)oc * plane + (size_t)y * w + x
+                                              : ((size_t)y * w + x) * cn + oc;
+                if (lc.out_dtype == 0) {
+                    ((uint8_t*)out)[idx] = (uint8_t)v;
+                } else {
+                    float f = lc.has_mean ? standardize_value(v, lc.mean[oc], lc.stddev[oc])
+                                          : (float)v;
+                    ((float*)out)[idx] = f;
+                }
+            }
+        }
+    }
+}
+
+// pixel_mask::transformer::transform (src/etl_pixel_mask.cpp:65-92)
+Img transform_mask(const Img& src, const orc_params& p)
+{
+    if (p.angle != 0) throw std::invalid_argument("oracle: rotation not restated yet");
+    if (p.crop_x < 0 || p.crop_y < 0 || p.crop_w <= 0 || p.crop_h <= 0 ||
+        p.crop_x + p.crop_w > src.w || p.crop_y + p.crop_h > src.h)
+        throw std::invalid_argument("cropbox outside mask");
+    Img crop = Img::view(src.row(p.crop_y) + (size_t)p.crop_x * src.cn, p.crop_w, p.crop_h,
+                         src.cn, src.stride);
+    Img out = Img::alloc(p.out_w, p.out_h, src.cn);
+    resize_any(crop, out, 1);
+    if (p.flip) flip_h(out);
+    return out;
+}
+
+template <typename F>
+int guarded(F&& f)
+{
+    try {
+        f();
+        return 0;
+    } catch (const std::exception& e) {
+        g_err = e.what();
+        return -1;
+    }
+}
+
+} // namespace
+
+extern "C" {
+
+void* orc_factory_create(const orc_aug_config* cfg) { return new Factory(*cfg); }
+void  orc_factory_destroy(void* f) { delete (Factory*)f; }
+
+int orc_make_params(void* f, uint32_t* state, int in_w, int in_h, int out_w, int out_h,
+                    orc_params* out)
+{
+    return guarded([&] {
+        Engine e(*state);
+        make_params(*(Factory*)f, e, in_w, in_h, out_w, out_h, out);
+        *state = e.last;
+    });
+}
+
+void orc_seed_slots(uint32_t seed, int n, uint32_t* states)
+{
+    // engine_i.seed(generator_seed()): minstd's seed(s) keeps s mod m (1 if that is 0),
+    // so the state word of slot i is the i-th output of minstd_rand0(seed).
+    std::minstd_rand0 g(seed);
+    for (int i = 0; i < n; i++) {
+        uint32_t s = g() % 2147483647u;
+        states[i]  = s == 0 ? 1 : s;
+    }
+}
+
+int orc_transform_image(const uint8_t* src, int w, int h, int cn, int stride, const orc_params* p,
+                        uint8_t* out)
+{
+    return guarded([&] {
+        Img s = Img::view(src, w, h, cn, stride);
+        Img o = transform_single_image(s, *p);
+        std::memcpy(out, o.data, (size_t)o.w * o.h * o.cn);
+    });
+}
+
+int orc_load_image(const uint8_t* img, int w, int h, const orc_load_config* lc, void* out)
+{
+    return guarded([&] { load_image(Img::view(img, w, h, lc->channels, w * lc->channels), *lc, out); });
+}
+
+int orc_transform_mask(const uint8_t* src, int w, int h, int stride, const orc_params* p,
+                       uint8_t* out)
+{
+    return guarded([&] {
+        Img o = transform_mask(Img::view(src, w, h, 1, stride), *p);
+        std::memcpy(out, o.data, (size_t)o.w * o.h);
+    });
+}
+
+int orc_resize_linear(const uint8_t* src, int sw, int sh, int sstride, int cn, uint8_t* dst, int dw,
+                      int dh)
+{
+    return guarded([&] {
+        Img s = Img::view(src, sw, sh, cn, sstride);
+        Img d = Img::view(dst, dw, dh, cn, dw * cn);
+        resize_linear(s, d);
+    });
+}
+
+int orc_resize_nearest(const uint8_t* src, int sw, int sh, int sstride, int cn, uint8_t* dst,
+                       int dw, int dh)
+{
+    return guarded([&] {
+        Img s = Img::view(src, sw, sh, cn, sstride);
+        Img d = Img::view(dst, dw, dh, cn, dw * cn);
+        resize_nearest(s, d);
+    });
+}
+
+void orc_cbsjitter(uint8_t* img, int w, int h, float contrast, float brightness, float saturation,
+                   int hue)
+{
+    Img m = Img::view(img, w, h, 3, w * 3);
+    cbsjitter(m, contrast, brightness, saturation, hue);
+}
+
+void orc_lighting(uint8_t* img, int w, int h, const float* l, int n, float sigma)
+{
+    Img m = Img::view(img, w, h, 3, w * 3);
+    lighting(m, l, n, sigma);
+}
+
+float orc_standardize_value(int x, double mean, double stddev)
+{
+    return standardize_value(x, mean, stddev);
+}
+
+// CPU baseline: aeon's thread_pool policy -- N workers pulling record indices from one
+// atomic counter (src/thread_pool.hpp:155-162), each running transform + load per record.
+double orc_batch_augment(int n, const uint8_t* const* srcs, const int* widths, const int* heights,
+                         const orc_params* params, const orc_load_config* lc, void* out,
+                         size_t item_bytes, int threads)
+{
+    std::atomic<int>  next{0};
+    std::atomic<bool> failed{false};
+    auto              work = [&] {
+        for (;;) {
+            int i = next.fetch_add(1);
+            if (i >= n) break;
+            try {
+                Img s = Img::view(srcs[i], widths[i], heights[i], lc->channels,
+                                  widths[i] * lc->channels);
+                Img o = transform_single_image(s, params[i]);
+                load_image(o, *lc, (char*)out + (size_t)i * item_bytes);
+            } catch (const std::exception& e) {
+                g_err = e.what();
+                failed = true;
+            }
+        }
+    };
+    auto t0 = std::chrono::steady_clock::now();
+    std::vector<std::thread> pool;
+    for (int t = 0; t < std::max(1, threads); t++) pool.emplace_back(work);
+    for (auto& t : pool) t.join();
+    auto t1 = std::chrono::steady_clock::now();
+    if (failed) return -1.0;
+    return std::chrono::duration<double>(t1 - t0).count();
+}
+
+const char* orc_last_error(void) { return g_err.c_str(); }
+
+} // extern "C"

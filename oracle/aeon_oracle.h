@@ -1,0 +1,102 @@
+/* aeon_oracle.h -- TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU restatement of NervanaSystems/aeon's image-augmentation path (the checker
+ * the HIP product is compared against).  Only tests/, __graft_entry__.smoke() and
+ * bench.py's cpu_baseline leg may load this library.  The product (aeon_amd/)
+ * never links or calls it.
+ *
+ * Parity anchor: pinned by aeon's golden vectors
+ * test/test_data/augment_output_linear_{train,eval}.bin (test/test_provider.cpp:96-261)
+ * and the KATs of test/test_image.cpp (see tests/test_oracle.py).  Stages that no
+ * reference fixture covers (saturation != 1, hue, lighting, 2x area path, scalar
+ * row tails) follow the OpenCV-2.4 semantics restated in SURVEY.md Appendix A and
+ * are "parity unpinned" -- see DESIGN.md.
+ */
+#pragma once
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* augment::image::param_factory configuration (src/augment_image.hpp:141-246). */
+typedef struct orc_aug_config {
+    float scale_min, scale_max;           /* "scale"                 */
+    int   angle_min, angle_max;           /* "angle"                 */
+    float lighting_mean, lighting_stddev; /* "lighting"              */
+    float hdist_min, hdist_max;           /* "horizontal_distortion" */
+    float contrast_min, contrast_max;
+    float brightness_min, brightness_max;
+    float saturation_min, saturation_max;
+    int   hue_min, hue_max;
+    int   flip_enable, center, crop_enable, do_area_scale;
+    int   resize_short_size, padding;
+    float fixed_scaling_factor;           /* -1 = unset */
+    int   interp;                         /* 0 LINEAR, 1 NEAREST */
+} orc_aug_config;
+
+/* augment::image::params (src/augment_image.hpp:99-119), the fields the image path reads. */
+typedef struct orc_params {
+    int   crop_x, crop_y, crop_w, crop_h;
+    int   resize_short_size;
+    int   out_w, out_h;
+    int   angle, flip, padding, pad_off_x, pad_off_y;
+    int   n_lighting;
+    float lighting[3];
+    float color_noise_std;
+    float contrast, brightness, saturation;
+    int   hue;
+    int   interp;
+} orc_params;
+
+/* image::loader configuration (src/etl_image.cpp:204-244). */
+typedef struct orc_load_config {
+    int    channels;       /* 1 or 3 */
+    int    channel_major;  /* CHW planes vs HWC */
+    int    bgr_to_rgb;
+    int    out_dtype;      /* 0 = uint8, 1 = float32 */
+    int    has_mean;       /* standardize enabled */
+    double mean[3];
+    double stddev[3];
+} orc_load_config;
+
+/* param_factory + per-record engine.  engine_state is the minstd_rand0 state word. */
+void* orc_factory_create(const orc_aug_config* cfg);
+void  orc_factory_destroy(void* f);
+int   orc_make_params(void* f, uint32_t* engine_state, int in_w, int in_h, int out_w, int out_h,
+                      orc_params* out);
+/* aeon deterministic-mode slot seeding (src/batch_decoder.cpp:47-54): n engine states. */
+void  orc_seed_slots(uint32_t seed, int n, uint32_t* states);
+
+/* transform_single_image (src/etl_image.cpp:146-202) -> out_h x out_w x cn uint8 HWC BGR. */
+int orc_transform_image(const uint8_t* src, int w, int h, int cn, int src_stride,
+                        const orc_params* p, uint8_t* out);
+/* image::loader::load (src/etl_image.cpp:246-341) for the non-fixed-aspect-ratio path. */
+int orc_load_image(const uint8_t* img, int w, int h, const orc_load_config* lc, void* out);
+/* pixel_mask::transformer::transform (src/etl_pixel_mask.cpp:65-92), 1-channel uint8. */
+int orc_transform_mask(const uint8_t* src, int w, int h, int src_stride, const orc_params* p,
+                       uint8_t* out);
+
+/* primitives, exposed for the KATs */
+int  orc_resize_linear(const uint8_t* src, int sw, int sh, int sstride, int cn, uint8_t* dst,
+                       int dw, int dh);
+int  orc_resize_nearest(const uint8_t* src, int sw, int sh, int sstride, int cn, uint8_t* dst,
+                        int dw, int dh);
+void orc_cbsjitter(uint8_t* img, int w, int h, float contrast, float brightness,
+                   float saturation, int hue);
+void orc_lighting(uint8_t* img, int w, int h, const float* lighting, int n, float color_noise_std);
+float orc_standardize_value(int x, double mean, double stddev);
+
+/* whole-record path (transform + load) over a batch on a thread pool -- CPU baseline.
+ * srcs[i] = HWC BGR uint8 image i (widths/heights per image), params[i] its params,
+ * out = batch of item_bytes slots.  Returns elapsed seconds. */
+double orc_batch_augment(int n, const uint8_t* const* srcs, const int* widths, const int* heights,
+                         const orc_params* params, const orc_load_config* lc, void* out,
+                         size_t item_bytes, int threads);
+
+const char* orc_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
