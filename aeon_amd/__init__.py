@@ -1,0 +1,250 @@
+"""aeon_amd -- MI355X (gfx950) image-augmentation stage for NervanaSystems/aeon.
+
+Python binding of the C ABI in include/aeon_hip.h (libaeon_hip.so, built in-tree).
+The pixel path runs only in the HIP kernels of that library: there is no CPU fallback, and
+importing this package fails loudly when the library is missing.  PyTorch is used only as
+plumbing (device memory and streams) by callers; the binding itself takes raw pointers.
+"""
+import ctypes
+import json
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libaeon_hip.so")
+HEADER = os.path.join(os.path.dirname(HERE), "include", "aeon_hip.h")
+
+AEON_HIP_OK = 0
+AEON_HIP_EINVAL = -1
+AEON_HIP_ERUNTIME = -2
+AEON_HIP_EUNSUPPORTED = -3
+AEON_HIP_EDEVICE = -4
+
+DTYPE_U8 = 0
+DTYPE_F32 = 1
+INTERP_LINEAR = 0
+INTERP_NEAREST = 1
+
+
+class ImgDesc(ctypes.Structure):
+    _fields_ = [("offset", ctypes.c_uint64), ("width", ctypes.c_int32), ("height", ctypes.c_int32),
+                ("stride", ctypes.c_int32), ("channels", ctypes.c_int32)]
+
+
+class AugParams(ctypes.Structure):
+    """POD mirror of augment::image::params (aeon src/augment_image.hpp:99-119)."""
+    _fields_ = [
+        ("crop_x", ctypes.c_int32), ("crop_y", ctypes.c_int32),
+        ("crop_w", ctypes.c_int32), ("crop_h", ctypes.c_int32),
+        ("resize_short_size", ctypes.c_int32),
+        ("out_w", ctypes.c_int32), ("out_h", ctypes.c_int32),
+        ("angle", ctypes.c_int32), ("flip", ctypes.c_int32),
+        ("padding", ctypes.c_int32), ("pad_off_x", ctypes.c_int32), ("pad_off_y", ctypes.c_int32),
+        ("n_lighting", ctypes.c_int32), ("lighting", ctypes.c_float * 3),
+        ("color_noise_std", ctypes.c_float),
+        ("contrast", ctypes.c_float), ("brightness", ctypes.c_float),
+        ("saturation", ctypes.c_float), ("hue", ctypes.c_int32),
+        ("interp", ctypes.c_int32),
+    ]
+
+    def as_dict(self):
+        d = {f: getattr(self, f) for f, _ in self._fields_}
+        d["lighting"] = list(self.lighting)
+        return d
+
+
+class OutDesc(ctypes.Structure):
+    """image::loader configuration + batch item stride (aeon src/etl_image.cpp:204-244)."""
+    _fields_ = [("dtype", ctypes.c_int32), ("channels", ctypes.c_int32),
+                ("channel_major", ctypes.c_int32), ("bgr_to_rgb", ctypes.c_int32),
+                ("has_mean", ctypes.c_int32), ("reserved", ctypes.c_int32),
+                ("mean", ctypes.c_double * 3), ("stddev", ctypes.c_double * 3),
+                ("item_stride", ctypes.c_uint64)]
+
+
+class AeonHipError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"aeon_hip error {code}: {msg}")
+        self.code = code
+
+
+_lib = None
+
+
+def lib():
+    """Load libaeon_hip.so (raises if it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} missing: run `python -c 'import __graft_entry__ as g; g.build()'`"
+                              " (the HIP extension is required; there is no CPU fallback)")
+        L = ctypes.CDLL(LIB_PATH)
+        P = ctypes.POINTER
+        vp = ctypes.c_void_p
+        L.aeon_hip_ctx_create.argtypes = [ctypes.c_int, P(vp)]
+        L.aeon_hip_ctx_destroy.argtypes = [vp]
+        for fn in (L.aeon_hip_augment_batch, L.aeon_hip_mask_batch):
+            fn.argtypes = [vp, ctypes.c_int, P(ImgDesc), vp, P(AugParams), P(OutDesc), vp, vp]
+        L.aeon_hip_synchronize.argtypes = [vp, vp]
+        L.aeon_hip_set_timing.argtypes = [vp, ctypes.c_int]
+        L.aeon_hip_kernel_times.argtypes = [vp, P(ctypes.c_double), P(ctypes.c_double), P(ctypes.c_long)]
+        L.aeon_param_factory_create.argtypes = [ctypes.c_char_p, P(vp)]
+        L.aeon_param_factory_destroy.argtypes = [vp]
+        L.aeon_make_params.argtypes = [vp, P(ctypes.c_uint32), ctypes.c_int, ctypes.c_int,
+                                       ctypes.c_int, ctypes.c_int, P(AugParams)]
+        L.aeon_seed_slots.argtypes = [ctypes.c_uint32, ctypes.c_int, P(ctypes.c_uint32)]
+        L.aeon_hip_host_alloc.argtypes = [ctypes.c_size_t, P(vp)]
+        L.aeon_hip_host_free.argtypes = [vp]
+        L.aeon_hip_last_error.restype = ctypes.c_char_p
+        L.aeon_hip_version.restype = ctypes.c_char_p
+        _lib = L
+    return _lib
+
+
+def _check(rc):
+    if rc != 0:
+        raise AeonHipError(rc, lib().aeon_hip_last_error().decode())
+    return rc
+
+
+def exported_symbols():
+    """Function names declared in include/aeon_hip.h."""
+    import re
+    text = open(HEADER).read()
+    return sorted(set(re.findall(r"^(?:int|const char\*)\s+(aeon_\w+)\s*\(", text, re.M)))
+
+
+# ---- parameters (host) -------------------------------------------------------------------------
+class ParamFactory:
+    """augment::image::param_factory (aeon src/augment_image.cpp:28-230)."""
+
+    def __init__(self, aug_config):
+        text = aug_config if isinstance(aug_config, str) else json.dumps(aug_config)
+        h = ctypes.c_void_p()
+        _check(lib().aeon_param_factory_create(text.encode(), ctypes.byref(h)))
+        self._h = h
+
+    def __del__(self):
+        if getattr(self, "_h", None) and _lib is not None:
+            _lib.aeon_param_factory_destroy(self._h)
+            self._h = None
+
+    def make_params(self, state, in_w, in_h, out_w, out_h):
+        """state: np.uint32 array of one element (minstd_rand0 state word, updated in place)."""
+        p = AugParams()
+        st = ctypes.c_uint32(int(state[0]))
+        _check(lib().aeon_make_params(self._h, ctypes.byref(st), in_w, in_h, out_w, out_h, ctypes.byref(p)))
+        state[0] = st.value
+        return p
+
+
+def seed_slots(seed, n):
+    """batch_decoder deterministic-mode engine states (aeon src/batch_decoder.cpp:47-54)."""
+    out = np.zeros(n, np.uint32)
+    _check(lib().aeon_seed_slots(seed, n, out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))))
+    return out
+
+
+def aug_params(**kw):
+    p = AugParams(contrast=1.0, brightness=1.0, saturation=1.0, interp=INTERP_LINEAR)
+    for k, v in kw.items():
+        if k == "lighting":
+            p.n_lighting = len(v)
+            for i, x in enumerate(v):
+                p.lighting[i] = x
+        else:
+            setattr(p, k, v)
+    return p
+
+
+def out_desc(channels=3, channel_major=True, bgr_to_rgb=False, dtype="float32", mean=None,
+             stddev=None, item_stride=0):
+    o = OutDesc(dtype=DTYPE_U8 if dtype == "uint8" else DTYPE_F32, channels=channels,
+                channel_major=int(channel_major), bgr_to_rgb=int(bgr_to_rgb), has_mean=0,
+                item_stride=item_stride)
+    if mean is not None:
+        o.has_mean = 1
+        for i in range(channels):
+            o.mean[i] = mean[i]
+            o.stddev[i] = stddev[i]
+    return o
+
+
+# ---- device stage --------------------------------------------------------------------------------
+class Context:
+    """One per GPU (aeon_hip_ctx)."""
+
+    def __init__(self, device=0):
+        h = ctypes.c_void_p()
+        _check(lib().aeon_hip_ctx_create(device, ctypes.byref(h)))
+        self._h = h
+        self.device = device
+
+    def close(self):
+        if getattr(self, "_h", None):
+            _check(lib().aeon_hip_ctx_destroy(self._h))
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _batch(self, fn, descs, src_ptr, params, out, out_ptr, stream):
+        n = len(descs)
+        d = (ImgDesc * n)(*descs)
+        p = (AugParams * n)(*params)
+        _check(fn(self._h, n, d, ctypes.c_void_p(src_ptr), p, ctypes.byref(out),
+                  ctypes.c_void_p(out_ptr), ctypes.c_void_p(stream or 0)))
+
+    def augment_batch(self, descs, src_ptr, params, out, out_ptr, stream=0):
+        """transform_single_image + loader::load for len(descs) records (async on stream)."""
+        self._batch(lib().aeon_hip_augment_batch, descs, src_ptr, params, out, out_ptr, stream)
+
+    def mask_batch(self, descs, src_ptr, params, out, out_ptr, stream=0):
+        """pixel_mask transform + load for len(descs) records (async on stream)."""
+        self._batch(lib().aeon_hip_mask_batch, descs, src_ptr, params, out, out_ptr, stream)
+
+    def set_timing(self, enable=True):
+        _check(lib().aeon_hip_set_timing(self._h, int(enable)))
+
+    def kernel_times(self):
+        """{'augment'|'stats'|'resize_short': (total_ms, total_algorithmic_bytes, launches)}"""
+        ms, by, ct = (ctypes.c_double * 3)(), (ctypes.c_double * 3)(), (ctypes.c_long * 3)()
+        _check(lib().aeon_hip_kernel_times(self._h, ms, by, ct))
+        return {k: (ms[i], by[i], ct[i]) for i, k in enumerate(("augment", "stats", "resize_short"))}
+
+    def synchronize(self, stream=0):
+        _check(lib().aeon_hip_synchronize(self._h, ctypes.c_void_p(stream or 0)))
+
+
+def pack_images(images, align=16):
+    """Concatenate HWC uint8 images into one byte arena; returns (arena, [ImgDesc])."""
+    descs, chunks, off = [], [], 0
+    for im in images:
+        im = np.ascontiguousarray(im, dtype=np.uint8)
+        h, w = im.shape[:2]
+        cn = 1 if im.ndim == 2 else im.shape[2]
+        descs.append(ImgDesc(offset=off, width=w, height=h, stride=w * cn, channels=cn))
+        b = im.reshape(-1)
+        pad = (-b.size) % align
+        chunks.append(b)
+        if pad:
+            chunks.append(np.zeros(pad, np.uint8))
+        off += b.size + pad
+    arena = np.concatenate(chunks) if chunks else np.zeros(0, np.uint8)
+    return arena, descs
+
+
+def synthetic_image(index, w, h, cn=3, seed=0x5EED):
+    """Counter-based synthetic HWC uint8 image: byte = splitmix64(seed^(img<<32)^idx)&0xFF."""
+    idx = np.arange(w * h * cn, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        z = (np.uint64(seed) ^ (np.uint64(index) << np.uint64(32)) ^ idx) + np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+    return (z & np.uint64(0xFF)).astype(np.uint8).reshape(h, w, cn) if cn > 1 else \
+        (z & np.uint64(0xFF)).astype(np.uint8).reshape(h, w)

@@ -1,0 +1,106 @@
+// aug_job.hpp -- per-image work descriptors shared by the host planner (plan.cpp) and the
+// HIP kernels (augment_kernels.hip).  One AugJob = one image's pass through
+// crop -> [add_padding] -> resize -> cbsjitter -> lighting -> flip -> loader::load
+// (aeon src/etl_image.cpp:146-202, 246-341), with every per-image constant that aeon
+// derives on the host (cv::transform matrix, lighting pixel, cropbox) precomputed.
+#pragma once
+#include <stdint.h>
+
+namespace aeon_hip {
+
+enum ResizeMode : int32_t {
+    RESIZE_COPY     = 0, // image::resize identity (size already matches, image.cpp:98-101)
+    RESIZE_LINEAR   = 1, // cv::resize INTER_LINEAR, 11-bit fixed point
+    RESIZE_AREA2X   = 2, // INTER_LINEAR at exactly 2x is routed to INTER_AREA's fast path
+    RESIZE_NEAREST  = 3, // cv::resize INTER_NEAREST (pixel masks)
+};
+
+enum PhotoFlags : int32_t {
+    PHOTO_BS       = 1, // brightness/saturation cv::transform
+    PHOTO_HUE      = 2, // BGR->HSV8, H=(H+hue)%180, HSV8->BGR
+    PHOTO_CONTRAST = 4, // x*c + (1-c)*mean(image)
+    PHOTO_LIGHTING = 8, // (x + pca_pixel)/(1+sigma)
+};
+
+enum BsKind : int32_t { BS_DIAG = 0, BS_FIXPT = 1, BS_FLOAT = 2 };
+
+enum OutDtype : int32_t { OUT_U8 = 0, OUT_F32 = 1 };
+
+// 16-byte aligned, plain data (copied H2D as an array).
+struct alignas(16) AugJob {
+    double   scale_x, scale_y;  // OpenCV's 1/inv_scale (bilinear/nearest coefficient maths)
+    uint64_t src_ptr;           // device address of the source image (HWC uint8)
+    uint64_t src_bytes;         // bytes readable from src_ptr (buffer-descriptor range)
+    uint64_t out_ptr;           // device address of the output item
+    int32_t  src_w, src_h, src_stride, cn;
+    int32_t  crop_x, crop_y, crop_w, crop_h; // region fed to the resize
+    int32_t  shift_x, shift_y, padded;       // add_padding (image.cpp:77-91) as a virtual zero
+                                             // border: resize-source (u,v) reads crop
+                                             // (u+shift_x, v+shift_y), zero outside the crop
+    int32_t  mode;                           // ResizeMode
+    int32_t  dst_w, dst_h;                   // full resize target
+    int32_t  win_x, win_y, win_w, win_h;     // window of the target produced by this job
+    int32_t  xv;                             // first element (x*cn+c) on OpenCV's scalar row tail
+    int32_t  flip;
+    int32_t  photo;                          // PhotoFlags
+    int32_t  bs_kind;                        // BsKind
+    int32_t  bsq[9];                         // 10-bit fixed-point transform coefficients
+    float    bsm[9];                         // float transform matrix (diag / float paths)
+    float    contrast;
+    int32_t  hue;
+    float    light_a;                        // (float)(1/(1+sigma))
+    int32_t  light_add[3];                   // cvRound(pixel_c / (1+sigma))
+    int32_t  tiles;                          // row tiles of this job
+    int32_t  stats_slot;                     // contrast partial-sum slot (-1 if none)
+    int32_t  src_scratch;                    // host bookkeeping: source lives in the slot scratch
+    int32_t  pad_;
+};
+
+// Per-launch uniform arguments.
+struct LaunchArgs {
+    const AugJob*  jobs;
+    const float*   lut;        // [3][256] standardized values (nullptr: no mean/stddev)
+    const int32_t* hsv_tables; // sdiv[256], hdiv180[256]
+    uint32_t*      partials;   // contrast partial sums [slots][max_tiles][4]
+    int32_t*       error;      // device error word (0 = ok)
+    int32_t        rows_per_tile;
+    int32_t        max_tiles;
+    int32_t        stage_rows; // capacity of the LDS staging area
+    int32_t        stage_pitch;// pixels per staged row (multiple of 4)
+    int32_t        max_win_w;  // capacity of the x table
+    int32_t        out_dtype;  // OutDtype
+    int32_t        channel_major;
+    int32_t        bgr_to_rgb;
+    int32_t        vec_ok;     // outputs 16-byte aligned and win_w % 4 == 0 for every job
+    int32_t        lds_bytes;
+};
+
+enum KernelMode : int { KM_FINAL = 0, KM_STATS = 1, KM_RAW = 2 };
+
+constexpr int kBlock = 256; // 4 wave64s per workgroup
+
+#if defined(__HIPCC__)
+#define AEON_HD __host__ __device__
+#else
+#define AEON_HD
+#endif
+
+// LDS carve of one workgroup (bytes; every region 16-byte aligned, see the CDNA guide G17).
+struct LdsLayout {
+    int hsv, lut, xt, yt, red, stage, total;
+};
+AEON_HD inline LdsLayout lds_layout(int max_win_w, int rows_per_tile, int stage_rows, int stage_pitch)
+{
+    LdsLayout L;
+    int       o = 0;
+    L.hsv = o;   o += 2 * 256 * 4;                       // sdiv / hdiv180 tables
+    L.lut = o;   o += 3 * 256 * 4;                       // standardize LUT
+    L.xt  = o;   o += ((max_win_w * 8 + 15) / 16) * 16;  // per-column taps + weights
+    L.yt  = o;   o += rows_per_tile * 16;                // per-row taps + weights
+    L.red = o;   o += 128;                               // reductions / contrast shifts
+    L.stage = o; o += stage_rows * stage_pitch * 4;      // source pixels, 4 B each (B,G,R,0)
+    L.total = o;
+    return L;
+}
+
+} // namespace aeon_hip

@@ -1,0 +1,690 @@
+// stage.cpp -- host side of the HIP augmentation stage: per-record planning (the host-side
+// arithmetic aeon does per record before touching pixels), the per-GPU context with its
+// pinned/device staging ring, kernel launches and the extern "C" boundary (include/aeon_hip.h).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+#include <cstring>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/aeon_hip.h"
+#include "aug_job.hpp"
+#include "json.hpp"
+#include "param_factory.hpp"
+
+namespace aeon_hip {
+hipError_t launch_tiles(int mode, const LaunchArgs& a, int n_jobs, hipStream_t stream);
+hipError_t set_kernel_lds_limit(int bytes);
+} // namespace aeon_hip
+
+using namespace aeon_hip;
+
+namespace {
+
+thread_local std::string g_err;
+
+struct aeon_error : std::runtime_error {
+    int code;
+    aeon_error(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+[[noreturn]] void fail(int code, const std::string& msg) { throw aeon_error(code, msg); }
+
+#define HIP_OK(expr)                                                                           \
+    do {                                                                                       \
+        hipError_t e_ = (expr);                                                                \
+        if (e_ != hipSuccess) fail(AEON_HIP_ERUNTIME, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+constexpr int kMaxLds        = 160 * 1024;
+constexpr int kStageBudget   = 48 * 1024;   // preferred LDS staging bytes per workgroup
+constexpr int kStageBudgetHi = 120 * 1024;  // fallback for very wide crops
+
+// ---------------------------------------------------------------------------------------------
+// Per-image constants (aeon computes these on the host per record, too)
+// ---------------------------------------------------------------------------------------------
+
+// OpenCV 2.4 cv::resize dispatch for 8U: identity, INTER_NEAREST, 2x INTER_LINEAR -> area fast
+// path, generic INTER_LINEAR.
+int choose_mode(int sw, int sh, int dw, int dh, int interp, int cn)
+{
+    if (sw == dw && sh == dh) return RESIZE_COPY;
+    if (interp == AEON_INTERP_NEAREST) return RESIZE_NEAREST;
+    double sx = 1. / ((double)dw / sw), sy = 1. / ((double)dh / sh);
+    int    ix = cv_round(sx), iy = cv_round(sy);
+    bool   fast = std::abs(sx - ix) < DBL_EPSILON && std::abs(sy - iy) < DBL_EPSILON;
+    if (fast && ix == 2 && iy == 2 && (cn == 1 || cn == 3)) return RESIZE_AREA2X;
+    return RESIZE_LINEAR;
+}
+
+// First element of a W-element destination row handled by OpenCV's scalar tail after
+// VResizeLinearVec_32s8u (16-wide loop while x <= W-16, 4-wide while x < W-4).
+int simd_boundary(int W)
+{
+    int x = W >= 16 ? (W / 16) * 16 : 0;
+    while (x < W - 4) x += 4;
+    return x;
+}
+
+// photometric::cbsjitter brightness/saturation matrix (src/image.cpp:362-373) and the
+// cv::transform path OpenCV 2.4 picks for it.
+void plan_bs(AugJob& J, float brightness, float saturation)
+{
+    const float g[3] = {0.0820f, 0.6094f, 0.3086f};
+    float       M[9];
+    float       oms = 1 - saturation;
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) {
+            float A = i == j ? saturation : 0.f;
+            float B = (float)((double)oms * (double)g[j]);
+            M[i * 3 + j] = brightness == 1.0f ? A + B
+                                              : (float)((double)A * brightness + (double)B * brightness + 0.0);
+        }
+    bool diag = true;
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++)
+            if (i != j && std::fabs((double)M[i * 3 + j]) > FLT_EPSILON) diag = false;
+    bool fixpt = true;
+    for (int k = 0; k < 9; k++)
+        if (!(std::fabs(M[k]) < 32.f)) fixpt = false;
+    for (int k = 0; k < 9; k++) {
+        J.bsm[k] = M[k];
+        J.bsq[k] = std::min(std::max(cv_roundf(M[k] * 1024), -32768), 32767);
+    }
+    J.bs_kind = diag ? BS_DIAG : (fixpt ? BS_FIXPT : BS_FLOAT);
+}
+
+// photometric::lighting (src/image.cpp:320-346): the PCA pixel and its (1+sigma) scaling.
+void plan_lighting(AugJob& J, const float* al, float sigma)
+{
+    static const float CPCA[3][3] = {{0.39731118f, 0.70119634f, -0.59200296f},
+                                     {-0.81698062f, -0.02354167f, -0.57618440f},
+                                     {0.41795513f, -0.71257945f, -0.56351045f}};
+    static const float CSTD[3]    = {19.72083305f, 37.09388853f, 121.78006099f};
+    float              v[3], px[3];
+    for (int k = 0; k < 3; k++) v[k] = CSTD[k] * al[k];
+    for (int i = 0; i < 3; i++) px[i] = CPCA[i][0] * v[0] + CPCA[i][1] * v[1] + CPCA[i][2] * v[2];
+    const double a = 1. / (1.0 + (double)sigma);
+    J.light_a      = (float)a;
+    for (int k = 0; k < 3; k++) J.light_add[k] = cv_round((double)px[k] * a);
+}
+
+// image::standardize arithmetic (src/image.cpp:129-174 over OpenCV 2.4 arithm_op: f64 work
+// type per op, rounded to f32 after each op) tabulated per channel and input value.
+void build_lut(const aeon_out_desc& o, float* lut)
+{
+    for (int c = 0; c < 3; c++)
+        for (int x = 0; x < 256; x++) {
+            if (!o.has_mean || c >= o.channels) {
+                lut[c * 256 + x] = (float)x;
+                continue;
+            }
+            float t1 = (float)((double)(float)x * (1. / 255.));
+            float t2 = (float)((double)t1 - o.mean[c]);
+            lut[c * 256 + x] = o.stddev[c] != 0 ? (float)((double)t2 * (1. / o.stddev[c])) : t2;
+        }
+}
+
+// source-footprint bounds used to size the LDS staging area
+int stage_cols(const AugJob& J)
+{
+    switch (J.mode) {
+    case RESIZE_LINEAR: return std::min(J.crop_w, (int)std::ceil((J.win_w - 1) * J.scale_x) + 4);
+    case RESIZE_NEAREST: return std::min(J.crop_w, (int)std::ceil((J.win_w - 1) * J.scale_x) + 3);
+    case RESIZE_AREA2X: return 2 * J.win_w;
+    default: return J.win_w;
+    }
+}
+int stage_rows_for(const AugJob& J, int tr)
+{
+    int rows = std::min(tr, J.win_h);
+    switch (J.mode) {
+    case RESIZE_LINEAR: return std::min(J.crop_h, (int)std::ceil((rows - 1) * J.scale_y) + 4);
+    case RESIZE_NEAREST: return std::min(J.crop_h, (int)std::ceil((rows - 1) * J.scale_y) + 3);
+    case RESIZE_AREA2X: return 2 * rows;
+    default: return rows;
+    }
+}
+
+struct LaunchPlan {
+    std::vector<AugJob> jobs;
+    int                 tr = 1, stage_rows = 0, stage_pitch = 0, max_win_w = 0, max_tiles = 0;
+    int                 lds = 0;
+    bool                vec_ok = true;
+    int                 stats_slots = 0;
+
+    void finalize()
+    {
+        if (jobs.empty()) return;
+        static const int trs[] = {32, 16, 8, 4, 2, 1};
+        int              budget = kStageBudget;
+        for (int pass = 0; pass < 2; pass++) {
+            for (int tr : trs) {
+                int rows = 0, pitch = 0, ww = 0;
+                for (const AugJob& J : jobs) {
+                    rows  = std::max(rows, stage_rows_for(J, tr));
+                    pitch = std::max(pitch, (stage_cols(J) + 3) & ~3);
+                    ww    = std::max(ww, J.win_w);
+                }
+                if ((long)rows * pitch * 4 <= budget || (tr == 1 && pass == 1)) {
+                    this->tr = tr, stage_rows = rows, stage_pitch = pitch, max_win_w = ww;
+                    lds = lds_layout(max_win_w, tr, stage_rows, stage_pitch).total;
+                    if (lds <= budget + 16 * 1024 || pass == 1) goto chosen;
+                }
+            }
+            budget = kStageBudgetHi;
+        }
+    chosen:
+        if (lds > kMaxLds)
+            fail(AEON_HIP_EUNSUPPORTED, "source crop too wide for one LDS-staged row band (" +
+                                            std::to_string(lds) + " bytes)");
+        max_tiles = 0;
+        for (AugJob& J : jobs) {
+            J.tiles   = (J.win_h + tr - 1) / tr;
+            max_tiles = std::max(max_tiles, J.tiles);
+        }
+    }
+};
+
+// Geometry + constants of one image-provider record (transform_single_image).
+void plan_image(const aeon_img_desc& d, const void* src_base, const aeon_aug_params& p,
+                const aeon_out_desc& o, uint8_t* out_item, bool is_mask, LaunchPlan& pre,
+                LaunchPlan& main, size_t& scratch_bytes, std::vector<size_t>& scratch_off)
+{
+    const int cn = d.channels;
+    if (cn != 1 && cn != 3) fail(AEON_HIP_EINVAL, "channels must be 1 or 3");
+    if (cn != o.channels) fail(AEON_HIP_EINVAL, "decoded channels do not match the output config");
+    if (d.width <= 0 || d.height <= 0 || d.stride < d.width * cn)
+        fail(AEON_HIP_EINVAL, "invalid source image descriptor");
+    if (p.angle != 0)
+        fail(AEON_HIP_EUNSUPPORTED, "rotation (angle != 0) is not implemented in the HIP stage");
+    const int interp = is_mask ? AEON_INTERP_NEAREST : p.interp;
+    if (interp != AEON_INTERP_LINEAR && interp != AEON_INTERP_NEAREST)
+        fail(AEON_HIP_EUNSUPPORTED, "only LINEAR and NEAREST interpolation are implemented");
+    if (p.out_w <= 0 || p.out_h <= 0) fail(AEON_HIP_EINVAL, "invalid output size");
+    const size_t elem = o.dtype == AEON_DTYPE_F32 ? 4 : 1;
+    if ((size_t)p.out_w * p.out_h * cn * elem > o.item_stride)
+        fail(AEON_HIP_EINVAL, "output item does not fit item_stride");
+
+    AugJob J{};
+    J.src_ptr    = (uint64_t)((const uint8_t*)src_base + d.offset);
+    J.src_bytes  = (uint64_t)d.stride * d.height;
+    J.src_w      = d.width, J.src_h = d.height, J.src_stride = d.stride, J.cn = cn;
+    J.stats_slot = -1;
+
+    int base_w = d.width, base_h = d.height;
+    if (!is_mask && p.resize_short_size > 0) {
+        // image::resize_short (image.cpp:118-127) into a device scratch, cropbox window only
+        int rw, rh;
+        get_resized_short_size(d.width, d.height, p.resize_short_size, &rw, &rh);
+        if (p.crop_x < 0 || p.crop_y < 0 || p.crop_w <= 0 || p.crop_h <= 0 ||
+            p.crop_x + p.crop_w > rw || p.crop_y + p.crop_h > rh)
+            fail(AEON_HIP_EINVAL, "cropbox outside the resize_short image");
+        AugJob P = J;
+        P.crop_x = 0, P.crop_y = 0, P.crop_w = d.width, P.crop_h = d.height;
+        P.mode    = choose_mode(d.width, d.height, rw, rh, interp, cn);
+        P.scale_x = 1. / ((double)rw / d.width);
+        P.scale_y = 1. / ((double)rh / d.height);
+        P.dst_w = rw, P.dst_h = rh;
+        P.win_x = p.crop_x, P.win_y = p.crop_y, P.win_w = p.crop_w, P.win_h = p.crop_h;
+        P.xv      = simd_boundary(rw * cn);
+        size_t off = (scratch_bytes + 15) & ~(size_t)15;
+        scratch_bytes = off + (size_t)p.crop_w * p.crop_h * cn + 16;
+        scratch_off.push_back(off);
+        P.out_ptr = off; // relocated to the slot's scratch by the caller
+        pre.jobs.push_back(P);
+        J.src_ptr = off; // likewise
+        J.src_bytes  = (uint64_t)p.crop_w * p.crop_h * cn;
+        J.src_w = p.crop_w, J.src_h = p.crop_h, J.src_stride = p.crop_w * cn;
+        J.crop_x = 0, J.crop_y = 0;
+        J.src_scratch = 1; // relocated to the slot's scratch by the caller
+        base_w = p.crop_w, base_h = p.crop_h;
+    } else {
+        if (p.crop_x < 0 || p.crop_y < 0 || p.crop_w <= 0 || p.crop_h <= 0 ||
+            p.crop_x + p.crop_w > base_w || p.crop_y + p.crop_h > base_h)
+            fail(AEON_HIP_EINVAL, "cropbox outside image");
+        J.crop_x = p.crop_x, J.crop_y = p.crop_y;
+    }
+    J.crop_w = p.crop_w, J.crop_h = p.crop_h;
+    if (!is_mask && !(p.padding == 0 || (p.pad_off_x == p.padding && p.pad_off_y == p.padding))) {
+        J.shift_x = p.pad_off_x - p.padding;
+        J.shift_y = p.pad_off_y - p.padding;
+        J.padded  = 1;
+    }
+    J.mode    = choose_mode(J.crop_w, J.crop_h, p.out_w, p.out_h, interp, cn);
+    J.scale_x = 1. / ((double)p.out_w / J.crop_w);
+    J.scale_y = 1. / ((double)p.out_h / J.crop_h);
+    J.dst_w = p.out_w, J.dst_h = p.out_h;
+    J.win_x = 0, J.win_y = 0, J.win_w = p.out_w, J.win_h = p.out_h;
+    J.xv      = simd_boundary(p.out_w * cn);
+    J.flip    = p.flip ? 1 : 0;
+    J.out_ptr = (uint64_t)out_item;
+
+    if (!is_mask) {
+        int photo = 0;
+        if (p.brightness != 1.0 || p.saturation != 1.0) photo |= PHOTO_BS;
+        if (p.hue != 0) photo |= PHOTO_HUE;
+        if (p.contrast != 1.0) photo |= PHOTO_CONTRAST;
+        if (p.n_lighting > 0) photo |= PHOTO_LIGHTING;
+        if (photo && cn != 3)
+            fail(AEON_HIP_EINVAL, "photometric augmentation needs a 3-channel image");
+        if (photo & PHOTO_BS) plan_bs(J, p.brightness, p.saturation);
+        J.contrast = p.contrast;
+        J.hue      = p.hue;
+        if (photo & PHOTO_LIGHTING) {
+            if (p.n_lighting != 3) fail(AEON_HIP_EINVAL, "lighting needs 3 values");
+            plan_lighting(J, p.lighting, p.color_noise_std);
+        }
+        if (photo & PHOTO_CONTRAST) J.stats_slot = main.stats_slots++;
+        J.photo = photo;
+    }
+    if ((J.out_ptr & 15) != 0 || (J.win_w & 3) != 0) main.vec_ok = false;
+    main.jobs.push_back(J);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Context: per-GPU state and a 4-deep staging ring (pinned host blob -> device blob per call)
+// ---------------------------------------------------------------------------------------------
+struct Slot {
+    hipEvent_t done     = nullptr;
+    bool       pending  = false;
+    uint8_t*   host     = nullptr;
+    size_t     host_cap = 0;
+    uint8_t*   dev      = nullptr;
+    size_t     dev_cap  = 0;
+    uint8_t*   scratch  = nullptr;
+    size_t     scratch_cap = 0;
+    uint32_t*  partials = nullptr;
+    size_t     partials_cap = 0;
+};
+
+} // namespace
+
+struct KernelTimer {
+    hipEvent_t start, stop;
+    int        kind;   // KernelMode
+    double     bytes;  // algorithmic bytes of the launch
+};
+
+struct aeon_hip_ctx {
+    int        device = 0;
+    int32_t*   d_error = nullptr;
+    int32_t*   d_hsv   = nullptr;
+    Slot       slots[4];
+    int        next = 0;
+    std::mutex mu;
+    // optional per-launch timing (aeon_hip_set_timing): events recorded on the launch stream
+    bool                     timing = false;
+    std::vector<KernelTimer> timers, free_timers;
+    double                   ms[3]    = {0, 0, 0};
+    double                   bytes[3] = {0, 0, 0};
+    long                     count[3] = {0, 0, 0};
+};
+
+struct aeon_param_factory {
+    param_factory f;
+    explicit aeon_param_factory(const Json& j) : f(j) {}
+};
+
+namespace {
+
+void grow(uint8_t*& p, size_t& cap, size_t need, bool pinned)
+{
+    if (need <= cap) return;
+    size_t n = std::max(need, cap * 2);
+    if (p) HIP_OK(pinned ? hipHostFree(p) : hipFree(p));
+    p   = nullptr;
+    cap = 0;
+    if (pinned) HIP_OK(hipHostMalloc((void**)&p, n, hipHostMallocDefault));
+    else HIP_OK(hipMalloc((void**)&p, n));
+    cap = n;
+}
+
+// Algorithmic bytes of one launch: the resampled u8 source footprint plus
+// the bytes written (KM_STATS writes nothing but re-reads the footprint).
+double launch_bytes(const LaunchPlan& L, int mode, size_t out_elem)
+{
+    double b = 0;
+    for (const AugJob& J : L.jobs) {
+        double rd = (double)J.crop_w * J.crop_h * J.cn;
+        if (J.mode == RESIZE_LINEAR || J.mode == RESIZE_NEAREST) {
+            // a window of the resize target reads only its share of the source
+            rd *= ((double)J.win_w / J.dst_w) * ((double)J.win_h / J.dst_h);
+        }
+        double wr = mode == KM_STATS ? 0.0
+                                     : (double)J.win_w * J.win_h * J.cn * (mode == KM_RAW ? 1 : out_elem);
+        b += rd + wr;
+    }
+    return b;
+}
+
+void timed_launch(aeon_hip_ctx* ctx, int mode, const LaunchArgs& a, int n, hipStream_t stream, double bytes)
+{
+    KernelTimer t{};
+    if (ctx->timing) {
+        if (!ctx->free_timers.empty()) {
+            t = ctx->free_timers.back();
+            ctx->free_timers.pop_back();
+        } else {
+            HIP_OK(hipEventCreate(&t.start));
+            HIP_OK(hipEventCreate(&t.stop));
+        }
+        t.kind  = mode;
+        t.bytes = bytes;
+        HIP_OK(hipEventRecord(t.start, stream));
+    }
+    HIP_OK(launch_tiles(mode, a, n, stream));
+    if (ctx->timing) {
+        HIP_OK(hipEventRecord(t.stop, stream));
+        ctx->timers.push_back(t);
+    }
+}
+
+int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* src_base,
+              const aeon_aug_params* params, const aeon_out_desc* out, void* out_dev, void* stream_,
+              bool is_mask)
+{
+    if (!ctx || n < 0 || (n > 0 && (!descs || !params || !out || !out_dev || !src_base)))
+        fail(AEON_HIP_EINVAL, "null argument");
+    if (n == 0) return 0;
+    if (n > 65535) fail(AEON_HIP_EINVAL, "at most 65535 records per call");
+    const aeon_out_desc& o = *out;
+    if (o.dtype != AEON_DTYPE_U8 && o.dtype != AEON_DTYPE_F32)
+        fail(AEON_HIP_EUNSUPPORTED, "output dtype must be uint8 or float32");
+    if (o.has_mean && o.dtype != AEON_DTYPE_F32)
+        fail(AEON_HIP_EINVAL,
+             "Standardization (mean, stddev) is supported only for float or double 'output_type'.");
+    if (o.bgr_to_rgb && o.channels != 3)
+        fail(AEON_HIP_EINVAL, "invalid config: bgr_to_rgb can be 'true' only for channels set to '3'");
+    hipStream_t stream = (hipStream_t)stream_;
+
+    std::lock_guard<std::mutex> lock(ctx->mu);
+    HIP_OK(hipSetDevice(ctx->device));
+
+    LaunchPlan          pre, main;
+    size_t              scratch_bytes = 0;
+    std::vector<size_t> scratch_off;
+    for (int i = 0; i < n; i++)
+        plan_image(descs[i], src_base, params[i], o, (uint8_t*)out_dev + (size_t)i * o.item_stride,
+                   is_mask, pre, main, scratch_bytes, scratch_off);
+    pre.finalize();
+    main.finalize();
+
+    Slot& s = ctx->slots[ctx->next];
+    ctx->next = (ctx->next + 1) % 4;
+    if (s.pending) {
+        HIP_OK(hipEventSynchronize(s.done));
+        s.pending = false;
+    }
+    const size_t lut_bytes  = 4096;
+    const size_t pre_bytes  = pre.jobs.size() * sizeof(AugJob);
+    const size_t main_bytes = main.jobs.size() * sizeof(AugJob);
+    const size_t blob       = lut_bytes + pre_bytes + main_bytes;
+    grow(s.host, s.host_cap, blob, true);
+    grow(s.dev, s.dev_cap, blob, false);
+    grow(s.scratch, s.scratch_cap, std::max<size_t>(scratch_bytes, 16), false);
+    size_t part_bytes = (size_t)std::max(main.stats_slots, 1) * std::max(main.max_tiles, 1) * 16;
+    {
+        uint8_t* p = (uint8_t*)s.partials;
+        grow(p, s.partials_cap, part_bytes, false);
+        s.partials = (uint32_t*)p;
+    }
+    // relocate scratch references
+    for (AugJob& P : pre.jobs) P.out_ptr += (uint64_t)s.scratch;
+    for (AugJob& J : main.jobs)
+        if (J.src_scratch) J.src_ptr += (uint64_t)s.scratch;
+    build_lut(o, (float*)s.host);
+    std::memcpy(s.host + lut_bytes, pre.jobs.data(), pre_bytes);
+    std::memcpy(s.host + lut_bytes + pre_bytes, main.jobs.data(), main_bytes);
+    HIP_OK(hipMemcpyAsync(s.dev, s.host, blob, hipMemcpyHostToDevice, stream));
+
+    auto args = [&](const LaunchPlan& L, const AugJob* jobs) {
+        LaunchArgs a{};
+        a.jobs          = jobs;
+        a.lut           = (o.dtype == AEON_DTYPE_F32 && o.has_mean) ? (const float*)s.dev : nullptr;
+        a.hsv_tables    = ctx->d_hsv;
+        a.partials      = s.partials;
+        a.error         = ctx->d_error;
+        a.rows_per_tile = L.tr;
+        a.max_tiles     = L.max_tiles;
+        a.stage_rows    = L.stage_rows;
+        a.stage_pitch   = L.stage_pitch;
+        a.max_win_w     = L.max_win_w;
+        a.out_dtype     = o.dtype == AEON_DTYPE_F32 ? OUT_F32 : OUT_U8;
+        a.channel_major = o.channel_major;
+        a.bgr_to_rgb    = o.bgr_to_rgb;
+        a.vec_ok        = L.vec_ok && o.channel_major;
+        a.lds_bytes     = L.lds;
+        return a;
+    };
+    const size_t oelem = o.dtype == AEON_DTYPE_F32 ? 4 : 1;
+    if (!pre.jobs.empty()) {
+        LaunchArgs a = args(pre, (const AugJob*)(s.dev + lut_bytes));
+        timed_launch(ctx, KM_RAW, a, (int)pre.jobs.size(), stream, launch_bytes(pre, KM_RAW, 1));
+    }
+    const AugJob* mj = (const AugJob*)(s.dev + lut_bytes + pre_bytes);
+    if (main.stats_slots > 0)
+        timed_launch(ctx, KM_STATS, args(main, mj), (int)main.jobs.size(), stream,
+                     launch_bytes(main, KM_STATS, oelem));
+    timed_launch(ctx, KM_FINAL, args(main, mj), (int)main.jobs.size(), stream,
+                 launch_bytes(main, KM_FINAL, oelem));
+    HIP_OK(hipEventRecord(s.done, stream));
+    s.pending = true;
+    return 0;
+}
+
+// std::minstd_rand0 whose state word can be read back (an LCG's state is its last output).
+struct TrackedEngine {
+    using result_type = std::minstd_rand0::result_type;
+    std::minstd_rand0 e;
+    result_type       last;
+    static constexpr result_type min() { return std::minstd_rand0::min(); }
+    static constexpr result_type max() { return std::minstd_rand0::max(); }
+    explicit TrackedEngine(uint32_t s) : e(s), last(s % 2147483647u == 0 ? 1 : s % 2147483647u) {}
+    result_type operator()() { return last = e(); }
+};
+
+template <typename F>
+int guarded(F&& f)
+{
+    try {
+        return f();
+    } catch (const aeon_error& e) {
+        g_err = e.what();
+        return e.code;
+    } catch (const std::invalid_argument& e) {
+        g_err = e.what();
+        return AEON_HIP_EINVAL;
+    } catch (const std::exception& e) {
+        g_err = e.what();
+        return AEON_HIP_ERUNTIME;
+    }
+}
+
+} // namespace
+
+extern "C" {
+
+int aeon_hip_ctx_create(int device, aeon_hip_ctx** out)
+{
+    return guarded([&] {
+        if (!out) fail(AEON_HIP_EINVAL, "null out");
+        auto* c   = new aeon_hip_ctx();
+        c->device = device;
+        try {
+            HIP_OK(hipSetDevice(device));
+            HIP_OK(set_kernel_lds_limit(kMaxLds));
+            HIP_OK(hipMalloc((void**)&c->d_error, sizeof(int32_t)));
+            HIP_OK(hipMemset(c->d_error, 0, sizeof(int32_t)));
+            // RGB2HSV_b division tables (hsv_shift = 12), as OpenCV builds them
+            int32_t tab[512];
+            tab[0] = tab[256] = 0;
+            for (int i = 1; i < 256; i++) {
+                tab[i]       = cv_round((255 << 12) / (1. * i));
+                tab[256 + i] = cv_round((180 << 12) / (6. * i));
+            }
+            HIP_OK(hipMalloc((void**)&c->d_hsv, sizeof(tab)));
+            HIP_OK(hipMemcpy(c->d_hsv, tab, sizeof(tab), hipMemcpyHostToDevice));
+            for (Slot& s : c->slots) HIP_OK(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
+        } catch (...) {
+            delete c;
+            throw;
+        }
+        *out = c;
+        return 0;
+    });
+}
+
+int aeon_hip_ctx_destroy(aeon_hip_ctx* c)
+{
+    return guarded([&] {
+        if (!c) return 0;
+        (void)hipSetDevice(c->device);
+        for (Slot& s : c->slots) {
+            if (s.pending) (void)hipEventSynchronize(s.done);
+            if (s.done) (void)hipEventDestroy(s.done);
+            if (s.host) (void)hipHostFree(s.host);
+            if (s.dev) (void)hipFree(s.dev);
+            if (s.scratch) (void)hipFree(s.scratch);
+            if (s.partials) (void)hipFree(s.partials);
+        }
+        for (auto* v : {&c->timers, &c->free_timers})
+            for (KernelTimer& t : *v) (void)hipEventDestroy(t.start), (void)hipEventDestroy(t.stop);
+        if (c->d_error) (void)hipFree(c->d_error);
+        if (c->d_hsv) (void)hipFree(c->d_hsv);
+        delete c;
+        return 0;
+    });
+}
+
+int aeon_hip_augment_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* src_base,
+                           const aeon_aug_params* params, const aeon_out_desc* out, void* out_dev,
+                           void* stream)
+{
+    return guarded([&] { return run_batch(ctx, n, descs, src_base, params, out, out_dev, stream, false); });
+}
+
+int aeon_hip_mask_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* src_base,
+                        const aeon_aug_params* params, const aeon_out_desc* out, void* out_dev,
+                        void* stream)
+{
+    return guarded([&] { return run_batch(ctx, n, descs, src_base, params, out, out_dev, stream, true); });
+}
+
+int aeon_hip_synchronize(aeon_hip_ctx* ctx, void* stream)
+{
+    return guarded([&] {
+        if (!ctx) fail(AEON_HIP_EINVAL, "null ctx");
+        HIP_OK(hipSetDevice(ctx->device));
+        HIP_OK(hipStreamSynchronize((hipStream_t)stream));
+        int32_t err = 0;
+        HIP_OK(hipMemcpy(&err, ctx->d_error, sizeof(err), hipMemcpyDeviceToHost));
+        if (err != 0) {
+            HIP_OK(hipMemset(ctx->d_error, 0, sizeof(int32_t)));
+            fail(AEON_HIP_EDEVICE, "device error word " + std::to_string(err) +
+                                       " (LDS staging footprint exceeded)");
+        }
+        return 0;
+    });
+}
+
+int aeon_hip_set_timing(aeon_hip_ctx* ctx, int enable)
+{
+    return guarded([&] {
+        if (!ctx) fail(AEON_HIP_EINVAL, "null ctx");
+        std::lock_guard<std::mutex> lock(ctx->mu);
+        ctx->timing = enable != 0;
+        return 0;
+    });
+}
+
+int aeon_hip_kernel_times(aeon_hip_ctx* ctx, double* ms, double* bytes, long* count)
+{
+    return guarded([&] {
+        if (!ctx || !ms || !bytes || !count) fail(AEON_HIP_EINVAL, "null argument");
+        std::lock_guard<std::mutex> lock(ctx->mu);
+        HIP_OK(hipSetDevice(ctx->device));
+        for (KernelTimer& t : ctx->timers) {
+            HIP_OK(hipEventSynchronize(t.stop));
+            float e = 0;
+            HIP_OK(hipEventElapsedTime(&e, t.start, t.stop));
+            ctx->ms[t.kind] += e;
+            ctx->bytes[t.kind] += t.bytes;
+            ctx->count[t.kind] += 1;
+            ctx->free_timers.push_back(t);
+        }
+        ctx->timers.clear();
+        for (int k = 0; k < 3; k++) {
+            ms[k] = ctx->ms[k], bytes[k] = ctx->bytes[k], count[k] = ctx->count[k];
+            ctx->ms[k] = ctx->bytes[k] = 0, ctx->count[k] = 0;
+        }
+        return 0;
+    });
+}
+
+int aeon_param_factory_create(const char* aug_json, aeon_param_factory** out)
+{
+    return guarded([&] {
+        if (!out) fail(AEON_HIP_EINVAL, "null out");
+        Json j = aug_json && *aug_json ? Json::parse(aug_json) : Json();
+        *out   = new aeon_param_factory(j);
+        return 0;
+    });
+}
+
+int aeon_param_factory_destroy(aeon_param_factory* f)
+{
+    delete f;
+    return 0;
+}
+
+int aeon_make_params(aeon_param_factory* f, uint32_t* state, int in_w, int in_h, int out_w, int out_h,
+                     aeon_aug_params* out)
+{
+    return guarded([&] {
+        if (!f || !state || !out) fail(AEON_HIP_EINVAL, "null argument");
+        TrackedEngine eng(*state);
+        f->f.make_params(eng, in_w, in_h, out_w, out_h, out);
+        *state = eng.last;
+        return 0;
+    });
+}
+
+int aeon_seed_slots(uint32_t seed, int n, uint32_t* states)
+{
+    return guarded([&] {
+        if (n < 0 || (n > 0 && !states)) fail(AEON_HIP_EINVAL, "bad arguments");
+        std::minstd_rand0 g(seed);
+        for (int i = 0; i < n; i++) {
+            uint32_t s = g() % 2147483647u;
+            states[i]  = s == 0 ? 1 : s;
+        }
+        return 0;
+    });
+}
+
+int aeon_hip_host_alloc(size_t bytes, void** out)
+{
+    return guarded([&] {
+        if (!out) fail(AEON_HIP_EINVAL, "null out");
+        HIP_OK(hipHostMalloc(out, bytes, hipHostMallocDefault));
+        return 0;
+    });
+}
+
+int aeon_hip_host_free(void* p)
+{
+    return guarded([&] {
+        if (p) HIP_OK(hipHostFree(p));
+        return 0;
+    });
+}
+
+const char* aeon_hip_last_error(void) { return g_err.c_str(); }
+const char* aeon_hip_version(void) { return "aeon-hip 0.1 (gfx950)"; }
+
+} // extern "C"

@@ -1,0 +1,276 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X image-augmentation stage (BASELINE.json metric).
+
+A "step" = one decode window of `batch` records through the HIP stage: random crop + flip +
+bilinear resize to 224x224 (+ photometric for C3), standardize, CHW fp32, with the decoded
+HWC uint8 sources already resident in HBM (device-resident metric).  The source pool spans
+more than the 256 MiB Infinity Cache so every step streams its sources from HBM.
+Augmentation parameters come from aeon's deterministic mode (random_seed 1 + node_id,
+one minstd_rand0 per decode slot) and are drawn on the host before the timed region.
+
+N GPUs: one process per GPU (torch.distributed.run), each an independent manifest slice
+(node_id = rank, node_count = N): no data-path collective; barrier + max-over-ranks timing.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "augmented images/s device-resident, 224×224 batch 256; achieved HBM GB/s"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="C2", choices=["C2", "C3"])
+    ap.add_argument("--batch", type=int, default=0, help="records per step (default: config's)")
+    ap.add_argument("--pool-mib", type=int, default=400, help="source pool size per GPU")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline sample budget")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extra", action="store_true", help="skip the C3 and end-to-end side runs")
+    ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
+    return ap.parse_args()
+
+
+class Workload:
+    """Synthetic already-decoded sources in HBM + pre-drawn params for every step."""
+
+    def __init__(self, A, C, torch, cfg, batch, steps, rank, pool_mib, src_wh=(256, 256)):
+        self.batch = batch
+        self.aug = {"C2": C.C2_AUG, "C3": C.C3_AUG}[cfg]
+        w, h = src_wh
+        img_bytes = w * h * 3
+        per_batch = batch * img_bytes
+        self.n_pool = max(1, (pool_mib << 20) // per_batch)
+        gen = torch.Generator(device="cuda")
+        gen.manual_seed(0x5EED + rank)
+        self.src = torch.randint(0, 256, (self.n_pool * per_batch,), dtype=torch.uint8,
+                                 device="cuda", generator=gen)
+        self.descs = [[A.ImgDesc(offset=(b * batch + i) * img_bytes, width=w, height=h, stride=w * 3,
+                                 channels=3) for i in range(batch)] for b in range(self.n_pool)]
+        self.out = C.out_desc_for(C.IMAGE_224, self.aug)
+        self.dst = [torch.empty(batch * self.out.item_stride, dtype=torch.uint8, device="cuda")
+                    for _ in range(2)]
+        # aeon deterministic mode: decoder seed = random_seed + node_id (src/loader.cpp:174),
+        # one engine per decode slot, persisting across windows (src/batch_decoder.cpp:47-70)
+        f = A.ParamFactory(self.aug)
+        states = A.seed_slots(1 + rank, batch)
+        t0 = time.perf_counter()
+        self.params = []
+        for s in range(steps):
+            ps = []
+            for i in range(batch):
+                st = states[i:i + 1]
+                ps.append(f.make_params(st, w, h, 224, 224))
+                states[i] = st[0]
+            self.params.append(ps)
+        self.param_us = (time.perf_counter() - t0) / max(1, steps * batch) * 1e6
+
+    def step(self, ctx, s, stream):
+        b = s % self.n_pool
+        ctx.augment_batch(self.descs[b], self.src.data_ptr(), self.params[s], self.out,
+                          self.dst[s & 1].data_ptr(), stream)
+
+
+def run_device(A, C, torch, cfg, batch, steps, warmup, rank, world, pool_mib, dist):
+    ctx = A.Context(torch.cuda.current_device())
+    wl = Workload(A, C, torch, cfg, batch, steps + warmup, rank, pool_mib)
+    stream = torch.cuda.current_stream().cuda_stream
+    for s in range(warmup):
+        wl.step(ctx, s, stream)
+    ctx.synchronize(stream)
+    ctx.kernel_times()  # drop warmup timings
+    ctx.set_timing(True)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for s in range(warmup, warmup + steps):
+        wl.step(ctx, s, stream)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    ctx.synchronize(stream)
+    kt = ctx.kernel_times()
+    ctx.set_timing(False)
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ctx.close()
+    return elapsed, kt, wl.param_us
+
+
+def run_e2e(A, C, torch, batch, steps):
+    """Host->host rate: pinned decoded pixels -> H2D -> kernel -> D2H into a pinned batch
+    buffer, with copies and kernels on separate streams (PCIe-inclusive)."""
+    ctx = A.Context(torch.cuda.current_device())
+    w = h = 256
+    img_bytes = w * h * 3
+    out = C.out_desc_for(C.IMAGE_224, C.C2_AUG)
+    host_src = [torch.randint(0, 256, (batch * img_bytes,), dtype=torch.uint8).pin_memory() for _ in range(2)]
+    host_dst = [torch.empty(batch * out.item_stride, dtype=torch.uint8).pin_memory() for _ in range(2)]
+    dev_src = [torch.empty(batch * img_bytes, dtype=torch.uint8, device="cuda") for _ in range(2)]
+    dev_dst = [torch.empty(batch * out.item_stride, dtype=torch.uint8, device="cuda") for _ in range(2)]
+    descs = [A.ImgDesc(offset=i * img_bytes, width=w, height=h, stride=w * 3, channels=3) for i in range(batch)]
+    f = A.ParamFactory(C.C2_AUG)
+    states = A.seed_slots(1, batch)
+    params = [[f.make_params(states[i:i + 1], w, h, 224, 224) for i in range(batch)] for _ in range(4)]
+    s_h2d, s_k, s_d2h = torch.cuda.Stream(), torch.cuda.Stream(), torch.cuda.Stream()
+    ev_in = [torch.cuda.Event() for _ in range(2)]
+    ev_k = [torch.cuda.Event() for _ in range(2)]
+    ev_out = [torch.cuda.Event() for _ in range(2)]
+
+    def one(s):
+        j = s & 1
+        with torch.cuda.stream(s_h2d):
+            s_h2d.wait_event(ev_k[j])  # previous kernel on this buffer done reading
+            dev_src[j].copy_(host_src[j], non_blocking=True)
+            ev_in[j].record(s_h2d)
+        s_k.wait_event(ev_in[j])
+        s_k.wait_event(ev_out[j])  # previous D2H of this buffer done
+        ctx.augment_batch(descs, dev_src[j].data_ptr(), params[s % 4], out, dev_dst[j].data_ptr(),
+                          s_k.cuda_stream)
+        ev_k[j].record(s_k)
+        with torch.cuda.stream(s_d2h):
+            s_d2h.wait_event(ev_k[j])
+            host_dst[j].copy_(dev_dst[j], non_blocking=True)
+            ev_out[j].record(s_d2h)
+
+    for s in range(2):
+        one(s)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for s in range(steps):
+        one(s)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    ctx.close()
+    return batch * steps / dt
+
+
+def cpu_baseline(A, C, budget_s):
+    """aeon's CPU path restated (oracle/, C++): thread pool of hc - min(2, hc/8) workers with a
+    dynamic atomic task counter (src/util.cpp:360-370, src/thread_pool.hpp:155-162)."""
+    import oracle as O
+    from tests import helpers as H
+    hc = int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
+    threads = max(1, hc - min(2, hc // 8))
+    n = 256
+    imgs = [A.synthetic_image(i, 256, 256, 3) for i in range(n)]
+    params = H.draw_params(C.C2_AUG, [(256, 256)] * n, 224, 224, seed=1)
+    q = [H.to_oracle_params(p) for p in params]
+    lc = H.oracle_load_config(C.out_desc_for(C.IMAGE_224, C.C2_AUG))
+    done, secs = 0, 0.0
+    while secs < budget_s:
+        _, dt = O.batch_augment(imgs, q, lc, (3, 224, 224), threads)
+        secs += dt
+        done += n
+    cpu = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                cpu = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"value": done / secs, "unit": "images/s", "cores": threads, "kind": "port",
+            "sample": f"C2 on {done} synthetic 256x256 records ({secs:.1f} s CPU wall), oracle/ C++ "
+                      f"restatement of aeon's transform+load on {threads} pool threads; CPU: {cpu}"}
+
+
+def load_traffic(path, cfg):
+    try:
+        d = json.load(open(path))
+        return d.get(cfg, {}).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def main():
+    args = parse()
+    import torch
+    import aeon_amd as A
+    from aeon_amd import configs as C
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", rank=rank, world_size=world,
+                                device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    batch = args.batch or C.CONFIGS[args.config]["batch_size"]
+
+    elapsed, kt, param_us = run_device(A, C, torch, args.config, batch, args.steps, args.warmup, rank,
+                                       world, args.pool_mib, dist)
+    total = batch * args.steps * world
+    value = total / elapsed
+    k_ms, k_bytes, k_n = kt["augment"]
+    achieved = (k_bytes / k_n) / (k_ms / k_n * 1e-3) / 1e9 if k_n else 0.0
+
+    extra = {}
+    if rank == 0 and world == 1 and not args.no_extra:
+        if args.config == "C2":
+            e3, kt3, _ = run_device(A, C, torch, "C3", 1024, max(5, args.steps // 5), 2, 0, 1,
+                                    args.pool_mib, None)
+            m3, b3, n3 = kt3["augment"]
+            s3 = kt3["stats"]
+            extra["C3"] = {"value": 1024 * max(5, args.steps // 5) / e3, "unit": "images/s",
+                           "batch": 1024, "augment_kernel_ms": m3 / max(n3, 1),
+                           "stats_kernel_ms": s3[0] / max(s3[2], 1),
+                           "augment_kernel_gbs": (b3 / max(n3, 1)) / (m3 / max(n3, 1) * 1e-3) / 1e9 if n3 else 0}
+        extra["e2e_host_to_host"] = {"value": run_e2e(A, C, torch, 256, 20), "unit": "images/s",
+                                     "what": "pinned H2D of decoded 256x256 u8 + kernel + D2H of fp32 CHW"}
+
+    line = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "images/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic: counter-free torch.randint HWC u8 256x256 sources resident in HBM",
+        "config": {"workload": f"{args.config}: " + {
+            "C2": "random crop + flip + bilinear resize to 224x224, standardize, CHW fp32",
+            "C3": "full augment_image (brightness/contrast/saturation/hue/lighting), CHW fp32"}[args.config],
+            "batch_per_gpu": batch, "global_batch": batch * world, "source": "256x256x3 u8 HWC",
+            "output": "3x224x224 float32 CHW", "parallelism": f"dp{world} (manifest node slices)"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS,
+                     "traffic": load_traffic(args.traffic_file, args.config),
+                     "kernel": "augment_tiles<KM_FINAL>", "kernel_ms": k_ms / max(k_n, 1),
+                     "algorithmic_bytes_per_launch": k_bytes / max(k_n, 1)},
+        "host_make_params_us_per_record": param_us,
+    }
+    if extra:
+        line["extra"] = extra
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(A, C, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

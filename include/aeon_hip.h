@@ -1,0 +1,140 @@
+/* aeon_hip.h -- C ABI of the MI355X (gfx950) image-augmentation stage for aeon.
+ *
+ * Drop-in boundary for aeon's decode hot path
+ *   batch_decoder::process (src/batch_decoder.cpp:62-71)
+ *     -> provider::image::provide (src/provider.cpp:160-184)
+ *        -> image::transformer::transform_single_image (src/etl_image.cpp:146-202)
+ *        -> image::loader::load (src/etl_image.cpp:246-341)
+ *     -> provider::pixelmask::provide (src/provider.cpp:365-393)
+ *        -> pixel_mask::transformer::transform (src/etl_pixel_mask.cpp:65-92)
+ * Host code keeps decode (image::extractor::extract) and seeded parameter sampling
+ * (param_factory::make_params) and calls these entry points once per decode window.
+ *
+ * Conventions: plain C types and pointers only; every function returns 0 on success or a
+ * negative AEON_HIP_E* code, with a thread-local message in aeon_hip_last_error().
+ * No C++ exception crosses this boundary.  `stream` is a hipStream_t (NULL = default stream).
+ * See INTEGRATION.md for the aeon-side call sites and a ctypes binding.
+ */
+#ifndef AEON_HIP_H
+#define AEON_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define AEON_HIP_OK 0
+#define AEON_HIP_EINVAL -1     /* invalid argument / configuration (aeon: std::invalid_argument) */
+#define AEON_HIP_ERUNTIME -2   /* HIP runtime failure (aeon: std::runtime_error) */
+#define AEON_HIP_EUNSUPPORTED -3 /* a feature this build does not implement (e.g. rotation) */
+#define AEON_HIP_EDEVICE -4    /* a kernel reported an inconsistency in its device error word */
+
+/* output element types (aeon output_type, src/typemap.hpp) */
+#define AEON_DTYPE_U8 0
+#define AEON_DTYPE_F32 1
+
+/* resize interpolation (image::config "interpolation_method") */
+#define AEON_INTERP_LINEAR 0
+#define AEON_INTERP_NEAREST 1
+
+typedef struct aeon_hip_ctx aeon_hip_ctx;
+typedef struct aeon_param_factory aeon_param_factory;
+
+/* One decoded source image, HWC uint8 (BGR for 3 channels, OpenCV imdecode layout), living in
+ * device memory at src_base + offset. Replaces cv::Mat image::decoded::get_image(0). */
+typedef struct aeon_img_desc {
+    uint64_t offset;   /* byte offset from the src_base passed to the batch call */
+    int32_t  width;    /* cols */
+    int32_t  height;   /* rows */
+    int32_t  stride;   /* bytes per row (>= width*channels) */
+    int32_t  channels; /* 1 or 3 */
+} aeon_img_desc;
+
+/* POD mirror of augment::image::params (src/augment_image.hpp:99-119): the fields the image
+ * and pixel-mask transformers read.  Produced by aeon_make_params (or by aeon itself). */
+typedef struct aeon_aug_params {
+    int32_t crop_x, crop_y, crop_w, crop_h; /* cropbox (cv::Rect) */
+    int32_t resize_short_size;              /* 0 = off */
+    int32_t out_w, out_h;                   /* output_size */
+    int32_t angle;                          /* rotation (degrees); only 0 supported here */
+    int32_t flip;                           /* horizontal flip after photometric */
+    int32_t padding, pad_off_x, pad_off_y;  /* padding + padding_crop_offset */
+    int32_t n_lighting;                     /* 0 or 3 */
+    float   lighting[3];                    /* PCA lighting alphas */
+    float   color_noise_std;                /* lighting stddev */
+    float   contrast, brightness, saturation;
+    int32_t hue;
+    int32_t interp;                         /* AEON_INTERP_* */
+} aeon_aug_params;
+
+/* image::loader configuration (src/etl_image.cpp:204-244) plus the batch-buffer geometry of
+ * fixed_buffer_map (src/buffer_batch.hpp:154-188). */
+typedef struct aeon_out_desc {
+    int32_t  dtype;         /* AEON_DTYPE_* */
+    int32_t  channels;      /* 1 or 3 */
+    int32_t  channel_major; /* 1: CHW planes, 0: HWC */
+    int32_t  bgr_to_rgb;    /* swap channels 0 and 2 (3-channel only) */
+    int32_t  has_mean;      /* standardize with mean/stddev (float output only) */
+    int32_t  reserved;
+    double   mean[3];
+    double   stddev[3];
+    uint64_t item_stride;   /* bytes between consecutive items of the batch buffer */
+} aeon_out_desc;
+
+/* ---- context ------------------------------------------------------------------------------ */
+/* Replaces the per-loader CPU decode state; one context per GPU (hipSetDevice(device)). */
+int aeon_hip_ctx_create(int device, aeon_hip_ctx** out);
+int aeon_hip_ctx_destroy(aeon_hip_ctx* ctx);
+
+/* ---- hot path ----------------------------------------------------------------------------- */
+/* The per-record body of provider::image::provide after extract + make_params, for n records
+ * at once: transform_single_image + image::loader::load of record i into
+ * out_dev + i*out->item_stride.  Asynchronous on `stream`; src/out must stay valid until the
+ * stream reaches this work.  descs/params are host arrays, consumed before return. */
+int aeon_hip_augment_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs,
+                           const void* src_base, const aeon_aug_params* params,
+                           const aeon_out_desc* out, void* out_dev, void* stream);
+
+/* provider::pixelmask::provide after extract: crop -> NEAREST resize -> flip -> load, with the
+ * SAME params as the image of the record (src/provider.cpp:378-391).  1-channel masks. */
+int aeon_hip_mask_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs,
+                        const void* src_base, const aeon_aug_params* params,
+                        const aeon_out_desc* out, void* out_dev, void* stream);
+
+/* Wait for `stream` and check the device error word of ctx. */
+int aeon_hip_synchronize(aeon_hip_ctx* ctx, void* stream);
+
+/* ---- measurement ---------------------------------------------------------------------------- */
+/* When enabled, every kernel launch is bracketed by HIP events on its own stream. */
+int aeon_hip_set_timing(aeon_hip_ctx* ctx, int enable);
+/* Drain the timers: per kernel kind [0]=augment (final), [1]=contrast statistics,
+ * [2]=resize_short pre-pass: total ms, total algorithmic bytes, launches. Resets the totals. */
+int aeon_hip_kernel_times(aeon_hip_ctx* ctx, double* ms, double* bytes, long* count);
+
+/* ---- augmentation parameters (host) ------------------------------------------------------- */
+/* augment::image::param_factory(json) (src/augment_image.cpp:28-89) from the JSON text of the
+ * "augmentation" object ({"type": "image", ...}).  Validators as aeon; like aeon (which skips
+ * verify_config here, src/augment_image.cpp:50) unknown keys are ignored. */
+int aeon_param_factory_create(const char* aug_json, aeon_param_factory** out);
+int aeon_param_factory_destroy(aeon_param_factory* f);
+/* param_factory::make_params (src/augment_image.cpp:107-230) drawing from the minstd_rand0
+ * engine whose state word is *engine_state (updated in place). */
+int aeon_make_params(aeon_param_factory* f, uint32_t* engine_state, int in_w, int in_h,
+                     int out_w, int out_h, aeon_aug_params* out);
+/* batch_decoder deterministic mode (src/batch_decoder.cpp:47-54): slot engine state words. */
+int aeon_seed_slots(uint32_t seed, int n, uint32_t* states);
+
+/* ---- host staging (replaces the dead cuMemAllocHost branch, src/buffer_batch.cpp:150-186) -- */
+int aeon_hip_host_alloc(size_t bytes, void** out);
+int aeon_hip_host_free(void* p);
+
+const char* aeon_hip_last_error(void);
+const char* aeon_hip_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* AEON_HIP_H */

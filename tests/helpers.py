@@ -1,0 +1,100 @@
+"""Shared helpers: run the same records through the HIP stage and through the CPU oracle."""
+import numpy as np
+
+import aeon_amd as A
+import oracle as O
+
+
+def oracle_aug_config(aug):
+    """aeon augmentation JSON -> oracle AugConfig (the checker's own plain struct)."""
+    kw = {}
+    for key, lo, hi in (("scale", "scale_min", "scale_max"),
+                        ("horizontal_distortion", "hdist_min", "hdist_max"),
+                        ("contrast", "contrast_min", "contrast_max"),
+                        ("brightness", "brightness_min", "brightness_max"),
+                        ("saturation", "saturation_min", "saturation_max")):
+        if key in aug:
+            kw[lo], kw[hi] = aug[key]
+    if "angle" in aug:
+        kw["angle_min"], kw["angle_max"] = aug["angle"]
+    if "hue" in aug:
+        kw["hue_min"], kw["hue_max"] = aug["hue"]
+    if "lighting" in aug:
+        kw["lighting_mean"], kw["lighting_stddev"] = aug["lighting"]
+    for key in ("flip_enable", "center", "crop_enable", "do_area_scale"):
+        if key in aug:
+            kw[key] = int(aug[key])
+    for key in ("resize_short_size", "padding"):
+        if key in aug:
+            kw[key] = aug[key]
+    if "fixed_scaling_factor" in aug:
+        kw["fixed_scaling_factor"] = aug["fixed_scaling_factor"]
+    if aug.get("interpolation_method", "LINEAR").upper() == "NEAREST":
+        kw["interp"] = 1
+    return O.aug_config(**kw)
+
+
+def oracle_load_config(out):
+    """aeon_amd.OutDesc -> oracle LoadConfig."""
+    return O.load_config(out.channels, bool(out.channel_major), bool(out.bgr_to_rgb),
+                         "uint8" if out.dtype == A.DTYPE_U8 else "float32",
+                         list(out.mean) if out.has_mean else None,
+                         list(out.stddev) if out.has_mean else None)
+
+
+def to_oracle_params(p):
+    q = O.Params()
+    for f, _ in O.Params._fields_:
+        if f == "lighting":
+            for i in range(3):
+                q.lighting[i] = p.lighting[i]
+        else:
+            setattr(q, f, getattr(p, f))
+    return q
+
+
+def oracle_records(images, params, out, mask=False):
+    lc = oracle_load_config(out)
+    res = []
+    for im, p in zip(images, params):
+        q = to_oracle_params(p)
+        if mask:
+            m = O.transform_mask(im, q)
+            res.append(O.load_image(m[:, :, None], lc))
+        else:
+            res.append(O.augment_record(im, q, lc))
+    return res
+
+
+def hip_records(ctx, images, params, out, mask=False, dtype=None):
+    """Run records through the HIP stage on cuda:0; returns one array per record."""
+    import torch
+    arena, descs = A.pack_images(images)
+    src = torch.from_numpy(arena).to("cuda") if arena.size else torch.zeros(16, dtype=torch.uint8, device="cuda")
+    n = len(images)
+    dst = torch.zeros(max(n, 1) * out.item_stride, dtype=torch.uint8, device="cuda")
+    stream = torch.cuda.current_stream().cuda_stream
+    fn = ctx.mask_batch if mask else ctx.augment_batch
+    fn(descs, src.data_ptr(), params, out, dst.data_ptr(), stream)
+    ctx.synchronize(stream)
+    host = dst.cpu().numpy()
+    res = []
+    for i, p in enumerate(params):
+        cn = out.channels
+        shape = (cn, p.out_h, p.out_w) if out.channel_major else (p.out_h, p.out_w, cn)
+        dt = np.uint8 if out.dtype == A.DTYPE_U8 else np.float32
+        nbytes = int(np.prod(shape)) * np.dtype(dt).itemsize
+        item = host[i * out.item_stride: i * out.item_stride + nbytes].view(dt).reshape(shape)
+        res.append(item.copy())
+    return res
+
+
+def draw_params(aug, sizes, out_w, out_h, seed=1):
+    """make_params per record with aeon deterministic-mode slot engines (one per record)."""
+    f = A.ParamFactory(aug)
+    states = A.seed_slots(seed, len(sizes))
+    res = []
+    for i, (w, h) in enumerate(sizes):
+        st = states[i:i + 1].copy()
+        res.append(f.make_params(st, w, h, out_w, out_h))
+    return res

@@ -1,0 +1,201 @@
+"""GPU parity: the HIP stage (through the C ABI) against aeon's goldens and the CPU oracle.
+
+Bar (BASELINE.json north_star): the uint8 image before standardize is
+bit-exact; the fp32 output is compared bit-exactly too (the standardize LUT reproduces
+aeon's f64-per-op arithmetic, pinned by the goldens), i.e. tolerance 0 <= 1e-5.
+"""
+import numpy as np
+import pytest
+
+import aeon_amd as A
+from aeon_amd import configs as C
+from tests import helpers as H
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need a GPU"
+    c = A.Context(0)
+    yield c
+    c.close()
+
+
+def _assert_same(hip, ref, what):
+    assert len(hip) == len(ref)
+    for i, (a, b) in enumerate(zip(hip, ref)):
+        assert a.shape == b.shape, (what, i, a.shape, b.shape)
+        if not np.array_equal(a, b):
+            bad = np.argwhere(a != b)
+            raise AssertionError(f"{what}: record {i}: {len(bad)} mismatches, first at {bad[0]}: "
+                                 f"hip={a[tuple(bad[0])]} ref={b[tuple(bad[0])]}")
+
+
+def _synthetic(n, w=256, h=256, seed=0x5EED, ragged=False):
+    rng = np.random.default_rng(7)
+    imgs = []
+    for i in range(n):
+        if ragged:
+            w, h = int(rng.integers(256, 513)), int(rng.integers(256, 513))
+        imgs.append(A.synthetic_image(i, w, h, 3, seed))
+    return imgs
+
+
+MEAN_OUT = dict(channels=3, channel_major=True, bgr_to_rgb=True, dtype="float32",
+                mean=C.MEAN, stddev=C.STDDEV, item_stride=3 * 224 * 224 * 4)
+
+
+def test_golden_train(ctx, golden):
+    """provider.image_paddle_imagenet_training_augmentation (test/test_provider.cpp:96-177)."""
+    p = A.aug_params(crop_x=50, crop_y=50, crop_w=171, crop_h=201, out_w=224, out_h=224, flip=1)
+    out = A.out_desc(**MEAN_OUT)
+    (res,) = H.hip_records(ctx, [golden["img"]], [p], out)
+    assert np.array_equal(res, golden["train"])
+
+
+def test_golden_eval(ctx, golden):
+    """provider.image_paddle_imagenet_validate_augmentation (test/test_provider.cpp:179-261):
+    resize_short 256 -> center crop 224 (the C1 configuration)."""
+    (p,) = H.draw_params(C.C1_AUG, [(480, 360)], 224, 224)
+    out = A.out_desc(**MEAN_OUT)
+    (res,) = H.hip_records(ctx, [golden["img"]], [p], out)
+    assert np.array_equal(res, golden["eval"])
+
+
+@pytest.mark.parametrize("aug_name", ["C1", "C2", "C3"])
+def test_configs_fixed_256(ctx, aug_name):
+    aug = {"C1": C.C1_AUG, "C2": C.C2_AUG, "C3": C.C3_AUG}[aug_name]
+    imgs = _synthetic(24)
+    params = H.draw_params(aug, [(256, 256)] * len(imgs), 224, 224, seed=3)
+    out = A.out_desc(**MEAN_OUT)
+    _assert_same(H.hip_records(ctx, imgs, params, out), H.oracle_records(imgs, params, out), aug_name)
+
+
+def test_c3_ragged(ctx):
+    imgs = _synthetic(24, ragged=True)
+    params = H.draw_params(C.C3_AUG, [(im.shape[1], im.shape[0]) for im in imgs], 224, 224, seed=11)
+    out = A.out_desc(**MEAN_OUT)
+    _assert_same(H.hip_records(ctx, imgs, params, out), H.oracle_records(imgs, params, out), "C3 ragged")
+
+
+def test_real_image_c3(ctx, golden):
+    imgs = [golden["img"]] * 16
+    params = H.draw_params(C.C3_AUG, [(480, 360)] * 16, 224, 224, seed=5)
+    out = A.out_desc(**MEAN_OUT)
+    _assert_same(H.hip_records(ctx, imgs, params, out), H.oracle_records(imgs, params, out), "C3 real")
+
+
+def test_c5_image_and_mask(ctx):
+    """etl [image 512, pixelmask 512]: the mask shares the image's params (provider.cpp:378-391)."""
+    rng = np.random.default_rng(3)
+    imgs, masks = [], []
+    for i in range(8):
+        w, h = int(rng.integers(300, 700)), int(rng.integers(300, 700))
+        imgs.append(A.synthetic_image(i, w, h, 3))
+        masks.append(((A.synthetic_image(100 + i, w, h, 1) > 127) * 255).astype(np.uint8))
+    params = H.draw_params(C.C5_AUG, [(im.shape[1], im.shape[0]) for im in imgs], 512, 512, seed=9)
+    iout = C.out_desc_for(C.IMAGE_512, C.C5_AUG)
+    mout = C.out_desc_for(C.MASK_512, C.C5_AUG)
+    _assert_same(H.hip_records(ctx, imgs, params, iout), H.oracle_records(imgs, params, iout), "C5 image")
+    mres = H.hip_records(ctx, masks, params, mout, mask=True)
+    _assert_same(mres, H.oracle_records(masks, params, mout, mask=True), "C5 mask")
+    for m in mres:  # test/test_pixel_mask.cpp invariant: NEAREST keeps only the source values
+        assert set(np.unique(m)) <= {0, 255}
+
+
+EDGE_CASES = [
+    # (name, src (w,h), params kwargs, out kwargs)
+    ("upscale_tiny", (7, 5), dict(crop_x=0, crop_y=0, crop_w=7, crop_h=5, out_w=224, out_h=224), {}),
+    ("one_pixel", (1, 1), dict(crop_x=0, crop_y=0, crop_w=1, crop_h=1, out_w=16, out_h=8), {}),
+    ("area2x", (448, 448), dict(crop_x=0, crop_y=0, crop_w=448, crop_h=448, out_w=224, out_h=224), {}),
+    ("area2x_flip", (500, 480), dict(crop_x=10, crop_y=7, crop_w=448, crop_h=448, out_w=224, out_h=224, flip=1), {}),
+    ("copy", (300, 300), dict(crop_x=13, crop_y=21, crop_w=224, crop_h=224, out_w=224, out_h=224), {}),
+    ("odd_width_tail", (333, 217), dict(crop_x=3, crop_y=2, crop_w=301, crop_h=199, out_w=223, out_h=97), {}),
+    ("narrow", (64, 512), dict(crop_x=0, crop_y=0, crop_w=5, crop_h=512, out_w=3, out_h=100), {}),
+    ("huge_downscale", (2000, 1500), dict(crop_x=100, crop_y=50, crop_w=1800, crop_h=1400, out_w=224, out_h=224), {}),
+    ("u8_hwc", (256, 256), dict(crop_x=5, crop_y=9, crop_w=200, crop_h=180, out_w=224, out_h=224, flip=1),
+     dict(dtype="uint8", channel_major=False, mean=None, stddev=None, item_stride=224 * 224 * 3)),
+    ("u8_chw_bgr", (256, 256), dict(crop_x=5, crop_y=9, crop_w=200, crop_h=180, out_w=224, out_h=224),
+     dict(dtype="uint8", bgr_to_rgb=False, mean=None, stddev=None, item_stride=224 * 224 * 3)),
+    ("f32_hwc_mean", (256, 256), dict(crop_x=5, crop_y=9, crop_w=200, crop_h=180, out_w=224, out_h=224),
+     dict(channel_major=False)),
+    ("f32_nomean", (256, 256), dict(crop_x=5, crop_y=9, crop_w=200, crop_h=180, out_w=224, out_h=224),
+     dict(mean=None, stddev=None)),
+    ("brightness_diag", (256, 256), dict(crop_x=0, crop_y=0, crop_w=256, crop_h=256, out_w=224, out_h=224,
+                                         brightness=0.6), {}),
+    ("saturation0", (256, 256), dict(crop_x=0, crop_y=0, crop_w=256, crop_h=256, out_w=224, out_h=224,
+                                     saturation=0.0, brightness=0.9), {}),
+    ("saturation_float_path", (256, 256), dict(crop_x=0, crop_y=0, crop_w=256, crop_h=256, out_w=224,
+                                               out_h=224, saturation=40.0), {}),
+    ("hue_neg", (256, 256), dict(crop_x=0, crop_y=0, crop_w=256, crop_h=256, out_w=224, out_h=224, hue=-179), {}),
+    ("hue_pos", (256, 256), dict(crop_x=0, crop_y=0, crop_w=256, crop_h=256, out_w=224, out_h=224, hue=180), {}),
+    ("contrast_only", (256, 256), dict(crop_x=0, crop_y=0, crop_w=256, crop_h=256, out_w=224, out_h=224,
+                                       contrast=0.3), {}),
+    ("lighting_only", (256, 256), dict(crop_x=0, crop_y=0, crop_w=256, crop_h=256, out_w=224, out_h=224,
+                                       lighting=[1.5, -2.0, 0.7], color_noise_std=0.1), {}),
+    ("nearest_interp", (256, 256), dict(crop_x=3, crop_y=3, crop_w=190, crop_h=211, out_w=224, out_h=224,
+                                        interp=1), {}),
+    ("padding", (32, 32), dict(crop_x=0, crop_y=0, crop_w=32, crop_h=32, out_w=32, out_h=32, padding=5,
+                               pad_off_x=2, pad_off_y=8), dict(item_stride=3 * 32 * 32 * 4)),
+    ("padding_resize", (30, 30), dict(crop_x=0, crop_y=0, crop_w=30, crop_h=30, out_w=64, out_h=48, padding=10,
+                                      pad_off_x=20, pad_off_y=0), dict(item_stride=3 * 64 * 48 * 4)),
+    ("resize_short_upscale", (120, 90), dict(crop_x=40, crop_y=0, crop_w=256, crop_h=256, out_w=224, out_h=224,
+                                             resize_short_size=256), {}),
+]
+
+
+@pytest.mark.parametrize("name,src,pk,ok", EDGE_CASES, ids=[c[0] for c in EDGE_CASES])
+def test_edge_cases(ctx, name, src, pk, ok):
+    w, h = src
+    imgs = [A.synthetic_image(i, w, h, 3) for i in range(3)]
+    params = [A.aug_params(**pk) for _ in imgs]
+    kw = dict(MEAN_OUT)
+    kw.update(ok)
+    out = A.out_desc(**kw)
+    _assert_same(H.hip_records(ctx, imgs, params, out), H.oracle_records(imgs, params, out), name)
+
+
+def test_grayscale(ctx):
+    imgs = [A.synthetic_image(i, 97, 61, 1) for i in range(4)]
+    params = [A.aug_params(crop_x=4, crop_y=2, crop_w=80, crop_h=50, out_w=64, out_h=48, flip=i % 2)
+              for i in range(4)]
+    out = A.out_desc(channels=1, channel_major=True, dtype="uint8", item_stride=64 * 48)
+    _assert_same(H.hip_records(ctx, imgs, params, out), H.oracle_records(imgs, params, out), "gray")
+
+
+def test_empty_batch(ctx):
+    import torch
+    out = A.out_desc(**MEAN_OUT)
+    buf = torch.zeros(16, dtype=torch.uint8, device="cuda")
+    ctx.augment_batch([], buf.data_ptr(), [], out, buf.data_ptr())
+    ctx.synchronize()
+
+
+def test_errors(ctx):
+    img = A.synthetic_image(0, 64, 64)
+    out = A.out_desc(**MEAN_OUT)
+    with pytest.raises(A.AeonHipError) as e:
+        H.hip_records(ctx, [img], [A.aug_params(crop_w=64, crop_h=64, out_w=224, out_h=224, angle=10)], out)
+    assert e.value.code == A.AEON_HIP_EUNSUPPORTED
+    with pytest.raises(A.AeonHipError) as e:
+        H.hip_records(ctx, [img], [A.aug_params(crop_x=10, crop_w=64, crop_h=64, out_w=224, out_h=224)], out)
+    assert e.value.code == A.AEON_HIP_EINVAL
+
+
+def test_full_batch_c3_properties(ctx):
+    """BASELINE.json C3 at its full size (batch 1024, 224x224 fp32): a 32-record sample matches
+    the oracle exactly; reruns are bit-identical (determinism)."""
+    import torch
+    n = 1024
+    imgs = _synthetic(n)
+    params = H.draw_params(C.C3_AUG, [(256, 256)] * n, 224, 224, seed=1)
+    out = A.out_desc(**MEAN_OUT)
+    r1 = H.hip_records(ctx, imgs, params, out)
+    r2 = H.hip_records(ctx, imgs, params, out)
+    assert all(np.array_equal(a, b) for a, b in zip(r1, r2))
+    sample = np.random.default_rng(0).choice(n, 32, replace=False)
+    ref = H.oracle_records([imgs[i] for i in sample], [params[i] for i in sample], out)
+    _assert_same([r1[i] for i in sample], ref, "C3 full-size sample")
+    torch.cuda.synchronize()
