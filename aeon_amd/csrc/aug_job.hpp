@@ -50,7 +50,7 @@ struct alignas(16) AugJob {
     int32_t  hue;
     float    light_a;                        // (float)(1/(1+sigma))
     int32_t  light_add[3];                   // cvRound(pixel_c / (1+sigma))
-    int32_t  tiles;                          // row tiles of this job
+    int32_t  tiles;                          // row chunks (workgroups) of this job
     int32_t  stats_slot;                     // contrast partial-sum slot (-1 if none)
     int32_t  src_scratch;                    // host bookkeeping: source lives in the slot scratch
     int32_t  pad_;
@@ -63,8 +63,9 @@ struct LaunchArgs {
     const int32_t* hsv_tables; // sdiv[256], hdiv180[256]
     uint32_t*      partials;   // contrast partial sums [slots][max_tiles][4]
     int32_t*       error;      // device error word (0 = ok)
-    int32_t        rows_per_tile;
-    int32_t        max_tiles;
+    int32_t        rows_per_tile;  // rows per LDS band (TR)
+    int32_t        rows_per_chunk; // rows per workgroup (a multiple of TR; = TR: one band)
+    int32_t        max_tiles;      // chunks per job (grid.x)
     int32_t        stage_rows; // capacity of the LDS staging area
     int32_t        stage_pitch;// pixels per staged row (multiple of 4)
     int32_t        max_win_w;  // capacity of the x table
@@ -73,6 +74,7 @@ struct LaunchArgs {
     int32_t        bgr_to_rgb;
     int32_t        vec_ok;     // outputs 16-byte aligned and win_w % 4 == 0 for every job
     int32_t        lds_bytes;
+    int32_t        has_hue;    // some job of the launch shifts hue (HSV tables in LDS)
 };
 
 enum KernelMode : int { KM_FINAL = 0, KM_STATS = 1, KM_RAW = 2 };
@@ -87,18 +89,22 @@ constexpr int kBlock = 256; // 4 wave64s per workgroup
 
 // LDS carve of one workgroup (bytes; every region 16-byte aligned, see the CDNA guide G17).
 struct LdsLayout {
-    int hsv, lut, xt, yt, red, stage, total;
+    int hsv, lut, xt, yt, red, stage, stage_bytes, total;
 };
-AEON_HD inline LdsLayout lds_layout(int max_win_w, int rows_per_tile, int stage_rows, int stage_pitch)
+// One staging buffer (the next band waits in registers while the current one is consumed);
+// two small row-tap tables.  The HSV tables are reserved only for hue launches.
+AEON_HD inline LdsLayout lds_layout(int max_win_w, int rows_per_tile, int stage_rows, int stage_pitch,
+                                    bool hue = true)
 {
     LdsLayout L;
     int       o = 0;
-    L.hsv = o;   o += 2 * 256 * 4;                       // sdiv / hdiv180 tables
+    L.hsv = o;   o += hue ? 2 * 256 * 4 : 0;             // sdiv / hdiv180 tables
     L.lut = o;   o += 3 * 256 * 4;                       // standardize LUT
     L.xt  = o;   o += ((max_win_w * 8 + 15) / 16) * 16;  // per-column taps + weights
-    L.yt  = o;   o += rows_per_tile * 16;                // per-row taps + weights
+    L.yt  = o;   o += 2 * rows_per_tile * 16;            // per-row taps + weights, x2
     L.red = o;   o += 128;                               // reductions / contrast shifts
-    L.stage = o; o += stage_rows * stage_pitch * 4;      // source pixels, 4 B each (B,G,R,0)
+    L.stage_bytes = stage_rows * stage_pitch * 4;        // source pixels, 4 B each (B,G,R,0)
+    L.stage = o; o += L.stage_bytes;
     L.total = o;
     return L;
 }

@@ -23,44 +23,40 @@ namespace aeon_hip {
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 typedef float    f32x4 __attribute__((ext_vector_type(4)));
+typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ int sat_u8(int v) { return min(max(v, 0), 255); }
 __device__ __forceinline__ int sat_s16(int v) { return min(max(v, -32768), 32767); }
 __device__ __forceinline__ int rnd(float v) { return (int)__builtin_rintf(v); }
 __device__ __forceinline__ int byte_of(uint32_t p, int c) { return (p >> (8 * c)) & 0xff; }
+// 16x16-bit signed product (v_mul_i32_i24 with word selects): both operands must fit int16
+__device__ __forceinline__ int mul16(int a, int b) { return (int)(short)a * (int)(short)b; }
 
 // ---- resize coefficients (OpenCV 2.4 resizeGeneric_ / resizeNN) -----------------------------
+// Taps are (sx, sx+1) and (r0, r1); a weight of 0 marks a single-tap column / row.
 struct XTap {
-    int sx, sx2, a0, a1;
+    int sx, a0, a1;
 };
 
-__device__ __forceinline__ XTap xcoef(const AugJob& J, int dx)
+template <int RM>
+__device__ __forceinline__ XTap xcoef(int dx, double scale, int sw)
 {
     XTap t;
-    const int sw = J.crop_w;
-    switch (J.mode) {
-    case RESIZE_LINEAR: {
-        float fx = (float)((dx + 0.5) * J.scale_x - 0.5);
+    if (RM == RESIZE_LINEAR) {
+        float fx = (float)((dx + 0.5) * scale - 0.5);
         int   sx = (int)floorf(fx);
         fx -= (float)sx;
         if (sx < 0) fx = 0.f, sx = 0;
         if (sx + 1 >= sw) fx = 0.f, sx = sw - 1;
-        t.sx  = sx;
-        t.a0  = sat_s16(rnd((1.f - fx) * 2048.f));
-        t.a1  = sat_s16(rnd(fx * 2048.f));
-        t.sx2 = t.a1 == 0 ? sx : sx + 1;
-        break;
-    }
-    case RESIZE_AREA2X:
-        t.sx = 2 * dx, t.sx2 = 2 * dx + 1, t.a0 = t.a1 = 0;
-        break;
-    case RESIZE_NEAREST: {
-        int sx = (int)floor(dx * J.scale_x);
-        t.sx = t.sx2 = min(sx, sw - 1), t.a0 = t.a1 = 0;
-        break;
-    }
-    default:
-        t.sx = t.sx2 = dx, t.a0 = t.a1 = 0;
+        t.sx = sx;
+        t.a0 = sat_s16(rnd((1.f - fx) * 2048.f));
+        t.a1 = sat_s16(rnd(fx * 2048.f));
+    } else if (RM == RESIZE_AREA2X) {
+        t.sx = 2 * dx, t.a0 = t.a1 = 0;
+    } else if (RM == RESIZE_NEAREST) {
+        t.sx = min((int)floor(dx * scale), sw - 1), t.a0 = t.a1 = 0;
+    } else {
+        t.sx = dx, t.a0 = t.a1 = 0;
     }
     return t;
 }
@@ -69,28 +65,23 @@ struct YTap {
     int r0, r1, b0, b1;
 };
 
-__device__ __forceinline__ YTap ycoef(const AugJob& J, int dy)
+template <int RM>
+__device__ __forceinline__ YTap ycoef(int dy, double scale, int sh)
 {
-    YTap      t;
-    const int sh = J.crop_h;
-    switch (J.mode) {
-    case RESIZE_LINEAR: {
-        float fy = (float)((dy + 0.5) * J.scale_y - 0.5);
+    YTap t;
+    if (RM == RESIZE_LINEAR) {
+        float fy = (float)((dy + 0.5) * scale - 0.5);
         int   sy = (int)floorf(fy);
         fy -= (float)sy;
         t.b0 = sat_s16(rnd((1.f - fy) * 2048.f));
         t.b1 = sat_s16(rnd(fy * 2048.f));
         t.r0 = min(max(sy, 0), sh - 1);
         t.r1 = min(max(sy + 1, 0), sh - 1);
-        break;
-    }
-    case RESIZE_AREA2X:
+    } else if (RM == RESIZE_AREA2X) {
         t.r0 = 2 * dy, t.r1 = 2 * dy + 1, t.b0 = t.b1 = 0;
-        break;
-    case RESIZE_NEAREST:
-        t.r0 = t.r1 = min((int)floor(dy * J.scale_y), sh - 1), t.b0 = t.b1 = 0;
-        break;
-    default:
+    } else if (RM == RESIZE_NEAREST) {
+        t.r0 = t.r1 = min((int)floor(dy * scale), sh - 1), t.b0 = t.b1 = 0;
+    } else {
         t.r0 = t.r1 = dy, t.b0 = t.b1 = 0;
     }
     return t;
@@ -170,120 +161,277 @@ __device__ __forceinline__ void hue_apply(const int32_t* sdiv, const int32_t* hd
 }
 
 // ---- source staging ----------------------------------------------------------------------------
-// Stage resize-source rows [v_lo, v_lo+nr) x cols [u_lo, u_lo+nc) as one 32-bit word per pixel.
-__device__ __forceinline__ void stage_rows(const AugJob& J, uint32_t* stage, int pitch, int v_lo,
-                                           int nr, int u_lo, int nc)
+// A band stages resize-source rows [v_lo, v_lo+nr) x cols [u_lo, u_lo+nc) into LDS as one
+// 32-bit word per pixel: four pixels per lane from one 16-byte buffer load (alignbyte re-packs
+// the 3-byte pixels).  Loads for band b+1 are issued into registers (kPrefetch per lane) before
+// band b is consumed and written to LDS after it, so their HBM latency hides under the compute.
+constexpr int kPrefetch = 3;
+
+struct StageGeom {
+    int v_lo, nr, u_lo, nc, groups;
+};
+
+struct Prefetch {
+    u32x4    d[kPrefetch];
+    uint32_t meta[kPrefetch]; // row j (12 b) | group g (14 b) | byte shift (2 b) | fast (1 b) | valid
+};
+
+__device__ __forceinline__ int stage_byte(const AugJob& J, int cy, int cx)
 {
-    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)J.src_ptr, (short)0, (int)J.src_bytes, 0x00020000);
-    const int cn     = J.cn;
-    const int groups = (nc + 3) >> 2;
-    const int total  = nr * groups;
-    for (int w = threadIdx.x; w < total; w += kBlock) {
-        const int j  = w / groups;
-        const int g  = w - j * groups;
-        const int v  = v_lo + j;
-        const int u0 = u_lo + 4 * g;
-        const int cy = v + J.shift_y;     // row inside the crop
-        const int cx = u0 + J.shift_x;    // first column inside the crop
-        uint32_t  px[4];
-        const bool row_ok = cy >= 0 && cy < J.crop_h;
-        if (row_ok && cx >= 0 && cx + 3 < J.crop_w) {
-            const int b = (J.crop_y + cy) * J.src_stride + (J.crop_x + cx) * cn;
-            const int a = b & ~3, sh = b & 3;
-            if (cn == 3) {
-                u32x4    d  = __builtin_amdgcn_raw_buffer_load_b128(rsrc, a, 0, 0);
-                uint32_t e0 = __builtin_amdgcn_alignbyte(d.y, d.x, sh);
-                uint32_t e1 = __builtin_amdgcn_alignbyte(d.z, d.y, sh);
-                uint32_t e2 = __builtin_amdgcn_alignbyte(d.w, d.z, sh);
-                px[0] = e0 & 0xffffff;
-                px[1] = (e0 >> 24) | ((e1 & 0xffff) << 8);
-                px[2] = (e1 >> 16) | ((e2 & 0xff) << 16);
-                px[3] = e2 >> 8;
-            } else {
-                u32x2    d  = __builtin_amdgcn_raw_buffer_load_b64(rsrc, a, 0, 0);
-                uint32_t e0 = __builtin_amdgcn_alignbyte(d.y, d.x, sh);
-                px[0] = e0 & 0xff, px[1] = (e0 >> 8) & 0xff, px[2] = (e0 >> 16) & 0xff, px[3] = e0 >> 24;
-            }
-        } else {
+    return (J.crop_y + cy) * J.src_stride + (J.crop_x + cx) * J.cn;
+}
+
+// Fast item: one 16-byte (8 for 1 channel) load holds the four source pixels -- or, unpadded,
+// pixels beyond the crop that only ever meet a zero resize weight.  The load must lie wholly
+// inside the image: a buffer load that crosses num_records returns 0 for the whole access.
+__device__ __forceinline__ bool stage_fast(const AugJob& J, int cy, int cx)
+{
+    const int  b      = stage_byte(J, cy, cx);
+    const bool inside = (uint32_t)((b & ~3) + (J.cn == 3 ? 16 : 8)) <= (uint32_t)J.src_bytes;
+    return inside && (!J.padded || (cy >= 0 && cy < J.crop_h && cx >= 0 && cx + 3 < J.crop_w));
+}
+
+__device__ __forceinline__ u32x4 stage_load(const AugJob& J, __amdgpu_buffer_rsrc_t rsrc, int b)
+{
+    if (J.cn == 3) return __builtin_amdgcn_raw_buffer_load_b128(rsrc, b & ~3, 0, 0);
+    u32x2 d = __builtin_amdgcn_raw_buffer_load_b64(rsrc, b & ~3, 0, 0);
+    return (u32x4){d.x, d.y, 0u, 0u};
+}
+
+__device__ __forceinline__ u32x4 stage_unpack(int cn, int sh, u32x4 d)
+{
+    if (cn == 3) {
+        uint32_t e0 = __builtin_amdgcn_alignbyte(d.y, d.x, sh);
+        uint32_t e1 = __builtin_amdgcn_alignbyte(d.z, d.y, sh);
+        uint32_t e2 = __builtin_amdgcn_alignbyte(d.w, d.z, sh);
+        return (u32x4){e0 & 0xffffff, (e0 >> 24) | ((e1 & 0xffff) << 8), (e1 >> 16) | ((e2 & 0xff) << 16),
+                       e2 >> 8};
+    }
+    uint32_t e0 = __builtin_amdgcn_alignbyte(d.y, d.x, sh);
+    return (u32x4){e0 & 0xff, (e0 >> 8) & 0xff, (e0 >> 16) & 0xff, e0 >> 24};
+}
+
+// Slow item (add_padding border / crop edge of a padded job): per-pixel byte loads, 0 outside.
+__device__ __forceinline__ u32x4 stage_slow(const AugJob& J, __amdgpu_buffer_rsrc_t rsrc, int cy, int cx)
+{
+    uint32_t   px[4];
+    const bool row_ok = cy >= 0 && cy < J.crop_h;
 #pragma unroll
-            for (int k = 0; k < 4; k++) {
-                const int x = cx + k;
-                uint32_t  p = 0;
-                if (row_ok && x >= 0 && x < J.crop_w) {
-                    const int b = (J.crop_y + cy) * J.src_stride + (J.crop_x + x) * cn;
-                    for (int c = 0; c < cn; c++)
-                        p |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rsrc, b + c, 0, 0) << (8 * c);
-                }
-                px[k] = p;
-            }
+    for (int k = 0; k < 4; k++) {
+        const int x = cx + k;
+        uint32_t  p = 0;
+        if (row_ok && x >= 0 && x < J.crop_w) {
+            const int b = stage_byte(J, cy, x);
+            for (int c = 0; c < J.cn; c++)
+                p |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rsrc, b + c, 0, 0) << (8 * c);
         }
-        u32x4 q = {px[0], px[1], px[2], px[3]};
+        px[k] = p;
+    }
+    return (u32x4){px[0], px[1], px[2], px[3]};
+}
+
+// Issue the first kPrefetch items of this lane for a band (fast items only).
+__device__ __forceinline__ void stage_issue(const AugJob& J, __amdgpu_buffer_rsrc_t rsrc, const StageGeom& G,
+                                            Prefetch& pf)
+{
+    const int total = G.nr * G.groups;
+    const int dj = kBlock / G.groups, dg = kBlock - dj * G.groups;
+    int       j = threadIdx.x / G.groups, g = threadIdx.x - j * G.groups;
+#pragma unroll
+    for (int k = 0; k < kPrefetch; k++, j += dj, g += dg) {
+        if (g >= G.groups) g -= G.groups, j++;
+        const int i = threadIdx.x + k * kBlock;
+        pf.meta[k]  = 0;
+        if (i >= total) continue;
+        const int  cy = G.v_lo + j + J.shift_y, cx = G.u_lo + 4 * g + J.shift_x;
+        const bool fast = stage_fast(J, cy, cx);
+        const int  b    = stage_byte(J, cy, cx);
+        pf.meta[k]      = ((uint32_t)j << 20) | ((uint32_t)g << 6) | ((b & 3) << 2) | (fast ? 2u : 0u) | 1u;
+        if (fast) pf.d[k] = stage_load(J, rsrc, b);
+    }
+}
+
+// Write this lane's items of a band to LDS (prefetched ones from registers, the rest loaded now).
+__device__ __forceinline__ void stage_commit(const AugJob& J, __amdgpu_buffer_rsrc_t rsrc, const StageGeom& G,
+                                             const Prefetch& pf, uint32_t* stage, int pitch)
+{
+#pragma unroll
+    for (int k = 0; k < kPrefetch; k++) {
+        const uint32_t m = pf.meta[k];
+        if (!(m & 1)) continue;
+        const int j = m >> 20, g = (m >> 6) & 0x3fff;
+        u32x4     q;
+        if (m & 2) q = stage_unpack(J.cn, (m >> 2) & 3, pf.d[k]);
+        else q = stage_slow(J, rsrc, G.v_lo + j + J.shift_y, G.u_lo + 4 * g + J.shift_x);
+        *(u32x4*)(stage + j * pitch + 4 * g) = q;
+    }
+    const int total = G.nr * G.groups;
+    const int i0    = threadIdx.x + kPrefetch * kBlock;
+    const int dj = kBlock / G.groups, dg = kBlock - dj * G.groups;
+    int       j = i0 / G.groups, g = i0 - j * G.groups;
+    for (int i = i0; i < total; i += kBlock, j += dj, g += dg) {
+        if (g >= G.groups) g -= G.groups, j++;
+        const int cy = G.v_lo + j + J.shift_y, cx = G.u_lo + 4 * g + J.shift_x;
+        u32x4     q;
+        if (stage_fast(J, cy, cx)) {
+            const int b = stage_byte(J, cy, cx);
+            q           = stage_unpack(J.cn, b & 3, stage_load(J, rsrc, b));
+        } else {
+            q = stage_slow(J, rsrc, cy, cx);
+        }
         *(u32x4*)(stage + j * pitch + 4 * g) = q;
     }
 }
 
+// Output cache policy: streaming stores (written once, read by the consumer of the batch).
+constexpr int kStoreAux = 2; // nt
+
+__device__ __forceinline__ void store_f32x4(__amdgpu_buffer_rsrc_t r, int off, float a, float b, float c,
+                                            float d)
+{
+    u32x4 v = {__float_as_uint(a), __float_as_uint(b), __float_as_uint(c), __float_as_uint(d)};
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, kStoreAux);
+}
+
+// One output pixel of the resize: 3 channels from the staged source (LDS).
+template <int RM>
+__device__ __forceinline__ void resize_px(const uint32_t* stage, int4 ytr, int2 xtt, int v[3])
+{
+    const uint32_t* r0p = stage + ytr.x + xtt.x;
+    if (RM == RESIZE_LINEAR) {
+        const uint32_t* r1p = stage + ytr.y + xtt.x;
+        const uint32_t  p00 = r0p[0], p01 = r0p[1], p10 = r1p[0], p11 = r1p[1];
+        const u16x2     w   = __builtin_bit_cast(u16x2, (uint32_t)xtt.y); // (a0, a1)
+#pragma unroll
+        for (int c = 0; c < 3; c++) {
+            // HResizeLinear: H = S[sx]*a0 + S[sx+1]*a1 (exact), one v_dot2_u32_u16 per row on
+            // the (S[sx], S[sx+1]) byte pair that v_perm_b32 gathers into two u16 lanes.
+            const uint32_t sel = (uint32_t)c | (0x0Cu << 8) | ((4u + c) << 16) | (0x0Cu << 24);
+            const uint32_t H0  = __builtin_amdgcn_udot2(
+                __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(p01, p00, sel)), w, 0u, false);
+            const uint32_t H1  = __builtin_amdgcn_udot2(
+                __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(p11, p10, sel)), w, 0u, false);
+            // VResizeLinearVec_32s8u (SSE2): ((H0>>4)*b0 >> 16) + ((H1>>4)*b1 >> 16) + 2 >> 2.
+            // The +2 rides in the high half of t0; the sum is <= 1023, so no saturation.
+            const uint32_t t0 = (uint32_t)__mul24((int)(H0 >> 4), ytr.z) + (2u << 16);
+            const uint32_t t1 = (uint32_t)__mul24((int)(H1 >> 4), ytr.w);
+            v[c]              = (int)(((t0 >> 16) + (t1 >> 16)) >> 2);
+        }
+    } else if (RM == RESIZE_AREA2X) {
+        const uint32_t* r1p = stage + ytr.y + xtt.x;
+        const uint32_t  p00 = r0p[0], p01 = r0p[1], p10 = r1p[0], p11 = r1p[1];
+#pragma unroll
+        for (int c = 0; c < 3; c++)
+            v[c] = (byte_of(p00, c) + byte_of(p01, c) + byte_of(p10, c) + byte_of(p11, c) + 2) >> 2;
+    } else {
+        const uint32_t p00 = r0p[0];
+#pragma unroll
+        for (int c = 0; c < 3; c++) v[c] = byte_of(p00, c);
+    }
+}
+
+// Elements of OpenCV's scalar row tail (e >= xv) use FixedPtCast<int, uchar, 22> instead.
+__device__ __forceinline__ void tail_fix(const uint32_t* stage, int4 ytr, int2 xtt, int e0, int xv, int v[3])
+{
+    const uint32_t* r0p = stage + ytr.x + xtt.x;
+    const uint32_t* r1p = stage + ytr.y + xtt.x;
+    const int       a0 = xtt.y & 0xffff, a1 = xtt.y >> 16;
+    for (int c = 0; c < 3; c++) {
+        if (e0 + c < xv) continue;
+        const int H0 = byte_of(r0p[0], c) * a0 + byte_of(r0p[1], c) * a1;
+        const int H1 = byte_of(r1p[0], c) * a0 + byte_of(r1p[1], c) * a1;
+        v[c]         = sat_u8((H0 * ytr.z + H1 * ytr.w + (1 << 21)) >> 22);
+    }
+}
+
+enum OutForm : int { OF_F32_CHW_VEC = 0, OF_GENERIC = 1 };
+
 // ---- the tile kernel -----------------------------------------------------------------------
-template <int MODE>
+// One workgroup = one chunk of rows_per_chunk output rows of one job, processed in bands of
+// rows_per_tile rows through double-buffered LDS.
+// KM: KM_FINAL (full record -> loader output), KM_STATS (contrast sums only), KM_RAW (resize
+// only, HWC uint8: the resize_short pre-pass).  RM: ResizeMode of every job in the launch.
+// PHOTO: the launch's jobs carry photometric work.  OF: output form (OF_F32_CHW_VEC = float32
+// CHW planes, win_w % 4 == 0, 16-byte aligned items: the ImageNet configuration).
+template <int KM, int RM, bool PHOTO, int OF>
 __global__ __launch_bounds__(kBlock) void augment_tiles(LaunchArgs a)
 {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const AugJob& J    = a.jobs[blockIdx.y];
-    const int     tile = blockIdx.x;
-    if (tile >= J.tiles) return;
-    if (MODE == KM_STATS && J.stats_slot < 0) return;
+    // The job descriptor is copied to registers before any store: the pixel loop then issues
+    // no global loads except the next band's staging, so stores rarely make a load wait.
+    const AugJob J     = a.jobs[blockIdx.y];
+    const int    chunk = blockIdx.x;
+    if (chunk >= J.tiles) return;
+    if (KM == KM_STATS && J.stats_slot < 0) return;
 
     const int TR    = a.rows_per_tile;
-    const int y0    = tile * TR;
-    const int nrows = min(TR, J.win_h - y0);
+    const int c0    = chunk * a.rows_per_chunk;
+    const int c1    = min(c0 + a.rows_per_chunk, J.win_h);
     const int tid   = threadIdx.x;
     const int cn    = J.cn;
+    const int win_w = J.win_w;
 
-    const LdsLayout L     = lds_layout(a.max_win_w, TR, a.stage_rows, a.stage_pitch);
+    const LdsLayout L     = lds_layout(a.max_win_w, TR, a.stage_rows, a.stage_pitch, PHOTO && a.has_hue);
     int32_t*        sdiv  = (int32_t*)(smem + L.hsv);
     int32_t*        hdiv  = sdiv + 256;
     float*          lut   = (float*)(smem + L.lut);
-    int4*           xt    = (int4*)(smem + L.xt);  // only .x/.y used (packed), 8 B per column
-    int4*           yt    = (int4*)(smem + L.yt);
+    int2*           xt    = (int2*)(smem + L.xt);
+    int4*           yt0   = (int4*)(smem + L.yt);
     int32_t*        red   = (int32_t*)(smem + L.red);
     double*         shift = (double*)(smem + L.red + 64);
     uint32_t*       stage = (uint32_t*)(smem + L.stage);
     const int       pitch = a.stage_pitch;
 
-    // source window of this band (uniform; resize coefficients are monotone in dx, dy)
-    const XTap xf = xcoef(J, J.win_x), xl = xcoef(J, J.win_x + J.win_w - 1);
-    const YTap yf = ycoef(J, J.win_y + y0), yl = ycoef(J, J.win_y + y0 + nrows - 1);
-    const int  u_lo = xf.sx;
-    const int  u_hi = max(xl.sx2, xl.sx);
-    const int  v_lo = yf.r0;
-    const int  v_hi = max(yl.r1, yl.r0);
-    const int nc = u_hi - u_lo + 1, nr = v_hi - v_lo + 1;
-    if (nc > pitch || nr > a.stage_rows || J.win_w > a.max_win_w) {
+    // source columns (the same for every band; taps are monotone in dx)
+    const XTap xf = xcoef<RM>(J.win_x, J.scale_x, J.crop_w);
+    const XTap xl = xcoef<RM>(J.win_x + win_w - 1, J.scale_x, J.crop_w);
+    const int  two_tap = (RM == RESIZE_LINEAR || RM == RESIZE_AREA2X) ? 1 : 0;
+    StageGeom  G;
+    G.u_lo   = xf.sx;
+    G.nc     = xl.sx + two_tap - G.u_lo + 1;
+    G.groups = (G.nc + 3) >> 2;
+    if (G.nc > pitch || win_w > a.max_win_w) {
         if (tid == 0) atomicOr(a.error, 1);
         return;
     }
+    auto band_rows = [&](int y0, StageGeom& g) { // rows of the band starting at window row y0
+        const int n = min(TR, c1 - y0);
+        g.v_lo      = ycoef<RM>(J.win_y + y0, J.scale_y, J.crop_h).r0;
+        g.nr        = ycoef<RM>(J.win_y + y0 + n - 1, J.scale_y, J.crop_h).r1 - g.v_lo + 1;
+        return n;
+    };
+    auto build_yt = [&](int y0, int n, const StageGeom& g, int4* yt) {
+        for (int r = tid; r < n; r += kBlock) {
+            const YTap t = ycoef<RM>(J.win_y + y0 + r, J.scale_y, J.crop_h);
+            yt[r]        = make_int4((t.r0 - g.v_lo) * pitch, (t.r1 - g.v_lo) * pitch, t.b0, t.b1);
+        }
+    };
 
-    // per-column taps (relative to u_lo) and weights; flip is applied on the output index
-    int2* xt2 = (int2*)xt;
-    for (int x = tid; x < J.win_w; x += kBlock) {
-        XTap t = xcoef(J, J.win_x + x);
-        xt2[x] = make_int2((t.sx - u_lo) | ((t.sx2 - u_lo) << 16), (t.a0 & 0xffff) | (t.a1 << 16));
+    const __amdgpu_buffer_rsrc_t srsrc =
+        __builtin_amdgcn_make_buffer_rsrc((void*)J.src_ptr, (short)0, (int)J.src_bytes, 0x00020000);
+    // band 0 loads go out first; the tables below are built while they are in flight
+    Prefetch pf;
+    int      n0 = band_rows(c0, G);
+    if (G.nr > a.stage_rows) {
+        if (tid == 0) atomicOr(a.error, 2);
+        return;
     }
-    for (int r = tid; r < nrows; r += kBlock) {
-        YTap t = ycoef(J, J.win_y + y0 + r);
-        yt[r]  = make_int4((t.r0 - v_lo) * pitch, (t.r1 - v_lo) * pitch, t.b0, t.b1);
+    stage_issue(J, srsrc, G, pf);
+
+    for (int x = tid; x < win_w; x += kBlock) {
+        const XTap t = xcoef<RM>(J.win_x + x, J.scale_x, J.crop_w);
+        xt[x]        = make_int2(t.sx - G.u_lo, (t.a0 & 0xffff) | (t.a1 << 16));
     }
-    const bool do_photo = MODE != KM_RAW && cn == 3;
-    const int  photo    = do_photo ? J.photo : 0;
+    const int photo = (PHOTO && KM != KM_RAW && cn == 3) ? J.photo : 0;
     if (photo & PHOTO_HUE) {
         sdiv[tid] = a.hsv_tables[tid];
         hdiv[tid] = a.hsv_tables[256 + tid];
     }
-    const bool use_lut = MODE == KM_FINAL && a.out_dtype == OUT_F32 && a.lut != nullptr;
+    const bool use_lut = KM == KM_FINAL && a.out_dtype == OUT_F32 && a.lut != nullptr;
     if (use_lut)
         for (int i = tid; i < 3 * 256; i += kBlock) lut[i] = a.lut[i];
-    if (MODE == KM_FINAL && (photo & PHOTO_CONTRAST) && tid < 64) {
-        // reduce the exact per-tile channel sums of this image (written by KM_STATS)
+    if (KM == KM_FINAL && (photo & PHOTO_CONTRAST) && tid < 64) {
+        // reduce the exact per-chunk channel sums of this image (written by KM_STATS)
         unsigned long long s0 = 0, s1 = 0, s2 = 0;
         for (int t = tid; t < J.tiles; t += 64) {
             const uint32_t* p = a.partials + ((size_t)J.stats_slot * a.max_tiles + t) * 4;
@@ -303,152 +451,160 @@ __global__ __launch_bounds__(kBlock) void augment_tiles(LaunchArgs a)
             shift[2] = k * ((double)s2 * inv_n);
         }
     }
-    stage_rows(J, stage, pitch, v_lo, nr, u_lo, nc);
+    build_yt(c0, n0, G, yt0);
+    stage_commit(J, srsrc, G, pf, stage, pitch);
     __syncthreads();
 
-    const int gpr   = (J.win_w + 3) >> 2;
-    const int total = nrows * gpr;
-    uint32_t  sum0 = 0, sum1 = 0, sum2 = 0;
-    double    sh0 = 0, sh1 = 0, sh2 = 0;
-    if (MODE == KM_FINAL && (photo & PHOTO_CONTRAST)) sh0 = shift[0], sh1 = shift[1], sh2 = shift[2];
+    uint32_t sum0 = 0, sum1 = 0, sum2 = 0;
+    double   sh0 = 0, sh1 = 0, sh2 = 0;
+    if (KM == KM_FINAL && (photo & PHOTO_CONTRAST)) sh0 = shift[0], sh1 = shift[1], sh2 = shift[2];
 
-    uint8_t* out_item = (uint8_t*)J.out_ptr;
-    const int plane   = J.win_w * J.win_h;
+    const int  elem  = (KM == KM_RAW || a.out_dtype == OUT_U8) ? 1 : 4;
+    const int  plane = win_w * J.win_h;
+    const auto orsrc = __builtin_amdgcn_make_buffer_rsrc((void*)J.out_ptr, (short)0,
+                                                         plane * cn * elem, 0x00020000);
+    const bool tail  = RM == RESIZE_LINEAR && J.xv < J.dst_w * cn; // OpenCV scalar row tail
+    const int  wx0   = J.win_x;
+    const int  xv    = J.xv;
+    const int  flip  = J.flip;
+    const int  gpr   = (win_w + 3) >> 2;
 
-    for (int w = tid; w < total; w += kBlock) {
-        const int  ry  = w / gpr;
-        const int  cg  = w - ry * gpr;
-        const int4 ytr = yt[ry];
-        const int  y   = y0 + ry; // window row
-        int        val[4][3];
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const int ox = cg * 4 + k;
-            val[k][0] = val[k][1] = val[k][2] = 0;
-            if (ox >= J.win_w) continue;
-            const int  x   = J.flip ? J.win_w - 1 - ox : ox;
-            const int2 xtt = xt2[x];
-            const int  sx = xtt.x & 0xffff, sx2 = xtt.x >> 16;
-            const uint32_t p00 = stage[ytr.x + sx], p01 = stage[ytr.x + sx2];
-            int            v3[3] = {0, 0, 0};
-            if (J.mode == RESIZE_LINEAR) {
-                const uint32_t p10 = stage[ytr.y + sx], p11 = stage[ytr.y + sx2];
-                const int      a0 = (short)(xtt.y & 0xffff), a1 = xtt.y >> 16;
-                const int      e0 = (J.win_x + x) * cn;
-#pragma unroll
-                for (int c = 0; c < 3; c++) {
-                    if (c >= cn) break;
-                    const int H0 = byte_of(p00, c) * a0 + byte_of(p01, c) * a1;
-                    const int H1 = byte_of(p10, c) * a0 + byte_of(p11, c) * a1;
-                    int       v;
-                    if (e0 + c < J.xv) { // VResizeLinearVec_32s8u (SSE2)
-                        const int m = ((H0 >> 4) * ytr.z >> 16) + ((H1 >> 4) * ytr.w >> 16);
-                        v = (m + 2) >> 2;
-                    } else { // FixedPtCast<int, uchar, 22>
-                        v = (H0 * ytr.z + H1 * ytr.w + (1 << 21)) >> 22;
-                    }
-                    v3[c] = sat_u8(v);
-                }
-            } else if (J.mode == RESIZE_AREA2X) {
-                const uint32_t p10 = stage[ytr.y + sx], p11 = stage[ytr.y + sx2];
-#pragma unroll
-                for (int c = 0; c < 3; c++)
-                    v3[c] = (byte_of(p00, c) + byte_of(p01, c) + byte_of(p10, c) + byte_of(p11, c) + 2) >> 2;
-            } else {
-#pragma unroll
-                for (int c = 0; c < 3; c++) v3[c] = byte_of(p00, c);
+    int buf = 0;
+    for (int y0 = c0; y0 < c1; y0 += TR) {
+        const int   nrows = min(TR, c1 - y0);
+        const int4* yt    = yt0 + buf * TR;
+        // issue the next band's loads; they land while this band is computed
+        StageGeom  Gn      = G;
+        int        nn      = 0;
+        const bool has_next = y0 + TR < c1;
+        if (has_next) {
+            nn = band_rows(y0 + TR, Gn);
+            if (Gn.nr > a.stage_rows) {
+                if (tid == 0) atomicOr(a.error, 2);
+                return; // uniform: every lane sees the same band geometry
             }
-            int b = v3[0], g = v3[1], r = v3[2];
-            if (photo & PHOTO_BS) bs_apply(J, b, g, r);
-            if (photo & PHOTO_HUE) hue_apply(sdiv, hdiv, J.hue, b, g, r);
-            if (MODE == KM_STATS) {
-                sum0 += b, sum1 += g, sum2 += r;
-                continue;
-            }
-            if (photo & PHOTO_CONTRAST) {
-                const float c = J.contrast;
-                b = sat_u8(rnd((float)((double)((float)b * c + 0.f) + sh0)));
-                g = sat_u8(rnd((float)((double)((float)g * c + 0.f) + sh1)));
-                r = sat_u8(rnd((float)((double)((float)r * c + 0.f) + sh2)));
-            }
-            if (photo & PHOTO_LIGHTING) {
-                const float la = J.light_a;
-                b = sat_u8(sat_u8(rnd((float)b * la + 0.f)) + J.light_add[0]);
-                g = sat_u8(sat_u8(rnd((float)g * la + 0.f)) + J.light_add[1]);
-                r = sat_u8(sat_u8(rnd((float)r * la + 0.f)) + J.light_add[2]);
-            }
-            val[k][0] = b, val[k][1] = g, val[k][2] = r;
+            stage_issue(J, srsrc, Gn, pf);
         }
-        if (MODE == KM_STATS) continue;
 
-        const int ox0 = cg * 4;
-        const int nk  = min(4, J.win_w - ox0);
-        if (MODE == KM_RAW) { // HWC uint8, source channel order
-            uint8_t* d = out_item + ((size_t)y * J.win_w + ox0) * cn;
-#pragma unroll
-            for (int k = 0; k < 4; k++)
-#pragma unroll
-                for (int c = 0; c < 3; c++)
-                    if (k < nk && c < cn) d[k * cn + c] = (uint8_t)val[k][c];
-            continue;
-        }
-        // image::loader::load -- from_to {0,2,1,1,2,0} when bgr_to_rgb (a 3-channel config)
-        if (a.bgr_to_rgb) {
+        const int dry = kBlock / gpr, dcg = kBlock - dry * gpr;
+        int       ry = tid / gpr, cg = tid - ry * gpr;
+        for (; ry < nrows; ry += dry, cg += dcg) {
+            if (cg >= gpr) cg -= gpr, ry++;
+            if (ry >= nrows) break;
+            const int4 ytr = yt[ry];
+            const int  y   = y0 + ry; // window row
+            const int  ox0 = cg * 4;
+            int        val[4][3];
 #pragma unroll
             for (int k = 0; k < 4; k++) {
-                const int t = val[k][0];
-                val[k][0]   = val[k][2];
-                val[k][2]   = t;
-            }
-        }
-        if (a.channel_major) {
-#pragma unroll
-            for (int oc = 0; oc < 3; oc++) {
-                if (oc >= cn) break;
-                const size_t idx = (size_t)oc * plane + (size_t)y * J.win_w + ox0;
-                if (a.out_dtype == OUT_F32) {
-                    float f[4];
-#pragma unroll
-                    for (int k = 0; k < 4; k++)
-                        f[k] = use_lut ? lut[oc * 256 + val[k][oc]] : (float)val[k][oc];
-                    float* d = (float*)out_item + idx;
-                    if (a.vec_ok) {
-                        f32x4 q = {f[0], f[1], f[2], f[3]};
-                        __builtin_nontemporal_store(q, (f32x4*)d);
-                    } else {
-#pragma unroll
-                        for (int k = 0; k < 4; k++)
-                            if (k < nk) d[k] = f[k];
-                    }
-                } else {
-                    uint8_t* d = out_item + idx;
-                    if (a.vec_ok) {
-                        *(uint32_t*)d = val[0][oc] | (val[1][oc] << 8) | (val[2][oc] << 16) |
-                                        ((uint32_t)val[3][oc] << 24);
-                    } else {
-#pragma unroll
-                        for (int k = 0; k < 4; k++)
-                            if (k < nk) d[k] = (uint8_t)val[k][oc];
-                    }
+                // columns past the window edge recompute the last one (never stored)
+                const int  ox  = min(ox0 + k, win_w - 1);
+                const int  x   = flip ? win_w - 1 - ox : ox;
+                const int2 xtt = xt[x];
+                resize_px<RM>(stage, ytr, xtt, val[k]);
+                if (RM == RESIZE_LINEAR && tail) {
+                    const int e0 = (wx0 + x) * cn;
+                    if (e0 + 2 >= xv) tail_fix(stage, ytr, xtt, e0, xv, val[k]);
                 }
             }
-        } else {
-            const size_t base = ((size_t)y * J.win_w + ox0) * cn;
+            if (PHOTO && photo) {
 #pragma unroll
-            for (int k = 0; k < 4; k++)
+                for (int k = 0; k < 4; k++) {
+                    int b = val[k][0], g = val[k][1], r = val[k][2];
+                    if (photo & PHOTO_BS) bs_apply(J, b, g, r);
+                    if (photo & PHOTO_HUE) hue_apply(sdiv, hdiv, J.hue, b, g, r);
+                    if (KM == KM_STATS) {
+                        if (ox0 + k < win_w) sum0 += b, sum1 += g, sum2 += r;
+                        continue;
+                    }
+                    if (photo & PHOTO_CONTRAST) {
+                        const float c = J.contrast;
+                        b = sat_u8(rnd((float)((double)((float)b * c + 0.f) + sh0)));
+                        g = sat_u8(rnd((float)((double)((float)g * c + 0.f) + sh1)));
+                        r = sat_u8(rnd((float)((double)((float)r * c + 0.f) + sh2)));
+                    }
+                    if (photo & PHOTO_LIGHTING) {
+                        const float la = J.light_a;
+                        b = sat_u8(sat_u8(rnd((float)b * la + 0.f)) + J.light_add[0]);
+                        g = sat_u8(sat_u8(rnd((float)g * la + 0.f)) + J.light_add[1]);
+                        r = sat_u8(sat_u8(rnd((float)r * la + 0.f)) + J.light_add[2]);
+                    }
+                    val[k][0] = b, val[k][1] = g, val[k][2] = r;
+                }
+            }
+            if (KM == KM_STATS) continue;
+
+            const int nk = min(4, win_w - ox0);
+            if (KM == KM_RAW) { // HWC uint8, source channel order
+                const int base = (y * win_w + ox0) * cn;
+#pragma unroll
+                for (int k = 0; k < 4; k++)
+#pragma unroll
+                    for (int c = 0; c < 3; c++)
+                        if (k < nk && c < cn)
+                            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)val[k][c], orsrc, base + k * cn + c, 0, 0);
+                continue;
+            }
+            // image::loader::load -- from_to {0,2,1,1,2,0} when bgr_to_rgb (a 3-channel config)
+            if (a.bgr_to_rgb) {
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const int t = val[k][0];
+                    val[k][0]   = val[k][2];
+                    val[k][2]   = t;
+                }
+            }
+            if (OF == OF_F32_CHW_VEC) {
+                const int idx = y * win_w + ox0;
+#pragma unroll
+                for (int oc = 0; oc < 3; oc++)
+                    store_f32x4(orsrc, (oc * plane + idx) * 4, lut[oc * 256 + val[0][oc]],
+                                lut[oc * 256 + val[1][oc]], lut[oc * 256 + val[2][oc]],
+                                lut[oc * 256 + val[3][oc]]);
+                continue;
+            }
+            if (a.channel_major) {
 #pragma unroll
                 for (int oc = 0; oc < 3; oc++) {
-                    if (k >= nk || oc >= cn) continue;
-                    if (a.out_dtype == OUT_F32)
-                        ((float*)out_item)[base + k * cn + oc] =
-                            use_lut ? lut[oc * 256 + val[k][oc]] : (float)val[k][oc];
-                    else
-                        out_item[base + k * cn + oc] = (uint8_t)val[k][oc];
+                    if (oc >= cn) break;
+                    const int idx = oc * plane + y * win_w + ox0;
+#pragma unroll
+                    for (int k = 0; k < 4; k++) {
+                        if (k >= nk) break;
+                        if (a.out_dtype == OUT_F32)
+                            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(lut[oc * 256 + val[k][oc]]),
+                                                                  orsrc, (idx + k) * 4, 0, kStoreAux);
+                        else
+                            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)val[k][oc], orsrc, idx + k, 0,
+                                                                 kStoreAux);
+                    }
                 }
+            } else {
+                const int base = (y * win_w + ox0) * cn;
+#pragma unroll
+                for (int k = 0; k < 4; k++)
+#pragma unroll
+                    for (int oc = 0; oc < 3; oc++) {
+                        if (k >= nk || oc >= cn) continue;
+                        const int i = base + k * cn + oc;
+                        if (a.out_dtype == OUT_F32)
+                            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(lut[oc * 256 + val[k][oc]]),
+                                                                  orsrc, i * 4, 0, kStoreAux);
+                        else
+                            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)val[k][oc], orsrc, i, 0, kStoreAux);
+                    }
+            }
         }
+        if (has_next) { // single staging buffer: everyone is done reading it before it is refilled
+            build_yt(y0 + TR, nn, Gn, yt0 + (buf ^ 1) * TR);
+            __syncthreads();
+            stage_commit(J, srsrc, Gn, pf, stage, pitch);
+            __syncthreads();
+        }
+        buf ^= 1;
     }
 
-    if (MODE == KM_STATS) {
+    if (KM == KM_STATS) {
         for (int o = 32; o > 0; o >>= 1) {
             sum0 += __shfl_xor(sum0, o);
             sum1 += __shfl_xor(sum1, o);
@@ -460,43 +616,58 @@ __global__ __launch_bounds__(kBlock) void augment_tiles(LaunchArgs a)
         if (tid < 3) {
             uint32_t s = 0;
             for (int wv = 0; wv < kBlock / 64; wv++) s += (uint32_t)red[wv * 4 + tid];
-            a.partials[((size_t)J.stats_slot * a.max_tiles + tile) * 4 + tid] = s;
+            a.partials[((size_t)J.stats_slot * a.max_tiles + chunk) * 4 + tid] = s;
         }
     }
 }
 
-template __global__ void augment_tiles<KM_FINAL>(LaunchArgs);
-template __global__ void augment_tiles<KM_STATS>(LaunchArgs);
-template __global__ void augment_tiles<KM_RAW>(LaunchArgs);
+// ---- host-side launch helpers (stage.cpp) ----------------------------------------------------
+typedef void (*KernelFn)(LaunchArgs);
 
-// Host-side launch helpers (called from plan.cpp / capi.cpp).
-hipError_t launch_tiles(int mode, const LaunchArgs& a, int n_jobs, hipStream_t stream)
+template <int KM, int RM>
+KernelFn pick_form(bool photo, int of)
 {
-    dim3 grid(a.max_tiles, n_jobs), block(kBlock);
-    switch (mode) {
-    case KM_FINAL:
-        hipLaunchKernelGGL(augment_tiles<KM_FINAL>, grid, block, a.lds_bytes, stream, a);
-        break;
-    case KM_STATS:
-        hipLaunchKernelGGL(augment_tiles<KM_STATS>, grid, block, a.lds_bytes, stream, a);
-        break;
-    default:
-        hipLaunchKernelGGL(augment_tiles<KM_RAW>, grid, block, a.lds_bytes, stream, a);
+    if (of == OF_F32_CHW_VEC)
+        return photo ? augment_tiles<KM, RM, true, OF_F32_CHW_VEC> : augment_tiles<KM, RM, false, OF_F32_CHW_VEC>;
+    return photo ? augment_tiles<KM, RM, true, OF_GENERIC> : augment_tiles<KM, RM, false, OF_GENERIC>;
+}
+
+template <int KM>
+KernelFn pick_rm(int rm, bool photo, int of)
+{
+    switch (rm) {
+    case RESIZE_LINEAR: return pick_form<KM, RESIZE_LINEAR>(photo, of);
+    case RESIZE_AREA2X: return pick_form<KM, RESIZE_AREA2X>(photo, of);
+    default: return pick_form<KM, RESIZE_NEAREST>(photo, of);
     }
+}
+
+KernelFn pick_kernel(int km, int rm, bool photo, int of)
+{
+    if (km == KM_FINAL) return pick_rm<KM_FINAL>(rm, photo, of);
+    if (km == KM_STATS) return pick_rm<KM_STATS>(rm, true, OF_GENERIC);
+    return pick_rm<KM_RAW>(rm, false, OF_GENERIC);
+}
+
+hipError_t launch_tiles(int km, int rm, bool photo, const LaunchArgs& a, int n_jobs, hipStream_t stream)
+{
+    const int of = (a.out_dtype == OUT_F32 && a.channel_major && a.vec_ok) ? OF_F32_CHW_VEC : OF_GENERIC;
+    dim3      grid(a.max_tiles, n_jobs), block(kBlock);
+    hipLaunchKernelGGL(pick_kernel(km, rm, photo, of), grid, block, a.lds_bytes, stream, a);
     return hipGetLastError();
 }
 
 hipError_t set_kernel_lds_limit(int bytes)
 {
-    hipError_t e;
-    if ((e = hipFuncSetAttribute((const void*)augment_tiles<KM_FINAL>,
-                                 hipFuncAttributeMaxDynamicSharedMemorySize, bytes)) != hipSuccess)
-        return e;
-    if ((e = hipFuncSetAttribute((const void*)augment_tiles<KM_STATS>,
-                                 hipFuncAttributeMaxDynamicSharedMemorySize, bytes)) != hipSuccess)
-        return e;
-    return hipFuncSetAttribute((const void*)augment_tiles<KM_RAW>,
-                               hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    for (int km = 0; km < 3; km++)
+        for (int rm = 0; rm < 4; rm++)
+            for (int ph = 0; ph < 2; ph++)
+                for (int of = 0; of < 2; of++) {
+                    hipError_t e = hipFuncSetAttribute((const void*)pick_kernel(km, rm, ph != 0, of),
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+                    if (e != hipSuccess) return e;
+                }
+    return hipSuccess;
 }
 
 } // namespace aeon_hip

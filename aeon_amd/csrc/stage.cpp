@@ -6,6 +6,7 @@
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <stdexcept>
@@ -18,7 +19,7 @@
 #include "param_factory.hpp"
 
 namespace aeon_hip {
-hipError_t launch_tiles(int mode, const LaunchArgs& a, int n_jobs, hipStream_t stream);
+hipError_t launch_tiles(int km, int rm, bool photo, const LaunchArgs& a, int n_jobs, hipStream_t stream);
 hipError_t set_kernel_lds_limit(int bytes);
 } // namespace aeon_hip
 
@@ -41,8 +42,9 @@ struct aeon_error : std::runtime_error {
     } while (0)
 
 constexpr int kMaxLds        = 160 * 1024;
-constexpr int kStageBudget   = 48 * 1024;   // preferred LDS staging bytes per workgroup
+constexpr int kStageBudget   = 16 * 1024;   // preferred LDS bytes per staged band
 constexpr int kStageBudgetHi = 120 * 1024;  // fallback for very wide crops
+constexpr int kBandsPerChunk = 2;
 
 // ---------------------------------------------------------------------------------------------
 // Per-image constants (aeon computes these on the host per record, too)
@@ -50,10 +52,13 @@ constexpr int kStageBudgetHi = 120 * 1024;  // fallback for very wide crops
 
 // OpenCV 2.4 cv::resize dispatch for 8U: identity, INTER_NEAREST, 2x INTER_LINEAR -> area fast
 // path, generic INTER_LINEAR.
+// An identity resize (image::resize's same-size shortcut) is planned as LINEAR / NEAREST: with
+// scale 1 every LINEAR tap is (sx = dx, weights 2048/0), which reproduces the source exactly
+// through both OpenCV vertical formulas, so no separate copy launch is needed.
 int choose_mode(int sw, int sh, int dw, int dh, int interp, int cn)
 {
-    if (sw == dw && sh == dh) return RESIZE_COPY;
     if (interp == AEON_INTERP_NEAREST) return RESIZE_NEAREST;
+    if (sw == dw && sh == dh) return RESIZE_LINEAR;
     double sx = 1. / ((double)dw / sw), sy = 1. / ((double)dh / sh);
     int    ix = cv_round(sx), iy = cv_round(sy);
     bool   fast = std::abs(sx - ix) < DBL_EPSILON && std::abs(sy - iy) < DBL_EPSILON;
@@ -133,7 +138,8 @@ void build_lut(const aeon_out_desc& o, float* lut)
 int stage_cols(const AugJob& J)
 {
     switch (J.mode) {
-    case RESIZE_LINEAR: return std::min(J.crop_w, (int)std::ceil((J.win_w - 1) * J.scale_x) + 4);
+    // +1: the second tap column is staged even where its weight is 0
+    case RESIZE_LINEAR: return std::min(J.crop_w + 1, (int)std::ceil((J.win_w - 1) * J.scale_x) + 4);
     case RESIZE_NEAREST: return std::min(J.crop_w, (int)std::ceil((J.win_w - 1) * J.scale_x) + 3);
     case RESIZE_AREA2X: return 2 * J.win_w;
     default: return J.win_w;
@@ -143,37 +149,50 @@ int stage_rows_for(const AugJob& J, int tr)
 {
     int rows = std::min(tr, J.win_h);
     switch (J.mode) {
-    case RESIZE_LINEAR: return std::min(J.crop_h, (int)std::ceil((rows - 1) * J.scale_y) + 4);
-    case RESIZE_NEAREST: return std::min(J.crop_h, (int)std::ceil((rows - 1) * J.scale_y) + 3);
+    case RESIZE_LINEAR: return std::min(J.crop_h, (int)std::ceil((rows - 1) * J.scale_y) + 3);
+    case RESIZE_NEAREST: return std::min(J.crop_h, (int)std::ceil((rows - 1) * J.scale_y) + 2);
     case RESIZE_AREA2X: return 2 * rows;
     default: return rows;
     }
 }
 
 struct LaunchPlan {
+    int                 rm = RESIZE_LINEAR;
+    bool                photo = false;
+    size_t              blob_off = 0;     // byte offset of this group's jobs in the slot blob
+    size_t              partial_off = 0;  // uint32 offset of this group's contrast partials
     std::vector<AugJob> jobs;
-    int                 tr = 1, stage_rows = 0, stage_pitch = 0, max_win_w = 0, max_tiles = 0;
+    int                 tr = 1, chunk_rows = 1, stage_rows = 0, stage_pitch = 0, max_win_w = 0, max_tiles = 0;
     int                 lds = 0;
     bool                vec_ok = true;
     int                 stats_slots = 0;
+    bool                has_hue = false;
 
     void finalize()
     {
         if (jobs.empty()) return;
-        static const int trs[] = {32, 16, 8, 4, 2, 1};
-        int              budget = kStageBudget;
+        int budget = kStageBudget;
+        int ww     = 0;
+        for (const AugJob& J : jobs) ww = std::max(ww, J.win_w);
+        // rows per tile: about two 4-pixel groups per lane (short tiles keep many workgroups
+        // resident per CU and the per-tile prologue small); knobs for experiments only
+        int tr_cap = std::min(32, std::max(1, (2 * kBlock * 4 + ww - 1) / std::max(ww, 1)));
+        if (const char* e = std::getenv("AEON_HIP_STAGE_KB")) budget = std::max(1, std::atoi(e)) * 1024;
+        if (const char* e = std::getenv("AEON_HIP_TR")) tr_cap = std::max(1, std::atoi(e));
         for (int pass = 0; pass < 2; pass++) {
-            for (int tr : trs) {
-                int rows = 0, pitch = 0, ww = 0;
+            for (int tr = tr_cap; tr >= 1; tr--) {
+                int rows = 0, pitch = 0;
                 for (const AugJob& J : jobs) {
                     rows  = std::max(rows, stage_rows_for(J, tr));
                     pitch = std::max(pitch, (stage_cols(J) + 3) & ~3);
-                    ww    = std::max(ww, J.win_w);
                 }
                 if ((long)rows * pitch * 4 <= budget || (tr == 1 && pass == 1)) {
                     this->tr = tr, stage_rows = rows, stage_pitch = pitch, max_win_w = ww;
-                    lds = lds_layout(max_win_w, tr, stage_rows, stage_pitch).total;
-                    if (lds <= budget + 16 * 1024 || pass == 1) goto chosen;
+                    bool hue = false;
+                    for (const AugJob& J : jobs) hue |= (J.photo & PHOTO_HUE) != 0;
+                    has_hue = hue;
+                    lds     = lds_layout(max_win_w, tr, stage_rows, stage_pitch, photo && hue).total;
+                    goto chosen;
                 }
             }
             budget = kStageBudgetHi;
@@ -182,9 +201,17 @@ struct LaunchPlan {
         if (lds > kMaxLds)
             fail(AEON_HIP_EUNSUPPORTED, "source crop too wide for one LDS-staged row band (" +
                                             std::to_string(lds) + " bytes)");
-        max_tiles = 0;
+        // rows per workgroup: kBandsPerChunk bands, so the next band's loads overlap this band's
+        // work and the per-workgroup tables are built once (measured best at 2 on C2 and C3)
+        int max_h = 0;
+        for (const AugJob& J : jobs) max_h = std::max(max_h, J.win_h);
+        int per = kBandsPerChunk;
+        if (const char* e = std::getenv("AEON_HIP_BANDS")) per = std::atoi(e);
+        per        = std::min(std::max(per, 1), (max_h + tr - 1) / tr);
+        chunk_rows = per * tr;
+        max_tiles  = 0;
         for (AugJob& J : jobs) {
-            J.tiles   = (J.win_h + tr - 1) / tr;
+            J.tiles   = (J.win_h + chunk_rows - 1) / chunk_rows;
             max_tiles = std::max(max_tiles, J.tiles);
         }
     }
@@ -279,7 +306,6 @@ void plan_image(const aeon_img_desc& d, const void* src_base, const aeon_aug_par
             if (p.n_lighting != 3) fail(AEON_HIP_EINVAL, "lighting needs 3 values");
             plan_lighting(J, p.lighting, p.color_noise_std);
         }
-        if (photo & PHOTO_CONTRAST) J.stats_slot = main.stats_slots++;
         J.photo = photo;
     }
     if ((J.out_ptr & 15) != 0 || (J.win_w & 3) != 0) main.vec_ok = false;
@@ -362,7 +388,8 @@ double launch_bytes(const LaunchPlan& L, int mode, size_t out_elem)
     return b;
 }
 
-void timed_launch(aeon_hip_ctx* ctx, int mode, const LaunchArgs& a, int n, hipStream_t stream, double bytes)
+void timed_launch(aeon_hip_ctx* ctx, int mode, const LaunchPlan& P, const LaunchArgs& a, hipStream_t stream,
+                  double bytes)
 {
     KernelTimer t{};
     if (ctx->timing) {
@@ -377,7 +404,7 @@ void timed_launch(aeon_hip_ctx* ctx, int mode, const LaunchArgs& a, int n, hipSt
         t.bytes = bytes;
         HIP_OK(hipEventRecord(t.start, stream));
     }
-    HIP_OK(launch_tiles(mode, a, n, stream));
+    HIP_OK(launch_tiles(mode, P.rm, P.photo, a, (int)P.jobs.size(), stream));
     if (ctx->timing) {
         HIP_OK(hipEventRecord(t.stop, stream));
         ctx->timers.push_back(t);
@@ -405,14 +432,35 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
     std::lock_guard<std::mutex> lock(ctx->mu);
     HIP_OK(hipSetDevice(ctx->device));
 
-    LaunchPlan          pre, main;
+    LaunchPlan          pre_all, main_all;
     size_t              scratch_bytes = 0;
     std::vector<size_t> scratch_off;
     for (int i = 0; i < n; i++)
         plan_image(descs[i], src_base, params[i], o, (uint8_t*)out_dev + (size_t)i * o.item_stride,
-                   is_mask, pre, main, scratch_bytes, scratch_off);
-    pre.finalize();
-    main.finalize();
+                   is_mask, pre_all, main_all, scratch_bytes, scratch_off);
+
+    // one launch per (resize mode, photometric) group: the kernels are specialised on both
+    std::vector<LaunchPlan> pre(4), main(8);
+    for (int rm = 0; rm < 4; rm++) {
+        pre[rm].rm = rm;
+        for (int ph = 0; ph < 2; ph++) main[rm * 2 + ph].rm = rm, main[rm * 2 + ph].photo = ph != 0;
+    }
+    for (const AugJob& J : pre_all.jobs) pre[J.mode].jobs.push_back(J);
+    for (const AugJob& J : main_all.jobs) main[J.mode * 2 + (J.photo ? 1 : 0)].jobs.push_back(J);
+    const size_t lut_bytes = 4096;
+    size_t       blob = lut_bytes, partial_words = 4;
+    for (auto* v : {&pre, &main})
+        for (LaunchPlan& P : *v) {
+            if (P.jobs.empty()) continue;
+            P.vec_ok = main_all.vec_ok;
+            P.finalize();
+            P.blob_off = blob;
+            blob += P.jobs.size() * sizeof(AugJob);
+            for (AugJob& J : P.jobs)
+                if (J.photo & PHOTO_CONTRAST) J.stats_slot = P.stats_slots++;
+            P.partial_off = partial_words;
+            partial_words += (size_t)P.stats_slots * P.max_tiles * 4;
+        }
 
     Slot& s = ctx->slots[ctx->next];
     ctx->next = (ctx->next + 1) % 4;
@@ -420,36 +468,34 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
         HIP_OK(hipEventSynchronize(s.done));
         s.pending = false;
     }
-    const size_t lut_bytes  = 4096;
-    const size_t pre_bytes  = pre.jobs.size() * sizeof(AugJob);
-    const size_t main_bytes = main.jobs.size() * sizeof(AugJob);
-    const size_t blob       = lut_bytes + pre_bytes + main_bytes;
     grow(s.host, s.host_cap, blob, true);
     grow(s.dev, s.dev_cap, blob, false);
     grow(s.scratch, s.scratch_cap, std::max<size_t>(scratch_bytes, 16), false);
-    size_t part_bytes = (size_t)std::max(main.stats_slots, 1) * std::max(main.max_tiles, 1) * 16;
     {
         uint8_t* p = (uint8_t*)s.partials;
-        grow(p, s.partials_cap, part_bytes, false);
+        grow(p, s.partials_cap, partial_words * 4, false);
         s.partials = (uint32_t*)p;
     }
-    // relocate scratch references
-    for (AugJob& P : pre.jobs) P.out_ptr += (uint64_t)s.scratch;
-    for (AugJob& J : main.jobs)
-        if (J.src_scratch) J.src_ptr += (uint64_t)s.scratch;
     build_lut(o, (float*)s.host);
-    std::memcpy(s.host + lut_bytes, pre.jobs.data(), pre_bytes);
-    std::memcpy(s.host + lut_bytes + pre_bytes, main.jobs.data(), main_bytes);
+    for (auto* v : {&pre, &main})
+        for (LaunchPlan& P : *v) {
+            for (AugJob& J : P.jobs) { // relocate scratch references
+                if (v == &pre) J.out_ptr += (uint64_t)s.scratch;
+                if (J.src_scratch) J.src_ptr += (uint64_t)s.scratch;
+            }
+            if (!P.jobs.empty()) std::memcpy(s.host + P.blob_off, P.jobs.data(), P.jobs.size() * sizeof(AugJob));
+        }
     HIP_OK(hipMemcpyAsync(s.dev, s.host, blob, hipMemcpyHostToDevice, stream));
 
-    auto args = [&](const LaunchPlan& L, const AugJob* jobs) {
+    auto args = [&](const LaunchPlan& L) {
         LaunchArgs a{};
-        a.jobs          = jobs;
-        a.lut           = (o.dtype == AEON_DTYPE_F32 && o.has_mean) ? (const float*)s.dev : nullptr;
+        a.jobs          = (const AugJob*)(s.dev + L.blob_off);
+        a.lut           = (const float*)s.dev; // [3][256]: standardized, or (float)x without mean
         a.hsv_tables    = ctx->d_hsv;
-        a.partials      = s.partials;
+        a.partials      = s.partials + L.partial_off;
         a.error         = ctx->d_error;
         a.rows_per_tile = L.tr;
+        a.rows_per_chunk = L.chunk_rows;
         a.max_tiles     = L.max_tiles;
         a.stage_rows    = L.stage_rows;
         a.stage_pitch   = L.stage_pitch;
@@ -459,19 +505,16 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
         a.bgr_to_rgb    = o.bgr_to_rgb;
         a.vec_ok        = L.vec_ok && o.channel_major;
         a.lds_bytes     = L.lds;
+        a.has_hue       = L.has_hue;
         return a;
     };
     const size_t oelem = o.dtype == AEON_DTYPE_F32 ? 4 : 1;
-    if (!pre.jobs.empty()) {
-        LaunchArgs a = args(pre, (const AugJob*)(s.dev + lut_bytes));
-        timed_launch(ctx, KM_RAW, a, (int)pre.jobs.size(), stream, launch_bytes(pre, KM_RAW, 1));
-    }
-    const AugJob* mj = (const AugJob*)(s.dev + lut_bytes + pre_bytes);
-    if (main.stats_slots > 0)
-        timed_launch(ctx, KM_STATS, args(main, mj), (int)main.jobs.size(), stream,
-                     launch_bytes(main, KM_STATS, oelem));
-    timed_launch(ctx, KM_FINAL, args(main, mj), (int)main.jobs.size(), stream,
-                 launch_bytes(main, KM_FINAL, oelem));
+    for (LaunchPlan& P : pre)
+        if (!P.jobs.empty()) timed_launch(ctx, KM_RAW, P, args(P), stream, launch_bytes(P, KM_RAW, 1));
+    for (LaunchPlan& P : main)
+        if (P.stats_slots > 0) timed_launch(ctx, KM_STATS, P, args(P), stream, launch_bytes(P, KM_STATS, oelem));
+    for (LaunchPlan& P : main)
+        if (!P.jobs.empty()) timed_launch(ctx, KM_FINAL, P, args(P), stream, launch_bytes(P, KM_FINAL, oelem));
     HIP_OK(hipEventRecord(s.done, stream));
     s.pending = true;
     return 0;

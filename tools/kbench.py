@@ -1,0 +1,41 @@
+"""Kernel micro-benchmark: per-launch kernel time and HBM rate for C2/C3 under tuning knobs.
+Usage: python tools/kbench.py [config] [knob=value ...]  (knobs are AEON_HIP_* env vars)."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import torch  # noqa: E402
+
+import aeon_amd as A  # noqa: E402
+import bench  # noqa: E402
+from aeon_amd import configs as C  # noqa: E402
+
+
+def measure(cfg, batch, steps=20, warmup=3):
+    """Per step (one batch): summed kernel time of each kind and its algorithmic-byte rate."""
+    torch.cuda.set_device(0)
+    _, kt, _ = bench.run_device(A, C, torch, cfg, batch, steps, warmup, 0, 1, 400, None)
+    res = {}
+    for k, (ms, by, n) in kt.items():
+        if n:
+            res[k] = (ms / steps, by / (ms * 1e-3) / 1e9)
+    return res
+
+
+if __name__ == "__main__":
+    variants = [dict()] + [dict(AEON_HIP_TR=str(t), AEON_HIP_BANDS=str(b)) for t in (8, 9) for b in (1, 2, 4, 7)]
+    cfgs = (("C2", 256), ("C3", 1024))
+    argv = sys.argv[1:]
+    if argv and argv[0] in ("C2", "C3"):
+        cfgs = tuple(c for c in cfgs if c[0] == argv[0])
+        argv = argv[1:]
+    if argv:
+        variants = [dict(kv.split("=", 1) for kv in argv)]
+    for cfg, batch in cfgs:
+        for v in variants:
+            for k in ("AEON_HIP_TR", "AEON_HIP_STAGE_KB", "AEON_HIP_BANDS"):
+                os.environ.pop(k, None)
+            os.environ.update(v)
+            r = measure(cfg, batch)
+            print(cfg, v, {k: f"{ms*1e3:.1f}us {gbs:.0f}GB/s" for k, (ms, gbs) in r.items()}, flush=True)
