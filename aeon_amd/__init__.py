@@ -63,6 +63,11 @@ class OutDesc(ctypes.Structure):
                 ("item_stride", ctypes.c_uint64)]
 
 
+class RecordElem(ctypes.Structure):
+    _fields_ = [("data", ctypes.c_void_p), ("width", ctypes.c_int32), ("height", ctypes.c_int32),
+                ("channels", ctypes.c_int32), ("stride", ctypes.c_int32)]
+
+
 class AeonHipError(RuntimeError):
     def __init__(self, code, msg):
         super().__init__(f"aeon_hip error {code}: {msg}")
@@ -79,6 +84,14 @@ def lib():
         if not os.path.exists(LIB_PATH):
             raise ImportError(f"{LIB_PATH} missing: run `python -c 'import __graft_entry__ as g; g.build()'`"
                               " (the HIP extension is required; there is no CPU fallback)")
+        # One HIP runtime per process: PyTorch ships its own libamdhip64 (SONAME libamdhip64.so.7,
+        # loaded by file name).  Loaded first, it also satisfies this library's dependency, so
+        # torch streams/events and this library's launches share one runtime.  Loaded after this
+        # library, it would bring a second runtime whose queues are not ordered with ours.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = ctypes.CDLL(LIB_PATH)
         P = ctypes.POINTER
         vp = ctypes.c_void_p
@@ -96,6 +109,16 @@ def lib():
         L.aeon_seed_slots.argtypes = [ctypes.c_uint32, ctypes.c_int, P(ctypes.c_uint32)]
         L.aeon_hip_host_alloc.argtypes = [ctypes.c_size_t, P(vp)]
         L.aeon_hip_host_free.argtypes = [vp]
+        L.aeon_decoder_create.argtypes = [ctypes.c_char_p, ctypes.c_int, P(vp)]
+        L.aeon_decoder_destroy.argtypes = [vp]
+        L.aeon_decoder_output_count.argtypes = [vp, P(ctypes.c_int)]
+        L.aeon_decoder_output_info.argtypes = [vp, ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t,
+                                               P(ctypes.c_int64), P(ctypes.c_int), P(ctypes.c_size_t),
+                                               P(ctypes.c_int)]
+        L.aeon_decoder_decode.argtypes = [vp, ctypes.c_int, P(RecordElem), P(vp), ctypes.c_int, vp]
+        L.aeon_decoder_last_error.restype = ctypes.c_char_p
+        L.aeon_manifest_node_slice.argtypes = [ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                               P(ctypes.c_int64), P(ctypes.c_int64)]
         L.aeon_hip_last_error.restype = ctypes.c_char_p
         L.aeon_hip_version.restype = ctypes.c_char_p
         _lib = L
@@ -248,3 +271,75 @@ def synthetic_image(index, w, h, cn=3, seed=0x5EED):
         z = z ^ (z >> np.uint64(31))
     return (z & np.uint64(0xFF)).astype(np.uint8).reshape(h, w, cn) if cn > 1 else \
         (z & np.uint64(0xFF)).astype(np.uint8).reshape(h, w)
+
+
+# ---- decode stage (provider_factory + batch_decoder, host C++) -----------------------------------
+def _check_host(rc):
+    if rc != 0:
+        raise AeonHipError(rc, lib().aeon_decoder_last_error().decode())
+    return rc
+
+
+class Decoder:
+    """aeon batch_decoder over provider_factory::create(config): decode windows of decoded
+    records (one HWC uint8 array per ETL element) into the provider output buffers."""
+
+    def __init__(self, config, device=0):
+        text = config if isinstance(config, str) else json.dumps(config)
+        h = ctypes.c_void_p()
+        _check_host(lib().aeon_decoder_create(text.encode(), device, ctypes.byref(h)))
+        self._h = h
+        n = ctypes.c_int()
+        _check_host(lib().aeon_decoder_output_count(self._h, ctypes.byref(n)))
+        self.outputs = []
+        for i in range(n.value):
+            name = ctypes.create_string_buffer(256)
+            shape = (ctypes.c_int64 * 8)()
+            nd, ib, dt = ctypes.c_int(), ctypes.c_size_t(), ctypes.c_int()
+            _check_host(lib().aeon_decoder_output_info(self._h, i, name, 256, shape, ctypes.byref(nd),
+                                                       ctypes.byref(ib), ctypes.byref(dt)))
+            self.outputs.append({"name": name.value.decode(), "shape": tuple(shape[:nd.value]),
+                                 "item_bytes": ib.value,
+                                 "dtype": {DTYPE_U8: np.uint8, DTYPE_F32: np.float32}.get(dt.value)})
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().aeon_decoder_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def decode(self, records, stream=0):
+        """records: list of tuples of HWC uint8 arrays (one per ETL element).  Returns one numpy
+        array per output buffer, shape (n,) + item shape."""
+        n = len(records)
+        ne = len(self.outputs)
+        keep = []
+        elems = (RecordElem * (n * ne))()
+        for i, rec in enumerate(records):
+            for k in range(ne):
+                a = np.ascontiguousarray(rec[k], dtype=np.uint8)
+                keep.append(a)
+                h, w = a.shape[:2]
+                cn = 1 if a.ndim == 2 else a.shape[2]
+                elems[i * ne + k] = RecordElem(a.ctypes.data, w, h, cn, w * cn)
+        outs = [np.zeros((n,) + o["shape"], o["dtype"]) for o in self.outputs]
+        ptrs = (ctypes.c_void_p * ne)(*[o.ctypes.data for o in outs])
+        _check_host(lib().aeon_decoder_decode(self._h, n, elems, ptrs, 0, ctypes.c_void_p(stream or 0)))
+        return outs
+
+
+def manifest_node_slice(record_count, batch_size, node_id, node_count):
+    """Record indices of one node (aeon manifest_file node slicing)."""
+    cnt = ctypes.c_int64()
+    _check_host(lib().aeon_manifest_node_slice(record_count, batch_size, node_id, node_count, None,
+                                               ctypes.byref(cnt)))
+    out = np.zeros(cnt.value, np.int64)
+    _check_host(lib().aeon_manifest_node_slice(record_count, batch_size, node_id, node_count,
+                                               out.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
+                                               ctypes.byref(cnt)))
+    return out

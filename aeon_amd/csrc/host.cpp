@@ -1,0 +1,692 @@
+// host.cpp -- provider plugin surface + decode stage of the HIP image path (see host.hpp).
+#include "host.hpp"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <map>
+#include <numeric>
+#include <set>
+#include <sstream>
+#include <stdexcept>
+
+namespace aeon_hip {
+
+namespace {
+
+[[noreturn]] void invalid(const std::string& m) { throw std::invalid_argument(m); }
+
+void hip_check(hipError_t e, const char* what)
+{
+    if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+void check(int rc)
+{
+    if (rc != 0) {
+        int code = rc;
+        std::string msg = aeon_hip_last_error();
+        if (code == AEON_HIP_EINVAL) throw std::invalid_argument(msg);
+        throw std::runtime_error(msg);
+    }
+}
+
+size_t levenshtein(const std::string& a, const std::string& b)
+{
+    std::vector<size_t> v0(b.size() + 1), v1(b.size() + 1);
+    std::iota(v0.begin(), v0.end(), 0);
+    for (size_t i = 0; i < a.size(); i++) {
+        v1[0] = i + 1;
+        for (size_t j = 0; j < b.size(); j++)
+            v1[j + 1] = std::min({v1[j] + 1, v0[j + 1] + 1, v0[j] + (a[i] == b[j] ? 0 : 1)});
+        std::swap(v0, v1);
+    }
+    return v0[b.size()];
+}
+
+// interface.cpp verify_config: unknown keys are an error, with the closest known key suggested
+void verify_config(const std::string& where, const std::set<std::string>& known, const Json& js)
+{
+    for (const auto& kv : js.object()) {
+        if (known.count(kv.first)) continue;
+        std::string best;
+        size_t      best_d = (size_t)-1;
+        for (const auto& k : known) {
+            size_t d = levenshtein(kv.first, k);
+            if (d < best_d) best_d = d, best = k;
+        }
+        invalid("config element {" + kv.first + "} is not understood in " + where +
+                (best.empty() ? std::string() : ", did you mean {" + best + "}?"));
+    }
+}
+
+template <typename T>
+void get_num(const Json& js, const char* key, T& v)
+{
+    if (js.has(key)) v = (T)js.at(key).number();
+}
+void get_bool(const Json& js, const char* key, bool& v)
+{
+    if (js.has(key)) v = js.at(key).boolean();
+}
+void get_str(const Json& js, const char* key, std::string& v)
+{
+    if (js.has(key)) v = js.at(key).str();
+}
+
+Json without_type(const Json& j, std::string& type)
+{
+    if (!j.has("type")) invalid("missing required 'type' element in etl object");
+    type = j.at("type").str();
+    return j;
+}
+
+} // namespace
+
+// ---- typemap -------------------------------------------------------------------------------
+output_type::output_type(const std::string& n) : name(n)
+{
+    static const std::map<std::string, std::pair<size_t, int>> all{
+        {"int8_t", {1, -1}},  {"uint8_t", {1, AEON_DTYPE_U8}}, {"int16_t", {2, -1}},
+        {"uint16_t", {2, -1}}, {"int32_t", {4, -1}}, {"uint32_t", {4, -1}},
+        {"float", {4, AEON_DTYPE_F32}}, {"double", {8, -1}}, {"char", {1, -1}}};
+    auto it = all.find(n);
+    if (it == all.end()) throw std::runtime_error("Unable to map output type " + n);
+    size  = it->second.first;
+    dtype = it->second.second;
+}
+
+bool output_type::is_valid_type(const std::string& n)
+{
+    try {
+        output_type t(n);
+        return true;
+    } catch (...) {
+        return false;
+    }
+}
+
+size_t shape_type::byte_size() const
+{
+    size_t n = otype.size;
+    for (size_t d : shape) n *= d;
+    return n;
+}
+
+// ---- image::config (etl_image.cpp:25-65) ------------------------------------------------------
+image_config::image_config(const Json& js)
+{
+    if (js.is_null()) throw std::runtime_error("missing image config in json config");
+    if (!js.has("height")) invalid("Required Argument: 'height' not set");
+    if (!js.has("width")) invalid("Required Argument: 'width' not set");
+    get_num(js, "height", height);
+    get_num(js, "width", width);
+    get_str(js, "name", name);
+    get_bool(js, "bgr_to_rgb", bgr_to_rgb);
+    get_bool(js, "channel_major", channel_major);
+    get_num(js, "channels", channels);
+    if (!(channels == 1 || channels == 3)) invalid("value for 'channels' out of range");
+    get_str(js, "output_type", output_type_name);
+    if (!output_type::is_valid_type(output_type_name)) invalid("value for 'output_type' out of range");
+    verify_config("image", {"type", "height", "width", "name", "bgr_to_rgb", "channel_major", "channels",
+                            "output_type"},
+                  js);
+    if (js.at("height").number() <= 0) invalid("invalid height");
+    if (js.at("width").number() <= 0) invalid("invalid width");
+    if (bgr_to_rgb && channels != 3)
+        invalid("invalid config: bgr_to_rgb can be 'true' only for channels set to '3'");
+    shape.otype = output_type(output_type_name);
+    if (channel_major) {
+        shape.shape = {channels, height, width};
+        shape.names = {"channels", "height", "width"};
+    } else {
+        shape.shape = {height, width, channels};
+        shape.names = {"height", "width", "channels"};
+    }
+}
+
+// ---- providers --------------------------------------------------------------------------------
+const shape_type& provider_interface::get_output_shape(const std::string& name) const
+{
+    for (const auto& p : m_output_shapes)
+        if (p.first == name) return p.second;
+    throw std::runtime_error("key '" + name + "' not found");
+}
+
+const std::vector<std::string>& provider_interface::get_buffer_names()
+{
+    if (m_buffer_names.empty())
+        for (const auto& p : m_output_shapes) m_buffer_names.push_back(p.first);
+    return m_buffer_names;
+}
+
+namespace {
+
+std::string create_name(const std::string& name, const std::string& base)
+{
+    return name.empty() ? base : name + "." + base;
+}
+
+// provider::image (provider.cpp:145-184): make_params when the record has none yet,
+// transform_single_image + image::loader::load on the GPU at post_process time.
+class image_provider : public etl_provider {
+public:
+    image_provider(const Json& js, const Json& aug)
+        : m_cfg(js), m_factory(aug), m_name(create_name(m_cfg.name, "image"))
+    {
+        // image::loader ctor (etl_image.cpp:204-244)
+        const auto& mean = m_factory.mean;
+        const auto& std_ = m_factory.stddev;
+        if (!mean.empty() || !std_.empty()) {
+            if (!(m_cfg.output_type_name == "float" || m_cfg.output_type_name == "double"))
+                invalid("Standardization (mean, stddev) is supported only for float or double 'output_type'.");
+            if (mean.size() != m_cfg.channels || std_.size() != m_cfg.channels)
+                invalid("Size of 'mean' and 'stddev' must be equal to number of channels or empty.");
+        }
+        if (m_factory.fixed_aspect_ratio)
+            throw std::runtime_error("fixed_aspect_ratio is not implemented in the HIP stage");
+        if (m_cfg.shape.otype.dtype < 0)
+            throw std::runtime_error("output_type '" + m_cfg.output_type_name +
+                                     "' is not implemented in the HIP stage (uint8_t, float)");
+    }
+    void provide(int, const decoded_element& in, augmentation& aug, std::minstd_rand0& random,
+                 aeon_aug_params& params) const override
+    {
+        if (!aug.has) {
+            m_factory.make_params(random, in.width, in.height, (int)m_cfg.width, (int)m_cfg.height, &aug.image);
+            aug.has = true;
+        }
+        params = aug.image;
+    }
+    bool               is_mask() const override { return false; }
+    const shape_type&  shape() const override { return m_cfg.shape; }
+    const std::string& buffer_name() const override { return m_name; }
+    aeon_out_desc      out_desc() const override
+    {
+        aeon_out_desc o{};
+        o.dtype         = m_cfg.shape.otype.dtype;
+        o.channels      = (int)m_cfg.channels;
+        o.channel_major = m_cfg.channel_major;
+        o.bgr_to_rgb    = m_cfg.bgr_to_rgb;
+        o.has_mean      = !m_factory.mean.empty();
+        for (size_t i = 0; i < m_factory.mean.size() && i < 3; i++)
+            o.mean[i] = m_factory.mean[i], o.stddev[i] = m_factory.stddev[i];
+        o.item_stride = m_cfg.shape.byte_size();
+        return o;
+    }
+
+private:
+    image_config  m_cfg;
+    param_factory m_factory;
+    std::string   m_name;
+};
+
+// provider::pixelmask (provider.cpp:353-393): shares the record's image params.
+class pixelmask_provider : public etl_provider {
+public:
+    pixelmask_provider(const Json& js, const Json& aug)
+        : m_cfg(js), m_factory(aug), m_name(create_name(m_cfg.name, "pixelmask"))
+    {
+        if (m_cfg.shape.otype.dtype < 0)
+            throw std::runtime_error("output_type '" + m_cfg.output_type_name +
+                                     "' is not implemented in the HIP stage (uint8_t, float)");
+    }
+    void provide(int, const decoded_element& in, augmentation& aug, std::minstd_rand0& random,
+                 aeon_aug_params& params) const override
+    {
+        if (!aug.has) {
+            m_factory.make_params(random, in.width, in.height, (int)m_cfg.width, (int)m_cfg.height, &aug.image);
+            aug.has = true;
+        }
+        params = aug.image;
+    }
+    bool               is_mask() const override { return true; }
+    const shape_type&  shape() const override { return m_cfg.shape; }
+    const std::string& buffer_name() const override { return m_name; }
+    aeon_out_desc      out_desc() const override
+    {
+        aeon_out_desc o{};
+        o.dtype         = m_cfg.shape.otype.dtype;
+        o.channels      = (int)m_cfg.channels;
+        o.channel_major = m_cfg.channel_major;
+        o.item_stride   = m_cfg.shape.byte_size();
+        return o;
+    }
+
+private:
+    image_config  m_cfg;
+    param_factory m_factory;
+    std::string   m_name;
+};
+
+} // namespace
+
+provider_base::provider_base(const Json& js, const std::vector<Json>& etl, const Json& aug)
+    : provider_interface(js, etl.size())
+{
+    for (const Json& j : etl) {
+        std::string type;
+        without_type(j, type);
+        std::unique_ptr<etl_provider> p;
+        if (type == "image") p.reset(new image_provider(j, aug));
+        else if (type == "pixelmask") p.reset(new pixelmask_provider(j, aug));
+        else if (type == "label" || type == "localization_rcnn" || type == "localization_ssd" ||
+                 type == "boundingbox" || type == "blob" || type == "video" || type == "char_map" ||
+                 type == "label_map")
+            throw std::runtime_error("etl type '" + type + "' is outside the HIP image stage");
+        else
+            invalid("unsupported etl type '" + type + "'");
+        m_output_shapes.emplace_back(p->buffer_name(), p->shape());
+        m_providers.push_back(std::move(p));
+    }
+}
+
+void provider_base::provide(int idx, const decoded_element* elems, decode_window& w,
+                            std::minstd_rand0& random) const
+{
+    draw(idx, elems, w, random);
+    stage(idx, elems, w);
+}
+
+void provider_base::draw(int idx, const decoded_element* elems, decode_window& w, std::minstd_rand0& random) const
+{
+    augmentation aug;
+    for (size_t k = 0; k < m_providers.size(); k++) {
+        const decoded_element& e = elems[k];
+        if (!e.data || e.width <= 0 || e.height <= 0) {
+            std::stringstream ss;
+            ss << "received " << (m_providers[k]->is_mask() ? "pixelmask" : "encoded image")
+               << " with size 0, at idx " << idx;
+            throw std::runtime_error(ss.str());
+        }
+        m_providers[k]->provide(idx, e, aug, random, w.params[k][idx]);
+    }
+}
+
+void provider_base::stage(int idx, const decoded_element* elems, decode_window& w) const
+{
+    for (size_t k = 0; k < m_providers.size(); k++) {
+        const decoded_element& e = elems[k];
+        const size_t row = (size_t)e.width * e.channels;
+        uint8_t*     dst = w.arena + w.offset[k][idx];
+        if ((size_t)e.stride == row) {
+            std::memcpy(dst, e.data, row * e.height);
+        } else {
+            for (int y = 0; y < e.height; y++) std::memcpy(dst + y * row, e.data + (size_t)y * e.stride, row);
+        }
+    }
+}
+
+void provider_base::post_process(aeon_hip_ctx* ctx, decode_window& w, const uint8_t* dev_arena,
+                                 void* const* outputs, void* stream) const
+{
+    for (size_t k = 0; k < m_providers.size(); k++) {
+        const etl_provider& p = *m_providers[k];
+        aeon_out_desc       o = p.out_desc();
+        if (p.is_mask())
+            check(aeon_hip_mask_batch(ctx, w.n, w.descs[k].data(), dev_arena, w.params[k].data(), &o,
+                                      outputs[k], stream));
+        else
+            check(aeon_hip_augment_batch(ctx, w.n, w.descs[k].data(), dev_arena, w.params[k].data(), &o,
+                                         outputs[k], stream));
+    }
+}
+
+std::shared_ptr<provider_base> provider_factory::create(const Json& config)
+{
+    if (!config.has("etl")) invalid("required argument 'etl' not set");
+    std::vector<Json> etl = config.at("etl").array();
+    Json              aug;
+    if (config.has("augmentation")) {
+        const auto& a = config.at("augmentation").array();
+        for (const Json& j : a)
+            if (!j.has("type")) invalid("augmentation missing 'type'");
+        if (!a.empty()) aug = a[0]; // provider_factory.cpp:39-43: only the first is used
+    }
+    return std::make_shared<provider_base>(config, etl, aug);
+}
+
+// ---- thread_pool ----------------------------------------------------------------------------------
+thread_pool::thread_pool(int nthreads)
+{
+    for (int i = 0; i < std::max(1, nthreads); i++) m_threads.emplace_back([this] { worker(); });
+}
+
+thread_pool::~thread_pool()
+{
+    {
+        std::lock_guard<std::mutex> l(m_mu);
+        m_stop = true;
+    }
+    m_cv.notify_all();
+    for (auto& t : m_threads) t.join();
+}
+
+void thread_pool::worker()
+{
+    long seen = 0;
+    for (;;) {
+        const std::function<void(int)>* fn;
+        int                            n;
+        {
+            std::unique_lock<std::mutex> l(m_mu);
+            m_cv.wait(l, [&] { return m_stop || m_generation != seen; });
+            if (m_stop) return;
+            seen = m_generation;
+            fn   = m_fn;
+            n    = m_n;
+        }
+        for (;;) { // dynamic task distribution (thread_pool.hpp:155-162)
+            int i = m_next.fetch_add(1);
+            if (i >= n) break;
+            try {
+                (*fn)(i);
+            } catch (...) {
+                std::lock_guard<std::mutex> l(m_mu);
+                if (!m_error) m_error = std::current_exception();
+            }
+        }
+        {
+            std::lock_guard<std::mutex> l(m_mu);
+            if (--m_active == 0) m_done_cv.notify_all();
+        }
+    }
+}
+
+void thread_pool::run(int n, const std::function<void(int)>& fn)
+{
+    {
+        std::lock_guard<std::mutex> l(m_mu);
+        m_fn     = &fn;
+        m_n      = n;
+        m_active = (int)m_threads.size();
+        m_error  = nullptr;
+        m_next   = 0;
+        m_generation++;
+    }
+    m_cv.notify_all();
+    std::unique_lock<std::mutex> l(m_mu);
+    m_done_cv.wait(l, [&] { return m_active == 0; });
+    if (m_error) std::rethrow_exception(m_error); // thread_pool.hpp:113-115
+}
+
+// ---- batch_decoder -------------------------------------------------------------------------------
+int aeon_thread_count(const std::string& cpu_list)
+{
+    // util.cpp:337-373: AEON_CPU_LIST / cpu_list, else hardware_concurrency - min(2, hc/8)
+    std::string list = cpu_list;
+    if (const char* e = std::getenv("AEON_CPU_LIST"))
+        if (*e) list = e;
+    if (!list.empty()) {
+        std::set<int>     cpus;
+        std::stringstream ss(list);
+        std::string       tok;
+        while (std::getline(ss, tok, ',')) {
+            auto dash = tok.find('-');
+            if (dash == std::string::npos) cpus.insert(std::stoi(tok));
+            else
+                for (int i = std::stoi(tok.substr(0, dash)); i <= std::stoi(tok.substr(dash + 1)); i++)
+                    cpus.insert(i);
+        }
+        return std::max<int>(1, (int)cpus.size());
+    }
+    int hc = (int)std::thread::hardware_concurrency();
+    return std::max(1, hc - std::min(2, hc / 8));
+}
+
+batch_decoder::batch_decoder(const Json& config, int device) : m_device(device)
+{
+    verify_config("loader", {"manifest_filename", "manifest_root", "batch_size", "cache_directory",
+                             "block_size", "batch_major", "subset_fraction", "shuffle_enable",
+                             "shuffle_manifest", "cpu_list", "pinned", "random_seed", "iteration_mode",
+                             "iteration_mode_count", "etl", "augmentation", "node_id", "node_count",
+                             "ssd_config", "decode_thread_count"},
+                  config);
+    if (!config.has("batch_size")) invalid("Required Argument: 'batch_size' not set");
+    get_num(config, "batch_size", m_batch_size);
+    if (m_batch_size <= 0) invalid("batch_size must be > 0");
+    uint32_t seed = 0, node_id = 0, node_count = 0;
+    get_num(config, "random_seed", seed);
+    get_num(config, "node_id", node_id);
+    get_num(config, "node_count", node_count);
+    if (node_count > 1) {
+        if (node_id >= node_count) throw std::runtime_error("node_id can't be greater than node_count");
+        if (seed == 0) seed = 1; // loader.cpp:109-113
+    }
+    std::string cpu_list;
+    get_str(config, "cpu_list", cpu_list);
+    int threads = aeon_thread_count(cpu_list);
+    get_num(config, "decode_thread_count", threads);
+    m_provider = provider_factory::create(config);
+    m_pool.reset(new thread_pool(threads));
+    m_local_random.seed(std::random_device{}());
+    // decoder seed = random_seed + node_id (loader.cpp:174); deterministic when non-zero
+    const uint32_t dseed = seed ? seed + node_id : 0;
+    m_deterministic      = dseed != 0;
+    if (m_deterministic) {
+        // slot engines are seeded lazily per window size from one minstd_rand0(seed)
+        m_random.clear();
+        std::minstd_rand0 g(dseed);
+        m_random.resize(4096);
+        for (auto& e : m_random) e.seed(g());
+    }
+    // the HIP context is created on the first window (configs validate without a GPU)
+    m_dev_out.assign(m_provider->providers().size(), nullptr);
+    m_dev_out_cap.assign(m_provider->providers().size(), 0);
+}
+
+batch_decoder::~batch_decoder()
+{
+    if (!m_ctx) return; // no window ran: nothing was allocated on the device
+    aeon_hip_ctx_destroy(m_ctx);
+    (void)hipSetDevice(m_device);
+    if (m_pinned) (void)hipHostFree(m_pinned);
+    if (m_dev_src) (void)hipFree(m_dev_src);
+    for (auto* p : m_dev_out)
+        if (p) (void)hipFree(p);
+}
+
+void batch_decoder::decode(int n, const decoded_element* records, void* const* outputs, bool on_device,
+                           void* stream_)
+{
+    if (n <= 0) return;
+    if (m_deterministic && n > (int)m_random.size())
+        invalid("decode window larger than the deterministic slot table (4096)");
+    if (!m_ctx) check(aeon_hip_ctx_create(m_device, &m_ctx));
+    hip_check(hipSetDevice(m_device), "hipSetDevice");
+    hipStream_t   stream = (hipStream_t)stream_;
+    const int     ne     = (int)m_provider->get_input_count();
+    decode_window w;
+    w.n = n;
+    w.descs.assign(ne, std::vector<aeon_img_desc>(n));
+    w.params.assign(ne, std::vector<aeon_aug_params>(n));
+    w.offset.assign(ne, std::vector<size_t>(n));
+    size_t total = 0;
+    for (int i = 0; i < n; i++)
+        for (int k = 0; k < ne; k++) {
+            const decoded_element& e = records[(size_t)i * ne + k];
+            const size_t           b = (size_t)std::max(e.width, 0) * std::max(e.height, 0) * std::max(e.channels, 0);
+            w.offset[k][i]           = total;
+            w.descs[k][i]            = aeon_img_desc{total, e.width, e.height, e.width * e.channels, e.channels};
+            total += (b + 15) & ~(size_t)15;
+        }
+    total = std::max<size_t>(total, 16);
+    if (total > m_pinned_cap) {
+        if (m_pinned) hip_check(hipHostFree(m_pinned), "hipHostFree");
+        m_pinned = nullptr;
+        hip_check(hipHostMalloc((void**)&m_pinned, total, hipHostMallocDefault), "hipHostMalloc");
+        m_pinned_cap = total;
+    }
+    if (total > m_dev_src_cap) {
+        if (m_dev_src) hip_check(hipFree(m_dev_src), "hipFree");
+        m_dev_src = nullptr;
+        hip_check(hipMalloc((void**)&m_dev_src, total), "hipMalloc");
+        m_dev_src_cap = total;
+    }
+    w.arena = m_pinned;
+    // batch_decoder::process: the slot engine of record i draws its params (deterministic mode
+    // swaps the slot engine in and out, batch_decoder.cpp:62-71).  The draws run in record
+    // order on this thread -- aeon's single-threaded order, the only reproducible one, since
+    // the lighting normal_distribution caches a value inside the shared factory -- and the
+    // pool threads stage the pixels into the pinned arena.
+    for (int i = 0; i < n; i++)
+        m_provider->draw(i, records + (size_t)i * ne, w, m_deterministic ? m_random[i] : m_local_random);
+    m_pool->run(n, [&](int i) { m_provider->stage(i, records + (size_t)i * ne, w); });
+    hip_check(hipMemcpyAsync(m_dev_src, m_pinned, total, hipMemcpyHostToDevice, stream), "hipMemcpyAsync");
+    std::vector<void*> outs(ne);
+    for (int k = 0; k < ne; k++) {
+        const size_t bytes = (size_t)n * m_provider->providers()[k]->shape().byte_size();
+        if (on_device) {
+            outs[k] = outputs[k];
+        } else {
+            if (bytes > m_dev_out_cap[k]) {
+                if (m_dev_out[k]) hip_check(hipFree(m_dev_out[k]), "hipFree");
+                m_dev_out[k] = nullptr;
+                hip_check(hipMalloc((void**)&m_dev_out[k], bytes), "hipMalloc");
+                m_dev_out_cap[k] = bytes;
+            }
+            outs[k] = m_dev_out[k];
+        }
+    }
+    m_provider->post_process(m_ctx, w, m_dev_src, outs.data(), stream);
+    if (!on_device)
+        for (int k = 0; k < ne; k++)
+            hip_check(hipMemcpyAsync(outputs[k], outs[k], (size_t)n * m_provider->providers()[k]->shape().byte_size(),
+                                     hipMemcpyDeviceToHost, stream),
+                      "hipMemcpyAsync");
+    // the pinned arena and the window's params must outlive the copies: finish the window
+    check(aeon_hip_synchronize(m_ctx, stream));
+}
+
+// ---- manifest_file node slicing ------------------------------------------------------------------
+std::vector<int64_t> manifest_node_slice(int64_t record_count, int batch_size, int node_id, int node_count)
+{
+    std::vector<int64_t> out;
+    if (node_count <= 1) {
+        out.resize(record_count);
+        std::iota(out.begin(), out.end(), 0);
+        return out;
+    }
+    if (node_id < 0 || node_id >= node_count) invalid("node_id can't be greater than node_count");
+    if (batch_size <= 0) invalid("batch_size must be > 0");
+    const int64_t count   = record_count / node_count;
+    const int64_t batches = count / batch_size;
+    out.resize(count);
+    for (int64_t i = 0; i < batches * batch_size; i++) {
+        const int64_t batch_num = i / batch_size, in_batch = i % batch_size;
+        out[i] = batch_num * batch_size * node_count + (int64_t)batch_size * node_id + in_batch;
+    }
+    const int64_t tail_count = count - batches * batch_size;
+    const int64_t tail_src   = batches * batch_size * node_count + tail_count * node_id;
+    const int64_t tail_dst   = batches * batch_size;
+    for (int64_t i = 0; i < tail_count; i++) out[i + tail_dst] = i + tail_src;
+    return out;
+}
+
+} // namespace aeon_hip
+
+// ---- C ABI of the host layer ---------------------------------------------------------------------
+struct aeon_decoder {
+    std::unique_ptr<aeon_hip::batch_decoder> d;
+};
+
+namespace {
+thread_local std::string g_host_err;
+
+template <typename F>
+int host_guarded(F&& f)
+{
+    try {
+        f();
+        return 0;
+    } catch (const std::invalid_argument& e) {
+        g_host_err = e.what();
+        return AEON_HIP_EINVAL;
+    } catch (const std::exception& e) {
+        g_host_err = e.what();
+        return AEON_HIP_ERUNTIME;
+    }
+}
+} // namespace
+
+extern "C" {
+
+int aeon_decoder_create(const char* config_json, int device, aeon_decoder** out)
+{
+    return host_guarded([&] {
+        if (!out || !config_json) throw std::invalid_argument("null argument");
+        auto* d = new aeon_decoder();
+        try {
+            d->d.reset(new aeon_hip::batch_decoder(aeon_hip::Json::parse(config_json), device));
+        } catch (...) {
+            delete d;
+            throw;
+        }
+        *out = d;
+    });
+}
+
+int aeon_decoder_destroy(aeon_decoder* d)
+{
+    delete d;
+    return 0;
+}
+
+int aeon_decoder_output_count(aeon_decoder* d, int* count)
+{
+    return host_guarded([&] {
+        if (!d || !count) throw std::invalid_argument("null argument");
+        *count = (int)d->d->provider().get_output_shapes().size();
+    });
+}
+
+int aeon_decoder_output_info(aeon_decoder* d, int index, char* name, size_t name_cap, int64_t* shape,
+                             int* ndim, size_t* item_bytes, int* dtype)
+{
+    return host_guarded([&] {
+        if (!d) throw std::invalid_argument("null decoder");
+        const auto& shapes = d->d->provider().get_output_shapes();
+        if (index < 0 || index >= (int)shapes.size()) throw std::invalid_argument("output index out of range");
+        const auto& s = shapes[index];
+        if (name && name_cap) {
+            std::strncpy(name, s.first.c_str(), name_cap - 1);
+            name[name_cap - 1] = 0;
+        }
+        if (ndim) *ndim = (int)s.second.shape.size();
+        if (shape)
+            for (size_t i = 0; i < s.second.shape.size(); i++) shape[i] = (int64_t)s.second.shape[i];
+        if (item_bytes) *item_bytes = s.second.byte_size();
+        if (dtype) *dtype = s.second.otype.dtype;
+    });
+}
+
+int aeon_decoder_decode(aeon_decoder* d, int n, const aeon_record_elem* elems, void* const* outputs,
+                        int outputs_on_device, void* stream)
+{
+    return host_guarded([&] {
+        if (!d || (n > 0 && (!elems || !outputs))) throw std::invalid_argument("null argument");
+        const int ne = (int)d->d->provider().get_input_count();
+        std::vector<aeon_hip::decoded_element> recs((size_t)n * ne);
+        for (size_t i = 0; i < recs.size(); i++)
+            recs[i] = aeon_hip::decoded_element{(const uint8_t*)elems[i].data, elems[i].width, elems[i].height,
+                                                elems[i].channels,
+                                                elems[i].stride ? elems[i].stride : elems[i].width * elems[i].channels};
+        d->d->decode(n, recs.data(), outputs, outputs_on_device != 0, stream);
+    });
+}
+
+int aeon_manifest_node_slice(int64_t record_count, int batch_size, int node_id, int node_count,
+                             int64_t* indices, int64_t* count)
+{
+    return host_guarded([&] {
+        if (!count) throw std::invalid_argument("null count");
+        auto v = aeon_hip::manifest_node_slice(record_count, batch_size, node_id, node_count);
+        if (indices) std::copy(v.begin(), v.end(), indices);
+        *count = (int64_t)v.size();
+    });
+}
+
+const char* aeon_decoder_last_error(void) { return g_host_err.c_str(); }
+
+} // extern "C"

@@ -1,0 +1,190 @@
+// host.hpp -- aeon's provider plugin surface and decode stage for the HIP image path (host C++).
+//
+// Mirrors, with the same names and argument meaning:
+//   provider_interface       src/provider_interface.hpp:32-85  (post_process = the GPU flush)
+//   provider_factory::create src/provider_factory.cpp:24-51
+//   provider::image          src/provider.cpp:145-184          (etl type "image")
+//   provider::pixelmask      src/provider.cpp:353-393          (etl type "pixelmask")
+//   image::config            src/etl_image.hpp:56-96, etl_image.cpp:25-65
+//   batch_decoder            src/batch_decoder.cpp:24-99        (thread pool + deterministic slots)
+//   thread_pool              src/thread_pool.hpp:82-175         (dynamic atomic task counter)
+//   manifest node slicing    src/manifest_file.cpp:278-295
+// Decoding (image::extractor::extract = cv::imdecode) stays with the caller: records arrive as
+// decoded HWC uint8 pixels.  Per record, the pool threads draw the augmentation params and
+// stage the pixels into pinned memory; one flush per decode window runs the HIP kernels.
+#pragma once
+#include <atomic>
+#include <condition_variable>
+#include <exception>
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <random>
+#include <string>
+#include <thread>
+#include <utility>
+#include <vector>
+
+#include "../../include/aeon_hip.h"
+#include "json.hpp"
+#include "param_factory.hpp"
+
+namespace aeon_hip {
+
+// typemap.hpp output_type (the types this stage writes)
+struct output_type {
+    std::string name;
+    size_t      size  = 1;
+    int         dtype = AEON_DTYPE_U8;
+    explicit output_type(const std::string& n = "uint8_t");
+    static bool is_valid_type(const std::string& n);
+};
+
+struct shape_type {
+    std::vector<size_t>      shape;
+    std::vector<std::string> names;
+    output_type              otype;
+    size_t                   byte_size() const;
+};
+
+// image::config
+struct image_config {
+    uint32_t    height = 0, width = 0;
+    std::string output_type_name = "uint8_t";
+    bool        bgr_to_rgb = false, channel_major = true;
+    uint32_t    channels = 3;
+    std::string name;
+    shape_type  shape;
+    explicit image_config(const Json& js);
+};
+
+// A decoded element of a record (what image::extractor::extract returns, as plain pixels).
+struct decoded_element {
+    const uint8_t* data = nullptr;
+    int            width = 0, height = 0, channels = 0, stride = 0;
+};
+
+// Per-window staging shared by the providers (filled concurrently by the pool threads).
+struct decode_window {
+    int                                       n = 0;
+    std::vector<std::vector<aeon_img_desc>>   descs;  // [provider][record]
+    std::vector<std::vector<aeon_aug_params>> params; // [provider][record]
+    std::vector<std::vector<size_t>>          offset; // [provider][record] in the pinned arena
+    uint8_t*                                  arena = nullptr;
+};
+
+// augmentation shared by the ETL providers of one record (provider.cpp:109-119)
+struct augmentation {
+    bool            has = false;
+    aeon_aug_params image{};
+};
+
+class provider_interface {
+public:
+    provider_interface(Json js, size_t input_count) : m_js(std::move(js)), m_input_count(input_count) {}
+    virtual ~provider_interface() = default;
+
+    size_t                                                  get_input_count() const { return m_input_count; }
+    const std::vector<std::pair<std::string, shape_type>>& get_output_shapes() const { return m_output_shapes; }
+    const shape_type&                                       get_output_shape(const std::string& name) const;
+    const std::vector<std::string>&                         get_buffer_names();
+    const Json&                                             get_config() const { return m_js; }
+
+protected:
+    std::vector<std::pair<std::string, shape_type>> m_output_shapes;
+    std::vector<std::string>                        m_buffer_names;
+    Json                                            m_js;
+    size_t                                          m_input_count = 0;
+};
+
+// One ETL element provider of the HIP stage (provider::image / provider::pixelmask).
+class etl_provider {
+public:
+    virtual ~etl_provider() = default;
+    // host half of provide(): params for record idx (shared through aug) + its descriptor
+    virtual void provide(int idx, const decoded_element& in, augmentation& aug, std::minstd_rand0& random,
+                         aeon_aug_params& params) const = 0;
+    virtual bool               is_mask() const = 0;
+    virtual const shape_type&  shape() const = 0;
+    virtual const std::string& buffer_name() const = 0;
+    virtual aeon_out_desc      out_desc() const = 0;
+};
+
+class provider_base : public provider_interface {
+public:
+    provider_base(const Json& js, const std::vector<Json>& etl, const Json& augmentation);
+    // record idx of the window: params for every ETL element from one shared augmentation
+    // (provider_base::provide, provider.cpp:109-119), then its pixels into the pinned arena
+    void provide(int idx, const decoded_element* elems, decode_window& w, std::minstd_rand0& random) const;
+    void draw(int idx, const decoded_element* elems, decode_window& w, std::minstd_rand0& random) const;
+    void stage(int idx, const decoded_element* elems, decode_window& w) const;
+    // aeon's vestigial post_process hook, used as the per-window GPU flush: outputs[k] receives
+    // n items of provider k (device pointers if on_device, else host memory)
+    void post_process(aeon_hip_ctx* ctx, decode_window& w, const uint8_t* dev_arena, void* const* outputs,
+                      void* stream) const;
+    const std::vector<std::unique_ptr<etl_provider>>& providers() const { return m_providers; }
+
+private:
+    std::vector<std::unique_ptr<etl_provider>> m_providers;
+};
+
+struct provider_factory {
+    static std::shared_ptr<provider_base> create(const Json& config);
+};
+
+// thread_pool (src/thread_pool.hpp): persistent workers, run(n, fn) hands out task ids from
+// one atomic counter; the first exception is kept and rethrown after the barrier.
+class thread_pool {
+public:
+    explicit thread_pool(int nthreads);
+    ~thread_pool();
+    void run(int n, const std::function<void(int)>& fn);
+    int  size() const { return (int)m_threads.size(); }
+
+private:
+    void                           worker();
+    std::vector<std::thread>       m_threads;
+    std::mutex                     m_mu;
+    std::condition_variable        m_cv, m_done_cv;
+    const std::function<void(int)>* m_fn = nullptr;
+    int                            m_n = 0, m_active = 0;
+    long                           m_generation = 0;
+    std::atomic<int>               m_next{0};
+    std::exception_ptr             m_error;
+    bool                           m_stop = false;
+};
+
+// batch_decoder: decode windows of records on the pool, flush each window to the GPU.
+class batch_decoder {
+public:
+    batch_decoder(const Json& config, int device);
+    ~batch_decoder();
+    // n records x input_count elements (row-major); outputs[k] per provider buffer
+    void decode(int n, const decoded_element* records, void* const* outputs, bool outputs_on_device,
+                void* stream);
+    provider_base& provider() { return *m_provider; }
+    int            batch_size() const { return m_batch_size; }
+
+private:
+    std::shared_ptr<provider_base> m_provider;
+    int                            m_batch_size = 1;
+    bool                           m_deterministic = false;
+    std::vector<std::minstd_rand0> m_random; // one engine per decode slot (batch_decoder.cpp:47-54)
+    std::minstd_rand0              m_local_random; // non-deterministic mode (util.cpp:266)
+    std::unique_ptr<thread_pool>   m_pool;
+    aeon_hip_ctx*                  m_ctx = nullptr;
+    int                            m_device = 0;
+    uint8_t*                       m_pinned = nullptr;
+    size_t                         m_pinned_cap = 0;
+    uint8_t*                       m_dev_src = nullptr;
+    size_t                         m_dev_src_cap = 0;
+    std::vector<uint8_t*>          m_dev_out;
+    std::vector<size_t>            m_dev_out_cap;
+};
+
+// manifest_file node slicing (generate_blocks, src/manifest_file.cpp:278-295)
+std::vector<int64_t> manifest_node_slice(int64_t record_count, int batch_size, int node_id, int node_count);
+
+int aeon_thread_count(const std::string& cpu_list); // get_thread_affinity_map policy
+
+} // namespace aeon_hip

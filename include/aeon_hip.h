@@ -126,6 +126,39 @@ int aeon_make_params(aeon_param_factory* f, uint32_t* engine_state, int in_w, in
 /* batch_decoder deterministic mode (src/batch_decoder.cpp:47-54): slot engine state words. */
 int aeon_seed_slots(uint32_t seed, int n, uint32_t* states);
 
+/* ---- decode stage: provider_factory + batch_decoder (host C++ above the kernels) --------------
+ * aeon_decoder = batch_decoder (src/batch_decoder.cpp:24-99) over provider_factory::create
+ * (src/provider_factory.cpp:24-51) with "image" / "pixelmask" ETL providers.  config_json is the
+ * aeon loader configuration ({"batch_size", "random_seed", "node_id", "cpu_list", "etl": [...],
+ * "augmentation": [...]}, src/loader.hpp:50-109; unknown keys are rejected like verify_config).
+ * Records arrive decoded (image::extractor::extract stays with the caller). */
+typedef struct aeon_decoder aeon_decoder;
+
+/* One decoded element of a record: HWC uint8 (BGR) pixels in host memory. */
+typedef struct aeon_record_elem {
+    const void* data;
+    int32_t     width, height, channels;
+    int32_t     stride; /* bytes per row; 0 = width*channels */
+} aeon_record_elem;
+
+int aeon_decoder_create(const char* config_json, int device, aeon_decoder** out);
+int aeon_decoder_destroy(aeon_decoder* d);
+/* provider_interface::get_output_shapes (src/provider_interface.hpp:61-65) */
+int aeon_decoder_output_count(aeon_decoder* d, int* count);
+int aeon_decoder_output_info(aeon_decoder* d, int index, char* name, size_t name_cap, int64_t* shape,
+                             int* ndim, size_t* item_bytes, int* dtype);
+/* One decode window: n records x input_count elements (row-major in elems).  outputs[k] holds
+ * n items of output k (host memory, or device memory when outputs_on_device).  Returns when
+ * the window is complete (batch_decoder::filler, src/batch_decoder.cpp:73-99). */
+int aeon_decoder_decode(aeon_decoder* d, int n, const aeon_record_elem* elems, void* const* outputs,
+                        int outputs_on_device, void* stream);
+const char* aeon_decoder_last_error(void);
+
+/* manifest_file node slicing (src/manifest_file.cpp:278-295): the record indices of node
+ * node_id of node_count (indices may be NULL to query *count). */
+int aeon_manifest_node_slice(int64_t record_count, int batch_size, int node_id, int node_count,
+                             int64_t* indices, int64_t* count);
+
 /* ---- host staging (replaces the dead cuMemAllocHost branch, src/buffer_batch.cpp:150-186) -- */
 int aeon_hip_host_alloc(size_t bytes, void** out);
 int aeon_hip_host_free(void* p);

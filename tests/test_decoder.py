@@ -1,0 +1,65 @@
+"""GPU: the decode stage (provider_factory + batch_decoder through the C ABI) against the oracle,
+with aeon's deterministic mode: slot engines seeded from minstd_rand0(random_seed + node_id)."""
+import numpy as np
+import pytest
+
+import aeon_amd as A
+from aeon_amd import configs as C
+from tests import helpers as H
+
+pytestmark = pytest.mark.gpu
+
+
+def _records(n, seed=0, mask=False):
+    rng = np.random.default_rng(seed)
+    recs = []
+    for i in range(n):
+        w, h = int(rng.integers(200, 700)), int(rng.integers(200, 700))
+        img = A.synthetic_image(i + 1000 * seed, w, h, 3)
+        if mask:
+            m = ((A.synthetic_image(50000 + i, w, h, 1) > 100) * 255).astype(np.uint8)
+            recs.append((img, m))
+        else:
+            recs.append((img,))
+    return recs
+
+
+def _oracle(recs, params, etl, aug, mask_k=None):
+    outs = []
+    for k, e in enumerate(etl):
+        od = C.out_desc_for(e, aug)
+        outs.append(np.stack(H.oracle_records([r[k] for r in recs], params, od, mask=(k == mask_k))))
+    return outs
+
+
+def test_decoder_c3_two_windows():
+    cfg = dict(batch_size=8, random_seed=5, etl=[C.IMAGE_224], augmentation=[C.C3_AUG])
+    d = A.Decoder(cfg)
+    f = A.ParamFactory(C.C3_AUG)  # the checker's params: same slots, same record order
+    states = A.seed_slots(5, 8)
+    for window in range(2):
+        recs = _records(8, seed=window)
+        params = [f.make_params(states[i:i + 1], r[0].shape[1], r[0].shape[0], 224, 224)
+                  for i, r in enumerate(recs)]
+        (out,) = d.decode(recs)
+        (ref,) = _oracle(recs, params, [C.IMAGE_224], C.C3_AUG)
+        assert np.array_equal(out, ref), f"window {window}"
+
+
+def test_decoder_c5_image_and_mask():
+    cfg = dict(batch_size=6, random_seed=3, node_id=1, node_count=2, etl=[C.IMAGE_512, C.MASK_512],
+               augmentation=[C.C5_AUG])
+    d = A.Decoder(cfg)
+    recs = _records(6, seed=2, mask=True)
+    params = H.draw_params(C.C5_AUG, [(r[0].shape[1], r[0].shape[0]) for r in recs], 512, 512, seed=3 + 1)
+    img, msk = d.decode(recs)
+    ref_img, ref_msk = _oracle(recs, params, [C.IMAGE_512, C.MASK_512], C.C5_AUG, mask_k=1)
+    assert np.array_equal(img, ref_img)
+    assert np.array_equal(msk, ref_msk)
+
+
+def test_decoder_empty_record_raises():
+    d = A.Decoder(dict(batch_size=2, etl=[C.IMAGE_224], augmentation=[C.C2_AUG]))
+    with pytest.raises(A.AeonHipError) as e:
+        d.decode([(np.zeros((0, 0, 3), np.uint8),)])
+    assert "size 0" in str(e.value)

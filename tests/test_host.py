@@ -1,0 +1,119 @@
+"""CPU: the host provider surface (provider_factory / image::config / loader keys) and aeon's
+manifest node slicing, including a 2-rank gloo run of the per-GPU slicing."""
+import os
+
+import numpy as np
+import pytest
+
+import aeon_amd as A
+from aeon_amd import configs as C
+
+
+def _dec(**kw):
+    cfg = dict(batch_size=4, random_seed=1, etl=[C.IMAGE_224], augmentation=[C.C2_AUG])
+    cfg.update(kw)
+    return A.Decoder(cfg)
+
+
+def test_output_shapes():
+    d = A.Decoder(dict(batch_size=8, etl=[dict(C.IMAGE_512, name="left"), C.MASK_512],
+                       augmentation=[C.C5_AUG]))
+    assert [o["name"] for o in d.outputs] == ["left.image", "pixelmask"]
+    assert d.outputs[0]["shape"] == (3, 512, 512) and d.outputs[0]["dtype"] == np.float32
+    assert d.outputs[1]["shape"] == (1, 512, 512) and d.outputs[1]["item_bytes"] == 512 * 512
+    hwc = A.Decoder(dict(batch_size=1, etl=[dict(C.IMAGE_224, channel_major=False, output_type="uint8_t")]))
+    assert hwc.outputs[0]["shape"] == (224, 224, 3)
+
+
+@pytest.mark.parametrize("bad", [
+    dict(etl=[dict(C.IMAGE_224, heigth=224)]),                 # unknown image key (verify_config)
+    dict(etl=[dict(C.IMAGE_224, channels=2)]),                 # channels must be 1 or 3
+    dict(etl=[dict(C.IMAGE_224, channels=1)]),                 # bgr_to_rgb needs 3 channels
+    dict(etl=[dict(C.IMAGE_224, output_type="float16")]),      # not an aeon output type
+    dict(etl=[dict(C.IMAGE_224, output_type="uint8_t")]),      # mean/stddev need float output
+    dict(etl=[{"height": 10, "width": 10}]),                   # etl object without type
+    dict(etl=[dict(C.IMAGE_224, type="videoo")]),              # unsupported etl type
+    dict(shuffle_manifst=True),                                # unknown loader key
+    dict(augmentation=[{"scale": [0.5, 1.0]}]),                # augmentation without type
+    dict(augmentation=[dict(C.C2_AUG, mean=[0.5, 0.5])]),      # mean size != channels
+    dict(etl=[dict(C.IMAGE_224, width=0)]),
+])
+def test_invalid_configs(bad):
+    with pytest.raises(A.AeonHipError) as e:
+        _dec(**bad)
+    assert e.value.code in (A.AEON_HIP_EINVAL, A.AEON_HIP_ERUNTIME)
+
+
+def test_missing_batch_size():
+    with pytest.raises(A.AeonHipError):
+        A.Decoder(dict(etl=[C.IMAGE_224]))
+
+
+def test_node_id_out_of_range():
+    with pytest.raises(A.AeonHipError):
+        _dec(node_id=2, node_count=2)
+
+
+def _ref_slice(n, b, node, nodes):
+    """aeon manifest_file::generate_blocks node slicing, restated (manifest_file.cpp:278-295)."""
+    if nodes <= 1:
+        return list(range(n))
+    cnt = n // nodes
+    batches = cnt // b
+    out = [(i // b) * b * nodes + b * node + i % b for i in range(batches * b)]
+    tail = cnt - batches * b
+    out += [batches * b * nodes + tail * node + i for i in range(tail)]
+    return out
+
+
+@pytest.mark.parametrize("n,b,nodes", [(10, 2, 2), (1000, 32, 8), (257, 7, 3), (5, 8, 2), (4096, 256, 8)])
+def test_manifest_node_slice(n, b, nodes):
+    seen = []
+    for node in range(nodes):
+        s = A.manifest_node_slice(n, b, node, nodes)
+        assert list(s) == _ref_slice(n, b, node, nodes)
+        seen += list(s)
+    assert len(seen) == len(set(seen))  # disjoint slices
+    assert all(0 <= i < n for i in seen)
+
+
+def test_manifest_interleave_like_aeon_test():
+    """test/test_manifest_tsv.cpp:113-205: two nodes take alternate batches."""
+    a = A.manifest_node_slice(8, 2, 0, 2)
+    b = A.manifest_node_slice(8, 2, 1, 2)
+    assert list(a) == [0, 1, 4, 5] and list(b) == [2, 3, 6, 7]
+
+
+def _gloo_worker(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    mine = torch.from_numpy(A.manifest_node_slice(4096, 256, rank, world))
+    allv = [torch.zeros_like(mine) for _ in range(world)]
+    dist.all_gather(allv, mine)
+    if rank == 0:
+        q.put(sorted(torch.cat(allv).tolist()))
+    dist.destroy_process_group()
+
+
+def test_gloo_two_ranks_cover_the_manifest():
+    """The bench's N-GPU sharding, rehearsed on CPU: each rank owns one aeon node slice; the
+    slices of all ranks are disjoint and cover every full batch of the manifest."""
+    import socket
+
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_gloo_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert got == list(range(4096))
