@@ -53,7 +53,7 @@ struct alignas(16) AugJob {
     int32_t  tiles;                          // row chunks (workgroups) of this job
     int32_t  stats_slot;                     // contrast partial-sum slot (-1 if none)
     int32_t  src_scratch;                    // host bookkeeping: source lives in the slot scratch
-    int32_t  pad_;
+    int32_t  stats_tiles;                    // chunks of the pass-1 job that wrote this slot's sums
 };
 
 // Per-launch uniform arguments.
@@ -61,7 +61,7 @@ struct LaunchArgs {
     const AugJob*  jobs;
     const float*   lut;        // [3][256] standardized values (nullptr: no mean/stddev)
     const int32_t* hsv_tables; // sdiv[256], hdiv180[256]
-    uint32_t*      partials;   // contrast partial sums [slots][max_tiles][4]
+    uint32_t*      partials;   // contrast partial sums [slots][partial_stride][4]
     int32_t*       error;      // device error word (0 = ok)
     int32_t        rows_per_tile;  // rows per LDS band (TR)
     int32_t        rows_per_chunk; // rows per workgroup (a multiple of TR; = TR: one band)
@@ -75,8 +75,12 @@ struct LaunchArgs {
     int32_t        vec_ok;     // outputs 16-byte aligned and win_w % 4 == 0 for every job
     int32_t        lds_bytes;
     int32_t        has_hue;    // some job of the launch shifts hue (HSV tables in LDS)
+    int32_t        partial_stride; // chunks per contrast slot in `partials`
 };
 
+// KM_FINAL: a record through to the loader output.  KM_STATS: contrast pass 1 -- resize +
+// brightness/saturation + hue into an HWC uint8 intermediate plus exact per-chunk channel sums
+// (the mean cv::mean needs).  KM_RAW: resize only, HWC uint8 (resize_short pre-pass).
 enum KernelMode : int { KM_FINAL = 0, KM_STATS = 1, KM_RAW = 2 };
 
 constexpr int kBlock = 256; // 4 wave64s per workgroup

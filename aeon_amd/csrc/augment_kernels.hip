@@ -24,6 +24,7 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 typedef float    f32x4 __attribute__((ext_vector_type(4)));
 typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
 
 __device__ __forceinline__ int sat_u8(int v) { return min(max(v, 0), 255); }
 __device__ __forceinline__ int sat_s16(int v) { return min(max(v, -32768), 32767); }
@@ -433,8 +434,8 @@ __global__ __launch_bounds__(kBlock) void augment_tiles(LaunchArgs a)
     if (KM == KM_FINAL && (photo & PHOTO_CONTRAST) && tid < 64) {
         // reduce the exact per-chunk channel sums of this image (written by KM_STATS)
         unsigned long long s0 = 0, s1 = 0, s2 = 0;
-        for (int t = tid; t < J.tiles; t += 64) {
-            const uint32_t* p = a.partials + ((size_t)J.stats_slot * a.max_tiles + t) * 4;
+        for (int t = tid; t < J.stats_tiles; t += 64) {
+            const uint32_t* p = a.partials + ((size_t)J.stats_slot * a.partial_stride + t) * 4;
             s0 += p[0], s1 += p[1], s2 += p[2];
         }
         for (int o = 32; o > 0; o >>= 1) {
@@ -459,7 +460,7 @@ __global__ __launch_bounds__(kBlock) void augment_tiles(LaunchArgs a)
     double   sh0 = 0, sh1 = 0, sh2 = 0;
     if (KM == KM_FINAL && (photo & PHOTO_CONTRAST)) sh0 = shift[0], sh1 = shift[1], sh2 = shift[2];
 
-    const int  elem  = (KM == KM_RAW || a.out_dtype == OUT_U8) ? 1 : 4;
+    const int  elem  = (KM != KM_FINAL || a.out_dtype == OUT_U8) ? 1 : 4;
     const int  plane = win_w * J.win_h;
     const auto orsrc = __builtin_amdgcn_make_buffer_rsrc((void*)J.out_ptr, (short)0,
                                                          plane * cn * elem, 0x00020000);
@@ -513,8 +514,9 @@ __global__ __launch_bounds__(kBlock) void augment_tiles(LaunchArgs a)
                     int b = val[k][0], g = val[k][1], r = val[k][2];
                     if (photo & PHOTO_BS) bs_apply(J, b, g, r);
                     if (photo & PHOTO_HUE) hue_apply(sdiv, hdiv, J.hue, b, g, r);
-                    if (KM == KM_STATS) {
+                    if (KM == KM_STATS) { // the intermediate keeps the post-hue pixel
                         if (ox0 + k < win_w) sum0 += b, sum1 += g, sum2 += r;
+                        val[k][0] = b, val[k][1] = g, val[k][2] = r;
                         continue;
                     }
                     if (photo & PHOTO_CONTRAST) {
@@ -532,10 +534,17 @@ __global__ __launch_bounds__(kBlock) void augment_tiles(LaunchArgs a)
                     val[k][0] = b, val[k][1] = g, val[k][2] = r;
                 }
             }
-            if (KM == KM_STATS) continue;
-
             const int nk = min(4, win_w - ox0);
-            if (KM == KM_RAW) { // HWC uint8, source channel order
+            if ((KM == KM_RAW || KM == KM_STATS) && cn == 3 && nk == 4) {
+                // HWC uint8, source channel order: 4 pixels = 12 bytes = one dwordx3 store
+                const uint32_t w0 = val[0][0] | (val[0][1] << 8) | (val[0][2] << 16) | ((uint32_t)val[1][0] << 24);
+                const uint32_t w1 = val[1][1] | (val[1][2] << 8) | (val[2][0] << 16) | ((uint32_t)val[2][1] << 24);
+                const uint32_t w2 = val[2][2] | (val[3][0] << 8) | (val[3][1] << 16) | ((uint32_t)val[3][2] << 24);
+                const u32x3    q  = {w0, w1, w2};
+                __builtin_amdgcn_raw_buffer_store_b96(q, orsrc, (y * win_w + ox0) * 3, 0, 0);
+                continue;
+            }
+            if (KM == KM_RAW || KM == KM_STATS) { // HWC uint8, source channel order
                 const int base = (y * win_w + ox0) * cn;
 #pragma unroll
                 for (int k = 0; k < 4; k++)
@@ -616,7 +625,7 @@ __global__ __launch_bounds__(kBlock) void augment_tiles(LaunchArgs a)
         if (tid < 3) {
             uint32_t s = 0;
             for (int wv = 0; wv < kBlock / 64; wv++) s += (uint32_t)red[wv * 4 + tid];
-            a.partials[((size_t)J.stats_slot * a.max_tiles + chunk) * 4 + tid] = s;
+            a.partials[((size_t)J.stats_slot * a.partial_stride + chunk) * 4 + tid] = s;
         }
     }
 }
@@ -638,7 +647,8 @@ KernelFn pick_rm(int rm, bool photo, int of)
     switch (rm) {
     case RESIZE_LINEAR: return pick_form<KM, RESIZE_LINEAR>(photo, of);
     case RESIZE_AREA2X: return pick_form<KM, RESIZE_AREA2X>(photo, of);
-    default: return pick_form<KM, RESIZE_NEAREST>(photo, of);
+    case RESIZE_NEAREST: return pick_form<KM, RESIZE_NEAREST>(photo, of);
+    default: return pick_form<KM, RESIZE_COPY>(photo, of);
     }
 }
 

@@ -220,7 +220,7 @@ struct LaunchPlan {
 // Geometry + constants of one image-provider record (transform_single_image).
 void plan_image(const aeon_img_desc& d, const void* src_base, const aeon_aug_params& p,
                 const aeon_out_desc& o, uint8_t* out_item, bool is_mask, LaunchPlan& pre,
-                LaunchPlan& main, size_t& scratch_bytes, std::vector<size_t>& scratch_off)
+                LaunchPlan& pass1, LaunchPlan& main, size_t& scratch_bytes)
 {
     const int cn = d.channels;
     if (cn != 1 && cn != 3) fail(AEON_HIP_EINVAL, "channels must be 1 or 3");
@@ -261,7 +261,6 @@ void plan_image(const aeon_img_desc& d, const void* src_base, const aeon_aug_par
         P.xv      = simd_boundary(rw * cn);
         size_t off = (scratch_bytes + 15) & ~(size_t)15;
         scratch_bytes = off + (size_t)p.crop_w * p.crop_h * cn + 16;
-        scratch_off.push_back(off);
         P.out_ptr = off; // relocated to the slot's scratch by the caller
         pre.jobs.push_back(P);
         J.src_ptr = off; // likewise
@@ -307,6 +306,29 @@ void plan_image(const aeon_img_desc& d, const void* src_base, const aeon_aug_par
             plan_lighting(J, p.lighting, p.color_noise_std);
         }
         J.photo = photo;
+        if (photo & PHOTO_CONTRAST) {
+            // contrast needs the mean of the post-hue image: pass 1 writes that image (HWC
+            // uint8, unflipped) and its exact per-chunk sums; pass 2 (this job) reads it back
+            AugJob P1     = J;
+            P1.flip       = 0;
+            P1.photo      = photo & (PHOTO_BS | PHOTO_HUE | PHOTO_CONTRAST);
+            P1.stats_slot = (int)pass1.jobs.size();
+            size_t off    = (scratch_bytes + 15) & ~(size_t)15;
+            scratch_bytes = off + (size_t)J.win_w * J.win_h * 3 + 16;
+            P1.out_ptr    = off; // relocated to the slot's scratch by the caller
+            pass1.jobs.push_back(P1);
+            J.stats_slot  = P1.stats_slot;
+            J.src_ptr     = off;
+            J.src_scratch = 1;
+            J.src_bytes   = (uint64_t)J.win_w * J.win_h * 3;
+            J.src_w = J.win_w, J.src_h = J.win_h, J.src_stride = J.win_w * 3;
+            J.crop_x = J.crop_y = 0, J.crop_w = J.win_w, J.crop_h = J.win_h;
+            J.shift_x = J.shift_y = J.padded = 0;
+            J.mode    = RESIZE_COPY;
+            J.scale_x = J.scale_y = 1.0;
+            J.xv      = simd_boundary(J.win_w * 3);
+            J.photo   = photo & (PHOTO_CONTRAST | PHOTO_LIGHTING);
+        }
     }
     if ((J.out_ptr & 15) != 0 || (J.win_w & 3) != 0) main.vec_ok = false;
     main.jobs.push_back(J);
@@ -371,7 +393,7 @@ void grow(uint8_t*& p, size_t& cap, size_t need, bool pinned)
 }
 
 // Algorithmic bytes of one launch: the resampled u8 source footprint plus
-// the bytes written (KM_STATS writes nothing but re-reads the footprint).
+// the bytes written (KM_STATS / KM_RAW write an HWC uint8 intermediate).
 double launch_bytes(const LaunchPlan& L, int mode, size_t out_elem)
 {
     double b = 0;
@@ -381,8 +403,7 @@ double launch_bytes(const LaunchPlan& L, int mode, size_t out_elem)
             // a window of the resize target reads only its share of the source
             rd *= ((double)J.win_w / J.dst_w) * ((double)J.win_h / J.dst_h);
         }
-        double wr = mode == KM_STATS ? 0.0
-                                     : (double)J.win_w * J.win_h * J.cn * (mode == KM_RAW ? 1 : out_elem);
+        double wr = (double)J.win_w * J.win_h * J.cn * (mode == KM_FINAL ? out_elem : 1);
         b += rd + wr;
     }
     return b;
@@ -432,35 +453,43 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
     std::lock_guard<std::mutex> lock(ctx->mu);
     HIP_OK(hipSetDevice(ctx->device));
 
-    LaunchPlan          pre_all, main_all;
-    size_t              scratch_bytes = 0;
-    std::vector<size_t> scratch_off;
+    LaunchPlan pre_all, pass1_all, main_all;
+    size_t     scratch_bytes = 0;
     for (int i = 0; i < n; i++)
         plan_image(descs[i], src_base, params[i], o, (uint8_t*)out_dev + (size_t)i * o.item_stride,
-                   is_mask, pre_all, main_all, scratch_bytes, scratch_off);
+                   is_mask, pre_all, pass1_all, main_all, scratch_bytes);
 
     // one launch per (resize mode, photometric) group: the kernels are specialised on both
-    std::vector<LaunchPlan> pre(4), main(8);
+    std::vector<LaunchPlan> pre(4), pass1(4), main(8);
     for (int rm = 0; rm < 4; rm++) {
-        pre[rm].rm = rm;
+        pre[rm].rm = pass1[rm].rm = rm;
+        pass1[rm].photo = true;
         for (int ph = 0; ph < 2; ph++) main[rm * 2 + ph].rm = rm, main[rm * 2 + ph].photo = ph != 0;
     }
     for (const AugJob& J : pre_all.jobs) pre[J.mode].jobs.push_back(J);
+    for (const AugJob& J : pass1_all.jobs) pass1[J.mode].jobs.push_back(J);
     for (const AugJob& J : main_all.jobs) main[J.mode * 2 + (J.photo ? 1 : 0)].jobs.push_back(J);
-    const size_t lut_bytes = 4096;
-    size_t       blob = lut_bytes, partial_words = 4;
-    for (auto* v : {&pre, &main})
+    const size_t     lut_bytes = 4096;
+    size_t           blob      = lut_bytes;
+    std::vector<int> slot_tiles(pass1_all.jobs.size(), 0);
+    int              partial_stride = 1;
+    for (auto* v : {&pre, &pass1, &main})
         for (LaunchPlan& P : *v) {
             if (P.jobs.empty()) continue;
             P.vec_ok = main_all.vec_ok;
             P.finalize();
             P.blob_off = blob;
             blob += P.jobs.size() * sizeof(AugJob);
-            for (AugJob& J : P.jobs)
-                if (J.photo & PHOTO_CONTRAST) J.stats_slot = P.stats_slots++;
-            P.partial_off = partial_words;
-            partial_words += (size_t)P.stats_slots * P.max_tiles * 4;
+            if (v == &pass1)
+                for (const AugJob& J : P.jobs) {
+                    slot_tiles[J.stats_slot] = J.tiles;
+                    partial_stride           = std::max(partial_stride, J.tiles);
+                }
+            if (v == &main)
+                for (AugJob& J : P.jobs)
+                    if (J.stats_slot >= 0) J.stats_tiles = slot_tiles[J.stats_slot];
         }
+    const size_t partial_words = std::max<size_t>(4, pass1_all.jobs.size() * partial_stride * 4);
 
     Slot& s = ctx->slots[ctx->next];
     ctx->next = (ctx->next + 1) % 4;
@@ -477,10 +506,10 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
         s.partials = (uint32_t*)p;
     }
     build_lut(o, (float*)s.host);
-    for (auto* v : {&pre, &main})
+    for (auto* v : {&pre, &pass1, &main})
         for (LaunchPlan& P : *v) {
             for (AugJob& J : P.jobs) { // relocate scratch references
-                if (v == &pre) J.out_ptr += (uint64_t)s.scratch;
+                if (v != &main) J.out_ptr += (uint64_t)s.scratch;
                 if (J.src_scratch) J.src_ptr += (uint64_t)s.scratch;
             }
             if (!P.jobs.empty()) std::memcpy(s.host + P.blob_off, P.jobs.data(), P.jobs.size() * sizeof(AugJob));
@@ -492,7 +521,8 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
         a.jobs          = (const AugJob*)(s.dev + L.blob_off);
         a.lut           = (const float*)s.dev; // [3][256]: standardized, or (float)x without mean
         a.hsv_tables    = ctx->d_hsv;
-        a.partials      = s.partials + L.partial_off;
+        a.partials      = s.partials;
+        a.partial_stride = partial_stride;
         a.error         = ctx->d_error;
         a.rows_per_tile = L.tr;
         a.rows_per_chunk = L.chunk_rows;
@@ -511,8 +541,8 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
     const size_t oelem = o.dtype == AEON_DTYPE_F32 ? 4 : 1;
     for (LaunchPlan& P : pre)
         if (!P.jobs.empty()) timed_launch(ctx, KM_RAW, P, args(P), stream, launch_bytes(P, KM_RAW, 1));
-    for (LaunchPlan& P : main)
-        if (P.stats_slots > 0) timed_launch(ctx, KM_STATS, P, args(P), stream, launch_bytes(P, KM_STATS, oelem));
+    for (LaunchPlan& P : pass1)
+        if (!P.jobs.empty()) timed_launch(ctx, KM_STATS, P, args(P), stream, launch_bytes(P, KM_STATS, oelem));
     for (LaunchPlan& P : main)
         if (!P.jobs.empty()) timed_launch(ctx, KM_FINAL, P, args(P), stream, launch_bytes(P, KM_FINAL, oelem));
     HIP_OK(hipEventRecord(s.done, stream));
