@@ -12,7 +12,8 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libaeon_hip.so")
+# AEON_HIP_LIB: a kernel tuning variant built by tools/build_variants.sh (development only)
+LIB_PATH = os.environ.get("AEON_HIP_LIB") or os.path.join(HERE, "libaeon_hip.so")
 HEADER = os.path.join(os.path.dirname(HERE), "include", "aeon_hip.h")
 
 AEON_HIP_OK = 0
@@ -217,8 +218,11 @@ class Context:
 
     def _batch(self, fn, descs, src_ptr, params, out, out_ptr, stream):
         n = len(descs)
-        d = (ImgDesc * n)(*descs)
-        p = (AugParams * n)(*params)
+        # prebuilt ctypes arrays pass straight through (the C++ host fills these in place)
+        d = descs if isinstance(descs, ctypes.Array) else (ImgDesc * n)(*descs)
+        p = params if isinstance(params, ctypes.Array) else (AugParams * n)(*params)
+        if len(p) < n:
+            raise ValueError(f"{len(p)} params for {n} records")
         _check(fn(self._h, n, d, ctypes.c_void_p(src_ptr), p, ctypes.byref(out),
                   ctypes.c_void_p(out_ptr), ctypes.c_void_p(stream or 0)))
 

@@ -18,6 +18,11 @@
 
 #include "aug_job.hpp"
 
+// Minimum waves per SIMD the register allocator must leave room for (__launch_bounds__).
+#ifndef AEON_HIP_MIN_WAVES
+#define AEON_HIP_MIN_WAVES 1
+#endif
+
 namespace aeon_hip {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -285,7 +290,10 @@ __device__ __forceinline__ void stage_commit(const AugJob& J, __amdgpu_buffer_rs
 }
 
 // Output cache policy: streaming stores (written once, read by the consumer of the batch).
-constexpr int kStoreAux = 2; // nt
+#ifndef AEON_HIP_STORE_AUX
+#define AEON_HIP_STORE_AUX 2 // nt
+#endif
+constexpr int kStoreAux = AEON_HIP_STORE_AUX;
 
 __device__ __forceinline__ void store_f32x4(__amdgpu_buffer_rsrc_t r, int off, float a, float b, float c,
                                             float d)
@@ -355,7 +363,7 @@ enum OutForm : int { OF_F32_CHW_VEC = 0, OF_GENERIC = 1 };
 // PHOTO: the launch's jobs carry photometric work.  OF: output form (OF_F32_CHW_VEC = float32
 // CHW planes, win_w % 4 == 0, 16-byte aligned items: the ImageNet configuration).
 template <int KM, int RM, bool PHOTO, int OF>
-__global__ __launch_bounds__(kBlock) void augment_tiles(LaunchArgs a)
+__global__ __launch_bounds__(kBlock, AEON_HIP_MIN_WAVES) void augment_tiles(LaunchArgs a)
 {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     // The job descriptor is copied to registers before any store: the pixel loop then issues

@@ -15,7 +15,7 @@ from aeon_amd import configs as C  # noqa: E402
 def measure(cfg, batch, steps=20, warmup=3):
     """Per step (one batch): summed kernel time of each kind and its algorithmic-byte rate."""
     torch.cuda.set_device(0)
-    _, kt, _ = bench.run_device(A, C, torch, cfg, batch, steps, warmup, 0, 1, 400, None)
+    _, kt, _, _ = bench.run_device(A, C, torch, cfg, batch, steps, warmup, 0, 1, 400, None)
     res = {}
     for k, (ms, by, n) in kt.items():
         if n:
@@ -30,7 +30,9 @@ if __name__ == "__main__":
     if argv and argv[0] in ("C2", "C3"):
         cfgs = tuple(c for c in cfgs if c[0] == argv[0])
         argv = argv[1:]
-    if argv:
+    if argv == ["default"]:
+        variants = [dict()]
+    elif argv:
         variants = [dict(kv.split("=", 1) for kv in argv)]
     for cfg, batch in cfgs:
         for v in variants:
