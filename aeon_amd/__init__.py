@@ -101,6 +101,7 @@ def lib():
         for fn in (L.aeon_hip_augment_batch, L.aeon_hip_mask_batch):
             fn.argtypes = [vp, ctypes.c_int, P(ImgDesc), vp, P(AugParams), P(OutDesc), vp, vp]
         L.aeon_hip_synchronize.argtypes = [vp, vp]
+        L.aeon_hip_transpose_batch.argtypes = [vp, vp, vp, ctypes.c_int64, ctypes.c_int64, ctypes.c_int, vp]
         L.aeon_hip_set_timing.argtypes = [vp, ctypes.c_int]
         L.aeon_hip_kernel_times.argtypes = [vp, P(ctypes.c_double), P(ctypes.c_double), P(ctypes.c_long)]
         L.aeon_param_factory_create.argtypes = [ctypes.c_char_p, P(vp)]
@@ -245,6 +246,11 @@ class Context:
 
     def synchronize(self, stream=0):
         _check(lib().aeon_hip_synchronize(self._h, ctypes.c_void_p(stream or 0)))
+
+    def transpose_batch(self, src_ptr, dst_ptr, rows, cols, element_size, stream=0):
+        """batch_major=false layout: dst[c*rows + r] = src[r*cols + c] (async on stream)."""
+        _check(lib().aeon_hip_transpose_batch(self._h, ctypes.c_void_p(src_ptr), ctypes.c_void_p(dst_ptr),
+                                              rows, cols, element_size, ctypes.c_void_p(stream or 0)))
 
 
 def pack_images(images, align=16):

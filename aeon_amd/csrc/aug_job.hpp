@@ -59,7 +59,8 @@ struct alignas(16) AugJob {
 // Per-launch uniform arguments.
 struct LaunchArgs {
     const AugJob*  jobs;
-    const float*   lut;        // [3][256] standardized values (nullptr: no mean/stddev)
+    const float*   lut;        // [3][256] per SOURCE channel: standardized value of output
+                               // channel (bgr_to_rgb ? 2-c : c), or (float)x without mean
     const int32_t* hsv_tables; // sdiv[256], hdiv180[256]
     uint32_t*      partials;   // contrast partial sums [slots][partial_stride][4]
     int32_t*       error;      // device error word (0 = ok)
@@ -76,6 +77,7 @@ struct LaunchArgs {
     int32_t        lds_bytes;
     int32_t        has_hue;    // some job of the launch shifts hue (HSV tables in LDS)
     int32_t        partial_stride; // chunks per contrast slot in `partials`
+    int32_t        threads;    // workgroup size (kBlockMin..kBlockMax, a multiple of 64)
 };
 
 // KM_FINAL: a record through to the loader output.  KM_STATS: contrast pass 1 -- resize +
@@ -83,7 +85,10 @@ struct LaunchArgs {
 // (the mean cv::mean needs).  KM_RAW: resize only, HWC uint8 (resize_short pre-pass).
 enum KernelMode : int { KM_FINAL = 0, KM_STATS = 1, KM_RAW = 2 };
 
-constexpr int kBlock = 256; // 4 wave64s per workgroup
+// Workgroups are 256..512 lanes: a multiple of the window's 4-pixel column groups, so every
+// lane keeps the same output columns (and their resize taps) for a whole chunk.
+constexpr int kBlockMin = 256;
+constexpr int kBlockMax = 512;
 
 #if defined(__HIPCC__)
 #define AEON_HD __host__ __device__
@@ -96,17 +101,18 @@ struct LdsLayout {
     int hsv, lut, xt, yt, red, stage, stage_bytes, total;
 };
 // One staging buffer (the next band waits in registers while the current one is consumed);
-// two small row-tap tables.  The HSV tables are reserved only for hue launches.
+// two small row-tap tables.  The HSV tables are reserved only for hue launches.  The LUT sits
+// at offset 0 so its per-channel reads use immediate LDS offsets.
 AEON_HD inline LdsLayout lds_layout(int max_win_w, int rows_per_tile, int stage_rows, int stage_pitch,
                                     bool hue = true)
 {
     LdsLayout L;
     int       o = 0;
+    L.lut = o;   o += 3 * 256 * 4;                       // standardize LUT (source channel order)
     L.hsv = o;   o += hue ? 2 * 256 * 4 : 0;             // sdiv / hdiv180 tables
-    L.lut = o;   o += 3 * 256 * 4;                       // standardize LUT
     L.xt  = o;   o += ((max_win_w * 8 + 15) / 16) * 16;  // per-column taps + weights
     L.yt  = o;   o += 2 * rows_per_tile * 16;            // per-row taps + weights, x2
-    L.red = o;   o += 128;                               // reductions / contrast shifts
+    L.red = o;   o += 160;                               // 8 waves x 4 sums, then 3 f64 shifts
     L.stage_bytes = stage_rows * stage_pitch * 4;        // source pixels, 4 B each (B,G,R,0)
     L.stage = o; o += L.stage_bytes;
     L.total = o;

@@ -38,6 +38,15 @@ __device__ __forceinline__ int byte_of(uint32_t p, int c) { return (p >> (8 * c)
 // 16x16-bit signed product (v_mul_i32_i24 with word selects): both operands must fit int16
 __device__ __forceinline__ int mul16(int a, int b) { return (int)(short)a * (int)(short)b; }
 
+// LDS accesses by byte address.  The kernel has no static LDS, so the dynamic area starts at
+// LDS address 0 (checked at kernel entry); addressing through local-address-space pointers made
+// from byte offsets lets the compiler fold constant parts into the ds_read offset field instead
+// of adding the dynamic area's base at run time.
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+typedef __attribute__((address_space(3))) float    lds_f32;
+__device__ __forceinline__ uint32_t lds_ld(int byte_addr) { return *(const lds_u32*)(size_t)(uint32_t)byte_addr; }
+__device__ __forceinline__ float    lds_ldf(int byte_addr) { return *(const lds_f32*)(size_t)(uint32_t)byte_addr; }
+
 // ---- resize coefficients (OpenCV 2.4 resizeGeneric_ / resizeNN) -----------------------------
 // Taps are (sx, sx+1) and (r0, r1); a weight of 0 marks a single-tap column / row.
 struct XTap {
@@ -236,17 +245,17 @@ __device__ __forceinline__ u32x4 stage_slow(const AugJob& J, __amdgpu_buffer_rsr
     return (u32x4){px[0], px[1], px[2], px[3]};
 }
 
-// Issue the first kPrefetch items of this lane for a band (fast items only).
+// Issue the first kPrefetch items of this lane for a band (fast items only).  nt = lanes.
 __device__ __forceinline__ void stage_issue(const AugJob& J, __amdgpu_buffer_rsrc_t rsrc, const StageGeom& G,
-                                            Prefetch& pf)
+                                            Prefetch& pf, int nt)
 {
     const int total = G.nr * G.groups;
-    const int dj = kBlock / G.groups, dg = kBlock - dj * G.groups;
+    const int dj = nt / G.groups, dg = nt - dj * G.groups;
     int       j = threadIdx.x / G.groups, g = threadIdx.x - j * G.groups;
 #pragma unroll
     for (int k = 0; k < kPrefetch; k++, j += dj, g += dg) {
         if (g >= G.groups) g -= G.groups, j++;
-        const int i = threadIdx.x + k * kBlock;
+        const int i = threadIdx.x + k * nt;
         pf.meta[k]  = 0;
         if (i >= total) continue;
         const int  cy = G.v_lo + j + J.shift_y, cx = G.u_lo + 4 * g + J.shift_x;
@@ -259,7 +268,7 @@ __device__ __forceinline__ void stage_issue(const AugJob& J, __amdgpu_buffer_rsr
 
 // Write this lane's items of a band to LDS (prefetched ones from registers, the rest loaded now).
 __device__ __forceinline__ void stage_commit(const AugJob& J, __amdgpu_buffer_rsrc_t rsrc, const StageGeom& G,
-                                             const Prefetch& pf, uint32_t* stage, int pitch)
+                                             const Prefetch& pf, uint32_t* stage, int pitch, int nt)
 {
 #pragma unroll
     for (int k = 0; k < kPrefetch; k++) {
@@ -272,10 +281,10 @@ __device__ __forceinline__ void stage_commit(const AugJob& J, __amdgpu_buffer_rs
         *(u32x4*)(stage + j * pitch + 4 * g) = q;
     }
     const int total = G.nr * G.groups;
-    const int i0    = threadIdx.x + kPrefetch * kBlock;
-    const int dj = kBlock / G.groups, dg = kBlock - dj * G.groups;
+    const int i0    = threadIdx.x + kPrefetch * nt;
+    const int dj = nt / G.groups, dg = nt - dj * G.groups;
     int       j = i0 / G.groups, g = i0 - j * G.groups;
-    for (int i = i0; i < total; i += kBlock, j += dj, g += dg) {
+    for (int i = i0; i < total; i += nt, j += dj, g += dg) {
         if (g >= G.groups) g -= G.groups, j++;
         const int cy = G.v_lo + j + J.shift_y, cx = G.u_lo + 4 * g + J.shift_x;
         u32x4     q;
@@ -303,14 +312,18 @@ __device__ __forceinline__ void store_f32x4(__amdgpu_buffer_rsrc_t r, int off, f
 }
 
 // One output pixel of the resize: 3 channels from the staged source (LDS).
-template <int RM>
-__device__ __forceinline__ void resize_px(const uint32_t* stage, int4 ytr, int2 xtt, int v[3])
+// ytr = (row-0, row-1 LDS byte addresses in the staged band, b0, b1); col = byte offset of the
+// first tap's column; wx = a0 | a1 << 16.  SCALED results are 4x the pixel value plus 0..3: the
+// standardize LUT is addressed by (s & ~3) with no further shifts, and s >> 2 is the pixel.
+// (Photometric kernels take plain values.)
+template <int RM, bool SCALED>
+__device__ __forceinline__ void resize_px(int4 ytr, int col, uint32_t wx, int s[3])
 {
-    const uint32_t* r0p = stage + ytr.x + xtt.x;
+    const int a0 = ytr.x + col;
     if (RM == RESIZE_LINEAR) {
-        const uint32_t* r1p = stage + ytr.y + xtt.x;
-        const uint32_t  p00 = r0p[0], p01 = r0p[1], p10 = r1p[0], p11 = r1p[1];
-        const u16x2     w   = __builtin_bit_cast(u16x2, (uint32_t)xtt.y); // (a0, a1)
+        const int      a1  = ytr.y + col;
+        const uint32_t p00 = lds_ld(a0), p01 = lds_ld(a0 + 4), p10 = lds_ld(a1), p11 = lds_ld(a1 + 4);
+        const u16x2     w   = __builtin_bit_cast(u16x2, wx); // (a0, a1)
 #pragma unroll
         for (int c = 0; c < 3; c++) {
             // HResizeLinear: H = S[sx]*a0 + S[sx+1]*a1 (exact), one v_dot2_u32_u16 per row on
@@ -324,34 +337,45 @@ __device__ __forceinline__ void resize_px(const uint32_t* stage, int4 ytr, int2 
             // The +2 rides in the high half of t0; the sum is <= 1023, so no saturation.
             const uint32_t t0 = (uint32_t)__mul24((int)(H0 >> 4), ytr.z) + (2u << 16);
             const uint32_t t1 = (uint32_t)__mul24((int)(H1 >> 4), ytr.w);
-            v[c]              = (int)(((t0 >> 16) + (t1 >> 16)) >> 2);
+            s[c]              = (int)((t0 >> 16) + (t1 >> 16));
+            if (!SCALED) s[c] >>= 2;
         }
     } else if (RM == RESIZE_AREA2X) {
-        const uint32_t* r1p = stage + ytr.y + xtt.x;
-        const uint32_t  p00 = r0p[0], p01 = r0p[1], p10 = r1p[0], p11 = r1p[1];
-#pragma unroll
-        for (int c = 0; c < 3; c++)
-            v[c] = (byte_of(p00, c) + byte_of(p01, c) + byte_of(p10, c) + byte_of(p11, c) + 2) >> 2;
+        const int      a1  = ytr.y + col;
+        const uint32_t p00 = lds_ld(a0), p01 = lds_ld(a0 + 4), p10 = lds_ld(a1), p11 = lds_ld(a1 + 4);
+        // INTER_AREA 2x fast path: (a + b + c + d + 2) >> 2 per channel; channels 0/2 and 1
+        // summed in 16-bit lanes (each sum <= 1022)
+        const uint32_t m  = 0x00ff00ffu;
+        const uint32_t lo = (p00 & m) + (p01 & m) + (p10 & m) + (p11 & m);
+        const uint32_t hi = ((p00 >> 8) & m) + ((p01 >> 8) & m) + ((p10 >> 8) & m) + ((p11 >> 8) & m);
+        s[0] = (int)(lo & 0xffff) + 2;
+        s[1] = (int)(hi & 0xffff) + 2;
+        s[2] = (int)(lo >> 16) + 2;
+        if (!SCALED) s[0] >>= 2, s[1] >>= 2, s[2] >>= 2;
     } else {
-        const uint32_t p00 = r0p[0];
+        const uint32_t p00 = lds_ld(a0);
 #pragma unroll
-        for (int c = 0; c < 3; c++) v[c] = byte_of(p00, c);
+        for (int c = 0; c < 3; c++) s[c] = byte_of(p00, c) << (SCALED ? 2 : 0);
     }
 }
 
 // Elements of OpenCV's scalar row tail (e >= xv) use FixedPtCast<int, uchar, 22> instead.
-__device__ __forceinline__ void tail_fix(const uint32_t* stage, int4 ytr, int2 xtt, int e0, int xv, int v[3])
+template <bool SCALED>
+__device__ __forceinline__ void tail_fix(int4 ytr, int col, uint32_t wx, int e0, int xv, int s[3])
 {
-    const uint32_t* r0p = stage + ytr.x + xtt.x;
-    const uint32_t* r1p = stage + ytr.y + xtt.x;
-    const int       a0 = xtt.y & 0xffff, a1 = xtt.y >> 16;
+    const uint32_t p00 = lds_ld(ytr.x + col), p01 = lds_ld(ytr.x + col + 4);
+    const uint32_t p10 = lds_ld(ytr.y + col), p11 = lds_ld(ytr.y + col + 4);
+    const int      a0 = wx & 0xffff, a1 = (int)(wx >> 16);
     for (int c = 0; c < 3; c++) {
         if (e0 + c < xv) continue;
-        const int H0 = byte_of(r0p[0], c) * a0 + byte_of(r0p[1], c) * a1;
-        const int H1 = byte_of(r1p[0], c) * a0 + byte_of(r1p[1], c) * a1;
-        v[c]         = sat_u8((H0 * ytr.z + H1 * ytr.w + (1 << 21)) >> 22);
+        const int H0 = byte_of(p00, c) * a0 + byte_of(p01, c) * a1;
+        const int H1 = byte_of(p10, c) * a0 + byte_of(p11, c) * a1;
+        s[c]         = sat_u8((H0 * ytr.z + H1 * ytr.w + (1 << 21)) >> 22) << (SCALED ? 2 : 0);
     }
 }
+
+// standardize LUT (LDS offset 0) entry for source channel c at scaled value s
+__device__ __forceinline__ float lut_at(int c, int s) { return lds_ldf(c * 1024 + (s & ~3)); }
 
 enum OutForm : int { OF_F32_CHW_VEC = 0, OF_GENERIC = 1 };
 
@@ -363,9 +387,13 @@ enum OutForm : int { OF_F32_CHW_VEC = 0, OF_GENERIC = 1 };
 // PHOTO: the launch's jobs carry photometric work.  OF: output form (OF_F32_CHW_VEC = float32
 // CHW planes, win_w % 4 == 0, 16-byte aligned items: the ImageNet configuration).
 template <int KM, int RM, bool PHOTO, int OF>
-__global__ __launch_bounds__(kBlock, AEON_HIP_MIN_WAVES) void augment_tiles(LaunchArgs a)
+__global__ __launch_bounds__(kBlockMax, AEON_HIP_MIN_WAVES) void augment_tiles(LaunchArgs a)
 {
     extern __shared__ __attribute__((aligned(16))) char smem[];
+    if ((uint32_t)(size_t)(__attribute__((address_space(3))) char*)smem != 0u) { // see lds_ld
+        if (threadIdx.x == 0) atomicOr(a.error, 4);
+        return;
+    }
     // The job descriptor is copied to registers before any store: the pixel loop then issues
     // no global loads except the next band's staging, so stores rarely make a load wait.
     const AugJob J     = a.jobs[blockIdx.y];
@@ -377,17 +405,18 @@ __global__ __launch_bounds__(kBlock, AEON_HIP_MIN_WAVES) void augment_tiles(Laun
     const int c0    = chunk * a.rows_per_chunk;
     const int c1    = min(c0 + a.rows_per_chunk, J.win_h);
     const int tid   = threadIdx.x;
+    const int nt    = blockDim.x;
     const int cn    = J.cn;
     const int win_w = J.win_w;
 
     const LdsLayout L     = lds_layout(a.max_win_w, TR, a.stage_rows, a.stage_pitch, PHOTO && a.has_hue);
+    float*          lut   = (float*)(smem + L.lut); // offset 0: immediate-offset reads per channel
     int32_t*        sdiv  = (int32_t*)(smem + L.hsv);
     int32_t*        hdiv  = sdiv + 256;
-    float*          lut   = (float*)(smem + L.lut);
     int2*           xt    = (int2*)(smem + L.xt);
     int4*           yt0   = (int4*)(smem + L.yt);
     int32_t*        red   = (int32_t*)(smem + L.red);
-    double*         shift = (double*)(smem + L.red + 64);
+    double*         shift = (double*)(smem + L.red + 128);
     uint32_t*       stage = (uint32_t*)(smem + L.stage);
     const int       pitch = a.stage_pitch;
 
@@ -410,9 +439,10 @@ __global__ __launch_bounds__(kBlock, AEON_HIP_MIN_WAVES) void augment_tiles(Laun
         return n;
     };
     auto build_yt = [&](int y0, int n, const StageGeom& g, int4* yt) {
-        for (int r = tid; r < n; r += kBlock) {
+        for (int r = tid; r < n; r += nt) {
             const YTap t = ycoef<RM>(J.win_y + y0 + r, J.scale_y, J.crop_h);
-            yt[r]        = make_int4((t.r0 - g.v_lo) * pitch, (t.r1 - g.v_lo) * pitch, t.b0, t.b1);
+            yt[r]        = make_int4(L.stage + (t.r0 - g.v_lo) * pitch * 4, L.stage + (t.r1 - g.v_lo) * pitch * 4,
+                                     t.b0, t.b1);
         }
     };
 
@@ -425,20 +455,18 @@ __global__ __launch_bounds__(kBlock, AEON_HIP_MIN_WAVES) void augment_tiles(Laun
         if (tid == 0) atomicOr(a.error, 2);
         return;
     }
-    stage_issue(J, srsrc, G, pf);
+    stage_issue(J, srsrc, G, pf, nt);
 
-    for (int x = tid; x < win_w; x += kBlock) {
+    for (int x = tid; x < win_w; x += nt) {
         const XTap t = xcoef<RM>(J.win_x + x, J.scale_x, J.crop_w);
         xt[x]        = make_int2(t.sx - G.u_lo, (t.a0 & 0xffff) | (t.a1 << 16));
     }
     const int photo = (PHOTO && KM != KM_RAW && cn == 3) ? J.photo : 0;
-    if (photo & PHOTO_HUE) {
-        sdiv[tid] = a.hsv_tables[tid];
-        hdiv[tid] = a.hsv_tables[256 + tid];
-    }
+    if (photo & PHOTO_HUE)
+        for (int i = tid; i < 512; i += nt) sdiv[i] = a.hsv_tables[i];
     const bool use_lut = KM == KM_FINAL && a.out_dtype == OUT_F32 && a.lut != nullptr;
     if (use_lut)
-        for (int i = tid; i < 3 * 256; i += kBlock) lut[i] = a.lut[i];
+        for (int i = tid; i < 3 * 256; i += nt) lut[i] = a.lut[i];
     if (KM == KM_FINAL && (photo & PHOTO_CONTRAST) && tid < 64) {
         // reduce the exact per-chunk channel sums of this image (written by KM_STATS)
         unsigned long long s0 = 0, s1 = 0, s2 = 0;
@@ -461,7 +489,7 @@ __global__ __launch_bounds__(kBlock, AEON_HIP_MIN_WAVES) void augment_tiles(Laun
         }
     }
     build_yt(c0, n0, G, yt0);
-    stage_commit(J, srsrc, G, pf, stage, pitch);
+    stage_commit(J, srsrc, G, pf, stage, pitch, nt);
     __syncthreads();
 
     uint32_t sum0 = 0, sum1 = 0, sum2 = 0;
@@ -476,146 +504,153 @@ __global__ __launch_bounds__(kBlock, AEON_HIP_MIN_WAVES) void augment_tiles(Laun
     const int  wx0   = J.win_x;
     const int  xv    = J.xv;
     const int  flip  = J.flip;
-    const int  gpr   = (win_w + 3) >> 2;
+    const int  bgr   = a.bgr_to_rgb && cn == 3;
+    // Lane -> (column group, row phase), fixed for the chunk: a lane's four output columns and
+    // their taps stay in registers while it walks the band's rows.
+    const int  gpr    = (win_w + 3) >> 2;
+    const int  ncg    = min(gpr, nt);
+    const int  nph    = nt / ncg;
+    const int  lph    = tid / ncg;
+    const int  lcg    = tid - lph * ncg;
+    const bool active = lph < nph;
+    // values carried from the resize to the store: 4x scaled (see resize_px) unless photometric
+    constexpr bool SC = !PHOTO;
+    auto lut_of       = [&](int c, int v) { return lut_at(c, SC ? v : v << 2); };
+    auto u8_of        = [&](int v) { return SC ? v >> 2 : v; };
 
     int buf = 0;
     for (int y0 = c0; y0 < c1; y0 += TR) {
         const int   nrows = min(TR, c1 - y0);
         const int4* yt    = yt0 + buf * TR;
-        // issue the next band's loads; they land while this band is computed
-        StageGeom  Gn      = G;
-        int        nn      = 0;
         const bool has_next = y0 + TR < c1;
-        if (has_next) {
-            nn = band_rows(y0 + TR, Gn);
-            if (Gn.nr > a.stage_rows) {
-                if (tid == 0) atomicOr(a.error, 2);
-                return; // uniform: every lane sees the same band geometry
-            }
-            stage_issue(J, srsrc, Gn, pf);
-        }
 
-        const int dry = kBlock / gpr, dcg = kBlock - dry * gpr;
-        int       ry = tid / gpr, cg = tid - ry * gpr;
-        for (; ry < nrows; ry += dry, cg += dcg) {
-            if (cg >= gpr) cg -= gpr, ry++;
-            if (ry >= nrows) break;
-            const int4 ytr = yt[ry];
-            const int  y   = y0 + ry; // window row
-            const int  ox0 = cg * 4;
-            int        val[4][3];
+        for (int cg = active ? lcg : gpr; cg < gpr; cg += ncg) {
+            const int ox0 = cg * 4;
+            const int nk  = min(4, win_w - ox0);
+            int       col[4];
+            uint32_t  wxk[4];
+            int       tmask = 0;
 #pragma unroll
             for (int k = 0; k < 4; k++) {
                 // columns past the window edge recompute the last one (never stored)
                 const int  ox  = min(ox0 + k, win_w - 1);
                 const int  x   = flip ? win_w - 1 - ox : ox;
                 const int2 xtt = xt[x];
-                resize_px<RM>(stage, ytr, xtt, val[k]);
-                if (RM == RESIZE_LINEAR && tail) {
-                    const int e0 = (wx0 + x) * cn;
-                    if (e0 + 2 >= xv) tail_fix(stage, ytr, xtt, e0, xv, val[k]);
-                }
+                col[k]         = xtt.x * 4; // byte offset in a staged row
+                wxk[k]         = (uint32_t)xtt.y;
+                if (RM == RESIZE_LINEAR && tail && (wx0 + x) * cn + 2 >= xv) tmask |= 1 << k;
             }
-            if (PHOTO && photo) {
+            for (int ry = lph; ry < nrows; ry += nph) {
+                const int4 ytr = yt[ry];
+                const int  y   = y0 + ry; // window row
+                int        val[4][3];
 #pragma unroll
-                for (int k = 0; k < 4; k++) {
-                    int b = val[k][0], g = val[k][1], r = val[k][2];
-                    if (photo & PHOTO_BS) bs_apply(J, b, g, r);
-                    if (photo & PHOTO_HUE) hue_apply(sdiv, hdiv, J.hue, b, g, r);
-                    if (KM == KM_STATS) { // the intermediate keeps the post-hue pixel
-                        if (ox0 + k < win_w) sum0 += b, sum1 += g, sum2 += r;
+                for (int k = 0; k < 4; k++) resize_px<RM, SC>(ytr, col[k], wxk[k], val[k]);
+                if (RM == RESIZE_LINEAR && tmask) {
+#pragma unroll
+                    for (int k = 0; k < 4; k++)
+                        if (tmask & (1 << k)) {
+                            const int ox = min(ox0 + k, win_w - 1);
+                            const int x  = flip ? win_w - 1 - ox : ox;
+                            tail_fix<SC>(ytr, col[k], wxk[k], (wx0 + x) * cn, xv, val[k]);
+                        }
+                }
+                if (PHOTO && photo) {
+#pragma unroll
+                    for (int k = 0; k < 4; k++) {
+                        int b = val[k][0], g = val[k][1], r = val[k][2];
+                        if (photo & PHOTO_BS) bs_apply(J, b, g, r);
+                        if (photo & PHOTO_HUE) hue_apply(sdiv, hdiv, J.hue, b, g, r);
+                        if (KM == KM_STATS) { // the intermediate keeps the post-hue pixel
+                            if (k < nk) sum0 += b, sum1 += g, sum2 += r;
+                            val[k][0] = b, val[k][1] = g, val[k][2] = r;
+                            continue;
+                        }
+                        if (photo & PHOTO_CONTRAST) {
+                            const float c = J.contrast;
+                            b = sat_u8(rnd((float)((double)((float)b * c + 0.f) + sh0)));
+                            g = sat_u8(rnd((float)((double)((float)g * c + 0.f) + sh1)));
+                            r = sat_u8(rnd((float)((double)((float)r * c + 0.f) + sh2)));
+                        }
+                        if (photo & PHOTO_LIGHTING) {
+                            const float la = J.light_a;
+                            b = sat_u8(sat_u8(rnd((float)b * la + 0.f)) + J.light_add[0]);
+                            g = sat_u8(sat_u8(rnd((float)g * la + 0.f)) + J.light_add[1]);
+                            r = sat_u8(sat_u8(rnd((float)r * la + 0.f)) + J.light_add[2]);
+                        }
                         val[k][0] = b, val[k][1] = g, val[k][2] = r;
-                        continue;
                     }
-                    if (photo & PHOTO_CONTRAST) {
-                        const float c = J.contrast;
-                        b = sat_u8(rnd((float)((double)((float)b * c + 0.f) + sh0)));
-                        g = sat_u8(rnd((float)((double)((float)g * c + 0.f) + sh1)));
-                        r = sat_u8(rnd((float)((double)((float)r * c + 0.f) + sh2)));
-                    }
-                    if (photo & PHOTO_LIGHTING) {
-                        const float la = J.light_a;
-                        b = sat_u8(sat_u8(rnd((float)b * la + 0.f)) + J.light_add[0]);
-                        g = sat_u8(sat_u8(rnd((float)g * la + 0.f)) + J.light_add[1]);
-                        r = sat_u8(sat_u8(rnd((float)r * la + 0.f)) + J.light_add[2]);
-                    }
-                    val[k][0] = b, val[k][1] = g, val[k][2] = r;
                 }
-            }
-            const int nk = min(4, win_w - ox0);
-            if ((KM == KM_RAW || KM == KM_STATS) && cn == 3 && nk == 4) {
-                // HWC uint8, source channel order: 4 pixels = 12 bytes = one dwordx3 store
-                const uint32_t w0 = val[0][0] | (val[0][1] << 8) | (val[0][2] << 16) | ((uint32_t)val[1][0] << 24);
-                const uint32_t w1 = val[1][1] | (val[1][2] << 8) | (val[2][0] << 16) | ((uint32_t)val[2][1] << 24);
-                const uint32_t w2 = val[2][2] | (val[3][0] << 8) | (val[3][1] << 16) | ((uint32_t)val[3][2] << 24);
-                const u32x3    q  = {w0, w1, w2};
-                __builtin_amdgcn_raw_buffer_store_b96(q, orsrc, (y * win_w + ox0) * 3, 0, 0);
-                continue;
-            }
-            if (KM == KM_RAW || KM == KM_STATS) { // HWC uint8, source channel order
-                const int base = (y * win_w + ox0) * cn;
+                if ((KM == KM_RAW || KM == KM_STATS) && cn == 3 && nk == 4) {
+                    // HWC uint8, source channel order: 4 pixels = 12 bytes = one dwordx3 store
+                    int v[4][3];
 #pragma unroll
-                for (int k = 0; k < 4; k++)
+                    for (int k = 0; k < 4; k++)
 #pragma unroll
-                    for (int c = 0; c < 3; c++)
-                        if (k < nk && c < cn)
-                            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)val[k][c], orsrc, base + k * cn + c, 0, 0);
-                continue;
-            }
-            // image::loader::load -- from_to {0,2,1,1,2,0} when bgr_to_rgb (a 3-channel config)
-            if (a.bgr_to_rgb) {
-#pragma unroll
-                for (int k = 0; k < 4; k++) {
-                    const int t = val[k][0];
-                    val[k][0]   = val[k][2];
-                    val[k][2]   = t;
+                        for (int c = 0; c < 3; c++) v[k][c] = u8_of(val[k][c]);
+                    const uint32_t w0 = v[0][0] | (v[0][1] << 8) | (v[0][2] << 16) | ((uint32_t)v[1][0] << 24);
+                    const uint32_t w1 = v[1][1] | (v[1][2] << 8) | (v[2][0] << 16) | ((uint32_t)v[2][1] << 24);
+                    const uint32_t w2 = v[2][2] | (v[3][0] << 8) | (v[3][1] << 16) | ((uint32_t)v[3][2] << 24);
+                    const u32x3    q  = {w0, w1, w2};
+                    __builtin_amdgcn_raw_buffer_store_b96(q, orsrc, (y * win_w + ox0) * 3, 0, 0);
+                    continue;
                 }
-            }
-            if (OF == OF_F32_CHW_VEC) {
-                const int idx = y * win_w + ox0;
+                if (KM == KM_RAW || KM == KM_STATS) { // HWC uint8, source channel order
+                    const int base = (y * win_w + ox0) * cn;
 #pragma unroll
-                for (int oc = 0; oc < 3; oc++)
-                    store_f32x4(orsrc, (oc * plane + idx) * 4, lut[oc * 256 + val[0][oc]],
-                                lut[oc * 256 + val[1][oc]], lut[oc * 256 + val[2][oc]],
-                                lut[oc * 256 + val[3][oc]]);
-                continue;
-            }
-            if (a.channel_major) {
+                    for (int k = 0; k < 4; k++)
 #pragma unroll
-                for (int oc = 0; oc < 3; oc++) {
-                    if (oc >= cn) break;
-                    const int idx = oc * plane + y * win_w + ox0;
+                        for (int c = 0; c < 3; c++)
+                            if (k < nk && c < cn)
+                                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)u8_of(val[k][c]), orsrc, base + k * cn + c,
+                                                                     0, 0);
+                    continue;
+                }
+                // image::loader::load: source channel c goes to output channel oc (mixChannels
+                // from_to {0,2,1,1,2,0} when bgr_to_rgb); the LUT is indexed by source channel
+                if (OF == OF_F32_CHW_VEC) {
+                    const int idx = y * win_w + ox0;
+#pragma unroll
+                    for (int c = 0; c < 3; c++) {
+                        const int oc = bgr ? 2 - c : c;
+                        store_f32x4(orsrc, (oc * plane + idx) * 4, lut_of(c, val[0][c]), lut_of(c, val[1][c]),
+                                    lut_of(c, val[2][c]), lut_of(c, val[3][c]));
+                    }
+                    continue;
+                }
+#pragma unroll
+                for (int c = 0; c < 3; c++) {
+                    if (c >= cn) break;
+                    const int oc = bgr ? 2 - c : c;
 #pragma unroll
                     for (int k = 0; k < 4; k++) {
                         if (k >= nk) break;
+                        const int i = a.channel_major ? oc * plane + y * win_w + ox0 + k
+                                                      : (y * win_w + ox0 + k) * cn + oc;
                         if (a.out_dtype == OUT_F32)
-                            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(lut[oc * 256 + val[k][oc]]),
-                                                                  orsrc, (idx + k) * 4, 0, kStoreAux);
+                            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(lut_of(c, val[k][c])), orsrc,
+                                                                  i * 4, 0, kStoreAux);
                         else
-                            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)val[k][oc], orsrc, idx + k, 0,
-                                                                 kStoreAux);
+                            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)u8_of(val[k][c]), orsrc, i, 0, kStoreAux);
                     }
                 }
-            } else {
-                const int base = (y * win_w + ox0) * cn;
-#pragma unroll
-                for (int k = 0; k < 4; k++)
-#pragma unroll
-                    for (int oc = 0; oc < 3; oc++) {
-                        if (k >= nk || oc >= cn) continue;
-                        const int i = base + k * cn + oc;
-                        if (a.out_dtype == OUT_F32)
-                            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(lut[oc * 256 + val[k][oc]]),
-                                                                  orsrc, i * 4, 0, kStoreAux);
-                        else
-                            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)val[k][oc], orsrc, i, 0, kStoreAux);
-                    }
             }
         }
-        if (has_next) { // single staging buffer: everyone is done reading it before it is refilled
+        if (has_next) {
+            // Next band: loaded only now.  Prefetching it during this band's compute would not
+            // hide its latency -- waiting for those loads also waits for this band's stores (one
+            // vector-memory counter) -- and would hold ~15 VGPRs across the pixel loop.
+            StageGeom Gn = G;
+            const int nn = band_rows(y0 + TR, Gn);
+            if (Gn.nr > a.stage_rows) {
+                if (tid == 0) atomicOr(a.error, 2);
+                return; // uniform: every lane sees the same band geometry
+            }
+            Prefetch pn;
+            stage_issue(J, srsrc, Gn, pn, nt);
             build_yt(y0 + TR, nn, Gn, yt0 + (buf ^ 1) * TR);
-            __syncthreads();
-            stage_commit(J, srsrc, Gn, pf, stage, pitch);
+            __syncthreads(); // single staging buffer: everyone is done reading it
+            stage_commit(J, srsrc, Gn, pn, stage, pitch, nt);
             __syncthreads();
         }
         buf ^= 1;
@@ -632,7 +667,7 @@ __global__ __launch_bounds__(kBlock, AEON_HIP_MIN_WAVES) void augment_tiles(Laun
         __syncthreads();
         if (tid < 3) {
             uint32_t s = 0;
-            for (int wv = 0; wv < kBlock / 64; wv++) s += (uint32_t)red[wv * 4 + tid];
+            for (int wv = 0; wv < (nt + 63) / 64; wv++) s += (uint32_t)red[wv * 4 + tid];
             a.partials[((size_t)J.stats_slot * a.partial_stride + chunk) * 4 + tid] = s;
         }
     }
@@ -644,9 +679,17 @@ typedef void (*KernelFn)(LaunchArgs);
 template <int KM, int RM>
 KernelFn pick_form(bool photo, int of)
 {
-    if (of == OF_F32_CHW_VEC)
-        return photo ? augment_tiles<KM, RM, true, OF_F32_CHW_VEC> : augment_tiles<KM, RM, false, OF_F32_CHW_VEC>;
-    return photo ? augment_tiles<KM, RM, true, OF_GENERIC> : augment_tiles<KM, RM, false, OF_GENERIC>;
+    if constexpr (RM == RESIZE_AREA2X) {
+        // the planner splits 2x-area records with photometric stages into a resize-only pre-pass
+        // and a copy pass, so these forms are never instantiated
+        if (photo) return nullptr;
+        return of == OF_F32_CHW_VEC ? augment_tiles<KM, RM, false, OF_F32_CHW_VEC>
+                                    : augment_tiles<KM, RM, false, OF_GENERIC>;
+    } else {
+        if (of == OF_F32_CHW_VEC)
+            return photo ? augment_tiles<KM, RM, true, OF_F32_CHW_VEC> : augment_tiles<KM, RM, false, OF_F32_CHW_VEC>;
+        return photo ? augment_tiles<KM, RM, true, OF_GENERIC> : augment_tiles<KM, RM, false, OF_GENERIC>;
+    }
 }
 
 template <int KM>
@@ -669,9 +712,11 @@ KernelFn pick_kernel(int km, int rm, bool photo, int of)
 
 hipError_t launch_tiles(int km, int rm, bool photo, const LaunchArgs& a, int n_jobs, hipStream_t stream)
 {
-    const int of = (a.out_dtype == OUT_F32 && a.channel_major && a.vec_ok) ? OF_F32_CHW_VEC : OF_GENERIC;
-    dim3      grid(a.max_tiles, n_jobs), block(kBlock);
-    hipLaunchKernelGGL(pick_kernel(km, rm, photo, of), grid, block, a.lds_bytes, stream, a);
+    const int      of = (a.out_dtype == OUT_F32 && a.channel_major && a.vec_ok) ? OF_F32_CHW_VEC : OF_GENERIC;
+    const KernelFn fn = pick_kernel(km, rm, photo, of);
+    if (!fn) return hipErrorInvalidDeviceFunction;
+    dim3 grid(a.max_tiles, n_jobs), block(a.threads);
+    hipLaunchKernelGGL(fn, grid, block, a.lds_bytes, stream, a);
     return hipGetLastError();
 }
 
@@ -681,8 +726,9 @@ hipError_t set_kernel_lds_limit(int bytes)
         for (int rm = 0; rm < 4; rm++)
             for (int ph = 0; ph < 2; ph++)
                 for (int of = 0; of < 2; of++) {
-                    hipError_t e = hipFuncSetAttribute((const void*)pick_kernel(km, rm, ph != 0, of),
-                                                       hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+                    const KernelFn fn = pick_kernel(km, rm, ph != 0, of);
+                    if (!fn) continue;
+                    hipError_t e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
                     if (e != hipSuccess) return e;
                 }
     return hipSuccess;

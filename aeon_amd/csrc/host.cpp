@@ -454,6 +454,7 @@ batch_decoder::batch_decoder(const Json& config, int device) : m_device(device)
         if (node_id >= node_count) throw std::runtime_error("node_id can't be greater than node_count");
         if (seed == 0) seed = 1; // loader.cpp:109-113
     }
+    get_bool(config, "batch_major", m_batch_major);
     std::string cpu_list;
     get_str(config, "cpu_list", cpu_list);
     int threads = aeon_thread_count(cpu_list);
@@ -474,6 +475,8 @@ batch_decoder::batch_decoder(const Json& config, int device) : m_device(device)
     // the HIP context is created on the first window (configs validate without a GPU)
     m_dev_out.assign(m_provider->providers().size(), nullptr);
     m_dev_out_cap.assign(m_provider->providers().size(), 0);
+    m_dev_tmp.assign(m_provider->providers().size(), nullptr);
+    m_dev_tmp_cap.assign(m_provider->providers().size(), 0);
 }
 
 batch_decoder::~batch_decoder()
@@ -483,14 +486,17 @@ batch_decoder::~batch_decoder()
     (void)hipSetDevice(m_device);
     if (m_pinned) (void)hipHostFree(m_pinned);
     if (m_dev_src) (void)hipFree(m_dev_src);
-    for (auto* p : m_dev_out)
-        if (p) (void)hipFree(p);
+    for (auto* v : {&m_dev_out, &m_dev_tmp})
+        for (auto* p : *v)
+            if (p) (void)hipFree(p);
 }
 
 void batch_decoder::decode(int n, const decoded_element* records, void* const* outputs, bool on_device,
                            void* stream_)
 {
     if (n <= 0) return;
+    if (!m_batch_major && n % m_batch_size != 0)
+        invalid("batch_major=false needs whole batches per decode window");
     if (m_deterministic && n > (int)m_random.size())
         invalid("decode window larger than the deterministic slot table (4096)");
     if (!m_ctx) check(aeon_hip_ctx_create(m_device, &m_ctx));
@@ -549,7 +555,33 @@ void batch_decoder::decode(int n, const decoded_element* records, void* const* o
             outs[k] = m_dev_out[k];
         }
     }
-    m_provider->post_process(m_ctx, w, m_dev_src, outs.data(), stream);
+    auto grow = [&](std::vector<uint8_t*>& v, std::vector<size_t>& cap, int k, size_t bytes) {
+        if (bytes <= cap[k]) return;
+        if (v[k]) hip_check(hipFree(v[k]), "hipFree");
+        v[k] = nullptr;
+        hip_check(hipMalloc((void**)&v[k], bytes), "hipMalloc");
+        cap[k] = bytes;
+    };
+    if (m_batch_major) {
+        m_provider->post_process(m_ctx, w, m_dev_src, outs.data(), stream);
+    } else {
+        std::vector<void*> tmp(ne);
+        for (int k = 0; k < ne; k++) {
+            grow(m_dev_tmp, m_dev_tmp_cap, k, (size_t)n * m_provider->providers()[k]->shape().byte_size());
+            tmp[k] = m_dev_tmp[k];
+        }
+        m_provider->post_process(m_ctx, w, m_dev_src, tmp.data(), stream);
+        for (int k = 0; k < ne; k++) {
+            const shape_type& sh    = m_provider->providers()[k]->shape();
+            const size_t      esize = sh.otype.size;
+            const size_t      item  = sh.byte_size();
+            for (int b = 0; b < n / m_batch_size; b++) {
+                const size_t off = (size_t)b * m_batch_size * item;
+                check(aeon_hip_transpose_batch(m_ctx, (uint8_t*)tmp[k] + off, (uint8_t*)outs[k] + off,
+                                               m_batch_size, (int64_t)(item / esize), (int)esize, stream));
+            }
+        }
+    }
     if (!on_device)
         for (int k = 0; k < ne; k++)
             hip_check(hipMemcpyAsync(outputs[k], outs[k], (size_t)n * m_provider->providers()[k]->shape().byte_size(),

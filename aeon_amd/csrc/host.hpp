@@ -180,6 +180,11 @@ private:
     size_t                         m_dev_src_cap = 0;
     std::vector<uint8_t*>          m_dev_out;
     std::vector<size_t>            m_dev_out_cap;
+    // batch_major=false (loader.hpp:63): outputs are produced batch-major into m_dev_tmp and
+    // transposed per batch into the caller's layout (batch_iterator.cpp:125-136)
+    bool                           m_batch_major = true;
+    std::vector<uint8_t*>          m_dev_tmp;
+    std::vector<size_t>            m_dev_tmp_cap;
 };
 
 // manifest_file node slicing (generate_blocks, src/manifest_file.cpp:278-295)

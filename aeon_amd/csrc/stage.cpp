@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
 #include <cfloat>
 #include <cmath>
 #include <cstdlib>
@@ -21,6 +23,8 @@
 namespace aeon_hip {
 hipError_t launch_tiles(int km, int rm, bool photo, const LaunchArgs& a, int n_jobs, hipStream_t stream);
 hipError_t set_kernel_lds_limit(int bytes);
+hipError_t launch_transpose(const void* src, void* dst, int64_t rows, int64_t cols, int element_size,
+                            hipStream_t stream);
 } // namespace aeon_hip
 
 using namespace aeon_hip;
@@ -42,9 +46,9 @@ struct aeon_error : std::runtime_error {
     } while (0)
 
 constexpr int kMaxLds        = 160 * 1024;
-constexpr int kStageBudget   = 16 * 1024;   // preferred LDS bytes per staged band
+constexpr int kStageBudget   = 24 * 1024;   // preferred LDS bytes per staged band
 constexpr int kStageBudgetHi = 120 * 1024;  // fallback for very wide crops
-constexpr int kBandsPerChunk = 2;
+constexpr int kBandsPerChunk = 1;
 
 // ---------------------------------------------------------------------------------------------
 // Per-image constants (aeon computes these on the host per record, too)
@@ -122,16 +126,20 @@ void plan_lighting(AugJob& J, const float* al, float sigma)
 // type per op, rounded to f32 after each op) tabulated per channel and input value.
 void build_lut(const aeon_out_desc& o, float* lut)
 {
-    for (int c = 0; c < 3; c++)
+    // indexed by SOURCE channel c; its value lands in output channel oc (mixChannels
+    // from_to {0,2,1,1,2,0} when bgr_to_rgb), standardized with that channel's mean/stddev
+    for (int c = 0; c < 3; c++) {
+        const int oc = (o.bgr_to_rgb && o.channels == 3) ? 2 - c : c;
         for (int x = 0; x < 256; x++) {
-            if (!o.has_mean || c >= o.channels) {
+            if (!o.has_mean || oc >= o.channels) {
                 lut[c * 256 + x] = (float)x;
                 continue;
             }
             float t1 = (float)((double)(float)x * (1. / 255.));
-            float t2 = (float)((double)t1 - o.mean[c]);
-            lut[c * 256 + x] = o.stddev[c] != 0 ? (float)((double)t2 * (1. / o.stddev[c])) : t2;
+            float t2 = (float)((double)t1 - o.mean[oc]);
+            lut[c * 256 + x] = o.stddev[oc] != 0 ? (float)((double)t2 * (1. / o.stddev[oc])) : t2;
         }
+    }
 }
 
 // source-footprint bounds used to size the LDS staging area
@@ -163,7 +171,7 @@ struct LaunchPlan {
     size_t              partial_off = 0;  // uint32 offset of this group's contrast partials
     std::vector<AugJob> jobs;
     int                 tr = 1, chunk_rows = 1, stage_rows = 0, stage_pitch = 0, max_win_w = 0, max_tiles = 0;
-    int                 lds = 0;
+    int                 lds = 0, threads = kBlockMax;
     bool                vec_ok = true;
     int                 stats_slots = 0;
     bool                has_hue = false;
@@ -174,13 +182,28 @@ struct LaunchPlan {
         int budget = kStageBudget;
         int ww     = 0;
         for (const AugJob& J : jobs) ww = std::max(ww, J.win_w);
-        // rows per tile: about two 4-pixel groups per lane (short tiles keep many workgroups
-        // resident per CU and the per-tile prologue small); knobs for experiments only
-        int tr_cap = std::min(32, std::max(1, (2 * kBlock * 4 + ww - 1) / std::max(ww, 1)));
+        // workgroup = 256..512 lanes holding whole 4-pixel column groups (fewest idle lanes;
+        // ties go to the larger group), row phases = lanes / column groups
+        const int gpr = (std::max(ww, 1) + 3) / 4;
+        const int ncg = std::min(gpr, kBlockMax);
+        threads       = kBlockMax;
+        int best_idle = kBlockMax;
+        for (int nt = kBlockMin; nt <= kBlockMax; nt += 64) {
+            const int idle = nt - (nt / ncg) * ncg;
+            // idle / nt <= best_idle / threads
+            if ((long)idle * threads <= (long)best_idle * nt) threads = nt, best_idle = idle;
+        }
+        if (const char* e = std::getenv("AEON_HIP_THREADS"))
+            threads = std::min(kBlockMax, std::max(kBlockMin, std::atoi(e) / 64 * 64));
+        const int nph = threads / ncg;
+        // rows per band: about two rows per lane, a multiple of the row phases; knobs for
+        // experiments only
+        int tr_cap = std::min(32, std::max(1, 2 * nph));
         if (const char* e = std::getenv("AEON_HIP_STAGE_KB")) budget = std::max(1, std::atoi(e)) * 1024;
         if (const char* e = std::getenv("AEON_HIP_TR")) tr_cap = std::max(1, std::atoi(e));
         for (int pass = 0; pass < 2; pass++) {
             for (int tr = tr_cap; tr >= 1; tr--) {
+                if (tr > nph && tr % nph) continue;
                 int rows = 0, pitch = 0;
                 for (const AugJob& J : jobs) {
                     rows  = std::max(rows, stage_rows_for(J, tr));
@@ -201,8 +224,8 @@ struct LaunchPlan {
         if (lds > kMaxLds)
             fail(AEON_HIP_EUNSUPPORTED, "source crop too wide for one LDS-staged row band (" +
                                             std::to_string(lds) + " bytes)");
-        // rows per workgroup: kBandsPerChunk bands, so the next band's loads overlap this band's
-        // work and the per-workgroup tables are built once (measured best at 2 on C2 and C3)
+        // rows per workgroup: kBandsPerChunk bands (one: a band's wait for the next band's loads
+        // would also wait for this band's stores -- one vector-memory counter on CDNA)
         int max_h = 0;
         for (const AugJob& J : jobs) max_h = std::max(max_h, J.win_h);
         int per = kBandsPerChunk;
@@ -218,9 +241,11 @@ struct LaunchPlan {
 };
 
 // Geometry + constants of one image-provider record (transform_single_image).
+// Launch order: pre (resize_short) -> pre2 (2x-area resize ahead of photometric stages) ->
+// pass1 (contrast statistics) -> main; each reads only what an earlier group wrote.
 void plan_image(const aeon_img_desc& d, const void* src_base, const aeon_aug_params& p,
                 const aeon_out_desc& o, uint8_t* out_item, bool is_mask, LaunchPlan& pre,
-                LaunchPlan& pass1, LaunchPlan& main, size_t& scratch_bytes)
+                LaunchPlan& pre2, LaunchPlan& pass1, LaunchPlan& main, size_t& scratch_bytes)
 {
     const int cn = d.channels;
     if (cn != 1 && cn != 3) fail(AEON_HIP_EINVAL, "channels must be 1 or 3");
@@ -306,6 +331,26 @@ void plan_image(const aeon_img_desc& d, const void* src_base, const aeon_aug_par
             plan_lighting(J, p.lighting, p.color_noise_std);
         }
         J.photo = photo;
+        if (photo && J.mode == RESIZE_AREA2X) {
+            // 2x-area resize first (resize-only pre-pass into scratch, unflipped), then the
+            // photometric stages as a copy pass over it
+            AugJob P      = J;
+            P.photo       = 0;
+            P.flip        = 0;
+            size_t off    = (scratch_bytes + 15) & ~(size_t)15;
+            scratch_bytes = off + (size_t)J.win_w * J.win_h * 3 + 16;
+            P.out_ptr     = off; // relocated to the slot's scratch by the caller
+            pre2.jobs.push_back(P);
+            J.src_ptr     = off;
+            J.src_scratch = 1;
+            J.src_bytes   = (uint64_t)J.win_w * J.win_h * 3;
+            J.src_w = J.win_w, J.src_h = J.win_h, J.src_stride = J.win_w * 3;
+            J.crop_x = J.crop_y = 0, J.crop_w = J.win_w, J.crop_h = J.win_h;
+            J.shift_x = J.shift_y = J.padded = 0;
+            J.mode    = RESIZE_COPY;
+            J.scale_x = J.scale_y = 1.0;
+            J.xv      = simd_boundary(J.win_w * 3);
+        }
         if (photo & PHOTO_CONTRAST) {
             // contrast needs the mean of the post-hue image: pass 1 writes that image (HWC
             // uint8, unflipped) and its exact per-chunk sums; pass 2 (this job) reads it back
@@ -338,7 +383,8 @@ void plan_image(const aeon_img_desc& d, const void* src_base, const aeon_aug_par
 // Context: per-GPU state and a 4-deep staging ring (pinned host blob -> device blob per call)
 // ---------------------------------------------------------------------------------------------
 struct Slot {
-    hipEvent_t done     = nullptr;
+    hipEvent_t done     = nullptr; // the slot's kernels finished (host reuses the slot after it)
+    hipEvent_t copied   = nullptr; // the slot's job table reached the device
     bool       pending  = false;
     uint8_t*   host     = nullptr;
     size_t     host_cap = 0;
@@ -364,11 +410,18 @@ struct aeon_hip_ctx {
     int32_t*   d_hsv   = nullptr;
     Slot       slots[4];
     int        next = 0;
+    // job tables go up on their own stream, so a call's H2D overlaps the previous call's kernels
+    // instead of queueing between them on the caller's stream
+    hipStream_t copy_stream = nullptr;
     std::mutex mu;
     // optional per-launch timing (aeon_hip_set_timing): events recorded on the launch stream
     bool                     timing = false;
     std::vector<KernelTimer> timers, free_timers;
     double                   ms[3]    = {0, 0, 0};
+    // AEON_HIP_HOST_PROFILE=1: host time per run_batch phase, printed when the context is destroyed
+    bool                     host_profile = false;
+    std::vector<double>      host_ns[8];  // per call, per phase
+    long                     host_calls   = 0;
     double                   bytes[3] = {0, 0, 0};
     long                     count[3] = {0, 0, 0};
 };
@@ -451,29 +504,40 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
     hipStream_t stream = (hipStream_t)stream_;
 
     std::lock_guard<std::mutex> lock(ctx->mu);
+    using clk = std::chrono::steady_clock;
+    auto t_prev = clk::now();
+    auto phase  = [&](int k) {
+        if (!ctx->host_profile) return;
+        auto t = clk::now();
+        ctx->host_ns[k].push_back(std::chrono::duration<double, std::nano>(t - t_prev).count());
+        t_prev = t;
+    };
     HIP_OK(hipSetDevice(ctx->device));
+    phase(0);
 
-    LaunchPlan pre_all, pass1_all, main_all;
+    LaunchPlan pre_all, pre2_all, pass1_all, main_all;
     size_t     scratch_bytes = 0;
     for (int i = 0; i < n; i++)
         plan_image(descs[i], src_base, params[i], o, (uint8_t*)out_dev + (size_t)i * o.item_stride,
-                   is_mask, pre_all, pass1_all, main_all, scratch_bytes);
+                   is_mask, pre_all, pre2_all, pass1_all, main_all, scratch_bytes);
 
+    phase(1);
     // one launch per (resize mode, photometric) group: the kernels are specialised on both
-    std::vector<LaunchPlan> pre(4), pass1(4), main(8);
+    std::vector<LaunchPlan> pre(4), pre2(4), pass1(4), main(8);
     for (int rm = 0; rm < 4; rm++) {
-        pre[rm].rm = pass1[rm].rm = rm;
+        pre[rm].rm = pre2[rm].rm = pass1[rm].rm = rm;
         pass1[rm].photo = true;
         for (int ph = 0; ph < 2; ph++) main[rm * 2 + ph].rm = rm, main[rm * 2 + ph].photo = ph != 0;
     }
     for (const AugJob& J : pre_all.jobs) pre[J.mode].jobs.push_back(J);
+    for (const AugJob& J : pre2_all.jobs) pre2[J.mode].jobs.push_back(J);
     for (const AugJob& J : pass1_all.jobs) pass1[J.mode].jobs.push_back(J);
     for (const AugJob& J : main_all.jobs) main[J.mode * 2 + (J.photo ? 1 : 0)].jobs.push_back(J);
     const size_t     lut_bytes = 4096;
     size_t           blob      = lut_bytes;
     std::vector<int> slot_tiles(pass1_all.jobs.size(), 0);
     int              partial_stride = 1;
-    for (auto* v : {&pre, &pass1, &main})
+    for (auto* v : {&pre, &pre2, &pass1, &main})
         for (LaunchPlan& P : *v) {
             if (P.jobs.empty()) continue;
             P.vec_ok = main_all.vec_ok;
@@ -491,12 +555,14 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
         }
     const size_t partial_words = std::max<size_t>(4, pass1_all.jobs.size() * partial_stride * 4);
 
+    phase(2);
     Slot& s = ctx->slots[ctx->next];
     ctx->next = (ctx->next + 1) % 4;
     if (s.pending) {
         HIP_OK(hipEventSynchronize(s.done));
         s.pending = false;
     }
+    phase(3);
     grow(s.host, s.host_cap, blob, true);
     grow(s.dev, s.dev_cap, blob, false);
     grow(s.scratch, s.scratch_cap, std::max<size_t>(scratch_bytes, 16), false);
@@ -506,7 +572,7 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
         s.partials = (uint32_t*)p;
     }
     build_lut(o, (float*)s.host);
-    for (auto* v : {&pre, &pass1, &main})
+    for (auto* v : {&pre, &pre2, &pass1, &main})
         for (LaunchPlan& P : *v) {
             for (AugJob& J : P.jobs) { // relocate scratch references
                 if (v != &main) J.out_ptr += (uint64_t)s.scratch;
@@ -514,7 +580,11 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
             }
             if (!P.jobs.empty()) std::memcpy(s.host + P.blob_off, P.jobs.data(), P.jobs.size() * sizeof(AugJob));
         }
-    HIP_OK(hipMemcpyAsync(s.dev, s.host, blob, hipMemcpyHostToDevice, stream));
+    phase(4);
+    HIP_OK(hipMemcpyAsync(s.dev, s.host, blob, hipMemcpyHostToDevice, ctx->copy_stream));
+    HIP_OK(hipEventRecord(s.copied, ctx->copy_stream));
+    HIP_OK(hipStreamWaitEvent(stream, s.copied, 0));
+    phase(5);
 
     auto args = [&](const LaunchPlan& L) {
         LaunchArgs a{};
@@ -536,17 +606,22 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
         a.vec_ok        = L.vec_ok && o.channel_major;
         a.lds_bytes     = L.lds;
         a.has_hue       = L.has_hue;
+        a.threads       = L.threads;
         return a;
     };
     const size_t oelem = o.dtype == AEON_DTYPE_F32 ? 4 : 1;
-    for (LaunchPlan& P : pre)
-        if (!P.jobs.empty()) timed_launch(ctx, KM_RAW, P, args(P), stream, launch_bytes(P, KM_RAW, 1));
+    for (auto* v : {&pre, &pre2})
+        for (LaunchPlan& P : *v)
+            if (!P.jobs.empty()) timed_launch(ctx, KM_RAW, P, args(P), stream, launch_bytes(P, KM_RAW, 1));
     for (LaunchPlan& P : pass1)
         if (!P.jobs.empty()) timed_launch(ctx, KM_STATS, P, args(P), stream, launch_bytes(P, KM_STATS, oelem));
     for (LaunchPlan& P : main)
         if (!P.jobs.empty()) timed_launch(ctx, KM_FINAL, P, args(P), stream, launch_bytes(P, KM_FINAL, oelem));
+    phase(6);
     HIP_OK(hipEventRecord(s.done, stream));
     s.pending = true;
+    phase(7);
+    ctx->host_calls++;
     return 0;
 }
 
@@ -602,7 +677,12 @@ int aeon_hip_ctx_create(int device, aeon_hip_ctx** out)
             }
             HIP_OK(hipMalloc((void**)&c->d_hsv, sizeof(tab)));
             HIP_OK(hipMemcpy(c->d_hsv, tab, sizeof(tab), hipMemcpyHostToDevice));
-            for (Slot& s : c->slots) HIP_OK(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
+            for (Slot& s : c->slots) {
+                HIP_OK(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
+                HIP_OK(hipEventCreateWithFlags(&s.copied, hipEventDisableTiming));
+            }
+            HIP_OK(hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
+            if (const char* e = std::getenv("AEON_HIP_HOST_PROFILE")) c->host_profile = std::atoi(e) != 0;
         } catch (...) {
             delete c;
             throw;
@@ -616,10 +696,23 @@ int aeon_hip_ctx_destroy(aeon_hip_ctx* c)
 {
     return guarded([&] {
         if (!c) return 0;
+        if (c->host_profile && c->host_calls) {
+            static const char* names[8] = {"set_device", "plan", "group+finalize", "slot_wait",
+                                           "blob_fill", "h2d+wait_event", "launches", "done_event"};
+            std::fprintf(stderr, "[aeon_hip host profile] %ld calls, median us per call:", c->host_calls);
+            for (int k = 0; k < 8; k++) {
+                std::vector<double> v = c->host_ns[k];
+                if (v.empty()) continue;
+                std::nth_element(v.begin(), v.begin() + v.size() / 2, v.end());
+                std::fprintf(stderr, " %s=%.1f", names[k], v[v.size() / 2] / 1e3);
+            }
+            std::fprintf(stderr, "\n");
+        }
         (void)hipSetDevice(c->device);
         for (Slot& s : c->slots) {
             if (s.pending) (void)hipEventSynchronize(s.done);
             if (s.done) (void)hipEventDestroy(s.done);
+            if (s.copied) (void)hipEventDestroy(s.copied);
             if (s.host) (void)hipHostFree(s.host);
             if (s.dev) (void)hipFree(s.dev);
             if (s.scratch) (void)hipFree(s.scratch);
@@ -627,9 +720,31 @@ int aeon_hip_ctx_destroy(aeon_hip_ctx* c)
         }
         for (auto* v : {&c->timers, &c->free_timers})
             for (KernelTimer& t : *v) (void)hipEventDestroy(t.start), (void)hipEventDestroy(t.stop);
+        if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
         if (c->d_error) (void)hipFree(c->d_error);
         if (c->d_hsv) (void)hipFree(c->d_hsv);
         delete c;
+        return 0;
+    });
+}
+
+int aeon_hip_transpose_batch(aeon_hip_ctx* ctx, const void* src_dev, void* dst_dev, int64_t rows, int64_t cols,
+                             int element_size, void* stream)
+{
+    return guarded([&] {
+        if (!ctx || !src_dev || !dst_dev) fail(AEON_HIP_EINVAL, "null argument");
+        if (rows < 0 || cols < 0) fail(AEON_HIP_EINVAL, "negative matrix size");
+        if (element_size != 1 && element_size != 2 && element_size != 4 && element_size != 8)
+            fail(AEON_HIP_EINVAL, "unsupported datatype for transpose");
+        if (rows / 64 >= 65535) fail(AEON_HIP_EINVAL, "too many rows for one transpose");
+        if (rows == 0 || cols == 0) return 0;
+        const uint8_t* s = (const uint8_t*)src_dev;
+        uint8_t*       d = (uint8_t*)dst_dev;
+        const size_t   bytes = (size_t)rows * cols * element_size;
+        if (s < d + bytes && d < s + bytes) fail(AEON_HIP_EINVAL, "transpose buffers overlap");
+        std::lock_guard<std::mutex> lock(ctx->mu);
+        HIP_OK(hipSetDevice(ctx->device));
+        HIP_OK(launch_transpose(src_dev, dst_dev, rows, cols, element_size, (hipStream_t)stream));
         return 0;
     });
 }

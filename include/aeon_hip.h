@@ -103,6 +103,16 @@ int aeon_hip_mask_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs,
                         const void* src_base, const aeon_aug_params* params,
                         const aeon_out_desc* out, void* out_dev, void* stream);
 
+/* batch_major=false output layout: fixed_buffer_map::copy(..., transpose=true) ->
+ * transpose_buf (src/buffer_batch.cpp:186-244, 251-280; called per batch by
+ * batch_iterator_fbm::filler, src/batch_iterator.cpp:125-136):
+ *   dst[c * rows + r] = src[r * cols + c]
+ * for a rows x cols matrix of element_size-byte elements (rows = batch size, cols = elements
+ * per item).  element_size 1, 2, 4 or 8; src and dst are device buffers that must not overlap.
+ * Async on `stream`. */
+int aeon_hip_transpose_batch(aeon_hip_ctx* ctx, const void* src_dev, void* dst_dev, int64_t rows,
+                             int64_t cols, int element_size, void* stream);
+
 /* Wait for `stream` and check the device error word of ctx. */
 int aeon_hip_synchronize(aeon_hip_ctx* ctx, void* stream);
 

@@ -101,6 +101,7 @@ def lib():
         L.orc_batch_augment.argtypes = [ctypes.c_int, P(ctypes.c_void_p), P(ctypes.c_int),
                                         P(ctypes.c_int), P(Params), P(LoadConfig), ctypes.c_void_p,
                                         ctypes.c_size_t, ctypes.c_int]
+        L.orc_transpose.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int]
         L.orc_last_error.restype = ctypes.c_char_p
         _lib = L
     return _lib
@@ -255,3 +256,14 @@ def batch_augment(srcs, params_list, lc, item_shape, threads):
     if secs < 0:
         raise RuntimeError("oracle: " + lib().orc_last_error().decode())
     return out, secs
+
+
+def transpose(src, rows, cols, element_size):
+    """transpose_buf: bytes of a rows x cols matrix of element_size-byte elements, transposed."""
+    src = np.ascontiguousarray(src).view(np.uint8).reshape(-1)
+    if src.size != rows * cols * element_size:
+        raise ValueError("size mismatch")
+    out = np.empty_like(src)
+    _check(lib().orc_transpose(out.ctypes.data, src.ctypes.data, ctypes.c_int64(rows), ctypes.c_int64(cols),
+                               element_size))
+    return out

@@ -647,6 +647,22 @@ int guarded(F&& f)
 
 } // namespace
 
+// transpose_regular<T> (src/buffer_batch.cpp:186-200): walks the destination in order, reading
+// the source down each column.  (transpose_buf's SSE variant for 16-aligned sizes computes the
+// same permutation.)
+template <typename T>
+static void transpose_regular(T* dest, const T* src, int64_t rows, int64_t cols)
+{
+    int64_t dst_indx = 0;
+    for (int64_t c = 0; c < cols; ++c) {
+        int64_t src_indx = c;
+        for (int64_t r = 0; r < rows; ++r) {
+            dest[dst_indx++] = src[src_indx];
+            src_indx += cols;
+        }
+    }
+}
+
 extern "C" {
 
 void* orc_factory_create(const orc_aug_config* cfg) { return new Factory(*cfg); }
@@ -765,6 +781,17 @@ double orc_batch_augment(int n, const uint8_t* const* srcs, const int* widths, c
     auto t1 = std::chrono::steady_clock::now();
     if (failed) return -1.0;
     return std::chrono::duration<double>(t1 - t0).count();
+}
+
+int orc_transpose(void* dest, const void* src, int64_t rows, int64_t cols, int element_size)
+{
+    switch (element_size) {
+    case 1: transpose_regular((uint8_t*)dest, (const uint8_t*)src, rows, cols); return 0;
+    case 2: transpose_regular((uint16_t*)dest, (const uint16_t*)src, rows, cols); return 0;
+    case 4: transpose_regular((uint32_t*)dest, (const uint32_t*)src, rows, cols); return 0;
+    case 8: transpose_regular((uint64_t*)dest, (const uint64_t*)src, rows, cols); return 0;
+    default: g_err = "unsupported datatype for transpose"; return -1;
+    }
 }
 
 const char* orc_last_error(void) { return g_err.c_str(); }

@@ -91,6 +91,10 @@ float orc_standardize_value(int x, double mean, double stddev);
 /* whole-record path (transform + load) over a batch on a thread pool -- CPU baseline.
  * srcs[i] = HWC BGR uint8 image i (widths/heights per image), params[i] its params,
  * out = batch of item_bytes slots.  Returns elapsed seconds. */
+/* transpose_regular (src/buffer_batch.cpp:186-200) as transpose_buf dispatches it (:202-244):
+ * dest[c * rows + r] = src[r * cols + c], element_size 1, 2, 4 or 8.  Returns -1 otherwise. */
+int orc_transpose(void* dest, const void* src, int64_t rows, int64_t cols, int element_size);
+
 double orc_batch_augment(int n, const uint8_t* const* srcs, const int* widths, const int* heights,
                          const orc_params* params, const orc_load_config* lc, void* out,
                          size_t item_bytes, int threads);

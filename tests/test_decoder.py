@@ -63,3 +63,25 @@ def test_decoder_empty_record_raises():
     with pytest.raises(A.AeonHipError) as e:
         d.decode([(np.zeros((0, 0, 3), np.uint8),)])
     assert "size 0" in str(e.value)
+
+
+def test_decoder_batch_major_false_transposes_each_batch():
+    # batch_major=false (loader.hpp:63): each batch arrives as [element][record]
+    # (batch_iterator.cpp:125-136 -> transpose_buf, buffer_batch.cpp:251-280)
+    import oracle as O
+    cfg = dict(batch_size=4, random_seed=9, etl=[C.IMAGE_224], augmentation=[C.C2_AUG])
+    recs = _records(8, seed=4)
+    (ref,) = A.Decoder(cfg).decode(recs)
+    (out,) = A.Decoder(dict(cfg, batch_major=False)).decode(recs)
+    item = ref[0].nbytes
+    raw = ref.reshape(-1).view(np.uint8)
+    got = out.reshape(-1).view(np.uint8)
+    for b in range(2):
+        blk = raw[b * 4 * item:(b + 1) * 4 * item]
+        assert np.array_equal(got[b * 4 * item:(b + 1) * 4 * item], O.transpose(blk, 4, item // 4, 4)), b
+
+
+def test_decoder_batch_major_false_needs_whole_batches():
+    cfg = dict(batch_size=4, random_seed=9, batch_major=False, etl=[C.IMAGE_224], augmentation=[C.C2_AUG])
+    with pytest.raises(A.AeonHipError, match="whole batches"):
+        A.Decoder(cfg).decode(_records(3, seed=4))

@@ -199,3 +199,32 @@ def test_full_batch_c3_properties(ctx):
     ref = H.oracle_records([imgs[i] for i in sample], [params[i] for i in sample], out)
     _assert_same([r1[i] for i in sample], ref, "C3 full-size sample")
     torch.cuda.synchronize()
+
+
+# ---- batch transpose (batch_major=false layout) ---------------------------------------------
+@pytest.mark.parametrize("rows,cols,esize", [(256, 150528, 4), (7, 1000, 4), (64, 64, 4), (1, 33, 4),
+                                             (33, 1, 4), (5, 127, 1), (130, 70, 2), (3, 65, 8)])
+def test_transpose_batch_matches_oracle(rows, cols, esize):
+    import torch
+    import oracle as O
+    n = rows * cols * esize
+    src = torch.randint(0, 256, (n,), dtype=torch.uint8, device="cuda")
+    dst = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    ctx = A.Context(0)
+    st = torch.cuda.current_stream().cuda_stream
+    ctx.transpose_batch(src.data_ptr(), dst.data_ptr(), rows, cols, esize, st)
+    ctx.synchronize(st)
+    ref = O.transpose(src.cpu().numpy(), rows, cols, esize)
+    assert np.array_equal(dst.cpu().numpy(), ref)
+    ctx.close()
+
+
+def test_transpose_batch_rejects_bad_arguments():
+    import torch
+    src = torch.zeros(64, dtype=torch.uint8, device="cuda")
+    ctx = A.Context(0)
+    with pytest.raises(A.AeonHipError, match="unsupported datatype"):
+        ctx.transpose_batch(src.data_ptr(), src.data_ptr() + 32, 2, 2, 3)
+    with pytest.raises(A.AeonHipError, match="overlap"):
+        ctx.transpose_batch(src.data_ptr(), src.data_ptr() + 8, 4, 4, 1)
+    ctx.close()

@@ -126,3 +126,14 @@ def test_standardize_values(oracle):
     # the f64-per-op formula pinned by the goldens, spot values
     v = oracle.lib().orc_standardize_value(255, 0.485, 0.229)
     assert abs(v - (1.0 - 0.485) / 0.229) < 1e-6
+
+
+@pytest.mark.parametrize("esize,dtype", [(1, np.uint8), (2, np.uint16), (4, np.uint32), (8, np.uint64)])
+def test_transpose_restatement(oracle, esize, dtype):
+    # transpose_regular (src/buffer_batch.cpp:186-200): dest[c*rows + r] = src[r*cols + c]
+    rows, cols = 5, 9
+    m = np.arange(rows * cols, dtype=dtype).reshape(rows, cols)
+    out = oracle.transpose(m, rows, cols, esize).view(dtype).reshape(cols, rows)
+    assert np.array_equal(out, m.T)
+    with pytest.raises(RuntimeError, match="unsupported datatype"):
+        oracle.transpose(np.zeros(15, np.uint8), 5, 1, 3)
