@@ -56,6 +56,16 @@ struct alignas(16) AugJob {
     int32_t  stats_tiles;                    // chunks of the pass-1 job that wrote this slot's sums
 };
 
+// image::rotate pre-pass of one record (rotate_kernels.hip): source -> same-size scratch image.
+struct alignas(16) RotJob {
+    double   M[6];     // warpAffine's inverted affine map (output -> source), as OpenCV computes it
+    uint64_t src_ptr;  // HWC uint8 source
+    uint64_t out_ptr;  // HWC uint8 rotated image (w * cn bytes per row)
+    int32_t  w, h, stride, cn;
+    int32_t  interp;   // AEON_INTERP_LINEAR (images) or AEON_INTERP_NEAREST (pixel masks)
+    int32_t  pad_;
+};
+
 // Per-launch uniform arguments.
 struct LaunchArgs {
     const AugJob*  jobs;

@@ -25,6 +25,7 @@ hipError_t launch_tiles(int km, int rm, bool photo, const LaunchArgs& a, int n_j
 hipError_t set_kernel_lds_limit(int bytes);
 hipError_t launch_transpose(const void* src, void* dst, int64_t rows, int64_t cols, int element_size,
                             hipStream_t stream);
+hipError_t launch_rotate(const RotJob* jobs, int n_jobs, int max_pixels, hipStream_t stream);
 } // namespace aeon_hip
 
 using namespace aeon_hip;
@@ -241,19 +242,39 @@ struct LaunchPlan {
 };
 
 // Geometry + constants of one image-provider record (transform_single_image).
-// Launch order: pre (resize_short) -> pre2 (2x-area resize ahead of photometric stages) ->
+// image::rotate (src/image.cpp:53-75): cv::getRotationMatrix2D(Point2i(cols/2, rows/2), angle, 1)
+// inverted the way cv::warpAffine does without WARP_INVERSE_MAP (OpenCV 2.4 imgwarp.cpp); double
+// arithmetic on the host, as aeon's.
+void rotation_inverse_map(int w, int h, int angle, double M[6])
+{
+    const float  cx = (float)(w / 2), cy = (float)(h / 2); // Point2i -> Point2f
+    const double a  = (double)angle * (3.1415926535897932384626433832795 / 180);
+    const double alpha = std::cos(a) * 1.0, beta = std::sin(a) * 1.0;
+    M[0] = alpha, M[1] = beta, M[2] = (1 - alpha) * cx - beta * cy;
+    M[3] = -beta, M[4] = alpha, M[5] = beta * cx + (1 - alpha) * cy;
+    double D = M[0] * M[4] - M[1] * M[3];
+    D        = D != 0 ? 1. / D : 0;
+    const double A11 = M[4] * D, A22 = M[0] * D;
+    M[0] = A11;
+    M[1] *= -D;
+    M[3] *= -D;
+    M[4] = A22;
+    const double b1 = -M[0] * M[2] - M[1] * M[5];
+    const double b2 = -M[3] * M[2] - M[4] * M[5];
+    M[2] = b1, M[5] = b2;
+}
+
+// Launch order: rot (image::rotate) -> pre (resize_short) -> pre2 (2x-area resize ahead of photometric stages) ->
 // pass1 (contrast statistics) -> main; each reads only what an earlier group wrote.
 void plan_image(const aeon_img_desc& d, const void* src_base, const aeon_aug_params& p,
-                const aeon_out_desc& o, uint8_t* out_item, bool is_mask, LaunchPlan& pre,
-                LaunchPlan& pre2, LaunchPlan& pass1, LaunchPlan& main, size_t& scratch_bytes)
+                const aeon_out_desc& o, uint8_t* out_item, bool is_mask, std::vector<RotJob>& rot,
+                LaunchPlan& pre, LaunchPlan& pre2, LaunchPlan& pass1, LaunchPlan& main, size_t& scratch_bytes)
 {
     const int cn = d.channels;
     if (cn != 1 && cn != 3) fail(AEON_HIP_EINVAL, "channels must be 1 or 3");
     if (cn != o.channels) fail(AEON_HIP_EINVAL, "decoded channels do not match the output config");
     if (d.width <= 0 || d.height <= 0 || d.stride < d.width * cn)
         fail(AEON_HIP_EINVAL, "invalid source image descriptor");
-    if (p.angle != 0)
-        fail(AEON_HIP_EUNSUPPORTED, "rotation (angle != 0) is not implemented in the HIP stage");
     const int interp = is_mask ? AEON_INTERP_NEAREST : p.interp;
     if (interp != AEON_INTERP_LINEAR && interp != AEON_INTERP_NEAREST)
         fail(AEON_HIP_EUNSUPPORTED, "only LINEAR and NEAREST interpolation are implemented");
@@ -267,6 +288,23 @@ void plan_image(const aeon_img_desc& d, const void* src_base, const aeon_aug_par
     J.src_bytes  = (uint64_t)d.stride * d.height;
     J.src_w      = d.width, J.src_h = d.height, J.src_stride = d.stride, J.cn = cn;
     J.stats_slot = -1;
+    if (p.angle != 0) {
+        // image::rotate into scratch (interpolated for images, nearest + border 0 for pixel
+        // masks, etl_pixel_mask.cpp:72-74); everything after reads the rotated record
+        RotJob R{};
+        rotation_inverse_map(d.width, d.height, p.angle, R.M);
+        R.src_ptr = J.src_ptr;
+        R.w = d.width, R.h = d.height, R.stride = d.stride, R.cn = cn;
+        R.interp      = is_mask ? AEON_INTERP_NEAREST : AEON_INTERP_LINEAR;
+        size_t off    = (scratch_bytes + 15) & ~(size_t)15;
+        scratch_bytes = off + (size_t)d.width * d.height * cn + 16;
+        R.out_ptr     = off; // relocated to the slot's scratch by the caller
+        rot.push_back(R);
+        J.src_ptr     = off;
+        J.src_scratch = 1;
+        J.src_bytes   = (uint64_t)d.width * d.height * cn;
+        J.src_stride  = d.width * cn;
+    }
 
     int base_w = d.width, base_h = d.height;
     if (!is_mask && p.resize_short_size > 0) {
@@ -515,11 +553,12 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
     HIP_OK(hipSetDevice(ctx->device));
     phase(0);
 
-    LaunchPlan pre_all, pre2_all, pass1_all, main_all;
+    LaunchPlan          pre_all, pre2_all, pass1_all, main_all;
+    std::vector<RotJob> rot;
     size_t     scratch_bytes = 0;
     for (int i = 0; i < n; i++)
         plan_image(descs[i], src_base, params[i], o, (uint8_t*)out_dev + (size_t)i * o.item_stride,
-                   is_mask, pre_all, pre2_all, pass1_all, main_all, scratch_bytes);
+                   is_mask, rot, pre_all, pre2_all, pass1_all, main_all, scratch_bytes);
 
     phase(1);
     // one launch per (resize mode, photometric) group: the kernels are specialised on both
@@ -534,7 +573,10 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
     for (const AugJob& J : pass1_all.jobs) pass1[J.mode].jobs.push_back(J);
     for (const AugJob& J : main_all.jobs) main[J.mode * 2 + (J.photo ? 1 : 0)].jobs.push_back(J);
     const size_t     lut_bytes = 4096;
-    size_t           blob      = lut_bytes;
+    const size_t     rot_off   = lut_bytes;
+    size_t           blob      = rot_off + rot.size() * sizeof(RotJob);
+    int              rot_max_px = 0;
+    for (const RotJob& R : rot) rot_max_px = std::max(rot_max_px, R.w * R.h);
     std::vector<int> slot_tiles(pass1_all.jobs.size(), 0);
     int              partial_stride = 1;
     for (auto* v : {&pre, &pre2, &pass1, &main})
@@ -572,6 +614,8 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
         s.partials = (uint32_t*)p;
     }
     build_lut(o, (float*)s.host);
+    for (RotJob& R : rot) R.out_ptr += (uint64_t)s.scratch;
+    if (!rot.empty()) std::memcpy(s.host + rot_off, rot.data(), rot.size() * sizeof(RotJob));
     for (auto* v : {&pre, &pre2, &pass1, &main})
         for (LaunchPlan& P : *v) {
             for (AugJob& J : P.jobs) { // relocate scratch references
@@ -610,6 +654,8 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
         return a;
     };
     const size_t oelem = o.dtype == AEON_DTYPE_F32 ? 4 : 1;
+    if (!rot.empty())
+        HIP_OK(launch_rotate((const RotJob*)(s.dev + rot_off), (int)rot.size(), rot_max_px, stream));
     for (auto* v : {&pre, &pre2})
         for (LaunchPlan& P : *v)
             if (!P.jobs.empty()) timed_launch(ctx, KM_RAW, P, args(P), stream, launch_bytes(P, KM_RAW, 1));

@@ -101,6 +101,7 @@ def lib():
         L.orc_batch_augment.argtypes = [ctypes.c_int, P(ctypes.c_void_p), P(ctypes.c_int),
                                         P(ctypes.c_int), P(Params), P(LoadConfig), ctypes.c_void_p,
                                         ctypes.c_size_t, ctypes.c_int]
+        L.orc_rotate.argtypes = [ctypes.c_void_p] + [ctypes.c_int] * 6 + [ctypes.c_void_p]
         L.orc_transpose.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int]
         L.orc_last_error.restype = ctypes.c_char_p
         _lib = L
@@ -266,4 +267,14 @@ def transpose(src, rows, cols, element_size):
     out = np.empty_like(src)
     _check(lib().orc_transpose(out.ctypes.data, src.ctypes.data, ctypes.c_int64(rows), ctypes.c_int64(cols),
                                element_size))
+    return out
+
+
+def rotate(src, angle, interpolate=True):
+    """image::rotate: warpAffine about (cols/2, rows/2), linear or nearest, zero border."""
+    src = np.ascontiguousarray(src, dtype=np.uint8)
+    h, w = src.shape[:2]
+    cn = 1 if src.ndim == 2 else src.shape[2]
+    out = np.empty_like(src)
+    _check(lib().orc_rotate(src.ctypes.data, w, h, cn, w * cn, angle, int(interpolate), out.ctypes.data))
     return out

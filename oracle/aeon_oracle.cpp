@@ -540,11 +540,101 @@ void flip_h(Img& m)
     }
 }
 
+// image::rotate (src/image.cpp:53-75): cv::getRotationMatrix2D(Point2i(cols/2, rows/2), angle,
+// 1.0) and cv::warpAffine(..., input.size(), INTER_LINEAR | INTER_NEAREST, BORDER_CONSTANT, 0),
+// restated from OpenCV 2.4 imgwarp.cpp:
+//  * the forward matrix is inverted in double (warpAffine without WARP_INVERSE_MAP);
+//  * per output pixel, with AB_BITS = 10, INTER_BITS = 5:
+//      X = cvRound((M1*y + M2)*1024) + round_delta + cvRound(M0*x*1024)   (likewise Y)
+//    round_delta = 512 (nearest) or 16 (linear); nearest takes (X >> 10, Y >> 10), linear takes
+//    (X >> 5 >> 5, Y >> 5 >> 5) plus the 5-bit fractions (X & 31, Y & 31);
+//  * remapBilinear: 15-bit weights from the 32x32 table initInterTab2D builds -- (32-fy)(32-fx)*32
+//    etc.; the (0,0) entry saturates to 32767 and its correction lands on the fourth tap:
+//    {32767, 0, 0, 1} -- then (sum + 2^14) >> 15; taps outside the image read the border 0.
+void rotation_inverse_map(int w, int h, int angle, double M[6])
+{
+    const float  cx = (float)(w / 2), cy = (float)(h / 2); // Point2i -> Point2f
+    const double a  = (double)angle * (3.1415926535897932384626433832795 / 180);
+    const double alpha = std::cos(a) * 1.0, beta = std::sin(a) * 1.0;
+    M[0] = alpha;
+    M[1] = beta;
+    M[2] = (1 - alpha) * cx - beta * cy;
+    M[3] = -beta;
+    M[4] = alpha;
+    M[5] = beta * cx + (1 - alpha) * cy;
+    double D = M[0] * M[4] - M[1] * M[3];
+    D        = D != 0 ? 1. / D : 0;
+    const double A11 = M[4] * D, A22 = M[0] * D;
+    M[0] = A11;
+    M[1] *= -D;
+    M[3] *= -D;
+    M[4] = A22;
+    const double b1 = -M[0] * M[2] - M[1] * M[5];
+    const double b2 = -M[3] * M[2] - M[4] * M[5];
+    M[2] = b1;
+    M[5] = b2;
+}
+
+static int sat_short(int v) { return std::min(std::max(v, -32768), 32767); }
+
+Img rotate(const Img& in, int angle, bool interpolate)
+{
+    Img out = Img::alloc(in.w, in.h, in.cn);
+    if (angle == 0) {
+        for (int y = 0; y < in.h; y++) std::memcpy(out.row(y), in.row(y), (size_t)in.w * in.cn);
+        return out;
+    }
+    double M[6];
+    rotation_inverse_map(in.w, in.h, angle, M);
+    const int        W = in.w, H = in.h, cn = in.cn;
+    std::vector<int> ad(W), bd(W);
+    for (int x = 0; x < W; x++) {
+        ad[x] = cv_round(M[0] * x * 1024);
+        bd[x] = cv_round(M[3] * x * 1024);
+    }
+    const int rdelta = interpolate ? 1024 / 32 / 2 : 1024 / 2;
+    auto      tap    = [&](int xx, int yy, int c) -> int {
+        return (xx >= 0 && xx < W && yy >= 0 && yy < H) ? in.row(yy)[xx * cn + c] : 0;
+    };
+    for (int y = 0; y < H; y++) {
+        const int X0 = cv_round((M[1] * y + M[2]) * 1024) + rdelta;
+        const int Y0 = cv_round((M[4] * y + M[5]) * 1024) + rdelta;
+        uint8_t*  d  = out.row(y);
+        for (int x = 0; x < W; x++) {
+            if (!interpolate) {
+                const int sx = sat_short((X0 + ad[x]) >> 10), sy = sat_short((Y0 + bd[x]) >> 10);
+                for (int c = 0; c < cn; c++) d[x * cn + c] = (uint8_t)tap(sx, sy, c);
+                continue;
+            }
+            const int X = (X0 + ad[x]) >> 5, Y = (Y0 + bd[x]) >> 5;
+            const int sx = sat_short(X >> 5), sy = sat_short(Y >> 5);
+            const int fx = X & 31, fy = Y & 31;
+            int       w[4];
+            if (fx == 0 && fy == 0) {
+                w[0] = 32767, w[1] = 0, w[2] = 0, w[3] = 1;
+            } else {
+                w[0] = (32 - fy) * (32 - fx) * 32, w[1] = (32 - fy) * fx * 32;
+                w[2] = fy * (32 - fx) * 32, w[3] = fy * fx * 32;
+            }
+            for (int c = 0; c < cn; c++) {
+                const int v = tap(sx, sy, c) * w[0] + tap(sx + 1, sy, c) * w[1] + tap(sx, sy + 1, c) * w[2] +
+                              tap(sx + 1, sy + 1, c) * w[3];
+                d[x * cn + c] = (uint8_t)std::min(std::max((v + (1 << 14)) >> 15, 0), 255);
+            }
+        }
+    }
+    return out;
+}
+
 // image::transformer::transform_single_image (src/etl_image.cpp:146-202)
 Img transform_single_image(const Img& src, const orc_params& p)
 {
-    if (p.angle != 0) throw std::invalid_argument("oracle: rotation not restated yet");
+    Img rot;
     Img base = Img::view(src.data, src.w, src.h, src.cn, src.stride);
+    if (p.angle != 0) { // image::rotate, interpolated (etl_image.cpp:150-151)
+        rot  = rotate(base, p.angle, true);
+        base = Img::view(rot.data, rot.w, rot.h, rot.cn, rot.stride);
+    }
     Img rs;
     if (p.resize_short_size != 0) {
         int rw, rh;
@@ -621,12 +711,17 @@ void load_image(const Img& img, const orc_load_config& lc, void* out)
 // pixel_mask::transformer::transform (src/etl_pixel_mask.cpp:65-92)
 Img transform_mask(const Img& src, const orc_params& p)
 {
-    if (p.angle != 0) throw std::invalid_argument("oracle: rotation not restated yet");
+    Img rot;
+    Img base = Img::view(src.data, src.w, src.h, src.cn, src.stride);
+    if (p.angle != 0) { // image::rotate(..., interpolate=false, border 0) (etl_pixel_mask.cpp:72-74)
+        rot  = rotate(base, p.angle, false);
+        base = Img::view(rot.data, rot.w, rot.h, rot.cn, rot.stride);
+    }
     if (p.crop_x < 0 || p.crop_y < 0 || p.crop_w <= 0 || p.crop_h <= 0 ||
-        p.crop_x + p.crop_w > src.w || p.crop_y + p.crop_h > src.h)
+        p.crop_x + p.crop_w > base.w || p.crop_y + p.crop_h > base.h)
         throw std::invalid_argument("cropbox outside mask");
-    Img crop = Img::view(src.row(p.crop_y) + (size_t)p.crop_x * src.cn, p.crop_w, p.crop_h,
-                         src.cn, src.stride);
+    Img crop = Img::view(base.row(p.crop_y) + (size_t)p.crop_x * base.cn, p.crop_w, p.crop_h,
+                         base.cn, base.stride);
     Img out = Img::alloc(p.out_w, p.out_h, src.cn);
     resize_any(crop, out, 1);
     if (p.flip) flip_h(out);
@@ -753,6 +848,14 @@ float orc_standardize_value(int x, double mean, double stddev)
 
 // CPU baseline: aeon's thread_pool policy -- N workers pulling record indices from one
 // atomic counter (src/thread_pool.hpp:155-162), each running transform + load per record.
+int orc_rotate(const uint8_t* src, int w, int h, int cn, int stride, int angle, int interpolate, uint8_t* out)
+{
+    return guarded([&] {
+        Img o = rotate(Img::view(src, w, h, cn, stride), angle, interpolate != 0);
+        std::memcpy(out, o.data, (size_t)w * h * cn);
+    });
+}
+
 double orc_batch_augment(int n, const uint8_t* const* srcs, const int* widths, const int* heights,
                          const orc_params* params, const orc_load_config* lc, void* out,
                          size_t item_bytes, int threads)

@@ -91,6 +91,10 @@ float orc_standardize_value(int x, double mean, double stddev);
 /* whole-record path (transform + load) over a batch on a thread pool -- CPU baseline.
  * srcs[i] = HWC BGR uint8 image i (widths/heights per image), params[i] its params,
  * out = batch of item_bytes slots.  Returns elapsed seconds. */
+/* image::rotate (src/image.cpp:53-75) over OpenCV 2.4 warpAffine: interpolate = INTER_LINEAR,
+ * else INTER_NEAREST; BORDER_CONSTANT 0; output w x h x cn packed. */
+int orc_rotate(const uint8_t* src, int w, int h, int cn, int stride, int angle, int interpolate, uint8_t* out);
+
 /* transpose_regular (src/buffer_batch.cpp:186-200) as transpose_buf dispatches it (:202-244):
  * dest[c * rows + r] = src[r * cols + c], element_size 1, 2, 4 or 8.  Returns -1 otherwise. */
 int orc_transpose(void* dest, const void* src, int64_t rows, int64_t cols, int element_size);

@@ -105,6 +105,36 @@ def test_c5_image_and_mask(ctx):
         assert set(np.unique(m)) <= {0, 255}
 
 
+# ---- image::rotate (angle != 0) --------------------------------------------------------------
+@pytest.mark.parametrize("aug_name", ["C1", "C2", "C3"])
+def test_rotation_configs(ctx, aug_name):
+    # "angle": [-20, 20] as aeon's own image test config (test/test_image.cpp:197)
+    aug = dict({"C1": C.C1_AUG, "C2": C.C2_AUG, "C3": C.C3_AUG}[aug_name], angle=[-20, 20])
+    imgs = _synthetic(16, ragged=True)
+    params = H.draw_params(aug, [(im.shape[1], im.shape[0]) for im in imgs], 224, 224, seed=21)
+    assert any(p.angle != 0 for p in params)
+    out = A.out_desc(**MEAN_OUT)
+    _assert_same(H.hip_records(ctx, imgs, params, out), H.oracle_records(imgs, params, out), aug_name + " rot")
+
+
+@pytest.mark.parametrize("angle", [45, -90, 180, 7, 359])
+def test_rotation_image_and_mask_fixed_angles(ctx, angle):
+    rng = np.random.default_rng(angle & 0xff)
+    w, h = int(rng.integers(200, 400)), int(rng.integers(200, 400))
+    img = A.synthetic_image(angle + 7, w, h, 3)
+    msk = np.zeros((h, w), np.uint8)
+    msk[h // 4:h // 2, w // 5:w // 2] = 3
+    msk[h // 2:, w // 3:] = 9
+    p = A.aug_params(crop_x=w // 8, crop_y=h // 8, crop_w=w - w // 4, crop_h=h - h // 4, out_w=224, out_h=224,
+                     angle=angle, flip=1)
+    iout = C.out_desc_for(C.IMAGE_224, C.C2_AUG)
+    mout = A.out_desc(channels=1, dtype="uint8", item_stride=224 * 224)
+    _assert_same(H.hip_records(ctx, [img], [p], iout), H.oracle_records([img], [p], iout), f"rot {angle}")
+    (m,) = H.hip_records(ctx, [msk], [p], mout, mask=True)
+    _assert_same([m], H.oracle_records([msk], [p], mout, mask=True), f"mask rot {angle}")
+    assert set(np.unique(m)) <= {0, 3, 9}  # test/test_pixel_mask.cpp:130-155 invariant
+
+
 EDGE_CASES = [
     # (name, src (w,h), params kwargs, out kwargs)
     ("upscale_tiny", (7, 5), dict(crop_x=0, crop_y=0, crop_w=7, crop_h=5, out_w=224, out_h=224), {}),
@@ -177,7 +207,7 @@ def test_errors(ctx):
     img = A.synthetic_image(0, 64, 64)
     out = A.out_desc(**MEAN_OUT)
     with pytest.raises(A.AeonHipError) as e:
-        H.hip_records(ctx, [img], [A.aug_params(crop_w=64, crop_h=64, out_w=224, out_h=224, angle=10)], out)
+        H.hip_records(ctx, [img], [A.aug_params(crop_w=64, crop_h=64, out_w=224, out_h=224, interp=2)], out)
     assert e.value.code == A.AEON_HIP_EUNSUPPORTED
     with pytest.raises(A.AeonHipError) as e:
         H.hip_records(ctx, [img], [A.aug_params(crop_x=10, crop_w=64, crop_h=64, out_w=224, out_h=224)], out)

@@ -137,3 +137,24 @@ def test_transpose_restatement(oracle, esize, dtype):
     assert np.array_equal(out, m.T)
     with pytest.raises(RuntimeError, match="unsupported datatype"):
         oracle.transpose(np.zeros(15, np.uint8), 5, 1, 3)
+
+
+# ---- image::rotate (src/image.cpp:53-75; OpenCV 2.4 warpAffine) -----------------------------
+@pytest.mark.parametrize("interp", [True, False])
+def test_rotate_exact_quarter_turns(oracle, interp):
+    # about the integer centre of an odd square, 180 degrees is an exact double flip and +90 is
+    # OpenCV's documented counter-clockwise quarter turn
+    img = (np.arange(9 * 9 * 3) % 251).astype(np.uint8).reshape(9, 9, 3)
+    assert np.array_equal(oracle.rotate(img, 180, interp), img[::-1, ::-1])
+    assert np.array_equal(oracle.rotate(img, 90, interp), np.rot90(img, 1))
+    assert np.array_equal(oracle.rotate(img, 0, interp), img)
+
+
+def test_rotate_mask_nearest_keeps_classes(oracle):
+    # test/test_pixel_mask.cpp:130-155 (pixel_mask rotate 45): nearest rotation invents no values
+    m = np.zeros((64, 80), np.uint8)
+    m[10:30, 5:40] = 7
+    m[35:60, 20:70] = 200
+    r = oracle.rotate(m, 45, False)
+    assert set(np.unique(r)) <= {0, 7, 200}
+    assert len(np.unique(oracle.rotate(m, 45, True))) > 3  # bilinear blends edges
