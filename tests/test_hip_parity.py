@@ -121,7 +121,7 @@ def test_rotation_configs(ctx, aug_name):
 def test_rotation_image_and_mask_fixed_angles(ctx, angle):
     rng = np.random.default_rng(angle & 0xff)
     w, h = int(rng.integers(200, 400)), int(rng.integers(200, 400))
-    img = A.synthetic_image(angle + 7, w, h, 3)
+    img = A.synthetic_image(abs(angle) + 7, w, h, 3)
     msk = np.zeros((h, w), np.uint8)
     msk[h // 4:h // 2, w // 5:w // 2] = 3
     msk[h // 2:, w // 3:] = 9
