@@ -386,7 +386,9 @@ enum OutForm : int { OF_F32_CHW_VEC = 0, OF_GENERIC = 1 };
 // only, HWC uint8: the resize_short pre-pass).  RM: ResizeMode of every job in the launch.
 // PHOTO: the launch's jobs carry photometric work.  OF: output form (OF_F32_CHW_VEC = float32
 // CHW planes, win_w % 4 == 0, 16-byte aligned items: the ImageNet configuration).
-template <int KM, int RM, bool PHOTO, int OF>
+// TAIL: some LINEAR job of the launch has OpenCV scalar-tail columns (3*dst_w not covered by the
+// SIMD loops); kept out of the common kernels, whose registers it would otherwise inflate.
+template <int KM, int RM, bool PHOTO, int OF, bool TAIL>
 __global__ __launch_bounds__(kBlockMax, AEON_HIP_MIN_WAVES) void augment_tiles(LaunchArgs a)
 {
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -500,7 +502,7 @@ __global__ __launch_bounds__(kBlockMax, AEON_HIP_MIN_WAVES) void augment_tiles(L
     const int  plane = win_w * J.win_h;
     const auto orsrc = __builtin_amdgcn_make_buffer_rsrc((void*)J.out_ptr, (short)0,
                                                          plane * cn * elem, 0x00020000);
-    const bool tail  = RM == RESIZE_LINEAR && J.xv < J.dst_w * cn; // OpenCV scalar row tail
+    const bool tail  = TAIL && RM == RESIZE_LINEAR && J.xv < J.dst_w * cn; // OpenCV scalar row tail
     const int  wx0   = J.win_x;
     const int  xv    = J.xv;
     const int  flip  = J.flip;
@@ -538,7 +540,7 @@ __global__ __launch_bounds__(kBlockMax, AEON_HIP_MIN_WAVES) void augment_tiles(L
                 const int2 xtt = xt[x];
                 col[k]         = xtt.x * 4; // byte offset in a staged row
                 wxk[k]         = (uint32_t)xtt.y;
-                if (RM == RESIZE_LINEAR && tail && (wx0 + x) * cn + 2 >= xv) tmask |= 1 << k;
+                if (TAIL && RM == RESIZE_LINEAR && tail && (wx0 + x) * cn + 2 >= xv) tmask |= 1 << k;
             }
             for (int ry = lph; ry < nrows; ry += nph) {
                 const int4 ytr = yt[ry];
@@ -546,7 +548,7 @@ __global__ __launch_bounds__(kBlockMax, AEON_HIP_MIN_WAVES) void augment_tiles(L
                 int        val[4][3];
 #pragma unroll
                 for (int k = 0; k < 4; k++) resize_px<RM, SC>(ytr, col[k], wxk[k], val[k]);
-                if (RM == RESIZE_LINEAR && tmask) {
+                if (TAIL && RM == RESIZE_LINEAR && tmask) {
 #pragma unroll
                     for (int k = 0; k < 4; k++)
                         if (tmask & (1 << k)) {
@@ -579,6 +581,7 @@ __global__ __launch_bounds__(kBlockMax, AEON_HIP_MIN_WAVES) void augment_tiles(L
                             r = sat_u8(sat_u8(rnd((float)r * la + 0.f)) + J.light_add[2]);
                         }
                         val[k][0] = b, val[k][1] = g, val[k][2] = r;
+                        __builtin_amdgcn_sched_barrier(0); // one pixel's chain live at a time
                     }
                 }
                 if ((KM == KM_RAW || KM == KM_STATS) && cn == 3 && nk == 4) {
@@ -615,6 +618,9 @@ __global__ __launch_bounds__(kBlockMax, AEON_HIP_MIN_WAVES) void augment_tiles(L
                         const int oc = bgr ? 2 - c : c;
                         store_f32x4(orsrc, (oc * plane + idx) * 4, lut_of(c, val[0][c]), lut_of(c, val[1][c]),
                                     lut_of(c, val[2][c]), lut_of(c, val[3][c]));
+                        // one channel's four LUT reads in flight at a time: hoisting all twelve
+                        // costs ~20 VGPRs (two waves per SIMD) for no measurable overlap
+                        __builtin_amdgcn_sched_barrier(0);
                     }
                     continue;
                 }
@@ -676,44 +682,46 @@ __global__ __launch_bounds__(kBlockMax, AEON_HIP_MIN_WAVES) void augment_tiles(L
 // ---- host-side launch helpers (stage.cpp) ----------------------------------------------------
 typedef void (*KernelFn)(LaunchArgs);
 
-template <int KM, int RM>
+template <int KM, int RM, bool TAIL>
 KernelFn pick_form(bool photo, int of)
 {
     if constexpr (RM == RESIZE_AREA2X) {
         // the planner splits 2x-area records with photometric stages into a resize-only pre-pass
         // and a copy pass, so these forms are never instantiated
         if (photo) return nullptr;
-        return of == OF_F32_CHW_VEC ? augment_tiles<KM, RM, false, OF_F32_CHW_VEC>
-                                    : augment_tiles<KM, RM, false, OF_GENERIC>;
+        return of == OF_F32_CHW_VEC ? augment_tiles<KM, RM, false, OF_F32_CHW_VEC, false>
+                                    : augment_tiles<KM, RM, false, OF_GENERIC, false>;
     } else {
         if (of == OF_F32_CHW_VEC)
-            return photo ? augment_tiles<KM, RM, true, OF_F32_CHW_VEC> : augment_tiles<KM, RM, false, OF_F32_CHW_VEC>;
-        return photo ? augment_tiles<KM, RM, true, OF_GENERIC> : augment_tiles<KM, RM, false, OF_GENERIC>;
+            return photo ? augment_tiles<KM, RM, true, OF_F32_CHW_VEC, TAIL>
+                         : augment_tiles<KM, RM, false, OF_F32_CHW_VEC, TAIL>;
+        return photo ? augment_tiles<KM, RM, true, OF_GENERIC, TAIL> : augment_tiles<KM, RM, false, OF_GENERIC, TAIL>;
     }
 }
 
 template <int KM>
-KernelFn pick_rm(int rm, bool photo, int of)
+KernelFn pick_rm(int rm, bool tail, bool photo, int of)
 {
     switch (rm) {
-    case RESIZE_LINEAR: return pick_form<KM, RESIZE_LINEAR>(photo, of);
-    case RESIZE_AREA2X: return pick_form<KM, RESIZE_AREA2X>(photo, of);
-    case RESIZE_NEAREST: return pick_form<KM, RESIZE_NEAREST>(photo, of);
-    default: return pick_form<KM, RESIZE_COPY>(photo, of);
+    case RESIZE_LINEAR:
+        return tail ? pick_form<KM, RESIZE_LINEAR, true>(photo, of) : pick_form<KM, RESIZE_LINEAR, false>(photo, of);
+    case RESIZE_AREA2X: return pick_form<KM, RESIZE_AREA2X, false>(photo, of);
+    case RESIZE_NEAREST: return pick_form<KM, RESIZE_NEAREST, false>(photo, of);
+    default: return pick_form<KM, RESIZE_COPY, false>(photo, of);
     }
 }
 
-KernelFn pick_kernel(int km, int rm, bool photo, int of)
+KernelFn pick_kernel(int km, int rm, bool tail, bool photo, int of)
 {
-    if (km == KM_FINAL) return pick_rm<KM_FINAL>(rm, photo, of);
-    if (km == KM_STATS) return pick_rm<KM_STATS>(rm, true, OF_GENERIC);
-    return pick_rm<KM_RAW>(rm, false, OF_GENERIC);
+    if (km == KM_FINAL) return pick_rm<KM_FINAL>(rm, tail, photo, of);
+    if (km == KM_STATS) return pick_rm<KM_STATS>(rm, tail, true, OF_GENERIC);
+    return pick_rm<KM_RAW>(rm, tail, false, OF_GENERIC);
 }
 
-hipError_t launch_tiles(int km, int rm, bool photo, const LaunchArgs& a, int n_jobs, hipStream_t stream)
+hipError_t launch_tiles(int km, int rm, bool tail, bool photo, const LaunchArgs& a, int n_jobs, hipStream_t stream)
 {
     const int      of = (a.out_dtype == OUT_F32 && a.channel_major && a.vec_ok) ? OF_F32_CHW_VEC : OF_GENERIC;
-    const KernelFn fn = pick_kernel(km, rm, photo, of);
+    const KernelFn fn = pick_kernel(km, rm, tail, photo, of);
     if (!fn) return hipErrorInvalidDeviceFunction;
     dim3 grid(a.max_tiles, n_jobs), block(a.threads);
     hipLaunchKernelGGL(fn, grid, block, a.lds_bytes, stream, a);
@@ -724,9 +732,9 @@ hipError_t set_kernel_lds_limit(int bytes)
 {
     for (int km = 0; km < 3; km++)
         for (int rm = 0; rm < 4; rm++)
-            for (int ph = 0; ph < 2; ph++)
+            for (int ph = 0; ph < 4; ph++)
                 for (int of = 0; of < 2; of++) {
-                    const KernelFn fn = pick_kernel(km, rm, ph != 0, of);
+                    const KernelFn fn = pick_kernel(km, rm, (ph & 2) != 0, (ph & 1) != 0, of);
                     if (!fn) continue;
                     hipError_t e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
                     if (e != hipSuccess) return e;

@@ -21,7 +21,7 @@
 #include "param_factory.hpp"
 
 namespace aeon_hip {
-hipError_t launch_tiles(int km, int rm, bool photo, const LaunchArgs& a, int n_jobs, hipStream_t stream);
+hipError_t launch_tiles(int km, int rm, bool tail, bool photo, const LaunchArgs& a, int n_jobs, hipStream_t stream);
 hipError_t set_kernel_lds_limit(int bytes);
 hipError_t launch_transpose(const void* src, void* dst, int64_t rows, int64_t cols, int element_size,
                             hipStream_t stream);
@@ -168,6 +168,7 @@ int stage_rows_for(const AugJob& J, int tr)
 struct LaunchPlan {
     int                 rm = RESIZE_LINEAR;
     bool                photo = false;
+    bool                tail  = false; // LINEAR jobs with OpenCV scalar-tail columns
     size_t              blob_off = 0;     // byte offset of this group's jobs in the slot blob
     size_t              partial_off = 0;  // uint32 offset of this group's contrast partials
     std::vector<AugJob> jobs;
@@ -516,7 +517,7 @@ void timed_launch(aeon_hip_ctx* ctx, int mode, const LaunchPlan& P, const Launch
         t.bytes = bytes;
         HIP_OK(hipEventRecord(t.start, stream));
     }
-    HIP_OK(launch_tiles(mode, P.rm, P.photo, a, (int)P.jobs.size(), stream));
+    HIP_OK(launch_tiles(mode, P.rm, P.tail, P.photo, a, (int)P.jobs.size(), stream));
     if (ctx->timing) {
         HIP_OK(hipEventRecord(t.stop, stream));
         ctx->timers.push_back(t);
@@ -562,16 +563,20 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
 
     phase(1);
     // one launch per (resize mode, photometric) group: the kernels are specialised on both
-    std::vector<LaunchPlan> pre(4), pre2(4), pass1(4), main(8);
-    for (int rm = 0; rm < 4; rm++) {
-        pre[rm].rm = pre2[rm].rm = pass1[rm].rm = rm;
-        pass1[rm].photo = true;
-        for (int ph = 0; ph < 2; ph++) main[rm * 2 + ph].rm = rm, main[rm * 2 + ph].photo = ph != 0;
+    // one launch per (resize mode, scalar tail, photometric) group: the kernels are specialised
+    // on all three
+    auto has_tail = [](const AugJob& J) { return J.mode == RESIZE_LINEAR && J.xv < J.dst_w * J.cn; };
+    std::vector<LaunchPlan> pre(8), pre2(8), pass1(8), main(16);
+    for (int g = 0; g < 8; g++) {
+        pre[g].rm = pre2[g].rm = pass1[g].rm = g >> 1;
+        pre[g].tail = pre2[g].tail = pass1[g].tail = (g & 1) != 0;
+        pass1[g].photo = true;
     }
-    for (const AugJob& J : pre_all.jobs) pre[J.mode].jobs.push_back(J);
-    for (const AugJob& J : pre2_all.jobs) pre2[J.mode].jobs.push_back(J);
-    for (const AugJob& J : pass1_all.jobs) pass1[J.mode].jobs.push_back(J);
-    for (const AugJob& J : main_all.jobs) main[J.mode * 2 + (J.photo ? 1 : 0)].jobs.push_back(J);
+    for (int g = 0; g < 16; g++) main[g].rm = g >> 2, main[g].tail = (g & 2) != 0, main[g].photo = (g & 1) != 0;
+    for (const AugJob& J : pre_all.jobs) pre[J.mode * 2 + has_tail(J)].jobs.push_back(J);
+    for (const AugJob& J : pre2_all.jobs) pre2[J.mode * 2 + has_tail(J)].jobs.push_back(J);
+    for (const AugJob& J : pass1_all.jobs) pass1[J.mode * 2 + has_tail(J)].jobs.push_back(J);
+    for (const AugJob& J : main_all.jobs) main[J.mode * 4 + has_tail(J) * 2 + (J.photo ? 1 : 0)].jobs.push_back(J);
     const size_t     lut_bytes = 4096;
     const size_t     rot_off   = lut_bytes;
     size_t           blob      = rot_off + rot.size() * sizeof(RotJob);
