@@ -101,7 +101,8 @@ def lib():
         for fn in (L.aeon_hip_augment_batch, L.aeon_hip_mask_batch):
             fn.argtypes = [vp, ctypes.c_int, P(ImgDesc), vp, P(AugParams), P(OutDesc), vp, vp]
         L.aeon_hip_synchronize.argtypes = [vp, vp]
-        L.aeon_hip_transpose_batch.argtypes = [vp, vp, vp, ctypes.c_int64, ctypes.c_int64, ctypes.c_int, vp]
+        if hasattr(L, "aeon_hip_transpose_batch"):  # absent only in older tuning-variant builds
+            L.aeon_hip_transpose_batch.argtypes = [vp, vp, vp, ctypes.c_int64, ctypes.c_int64, ctypes.c_int, vp]
         L.aeon_hip_set_timing.argtypes = [vp, ctypes.c_int]
         L.aeon_hip_kernel_times.argtypes = [vp, P(ctypes.c_double), P(ctypes.c_double), P(ctypes.c_long)]
         L.aeon_param_factory_create.argtypes = [ctypes.c_char_p, P(vp)]
