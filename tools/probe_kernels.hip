@@ -5,6 +5,10 @@
 //   1: write-only, persistent grid-stride over tiles
 //   2: load the tile's u8 source footprint (stage-like, 16 B per lane) then write
 //   3: like 2, persistent
+//   4: like 2, but the tile's source address comes from a 256-byte per-item descriptor loaded
+//      first (a dependent round trip, as augment_tiles' job load)
+//   5: like 2, plus `work` dependent VALU iterations per lane between the loads and the stores
+//   6: 4 + 5
 // Build: hipcc -O3 --offload-arch=gfx950 -shared -fPIC tools/probe_kernels.hip -o tools/libprobe.so
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -15,25 +19,33 @@ constexpr int W = 224, H = 224;
 
 template <int MODE>
 __global__ __launch_bounds__(256) void probe(const uint8_t* src, float* out, int n_items, int rows,
-                                               int src_item_bytes, int src_tile_bytes, int grid_tiles)
+                                               int src_item_bytes, int src_tile_bytes, int grid_tiles, int work,
+                                               const uint64_t* desc)
 {
     const int tiles_per_item = (H + rows - 1) / rows;
     const int total          = n_items * tiles_per_item;
     const bool persistent    = MODE == 1 || MODE == 3;
     const bool load          = MODE >= 2;
+    const bool dep           = MODE == 4 || MODE == 6;
+    const bool valu          = MODE == 5 || MODE == 6;
     __shared__ u32x4 lds[1024];
     for (int t = blockIdx.x; t < total; t += persistent ? gridDim.x : total) {
         const int item = t / tiles_per_item, tile = t - item * tiles_per_item;
         uint32_t  acc  = 0;
         if (load) {
-            const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)(src + (size_t)item * src_item_bytes), 0,
-                                                              src_item_bytes, 0x00020000);
+            const uint8_t* base = dep ? (const uint8_t*)desc[item * 32] : src + (size_t)item * src_item_bytes;
+            const auto     rs   = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, src_item_bytes, 0x00020000);
             for (int i = threadIdx.x; i * 16 < src_tile_bytes; i += 256) {
                 u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, tile * src_tile_bytes / 2 + i * 16, 0, 0);
                 lds[i & 1023] = v;
             }
             __syncthreads();
             acc = lds[threadIdx.x].x & 1;
+        }
+        if (valu) {
+            uint32_t x = acc + threadIdx.x;
+            for (int i = 0; i < work; i++) x = (x ^ (x >> 3)) + 0x9e3779b9u; // 3 full-rate VALU ops
+            acc = x & 1;
         }
         const int  plane = W * H;
         const auto orsrc = __builtin_amdgcn_make_buffer_rsrc((void*)(out + (size_t)item * 3 * plane), 0,
@@ -53,18 +65,21 @@ __global__ __launch_bounds__(256) void probe(const uint8_t* src, float* out, int
 }
 
 extern "C" int probe_launch(int mode, const void* src, void* out, int n_items, int rows, int src_item_bytes,
-                            int src_tile_bytes, int grid, void* stream)
+                            int src_tile_bytes, int grid, int work, const void* desc, void* stream)
 {
     const int tiles = n_items * ((H + rows - 1) / rows);
     dim3      g(mode == 1 || mode == 3 ? grid : tiles);
     auto      s = (hipStream_t)stream;
 #define L(M) hipLaunchKernelGGL(probe<M>, g, dim3(256), 0, s, (const uint8_t*)src, (float*)out, n_items, rows, \
-                                src_item_bytes, src_tile_bytes, grid)
+                                src_item_bytes, src_tile_bytes, grid, work, (const uint64_t*)desc)
     switch (mode) {
     case 0: L(0); break;
     case 1: L(1); break;
     case 2: L(2); break;
-    default: L(3); break;
+    case 3: L(3); break;
+    case 4: L(4); break;
+    case 5: L(5); break;
+    default: L(6); break;
     }
     return (int)hipGetLastError();
 }
