@@ -83,3 +83,19 @@ extern "C" int probe_launch(int mode, const void* src, void* out, int n_items, i
     }
     return (int)hipGetLastError();
 }
+
+// Unaligned buffer loads: lane i reads 16 bytes at byte offset i (returns the bytes as loaded).
+__global__ void probe_unaligned_k(const uint8_t* src, uint32_t* out, int n_bytes)
+{
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)src, 0, n_bytes, 0x00020000);
+    const int  i  = threadIdx.x;
+    u32x4      v  = __builtin_amdgcn_raw_buffer_load_b128(rs, i, 0, 0);
+    out[i * 4 + 0] = v.x, out[i * 4 + 1] = v.y, out[i * 4 + 2] = v.z, out[i * 4 + 3] = v.w;
+}
+
+extern "C" int probe_unaligned(const void* src, void* out, int n_bytes, void* stream)
+{
+    hipLaunchKernelGGL(probe_unaligned_k, dim3(1), dim3(64), 0, (hipStream_t)stream, (const uint8_t*)src,
+                       (uint32_t*)out, n_bytes);
+    return (int)hipGetLastError();
+}
