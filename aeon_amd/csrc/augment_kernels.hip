@@ -176,57 +176,82 @@ __device__ __forceinline__ void hue_apply(const int32_t* sdiv, const int32_t* hd
 }
 
 // ---- source staging ----------------------------------------------------------------------------
-// A band stages resize-source rows [v_lo, v_lo+nr) x cols [u_lo, u_lo+nc) into LDS as one
-// 32-bit word per pixel: four pixels per lane from one 16-byte buffer load (alignbyte re-packs
-// the 3-byte pixels).  Loads for band b+1 are issued into registers (kPrefetch per lane) before
-// band b is consumed and written to LDS after it, so their HBM latency hides under the compute.
-constexpr int kPrefetch = 3;
+// A band stages resize-source rows [v_lo, v_lo+nr) x cols [u_lo, u_lo+nc) into LDS as one 32-bit
+// word per pixel.  Items are 4-pixel groups; lane t takes items t, t+nt, ... in batches of
+// kPrefetch whose loads are all in flight before the first is unpacked.  Each item is ONE load
+// at its exact byte offset (12 bytes for 3 channels, 4 for 1 -- dword-unaligned buffer loads
+// return the exact bytes on gfx950), unpacked with two v_perm, and written with one ds_write_b128.
+// The walk over items keeps byte offsets incrementally: no 32-bit multiplies per item.
+constexpr int kPrefetch = 4;
 
 struct StageGeom {
     int v_lo, nr, u_lo, nc, groups;
 };
 
-struct Prefetch {
-    u32x4    d[kPrefetch];
-    uint32_t meta[kPrefetch]; // row j (12 b) | group g (14 b) | byte shift (2 b) | fast (1 b) | valid
+struct Walk { // lane-private position of its next item
+    int j, g; // staged row / 4-pixel group
+    int src;  // source byte offset of the group's first pixel
+    int lds;  // LDS byte address of the item
 };
 
-__device__ __forceinline__ int stage_byte(const AugJob& J, int cy, int cx)
+struct WalkStep { // uniform: advancing by nt items
+    int dj, dg, dsrc, dlds, wrap_src, wrap_lds;
+};
+
+struct Prefetch {
+    u32x3    d[kPrefetch];
+    uint32_t lds[kPrefetch]; // LDS byte address | 2 (item) | 1 (fast); 0 = no item
+};
+
+__device__ __forceinline__ void walk_init(const AugJob& J, const StageGeom& G, int i, int pitch, int stage_base,
+                                          int nt, Walk& w, WalkStep& st)
 {
-    return (J.crop_y + cy) * J.src_stride + (J.crop_x + cx) * J.cn;
+    w.j   = i / G.groups;
+    w.g   = i - w.j * G.groups;
+    w.src = (J.crop_y + G.v_lo + J.shift_y + w.j) * J.src_stride + (J.crop_x + G.u_lo + J.shift_x + 4 * w.g) * J.cn;
+    w.lds = stage_base + (w.j * pitch + 4 * w.g) * 4;
+    st.dj       = nt / G.groups;
+    st.dg       = nt - st.dj * G.groups;
+    st.dsrc     = st.dj * J.src_stride + st.dg * 4 * J.cn;
+    st.dlds     = (st.dj * pitch + 4 * st.dg) * 4;
+    st.wrap_src = J.src_stride - G.groups * 4 * J.cn;
+    st.wrap_lds = (pitch - 4 * G.groups) * 4;
 }
 
-// Fast item: one 16-byte (8 for 1 channel) load holds the four source pixels -- or, unpadded,
-// pixels beyond the crop that only ever meet a zero resize weight.  The load must lie wholly
-// inside the image: a buffer load that crosses num_records returns 0 for the whole access.
-__device__ __forceinline__ bool stage_fast(const AugJob& J, int cy, int cx)
+__device__ __forceinline__ void walk_next(const StageGeom& G, const WalkStep& st, Walk& w)
 {
-    const int  b      = stage_byte(J, cy, cx);
-    const bool inside = (uint32_t)((b & ~3) + (J.cn == 3 ? 16 : 8)) <= (uint32_t)J.src_bytes;
-    return inside && (!J.padded || (cy >= 0 && cy < J.crop_h && cx >= 0 && cx + 3 < J.crop_w));
+    w.j += st.dj, w.g += st.dg, w.src += st.dsrc, w.lds += st.dlds;
+    if (w.g >= G.groups) w.g -= G.groups, w.j++, w.src += st.wrap_src, w.lds += st.wrap_lds;
 }
 
-__device__ __forceinline__ u32x4 stage_load(const AugJob& J, __amdgpu_buffer_rsrc_t rsrc, int b)
+// Fast item: the load lies wholly inside the image buffer (a buffer load that crosses num_records
+// returns 0 for the whole access) and, for a padded job, inside the crop (outside it add_padding's
+// zero border applies).  Unpadded, pixels right of the crop only ever meet a zero resize weight.
+__device__ __forceinline__ bool stage_fast(const AugJob& J, const StageGeom& G, const Walk& w)
 {
-    if (J.cn == 3) return __builtin_amdgcn_raw_buffer_load_b128(rsrc, b & ~3, 0, 0);
-    u32x2 d = __builtin_amdgcn_raw_buffer_load_b64(rsrc, b & ~3, 0, 0);
-    return (u32x4){d.x, d.y, 0u, 0u};
+    const bool inside = (uint32_t)w.src + (J.cn == 3 ? 12u : 4u) <= (uint32_t)J.src_bytes;
+    if (!J.padded) return inside;
+    const int cy = G.v_lo + w.j + J.shift_y, cx = G.u_lo + 4 * w.g + J.shift_x;
+    return inside && w.src >= 0 && cy >= 0 && cy < J.crop_h && cx >= 0 && cx + 3 < J.crop_w;
 }
 
-__device__ __forceinline__ u32x4 stage_unpack(int cn, int sh, u32x4 d)
+__device__ __forceinline__ u32x3 stage_load(const AugJob& J, __amdgpu_buffer_rsrc_t rsrc, int b)
 {
-    if (cn == 3) {
-        uint32_t e0 = __builtin_amdgcn_alignbyte(d.y, d.x, sh);
-        uint32_t e1 = __builtin_amdgcn_alignbyte(d.z, d.y, sh);
-        uint32_t e2 = __builtin_amdgcn_alignbyte(d.w, d.z, sh);
-        return (u32x4){e0 & 0xffffff, (e0 >> 24) | ((e1 & 0xffff) << 8), (e1 >> 16) | ((e2 & 0xff) << 16),
-                       e2 >> 8};
-    }
-    uint32_t e0 = __builtin_amdgcn_alignbyte(d.y, d.x, sh);
-    return (u32x4){e0 & 0xff, (e0 >> 8) & 0xff, (e0 >> 16) & 0xff, e0 >> 24};
+    if (J.cn == 3) return __builtin_amdgcn_raw_buffer_load_b96(rsrc, b, 0, 0);
+    return (u32x3){__builtin_amdgcn_raw_buffer_load_b32(rsrc, b, 0, 0), 0u, 0u};
 }
 
-// Slow item (add_padding border / crop edge of a padded job): per-pixel byte loads, 0 outside.
+__device__ __forceinline__ u32x4 stage_unpack(int cn, u32x3 d)
+{
+    if (cn == 3) // 12 bytes BGR BGR BGR BGR -> four (B, G, R, 0) words
+        return (u32x4){d.x & 0xffffffu, __builtin_amdgcn_perm(d.y, d.x, 0x0C050403u),
+                       __builtin_amdgcn_perm(d.z, d.y, 0x0C040302u), d.z >> 8};
+    return (u32x4){d.x & 0xffu, __builtin_amdgcn_perm(0u, d.x, 0x0C0C0C01u), __builtin_amdgcn_perm(0u, d.x, 0x0C0C0C02u),
+                   d.x >> 24};
+}
+
+// Slow item (add_padding border / crop edge of a padded job / buffer end): per-pixel byte loads,
+// 0 outside the crop.
 __device__ __forceinline__ u32x4 stage_slow(const AugJob& J, __amdgpu_buffer_rsrc_t rsrc, int cy, int cx)
 {
     uint32_t   px[4];
@@ -236,7 +261,7 @@ __device__ __forceinline__ u32x4 stage_slow(const AugJob& J, __amdgpu_buffer_rsr
         const int x = cx + k;
         uint32_t  p = 0;
         if (row_ok && x >= 0 && x < J.crop_w) {
-            const int b = stage_byte(J, cy, x);
+            const int b = (J.crop_y + cy) * J.src_stride + (J.crop_x + x) * J.cn;
             for (int c = 0; c < J.cn; c++)
                 p |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rsrc, b + c, 0, 0) << (8 * c);
         }
@@ -245,56 +270,50 @@ __device__ __forceinline__ u32x4 stage_slow(const AugJob& J, __amdgpu_buffer_rsr
     return (u32x4){px[0], px[1], px[2], px[3]};
 }
 
-// Issue the first kPrefetch items of this lane for a band (fast items only).  nt = lanes.
+// Issue the loads of this lane's next kPrefetch items (fast items only) and advance the walk.
 __device__ __forceinline__ void stage_issue(const AugJob& J, __amdgpu_buffer_rsrc_t rsrc, const StageGeom& G,
-                                            Prefetch& pf, int nt)
-{
-    const int total = G.nr * G.groups;
-    const int dj = nt / G.groups, dg = nt - dj * G.groups;
-    int       j = threadIdx.x / G.groups, g = threadIdx.x - j * G.groups;
-#pragma unroll
-    for (int k = 0; k < kPrefetch; k++, j += dj, g += dg) {
-        if (g >= G.groups) g -= G.groups, j++;
-        const int i = threadIdx.x + k * nt;
-        pf.meta[k]  = 0;
-        if (i >= total) continue;
-        const int  cy = G.v_lo + j + J.shift_y, cx = G.u_lo + 4 * g + J.shift_x;
-        const bool fast = stage_fast(J, cy, cx);
-        const int  b    = stage_byte(J, cy, cx);
-        pf.meta[k]      = ((uint32_t)j << 20) | ((uint32_t)g << 6) | ((b & 3) << 2) | (fast ? 2u : 0u) | 1u;
-        if (fast) pf.d[k] = stage_load(J, rsrc, b);
-    }
-}
-
-// Write this lane's items of a band to LDS (prefetched ones from registers, the rest loaded now).
-__device__ __forceinline__ void stage_commit(const AugJob& J, __amdgpu_buffer_rsrc_t rsrc, const StageGeom& G,
-                                             const Prefetch& pf, uint32_t* stage, int pitch, int nt)
+                                            const WalkStep& st, Walk& w, Prefetch& pf)
 {
 #pragma unroll
     for (int k = 0; k < kPrefetch; k++) {
-        const uint32_t m = pf.meta[k];
-        if (!(m & 1)) continue;
-        const int j = m >> 20, g = (m >> 6) & 0x3fff;
-        u32x4     q;
-        if (m & 2) q = stage_unpack(J.cn, (m >> 2) & 3, pf.d[k]);
-        else q = stage_slow(J, rsrc, G.v_lo + j + J.shift_y, G.u_lo + 4 * g + J.shift_x);
-        *(u32x4*)(stage + j * pitch + 4 * g) = q;
-    }
-    const int total = G.nr * G.groups;
-    const int i0    = threadIdx.x + kPrefetch * nt;
-    const int dj = nt / G.groups, dg = nt - dj * G.groups;
-    int       j = i0 / G.groups, g = i0 - j * G.groups;
-    for (int i = i0; i < total; i += nt, j += dj, g += dg) {
-        if (g >= G.groups) g -= G.groups, j++;
-        const int cy = G.v_lo + j + J.shift_y, cx = G.u_lo + 4 * g + J.shift_x;
-        u32x4     q;
-        if (stage_fast(J, cy, cx)) {
-            const int b = stage_byte(J, cy, cx);
-            q           = stage_unpack(J.cn, b & 3, stage_load(J, rsrc, b));
-        } else {
-            q = stage_slow(J, rsrc, cy, cx);
+        pf.lds[k] = 0;
+        if (w.j < G.nr) {
+            const bool fast = stage_fast(J, G, w);
+            pf.lds[k]       = (uint32_t)w.lds | (fast ? 1u : 0u) | 2u;
+            if (fast) pf.d[k] = stage_load(J, rsrc, w.src);
+            walk_next(G, st, w);
         }
-        *(u32x4*)(stage + j * pitch + 4 * g) = q;
+    }
+}
+
+// Unpack / load-slow and write this batch's items to LDS.
+__device__ __forceinline__ void stage_commit(const AugJob& J, __amdgpu_buffer_rsrc_t rsrc, const StageGeom& G,
+                                             const Prefetch& pf, int stage_base, int pitch)
+{
+#pragma unroll
+    for (int k = 0; k < kPrefetch; k++) {
+        const uint32_t m = pf.lds[k];
+        if (!(m & 2)) continue;
+        u32x4 q;
+        if (m & 1) {
+            q = stage_unpack(J.cn, pf.d[k]);
+        } else { // rare: recover (row, group) from the LDS address
+            const int o = (int)(m & ~3u) - stage_base;
+            const int j = o / (pitch * 4), g = (o - j * pitch * 4) >> 4;
+            q           = stage_slow(J, rsrc, G.v_lo + j + J.shift_y, G.u_lo + 4 * g + J.shift_x);
+        }
+        *(__attribute__((address_space(3))) u32x4*)(size_t)(m & ~3u) = q;
+    }
+}
+
+// Stage a whole band: first batch already issued by the caller (pf, w), the rest here.
+__device__ __forceinline__ void stage_finish(const AugJob& J, __amdgpu_buffer_rsrc_t rsrc, const StageGeom& G,
+                                             const WalkStep& st, Walk& w, Prefetch& pf, int stage_base, int pitch)
+{
+    stage_commit(J, rsrc, G, pf, stage_base, pitch);
+    while (w.j < G.nr) {
+        stage_issue(J, rsrc, G, st, w, pf);
+        stage_commit(J, rsrc, G, pf, stage_base, pitch);
     }
 }
 
@@ -419,7 +438,6 @@ __global__ __launch_bounds__(kBlockMax, AEON_HIP_MIN_WAVES) void augment_tiles(L
     int4*           yt0   = (int4*)(smem + L.yt);
     int32_t*        red   = (int32_t*)(smem + L.red);
     double*         shift = (double*)(smem + L.red + 128);
-    uint32_t*       stage = (uint32_t*)(smem + L.stage);
     const int       pitch = a.stage_pitch;
 
     // source columns (the same for every band; taps are monotone in dx)
@@ -452,12 +470,15 @@ __global__ __launch_bounds__(kBlockMax, AEON_HIP_MIN_WAVES) void augment_tiles(L
         __builtin_amdgcn_make_buffer_rsrc((void*)J.src_ptr, (short)0, (int)J.src_bytes, 0x00020000);
     // band 0 loads go out first; the tables below are built while they are in flight
     Prefetch pf;
+    Walk     wk;
+    WalkStep ws;
     int      n0 = band_rows(c0, G);
     if (G.nr > a.stage_rows) {
         if (tid == 0) atomicOr(a.error, 2);
         return;
     }
-    stage_issue(J, srsrc, G, pf, nt);
+    walk_init(J, G, tid, pitch, L.stage, nt, wk, ws);
+    stage_issue(J, srsrc, G, ws, wk, pf);
 
     for (int x = tid; x < win_w; x += nt) {
         const XTap t = xcoef<RM>(J.win_x + x, J.scale_x, J.crop_w);
@@ -491,7 +512,7 @@ __global__ __launch_bounds__(kBlockMax, AEON_HIP_MIN_WAVES) void augment_tiles(L
         }
     }
     build_yt(c0, n0, G, yt0);
-    stage_commit(J, srsrc, G, pf, stage, pitch, nt);
+    stage_finish(J, srsrc, G, ws, wk, pf, L.stage, pitch);
     __syncthreads();
 
     uint32_t sum0 = 0, sum1 = 0, sum2 = 0;
@@ -652,11 +673,14 @@ __global__ __launch_bounds__(kBlockMax, AEON_HIP_MIN_WAVES) void augment_tiles(L
                 if (tid == 0) atomicOr(a.error, 2);
                 return; // uniform: every lane sees the same band geometry
             }
+            Walk     wn;
+            WalkStep sn;
             Prefetch pn;
-            stage_issue(J, srsrc, Gn, pn, nt);
+            walk_init(J, Gn, tid, pitch, L.stage, nt, wn, sn);
+            stage_issue(J, srsrc, Gn, sn, wn, pn);
             build_yt(y0 + TR, nn, Gn, yt0 + (buf ^ 1) * TR);
             __syncthreads(); // single staging buffer: everyone is done reading it
-            stage_commit(J, srsrc, Gn, pn, stage, pitch, nt);
+            stage_finish(J, srsrc, Gn, sn, wn, pn, L.stage, pitch);
             __syncthreads();
         }
         buf ^= 1;

@@ -47,7 +47,7 @@ struct aeon_error : std::runtime_error {
     } while (0)
 
 constexpr int kMaxLds        = 160 * 1024;
-constexpr int kStageBudget   = 24 * 1024;   // preferred LDS bytes per staged band
+constexpr int kStageBudget   = 48 * 1024;   // preferred LDS bytes per staged band
 constexpr int kStageBudgetHi = 120 * 1024;  // fallback for very wide crops
 constexpr int kBandsPerChunk = 1;
 
@@ -198,9 +198,9 @@ struct LaunchPlan {
         if (const char* e = std::getenv("AEON_HIP_THREADS"))
             threads = std::min(kBlockMax, std::max(kBlockMin, std::atoi(e) / 64 * 64));
         const int nph = threads / ncg;
-        // rows per band: about two rows per lane, a multiple of the row phases; knobs for
-        // experiments only
-        int tr_cap = std::min(32, std::max(1, 2 * nph));
+        // rows per band: about four rows per lane (amortises the per-workgroup prologue: job,
+        // tap tables, LUT, staging), a multiple of the row phases; knobs for experiments only
+        int tr_cap = std::min(32, std::max(1, 4 * nph));
         if (const char* e = std::getenv("AEON_HIP_STAGE_KB")) budget = std::max(1, std::atoi(e)) * 1024;
         if (const char* e = std::getenv("AEON_HIP_TR")) tr_cap = std::max(1, std::atoi(e));
         for (int pass = 0; pass < 2; pass++) {
