@@ -236,8 +236,9 @@ class Context:
         """pixel_mask transform + load for len(descs) records (async on stream)."""
         self._batch(lib().aeon_hip_mask_batch, descs, src_ptr, params, out, out_ptr, stream)
 
-    def set_timing(self, enable=True):
-        _check(lib().aeon_hip_set_timing(self._h, int(enable)))
+    def set_timing(self, every=1):
+        """Time the launches of one call in `every` (0 = off) with HIP events on their stream."""
+        _check(lib().aeon_hip_set_timing(self._h, int(every)))
 
     def kernel_times(self):
         """{'augment'|'stats'|'resize_short': (total_ms, total_algorithmic_bytes, launches)}"""

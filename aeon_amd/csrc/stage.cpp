@@ -424,9 +424,11 @@ void plan_image(const aeon_img_desc& d, const void* src_base, const aeon_aug_par
 struct Slot {
     hipEvent_t done     = nullptr; // the slot's kernels finished (host reuses the slot after it)
     hipEvent_t copied   = nullptr; // the slot's job table reached the device
-    bool       pending  = false;
+    bool       pending  = false; // the slot's kernels may still run: wait for slots[cover].done
+    int        cover    = -1;
     uint8_t*   host     = nullptr;
     size_t     host_cap = 0;
+    uint8_t*   host_dev = nullptr; // device view of `host` (zero-copy job tables)
     uint8_t*   dev      = nullptr;
     size_t     dev_cap  = 0;
     uint8_t*   scratch  = nullptr;
@@ -447,11 +449,30 @@ struct aeon_hip_ctx {
     int        device = 0;
     int32_t*   d_error = nullptr;
     int32_t*   d_hsv   = nullptr;
-    Slot       slots[4];
+    // staging ring: a slot (job table, scratch) is reused only after the kernels that read it
+    // finished.  A completion event is recorded once per `done_every` calls on a stream and
+    // covers the calls since the previous one (each event costs GPU time between launches).
+    static constexpr int kSlots = 16;
+    Slot       slots[kSlots];
     int        next = 0;
+    int        done_every = 8;
+    std::vector<int> open_slots; // used since the last completion event, on open_stream
+    hipStream_t      open_stream = nullptr;
     // job tables go up on their own stream, so a call's H2D overlaps the previous call's kernels
     // instead of queueing between them on the caller's stream
     hipStream_t copy_stream = nullptr;
+    // job-table transport: 0 = H2D on copy_stream + cross-stream event, 1 = H2D on the launch
+    // stream, 2 = kernels read the pinned table in place (AEON_HIP_JOBS for experiments)
+    int         jobs_mode = 0;
+    // standardize LUTs stay resident per distinct output config (a new one is uploaded once)
+    struct Lut {
+        float  host[768];
+        float* dev = nullptr;
+    };
+    std::vector<Lut> luts;
+    // per-launch timing events on every `timing_every`-th call only (they cost GPU time)
+    int         timing_every = 1;
+    long        timing_calls = 0;
     std::mutex mu;
     // optional per-launch timing (aeon_hip_set_timing): events recorded on the launch stream
     bool                     timing = false;
@@ -484,6 +505,26 @@ void grow(uint8_t*& p, size_t& cap, size_t need, bool pinned)
     cap = n;
 }
 
+// Device copy of the standardize LUT of output config `o` (uploaded the first time it is seen).
+const float* resident_lut(aeon_hip_ctx* ctx, const aeon_out_desc& o)
+{
+    float lut[768];
+    build_lut(o, lut);
+    for (auto& L : ctx->luts)
+        if (std::memcmp(L.host, lut, sizeof(lut)) == 0) return L.dev;
+    if (ctx->luts.size() >= 16) { // many configs on one context: start over once the device is idle
+        HIP_OK(hipDeviceSynchronize());
+        for (auto& L : ctx->luts) HIP_OK(hipFree(L.dev));
+        ctx->luts.clear();
+    }
+    aeon_hip_ctx::Lut L;
+    std::memcpy(L.host, lut, sizeof(lut));
+    HIP_OK(hipMalloc((void**)&L.dev, sizeof(lut)));
+    HIP_OK(hipMemcpy(L.dev, lut, sizeof(lut), hipMemcpyHostToDevice));
+    ctx->luts.push_back(L);
+    return L.dev;
+}
+
 // Algorithmic bytes of one launch: the resampled u8 source footprint plus
 // the bytes written (KM_STATS / KM_RAW write an HWC uint8 intermediate).
 double launch_bytes(const LaunchPlan& L, int mode, size_t out_elem)
@@ -501,11 +542,21 @@ double launch_bytes(const LaunchPlan& L, int mode, size_t out_elem)
     return b;
 }
 
+// One completion event after the open slots' kernels (on their stream) covers all of them.
+void close_slots(aeon_hip_ctx* ctx)
+{
+    if (ctx->open_slots.empty()) return;
+    const int last = ctx->open_slots.back();
+    HIP_OK(hipEventRecord(ctx->slots[last].done, ctx->open_stream));
+    for (int i : ctx->open_slots) ctx->slots[i].pending = true, ctx->slots[i].cover = last;
+    ctx->open_slots.clear();
+}
+
 void timed_launch(aeon_hip_ctx* ctx, int mode, const LaunchPlan& P, const LaunchArgs& a, hipStream_t stream,
-                  double bytes)
+                  double bytes, bool timed)
 {
     KernelTimer t{};
-    if (ctx->timing) {
+    if (timed) {
         if (!ctx->free_timers.empty()) {
             t = ctx->free_timers.back();
             ctx->free_timers.pop_back();
@@ -518,7 +569,7 @@ void timed_launch(aeon_hip_ctx* ctx, int mode, const LaunchPlan& P, const Launch
         HIP_OK(hipEventRecord(t.start, stream));
     }
     HIP_OK(launch_tiles(mode, P.rm, P.tail, P.photo, a, (int)P.jobs.size(), stream));
-    if (ctx->timing) {
+    if (timed) {
         HIP_OK(hipEventRecord(t.stop, stream));
         ctx->timers.push_back(t);
     }
@@ -577,8 +628,7 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
     for (const AugJob& J : pre2_all.jobs) pre2[J.mode * 2 + has_tail(J)].jobs.push_back(J);
     for (const AugJob& J : pass1_all.jobs) pass1[J.mode * 2 + has_tail(J)].jobs.push_back(J);
     for (const AugJob& J : main_all.jobs) main[J.mode * 4 + has_tail(J) * 2 + (J.photo ? 1 : 0)].jobs.push_back(J);
-    const size_t     lut_bytes = 4096;
-    const size_t     rot_off   = lut_bytes;
+    const size_t     rot_off   = 0;
     size_t           blob      = rot_off + rot.size() * sizeof(RotJob);
     int              rot_max_px = 0;
     for (const RotJob& R : rot) rot_max_px = std::max(rot_max_px, R.w * R.h);
@@ -603,22 +653,29 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
     const size_t partial_words = std::max<size_t>(4, pass1_all.jobs.size() * partial_stride * 4);
 
     phase(2);
-    Slot& s = ctx->slots[ctx->next];
-    ctx->next = (ctx->next + 1) % 4;
+    // calls on another stream than the open ones: close those with an event on their stream
+    if (!ctx->open_slots.empty() && ctx->open_stream != stream) close_slots(ctx);
+    const int slot = ctx->next;
+    Slot&     s    = ctx->slots[slot];
+    ctx->next      = (ctx->next + 1) % aeon_hip_ctx::kSlots;
     if (s.pending) {
-        HIP_OK(hipEventSynchronize(s.done));
+        HIP_OK(hipEventSynchronize(ctx->slots[s.cover].done));
         s.pending = false;
     }
     phase(3);
-    grow(s.host, s.host_cap, blob, true);
-    grow(s.dev, s.dev_cap, blob, false);
+    const float* d_lut = resident_lut(ctx, o);
+    blob = std::max<size_t>(blob, 16);
+    if (blob > s.host_cap) {
+        grow(s.host, s.host_cap, blob, true);
+        HIP_OK(hipHostGetDevicePointer((void**)&s.host_dev, s.host, 0));
+    }
+    if (ctx->jobs_mode != 2) grow(s.dev, s.dev_cap, blob, false);
     grow(s.scratch, s.scratch_cap, std::max<size_t>(scratch_bytes, 16), false);
     {
         uint8_t* p = (uint8_t*)s.partials;
         grow(p, s.partials_cap, partial_words * 4, false);
         s.partials = (uint32_t*)p;
     }
-    build_lut(o, (float*)s.host);
     for (RotJob& R : rot) R.out_ptr += (uint64_t)s.scratch;
     if (!rot.empty()) std::memcpy(s.host + rot_off, rot.data(), rot.size() * sizeof(RotJob));
     for (auto* v : {&pre, &pre2, &pass1, &main})
@@ -630,15 +687,22 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
             if (!P.jobs.empty()) std::memcpy(s.host + P.blob_off, P.jobs.data(), P.jobs.size() * sizeof(AugJob));
         }
     phase(4);
-    HIP_OK(hipMemcpyAsync(s.dev, s.host, blob, hipMemcpyHostToDevice, ctx->copy_stream));
-    HIP_OK(hipEventRecord(s.copied, ctx->copy_stream));
-    HIP_OK(hipStreamWaitEvent(stream, s.copied, 0));
+    const uint8_t* table = s.dev;
+    if (ctx->jobs_mode == 0) {
+        HIP_OK(hipMemcpyAsync(s.dev, s.host, blob, hipMemcpyHostToDevice, ctx->copy_stream));
+        HIP_OK(hipEventRecord(s.copied, ctx->copy_stream));
+        HIP_OK(hipStreamWaitEvent(stream, s.copied, 0));
+    } else if (ctx->jobs_mode == 1) {
+        HIP_OK(hipMemcpyAsync(s.dev, s.host, blob, hipMemcpyHostToDevice, stream));
+    } else {
+        table = s.host_dev;
+    }
     phase(5);
 
     auto args = [&](const LaunchPlan& L) {
         LaunchArgs a{};
-        a.jobs          = (const AugJob*)(s.dev + L.blob_off);
-        a.lut           = (const float*)s.dev; // [3][256]: standardized, or (float)x without mean
+        a.jobs          = (const AugJob*)(table + L.blob_off);
+        a.lut           = d_lut; // [3][256]: standardized, or (float)x without mean
         a.hsv_tables    = ctx->d_hsv;
         a.partials      = s.partials;
         a.partial_stride = partial_stride;
@@ -659,18 +723,21 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
         return a;
     };
     const size_t oelem = o.dtype == AEON_DTYPE_F32 ? 4 : 1;
+    // timing events on one call in timing_every (each event pair costs GPU time between launches)
+    const bool timed = ctx->timing && (ctx->timing_calls++ % ctx->timing_every) == 0;
     if (!rot.empty())
-        HIP_OK(launch_rotate((const RotJob*)(s.dev + rot_off), (int)rot.size(), rot_max_px, stream));
+        HIP_OK(launch_rotate((const RotJob*)(table + rot_off), (int)rot.size(), rot_max_px, stream));
     for (auto* v : {&pre, &pre2})
         for (LaunchPlan& P : *v)
-            if (!P.jobs.empty()) timed_launch(ctx, KM_RAW, P, args(P), stream, launch_bytes(P, KM_RAW, 1));
+            if (!P.jobs.empty()) timed_launch(ctx, KM_RAW, P, args(P), stream, launch_bytes(P, KM_RAW, 1), timed);
     for (LaunchPlan& P : pass1)
-        if (!P.jobs.empty()) timed_launch(ctx, KM_STATS, P, args(P), stream, launch_bytes(P, KM_STATS, oelem));
+        if (!P.jobs.empty()) timed_launch(ctx, KM_STATS, P, args(P), stream, launch_bytes(P, KM_STATS, oelem), timed);
     for (LaunchPlan& P : main)
-        if (!P.jobs.empty()) timed_launch(ctx, KM_FINAL, P, args(P), stream, launch_bytes(P, KM_FINAL, oelem));
+        if (!P.jobs.empty()) timed_launch(ctx, KM_FINAL, P, args(P), stream, launch_bytes(P, KM_FINAL, oelem), timed);
     phase(6);
-    HIP_OK(hipEventRecord(s.done, stream));
-    s.pending = true;
+    ctx->open_slots.push_back(slot);
+    ctx->open_stream = stream;
+    if ((int)ctx->open_slots.size() >= ctx->done_every) close_slots(ctx);
     phase(7);
     ctx->host_calls++;
     return 0;
@@ -734,6 +801,9 @@ int aeon_hip_ctx_create(int device, aeon_hip_ctx** out)
             }
             HIP_OK(hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
             if (const char* e = std::getenv("AEON_HIP_HOST_PROFILE")) c->host_profile = std::atoi(e) != 0;
+            if (const char* e = std::getenv("AEON_HIP_JOBS")) c->jobs_mode = std::min(2, std::max(0, std::atoi(e)));
+            if (const char* e = std::getenv("AEON_HIP_DONE_EVERY"))
+                c->done_every = std::min(aeon_hip_ctx::kSlots / 2, std::max(1, std::atoi(e)));
         } catch (...) {
             delete c;
             throw;
@@ -760,8 +830,10 @@ int aeon_hip_ctx_destroy(aeon_hip_ctx* c)
             std::fprintf(stderr, "\n");
         }
         (void)hipSetDevice(c->device);
+        if (!c->open_slots.empty()) (void)hipStreamSynchronize(c->open_stream);
+        for (Slot& s : c->slots)
+            if (s.pending) (void)hipEventSynchronize(c->slots[s.cover].done);
         for (Slot& s : c->slots) {
-            if (s.pending) (void)hipEventSynchronize(s.done);
             if (s.done) (void)hipEventDestroy(s.done);
             if (s.copied) (void)hipEventDestroy(s.copied);
             if (s.host) (void)hipHostFree(s.host);
@@ -772,6 +844,7 @@ int aeon_hip_ctx_destroy(aeon_hip_ctx* c)
         for (auto* v : {&c->timers, &c->free_timers})
             for (KernelTimer& t : *v) (void)hipEventDestroy(t.start), (void)hipEventDestroy(t.stop);
         if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
+        for (auto& L : c->luts) (void)hipFree(L.dev);
         if (c->d_error) (void)hipFree(c->d_error);
         if (c->d_hsv) (void)hipFree(c->d_hsv);
         delete c;
@@ -836,7 +909,9 @@ int aeon_hip_set_timing(aeon_hip_ctx* ctx, int enable)
     return guarded([&] {
         if (!ctx) fail(AEON_HIP_EINVAL, "null ctx");
         std::lock_guard<std::mutex> lock(ctx->mu);
-        ctx->timing = enable != 0;
+        ctx->timing       = enable > 0;
+        ctx->timing_every = std::max(1, enable);
+        ctx->timing_calls = 0;
         return 0;
     });
 }

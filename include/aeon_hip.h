@@ -117,8 +117,10 @@ int aeon_hip_transpose_batch(aeon_hip_ctx* ctx, const void* src_dev, void* dst_d
 int aeon_hip_synchronize(aeon_hip_ctx* ctx, void* stream);
 
 /* ---- measurement ---------------------------------------------------------------------------- */
-/* When enabled, every kernel launch is bracketed by HIP events on its own stream. */
-int aeon_hip_set_timing(aeon_hip_ctx* ctx, int enable);
+/* every > 0: the kernel launches of one augment/mask call in `every` are bracketed by HIP events
+ * on their own stream (an event pair costs GPU time between launches, so benchmarks sample);
+ * 0 disables timing. */
+int aeon_hip_set_timing(aeon_hip_ctx* ctx, int every);
 /* Drain the timers: per kernel kind [0]=augment (final), [1]=contrast statistics,
  * [2]=resize_short pre-pass: total ms, total algorithmic bytes, launches. Resets the totals. */
 int aeon_hip_kernel_times(aeon_hip_ctx* ctx, double* ms, double* bytes, long* count);

@@ -5,10 +5,10 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 900 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1 && echo "pytest gpu ok" \
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 && echo "pytest gpu ok" \
 && timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 && echo "smoke ok" \
-&& timeout -k 10 600 python bench.py --steps 30 --warmup 5 --cpu-seconds 8 > gpurun_out/bench.log 2>gpurun_out/bench.err && echo "bench ok" \
-&& cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 20 --warmup 3 --no-cpu-baseline --no-extra > "$GRAFT_REPO_ROOT/gpurun_out/prof_bench.log" 2>&1 && echo "rocprof ok"
+&& timeout -k 10 600 python bench.py --steps 200 --warmup 10 --cpu-seconds 8 > gpurun_out/bench.log 2>gpurun_out/bench.err && echo "bench ok" \
+&& cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 100 --warmup 5 --no-cpu-baseline --no-extra > "$GRAFT_REPO_ROOT/gpurun_out/prof_bench.log" 2>&1 && echo "rocprof ok"
 rc=$?
 cd "${GRAFT_REPO_ROOT}"
 tail -3 gpurun_out/pytest_gpu.log; tail -2 gpurun_out/smoke.log 2>/dev/null; cat gpurun_out/bench.log 2>/dev/null
