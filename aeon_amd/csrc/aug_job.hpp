@@ -73,20 +73,22 @@ struct LaunchArgs {
                                // channel (bgr_to_rgb ? 2-c : c), or (float)x without mean
     const int32_t* hsv_tables; // sdiv[256], hdiv180[256]
     uint32_t*      partials;   // contrast partial sums [slots][partial_stride][4]
+    double*        shifts;     // contrast (1-c)*mean per slot [slots][4] (contrast_reduce)
     int32_t*       error;      // device error word (0 = ok)
-    int32_t        rows_per_tile;  // rows per LDS band (TR)
-    int32_t        rows_per_chunk; // rows per workgroup (a multiple of TR; = TR: one band)
-    int32_t        max_tiles;      // chunks per job (grid.x)
-    int32_t        stage_rows; // capacity of the LDS staging area
-    int32_t        stage_pitch;// pixels per staged row (multiple of 4)
-    int32_t        max_win_w;  // capacity of the x table
+    uint32_t*      trace;      // development only: per-workgroup phase timestamps (null = off)
+    int32_t        rows_per_tile;  // output rows per tile (TR)
+    int32_t        max_tiles;      // tiles per job (tile t = band t % max_tiles of job t / max_tiles)
+    int32_t        total_tiles;    // jobs * max_tiles
+    int32_t        stage_bytes;    // capacity of one LDS staging buffer (multiple of 1 KiB)
+    int32_t        stage_buffers;  // 2: the next tile's staging overlaps this tile's compute; 1: serial
+    int32_t        max_win_w;  // capacity of the column-tap tables
     int32_t        out_dtype;  // OutDtype
     int32_t        channel_major;
     int32_t        bgr_to_rgb;
     int32_t        vec_ok;     // outputs 16-byte aligned and win_w % 4 == 0 for every job
     int32_t        lds_bytes;
     int32_t        has_hue;    // some job of the launch shifts hue (HSV tables in LDS)
-    int32_t        partial_stride; // chunks per contrast slot in `partials`
+    int32_t        partial_stride; // (tile, wave) entries per contrast slot in `partials`
     int32_t        threads;    // workgroup size (kBlockMin..kBlockMax, a multiple of 64)
 };
 
@@ -108,23 +110,22 @@ constexpr int kBlockMax = 512;
 
 // LDS carve of one workgroup (bytes; every region 16-byte aligned, see the CDNA guide G17).
 struct LdsLayout {
-    int hsv, lut, xt, yt, red, stage, stage_bytes, total;
+    int lut, hsv, xt, yt, pf, stage, stage_bytes, total;
 };
-// One staging buffer (the next band waits in registers while the current one is consumed);
-// two small row-tap tables.  The HSV tables are reserved only for hue launches.  The LUT sits
+// One or two staging buffers and copies of the tap tables (with two, the next tile's are filled
+// while the current tile is computed).  The HSV tables are reserved only for hue launches.  The LUT sits
 // at offset 0 so its per-channel reads use immediate LDS offsets.
-AEON_HD inline LdsLayout lds_layout(int max_win_w, int rows_per_tile, int stage_rows, int stage_pitch,
-                                    bool hue = true)
+AEON_HD inline LdsLayout lds_layout(int max_win_w, int rows_per_tile, int stage_bytes, bool hue, int buffers)
 {
     LdsLayout L;
     int       o = 0;
-    L.lut = o;   o += 3 * 256 * 4;                       // standardize LUT (source channel order)
-    L.hsv = o;   o += hue ? 2 * 256 * 4 : 0;             // sdiv / hdiv180 tables
-    L.xt  = o;   o += ((max_win_w * 8 + 15) / 16) * 16;  // per-column taps + weights
-    L.yt  = o;   o += 2 * rows_per_tile * 16;            // per-row taps + weights, x2
-    L.red = o;   o += 160;                               // 8 waves x 4 sums, then 3 f64 shifts
-    L.stage_bytes = stage_rows * stage_pitch * 4;        // source pixels, 4 B each (B,G,R,0)
-    L.stage = o; o += L.stage_bytes;
+    L.lut = o; o += 3 * 256 * 4;                             // standardize LUT (source channel order)
+    L.hsv = o; o += hue ? 2 * 256 * 4 : 0;                   // sdiv / hdiv180 tables
+    L.xt  = o; o += buffers * ((max_win_w * 8 + 15) / 16) * 16; // per-column taps + weights
+    L.yt  = o; o += buffers * rows_per_tile * 16;               // per-row taps + weights
+    L.pf  = o; o += 256;                                     // LDS-DMA sink of job prefetches
+    L.stage_bytes = stage_bytes;                             // source pixels, 4 B each (B,G,R,x)
+    L.stage = o; o += buffers * stage_bytes;
     L.total = o;
     return L;
 }

@@ -30,6 +30,15 @@ typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 typedef float    f32x4 __attribute__((ext_vector_type(4)));
 typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
+typedef int32_t  i32x4 __attribute__((ext_vector_type(4)));
+typedef int32_t  i32x2 __attribute__((ext_vector_type(2)));
+
+// Job descriptors are read through the constant address space: uniform, scalar loads.
+typedef const __attribute__((address_space(4))) AugJob cjob;
+__device__ __forceinline__ cjob& job_ref(const LaunchArgs& a, int job)
+{
+    return ((cjob*)(uintptr_t)a.jobs)[job];
+}
 
 __device__ __forceinline__ int sat_u8(int v) { return min(max(v, 0), 255); }
 __device__ __forceinline__ int sat_s16(int v) { return min(max(v, -32768), 32767); }
@@ -45,6 +54,13 @@ __device__ __forceinline__ int mul16(int a, int b) { return (int)(short)a * (int
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
 typedef __attribute__((address_space(3))) float    lds_f32;
 __device__ __forceinline__ uint32_t lds_ld(int byte_addr) { return *(const lds_u32*)(size_t)(uint32_t)byte_addr; }
+// Typed LDS pointer from a byte address.  All LDS traffic of the kernel goes through such
+// integer-derived pointers (see lds_dma).
+template <typename T>
+__device__ __forceinline__ __attribute__((address_space(3))) T* lds_ptr(int byte_addr)
+{
+    return (__attribute__((address_space(3))) T*)(size_t)(uint32_t)byte_addr;
+}
 __device__ __forceinline__ float    lds_ldf(int byte_addr) { return *(const lds_f32*)(size_t)(uint32_t)byte_addr; }
 
 // ---- resize coefficients (OpenCV 2.4 resizeGeneric_ / resizeNN) -----------------------------
@@ -103,20 +119,20 @@ __device__ __forceinline__ YTap ycoef(int dy, double scale, int sh)
 }
 
 // ---- photometric stages (aeon src/image.cpp:336-406 over OpenCV 2.4) ------------------------
-__device__ __forceinline__ void bs_apply(const AugJob& J, int& b, int& g, int& r)
+__device__ __forceinline__ void bs_apply(cjob& J, int& b, int& g, int& r)
 {
     if (J.bs_kind == BS_DIAG) { // diagtransform_8u
         b = sat_u8(rnd(J.bsm[0] * (float)b + 0.f));
         g = sat_u8(rnd(J.bsm[4] * (float)g + 0.f));
         r = sat_u8(rnd(J.bsm[8] * (float)r + 0.f));
     } else if (J.bs_kind == BS_FIXPT) { // transform_8u, 10-bit fixed point
-        const int* q  = J.bsq;
+        const int  q[9] = {J.bsq[0], J.bsq[1], J.bsq[2], J.bsq[3], J.bsq[4], J.bsq[5], J.bsq[6], J.bsq[7], J.bsq[8]};
         int        t0 = (q[0] * b + q[1] * g + q[2] * r + 512) >> 10;
         int        t1 = (q[3] * b + q[4] * g + q[5] * r + 512) >> 10;
         int        t2 = (q[6] * b + q[7] * g + q[8] * r + 512) >> 10;
         b = sat_u8(t0), g = sat_u8(t1), r = sat_u8(t2);
     } else { // transform_<uchar,float>
-        const float* m  = J.bsm;
+        const float m[9] = {J.bsm[0], J.bsm[1], J.bsm[2], J.bsm[3], J.bsm[4], J.bsm[5], J.bsm[6], J.bsm[7], J.bsm[8]};
         float        fb = (float)b, fg = (float)g, fr = (float)r;
         int          t0 = rnd(m[0] * fb + m[1] * fg + m[2] * fr + 0.f);
         int          t1 = rnd(m[3] * fb + m[4] * fg + m[5] * fr + 0.f);
@@ -135,8 +151,8 @@ constexpr int kSectorR = pack_sectors(0, 2, 1, 1, 3, 0);
 
 // cvtColor(BGR2HSV) [RGB2HSV_b], H = (H + hue) % 180 stored as uchar, cvtColor(HSV2BGR)
 // [HSV2RGB_b over HSV2RGB_f].
-__device__ __forceinline__ void hue_apply(const int32_t* sdiv, const int32_t* hdiv, int hue, int& b,
-                                          int& g, int& r)
+template <typename TAB>
+__device__ __forceinline__ void hue_apply(TAB sdiv, TAB hdiv, int hue, int& b, int& g, int& r)
 {
     int v = max(b, max(g, r)), vmin = min(b, min(g, r));
     int diff = v - vmin;
@@ -175,146 +191,190 @@ __device__ __forceinline__ void hue_apply(const int32_t* sdiv, const int32_t* hd
     r = sat_u8(rnd(rr * 255.f));
 }
 
-// ---- source staging ----------------------------------------------------------------------------
-// A band stages resize-source rows [v_lo, v_lo+nr) x cols [u_lo, u_lo+nc) into LDS as one 32-bit
-// word per pixel.  Items are 4-pixel groups; lane t takes items t, t+nt, ... in batches of
-// kPrefetch whose loads are all in flight before the first is unpacked.  Each item is ONE load
-// at its exact byte offset (12 bytes for 3 channels, 4 for 1 -- dword-unaligned buffer loads
-// return the exact bytes on gfx950), unpacked with two v_perm, and written with one ds_write_b128.
-// The walk over items keeps byte offsets incrementally: no 32-bit multiplies per item.
-constexpr int kPrefetch = 4;
+// ---- source staging (LDS-DMA) ------------------------------------------------------------------
+// A tile (a band of TR output rows of one record) needs source rows [v_lo, v_lo+nr) x cols
+// [u_lo, u_lo+nc), staged as one 32-bit word per pixel (B, G, R, x), rows `pitch` = 4*ng words
+// apart (ng = ceil(nc/4) groups of 4 pixels), in one of the workgroup's two LDS staging buffers.
+// (1) LDS-DMA, no VGPR round trip: for BGR, group q = j*ng + g is loaded by lane q%64 of
+// wave-instruction q/64 as the 12 bytes at its exact, unaligned source offset; a dwordx3 LDS-DMA
+// lands each lane's 12 bytes in a 16-byte slot (measured, tools/probes/glds_probe.py), i.e. exactly
+// where the group's four words go.  For one channel: one pixel per lane, 4 bytes from its own
+// offset (bytes 1-3 ignored).  The next tile's loads are issued before the current tile is
+// computed.  (2) After the issuing wave's own vmcnt wait, each lane unpacks the BGR slots it
+// loaded, in place.  The byte-exact rules are applied in (2): pixels outside the crop of a padded
+// job are 0 (add_padding's border); a load that crossed the end of the source buffer (a buffer
+// load past num_records returns 0 for the whole access) is re-read byte by byte.
+constexpr uint32_t kOutOfRange = 0x80000000u;
 
-struct StageGeom {
-    int v_lo, nr, u_lo, nc, groups;
+// buffer_load_dwordx3 ... lds: lane l -> LDS bytes lds_base + 16*l (12 written);
+// buffer_load_dword ... lds: lane l -> lds_base + 4*l.  Inline asm on purpose: hipcc tracks its
+// own LDS-DMA builtins and then waits vmcnt(0) before LDS reads inside the compute loops (they
+// may alias, as far as it can tell), which would drain the next tile's loads at the first pixel.
+// The kernel orders these loads itself: counted vmcnt, then a barrier.  M0 is set here and used
+// by nothing else in these kernels.
+template <int BYTES>
+__device__ __forceinline__ void lds_dma(__amdgpu_buffer_rsrc_t rsrc, int lds_base, uint32_t voff)
+{
+    if (BYTES == 12)
+        asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx3 %1, %2, 0 offen lds"
+                     :
+                     : "s"(__builtin_amdgcn_readfirstlane(lds_base)), "v"(voff), "s"(rsrc)
+                     : "memory");
+    else
+        asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dword %1, %2, 0 offen lds"
+                     :
+                     : "s"(__builtin_amdgcn_readfirstlane(lds_base)), "v"(voff), "s"(rsrc)
+                     : "memory");
+}
+
+// Buffer resource with its fields forced into scalar registers (the LDS-DMA asm takes an SGPR
+// quad; the values are uniform, but the compiler cannot always prove it).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* p, int bytes)
+{
+    const uint64_t v  = (uint64_t)p;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), (short)0,
+                                             __builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+
+struct StageGeom { // uniform: the staged source of one tile
+    int v_lo, nr, u_lo, nc, ng, pitch;
 };
 
-struct Walk { // lane-private position of its next item
-    int j, g; // staged row / 4-pixel group
-    int src;  // source byte offset of the group's first pixel
-    int lds;  // LDS byte address of the item
-};
-
-struct WalkStep { // uniform: advancing by nt items
-    int dj, dg, dsrc, dlds, wrap_src, wrap_lds;
-};
-
-struct Prefetch {
-    u32x3    d[kPrefetch];
-    uint32_t lds[kPrefetch]; // LDS byte address | 2 (item) | 1 (fast); 0 = no item
-};
-
-__device__ __forceinline__ void walk_init(const AugJob& J, const StageGeom& G, int i, int pitch, int stage_base,
-                                          int nt, Walk& w, WalkStep& st)
+// byte offset in the source buffer of staged pixel (row j, column u); negative above/left of a
+// padded crop
+__device__ __forceinline__ int src_off(cjob& J, const StageGeom& G, int j, int u)
 {
-    w.j   = i / G.groups;
-    w.g   = i - w.j * G.groups;
-    w.src = (J.crop_y + G.v_lo + J.shift_y + w.j) * J.src_stride + (J.crop_x + G.u_lo + J.shift_x + 4 * w.g) * J.cn;
-    w.lds = stage_base + (w.j * pitch + 4 * w.g) * 4;
-    st.dj       = nt / G.groups;
-    st.dg       = nt - st.dj * G.groups;
-    st.dsrc     = st.dj * J.src_stride + st.dg * 4 * J.cn;
-    st.dlds     = (st.dj * pitch + 4 * st.dg) * 4;
-    st.wrap_src = J.src_stride - G.groups * 4 * J.cn;
-    st.wrap_lds = (pitch - 4 * G.groups) * 4;
+    return (J.crop_y + G.v_lo + J.shift_y + j) * J.src_stride + (J.crop_x + G.u_lo + J.shift_x + u) * J.cn;
 }
 
-__device__ __forceinline__ void walk_next(const StageGeom& G, const WalkStep& st, Walk& w)
-{
-    w.j += st.dj, w.g += st.dg, w.src += st.dsrc, w.lds += st.dlds;
-    if (w.g >= G.groups) w.g -= G.groups, w.j++, w.src += st.wrap_src, w.lds += st.wrap_lds;
-}
+// Units (BGR groups or gray pixels) per staged row, and their count.
+__device__ __forceinline__ int stage_units_per_row(cjob& J, const StageGeom& G) { return J.cn == 3 ? G.ng : G.pitch; }
 
-// Fast item: the load lies wholly inside the image buffer (a buffer load that crosses num_records
-// returns 0 for the whole access) and, for a padded job, inside the crop (outside it add_padding's
-// zero border applies).  Unpadded, pixels right of the crop only ever meet a zero resize weight.
-__device__ __forceinline__ bool stage_fast(const AugJob& J, const StageGeom& G, const Walk& w)
+// (1) This wave's share of the tile's LDS-DMA loads: instructions wave, wave + nw, ...
+__device__ __forceinline__ void stage_issue(cjob& J, const StageGeom& G, int buf, int wave, int nw)
 {
-    const bool inside = (uint32_t)w.src + (J.cn == 3 ? 12u : 4u) <= (uint32_t)J.src_bytes;
-    if (!J.padded) return inside;
-    const int cy = G.v_lo + w.j + J.shift_y, cx = G.u_lo + 4 * w.g + J.shift_x;
-    return inside && w.src >= 0 && cy >= 0 && cy < J.crop_h && cx >= 0 && cx + 3 < J.crop_w;
-}
-
-__device__ __forceinline__ u32x3 stage_load(const AugJob& J, __amdgpu_buffer_rsrc_t rsrc, int b)
-{
-    if (J.cn == 3) return __builtin_amdgcn_raw_buffer_load_b96(rsrc, b, 0, 0);
-    return (u32x3){__builtin_amdgcn_raw_buffer_load_b32(rsrc, b, 0, 0), 0u, 0u};
-}
-
-__device__ __forceinline__ u32x4 stage_unpack(int cn, u32x3 d)
-{
-    if (cn == 3) // 12 bytes BGR BGR BGR BGR -> four (B, G, R, 0) words
-        return (u32x4){d.x & 0xffffffu, __builtin_amdgcn_perm(d.y, d.x, 0x0C050403u),
-                       __builtin_amdgcn_perm(d.z, d.y, 0x0C040302u), d.z >> 8};
-    return (u32x4){d.x & 0xffu, __builtin_amdgcn_perm(0u, d.x, 0x0C0C0C01u), __builtin_amdgcn_perm(0u, d.x, 0x0C0C0C02u),
-                   d.x >> 24};
-}
-
-// Slow item (add_padding border / crop edge of a padded job / buffer end): per-pixel byte loads,
-// 0 outside the crop.
-__device__ __forceinline__ u32x4 stage_slow(const AugJob& J, __amdgpu_buffer_rsrc_t rsrc, int cy, int cx)
-{
-    uint32_t   px[4];
-    const bool row_ok = cy >= 0 && cy < J.crop_h;
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const int x = cx + k;
-        uint32_t  p = 0;
-        if (row_ok && x >= 0 && x < J.crop_w) {
-            const int b = (J.crop_y + cy) * J.src_stride + (J.crop_x + x) * J.cn;
-            for (int c = 0; c < J.cn; c++)
-                p |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rsrc, b + c, 0, 0) << (8 * c);
+    const int   lane = threadIdx.x & 63;
+    const int   cn   = J.cn;
+    const auto  rsrc = uniform_rsrc((const void*)J.src_ptr, (int)J.src_bytes);
+    const int   upr  = stage_units_per_row(J, G);
+    const int   Q    = G.nr * upr;
+    const float inv  = 1.f / (float)upr;
+    for (int i = wave; i * 64 < Q; i += nw) {
+        const int q    = i * 64 + lane;
+        uint32_t  voff = kOutOfRange;
+        if (q < Q) {
+            const int j = (int)(((float)q + 0.5f) * inv); // exact in f32 for q < 2^20
+            const int b = src_off(J, G, j, (q - j * upr) * (cn == 3 ? 4 : 1));
+            voff        = b >= 0 ? (uint32_t)b : kOutOfRange; // (padded jobs: fixed in stage_unpack)
         }
-        px[k] = p;
+        if (cn == 3) lds_dma<12>(rsrc, buf + i * 1024, voff);
+        else lds_dma<4>(rsrc, buf + i * 256, voff);
     }
-    return (u32x4){px[0], px[1], px[2], px[3]};
 }
 
-// Issue the loads of this lane's next kPrefetch items (fast items only) and advance the walk.
-__device__ __forceinline__ void stage_issue(const AugJob& J, __amdgpu_buffer_rsrc_t rsrc, const StageGeom& G,
-                                            const WalkStep& st, Walk& w, Prefetch& pf)
+// (2) After this wave's loads landed: unpack its BGR slots in place; zero border of a padded job;
+// re-read loads that crossed the end of the buffer (rare; uniformly skipped otherwise for gray).
+__device__ __forceinline__ void stage_unpack(cjob& J, const StageGeom& G, int buf, int wave, int nw)
 {
+    const int  lane      = threadIdx.x & 63;
+    const int  cn        = J.cn;
+    const int  src_bytes = (int)J.src_bytes;
+    const bool padded    = J.padded != 0;
+    const bool at_end    = src_off(J, G, G.nr - 1, G.pitch) + 12 > src_bytes;
+    if (cn != 3 && !padded && !at_end) return;
+    const int   upr = stage_units_per_row(J, G);
+    const int   Q   = G.nr * upr;
+    if (cn == 3 && !padded && !at_end) {
+        // common case: in-place unpack of this wave's slots, reads of several instructions in
+        // flight before their writes
+        int i = wave;
+        for (; (i + 2 * nw) * 64 < Q; i += 3 * nw) {
+            u32x4 w[3];
 #pragma unroll
-    for (int k = 0; k < kPrefetch; k++) {
-        pf.lds[k] = 0;
-        if (w.j < G.nr) {
-            const bool fast = stage_fast(J, G, w);
-            pf.lds[k]       = (uint32_t)w.lds | (fast ? 1u : 0u) | 2u;
-            if (fast) pf.d[k] = stage_load(J, rsrc, w.src);
-            walk_next(G, st, w);
+            for (int k = 0; k < 3; k++) w[k] = *lds_ptr<const u32x4>(buf + ((i + k * nw) * 64 + lane) * 16);
+#pragma unroll
+            for (int k = 0; k < 3; k++) {
+                const int q = (i + k * nw) * 64 + lane;
+                if (q < Q)
+                    *lds_ptr<u32x4>(buf + q * 16) =
+                        (u32x4){w[k].x & 0xffffffu, __builtin_amdgcn_perm(w[k].y, w[k].x, 0x0C050403u),
+                                __builtin_amdgcn_perm(w[k].z, w[k].y, 0x0C040302u), w[k].z >> 8};
+            }
+        }
+        for (; i * 64 < Q; i += nw) {
+            const int q = i * 64 + lane;
+            if (q >= Q) continue;
+            const auto  slot = lds_ptr<u32x4>(buf + q * 16);
+            const u32x4 w    = *slot;
+            *slot = (u32x4){w.x & 0xffffffu, __builtin_amdgcn_perm(w.y, w.x, 0x0C050403u),
+                            __builtin_amdgcn_perm(w.z, w.y, 0x0C040302u), w.z >> 8};
+        }
+        return;
+    }
+    const float inv = 1.f / (float)upr;
+    for (int i = wave; i * 64 < Q; i += nw) {
+        const int q = i * 64 + lane;
+        if (q >= Q) continue;
+        const int j  = (int)(((float)q + 0.5f) * inv);
+        const int u0 = (q - j * upr) * (cn == 3 ? 4 : 1); // first staged column of this unit
+        const int np = cn == 3 ? 4 : 1;                   // pixels of this unit
+        const int b  = src_off(J, G, j, u0);
+        const bool slow = padded || b < 0 || (at_end && b + (cn == 3 ? 12 : 4) > src_bytes);
+        if (cn == 3 && !slow) {
+            const auto slot = lds_ptr<u32x4>(buf + q * 16);
+            const u32x4 w   = *slot; // 12 bytes BGR BGR BGR BGR -> four (B, G, R, 0) words
+            *slot = (u32x4){w.x & 0xffffffu, __builtin_amdgcn_perm(w.y, w.x, 0x0C050403u),
+                            __builtin_amdgcn_perm(w.z, w.y, 0x0C040302u), w.z >> 8};
+        } else if (slow) {
+            const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)J.src_ptr, (short)0, src_bytes, 0x00020000);
+            for (int k = 0; k < np; k++) {
+                const int cy = G.v_lo + j + J.shift_y, cx = G.u_lo + u0 + k + J.shift_x;
+                uint32_t  p  = 0;
+                if (!padded || (cy >= 0 && cy < J.crop_h && cx >= 0 && cx < J.crop_w)) {
+                    const int bb = b + k * cn;
+                    if (bb >= 0)
+                        for (int c = 0; c < cn; c++)
+                            p |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rsrc, bb + c, 0, 0) << (8 * c);
+                }
+                *lds_ptr<uint32_t>(buf + (q * np + k) * 4) = p;
+            }
         }
     }
 }
 
-// Unpack / load-slow and write this batch's items to LDS.
-__device__ __forceinline__ void stage_commit(const AugJob& J, __amdgpu_buffer_rsrc_t rsrc, const StageGeom& G,
-                                             const Prefetch& pf, int stage_base, int pitch)
+// Pull the job descriptor of a future tile into L2 (an LDS-DMA into a sink nobody reads): its
+// scalar loads then hit L2 instead of paying an HBM round trip at the head of that tile.
+__device__ __forceinline__ void prefetch_job(const LaunchArgs& a, int t, int lds_sink)
 {
-#pragma unroll
-    for (int k = 0; k < kPrefetch; k++) {
-        const uint32_t m = pf.lds[k];
-        if (!(m & 2)) continue;
-        u32x4 q;
-        if (m & 1) {
-            q = stage_unpack(J.cn, pf.d[k]);
-        } else { // rare: recover (row, group) from the LDS address
-            const int o = (int)(m & ~3u) - stage_base;
-            const int j = o / (pitch * 4), g = (o - j * pitch * 4) >> 4;
-            q           = stage_slow(J, rsrc, G.v_lo + j + J.shift_y, G.u_lo + 4 * g + J.shift_x);
-        }
-        *(__attribute__((address_space(3))) u32x4*)(size_t)(m & ~3u) = q;
-    }
+    if (t >= a.total_tiles) return;
+    const int      job  = t / a.max_tiles;
+    const auto     rs   = uniform_rsrc((const void*)(a.jobs + job), (int)sizeof(AugJob));
+    const uint32_t lane = threadIdx.x & 63;
+    lds_dma<4>(rs, lds_sink, lane * 4 < sizeof(AugJob) ? lane * 4 : kOutOfRange);
 }
 
-// Stage a whole band: first batch already issued by the caller (pf, w), the rest here.
-__device__ __forceinline__ void stage_finish(const AugJob& J, __amdgpu_buffer_rsrc_t rsrc, const StageGeom& G,
-                                             const WalkStep& st, Walk& w, Prefetch& pf, int stage_base, int pitch)
+// Wait until at most n vector-memory instructions of this wave are outstanding (the immediate
+// must be a constant: buckets, rounding n down).
+__device__ __forceinline__ void wait_vm_upto(int n)
 {
-    stage_commit(J, rsrc, G, pf, stage_base, pitch);
-    while (w.j < G.nr) {
-        stage_issue(J, rsrc, G, st, w, pf);
-        stage_commit(J, rsrc, G, pf, stage_base, pitch);
-    }
+    if (n >= 48) asm volatile("s_waitcnt vmcnt(48)" ::: "memory");
+    else if (n >= 24) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+    else if (n >= 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    else if (n >= 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else if (n >= 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// Workgroup barrier that leaves vector-memory operations in flight (__syncthreads() would drain
+// vmcnt): LDS writes are made visible (lgkmcnt 0) and the compiler may not move memory
+// operations across it.
+__device__ __forceinline__ void lds_barrier()
+{
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
 }
 
 // Output cache policy: streaming stores (written once, read by the consumer of the batch).
@@ -336,7 +396,7 @@ __device__ __forceinline__ void store_f32x4(__amdgpu_buffer_rsrc_t r, int off, f
 // standardize LUT is addressed by (s & ~3) with no further shifts, and s >> 2 is the pixel.
 // (Photometric kernels take plain values.)
 template <int RM, bool SCALED>
-__device__ __forceinline__ void resize_px(int4 ytr, int col, uint32_t wx, int s[3])
+__device__ __forceinline__ void resize_px(i32x4 ytr, int col, uint32_t wx, int s[3])
 {
     const int a0 = ytr.x + col;
     if (RM == RESIZE_LINEAR) {
@@ -380,7 +440,7 @@ __device__ __forceinline__ void resize_px(int4 ytr, int col, uint32_t wx, int s[
 
 // Elements of OpenCV's scalar row tail (e >= xv) use FixedPtCast<int, uchar, 22> instead.
 template <bool SCALED>
-__device__ __forceinline__ void tail_fix(int4 ytr, int col, uint32_t wx, int e0, int xv, int s[3])
+__device__ __forceinline__ void tail_fix(i32x4 ytr, int col, uint32_t wx, int e0, int xv, int s[3])
 {
     const uint32_t p00 = lds_ld(ytr.x + col), p01 = lds_ld(ytr.x + col + 4);
     const uint32_t p10 = lds_ld(ytr.y + col), p11 = lds_ld(ytr.y + col + 4);
@@ -394,158 +454,150 @@ __device__ __forceinline__ void tail_fix(int4 ytr, int col, uint32_t wx, int e0,
 }
 
 // standardize LUT (LDS offset 0) entry for source channel c at scaled value s
+#ifdef AEON_HIP_EXP_NOLUT // development ablation: no LUT reads (wrong values)
+__device__ __forceinline__ float lut_at(int c, int s) { return (float)(s + c); }
+#else
 __device__ __forceinline__ float lut_at(int c, int s) { return lds_ldf(c * 1024 + (s & ~3)); }
+#endif
 
 enum OutForm : int { OF_F32_CHW_VEC = 0, OF_GENERIC = 1 };
 
-// ---- the tile kernel -----------------------------------------------------------------------
-// One workgroup = one chunk of rows_per_chunk output rows of one job, processed in bands of
-// rows_per_tile rows through double-buffered LDS.
-// KM: KM_FINAL (full record -> loader output), KM_STATS (contrast sums only), KM_RAW (resize
-// only, HWC uint8: the resize_short pre-pass).  RM: ResizeMode of every job in the launch.
-// PHOTO: the launch's jobs carry photometric work.  OF: output form (OF_F32_CHW_VEC = float32
-// CHW planes, win_w % 4 == 0, 16-byte aligned items: the ImageNet configuration).
-// TAIL: some LINEAR job of the launch has OpenCV scalar-tail columns (3*dst_w not covered by the
-// SIMD loops); kept out of the common kernels, whose registers it would otherwise inflate.
+// ---- the band kernel -----------------------------------------------------------------------
+// A launch covers n_jobs x max_tiles tiles: tile t = band (t % max_tiles) of job (t / max_tiles),
+// a band being TR consecutive output rows of the job's window.  Workgroups are persistent (the
+// host sizes the grid to what the CUs hold at once) and take tiles blockIdx.x, +gridDim.x, ...
+// Per tile, with two LDS staging buffers:
+//   issue the LDS-DMA staging of the NEXT tile (and build its row / column tap tables) ->
+//   compute and store the current tile from LDS -> counted vmcnt wait that retires the next
+//   tile's loads but not this tile's stores -> unpack own slots -> barrier.
+// A workgroup = 256..512 lanes holding whole 4-pixel column groups of the window (448 = 8 x 56
+// for 224-wide outputs); a lane keeps the same four output columns for the whole tile, so their
+// resize taps, LDS byte offsets, flip and scalar-tail masks stay in registers, and writes each
+// output plane row segment with one 16-byte store per channel.
+// KM: KM_FINAL (full record -> loader output), KM_STATS (contrast pass 1: resize + brightness/
+// saturation + hue into an HWC uint8 intermediate + exact per-(tile, wave) channel sums), KM_RAW
+// (resize only, HWC uint8: the pre-passes).  RM: ResizeMode of every job in the launch.  PHOTO:
+// the launch's jobs carry photometric work.  OF: output form (OF_F32_CHW_VEC = float32 CHW planes,
+// win_w % 4 == 0, 16-byte aligned items: the ImageNet configuration).  TAIL: some LINEAR job of the
+// launch has OpenCV scalar-tail columns (3*dst_w not covered by the SIMD loops).
+
+
 template <int KM, int RM, bool PHOTO, int OF, bool TAIL>
-__global__ __launch_bounds__(kBlockMax, AEON_HIP_MIN_WAVES) void augment_tiles(LaunchArgs a)
-{
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    if ((uint32_t)(size_t)(__attribute__((address_space(3))) char*)smem != 0u) { // see lds_ld
-        if (threadIdx.x == 0) atomicOr(a.error, 4);
-        return;
-    }
-    // The job descriptor is copied to registers before any store: the pixel loop then issues
-    // no global loads except the next band's staging, so stores rarely make a load wait.
-    const AugJob J     = a.jobs[blockIdx.y];
-    const int    chunk = blockIdx.x;
-    if (chunk >= J.tiles) return;
-    if (KM == KM_STATS && J.stats_slot < 0) return;
+struct Bands {
+    const LaunchArgs& a;
+    const LdsLayout&  L;
+    int               wave, nw;
 
-    const int TR    = a.rows_per_tile;
-    const int c0    = chunk * a.rows_per_chunk;
-    const int c1    = min(c0 + a.rows_per_chunk, J.win_h);
-    const int tid   = threadIdx.x;
-    const int nt    = blockDim.x;
-    const int cn    = J.cn;
-    const int win_w = J.win_w;
-
-    const LdsLayout L     = lds_layout(a.max_win_w, TR, a.stage_rows, a.stage_pitch, PHOTO && a.has_hue);
-    float*          lut   = (float*)(smem + L.lut); // offset 0: immediate-offset reads per channel
-    int32_t*        sdiv  = (int32_t*)(smem + L.hsv);
-    int32_t*        hdiv  = sdiv + 256;
-    int2*           xt    = (int2*)(smem + L.xt);
-    int4*           yt0   = (int4*)(smem + L.yt);
-    int32_t*        red   = (int32_t*)(smem + L.red);
-    double*         shift = (double*)(smem + L.red + 128);
-    const int       pitch = a.stage_pitch;
-
-    // source columns (the same for every band; taps are monotone in dx)
-    const XTap xf = xcoef<RM>(J.win_x, J.scale_x, J.crop_w);
-    const XTap xl = xcoef<RM>(J.win_x + win_w - 1, J.scale_x, J.crop_w);
-    const int  two_tap = (RM == RESIZE_LINEAR || RM == RESIZE_AREA2X) ? 1 : 0;
-    StageGeom  G;
-    G.u_lo   = xf.sx;
-    G.nc     = xl.sx + two_tap - G.u_lo + 1;
-    G.groups = (G.nc + 3) >> 2;
-    if (G.nc > pitch || win_w > a.max_win_w) {
-        if (tid == 0) atomicOr(a.error, 1);
-        return;
-    }
-    auto band_rows = [&](int y0, StageGeom& g) { // rows of the band starting at window row y0
-        const int n = min(TR, c1 - y0);
-        g.v_lo      = ycoef<RM>(J.win_y + y0, J.scale_y, J.crop_h).r0;
-        g.nr        = ycoef<RM>(J.win_y + y0 + n - 1, J.scale_y, J.crop_h).r1 - g.v_lo + 1;
-        return n;
+    // uniform: tile t -> (job, band) with work, and its staged-source geometry
+    struct Info {
+        bool      ok;
+        int       job, band, y0, nrows;
+        StageGeom G;
     };
-    auto build_yt = [&](int y0, int n, const StageGeom& g, int4* yt) {
-        for (int r = tid; r < n; r += nt) {
-            const YTap t = ycoef<RM>(J.win_y + y0 + r, J.scale_y, J.crop_h);
-            yt[r]        = make_int4(L.stage + (t.r0 - g.v_lo) * pitch * 4, L.stage + (t.r1 - g.v_lo) * pitch * 4,
-                                     t.b0, t.b1);
+    __device__ __forceinline__ Info info(int t) const
+    {
+        Info f;
+        f.ok   = false;
+        f.job  = t / a.max_tiles;
+        f.band = t - f.job * a.max_tiles;
+        cjob& J = job_ref(a, f.job);
+        if (f.band >= J.tiles) return f;
+        if (KM == KM_STATS && J.stats_slot < 0) return f;
+        const int TR = a.rows_per_tile;
+        f.y0         = f.band * TR;
+        f.nrows      = min(TR, J.win_h - f.y0);
+        // source columns (taps are monotone in dx)
+        const XTap xf      = xcoef<RM>(J.win_x, J.scale_x, J.crop_w);
+        const XTap xl      = xcoef<RM>(J.win_x + J.win_w - 1, J.scale_x, J.crop_w);
+        const int  two_tap = (RM == RESIZE_LINEAR || RM == RESIZE_AREA2X) ? 1 : 0;
+        StageGeom& G       = f.G;
+        G.u_lo  = xf.sx;
+        G.nc    = xl.sx + two_tap - G.u_lo + 1;
+        G.ng    = (G.nc + 3) >> 2;
+        G.pitch = 4 * G.ng;
+        G.v_lo  = ycoef<RM>(J.win_y + f.y0, J.scale_y, J.crop_h).r0;
+        G.nr    = ycoef<RM>(J.win_y + f.y0 + f.nrows - 1, J.scale_y, J.crop_h).r1 - G.v_lo + 1;
+        // whole DMA instructions: 64 groups (1 KiB) or 64 gray pixels (256 B)
+        const int need = J.cn == 3 ? (G.nr * G.ng + 63) / 64 * 1024 : (G.nr * G.pitch + 63) / 64 * 256;
+        if (need > L.stage_bytes || J.win_w > a.max_win_w || f.nrows <= 0) {
+            if (threadIdx.x == 0) atomicOr(a.error, 2);
+            return f;
         }
-    };
-
-    const __amdgpu_buffer_rsrc_t srsrc =
-        __builtin_amdgcn_make_buffer_rsrc((void*)J.src_ptr, (short)0, (int)J.src_bytes, 0x00020000);
-    // band 0 loads go out first; the tables below are built while they are in flight
-    Prefetch pf;
-    Walk     wk;
-    WalkStep ws;
-    int      n0 = band_rows(c0, G);
-    if (G.nr > a.stage_rows) {
-        if (tid == 0) atomicOr(a.error, 2);
-        return;
+        f.ok = true;
+        return f;
     }
-    walk_init(J, G, tid, pitch, L.stage, nt, wk, ws);
-    stage_issue(J, srsrc, G, ws, wk, pf);
 
-    for (int x = tid; x < win_w; x += nt) {
-        const XTap t = xcoef<RM>(J.win_x + x, J.scale_x, J.crop_w);
-        xt[x]        = make_int2(t.sx - G.u_lo, (t.a0 & 0xffff) | (t.a1 << 16));
-    }
-    const int photo = (PHOTO && KM != KM_RAW && cn == 3) ? J.photo : 0;
-    if (photo & PHOTO_HUE)
-        for (int i = tid; i < 512; i += nt) sdiv[i] = a.hsv_tables[i];
-    const bool use_lut = KM == KM_FINAL && a.out_dtype == OUT_F32 && a.lut != nullptr;
-    if (use_lut)
-        for (int i = tid; i < 3 * 256; i += nt) lut[i] = a.lut[i];
-    if (KM == KM_FINAL && (photo & PHOTO_CONTRAST) && tid < 64) {
-        // reduce the exact per-chunk channel sums of this image (written by KM_STATS)
-        unsigned long long s0 = 0, s1 = 0, s2 = 0;
-        for (int t = tid; t < J.stats_tiles; t += 64) {
-            const uint32_t* p = a.partials + ((size_t)J.stats_slot * a.partial_stride + t) * 4;
-            s0 += p[0], s1 += p[1], s2 += p[2];
+    // Stage a tile into buffer b (loads in flight on return) and build its row taps; its column
+    // taps too unless buffer b already holds this job's (consecutive tiles of one record).
+    __device__ __forceinline__ void prep(const Info& f, int b, bool build_xt) const
+    {
+        if (!f.ok) return;
+        cjob&      J     = job_ref(a, f.job);
+        const StageGeom& G = f.G;
+        const int  stage = L.stage + b * L.stage_bytes;
+        stage_issue(J, G, stage, wave, nw);
+        const int  tid = threadIdx.x, nt = blockDim.x;
+        if (build_xt) {
+            const auto xt = lds_ptr<i32x2>(L.xt) + b * a.max_win_w;
+            for (int x = tid; x < J.win_w; x += nt) {
+                const XTap c = xcoef<RM>(J.win_x + x, J.scale_x, J.crop_w);
+                xt[x]        = (i32x2){c.sx - G.u_lo, (c.a0 & 0xffff) | (c.a1 << 16)};
+            }
         }
-        for (int o = 32; o > 0; o >>= 1) {
-            s0 += __shfl_xor(s0, o);
-            s1 += __shfl_xor(s1, o);
-            s2 += __shfl_xor(s2, o);
-        }
-        if (tid == 0) {
-            // cv::mean = sum * (1./N); (1.0 - c) * mean, kept in f64
-            const double inv_n = 1. / (double)(J.win_w * J.win_h);
-            const double k     = 1.0 - (double)J.contrast;
-            shift[0] = k * ((double)s0 * inv_n);
-            shift[1] = k * ((double)s1 * inv_n);
-            shift[2] = k * ((double)s2 * inv_n);
+        const auto yt = lds_ptr<i32x4>(L.yt) + b * a.rows_per_tile;
+        for (int r = tid; r < f.nrows; r += nt) {
+            const YTap y = ycoef<RM>(J.win_y + f.y0 + r, J.scale_y, J.crop_h);
+            yt[r]        = (i32x4){stage + (y.r0 - G.v_lo) * G.pitch * 4, stage + (y.r1 - G.v_lo) * G.pitch * 4, y.b0, y.b1};
         }
     }
-    build_yt(c0, n0, G, yt0);
-    stage_finish(J, srsrc, G, ws, wk, pf, L.stage, pitch);
-    __syncthreads();
 
-    uint32_t sum0 = 0, sum1 = 0, sum2 = 0;
-    double   sh0 = 0, sh1 = 0, sh2 = 0;
-    if (KM == KM_FINAL && (photo & PHOTO_CONTRAST)) sh0 = shift[0], sh1 = shift[1], sh2 = shift[2];
+    __device__ __forceinline__ void unpack(const Info& f, int b) const
+    {
+        if (f.ok) stage_unpack(job_ref(a, f.job), f.G, L.stage + b * L.stage_bytes, wave, nw);
+    }
 
-    const int  elem  = (KM != KM_FINAL || a.out_dtype == OUT_U8) ? 1 : 4;
-    const int  plane = win_w * J.win_h;
-    const auto orsrc = __builtin_amdgcn_make_buffer_rsrc((void*)J.out_ptr, (short)0,
-                                                         plane * cn * elem, 0x00020000);
-    const bool tail  = TAIL && RM == RESIZE_LINEAR && J.xv < J.dst_w * cn; // OpenCV scalar row tail
-    const int  wx0   = J.win_x;
-    const int  xv    = J.xv;
-    const int  flip  = J.flip;
-    const int  bgr   = a.bgr_to_rgb && cn == 3;
-    // Lane -> (column group, row phase), fixed for the chunk: a lane's four output columns and
-    // their taps stay in registers while it walks the band's rows.
-    const int  gpr    = (win_w + 3) >> 2;
-    const int  ncg    = min(gpr, nt);
-    const int  nph    = nt / ncg;
-    const int  lph    = tid / ncg;
-    const int  lcg    = tid - lph * ncg;
-    const bool active = lph < nph;
-    // values carried from the resize to the store: 4x scaled (see resize_px) unless photometric
-    constexpr bool SC = !PHOTO;
-    auto lut_of       = [&](int c, int v) { return lut_at(c, SC ? v : v << 2); };
-    auto u8_of        = [&](int v) { return SC ? v >> 2 : v; };
+    // Compute and store tile t from buffer b.  Returns a lower bound on the vector-memory
+    // instructions this wave issued (its stores): all younger than the next tile's staging loads.
+    __device__ __forceinline__ int compute(const Info& f, int b) const
+    {
+        if (!f.ok) return 0;
+        const int  band = f.band, y0 = f.y0, nrows = f.nrows;
+        cjob&      J     = job_ref(a, f.job);
+        const int  tid   = threadIdx.x;
+        const int  nt    = blockDim.x;
+        const int  cn    = J.cn;
+        const int  win_w = J.win_w;
+        const auto xt    = lds_ptr<const i32x2>(L.xt) + b * a.max_win_w;
+        const auto yt    = lds_ptr<const i32x4>(L.yt) + b * a.rows_per_tile;
+        const auto sdiv  = lds_ptr<const int32_t>(L.hsv);
+        const auto hdiv  = sdiv + 256;
+        const int  photo = (PHOTO && KM != KM_RAW && cn == 3) ? J.photo : 0;
+        double     sh0 = 0, sh1 = 0, sh2 = 0;
+        if (KM == KM_FINAL && (photo & PHOTO_CONTRAST)) {
+            const double* sh = a.shifts + (size_t)J.stats_slot * 4;
+            sh0 = sh[0], sh1 = sh[1], sh2 = sh[2];
+        }
+        uint32_t sum0 = 0, sum1 = 0, sum2 = 0;
 
-    int buf = 0;
-    for (int y0 = c0; y0 < c1; y0 += TR) {
-        const int   nrows = min(TR, c1 - y0);
-        const int4* yt    = yt0 + buf * TR;
-        const bool has_next = y0 + TR < c1;
+        const int  elem  = (KM != KM_FINAL || a.out_dtype == OUT_U8) ? 1 : 4;
+        const int  plane = win_w * J.win_h;
+        const auto orsrc = __builtin_amdgcn_make_buffer_rsrc((void*)J.out_ptr, (short)0, plane * cn * elem, 0x00020000);
+        const bool tail  = TAIL && RM == RESIZE_LINEAR && J.xv < J.dst_w * cn; // OpenCV scalar row tail
+        const int  wx0   = J.win_x;
+        const int  xv    = J.xv;
+        const int  flip  = J.flip;
+        const int  bgr   = a.bgr_to_rgb && cn == 3;
+        // Lane -> (column group, row phase), fixed for the tile
+        const int  gpr    = (win_w + 3) >> 2;
+        const int  ncg    = min(gpr, nt);
+        const int  nph    = nt / ncg;
+        const int  lph    = tid / ncg;
+        const int  lcg    = tid - lph * ncg;
+        const bool active = lph < nph;
+        // values carried from the resize to the store: 4x scaled (see resize_px) unless photometric
+        constexpr bool SC = !PHOTO;
+        auto lut_of = [&](int c, int v) { return lut_at(c, SC ? v : v << 2); };
+        auto u8_of  = [&](int v) { return SC ? v >> 2 : v; };
 
         for (int cg = active ? lcg : gpr; cg < gpr; cg += ncg) {
             const int ox0 = cg * 4;
@@ -558,17 +610,23 @@ __global__ __launch_bounds__(kBlockMax, AEON_HIP_MIN_WAVES) void augment_tiles(L
                 // columns past the window edge recompute the last one (never stored)
                 const int  ox  = min(ox0 + k, win_w - 1);
                 const int  x   = flip ? win_w - 1 - ox : ox;
-                const int2 xtt = xt[x];
+                const i32x2 xtt = xt[x];
                 col[k]         = xtt.x * 4; // byte offset in a staged row
                 wxk[k]         = (uint32_t)xtt.y;
                 if (TAIL && RM == RESIZE_LINEAR && tail && (wx0 + x) * cn + 2 >= xv) tmask |= 1 << k;
             }
             for (int ry = lph; ry < nrows; ry += nph) {
-                const int4 ytr = yt[ry];
-                const int  y   = y0 + ry; // window row
-                int        val[4][3];
+                const i32x4 ytr = yt[ry];
+                const int   y   = y0 + ry; // window row
+                int         val[4][3];
 #pragma unroll
-                for (int k = 0; k < 4; k++) resize_px<RM, SC>(ytr, col[k], wxk[k], val[k]);
+                for (int k = 0; k < 4; k++) {
+#ifdef AEON_HIP_EXP_NORESIZE // development ablation: no gathers / resize math (wrong values)
+                    val[k][0] = ytr.x + col[k], val[k][1] = ytr.y + col[k], val[k][2] = ytr.z + (int)wxk[k];
+#else
+                    resize_px<RM, SC>(ytr, col[k], wxk[k], val[k]);
+#endif
+                }
                 if (TAIL && RM == RESIZE_LINEAR && tmask) {
 #pragma unroll
                     for (int k = 0; k < 4; k++)
@@ -581,27 +639,27 @@ __global__ __launch_bounds__(kBlockMax, AEON_HIP_MIN_WAVES) void augment_tiles(L
                 if (PHOTO && photo) {
 #pragma unroll
                     for (int k = 0; k < 4; k++) {
-                        int b = val[k][0], g = val[k][1], r = val[k][2];
-                        if (photo & PHOTO_BS) bs_apply(J, b, g, r);
-                        if (photo & PHOTO_HUE) hue_apply(sdiv, hdiv, J.hue, b, g, r);
+                        int bb = val[k][0], gg = val[k][1], rr = val[k][2];
+                        if (photo & PHOTO_BS) bs_apply(J, bb, gg, rr);
+                        if (photo & PHOTO_HUE) hue_apply(sdiv, hdiv, J.hue, bb, gg, rr);
                         if (KM == KM_STATS) { // the intermediate keeps the post-hue pixel
-                            if (k < nk) sum0 += b, sum1 += g, sum2 += r;
-                            val[k][0] = b, val[k][1] = g, val[k][2] = r;
+                            if (k < nk) sum0 += bb, sum1 += gg, sum2 += rr;
+                            val[k][0] = bb, val[k][1] = gg, val[k][2] = rr;
                             continue;
                         }
                         if (photo & PHOTO_CONTRAST) {
                             const float c = J.contrast;
-                            b = sat_u8(rnd((float)((double)((float)b * c + 0.f) + sh0)));
-                            g = sat_u8(rnd((float)((double)((float)g * c + 0.f) + sh1)));
-                            r = sat_u8(rnd((float)((double)((float)r * c + 0.f) + sh2)));
+                            bb = sat_u8(rnd((float)((double)((float)bb * c + 0.f) + sh0)));
+                            gg = sat_u8(rnd((float)((double)((float)gg * c + 0.f) + sh1)));
+                            rr = sat_u8(rnd((float)((double)((float)rr * c + 0.f) + sh2)));
                         }
                         if (photo & PHOTO_LIGHTING) {
                             const float la = J.light_a;
-                            b = sat_u8(sat_u8(rnd((float)b * la + 0.f)) + J.light_add[0]);
-                            g = sat_u8(sat_u8(rnd((float)g * la + 0.f)) + J.light_add[1]);
-                            r = sat_u8(sat_u8(rnd((float)r * la + 0.f)) + J.light_add[2]);
+                            bb = sat_u8(sat_u8(rnd((float)bb * la + 0.f)) + J.light_add[0]);
+                            gg = sat_u8(sat_u8(rnd((float)gg * la + 0.f)) + J.light_add[1]);
+                            rr = sat_u8(sat_u8(rnd((float)rr * la + 0.f)) + J.light_add[2]);
                         }
-                        val[k][0] = b, val[k][1] = g, val[k][2] = r;
+                        val[k][0] = bb, val[k][1] = gg, val[k][2] = rr;
                         __builtin_amdgcn_sched_barrier(0); // one pixel's chain live at a time
                     }
                 }
@@ -637,6 +695,9 @@ __global__ __launch_bounds__(kBlockMax, AEON_HIP_MIN_WAVES) void augment_tiles(L
 #pragma unroll
                     for (int c = 0; c < 3; c++) {
                         const int oc = bgr ? 2 - c : c;
+#ifdef AEON_HIP_EXP_NOSTORE // development ablation: no output stores
+                        if (lut_of(c, val[0][c]) == 1234.5f)
+#endif
                         store_f32x4(orsrc, (oc * plane + idx) * 4, lut_of(c, val[0][c]), lut_of(c, val[1][c]),
                                     lut_of(c, val[2][c]), lut_of(c, val[3][c]));
                         // one channel's four LUT reads in flight at a time: hoisting all twelve
@@ -663,43 +724,139 @@ __global__ __launch_bounds__(kBlockMax, AEON_HIP_MIN_WAVES) void augment_tiles(L
                 }
             }
         }
-        if (has_next) {
-            // Next band: loaded only now.  Prefetching it during this band's compute would not
-            // hide its latency -- waiting for those loads also waits for this band's stores (one
-            // vector-memory counter) -- and would hold ~15 VGPRs across the pixel loop.
-            StageGeom Gn = G;
-            const int nn = band_rows(y0 + TR, Gn);
-            if (Gn.nr > a.stage_rows) {
-                if (tid == 0) atomicOr(a.error, 2);
-                return; // uniform: every lane sees the same band geometry
-            }
-            Walk     wn;
-            WalkStep sn;
-            Prefetch pn;
-            walk_init(J, Gn, tid, pitch, L.stage, nt, wn, sn);
-            stage_issue(J, srsrc, Gn, sn, wn, pn);
-            build_yt(y0 + TR, nn, Gn, yt0 + (buf ^ 1) * TR);
-            __syncthreads(); // single staging buffer: everyone is done reading it
-            stage_finish(J, srsrc, Gn, sn, wn, pn, L.stage, pitch);
-            __syncthreads();
-        }
-        buf ^= 1;
-    }
 
-    if (KM == KM_STATS) {
-        for (int o = 32; o > 0; o >>= 1) {
-            sum0 += __shfl_xor(sum0, o);
-            sum1 += __shfl_xor(sum1, o);
-            sum2 += __shfl_xor(sum2, o);
+        if (KM == KM_STATS) { // exact per-(tile, wave) sums; unused wave slots are zeroed
+            for (int o = 32; o > 0; o >>= 1) {
+                sum0 += __shfl_xor(sum0, o);
+                sum1 += __shfl_xor(sum1, o);
+                sum2 += __shfl_xor(sum2, o);
+            }
+            const int lane = tid & 63;
+            uint32_t* p    = a.partials + ((size_t)J.stats_slot * a.partial_stride + (size_t)band * 8) * 4;
+            if (lane == 0) p[wave * 4 + 0] = sum0, p[wave * 4 + 1] = sum1, p[wave * 4 + 2] = sum2;
+            if (wave == 0 && lane >= nw && lane < 8) p[lane * 4 + 0] = p[lane * 4 + 1] = p[lane * 4 + 2] = 0;
         }
-        const int wave = tid >> 6, lane = tid & 63;
-        if (lane == 0) red[wave * 4 + 0] = sum0, red[wave * 4 + 1] = sum1, red[wave * 4 + 2] = sum2;
-        __syncthreads();
-        if (tid < 3) {
-            uint32_t s = 0;
-            for (int wv = 0; wv < (nt + 63) / 64; wv++) s += (uint32_t)red[wv * 4 + tid];
-            a.partials[((size_t)J.stats_slot * a.partial_stride + chunk) * 4 + tid] = s;
+        // stores per wave when every lane is busy on whole rows of whole 4-pixel groups (one row
+        // set of nrows / nph rows per lane): 3 per row for float32 planes, 1 (a 12-byte group)
+        // for the HWC uint8 intermediates; otherwise 0 (the caller then drains everything)
+        const bool regular = ncg == gpr && nt % ncg == 0 && (win_w & 3) == 0 && nrows % nph == 0;
+        const int  per_row = (KM == KM_FINAL && OF == OF_F32_CHW_VEC) ? 3 : ((KM != KM_FINAL && cn == 3) ? 1 : 0);
+        return regular ? per_row * (nrows / nph) : 0;
+    }
+};
+
+template <int KM, int RM, bool PHOTO, int OF, bool TAIL>
+__global__ __launch_bounds__(kBlockMax, AEON_HIP_MIN_WAVES) void augment_tiles(LaunchArgs a)
+{
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    if ((uint32_t)(size_t)(__attribute__((address_space(3))) char*)smem != 0u) { // see lds_ld
+        if (threadIdx.x == 0) atomicOr(a.error, 4);
+        return;
+    }
+    const int       tid = threadIdx.x, nt = blockDim.x;
+    const int       wave = __builtin_amdgcn_readfirstlane(tid >> 6), nw = nt >> 6;
+    const LdsLayout L = lds_layout(a.max_win_w, a.rows_per_tile, a.stage_bytes, PHOTO && a.has_hue, a.stage_buffers);
+    const Bands<KM, RM, PHOTO, OF, TAIL> W{a, L, wave, nw};
+
+    // per-launch tables
+    if (KM == KM_FINAL && a.out_dtype == OUT_F32) {
+        const auto lut = lds_ptr<float>(L.lut);
+        for (int i = tid; i < 3 * 256; i += nt) lut[i] = a.lut[i];
+    }
+    if (PHOTO && KM != KM_RAW && a.has_hue) {
+        const auto hsv = lds_ptr<int32_t>(L.hsv);
+        for (int i = tid; i < 512; i += nt) hsv[i] = a.hsv_tables[i];
+    }
+    // static schedule: tiles blockIdx.x, +G, +2G, ... -- the tiles in flight at any moment are
+    // consecutive bands of a few records (measured faster than contiguous ranges per workgroup,
+    // and than a counter-fed dynamic schedule, whose fetch-ahead leaves the same tail)
+    const int T   = a.total_tiles, G = gridDim.x;
+    int       t   = blockIdx.x;
+    int       buf = 0;
+    // development: s_memtime stamps per (workgroup, iteration, phase) when a.trace is set;
+    // s_memrealtime (chip-wide 100 MHz) at entry and exit
+    auto stamp = [&](int it, int ph) {
+        if (a.trace && tid == 0 && it < 16)
+            a.trace[(blockIdx.x * 16 + it) * 8 + ph] = (uint32_t)__builtin_amdgcn_s_memtime();
+    };
+    if (a.trace && tid == 0) a.trace[(blockIdx.x * 16) * 8 + 7] = (uint32_t)__builtin_amdgcn_s_memrealtime();
+    using Info = typename Bands<KM, RM, PHOTO, OF, TAIL>::Info;
+    if (a.stage_buffers == 1) {
+        // one buffer (compute-heavy photometric launches, more rows per tile): stage, wait,
+        // compute; the CU's other workgroups cover the latency
+        for (; t < T; t += G) {
+            const Info f = W.info(t);
+            if (wave == 0) prefetch_job(a, t + G, L.pf);
+            W.prep(f, 0, true);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            W.unpack(f, 0);
+            __syncthreads();
+            W.compute(f, 0);
+            lds_barrier(); // everyone is done reading the buffer before it is refilled
         }
+        return;
+    }
+    Info cur = W.info(t < T ? t : 0);
+    if (t < T) {
+        if (wave == 0) prefetch_job(a, t + G, L.pf);
+        W.prep(cur, 0, true);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        W.unpack(cur, 0);
+    }
+    __syncthreads();
+    for (int it = 0; t < T; t += G, it++) {
+        const bool more = t + G < T;
+        Info       nxt  = cur;
+        stamp(it, 0);
+        if (more) {
+            if (wave == 0) prefetch_job(a, t + 2 * G, L.pf);
+            nxt = W.info(t + G);
+            W.prep(nxt, buf ^ 1, true); // lands during this tile's compute
+        }
+        stamp(it, 1);
+        const int stores = W.compute(cur, buf);
+        stamp(it, 2);
+        if (!more) break;
+        // the next tile's loads were issued before this tile's stores: retire them, not the stores
+        wait_vm_upto(stores);
+        stamp(it, 3);
+        W.unpack(nxt, buf ^ 1);
+        stamp(it, 4);
+        lds_barrier();
+        stamp(it, 5);
+        buf ^= 1;
+        cur = nxt;
+    }
+    if (a.trace && tid == 0) a.trace[(blockIdx.x * 16 + 1) * 8 + 7] = (uint32_t)__builtin_amdgcn_s_memrealtime();
+}
+
+// Contrast pass 2 prologue: per stats slot, (1-c)*mean per channel from the exact per-(tile,
+// wave) sums of pass 1 (cv::mean = sum * (1./N), kept in f64).  One 64-lane workgroup per job
+// of the pass-2 launch.
+__global__ __launch_bounds__(64) void contrast_reduce(LaunchArgs a, int n_jobs)
+{
+    const int job = blockIdx.x;
+    if (job >= n_jobs) return;
+    cjob& J = job_ref(a, job);
+    if (J.stats_slot < 0 || J.cn != 3 || !(J.photo & PHOTO_CONTRAST)) return;
+    const int          tid = threadIdx.x;
+    unsigned long long s0 = 0, s1 = 0, s2 = 0;
+    for (int e = tid; e < J.stats_tiles * 8; e += 64) {
+        const uint32_t* p = a.partials + ((size_t)J.stats_slot * a.partial_stride + e) * 4;
+        s0 += p[0], s1 += p[1], s2 += p[2];
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        s0 += __shfl_xor(s0, o);
+        s1 += __shfl_xor(s1, o);
+        s2 += __shfl_xor(s2, o);
+    }
+    if (tid == 0) {
+        const double inv_n = 1. / (double)(J.win_w * J.win_h);
+        const double k     = 1.0 - (double)J.contrast;
+        double*      sh    = a.shifts + (size_t)J.stats_slot * 4;
+        sh[0] = k * ((double)s0 * inv_n);
+        sh[1] = k * ((double)s1 * inv_n);
+        sh[2] = k * ((double)s2 * inv_n);
     }
 }
 
@@ -742,14 +899,28 @@ KernelFn pick_kernel(int km, int rm, bool tail, bool photo, int of)
     return pick_rm<KM_RAW>(rm, tail, false, OF_GENERIC);
 }
 
-hipError_t launch_tiles(int km, int rm, bool tail, bool photo, const LaunchArgs& a, int n_jobs, hipStream_t stream)
+int out_form(const LaunchArgs& a) { return (a.out_dtype == OUT_F32 && a.channel_major && a.vec_ok) ? OF_F32_CHW_VEC : OF_GENERIC; }
+
+hipError_t launch_tiles(int km, int rm, bool tail, bool photo, const LaunchArgs& a, int grid, hipStream_t stream)
 {
-    const int      of = (a.out_dtype == OUT_F32 && a.channel_major && a.vec_ok) ? OF_F32_CHW_VEC : OF_GENERIC;
-    const KernelFn fn = pick_kernel(km, rm, tail, photo, of);
+    const KernelFn fn = pick_kernel(km, rm, tail, photo, out_form(a));
     if (!fn) return hipErrorInvalidDeviceFunction;
-    dim3 grid(a.max_tiles, n_jobs), block(a.threads);
-    hipLaunchKernelGGL(fn, grid, block, a.lds_bytes, stream, a);
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(a.threads), a.lds_bytes, stream, a);
     return hipGetLastError();
+}
+
+hipError_t launch_contrast_reduce(const LaunchArgs& a, int n_jobs, hipStream_t stream)
+{
+    hipLaunchKernelGGL(contrast_reduce, dim3(n_jobs), dim3(64), 0, stream, a, n_jobs);
+    return hipGetLastError();
+}
+
+// Workgroups of this kernel form one CU holds at once (persistent grid sizing).
+hipError_t kernel_occupancy(int km, int rm, bool tail, bool photo, const LaunchArgs& a, int* blocks)
+{
+    const KernelFn fn = pick_kernel(km, rm, tail, photo, out_form(a));
+    if (!fn) return hipErrorInvalidDeviceFunction;
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, (const void*)fn, a.threads, a.lds_bytes);
 }
 
 hipError_t set_kernel_lds_limit(int bytes)

@@ -21,7 +21,9 @@
 #include "param_factory.hpp"
 
 namespace aeon_hip {
-hipError_t launch_tiles(int km, int rm, bool tail, bool photo, const LaunchArgs& a, int n_jobs, hipStream_t stream);
+hipError_t launch_tiles(int km, int rm, bool tail, bool photo, const LaunchArgs& a, int grid, hipStream_t stream);
+hipError_t launch_contrast_reduce(const LaunchArgs& a, int n_jobs, hipStream_t stream);
+hipError_t kernel_occupancy(int km, int rm, bool tail, bool photo, const LaunchArgs& a, int* blocks);
 hipError_t set_kernel_lds_limit(int bytes);
 hipError_t launch_transpose(const void* src, void* dst, int64_t rows, int64_t cols, int element_size,
                             hipStream_t stream);
@@ -47,9 +49,8 @@ struct aeon_error : std::runtime_error {
     } while (0)
 
 constexpr int kMaxLds        = 160 * 1024;
-constexpr int kStageBudget   = 48 * 1024;   // preferred LDS bytes per staged band
-constexpr int kStageBudgetHi = 120 * 1024;  // fallback for very wide crops
-constexpr int kBandsPerChunk = 1;
+constexpr int kStageBudget   = 48 * 1024;   // preferred LDS bytes of the two staging buffers
+constexpr int kStageBudgetHi = 140 * 1024;  // fallback for very wide crops
 
 // ---------------------------------------------------------------------------------------------
 // Per-image constants (aeon computes these on the host per record, too)
@@ -170,23 +171,21 @@ struct LaunchPlan {
     bool                photo = false;
     bool                tail  = false; // LINEAR jobs with OpenCV scalar-tail columns
     size_t              blob_off = 0;     // byte offset of this group's jobs in the slot blob
-    size_t              partial_off = 0;  // uint32 offset of this group's contrast partials
     std::vector<AugJob> jobs;
-    int                 tr = 1, chunk_rows = 1, stage_rows = 0, stage_pitch = 0, max_win_w = 0, max_tiles = 0;
+    int                 tr = 1, stage_bytes = 0, max_win_w = 0, max_tiles = 0, buffers = 2;
     int                 lds = 0, threads = kBlockMax;
     bool                vec_ok = true;
-    int                 stats_slots = 0;
-    bool                has_hue = false;
+    bool                has_hue = false, has_contrast = false;
 
     void finalize()
     {
         if (jobs.empty()) return;
-        int budget = kStageBudget;
-        int ww     = 0;
+        int ww = 0;
         for (const AugJob& J : jobs) ww = std::max(ww, J.win_w);
+        max_win_w = std::max(ww, 1);
         // workgroup = 256..512 lanes holding whole 4-pixel column groups (fewest idle lanes;
         // ties go to the larger group), row phases = lanes / column groups
-        const int gpr = (std::max(ww, 1) + 3) / 4;
+        const int gpr = (max_win_w + 3) / 4;
         const int ncg = std::min(gpr, kBlockMax);
         threads       = kBlockMax;
         int best_idle = kBlockMax;
@@ -198,45 +197,49 @@ struct LaunchPlan {
         if (const char* e = std::getenv("AEON_HIP_THREADS"))
             threads = std::min(kBlockMax, std::max(kBlockMin, std::atoi(e) / 64 * 64));
         const int nph = threads / ncg;
-        // rows per band: about four rows per lane (amortises the per-workgroup prologue: job,
-        // tap tables, LUT, staging), a multiple of the row phases; knobs for experiments only
-        int tr_cap = std::min(32, std::max(1, 4 * nph));
+        // one staging buffer and four rows per lane (a multiple of the row phases): the CU's other
+        // workgroups cover a tile's staging latency.  Measured on C2/C3 against two buffers
+        // (the next tile's loads in flight during the current tile's compute) at two rows per
+        // lane: 42 vs 45 us (C2), 152/291 vs 186/370 us (C3 pass 2 / pass 1) -- the second
+        // buffer costs occupancy and halves the rows per tile.  Knobs for experiments only.
+        buffers    = 1;
+        if (const char* e = std::getenv("AEON_HIP_BUFFERS")) buffers = std::atoi(e) == 1 ? 1 : 2;
+        int tr_cap = std::min(64, std::max(1, (buffers == 1 ? 4 : 2) * nph));
+        int budget = kStageBudget;
         if (const char* e = std::getenv("AEON_HIP_STAGE_KB")) budget = std::max(1, std::atoi(e)) * 1024;
-        if (const char* e = std::getenv("AEON_HIP_TR")) tr_cap = std::max(1, std::atoi(e));
+        if (const char* e = std::getenv("AEON_HIP_TR")) tr_cap = std::min(64, std::max(1, std::atoi(e)));
+        bool hue = false, contrast = false;
+        for (const AugJob& J : jobs) {
+            hue |= (J.photo & PHOTO_HUE) != 0;
+            contrast |= (J.photo & PHOTO_CONTRAST) != 0 && J.stats_slot >= 0;
+        }
+        has_hue = hue, has_contrast = contrast;
         for (int pass = 0; pass < 2; pass++) {
-            for (int tr = tr_cap; tr >= 1; tr--) {
-                if (tr > nph && tr % nph) continue;
-                int rows = 0, pitch = 0;
+            for (int t = tr_cap; t >= 1; t--) {
+                if (t > nph && t % nph) continue;
+                // staged rows x whole 4-pixel groups, in whole DMA instructions (64 groups = 1 KiB
+                // for BGR, 64 gray pixels = 256 B)
+                long by = 0;
                 for (const AugJob& J : jobs) {
-                    rows  = std::max(rows, stage_rows_for(J, tr));
-                    pitch = std::max(pitch, (stage_cols(J) + 3) & ~3);
+                    const long groups = (long)stage_rows_for(J, t) * ((stage_cols(J) + 3) / 4);
+                    by = std::max(by, J.cn == 3 ? (groups + 63) / 64 * 1024 : (groups * 4 + 63) / 64 * 256);
                 }
-                if ((long)rows * pitch * 4 <= budget || (tr == 1 && pass == 1)) {
-                    this->tr = tr, stage_rows = rows, stage_pitch = pitch, max_win_w = ww;
-                    bool hue = false;
-                    for (const AugJob& J : jobs) hue |= (J.photo & PHOTO_HUE) != 0;
-                    has_hue = hue;
-                    lds     = lds_layout(max_win_w, tr, stage_rows, stage_pitch, photo && hue).total;
+                by = (by + 1023) / 1024 * 1024;
+                if (buffers * by <= budget || (t == 1 && pass == 1)) {
+                    tr = t, stage_bytes = (int)by;
                     goto chosen;
                 }
             }
             budget = kStageBudgetHi;
         }
     chosen:
+        lds = lds_layout(max_win_w, tr, stage_bytes, photo && hue, buffers).total;
         if (lds > kMaxLds)
-            fail(AEON_HIP_EUNSUPPORTED, "source crop too wide for one LDS-staged row band (" +
-                                            std::to_string(lds) + " bytes)");
-        // rows per workgroup: kBandsPerChunk bands (one: a band's wait for the next band's loads
-        // would also wait for this band's stores -- one vector-memory counter on CDNA)
-        int max_h = 0;
-        for (const AugJob& J : jobs) max_h = std::max(max_h, J.win_h);
-        int per = kBandsPerChunk;
-        if (const char* e = std::getenv("AEON_HIP_BANDS")) per = std::atoi(e);
-        per        = std::min(std::max(per, 1), (max_h + tr - 1) / tr);
-        chunk_rows = per * tr;
-        max_tiles  = 0;
+            fail(AEON_HIP_EUNSUPPORTED, "source crop too wide for LDS-staged row bands (" + std::to_string(lds) +
+                                            " bytes)");
+        max_tiles = 0;
         for (AugJob& J : jobs) {
-            J.tiles   = (J.win_h + chunk_rows - 1) / chunk_rows;
+            J.tiles   = (J.win_h + tr - 1) / tr;
             max_tiles = std::max(max_tiles, J.tiles);
         }
     }
@@ -435,6 +438,8 @@ struct Slot {
     size_t     scratch_cap = 0;
     uint32_t*  partials = nullptr;
     size_t     partials_cap = 0;
+    double*    shifts = nullptr; // contrast (1-c)*mean per stats slot (contrast_reduce)
+    size_t     shifts_cap = 0;
 };
 
 } // namespace
@@ -464,6 +469,9 @@ struct aeon_hip_ctx {
     // job-table transport: 0 = H2D on copy_stream + cross-stream event, 1 = H2D on the launch
     // stream, 2 = kernels read the pinned table in place (AEON_HIP_JOBS for experiments)
     int         jobs_mode = 0;
+    int         n_cu      = 0;
+    int         wg_per_cu = 0; // AEON_HIP_WG_PER_CU: experiments only (0 = occupancy API)
+    std::vector<std::pair<std::vector<int>, int>> occ; // launch shape -> workgroups per CU
     // standardize LUTs stay resident per distinct output config (a new one is uploaded once)
     struct Lut {
         float  host[768];
@@ -542,6 +550,29 @@ double launch_bytes(const LaunchPlan& L, int mode, size_t out_elem)
     return b;
 }
 
+// Persistent grid: as many workgroups as the CUs hold at once, never more than the tiles.
+int grid_for(aeon_hip_ctx* ctx, int mode, const LaunchPlan& P, const LaunchArgs& a)
+{
+    int per_cu = ctx->wg_per_cu;
+    if (per_cu <= 0) {
+        const std::vector<int> key = {mode, P.rm, (int)P.tail, (int)P.photo, a.threads, a.lds_bytes, a.vec_ok,
+                                      a.out_dtype, a.channel_major, a.stage_buffers};
+        for (auto& e : ctx->occ)
+            if (e.first == key) per_cu = e.second;
+        if (per_cu <= 0) {
+            HIP_OK(kernel_occupancy(mode, P.rm, P.tail, P.photo, a, &per_cu));
+            per_cu = std::max(per_cu, 1);
+            ctx->occ.push_back({key, per_cu});
+            if (ctx->host_profile)
+                std::fprintf(stderr, "[aeon_hip] kernel km=%d rm=%d tail=%d photo=%d: %d threads, %d B LDS, TR %d, "
+                                     "%d workgroups/CU x %d CUs, %d tiles\n",
+                             mode, P.rm, (int)P.tail, (int)P.photo, a.threads, a.lds_bytes, a.rows_per_tile, per_cu,
+                             ctx->n_cu, a.total_tiles);
+        }
+    }
+    return (int)std::min<long>((long)a.total_tiles, (long)per_cu * ctx->n_cu);
+}
+
 // One completion event after the open slots' kernels (on their stream) covers all of them.
 void close_slots(aeon_hip_ctx* ctx)
 {
@@ -568,7 +599,7 @@ void timed_launch(aeon_hip_ctx* ctx, int mode, const LaunchPlan& P, const Launch
         t.bytes = bytes;
         HIP_OK(hipEventRecord(t.start, stream));
     }
-    HIP_OK(launch_tiles(mode, P.rm, P.tail, P.photo, a, (int)P.jobs.size(), stream));
+    HIP_OK(launch_tiles(mode, P.rm, P.tail, P.photo, a, grid_for(ctx, mode, P, a), stream));
     if (timed) {
         HIP_OK(hipEventRecord(t.stop, stream));
         ctx->timers.push_back(t);
@@ -644,7 +675,7 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
             if (v == &pass1)
                 for (const AugJob& J : P.jobs) {
                     slot_tiles[J.stats_slot] = J.tiles;
-                    partial_stride           = std::max(partial_stride, J.tiles);
+                    partial_stride           = std::max(partial_stride, J.tiles * 8); // (tile, wave) sums
                 }
             if (v == &main)
                 for (AugJob& J : P.jobs)
@@ -675,6 +706,9 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
         uint8_t* p = (uint8_t*)s.partials;
         grow(p, s.partials_cap, partial_words * 4, false);
         s.partials = (uint32_t*)p;
+        uint8_t* q = (uint8_t*)s.shifts;
+        grow(q, s.shifts_cap, std::max<size_t>(1, pass1_all.jobs.size()) * 4 * sizeof(double), false);
+        s.shifts = (double*)q;
     }
     for (RotJob& R : rot) R.out_ptr += (uint64_t)s.scratch;
     if (!rot.empty()) std::memcpy(s.host + rot_off, rot.data(), rot.size() * sizeof(RotJob));
@@ -705,13 +739,15 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
         a.lut           = d_lut; // [3][256]: standardized, or (float)x without mean
         a.hsv_tables    = ctx->d_hsv;
         a.partials      = s.partials;
+        a.shifts        = s.shifts;
         a.partial_stride = partial_stride;
         a.error         = ctx->d_error;
+        if (const char* e = std::getenv("AEON_HIP_TRACE_PTR")) a.trace = (uint32_t*)std::strtoull(e, nullptr, 0);
         a.rows_per_tile = L.tr;
-        a.rows_per_chunk = L.chunk_rows;
         a.max_tiles     = L.max_tiles;
-        a.stage_rows    = L.stage_rows;
-        a.stage_pitch   = L.stage_pitch;
+        a.total_tiles   = L.max_tiles * (int)L.jobs.size();
+        a.stage_bytes   = L.stage_bytes;
+        a.stage_buffers = L.buffers;
         a.max_win_w     = L.max_win_w;
         a.out_dtype     = o.dtype == AEON_DTYPE_F32 ? OUT_F32 : OUT_U8;
         a.channel_major = o.channel_major;
@@ -732,8 +768,11 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
             if (!P.jobs.empty()) timed_launch(ctx, KM_RAW, P, args(P), stream, launch_bytes(P, KM_RAW, 1), timed);
     for (LaunchPlan& P : pass1)
         if (!P.jobs.empty()) timed_launch(ctx, KM_STATS, P, args(P), stream, launch_bytes(P, KM_STATS, oelem), timed);
-    for (LaunchPlan& P : main)
-        if (!P.jobs.empty()) timed_launch(ctx, KM_FINAL, P, args(P), stream, launch_bytes(P, KM_FINAL, oelem), timed);
+    for (LaunchPlan& P : main) {
+        if (P.jobs.empty()) continue;
+        if (P.has_contrast) HIP_OK(launch_contrast_reduce(args(P), (int)P.jobs.size(), stream));
+        timed_launch(ctx, KM_FINAL, P, args(P), stream, launch_bytes(P, KM_FINAL, oelem), timed);
+    }
     phase(6);
     ctx->open_slots.push_back(slot);
     ctx->open_stream = stream;
@@ -802,6 +841,8 @@ int aeon_hip_ctx_create(int device, aeon_hip_ctx** out)
             HIP_OK(hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
             if (const char* e = std::getenv("AEON_HIP_HOST_PROFILE")) c->host_profile = std::atoi(e) != 0;
             if (const char* e = std::getenv("AEON_HIP_JOBS")) c->jobs_mode = std::min(2, std::max(0, std::atoi(e)));
+            HIP_OK(hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, device));
+            if (const char* e = std::getenv("AEON_HIP_WG_PER_CU")) c->wg_per_cu = std::atoi(e);
             if (const char* e = std::getenv("AEON_HIP_DONE_EVERY"))
                 c->done_every = std::min(aeon_hip_ctx::kSlots / 2, std::max(1, std::atoi(e)));
         } catch (...) {
@@ -840,6 +881,7 @@ int aeon_hip_ctx_destroy(aeon_hip_ctx* c)
             if (s.dev) (void)hipFree(s.dev);
             if (s.scratch) (void)hipFree(s.scratch);
             if (s.partials) (void)hipFree(s.partials);
+            if (s.shifts) (void)hipFree(s.shifts);
         }
         for (auto* v : {&c->timers, &c->free_timers})
             for (KernelTimer& t : *v) (void)hipEventDestroy(t.start), (void)hipEventDestroy(t.stop);

@@ -1,6 +1,6 @@
 """Development: per-phase s_memtime stamps of the streaming kernel (C2), via AEON_HIP_TRACE_PTR.
 Phases per iteration: 0 start, 1 after next-tile prep issued, 2 after compute, 3 after the counted
-wait, 4 after the barrier; slot 7 of iteration 0 = kernel entry."""
+wait, 4 after the unpack, 5 after the barrier; slot 7 of iteration 0 = kernel entry."""
 import os
 import sys
 
@@ -35,10 +35,40 @@ d = []
 for w in range(len(t)):
     for i in range(16):
         r = t[w, i]
-        if r[0] and r[3] and i + 1 < 16 and t[w, i + 1, 0]:
-            d.append([r[1] - r[0], r[2] - r[1], r[3] - r[2], t[w, i + 1, 0] - r[3]])
+        if r[0] and r[5]:
+            d.append([r[1] - r[0], r[2] - r[1], r[3] - r[2], r[4] - r[3], r[5] - r[4]])
 d = np.array(d)
-print("per full iteration (median ticks): prep %d  compute %d  wait %d  fix %d" % tuple(np.median(d, axis=0)))
+print("per full iteration (median ticks): prep %d  compute %d  wait %d  unpack %d  barrier %d" % tuple(np.median(d, axis=0)))
+print("per full iteration (mean ticks):   prep %d  compute %d  wait %d  unpack %d  barrier %d" % tuple(np.mean(d, axis=0)))
 print("prologue (entry -> first iteration start) median:", np.median(t[:, 0, 0] - t[:, 0, 7]))
 life = end - entry
 print("wave life median %d ticks; iterations per wave median %d" % (np.median(life), np.median([sum(1 for i in range(16) if t[w, i, 0]) for w in range(len(t))])))
+
+# per-XCD view (workgroup i runs on XCD i % 8; each XCD has its own clock): entry and exit times
+# relative to the XCD's first entry
+ids = used
+for xcd in range(8):
+    sel = [k for k, w in enumerate(ids) if w % 8 == xcd]
+    if not sel:
+        continue
+    e = t[sel, 0, 7]
+    x0 = e.min()
+    ends = []
+    for k in sel:
+        its = [i for i in range(16) if t[k, i, 0]]
+        last = its[-1]
+        ends.append((t[k, last, 2] if t[k, last, 2] else t[k, last, 1]) - x0)
+    ent = e - x0
+    print(f"xcd {xcd}: {len(sel)} wgs, entry p50 {np.median(ent):.0f} p90 {np.percentile(ent, 90):.0f} max {ent.max()}, "
+          f"end p10 {np.percentile(ends, 10):.0f} p50 {np.median(ends):.0f} max {max(ends)}")
+
+# global timeline from s_memrealtime (100 MHz, chip-wide): slot [wg, 0, 7] entry, [wg, 1, 7] exit
+ent = t[:, 0, 7].astype(np.int64)
+ext = t[:, 1, 7].astype(np.int64)
+ok = ext > 0
+r0 = ent[ok].min()
+ent_us = (ent[ok] - r0) / 100.0
+ext_us = (ext[ok] - r0) / 100.0
+print("realtime: entry us p0/p50/p90/max %.2f %.2f %.2f %.2f" % (ent_us.min(), np.median(ent_us), np.percentile(ent_us, 90), ent_us.max()))
+print("realtime: exit  us p10/p50/p90/max %.2f %.2f %.2f %.2f" % (np.percentile(ext_us, 10), np.median(ext_us), np.percentile(ext_us, 90), ext_us.max()))
+print("realtime: workgroup life us p50 %.2f" % np.median(ext_us - ent_us))
