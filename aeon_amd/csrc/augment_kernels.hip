@@ -14,6 +14,7 @@
 //
 // Build with -ffp-contract=off: the float/double expressions must round exactly as
 // aeon's x86 SSE2 build does (no FMA contraction).
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include "aug_job.hpp"
@@ -901,10 +902,18 @@ KernelFn pick_kernel(int km, int rm, bool tail, bool photo, int of)
 
 int out_form(const LaunchArgs& a) { return (a.out_dtype == OUT_F32 && a.channel_major && a.vec_ok) ? OF_F32_CHW_VEC : OF_GENERIC; }
 
-hipError_t launch_tiles(int km, int rm, bool tail, bool photo, const LaunchArgs& a, int grid, hipStream_t stream)
+// start/stop (optional): events the dispatch itself stamps when the kernel starts and ends
+// (hipExtLaunchKernel), i.e. the kernel's own duration -- the same interval rocprofv3 reports --
+// with no extra packets between launches.
+hipError_t launch_tiles(int km, int rm, bool tail, bool photo, const LaunchArgs& a, int grid, hipStream_t stream,
+                        hipEvent_t start, hipEvent_t stop)
 {
     const KernelFn fn = pick_kernel(km, rm, tail, photo, out_form(a));
     if (!fn) return hipErrorInvalidDeviceFunction;
+    if (start || stop) {
+        void* args[1] = {(void*)&a};
+        return hipExtLaunchKernel((const void*)fn, dim3(grid), dim3(a.threads), args, a.lds_bytes, stream, start, stop, 0);
+    }
     hipLaunchKernelGGL(fn, dim3(grid), dim3(a.threads), a.lds_bytes, stream, a);
     return hipGetLastError();
 }

@@ -21,7 +21,8 @@
 #include "param_factory.hpp"
 
 namespace aeon_hip {
-hipError_t launch_tiles(int km, int rm, bool tail, bool photo, const LaunchArgs& a, int grid, hipStream_t stream);
+hipError_t launch_tiles(int km, int rm, bool tail, bool photo, const LaunchArgs& a, int grid, hipStream_t stream,
+                        hipEvent_t start, hipEvent_t stop);
 hipError_t launch_contrast_reduce(const LaunchArgs& a, int n_jobs, hipStream_t stream);
 hipError_t kernel_occupancy(int km, int rm, bool tail, bool photo, const LaunchArgs& a, int* blocks);
 hipError_t set_kernel_lds_limit(int bytes);
@@ -597,13 +598,10 @@ void timed_launch(aeon_hip_ctx* ctx, int mode, const LaunchPlan& P, const Launch
         }
         t.kind  = mode;
         t.bytes = bytes;
-        HIP_OK(hipEventRecord(t.start, stream));
     }
-    HIP_OK(launch_tiles(mode, P.rm, P.tail, P.photo, a, grid_for(ctx, mode, P, a), stream));
-    if (timed) {
-        HIP_OK(hipEventRecord(t.stop, stream));
-        ctx->timers.push_back(t);
-    }
+    HIP_OK(launch_tiles(mode, P.rm, P.tail, P.photo, a, grid_for(ctx, mode, P, a), stream, timed ? t.start : nullptr,
+                        timed ? t.stop : nullptr));
+    if (timed) ctx->timers.push_back(t);
 }
 
 int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* src_base,
