@@ -59,9 +59,9 @@ class OutDesc(ctypes.Structure):
     """image::loader configuration + batch item stride (aeon src/etl_image.cpp:204-244)."""
     _fields_ = [("dtype", ctypes.c_int32), ("channels", ctypes.c_int32),
                 ("channel_major", ctypes.c_int32), ("bgr_to_rgb", ctypes.c_int32),
-                ("has_mean", ctypes.c_int32), ("reserved", ctypes.c_int32),
+                ("has_mean", ctypes.c_int32), ("fixed_aspect_ratio", ctypes.c_int32),
                 ("mean", ctypes.c_double * 3), ("stddev", ctypes.c_double * 3),
-                ("item_stride", ctypes.c_uint64)]
+                ("item_stride", ctypes.c_uint64), ("canvas_w", ctypes.c_int32), ("canvas_h", ctypes.c_int32)]
 
 
 class RecordElem(ctypes.Structure):
@@ -185,10 +185,11 @@ def aug_params(**kw):
 
 
 def out_desc(channels=3, channel_major=True, bgr_to_rgb=False, dtype="float32", mean=None,
-             stddev=None, item_stride=0):
+             stddev=None, item_stride=0, fixed_aspect_ratio=False, canvas=(0, 0)):
     o = OutDesc(dtype=DTYPE_U8 if dtype == "uint8" else DTYPE_F32, channels=channels,
                 channel_major=int(channel_major), bgr_to_rgb=int(bgr_to_rgb), has_mean=0,
-                item_stride=item_stride)
+                item_stride=item_stride, fixed_aspect_ratio=int(fixed_aspect_ratio),
+                canvas_w=canvas[0], canvas_h=canvas[1])
     if mean is not None:
         o.has_mean = 1
         for i in range(channels):

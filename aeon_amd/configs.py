@@ -44,4 +44,5 @@ def out_desc_for(etl, aug, item_stride=None):
     return A.out_desc(channels=cn, channel_major=etl.get("channel_major", True),
                       bgr_to_rgb=etl.get("bgr_to_rgb", False), dtype=dtype,
                       mean=mean if mean else None, stddev=std if mean else None,
-                      item_stride=item_stride)
+                      item_stride=item_stride, fixed_aspect_ratio=bool(aug.get("fixed_aspect_ratio", False)),
+                      canvas=(etl["width"], etl["height"]))

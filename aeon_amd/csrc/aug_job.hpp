@@ -54,6 +54,8 @@ struct alignas(16) AugJob {
     int32_t  stats_slot;                     // contrast partial-sum slot (-1 if none)
     int32_t  src_scratch;                    // host bookkeeping: source lives in the slot scratch
     int32_t  stats_tiles;                    // chunks of the pass-1 job that wrote this slot's sums
+    int32_t  out_pitch, out_plane;           // loader output row pitch / plane stride (elements):
+                                             // win_w / win_w*win_h, or the fixed_aspect_ratio canvas
 };
 
 // image::rotate pre-pass of one record (rotate_kernels.hip): source -> same-size scratch image.

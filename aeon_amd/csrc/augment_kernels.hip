@@ -532,11 +532,19 @@ struct Bands {
     // taps too unless buffer b already holds this job's (consecutive tiles of one record).
     __device__ __forceinline__ void prep(const Info& f, int b, bool build_xt) const
     {
+        issue(f, b);
+        tables(f, b, build_xt);
+    }
+    __device__ __forceinline__ void issue(const Info& f, int b) const
+    {
+        if (f.ok) stage_issue(job_ref(a, f.job), f.G, L.stage + b * L.stage_bytes, wave, nw);
+    }
+    __device__ __forceinline__ void tables(const Info& f, int b, bool build_xt) const
+    {
         if (!f.ok) return;
         cjob&      J     = job_ref(a, f.job);
         const StageGeom& G = f.G;
         const int  stage = L.stage + b * L.stage_bytes;
-        stage_issue(J, G, stage, wave, nw);
         const int  tid = threadIdx.x, nt = blockDim.x;
         if (build_xt) {
             const auto xt = lds_ptr<i32x2>(L.xt) + b * a.max_win_w;
@@ -582,7 +590,8 @@ struct Bands {
 
         const int  elem  = (KM != KM_FINAL || a.out_dtype == OUT_U8) ? 1 : 4;
         const int  plane = win_w * J.win_h;
-        const auto orsrc = __builtin_amdgcn_make_buffer_rsrc((void*)J.out_ptr, (short)0, plane * cn * elem, 0x00020000);
+        const int  obytes = (KM == KM_FINAL ? J.out_plane : plane) * cn * elem;
+        const auto orsrc = __builtin_amdgcn_make_buffer_rsrc((void*)J.out_ptr, (short)0, obytes, 0x00020000);
         const bool tail  = TAIL && RM == RESIZE_LINEAR && J.xv < J.dst_w * cn; // OpenCV scalar row tail
         const int  wx0   = J.win_x;
         const int  xv    = J.xv;
@@ -714,8 +723,8 @@ struct Bands {
 #pragma unroll
                     for (int k = 0; k < 4; k++) {
                         if (k >= nk) break;
-                        const int i = a.channel_major ? oc * plane + y * win_w + ox0 + k
-                                                      : (y * win_w + ox0 + k) * cn + oc;
+                        const int i = a.channel_major ? oc * J.out_plane + y * J.out_pitch + ox0 + k
+                                                      : (y * J.out_pitch + ox0 + k) * cn + oc;
                         if (a.out_dtype == OUT_F32)
                             __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(lut_of(c, val[k][c])), orsrc,
                                                                   i * 4, 0, kStoreAux);
@@ -779,9 +788,9 @@ __global__ __launch_bounds__(kBlockMax, AEON_HIP_MIN_WAVES) void augment_tiles(L
     // s_memrealtime (chip-wide 100 MHz) at entry and exit
     auto stamp = [&](int it, int ph) {
         if (a.trace && tid == 0 && it < 16)
-            a.trace[(blockIdx.x * 16 + it) * 8 + ph] = (uint32_t)__builtin_amdgcn_s_memtime();
+            a.trace[(blockIdx.x * 16 + it) * 16 + ph] = (uint32_t)__builtin_amdgcn_s_memtime();
     };
-    if (a.trace && tid == 0) a.trace[(blockIdx.x * 16) * 8 + 7] = (uint32_t)__builtin_amdgcn_s_memrealtime();
+    if (a.trace && tid == 0) a.trace[(blockIdx.x * 16) * 16 + 15] = (uint32_t)__builtin_amdgcn_s_memrealtime();
     using Info = typename Bands<KM, RM, PHOTO, OF, TAIL>::Info;
     if (a.stage_buffers == 1) {
         // one buffer (compute-heavy photometric launches, more rows per tile): stage, wait,
@@ -789,20 +798,24 @@ __global__ __launch_bounds__(kBlockMax, AEON_HIP_MIN_WAVES) void augment_tiles(L
         for (int it = 0; t < T; t += G, it++) {
             stamp(it, 0);
             const Info f = W.info(t);
-            if (wave == 0) prefetch_job(a, t + G, L.pf);
-            W.prep(f, 0, true);
             stamp(it, 1);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (wave == 0) prefetch_job(a, t + G, L.pf);
+            W.issue(f, 0);
             stamp(it, 2);
-            W.unpack(f, 0);
+            W.tables(f, 0, true);
             stamp(it, 3);
-            __syncthreads();
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             stamp(it, 4);
-            W.compute(f, 0);
+            W.unpack(f, 0);
             stamp(it, 5);
+            __syncthreads();
+            stamp(it, 6);
+            W.compute(f, 0);
+            stamp(it, 7);
             lds_barrier(); // everyone is done reading the buffer before it is refilled
+            stamp(it, 8);
         }
-        if (a.trace && tid == 0) a.trace[(blockIdx.x * 16 + 1) * 8 + 7] = (uint32_t)__builtin_amdgcn_s_memrealtime();
+        if (a.trace && tid == 0) a.trace[(blockIdx.x * 16 + 1) * 16 + 15] = (uint32_t)__builtin_amdgcn_s_memrealtime();
         return;
     }
     Info cur = W.info(t < T ? t : 0);
@@ -836,7 +849,7 @@ __global__ __launch_bounds__(kBlockMax, AEON_HIP_MIN_WAVES) void augment_tiles(L
         buf ^= 1;
         cur = nxt;
     }
-    if (a.trace && tid == 0) a.trace[(blockIdx.x * 16 + 1) * 8 + 7] = (uint32_t)__builtin_amdgcn_s_memrealtime();
+    if (a.trace && tid == 0) a.trace[(blockIdx.x * 16 + 1) * 16 + 15] = (uint32_t)__builtin_amdgcn_s_memrealtime();
 }
 
 // Contrast pass 2 prologue: per stats slot, (1-c)*mean per channel from the exact per-(tile,

@@ -184,8 +184,8 @@ public:
             if (mean.size() != m_cfg.channels || std_.size() != m_cfg.channels)
                 invalid("Size of 'mean' and 'stddev' must be equal to number of channels or empty.");
         }
-        if (m_factory.fixed_aspect_ratio)
-            throw std::runtime_error("fixed_aspect_ratio is not implemented in the HIP stage");
+        if (m_factory.fixed_aspect_ratio && m_cfg.shape.otype.dtype != AEON_DTYPE_U8)
+            throw std::runtime_error("fixed_aspect_ratio is implemented for uint8_t output only in the HIP stage");
         if (m_cfg.shape.otype.dtype < 0)
             throw std::runtime_error("output_type '" + m_cfg.output_type_name +
                                      "' is not implemented in the HIP stage (uint8_t, float)");
@@ -213,6 +213,8 @@ public:
         for (size_t i = 0; i < m_factory.mean.size() && i < 3; i++)
             o.mean[i] = m_factory.mean[i], o.stddev[i] = m_factory.stddev[i];
         o.item_stride = m_cfg.shape.byte_size();
+        o.fixed_aspect_ratio = m_factory.fixed_aspect_ratio;
+        o.canvas_w = (int)m_cfg.width, o.canvas_h = (int)m_cfg.height;
         return o;
     }
 
@@ -231,6 +233,9 @@ public:
         if (m_cfg.shape.otype.dtype < 0)
             throw std::runtime_error("output_type '" + m_cfg.output_type_name +
                                      "' is not implemented in the HIP stage (uint8_t, float)");
+        // the image::loader it shares (provider.cpp:359) takes the augmentation's fixed_aspect_ratio
+        if (m_factory.fixed_aspect_ratio && m_cfg.shape.otype.dtype != AEON_DTYPE_U8)
+            throw std::runtime_error("fixed_aspect_ratio is implemented for uint8_t output only in the HIP stage");
     }
     void provide(int, const decoded_element& in, augmentation& aug, std::minstd_rand0& random,
                  aeon_aug_params& params) const override
@@ -251,6 +256,8 @@ public:
         o.channels      = (int)m_cfg.channels;
         o.channel_major = m_cfg.channel_major;
         o.item_stride   = m_cfg.shape.byte_size();
+        o.fixed_aspect_ratio = m_factory.fixed_aspect_ratio;
+        o.canvas_w = (int)m_cfg.width, o.canvas_h = (int)m_cfg.height;
         return o;
     }
 

@@ -287,6 +287,8 @@ void plan_image(const aeon_img_desc& d, const void* src_base, const aeon_aug_par
     const size_t elem = o.dtype == AEON_DTYPE_F32 ? 4 : 1;
     if ((size_t)p.out_w * p.out_h * cn * elem > o.item_stride)
         fail(AEON_HIP_EINVAL, "output item does not fit item_stride");
+    if (o.fixed_aspect_ratio && (p.out_w > o.canvas_w || p.out_h > o.canvas_h))
+        fail(AEON_HIP_EINVAL, "fixed_aspect_ratio: output_size larger than the image canvas");
 
     AugJob J{};
     J.src_ptr    = (uint64_t)((const uint8_t*)src_base + d.offset);
@@ -357,6 +359,10 @@ void plan_image(const aeon_img_desc& d, const void* src_base, const aeon_aug_par
     J.xv      = simd_boundary(p.out_w * cn);
     J.flip    = p.flip ? 1 : 0;
     J.out_ptr = (uint64_t)out_item;
+    // image::loader::load (etl_image.cpp:258-306): planes of the record's own size, or with
+    // fixed_aspect_ratio the record at the top-left of the (zeroed) config-sized canvas
+    J.out_pitch = o.fixed_aspect_ratio ? o.canvas_w : p.out_w;
+    J.out_plane = o.fixed_aspect_ratio ? o.canvas_w * o.canvas_h : p.out_w * p.out_h;
 
     if (!is_mask) {
         int photo = 0;
@@ -418,7 +424,7 @@ void plan_image(const aeon_img_desc& d, const void* src_base, const aeon_aug_par
             J.photo   = photo & (PHOTO_CONTRAST | PHOTO_LIGHTING);
         }
     }
-    if ((J.out_ptr & 15) != 0 || (J.win_w & 3) != 0) main.vec_ok = false;
+    if ((J.out_ptr & 15) != 0 || (J.win_w & 3) != 0 || o.fixed_aspect_ratio) main.vec_ok = false;
     main.jobs.push_back(J);
 }
 
@@ -620,6 +626,15 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
              "Standardization (mean, stddev) is supported only for float or double 'output_type'.");
     if (o.bgr_to_rgb && o.channels != 3)
         fail(AEON_HIP_EINVAL, "invalid config: bgr_to_rgb can be 'true' only for channels set to '3'");
+    if (o.fixed_aspect_ratio) {
+        // aeon's fixed-aspect loader views the canvas as CV_8U planes whatever the output type
+        // (etl_image.cpp:263-305), so only uint8 output has a meaningful layout
+        if (o.dtype != AEON_DTYPE_U8)
+            fail(AEON_HIP_EUNSUPPORTED, "fixed_aspect_ratio is implemented for uint8_t output only (aeon's "
+                                        "loader writes uint8 pixels into the canvas)");
+        if (o.canvas_w <= 0 || o.canvas_h <= 0 || (size_t)o.canvas_w * o.canvas_h * o.channels > o.item_stride)
+            fail(AEON_HIP_EINVAL, "fixed_aspect_ratio: canvas does not fit item_stride");
+    }
     hipStream_t stream = (hipStream_t)stream_;
 
     std::lock_guard<std::mutex> lock(ctx->mu);
@@ -759,6 +774,8 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
     const size_t oelem = o.dtype == AEON_DTYPE_F32 ? 4 : 1;
     // timing events on one call in timing_every (each event pair costs GPU time between launches)
     const bool timed = ctx->timing && (ctx->timing_calls++ % ctx->timing_every) == 0;
+    if (o.fixed_aspect_ratio) // std::fill_n of each item's canvas (etl_image.cpp:263)
+        HIP_OK(hipMemset2DAsync(out_dev, o.item_stride, 0, (size_t)o.canvas_w * o.canvas_h * o.channels, n, stream));
     if (!rot.empty())
         HIP_OK(launch_rotate((const RotJob*)(table + rot_off), (int)rot.size(), rot_max_px, stream));
     for (auto* v : {&pre, &pre2})
@@ -859,14 +876,19 @@ int aeon_hip_ctx_destroy(aeon_hip_ctx* c)
         if (c->host_profile && c->host_calls) {
             static const char* names[8] = {"set_device", "plan", "group+finalize", "slot_wait",
                                            "blob_fill", "h2d+wait_event", "launches", "done_event"};
-            std::fprintf(stderr, "[aeon_hip host profile] %ld calls, median us per call:", c->host_calls);
+            std::fprintf(stderr, "[aeon_hip host profile] %ld calls, us per call (median/mean/p90):", c->host_calls);
+            double total = 0;
             for (int k = 0; k < 8; k++) {
                 std::vector<double> v = c->host_ns[k];
                 if (v.empty()) continue;
-                std::nth_element(v.begin(), v.begin() + v.size() / 2, v.end());
-                std::fprintf(stderr, " %s=%.1f", names[k], v[v.size() / 2] / 1e3);
+                double sum = 0;
+                for (double x : v) sum += x;
+                total += sum / v.size();
+                std::sort(v.begin(), v.end());
+                std::fprintf(stderr, " %s=%.1f/%.1f/%.1f", names[k], v[v.size() / 2] / 1e3, sum / v.size() / 1e3,
+                             v[v.size() * 9 / 10] / 1e3);
             }
-            std::fprintf(stderr, "\n");
+            std::fprintf(stderr, "; mean total %.1f us\n", total / 1e3);
         }
         (void)hipSetDevice(c->device);
         if (!c->open_slots.empty()) (void)hipStreamSynchronize(c->open_stream);

@@ -77,10 +77,13 @@ typedef struct aeon_out_desc {
     int32_t  channel_major; /* 1: CHW planes, 0: HWC */
     int32_t  bgr_to_rgb;    /* swap channels 0 and 2 (3-channel only) */
     int32_t  has_mean;      /* standardize with mean/stddev (float output only) */
-    int32_t  reserved;
+    int32_t  fixed_aspect_ratio; /* image::loader m_fixed_aspect_ratio (etl_image.cpp:258-306):
+                                  * each item is a zeroed canvas_w x canvas_h canvas with the
+                                  * record written at its top-left; uint8 output only */
     double   mean[3];
     double   stddev[3];
     uint64_t item_stride;   /* bytes between consecutive items of the batch buffer */
+    int32_t  canvas_w, canvas_h; /* image::config width/height (fixed_aspect_ratio only) */
 } aeon_out_desc;
 
 /* ---- context ------------------------------------------------------------------------------ */

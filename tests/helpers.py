@@ -66,6 +66,37 @@ def oracle_records(images, params, out, mask=False):
     return res
 
 
+def place_canvas(rec, out):
+    """image::loader with fixed_aspect_ratio (aeon src/etl_image.cpp:258-306): a zeroed
+    canvas_w x canvas_h canvas with the record at its top-left (uint8 output)."""
+    cn = out.channels
+    if out.channel_major:
+        c = np.zeros((cn, out.canvas_h, out.canvas_w), np.uint8)
+        c[:, :rec.shape[1], :rec.shape[2]] = rec
+    else:
+        c = np.zeros((out.canvas_h, out.canvas_w, cn), np.uint8)
+        c[:rec.shape[0], :rec.shape[1], :] = rec
+    return c
+
+
+def hip_canvases(ctx, images, params, out, mask=False):
+    """fixed_aspect_ratio: the whole canvas of every item (the output buffer starts as 0xAB so
+    the zero fill is checked too)."""
+    import torch
+    arena, descs = A.pack_images(images)
+    src = torch.from_numpy(arena).to("cuda")
+    n = len(images)
+    dst = torch.full((n * out.item_stride,), 0xAB, dtype=torch.uint8, device="cuda")
+    stream = torch.cuda.current_stream().cuda_stream
+    (ctx.mask_batch if mask else ctx.augment_batch)(descs, src.data_ptr(), params, out, dst.data_ptr(), stream)
+    ctx.synchronize(stream)
+    host = dst.cpu().numpy()
+    cn = out.channels
+    shape = (cn, out.canvas_h, out.canvas_w) if out.channel_major else (out.canvas_h, out.canvas_w, cn)
+    nb = int(np.prod(shape))
+    return [host[i * out.item_stride: i * out.item_stride + nb].reshape(shape).copy() for i in range(n)]
+
+
 def hip_records(ctx, images, params, out, mask=False, dtype=None):
     """Run records through the HIP stage on cuda:0; returns one array per record."""
     import torch

@@ -105,6 +105,39 @@ def test_c5_image_and_mask(ctx):
         assert set(np.unique(m)) <= {0, 255}
 
 
+@pytest.mark.parametrize("channel_major", [True, False])
+def test_fixed_aspect_ratio_canvas(ctx, channel_major):
+    """image::loader with fixed_aspect_ratio (etl_image.cpp:258-306) after crop_enable=false
+    params (augment_image.cpp:132-151: the record scaled to fit, image.var_resize_fixed_ratio
+    300x200 -> 400x267, test/test_image.cpp:1070-1100): the record at the top-left of a zeroed
+    canvas; the pixelmask shares the params and the loader (provider.cpp:353-391)."""
+    aug = {"type": "image", "fixed_aspect_ratio": True, "crop_enable": False, "flip_enable": True}
+    etl = {"type": "image", "height": 400, "width": 400, "channels": 3, "output_type": "uint8_t",
+           "channel_major": channel_major, "bgr_to_rgb": True}
+    metl = {"type": "pixelmask", "height": 400, "width": 400, "channels": 1, "output_type": "uint8_t",
+            "channel_major": channel_major}
+    sizes = [(300, 200), (200, 300), (400, 400), (123, 457), (640, 480), (31, 17), (801, 399)]
+    imgs = [A.synthetic_image(i, w, h, 3) for i, (w, h) in enumerate(sizes)]
+    masks = [A.synthetic_image(50 + i, w, h, 1) for i, (w, h) in enumerate(sizes)]
+    params = H.draw_params(aug, sizes, 400, 400, seed=4)
+    assert (params[0].out_w, params[0].out_h) == (400, 267)
+    assert any(p.flip for p in params) and any(not p.flip for p in params)
+    out, mout = C.out_desc_for(etl, aug), C.out_desc_for(metl, aug)
+    ref = [H.place_canvas(r, out) for r in H.oracle_records(imgs, params, out)]
+    _assert_same(H.hip_canvases(ctx, imgs, params, out), ref, "fixed_aspect image")
+    mref = [H.place_canvas(r, mout) for r in H.oracle_records(masks, params, mout, mask=True)]
+    _assert_same(H.hip_canvases(ctx, masks, params, mout, mask=True), mref, "fixed_aspect mask")
+
+
+def test_fixed_aspect_ratio_float_is_unsupported(ctx):
+    aug = {"type": "image", "fixed_aspect_ratio": True, "crop_enable": False}
+    etl = {"type": "image", "height": 64, "width": 64, "channels": 3, "output_type": "float"}
+    out = C.out_desc_for(etl, aug)
+    params = H.draw_params(aug, [(40, 30)], 64, 64)
+    with pytest.raises(A.AeonHipError, match="uint8_t output only"):
+        H.hip_records(ctx, [A.synthetic_image(0, 40, 30, 3)], params, out)
+
+
 # ---- image::rotate (angle != 0) --------------------------------------------------------------
 @pytest.mark.parametrize("aug_name", ["C1", "C2", "C3"])
 def test_rotation_configs(ctx, aug_name):

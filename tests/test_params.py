@@ -77,3 +77,14 @@ def test_bad_json():
         A.ParamFactory("{not json")
     # aeon does not verify unknown augmentation keys (augment_image.cpp:50)
     A.ParamFactory(json.dumps({"type": "image", "some_future_key": 1}))
+
+
+def test_fixed_aspect_ratio_output_sizes():
+    """image.var_resize_fixed_ratio / var_resize_fixed_scale (test/test_image.cpp:1070-1130):
+    crop_enable=false scales the whole record to fit the 400x400 canvas (300x200 -> 400x267),
+    or by fixed_scaling_factor (1.0 -> 300x200)."""
+    for extra, want in (({}, (400, 267)), ({"fixed_scaling_factor": 1.0}, (300, 200))):
+        aug = dict({"type": "image", "fixed_aspect_ratio": True, "crop_enable": False}, **extra)
+        (p,) = H.draw_params(aug, [(300, 200)], 400, 400)
+        assert (p.out_w, p.out_h) == want
+        assert (p.crop_x, p.crop_y, p.crop_w, p.crop_h) == (0, 0, 300, 200)
