@@ -30,7 +30,8 @@ INTERP_NEAREST = 1
 
 class ImgDesc(ctypes.Structure):
     _fields_ = [("offset", ctypes.c_uint64), ("width", ctypes.c_int32), ("height", ctypes.c_int32),
-                ("stride", ctypes.c_int32), ("channels", ctypes.c_int32)]
+                ("stride", ctypes.c_int32), ("channels", ctypes.c_int32), ("elem_bytes", ctypes.c_int32),
+                ("reserved", ctypes.c_int32)]
 
 
 class AugParams(ctypes.Structure):
@@ -98,7 +99,7 @@ def lib():
         vp = ctypes.c_void_p
         L.aeon_hip_ctx_create.argtypes = [ctypes.c_int, P(vp)]
         L.aeon_hip_ctx_destroy.argtypes = [vp]
-        for fn in (L.aeon_hip_augment_batch, L.aeon_hip_mask_batch):
+        for fn in (L.aeon_hip_augment_batch, L.aeon_hip_mask_batch, L.aeon_hip_depthmap_batch):
             fn.argtypes = [vp, ctypes.c_int, P(ImgDesc), vp, P(AugParams), P(OutDesc), vp, vp]
         L.aeon_hip_synchronize.argtypes = [vp, vp]
         if hasattr(L, "aeon_hip_transpose_batch"):  # absent only in older tuning-variant builds
@@ -236,6 +237,10 @@ class Context:
     def mask_batch(self, descs, src_ptr, params, out, out_ptr, stream=0):
         """pixel_mask transform + load for len(descs) records (async on stream)."""
         self._batch(lib().aeon_hip_mask_batch, descs, src_ptr, params, out, out_ptr, stream)
+
+    def depthmap_batch(self, descs, src_ptr, params, out, out_ptr, stream=0):
+        """depthmap transform + load (aeon src/etl_depthmap.cpp) for len(descs) records."""
+        self._batch(lib().aeon_hip_depthmap_batch, descs, src_ptr, params, out, out_ptr, stream)
 
     def set_timing(self, every=1):
         """Time the launches of one call in `every` (0 = off) with HIP events on their stream."""

@@ -1,0 +1,21 @@
+// mask16.hpp -- job descriptor of the 16-bit pixel-mask / depth-map pass (mask16_kernels.hip).
+#pragma once
+#include <stdint.h>
+
+namespace aeon_hip {
+
+// One 16-bit single-channel record: crop -> INTER_NEAREST resize -> flip -> convert.
+struct alignas(16) Mask16Job {
+    double   scale_x, scale_y;        // OpenCV's ifx/ify = 1 / (dst / src), as the 8-bit path
+    uint64_t src_ptr;                 // device address of the (rotation-free) record
+    uint64_t out_ptr;                 // output item
+    int32_t  src_stride;              // bytes per source row
+    int32_t  crop_x, crop_y, crop_w, crop_h;
+    int32_t  out_w, out_h, out_pitch; // output size; elements per output row (canvas width
+                                      // with fixed_aspect_ratio)
+    int32_t  flip;
+    int32_t  dtype;                   // 0 = uint8 (saturate), 1 = float32
+    int32_t  pad_[2];
+};
+
+} // namespace aeon_hip

@@ -17,6 +17,7 @@
 
 #include "../../include/aeon_hip.h"
 #include "aug_job.hpp"
+#include "mask16.hpp"
 #include "json.hpp"
 #include "param_factory.hpp"
 
@@ -29,6 +30,7 @@ hipError_t set_kernel_lds_limit(int bytes);
 hipError_t launch_transpose(const void* src, void* dst, int64_t rows, int64_t cols, int element_size,
                             hipStream_t stream);
 hipError_t launch_rotate(const RotJob* jobs, int n_jobs, int max_pixels, hipStream_t stream);
+hipError_t launch_nearest16(const Mask16Job* jobs, int n_jobs, int max_h, hipStream_t stream);
 } // namespace aeon_hip
 
 using namespace aeon_hip;
@@ -267,6 +269,38 @@ void rotation_inverse_map(int w, int h, int angle, double M[6])
     const double b1 = -M[0] * M[2] - M[1] * M[5];
     const double b2 = -M[3] * M[2] - M[4] * M[5];
     M[2] = b1, M[5] = b2;
+}
+
+// A 16-bit (CV_16U, ANYDEPTH) pixel-mask / depth-map record: crop -> INTER_NEAREST -> flip ->
+// convertTo (etl_pixel_mask.cpp:65-92, etl_depthmap.cpp:65-96, image.cpp:176-212).
+void plan_mask16(const aeon_img_desc& d, const void* src_base, const aeon_aug_params& p, const aeon_out_desc& o,
+                 uint8_t* out_item, bool is_mask, std::vector<Mask16Job>& m16)
+{
+    if (!is_mask) fail(AEON_HIP_EUNSUPPORTED, "16-bit sources are implemented for pixel masks / depth maps only");
+    if (d.channels != 1 || o.channels != 1) fail(AEON_HIP_EINVAL, "16-bit masks must have one channel");
+    if (d.width <= 0 || d.height <= 0 || d.stride < d.width * 2 || (d.stride & 1) || (d.offset & 1))
+        fail(AEON_HIP_EINVAL, "invalid 16-bit source image descriptor");
+    if (p.angle != 0) fail(AEON_HIP_EUNSUPPORTED, "rotation of 16-bit masks is not implemented");
+    if (p.out_w <= 0 || p.out_h <= 0) fail(AEON_HIP_EINVAL, "invalid output size");
+    const size_t elem = o.dtype == AEON_DTYPE_F32 ? 4 : 1;
+    if ((size_t)p.out_w * p.out_h * elem > o.item_stride) fail(AEON_HIP_EINVAL, "output item does not fit item_stride");
+    if (o.fixed_aspect_ratio && (p.out_w > o.canvas_w || p.out_h > o.canvas_h))
+        fail(AEON_HIP_EINVAL, "fixed_aspect_ratio: output_size larger than the image canvas");
+    if (p.crop_x < 0 || p.crop_y < 0 || p.crop_w <= 0 || p.crop_h <= 0 || p.crop_x + p.crop_w > d.width ||
+        p.crop_y + p.crop_h > d.height)
+        fail(AEON_HIP_EINVAL, "cropbox outside image");
+    Mask16Job M{};
+    M.scale_x    = 1. / ((double)p.out_w / p.crop_w);
+    M.scale_y    = 1. / ((double)p.out_h / p.crop_h);
+    M.src_ptr    = (uint64_t)((const uint8_t*)src_base + d.offset);
+    M.out_ptr    = (uint64_t)out_item;
+    M.src_stride = d.stride;
+    M.crop_x = p.crop_x, M.crop_y = p.crop_y, M.crop_w = p.crop_w, M.crop_h = p.crop_h;
+    M.out_w = p.out_w, M.out_h = p.out_h;
+    M.out_pitch = o.fixed_aspect_ratio ? o.canvas_w : p.out_w;
+    M.flip      = p.flip ? 1 : 0;
+    M.dtype     = o.dtype == AEON_DTYPE_F32 ? 1 : 0;
+    m16.push_back(M);
 }
 
 // Launch order: rot (image::rotate) -> pre (resize_short) -> pre2 (2x-area resize ahead of photometric stages) ->
@@ -649,12 +683,18 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
     HIP_OK(hipSetDevice(ctx->device));
     phase(0);
 
-    LaunchPlan          pre_all, pre2_all, pass1_all, main_all;
-    std::vector<RotJob> rot;
+    LaunchPlan             pre_all, pre2_all, pass1_all, main_all;
+    std::vector<RotJob>    rot;
+    std::vector<Mask16Job> m16;
     size_t     scratch_bytes = 0;
-    for (int i = 0; i < n; i++)
-        plan_image(descs[i], src_base, params[i], o, (uint8_t*)out_dev + (size_t)i * o.item_stride,
-                   is_mask, rot, pre_all, pre2_all, pass1_all, main_all, scratch_bytes);
+    for (int i = 0; i < n; i++) {
+        uint8_t* item = (uint8_t*)out_dev + (size_t)i * o.item_stride;
+        if (descs[i].elem_bytes == 2) plan_mask16(descs[i], src_base, params[i], o, item, is_mask, m16);
+        else if (descs[i].elem_bytes == 0 || descs[i].elem_bytes == 1)
+            plan_image(descs[i], src_base, params[i], o, item, is_mask, rot, pre_all, pre2_all, pass1_all, main_all,
+                       scratch_bytes);
+        else fail(AEON_HIP_EINVAL, "elem_bytes must be 1 (CV_8U) or 2 (CV_16U)");
+    }
 
     phase(1);
     // one launch per (resize mode, photometric) group: the kernels are specialised on both
@@ -673,7 +713,10 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
     for (const AugJob& J : pass1_all.jobs) pass1[J.mode * 2 + has_tail(J)].jobs.push_back(J);
     for (const AugJob& J : main_all.jobs) main[J.mode * 4 + has_tail(J) * 2 + (J.photo ? 1 : 0)].jobs.push_back(J);
     const size_t     rot_off   = 0;
-    size_t           blob      = rot_off + rot.size() * sizeof(RotJob);
+    const size_t     m16_off   = rot_off + rot.size() * sizeof(RotJob);
+    size_t           blob      = m16_off + m16.size() * sizeof(Mask16Job);
+    int              m16_max_h = 0;
+    for (const Mask16Job& M : m16) m16_max_h = std::max(m16_max_h, M.out_h);
     int              rot_max_px = 0;
     for (const RotJob& R : rot) rot_max_px = std::max(rot_max_px, R.w * R.h);
     std::vector<int> slot_tiles(pass1_all.jobs.size(), 0);
@@ -725,6 +768,7 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
     }
     for (RotJob& R : rot) R.out_ptr += (uint64_t)s.scratch;
     if (!rot.empty()) std::memcpy(s.host + rot_off, rot.data(), rot.size() * sizeof(RotJob));
+    if (!m16.empty()) std::memcpy(s.host + m16_off, m16.data(), m16.size() * sizeof(Mask16Job));
     for (auto* v : {&pre, &pre2, &pass1, &main})
         for (LaunchPlan& P : *v) {
             for (AugJob& J : P.jobs) { // relocate scratch references
@@ -776,6 +820,8 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
     const bool timed = ctx->timing && (ctx->timing_calls++ % ctx->timing_every) == 0;
     if (o.fixed_aspect_ratio) // std::fill_n of each item's canvas (etl_image.cpp:263)
         HIP_OK(hipMemset2DAsync(out_dev, o.item_stride, 0, (size_t)o.canvas_w * o.canvas_h * o.channels, n, stream));
+    if (!m16.empty())
+        HIP_OK(launch_nearest16((const Mask16Job*)(table + m16_off), (int)m16.size(), m16_max_h, stream));
     if (!rot.empty())
         HIP_OK(launch_rotate((const RotJob*)(table + rot_off), (int)rot.size(), rot_max_px, stream));
     for (auto* v : {&pre, &pre2})
@@ -947,6 +993,16 @@ int aeon_hip_mask_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, co
                         void* stream)
 {
     return guarded([&] { return run_batch(ctx, n, descs, src_base, params, out, out_dev, stream, true); });
+}
+
+int aeon_hip_depthmap_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* src_base,
+                            const aeon_aug_params* params, const aeon_out_desc* out, void* out_dev, void* stream)
+{
+    return guarded([&] {
+        if (out && out->fixed_aspect_ratio)
+            fail(AEON_HIP_EINVAL, "depthmap::loader has no fixed_aspect_ratio canvas (etl_depthmap.cpp:98-134)");
+        return run_batch(ctx, n, descs, src_base, params, out, out_dev, stream, true);
+    });
 }
 
 int aeon_hip_synchronize(aeon_hip_ctx* ctx, void* stream)

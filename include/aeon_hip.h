@@ -48,8 +48,12 @@ typedef struct aeon_img_desc {
     uint64_t offset;   /* byte offset from the src_base passed to the batch call */
     int32_t  width;    /* cols */
     int32_t  height;   /* rows */
-    int32_t  stride;   /* bytes per row (>= width*channels) */
+    int32_t  stride;   /* bytes per row (>= width*channels*elem_bytes) */
     int32_t  channels; /* 1 or 3 */
+    int32_t  elem_bytes; /* bytes per channel element: 1 (CV_8U; 0 means 1) or 2 (CV_16U, the
+                          * ANYDEPTH pixel masks / depth maps of etl_pixel_mask.cpp:35 and
+                          * etl_depthmap.cpp:35; one channel, masks only, no rotation) */
+    int32_t  reserved;
 } aeon_img_desc;
 
 /* POD mirror of augment::image::params (src/augment_image.hpp:99-119): the fields the image
@@ -105,6 +109,14 @@ int aeon_hip_augment_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs,
 int aeon_hip_mask_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs,
                         const void* src_base, const aeon_aug_params* params,
                         const aeon_out_desc* out, void* out_dev, void* stream);
+
+/* depthmap::extractor -> transformer -> loader (src/etl_depthmap.cpp:30-134) after extract: the
+ * pixel-mask transform (rotate nearest -> crop -> NEAREST resize -> flip) and a plain
+ * convert_mix_channels load (no fixed_aspect_ratio canvas).  aeon's provider_factory does not
+ * construct depth maps (src/provider.cpp:43-99); this is the entry a depthmap provider calls. */
+int aeon_hip_depthmap_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs,
+                            const void* src_base, const aeon_aug_params* params,
+                            const aeon_out_desc* out, void* out_dev, void* stream);
 
 /* batch_major=false output layout: fixed_buffer_map::copy(..., transpose=true) ->
  * transpose_buf (src/buffer_batch.cpp:186-244, 251-280; called per batch by

@@ -291,3 +291,63 @@ def test_transpose_batch_rejects_bad_arguments():
     with pytest.raises(A.AeonHipError, match="overlap"):
         ctx.transpose_batch(src.data_ptr(), src.data_ptr() + 8, 4, 4, 1)
     ctx.close()
+
+
+def _pack16(masks):
+    """16-bit single-channel records -> (uint8 arena, ImgDesc with elem_bytes=2)."""
+    chunks, descs, off = [], [], 0
+    for m in masks:
+        b = np.ascontiguousarray(m, dtype="<u2").view(np.uint8).reshape(-1)
+        pad = (-len(b)) % 16
+        chunks.append(np.concatenate([b, np.zeros(pad, np.uint8)]))
+        h, w = m.shape
+        descs.append(A.ImgDesc(offset=off, width=w, height=h, stride=2 * w, channels=1, elem_bytes=2))
+        off += len(b) + pad
+    return np.concatenate(chunks), (A.ImgDesc * len(descs))(*descs)
+
+
+@pytest.mark.parametrize("dtype", ["uint8", "float32"])
+@pytest.mark.parametrize("entry", ["mask", "depthmap"])
+def test_16bit_masks_and_depthmaps(ctx, dtype, entry):
+    """ANYDEPTH records (etl_pixel_mask.cpp:35, etl_depthmap.cpp:35) stay 16-bit through
+    crop -> NEAREST -> flip and are converted by the loader (saturate_cast<uchar> / exact float).
+    NEAREST is a pure gather, so the oracle reference is its 8-bit transform of the low and high
+    byte planes recombined (parity unpinned by aeon's own fixtures: none are 16-bit)."""
+    import torch
+    rng = np.random.default_rng(16)
+    sizes = [(int(rng.integers(40, 300)), int(rng.integers(40, 300))) for _ in range(9)]
+    masks = [rng.integers(0, 65536, (h, w), dtype=np.uint16) for w, h in sizes]
+    masks[0][:] = rng.integers(0, 256, masks[0].shape)  # values within uint8 too
+    params = H.draw_params(C.C5_AUG, sizes, 128, 96, seed=12)
+    esz = 4 if dtype == "float32" else 1
+    out = A.out_desc(channels=1, channel_major=True, dtype=dtype, item_stride=128 * 96 * esz)
+    arena, descs = _pack16(masks)
+    src = torch.from_numpy(arena).to("cuda")
+    dst = torch.full((len(masks) * out.item_stride,), 0x5A, dtype=torch.uint8, device="cuda")
+    stream = torch.cuda.current_stream().cuda_stream
+    getattr(ctx, entry + "_batch")(descs, src.data_ptr(), params, out, dst.data_ptr(), stream)
+    ctx.synchronize(stream)
+    host = dst.cpu().numpy()
+    o8 = A.out_desc(channels=1, channel_major=True, dtype="uint8", item_stride=128 * 96)
+    lo = H.oracle_records([(m & 0xff).astype(np.uint8) for m in masks], params, o8, mask=True)
+    hi = H.oracle_records([(m >> 8).astype(np.uint8) for m in masks], params, o8, mask=True)
+    for i, p in enumerate(params):
+        v = hi[i].astype(np.uint32) * 256 + lo[i]
+        want = np.minimum(v, 255).astype(np.uint8) if dtype == "uint8" else v.astype(np.float32)
+        got = host[i * out.item_stride: i * out.item_stride + v.size * esz].view(want.dtype).reshape(v.shape)
+        assert np.array_equal(got, want), (entry, dtype, i)
+
+
+def test_16bit_errors(ctx):
+    import torch
+    m = np.zeros((20, 30), np.uint16)
+    arena, descs = _pack16([m])
+    src = torch.from_numpy(arena).to("cuda")
+    dst = torch.zeros(64 * 64, dtype=torch.uint8, device="cuda")
+    out = A.out_desc(channels=1, dtype="uint8", item_stride=64 * 64)
+    (p,) = H.draw_params(C.C5_AUG, [(30, 20)], 64, 64)
+    with pytest.raises(A.AeonHipError, match="pixel masks / depth maps only"):
+        ctx.augment_batch(descs, src.data_ptr(), [p], out, dst.data_ptr())
+    p.angle = 90
+    with pytest.raises(A.AeonHipError, match="rotation of 16-bit"):
+        ctx.mask_batch(descs, src.data_ptr(), [p], out, dst.data_ptr())
