@@ -85,3 +85,19 @@ def test_decoder_batch_major_false_needs_whole_batches():
     cfg = dict(batch_size=4, random_seed=9, batch_major=False, etl=[C.IMAGE_224], augmentation=[C.C2_AUG])
     with pytest.raises(A.AeonHipError, match="whole batches"):
         A.Decoder(cfg).decode(_records(3, seed=4))
+
+
+def test_decoder_fixed_aspect_ratio_uint8():
+    """provider::image with the augmentation's fixed_aspect_ratio (image::loader ctor,
+    provider.cpp:145-158): each record scaled to fit and written at the top-left of its zeroed
+    256x256 uint8 canvas."""
+    aug = {"type": "image", "fixed_aspect_ratio": True, "crop_enable": False, "flip_enable": True}
+    etl = {"type": "image", "height": 256, "width": 256, "channels": 3, "output_type": "uint8_t",
+           "channel_major": True, "bgr_to_rgb": True}
+    d = A.Decoder(dict(batch_size=6, random_seed=9, etl=[etl], augmentation=[aug]))
+    recs = _records(6, seed=4)
+    params = H.draw_params(aug, [(r[0].shape[1], r[0].shape[0]) for r in recs], 256, 256, seed=9)
+    (out,) = d.decode(recs)
+    od = C.out_desc_for(etl, aug)
+    ref = np.stack([H.place_canvas(r, od) for r in H.oracle_records([r[0] for r in recs], params, od)])
+    assert np.array_equal(out, ref)
