@@ -73,7 +73,7 @@ struct LaunchArgs {
     const AugJob*  jobs;
     const float*   lut;        // [3][256] per SOURCE channel: standardized value of output
                                // channel (bgr_to_rgb ? 2-c : c), or (float)x without mean
-    const int32_t* hsv_tables; // sdiv[256], hdiv180[256]
+    const int32_t* hsv_tables; // sdiv[256], hdiv180[256], hfrac[256] (float bits), hsel[256]
     uint32_t*      partials;   // contrast partial sums [slots][partial_stride][4]
     double*        shifts;     // contrast (1-c)*mean per slot [slots][4] (contrast_reduce)
     int32_t*       error;      // device error word (0 = ok)
@@ -122,7 +122,7 @@ AEON_HD inline LdsLayout lds_layout(int max_win_w, int rows_per_tile, int stage_
     LdsLayout L;
     int       o = 0;
     L.lut = o; o += 3 * 256 * 4;                             // standardize LUT (source channel order)
-    L.hsv = o; o += hue ? 2 * 256 * 4 : 0;                   // sdiv / hdiv180 tables
+    L.hsv = o; o += hue ? 4 * 256 * 4 : 0;                   // sdiv / hdiv180 / hfrac / hsel
     L.xt  = o; o += buffers * ((max_win_w * 8 + 15) / 16) * 16; // per-column taps + weights
     L.yt  = o; o += buffers * rows_per_tile * 16;               // per-row taps + weights
     L.pf  = o; o += 256;                                     // LDS-DMA sink of job prefetches

@@ -142,18 +142,14 @@ __device__ __forceinline__ void bs_apply(cjob& J, int& b, int& g, int& r)
     }
 }
 
-constexpr int pack_sectors(int s0, int s1, int s2, int s3, int s4, int s5)
-{
-    return s0 | (s1 << 2) | (s2 << 4) | (s3 << 6) | (s4 << 8) | (s5 << 10);
-}
-constexpr int kSectorB = pack_sectors(1, 1, 3, 0, 0, 2);
-constexpr int kSectorG = pack_sectors(3, 0, 0, 2, 1, 1);
-constexpr int kSectorR = pack_sectors(0, 2, 1, 1, 3, 0);
 
 // cvtColor(BGR2HSV) [RGB2HSV_b], H = (H + hue) % 180 stored as uchar, cvtColor(HSV2BGR)
-// [HSV2RGB_b over HSV2RGB_f].
+// [HSV2RGB_b over HSV2RGB_f].  HSV2RGB_f's sector and fraction depend only on the uchar H, so
+// they come from a 256-entry table built on the host with the same float operations
+// (hfrac = frac(H * 6/180 mod 6), hsel = the sector's t-index per output channel); with s == 0
+// every t equals v exactly, so OpenCV's s == 0 branch needs no special case.
 template <typename TAB>
-__device__ __forceinline__ void hue_apply(TAB sdiv, TAB hdiv, int hue, int& b, int& g, int& r)
+__device__ __forceinline__ void hue_apply(TAB sdiv, TAB hdiv, TAB hfrac, TAB hsel, int hue, int& b, int& g, int& r)
 {
     int v = max(b, max(g, r)), vmin = min(b, min(g, r));
     int diff = v - vmin;
@@ -162,31 +158,20 @@ __device__ __forceinline__ void hue_apply(TAB sdiv, TAB hdiv, int hue, int& b, i
     int h = (vr & (g - b)) + (~vr & ((vg & (b - r + 2 * diff)) + ((~vg) & (r - g + 4 * diff))));
     h = (h * hdiv[diff] + (1 << 11)) >> 12;
     h += h < 0 ? 180 : 0;
-    int H = sat_u8(h);
-    H     = ((H + hue) % 180) & 0xff;
+    const int x = sat_u8(h) + hue; // H in [0, 180]
+    // C's % (truncating) then the uchar store; for |hue| < 180, x is in (-180, 360)
+    const int H = (hue > -180 && hue < 180 ? (x >= 180 ? x - 180 : x) : x % 180) & 0xff;
 
-    float hf = (float)H, sf = (float)s * (1.f / 255), vf = (float)v * (1.f / 255);
-    float bb, gg, rr;
-    if (sf == 0.f) {
-        bb = gg = rr = vf;
-    } else {
-        hf *= 6.f / 180.f;
-        while (hf >= 6.f) hf -= 6.f; // h >= 0 always here
-        int sector = (int)floorf(hf);
-        hf -= (float)sector;
-        if ((unsigned)sector >= 6u) sector = 0, hf = 0.f;
-        float t0 = vf;
-        float t1 = vf * (1.f - sf);
-        float t2 = vf * (1.f - sf * hf);
-        float t3 = vf * (1.f - sf * (1.f - hf));
-        // sector_data = {{1,3,0},{1,0,2},{3,0,1},{0,2,1},{0,1,3},{2,1,0}}, 2 bits per sector
-        const int ib = (kSectorB >> (2 * sector)) & 3;
-        const int ig = (kSectorG >> (2 * sector)) & 3;
-        const int ir = (kSectorR >> (2 * sector)) & 3;
-        bb = ib == 0 ? t0 : ib == 1 ? t1 : ib == 2 ? t2 : t3;
-        gg = ig == 0 ? t0 : ig == 1 ? t1 : ig == 2 ? t2 : t3;
-        rr = ir == 0 ? t0 : ir == 1 ? t1 : ir == 2 ? t2 : t3;
-    }
+    const float hf = __int_as_float(hfrac[H]);
+    const int   sel = hsel[H];
+    const float sf = (float)s * (1.f / 255), vf = (float)v * (1.f / 255);
+    const float t0 = vf;
+    const float t1 = vf * (1.f - sf);
+    const float t2 = vf * (1.f - sf * hf);
+    const float t3 = vf * (1.f - sf * (1.f - hf));
+    const float bb = (sel & 2) ? ((sel & 1) ? t3 : t2) : ((sel & 1) ? t1 : t0);
+    const float gg = (sel & 8) ? ((sel & 4) ? t3 : t2) : ((sel & 4) ? t1 : t0);
+    const float rr = (sel & 32) ? ((sel & 16) ? t3 : t2) : ((sel & 16) ? t1 : t0);
     b = sat_u8(rnd(bb * 255.f));
     g = sat_u8(rnd(gg * 255.f));
     r = sat_u8(rnd(rr * 255.f));
@@ -659,7 +644,7 @@ struct Bands {
                     for (int k = 0; k < 4; k++) {
                         int bb = val[k][0], gg = val[k][1], rr = val[k][2];
                         if (photo & PHOTO_BS) bs_apply(J, bb, gg, rr);
-                        if (photo & PHOTO_HUE) hue_apply(sdiv, hdiv, J.hue, bb, gg, rr);
+                        if (photo & PHOTO_HUE) hue_apply(sdiv, hdiv, hdiv + 256, hdiv + 512, J.hue, bb, gg, rr);
                         if (KM == KM_STATS) { // the intermediate keeps the post-hue pixel
                             if (k < nk) sum0 += bb, sum1 += gg, sum2 += rr;
                             val[k][0] = bb, val[k][1] = gg, val[k][2] = rr;
@@ -783,7 +768,7 @@ __global__ __launch_bounds__(kBlockMax, AEON_HIP_MIN_WAVES) void augment_tiles(L
     }
     if (PHOTO && KM != KM_RAW && a.has_hue) {
         const auto hsv = lds_ptr<int32_t>(L.hsv);
-        for (int i = tid; i < 512; i += nt) hsv[i] = a.hsv_tables[i];
+        for (int i = tid; i < 1024; i += nt) hsv[i] = a.hsv_tables[i];
     }
     // static schedule: tiles blockIdx.x, +G, +2G, ... -- the tiles in flight at any moment are
     // consecutive bands of a few records (measured faster than contiguous ranges per workgroup,

@@ -886,12 +886,26 @@ int aeon_hip_ctx_create(int device, aeon_hip_ctx** out)
             HIP_OK(set_kernel_lds_limit(kMaxLds));
             HIP_OK(hipMalloc((void**)&c->d_error, sizeof(int32_t)));
             HIP_OK(hipMemset(c->d_error, 0, sizeof(int32_t)));
-            // RGB2HSV_b division tables (hsv_shift = 12), as OpenCV builds them
-            int32_t tab[512];
+            // RGB2HSV_b division tables (hsv_shift = 12), as OpenCV builds them, then per uchar H
+            // HSV2RGB_f's sector fraction and t-indices (b | g << 2 | r << 4), computed with
+            // HSV2RGB_f's own float operations
+            int32_t tab[1024];
             tab[0] = tab[256] = 0;
             for (int i = 1; i < 256; i++) {
                 tab[i]       = cv_round((255 << 12) / (1. * i));
                 tab[256 + i] = cv_round((180 << 12) / (6. * i));
+            }
+            static const int sector_data[6][3] = {{1, 3, 0}, {1, 0, 2}, {3, 0, 1}, {0, 2, 1}, {0, 1, 3}, {2, 1, 0}};
+            for (int H = 0; H < 256; H++) {
+                volatile float hf = (float)H;
+                hf = hf * (6.f / 180.f);
+                while (hf >= 6.f) hf = hf - 6.f;
+                int sector = (int)std::floor((float)hf);
+                hf         = hf - (float)sector;
+                if ((unsigned)sector >= 6u) sector = 0, hf = 0.f;
+                const float f = hf;
+                std::memcpy(&tab[512 + H], &f, 4);
+                tab[768 + H] = sector_data[sector][0] | sector_data[sector][1] << 2 | sector_data[sector][2] << 4;
             }
             HIP_OK(hipMalloc((void**)&c->d_hsv, sizeof(tab)));
             HIP_OK(hipMemcpy(c->d_hsv, tab, sizeof(tab), hipMemcpyHostToDevice));
