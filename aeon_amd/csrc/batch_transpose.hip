@@ -48,4 +48,25 @@ hipError_t launch_transpose(const void* src, void* dst, int64_t rows, int64_t co
     return hipGetLastError();
 }
 
+// Job-table upload as a kernel on the launch stream (AEON_HIP_JOBS=3): the slot's pinned host
+// table is read over PCIe with system-coherent 16-byte loads (no L2 copy of an older use of the
+// slot can be returned) and written to the slot's device table.  Kernel-to-kernel ordering on one
+// queue then replaces the cross-queue wait on an SDMA copy.
+__global__ __launch_bounds__(256) void upload_table(const void* host_src, uint4* __restrict__ dst, int n16)
+{
+    const auto src = __builtin_amdgcn_make_buffer_rsrc((void*)host_src, (short)0, n16 * 16, 0x00020000);
+    const int  i   = blockIdx.x * 256 + threadIdx.x;
+    if (i < n16) {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(src, i * 16, 0, 1 | 16); // sc0 sc1
+        dst[i]       = make_uint4(v[0], v[1], v[2], v[3]);
+    }
+}
+
+hipError_t launch_upload_table(const void* host_dev, void* dst, size_t bytes, hipStream_t stream)
+{
+    const int n16 = (int)((bytes + 15) / 16);
+    hipLaunchKernelGGL(upload_table, dim3((n16 + 255) / 256), dim3(256), 0, stream, host_dev, (uint4*)dst, n16);
+    return hipGetLastError();
+}
+
 } // namespace aeon_hip
