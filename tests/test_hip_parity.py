@@ -206,6 +206,15 @@ EDGE_CASES = [
                                       pad_off_x=20, pad_off_y=0), dict(item_stride=3 * 64 * 48 * 4)),
     ("resize_short_upscale", (120, 90), dict(crop_x=40, crop_y=0, crop_w=256, crop_h=256, out_w=224, out_h=224,
                                              resize_short_size=256), {}),
+    # maximum sizes: outputs wider than a workgroup's column groups, 12-megapixel sources
+    ("wide_output", (1500, 100), dict(crop_x=7, crop_y=3, crop_w=1480, crop_h=90, out_w=1200, out_h=40, flip=1),
+     dict(item_stride=3 * 1200 * 40 * 4)),
+    ("very_wide_output", (1300, 40), dict(crop_x=0, crop_y=0, crop_w=1300, crop_h=40, out_w=2500, out_h=16),
+     dict(item_stride=3 * 2500 * 16 * 4)),
+    ("big_source", (4096, 3072), dict(crop_x=11, crop_y=5, crop_w=4000, crop_h=3000, out_w=512, out_h=384, flip=1),
+     dict(item_stride=3 * 512 * 384 * 4)),
+    ("big_source_c3", (4096, 3072), dict(crop_x=0, crop_y=0, crop_w=4096, crop_h=3072, out_w=224, out_h=224,
+                                         brightness=0.7, saturation=1.6, contrast=0.6, hue=9), {}),
 ]
 
 
