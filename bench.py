@@ -168,6 +168,64 @@ def run_e2e(A, C, torch, batch, steps):
     return batch * steps / dt
 
 
+def run_c5(A, C, torch, steps, warmup, pool_mib, src_wh=(640, 480)):
+    """C5 (BASELINE configs[4]): image + pixel mask drawn with ONE shared params set per record
+    (aeon provider_base::provide, src/provider.cpp:109-119): joint crop/flip, bilinear image
+    -> 512x512x3 f32 CHW, NEAREST mask -> 512x512x1 u8, batch 128, device-resident sources."""
+    ctx = A.Context(torch.cuda.current_device())
+    batch = C.CONFIGS["C5"]["batch_size"]
+    w, h = src_wh
+    ib, mb = w * h * 3, w * h
+    n_pool = max(1, (pool_mib << 20) // (batch * (ib + mb)))
+    gen = torch.Generator(device="cuda")
+    gen.manual_seed(0x5EED5)
+    img = torch.randint(0, 256, (n_pool * batch * ib,), dtype=torch.uint8, device="cuda", generator=gen)
+    msk = torch.randint(0, 21, (n_pool * batch * mb,), dtype=torch.uint8, device="cuda", generator=gen)
+    idescs = [(A.ImgDesc * batch)(*[A.ImgDesc(offset=(b * batch + i) * ib, width=w, height=h, stride=w * 3,
+                                              channels=3) for i in range(batch)]) for b in range(n_pool)]
+    mdescs = [(A.ImgDesc * batch)(*[A.ImgDesc(offset=(b * batch + i) * mb, width=w, height=h, stride=w,
+                                              channels=1) for i in range(batch)]) for b in range(n_pool)]
+    iout = C.out_desc_for(C.IMAGE_512, C.C5_AUG)
+    mout = C.out_desc_for(C.MASK_512, C.C5_AUG)
+    idst = [torch.empty(batch * iout.item_stride, dtype=torch.uint8, device="cuda") for _ in range(2)]
+    mdst = [torch.empty(batch * mout.item_stride, dtype=torch.uint8, device="cuda") for _ in range(2)]
+    f = A.ParamFactory(C.C5_AUG)
+    states = A.seed_slots(1, batch)
+    params = []
+    for _ in range(steps + warmup):
+        ps = []
+        for i in range(batch):
+            st = states[i:i + 1]
+            ps.append(f.make_params(st, w, h, 512, 512))
+            states[i] = st[0]
+        params.append((A.AugParams * batch)(*ps))
+    stream = torch.cuda.current_stream().cuda_stream
+
+    def step(s):
+        b = s % n_pool
+        ctx.augment_batch(idescs[b], img.data_ptr(), params[s], iout, idst[s & 1].data_ptr(), stream)
+        ctx.mask_batch(mdescs[b], msk.data_ptr(), params[s], mout, mdst[s & 1].data_ptr(), stream)
+
+    for s in range(warmup):
+        step(s)
+    torch.cuda.synchronize()
+    ctx.kernel_times()
+    ctx.set_timing(1)
+    t0 = time.perf_counter()
+    for s in range(warmup, warmup + steps):
+        step(s)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    ctx.synchronize(stream)
+    k_ms, k_bytes, k_n = ctx.kernel_times()["augment"]
+    ctx.set_timing(False)
+    ctx.close()
+    return {"value": batch * steps / dt, "unit": "images/s (image+mask pairs)", "batch": batch,
+            "ms_per_step": dt / steps * 1e3, "source": f"{w}x{h} u8 HWC image + {w}x{h} u8 mask",
+            "kernels_ms_per_step": k_ms / steps, "kernels_gbs": k_bytes / (k_ms * 1e-3) / 1e9 if k_ms else 0,
+            "what": "image 512x512x3 f32 CHW (bilinear) + mask 512x512 u8 (nearest), shared params"}
+
+
 def cpu_baseline(A, C, budget_s):
     """aeon's CPU path restated (oracle/, C++): thread pool of hc - min(2, hc/8) workers with a
     dynamic atomic task counter (src/util.cpp:360-370, src/thread_pool.hpp:155-162)."""
@@ -258,6 +316,7 @@ def main():
             extra["two_streams"] = {"value": batch * args.steps / e2, "unit": "images/s",
                                     "ms_per_step": e2 / args.steps * 1e3,
                                     "what": "same workload, consecutive batches on two streams"}
+        extra["C5"] = run_c5(A, C, torch, max(5, args.steps // 5), 2, args.pool_mib)
         extra["e2e_host_to_host"] = {"value": run_e2e(A, C, torch, 256, 20), "unit": "images/s",
                                      "what": "pinned H2D of decoded 256x256 u8 + kernel + D2H of fp32 CHW"}
 
