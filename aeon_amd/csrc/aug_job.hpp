@@ -73,7 +73,7 @@ struct LaunchArgs {
     const AugJob*  jobs;
     const float*   lut;        // [3][256] per SOURCE channel: standardized value of output
                                // channel (bgr_to_rgb ? 2-c : c), or (float)x without mean
-    const int32_t* hsv_tables; // sdiv[256], hdiv180[256], hfrac[256] (float bits), hsel[256]
+    const int32_t* hsv_tables; // sdiv[256], hdiv180[256], then per uchar H the HSV2RGB weights (B, G, R, 0) as float bits
     uint32_t*      partials;   // contrast partial sums [slots][partial_stride][4]
     double*        shifts;     // contrast (1-c)*mean per slot [slots][4] (contrast_reduce)
     int32_t*       error;      // device error word (0 = ok)
@@ -103,6 +103,7 @@ enum KernelMode : int { KM_FINAL = 0, KM_STATS = 1, KM_RAW = 2 };
 // lane keeps the same output columns (and their resize taps) for a whole chunk.
 constexpr int kBlockMin = 256;
 constexpr int kBlockMax = 512;
+constexpr int kHsvWords = 512 + 256 * 4; // RGB2HSV division tables + HSV2RGB per-H weights
 
 #if defined(__HIPCC__)
 #define AEON_HD __host__ __device__
@@ -122,7 +123,7 @@ AEON_HD inline LdsLayout lds_layout(int max_win_w, int rows_per_tile, int stage_
     LdsLayout L;
     int       o = 0;
     L.lut = o; o += 3 * 256 * 4;                             // standardize LUT (source channel order)
-    L.hsv = o; o += hue ? 4 * 256 * 4 : 0;                   // sdiv / hdiv180 / hfrac / hsel
+    L.hsv = o; o += hue ? kHsvWords * 4 : 0;                 // sdiv / hdiv180 / HSV2RGB weights
     L.xt  = o; o += buffers * ((max_win_w * 8 + 15) / 16) * 16; // per-column taps + weights
     L.yt  = o; o += buffers * rows_per_tile * 16;               // per-row taps + weights
     L.pf  = o; o += 256;                                     // LDS-DMA sink of job prefetches

@@ -144,12 +144,14 @@ __device__ __forceinline__ void bs_apply(cjob& J, int& b, int& g, int& r)
 
 
 // cvtColor(BGR2HSV) [RGB2HSV_b], H = (H + hue) % 180 stored as uchar, cvtColor(HSV2BGR)
-// [HSV2RGB_b over HSV2RGB_f].  HSV2RGB_f's sector and fraction depend only on the uchar H, so
-// they come from a 256-entry table built on the host with the same float operations
-// (hfrac = frac(H * 6/180 mod 6), hsel = the sector's t-index per output channel); with s == 0
-// every t equals v exactly, so OpenCV's s == 0 branch needs no special case.
-template <typename TAB>
-__device__ __forceinline__ void hue_apply(TAB sdiv, TAB hdiv, TAB hfrac, TAB hsel, int hue, int& b, int& g, int& r)
+// [HSV2RGB_b over HSV2RGB_f].  HSV2RGB_f's sector and fraction depend only on the uchar H, and
+// each output channel is one of t0 = v, t1 = v(1-s), t2 = v(1-s*f), t3 = v(1-s(1-f)), i.e.
+// v*(1 - s*w) with w in {0, 1, f, 1-f}: a 256-entry table of per-channel weights (B, G, R, 0),
+// built on the host with HSV2RGB_f's own float operations, gives every t exactly (s*0 = 0,
+// s*1 = s, and 1-f rounded once as OpenCV does).  With s == 0 every t equals v exactly, so
+// OpenCV's s == 0 branch needs no special case.
+template <typename TAB, typename WTAB>
+__device__ __forceinline__ void hue_apply(TAB sdiv, TAB hdiv, WTAB wtab, int hue, int& b, int& g, int& r)
 {
     int v = max(b, max(g, r)), vmin = min(b, min(g, r));
     int diff = v - vmin;
@@ -162,19 +164,15 @@ __device__ __forceinline__ void hue_apply(TAB sdiv, TAB hdiv, TAB hfrac, TAB hse
     // C's % (truncating) then the uchar store; for |hue| < 180, x is in (-180, 360)
     const int H = (hue > -180 && hue < 180 ? (x >= 180 ? x - 180 : x) : x % 180) & 0xff;
 
-    const float hf = __int_as_float(hfrac[H]);
-    const int   sel = hsel[H];
+    const f32x4 w  = wtab[H];
     const float sf = (float)s * (1.f / 255), vf = (float)v * (1.f / 255);
-    const float t0 = vf;
-    const float t1 = vf * (1.f - sf);
-    const float t2 = vf * (1.f - sf * hf);
-    const float t3 = vf * (1.f - sf * (1.f - hf));
-    const float bb = (sel & 2) ? ((sel & 1) ? t3 : t2) : ((sel & 1) ? t1 : t0);
-    const float gg = (sel & 8) ? ((sel & 4) ? t3 : t2) : ((sel & 4) ? t1 : t0);
-    const float rr = (sel & 32) ? ((sel & 16) ? t3 : t2) : ((sel & 16) ? t1 : t0);
-    b = sat_u8(rnd(bb * 255.f));
-    g = sat_u8(rnd(gg * 255.f));
-    r = sat_u8(rnd(rr * 255.f));
+    const float bb = vf * (1.f - sf * w[0]);
+    const float gg = vf * (1.f - sf * w[1]);
+    const float rr = vf * (1.f - sf * w[2]);
+    // v, s in [0, 1] and w in [0, 1]: every product is in [0, 255], no saturation needed
+    b = rnd(bb * 255.f);
+    g = rnd(gg * 255.f);
+    r = rnd(rr * 255.f);
 }
 
 // ---- source staging (LDS-DMA) ------------------------------------------------------------------
@@ -644,7 +642,7 @@ struct Bands {
                     for (int k = 0; k < 4; k++) {
                         int bb = val[k][0], gg = val[k][1], rr = val[k][2];
                         if (photo & PHOTO_BS) bs_apply(J, bb, gg, rr);
-                        if (photo & PHOTO_HUE) hue_apply(sdiv, hdiv, hdiv + 256, hdiv + 512, J.hue, bb, gg, rr);
+                        if (photo & PHOTO_HUE) hue_apply(sdiv, hdiv, lds_ptr<const f32x4>(L.hsv + 2048), J.hue, bb, gg, rr);
                         if (KM == KM_STATS) { // the intermediate keeps the post-hue pixel
                             if (k < nk) sum0 += bb, sum1 += gg, sum2 += rr;
                             val[k][0] = bb, val[k][1] = gg, val[k][2] = rr;
@@ -768,7 +766,7 @@ __global__ __launch_bounds__(kBlockMax, AEON_HIP_MIN_WAVES) void augment_tiles(L
     }
     if (PHOTO && KM != KM_RAW && a.has_hue) {
         const auto hsv = lds_ptr<int32_t>(L.hsv);
-        for (int i = tid; i < 1024; i += nt) hsv[i] = a.hsv_tables[i];
+        for (int i = tid; i < kHsvWords; i += nt) hsv[i] = a.hsv_tables[i];
     }
     // static schedule: tiles blockIdx.x, +G, +2G, ... -- the tiles in flight at any moment are
     // consecutive bands of a few records (measured faster than contiguous ranges per workgroup,

@@ -893,9 +893,9 @@ int aeon_hip_ctx_create(int device, aeon_hip_ctx** out)
             HIP_OK(hipMalloc((void**)&c->d_error, sizeof(int32_t)));
             HIP_OK(hipMemset(c->d_error, 0, sizeof(int32_t)));
             // RGB2HSV_b division tables (hsv_shift = 12), as OpenCV builds them, then per uchar H
-            // HSV2RGB_f's sector fraction and t-indices (b | g << 2 | r << 4), computed with
-            // HSV2RGB_f's own float operations
-            int32_t tab[1024];
+            // HSV2RGB_f's sector fraction f (its own float operations) turned into the weight w of
+            // each output channel in t = v*(1 - s*w): t0 w=0, t1 w=1, t2 w=f, t3 w=1-f
+            int32_t tab[kHsvWords];
             tab[0] = tab[256] = 0;
             for (int i = 1; i < 256; i++) {
                 tab[i]       = cv_round((255 << 12) / (1. * i));
@@ -909,9 +909,10 @@ int aeon_hip_ctx_create(int device, aeon_hip_ctx** out)
                 int sector = (int)std::floor((float)hf);
                 hf         = hf - (float)sector;
                 if ((unsigned)sector >= 6u) sector = 0, hf = 0.f;
-                const float f = hf;
-                std::memcpy(&tab[512 + H], &f, 4);
-                tab[768 + H] = sector_data[sector][0] | sector_data[sector][1] << 2 | sector_data[sector][2] << 4;
+                const float f      = hf;
+                const float wt[4]  = {0.f, 1.f, f, 1.f - f};
+                const float w[4]   = {wt[sector_data[sector][0]], wt[sector_data[sector][1]], wt[sector_data[sector][2]], 0.f};
+                std::memcpy(&tab[512 + 4 * H], w, sizeof(w));
             }
             HIP_OK(hipMalloc((void**)&c->d_hsv, sizeof(tab)));
             HIP_OK(hipMemcpy(c->d_hsv, tab, sizeof(tab), hipMemcpyHostToDevice));
