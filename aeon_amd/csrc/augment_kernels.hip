@@ -119,6 +119,22 @@ __device__ __forceinline__ YTap ycoef(int dy, double scale, int sh)
     return t;
 }
 
+// 24-bit signed multiply-add, full rate.  Spelled in asm: for __mul24 the backend sometimes
+// sign-extends on the scalar unit and then selects the quarter-rate v_mul_lo_u32.  Callers
+// guarantee |operands| < 2^23.  The `_s` form takes a uniform (SGPR) first operand.
+__device__ __forceinline__ int mad_i24(int a, int b, int c)
+{
+    int r;
+    asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+__device__ __forceinline__ int mad_i24_s(int a_uniform, int b, int c)
+{
+    int r;
+    asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(r) : "s"(a_uniform), "v"(b), "v"(c));
+    return r;
+}
+
 // ---- photometric stages (aeon src/image.cpp:336-406 over OpenCV 2.4) ------------------------
 __device__ __forceinline__ void bs_apply(cjob& J, int& b, int& g, int& r)
 {
@@ -128,9 +144,10 @@ __device__ __forceinline__ void bs_apply(cjob& J, int& b, int& g, int& r)
         r = sat_u8(rnd(J.bsm[8] * (float)r + 0.f));
     } else if (J.bs_kind == BS_FIXPT) { // transform_8u, 10-bit fixed point
         const int  q[9] = {J.bsq[0], J.bsq[1], J.bsq[2], J.bsq[3], J.bsq[4], J.bsq[5], J.bsq[6], J.bsq[7], J.bsq[8]};
-        int        t0 = (q[0] * b + q[1] * g + q[2] * r + 512) >> 10;
-        int        t1 = (q[3] * b + q[4] * g + q[5] * r + 512) >> 10;
-        int        t2 = (q[6] * b + q[7] * g + q[8] * r + 512) >> 10;
+        // |q| < 2^15, x < 2^8: full-rate 24-bit multiply-adds
+        int        t0 = mad_i24_s(q[0], b, mad_i24_s(q[1], g, mad_i24_s(q[2], r, 512))) >> 10;
+        int        t1 = mad_i24_s(q[3], b, mad_i24_s(q[4], g, mad_i24_s(q[5], r, 512))) >> 10;
+        int        t2 = mad_i24_s(q[6], b, mad_i24_s(q[7], g, mad_i24_s(q[8], r, 512))) >> 10;
         b = sat_u8(t0), g = sat_u8(t1), r = sat_u8(t2);
     } else { // transform_<uchar,float>
         const float m[9] = {J.bsm[0], J.bsm[1], J.bsm[2], J.bsm[3], J.bsm[4], J.bsm[5], J.bsm[6], J.bsm[7], J.bsm[8]};
@@ -156,9 +173,10 @@ __device__ __forceinline__ void hue_apply(TAB sdiv, TAB hdiv, WTAB wtab, int hue
     int v = max(b, max(g, r)), vmin = min(b, min(g, r));
     int diff = v - vmin;
     int vr = v == r ? -1 : 0, vg = v == g ? -1 : 0;
-    int s = (diff * sdiv[v] + (1 << 11)) >> 12;
+    // operands < 2^23 in magnitude (sdiv <= 255<<12, hdiv <= 30<<12, |h| <= 5*255)
+    int s = mad_i24(diff, sdiv[v], 1 << 11) >> 12;
     int h = (vr & (g - b)) + (~vr & ((vg & (b - r + 2 * diff)) + ((~vg) & (r - g + 4 * diff))));
-    h = (h * hdiv[diff] + (1 << 11)) >> 12;
+    h = mad_i24(h, hdiv[diff], 1 << 11) >> 12;
     h += h < 0 ? 180 : 0;
     const int x = sat_u8(h) + hue; // H in [0, 180]
     // C's % (truncating) then the uchar store; for |hue| < 180, x is in (-180, 360)
@@ -439,9 +457,9 @@ __device__ __forceinline__ void tail_fix(i32x4 ytr, int col, uint32_t wx, int e0
     const int      a0 = wx & 0xffff, a1 = (int)(wx >> 16);
     for (int c = 0; c < 3; c++) {
         if (e0 + c < xv) continue;
-        const int H0 = byte_of(p00, c) * a0 + byte_of(p01, c) * a1;
-        const int H1 = byte_of(p10, c) * a0 + byte_of(p11, c) * a1;
-        s[c]         = sat_u8((H0 * ytr.z + H1 * ytr.w + (1 << 21)) >> 22) << (SCALED ? 2 : 0);
+        const int H0 = __mul24(byte_of(p00, c), a0) + __mul24(byte_of(p01, c), a1);
+        const int H1 = __mul24(byte_of(p10, c), a0) + __mul24(byte_of(p11, c), a1);
+        s[c]         = sat_u8((__mul24(H0, ytr.z) + __mul24(H1, ytr.w) + (1 << 21)) >> 22) << (SCALED ? 2 : 0);
     }
 }
 
