@@ -198,6 +198,9 @@ struct LaunchPlan {
             // idle / nt <= best_idle / threads
             if ((long)idle * threads <= (long)best_idle * nt) threads = nt, best_idle = idle;
         }
+        // contrast pass 2 (photometric over the u8 intermediate, no resize): full workgroups
+        // beat the fewest-idle-lanes choice (C3: 140 vs 158 us at 512 vs 448 lanes)
+        if (rm == RESIZE_COPY && photo) threads = kBlockMax;
         if (const char* e = std::getenv("AEON_HIP_THREADS"))
             threads = std::min(kBlockMax, std::max(kBlockMin, std::atoi(e) / 64 * 64));
         const int nph = threads / ncg;
