@@ -725,6 +725,26 @@ struct Bands {
                     }
                     continue;
                 }
+                if (a.out_dtype != OUT_F32 && (a.channel_major || cn == 1) && nk == 4) {
+                    // uint8 planes (pixel masks, uint8 images): a lane's 4 consecutive output
+                    // bytes of a plane as one dword store when the 4-byte group is aligned
+#pragma unroll
+                    for (int c = 0; c < 3; c++) {
+                        if (c >= cn) break;
+                        const int oc = bgr ? 2 - c : c;
+                        const int i0 = (cn == 1 ? 0 : oc * J.out_plane) + y * J.out_pitch + ox0;
+                        const uint32_t w = ((uint32_t)u8_of(val[0][c]) & 0xff) | (((uint32_t)u8_of(val[1][c]) & 0xff) << 8) |
+                                           (((uint32_t)u8_of(val[2][c]) & 0xff) << 16) | ((uint32_t)u8_of(val[3][c]) << 24);
+                        if ((i0 & 3) == 0) {
+                            __builtin_amdgcn_raw_buffer_store_b32(w, orsrc, i0, 0, kStoreAux);
+                        } else {
+#pragma unroll
+                            for (int k = 0; k < 4; k++)
+                                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(w >> (8 * k)), orsrc, i0 + k, 0, kStoreAux);
+                        }
+                    }
+                    continue;
+                }
 #pragma unroll
                 for (int c = 0; c < 3; c++) {
                     if (c >= cn) break;

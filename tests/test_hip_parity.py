@@ -215,6 +215,12 @@ EDGE_CASES = [
      dict(item_stride=3 * 512 * 384 * 4)),
     ("big_source_c3", (4096, 3072), dict(crop_x=0, crop_y=0, crop_w=4096, crop_h=3072, out_w=224, out_h=224,
                                          brightness=0.7, saturation=1.6, contrast=0.6, hue=9), {}),
+    # uint8 planes: 4-byte groups stored as dwords when aligned, bytewise when the plane's rows are not
+    ("u8_chw_odd_width", (256, 256), dict(crop_x=5, crop_y=9, crop_w=200, crop_h=180, out_w=221, out_h=37, flip=1),
+     dict(dtype="uint8", mean=None, stddev=None, item_stride=221 * 37 * 3)),
+    ("u8_chw_c3_odd", (256, 256), dict(crop_x=0, crop_y=0, crop_w=256, crop_h=256, out_w=223, out_h=31,
+                                      brightness=0.8, saturation=1.3, contrast=0.7, hue=-12),
+     dict(dtype="uint8", mean=None, stddev=None, item_stride=223 * 31 * 3)),
 ]
 
 
@@ -235,6 +241,17 @@ def test_grayscale(ctx):
               for i in range(4)]
     out = A.out_desc(channels=1, channel_major=True, dtype="uint8", item_stride=64 * 48)
     _assert_same(H.hip_records(ctx, imgs, params, out), H.oracle_records(imgs, params, out), "gray")
+
+
+@pytest.mark.parametrize("ow,oh", [(64, 48), (61, 47), (510, 3)])
+def test_mask_u8_widths(ctx, ow, oh):
+    """1-channel uint8 output rows of any width (dword stores only on aligned 4-byte groups)."""
+    masks = [A.synthetic_image(30 + i, 97, 61, 1) for i in range(4)]
+    params = [A.aug_params(crop_x=3, crop_y=1, crop_w=90, crop_h=57, out_w=ow, out_h=oh, flip=i % 2)
+              for i in range(4)]
+    out = A.out_desc(channels=1, channel_major=True, dtype="uint8", item_stride=ow * oh)
+    res = H.hip_records(ctx, masks, params, out, mask=True)
+    _assert_same(res, H.oracle_records(masks, params, out, mask=True), f"mask {ow}x{oh}")
 
 
 def test_empty_batch(ctx):
