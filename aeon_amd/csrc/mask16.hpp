@@ -1,10 +1,11 @@
-// mask16.hpp -- job descriptor of the 16-bit pixel-mask / depth-map pass (mask16_kernels.hip).
+// mask16.hpp -- job descriptor of the single-channel NEAREST pass of pixel masks / depth maps
+// (mask16_kernels.hip): 16-bit sources, and rotation-free 8-bit ones.
 #pragma once
 #include <stdint.h>
 
 namespace aeon_hip {
 
-// One 16-bit single-channel record: crop -> INTER_NEAREST resize -> flip -> convert.
+// One single-channel record: crop -> INTER_NEAREST resize -> flip -> convert.
 struct alignas(16) Mask16Job {
     double   scale_x, scale_y;        // OpenCV's ifx/ify = 1 / (dst / src), as the 8-bit path
     uint64_t src_ptr;                 // device address of the (rotation-free) record
@@ -15,7 +16,8 @@ struct alignas(16) Mask16Job {
                                       // with fixed_aspect_ratio)
     int32_t  flip;
     int32_t  dtype;                   // 0 = uint8 (saturate), 1 = float32
-    int32_t  pad_[2];
+    int32_t  src_elem;                // bytes per source element: 1 (CV_8U) or 2 (CV_16U)
+    int32_t  pad_;
 };
 
 } // namespace aeon_hip

@@ -30,7 +30,8 @@ hipError_t set_kernel_lds_limit(int bytes);
 hipError_t launch_transpose(const void* src, void* dst, int64_t rows, int64_t cols, int element_size,
                             hipStream_t stream);
 hipError_t launch_rotate(const RotJob* jobs, int n_jobs, int max_pixels, hipStream_t stream);
-hipError_t launch_nearest16(const Mask16Job* jobs, int n_jobs, int max_h, hipStream_t stream);
+hipError_t launch_nearest(const Mask16Job* jobs, int n_jobs, int max_h, int max_w, hipStream_t stream,
+                          hipEvent_t start, hipEvent_t stop);
 hipError_t launch_upload_table(const void* host_dev, void* dst, size_t bytes, hipStream_t stream);
 } // namespace aeon_hip
 
@@ -275,14 +276,16 @@ void rotation_inverse_map(int w, int h, int angle, double M[6])
     M[2] = b1, M[5] = b2;
 }
 
-// A 16-bit (CV_16U, ANYDEPTH) pixel-mask / depth-map record: crop -> INTER_NEAREST -> flip ->
-// convertTo (etl_pixel_mask.cpp:65-92, etl_depthmap.cpp:65-96, image.cpp:176-212).
+// A single-channel pixel-mask / depth-map record, 16-bit (CV_16U, ANYDEPTH) or rotation-free
+// 8-bit: crop -> INTER_NEAREST -> flip -> convertTo (etl_pixel_mask.cpp:65-92,
+// etl_depthmap.cpp:65-96, image.cpp:176-212), one gather pass (mask16_kernels.hip).
 void plan_mask16(const aeon_img_desc& d, const void* src_base, const aeon_aug_params& p, const aeon_out_desc& o,
                  uint8_t* out_item, bool is_mask, std::vector<Mask16Job>& m16)
 {
+    const int eb = d.elem_bytes == 2 ? 2 : 1;
     if (!is_mask) fail(AEON_HIP_EUNSUPPORTED, "16-bit sources are implemented for pixel masks / depth maps only");
     if (d.channels != 1 || o.channels != 1) fail(AEON_HIP_EINVAL, "16-bit masks must have one channel");
-    if (d.width <= 0 || d.height <= 0 || d.stride < d.width * 2 || (d.stride & 1) || (d.offset & 1))
+    if (d.width <= 0 || d.height <= 0 || d.stride < d.width * eb || (eb == 2 && ((d.stride & 1) || (d.offset & 1))))
         fail(AEON_HIP_EINVAL, "invalid 16-bit source image descriptor");
     if (p.angle != 0) fail(AEON_HIP_EUNSUPPORTED, "rotation of 16-bit masks is not implemented");
     if (p.out_w <= 0 || p.out_h <= 0) fail(AEON_HIP_EINVAL, "invalid output size");
@@ -304,6 +307,7 @@ void plan_mask16(const aeon_img_desc& d, const void* src_base, const aeon_aug_pa
     M.out_pitch = o.fixed_aspect_ratio ? o.canvas_w : p.out_w;
     M.flip      = p.flip ? 1 : 0;
     M.dtype     = o.dtype == AEON_DTYPE_F32 ? 1 : 0;
+    M.src_elem  = eb;
     m16.push_back(M);
 }
 
@@ -631,21 +635,26 @@ void close_slots(aeon_hip_ctx* ctx)
     ctx->open_slots.clear();
 }
 
+KernelTimer take_timer(aeon_hip_ctx* ctx, int kind, double bytes)
+{
+    KernelTimer t{};
+    if (!ctx->free_timers.empty()) {
+        t = ctx->free_timers.back();
+        ctx->free_timers.pop_back();
+    } else {
+        HIP_OK(hipEventCreate(&t.start));
+        HIP_OK(hipEventCreate(&t.stop));
+    }
+    t.kind  = kind;
+    t.bytes = bytes;
+    return t;
+}
+
 void timed_launch(aeon_hip_ctx* ctx, int mode, const LaunchPlan& P, const LaunchArgs& a, hipStream_t stream,
                   double bytes, bool timed)
 {
     KernelTimer t{};
-    if (timed) {
-        if (!ctx->free_timers.empty()) {
-            t = ctx->free_timers.back();
-            ctx->free_timers.pop_back();
-        } else {
-            HIP_OK(hipEventCreate(&t.start));
-            HIP_OK(hipEventCreate(&t.stop));
-        }
-        t.kind  = mode;
-        t.bytes = bytes;
-    }
+    if (timed) t = take_timer(ctx, mode, bytes);
     HIP_OK(launch_tiles(mode, P.rm, P.tail, P.photo, a, grid_for(ctx, mode, P, a), stream, timed ? t.start : nullptr,
                         timed ? t.stop : nullptr));
     if (timed) ctx->timers.push_back(t);
@@ -696,7 +705,11 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
     size_t     scratch_bytes = 0;
     for (int i = 0; i < n; i++) {
         uint8_t* item = (uint8_t*)out_dev + (size_t)i * o.item_stride;
-        if (descs[i].elem_bytes == 2) plan_mask16(descs[i], src_base, params[i], o, item, is_mask, m16);
+        // pixel masks without rotation (and every 16-bit record): the NEAREST gather pass
+        const bool gather = descs[i].elem_bytes == 2 ||
+                            (is_mask && descs[i].channels == 1 && o.channels == 1 && params[i].angle == 0 &&
+                             (descs[i].elem_bytes == 0 || descs[i].elem_bytes == 1));
+        if (gather) plan_mask16(descs[i], src_base, params[i], o, item, is_mask, m16);
         else if (descs[i].elem_bytes == 0 || descs[i].elem_bytes == 1)
             plan_image(descs[i], src_base, params[i], o, item, is_mask, rot, pre_all, pre2_all, pass1_all, main_all,
                        scratch_bytes);
@@ -722,8 +735,12 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
     const size_t     rot_off   = 0;
     const size_t     m16_off   = rot_off + rot.size() * sizeof(RotJob);
     size_t           blob      = m16_off + m16.size() * sizeof(Mask16Job);
-    int              m16_max_h = 0;
-    for (const Mask16Job& M : m16) m16_max_h = std::max(m16_max_h, M.out_h);
+    int              m16_max_h = 0, m16_max_w = 0;
+    double           m16_bytes = 0; // algorithmic: crop read once + output written once
+    for (const Mask16Job& M : m16) {
+        m16_max_h = std::max(m16_max_h, M.out_h), m16_max_w = std::max(m16_max_w, M.out_w);
+        m16_bytes += (double)M.crop_w * M.crop_h * M.src_elem + (double)M.out_w * M.out_h * (M.dtype == 1 ? 4 : 1);
+    }
     int              rot_max_px = 0;
     for (const RotJob& R : rot) rot_max_px = std::max(rot_max_px, R.w * R.h);
     std::vector<int> slot_tiles(pass1_all.jobs.size(), 0);
@@ -829,8 +846,13 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
     const bool timed = ctx->timing && (ctx->timing_calls++ % ctx->timing_every) == 0;
     if (o.fixed_aspect_ratio) // std::fill_n of each item's canvas (etl_image.cpp:263)
         HIP_OK(hipMemset2DAsync(out_dev, o.item_stride, 0, (size_t)o.canvas_w * o.canvas_h * o.channels, n, stream));
-    if (!m16.empty())
-        HIP_OK(launch_nearest16((const Mask16Job*)(table + m16_off), (int)m16.size(), m16_max_h, stream));
+    if (!m16.empty()) {
+        KernelTimer t{};
+        if (timed) t = take_timer(ctx, KM_FINAL, m16_bytes);
+        HIP_OK(launch_nearest((const Mask16Job*)(table + m16_off), (int)m16.size(), m16_max_h, m16_max_w, stream,
+                              timed ? t.start : nullptr, timed ? t.stop : nullptr));
+        if (timed) ctx->timers.push_back(t);
+    }
     if (!rot.empty())
         HIP_OK(launch_rotate((const RotJob*)(table + rot_off), (int)rot.size(), rot_max_px, stream));
     for (auto* v : {&pre, &pre2})
