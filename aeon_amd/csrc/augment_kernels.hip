@@ -121,40 +121,55 @@ __device__ __forceinline__ YTap ycoef(int dy, double scale, int sh)
 
 // 24-bit signed multiply-add, full rate.  Spelled in asm: for __mul24 the backend sometimes
 // sign-extends on the scalar unit and then selects the quarter-rate v_mul_lo_u32.  Callers
-// guarantee |operands| < 2^23.  The `_s` form takes a uniform (SGPR) first operand.
+// guarantee |operands| < 2^23.
 __device__ __forceinline__ int mad_i24(int a, int b, int c)
 {
     int r;
     asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
     return r;
 }
-__device__ __forceinline__ int mad_i24_s(int a_uniform, int b, int c)
-{
-    int r;
-    asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(r) : "s"(a_uniform), "v"(b), "v"(c));
-    return r;
-}
 
 // ---- photometric stages (aeon src/image.cpp:336-406 over OpenCV 2.4) ------------------------
-__device__ __forceinline__ void bs_apply(cjob& J, int& b, int& g, int& r)
+// The cv::transform coefficients of the tile's record, copied once per tile into VGPRs (the
+// fixed-point ones for BS_FIXPT, the float ones' bits otherwise): held in SGPRs the compiler
+// re-loads them per pixel under SGPR pressure, and every such scalar load's lgkmcnt(0) wait
+// also drains the pixel's LDS reads.
+struct BsRegs {
+    uint32_t w[9];
+};
+__device__ __forceinline__ uint32_t to_vgpr(uint32_t s)
 {
-    if (J.bs_kind == BS_DIAG) { // diagtransform_8u
-        b = sat_u8(rnd(J.bsm[0] * (float)b + 0.f));
-        g = sat_u8(rnd(J.bsm[4] * (float)g + 0.f));
-        r = sat_u8(rnd(J.bsm[8] * (float)r + 0.f));
-    } else if (J.bs_kind == BS_FIXPT) { // transform_8u, 10-bit fixed point
-        const int  q[9] = {J.bsq[0], J.bsq[1], J.bsq[2], J.bsq[3], J.bsq[4], J.bsq[5], J.bsq[6], J.bsq[7], J.bsq[8]};
+    uint32_t v;
+    asm("v_mov_b32 %0, %1" : "=v"(v) : "s"(s));
+    return v;
+}
+__device__ __forceinline__ BsRegs bs_regs(cjob& J)
+{
+    BsRegs R;
+    const bool fix = J.bs_kind == BS_FIXPT;
+#pragma unroll
+    for (int k = 0; k < 9; k++) R.w[k] = to_vgpr(fix ? (uint32_t)J.bsq[k] : __float_as_uint(J.bsm[k]));
+    return R;
+}
+__device__ __forceinline__ void bs_apply(int kind, const BsRegs& R, int& b, int& g, int& r)
+{
+    const auto m = [&](int k) { return __uint_as_float(R.w[k]); };
+    if (kind == BS_DIAG) { // diagtransform_8u
+        b = sat_u8(rnd(m(0) * (float)b + 0.f));
+        g = sat_u8(rnd(m(4) * (float)g + 0.f));
+        r = sat_u8(rnd(m(8) * (float)r + 0.f));
+    } else if (kind == BS_FIXPT) { // transform_8u, 10-bit fixed point
+        const auto q = [&](int k) { return (int)R.w[k]; };
         // |q| < 2^15, x < 2^8: full-rate 24-bit multiply-adds
-        int        t0 = mad_i24_s(q[0], b, mad_i24_s(q[1], g, mad_i24_s(q[2], r, 512))) >> 10;
-        int        t1 = mad_i24_s(q[3], b, mad_i24_s(q[4], g, mad_i24_s(q[5], r, 512))) >> 10;
-        int        t2 = mad_i24_s(q[6], b, mad_i24_s(q[7], g, mad_i24_s(q[8], r, 512))) >> 10;
+        int t0 = mad_i24(q(0), b, mad_i24(q(1), g, mad_i24(q(2), r, 512))) >> 10;
+        int t1 = mad_i24(q(3), b, mad_i24(q(4), g, mad_i24(q(5), r, 512))) >> 10;
+        int t2 = mad_i24(q(6), b, mad_i24(q(7), g, mad_i24(q(8), r, 512))) >> 10;
         b = sat_u8(t0), g = sat_u8(t1), r = sat_u8(t2);
     } else { // transform_<uchar,float>
-        const float m[9] = {J.bsm[0], J.bsm[1], J.bsm[2], J.bsm[3], J.bsm[4], J.bsm[5], J.bsm[6], J.bsm[7], J.bsm[8]};
-        float        fb = (float)b, fg = (float)g, fr = (float)r;
-        int          t0 = rnd(m[0] * fb + m[1] * fg + m[2] * fr + 0.f);
-        int          t1 = rnd(m[3] * fb + m[4] * fg + m[5] * fr + 0.f);
-        int          t2 = rnd(m[6] * fb + m[7] * fg + m[8] * fr + 0.f);
+        float fb = (float)b, fg = (float)g, fr = (float)r;
+        int   t0 = rnd(m(0) * fb + m(1) * fg + m(2) * fr + 0.f);
+        int   t1 = rnd(m(3) * fb + m(4) * fg + m(5) * fr + 0.f);
+        int   t2 = rnd(m(6) * fb + m(7) * fg + m(8) * fr + 0.f);
         b = sat_u8(t0), g = sat_u8(t1), r = sat_u8(t2);
     }
 }
@@ -596,6 +611,9 @@ struct Bands {
             sh0 = sh[0], sh1 = sh[1], sh2 = sh[2];
         }
         uint32_t sum0 = 0, sum1 = 0, sum2 = 0;
+        BsRegs   bsr{};
+        int      bs_kind = 0;
+        if (PHOTO && (photo & PHOTO_BS)) bs_kind = J.bs_kind, bsr = bs_regs(J);
 
         const int  elem  = (KM != KM_FINAL || a.out_dtype == OUT_U8) ? 1 : 4;
         const int  plane = win_w * J.win_h;
@@ -659,7 +677,7 @@ struct Bands {
 #pragma unroll
                     for (int k = 0; k < 4; k++) {
                         int bb = val[k][0], gg = val[k][1], rr = val[k][2];
-                        if (photo & PHOTO_BS) bs_apply(J, bb, gg, rr);
+                        if (photo & PHOTO_BS) bs_apply(bs_kind, bsr, bb, gg, rr);
                         if (photo & PHOTO_HUE) hue_apply(sdiv, hdiv, lds_ptr<const f32x4>(L.hsv + 2048), J.hue, bb, gg, rr);
                         if (KM == KM_STATS) { // the intermediate keeps the post-hue pixel
                             if (k < nk) sum0 += bb, sum1 += gg, sum2 += rr;
