@@ -44,6 +44,9 @@ __device__ __forceinline__ cjob& job_ref(const LaunchArgs& a, int job)
 __device__ __forceinline__ int sat_u8(int v) { return min(max(v, 0), 255); }
 __device__ __forceinline__ int sat_s16(int v) { return min(max(v, -32768), 32767); }
 __device__ __forceinline__ int rnd(float v) { return (int)__builtin_rintf(v); }
+// saturate_cast<uchar>(float) = sat_u8(cvRound(v)) in one instruction: v_cvt_pk_u8_f32 rounds to
+// nearest even (the default mode) and clamps to [0, 255]
+__device__ __forceinline__ int u8rnd(float v) { return (int)__builtin_amdgcn_cvt_pk_u8_f32(v, 0u, 0u); }
 __device__ __forceinline__ int byte_of(uint32_t p, int c) { return (p >> (8 * c)) & 0xff; }
 // 16x16-bit signed product (v_mul_i32_i24 with word selects): both operands must fit int16
 __device__ __forceinline__ int mul16(int a, int b) { return (int)(short)a * (int)(short)b; }
@@ -155,9 +158,9 @@ __device__ __forceinline__ void bs_apply(int kind, const BsRegs& R, int& b, int&
 {
     const auto m = [&](int k) { return __uint_as_float(R.w[k]); };
     if (kind == BS_DIAG) { // diagtransform_8u
-        b = sat_u8(rnd(m(0) * (float)b + 0.f));
-        g = sat_u8(rnd(m(4) * (float)g + 0.f));
-        r = sat_u8(rnd(m(8) * (float)r + 0.f));
+        b = u8rnd(m(0) * (float)b + 0.f);
+        g = u8rnd(m(4) * (float)g + 0.f);
+        r = u8rnd(m(8) * (float)r + 0.f);
     } else if (kind == BS_FIXPT) { // transform_8u, 10-bit fixed point
         const auto q = [&](int k) { return (int)R.w[k]; };
         // |q| < 2^15, x < 2^8: full-rate 24-bit multiply-adds
@@ -167,10 +170,9 @@ __device__ __forceinline__ void bs_apply(int kind, const BsRegs& R, int& b, int&
         b = sat_u8(t0), g = sat_u8(t1), r = sat_u8(t2);
     } else { // transform_<uchar,float>
         float fb = (float)b, fg = (float)g, fr = (float)r;
-        int   t0 = rnd(m(0) * fb + m(1) * fg + m(2) * fr + 0.f);
-        int   t1 = rnd(m(3) * fb + m(4) * fg + m(5) * fr + 0.f);
-        int   t2 = rnd(m(6) * fb + m(7) * fg + m(8) * fr + 0.f);
-        b = sat_u8(t0), g = sat_u8(t1), r = sat_u8(t2);
+        b = u8rnd(m(0) * fb + m(1) * fg + m(2) * fr + 0.f);
+        g = u8rnd(m(3) * fb + m(4) * fg + m(5) * fr + 0.f);
+        r = u8rnd(m(6) * fb + m(7) * fg + m(8) * fr + 0.f);
     }
 }
 
@@ -203,9 +205,9 @@ __device__ __forceinline__ void hue_apply(TAB sdiv, TAB hdiv, WTAB wtab, int hue
     const float gg = vf * (1.f - sf * w[1]);
     const float rr = vf * (1.f - sf * w[2]);
     // v, s in [0, 1] and w in [0, 1]: every product is in [0, 255], no saturation needed
-    b = rnd(bb * 255.f);
-    g = rnd(gg * 255.f);
-    r = rnd(rr * 255.f);
+    b = u8rnd(bb * 255.f);
+    g = u8rnd(gg * 255.f);
+    r = u8rnd(rr * 255.f);
 }
 
 // ---- source staging (LDS-DMA) ------------------------------------------------------------------
@@ -686,15 +688,15 @@ struct Bands {
                         }
                         if (photo & PHOTO_CONTRAST) {
                             const float c = J.contrast;
-                            bb = sat_u8(rnd((float)((double)((float)bb * c + 0.f) + sh0)));
-                            gg = sat_u8(rnd((float)((double)((float)gg * c + 0.f) + sh1)));
-                            rr = sat_u8(rnd((float)((double)((float)rr * c + 0.f) + sh2)));
+                            bb = u8rnd((float)((double)((float)bb * c + 0.f) + sh0));
+                            gg = u8rnd((float)((double)((float)gg * c + 0.f) + sh1));
+                            rr = u8rnd((float)((double)((float)rr * c + 0.f) + sh2));
                         }
                         if (photo & PHOTO_LIGHTING) {
                             const float la = J.light_a;
-                            bb = sat_u8(sat_u8(rnd((float)bb * la + 0.f)) + J.light_add[0]);
-                            gg = sat_u8(sat_u8(rnd((float)gg * la + 0.f)) + J.light_add[1]);
-                            rr = sat_u8(sat_u8(rnd((float)rr * la + 0.f)) + J.light_add[2]);
+                            bb = sat_u8(u8rnd((float)bb * la + 0.f) + J.light_add[0]);
+                            gg = sat_u8(u8rnd((float)gg * la + 0.f) + J.light_add[1]);
+                            rr = sat_u8(u8rnd((float)rr * la + 0.f) + J.light_add[2]);
                         }
                         val[k][0] = bb, val[k][1] = gg, val[k][2] = rr;
                         __builtin_amdgcn_sched_barrier(0); // one pixel's chain live at a time

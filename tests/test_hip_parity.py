@@ -188,6 +188,12 @@ EDGE_CASES = [
      dict(mean=None, stddev=None)),
     ("brightness_diag", (256, 256), dict(crop_x=0, crop_y=0, crop_w=256, crop_h=256, out_w=224, out_h=224,
                                          brightness=0.6), {}),
+    # x*0.5 and x*1.5 land exactly on .5 for odd x: saturate_cast's round-half-to-even (aeon's
+    # brightness KAT: 127*1.5 -> 190)
+    ("brightness_ties_half", (256, 256), dict(crop_x=0, crop_y=0, crop_w=256, crop_h=256, out_w=224, out_h=224,
+                                              brightness=0.5), {}),
+    ("brightness_ties_1_5", (256, 256), dict(crop_x=0, crop_y=0, crop_w=256, crop_h=256, out_w=224, out_h=224,
+                                             brightness=1.5), {}),
     ("saturation0", (256, 256), dict(crop_x=0, crop_y=0, crop_w=256, crop_h=256, out_w=224, out_h=224,
                                      saturation=0.0, brightness=0.9), {}),
     ("saturation_float_path", (256, 256), dict(crop_x=0, crop_y=0, crop_w=256, crop_h=256, out_w=224,
