@@ -286,7 +286,7 @@ void plan_mask16(const aeon_img_desc& d, const void* src_base, const aeon_aug_pa
     if (!is_mask) fail(AEON_HIP_EUNSUPPORTED, "16-bit sources are implemented for pixel masks / depth maps only");
     if (d.channels != 1 || o.channels != 1) fail(AEON_HIP_EINVAL, "16-bit masks must have one channel");
     if (d.width <= 0 || d.height <= 0 || d.stride < d.width * eb || (eb == 2 && ((d.stride & 1) || (d.offset & 1))))
-        fail(AEON_HIP_EINVAL, "invalid 16-bit source image descriptor");
+        fail(AEON_HIP_EINVAL, eb == 2 ? "invalid 16-bit source image descriptor" : "invalid source image descriptor");
     if (p.angle != 0) fail(AEON_HIP_EUNSUPPORTED, "rotation of 16-bit masks is not implemented");
     if (p.out_w <= 0 || p.out_h <= 0) fail(AEON_HIP_EINVAL, "invalid output size");
     const size_t elem = o.dtype == AEON_DTYPE_F32 ? 4 : 1;
