@@ -56,6 +56,7 @@ struct aeon_error : std::runtime_error {
 constexpr int kMaxLds        = 160 * 1024;
 constexpr int kStageBudget   = 48 * 1024;   // preferred LDS bytes of the two staging buffers
 constexpr int kStageBudgetHi = 140 * 1024;  // fallback for very wide crops
+constexpr size_t kUploadKernelMax = 128 * 1024; // job tables above this go up by SDMA (jobs_mode)
 
 // ---------------------------------------------------------------------------------------------
 // Per-image constants (aeon computes these on the host per record, too)
@@ -519,8 +520,11 @@ struct aeon_hip_ctx {
     // table over PCIe (kernel-to-kernel order, no cross-queue wait: 43.5 vs 44.2 us per C2
     // step); 0 = SDMA H2D on copy_stream + cross-stream event (a ~6.6 us dispatch gap per
     // step); 1 = H2D on the launch stream; 2 = kernels read the pinned table in place
-    // (AEON_HIP_JOBS for experiments)
-    int         jobs_mode = 3;
+    // (AEON_HIP_JOBS for experiments).  -1 (default) = 3 for tables up to kUploadKernelMax,
+    // 0 above: the upload kernel reads PCIe at ~34 GB/s while an SDMA copy of a large table
+    // overlaps the previous call's kernels (C3, 512 KB: 347 vs 357 us per step; C2, 64 KB:
+    // the kernel wins)
+    int         jobs_mode = -1;
     int         n_cu      = 0;
     int         wg_per_cu = 0; // AEON_HIP_WG_PER_CU: experiments only (0 = occupancy API)
     std::vector<std::pair<std::vector<int>, int>> occ; // launch shape -> workgroups per CU
@@ -803,13 +807,14 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
         }
     phase(4);
     const uint8_t* table = s.dev;
-    if (ctx->jobs_mode == 0) {
+    const int      jobs_mode = ctx->jobs_mode >= 0 ? ctx->jobs_mode : (blob > kUploadKernelMax ? 0 : 3);
+    if (jobs_mode == 0) {
         HIP_OK(hipMemcpyAsync(s.dev, s.host, blob, hipMemcpyHostToDevice, ctx->copy_stream));
         HIP_OK(hipEventRecord(s.copied, ctx->copy_stream));
         HIP_OK(hipStreamWaitEvent(stream, s.copied, 0));
-    } else if (ctx->jobs_mode == 3) {
+    } else if (jobs_mode == 3) {
         HIP_OK(launch_upload_table(s.host_dev, s.dev, blob, stream));
-    } else if (ctx->jobs_mode == 1) {
+    } else if (jobs_mode == 1) {
         HIP_OK(hipMemcpyAsync(s.dev, s.host, blob, hipMemcpyHostToDevice, stream));
     } else {
         table = s.host_dev;
