@@ -111,6 +111,9 @@ def lib():
         L.aeon_make_params.argtypes = [vp, P(ctypes.c_uint32), ctypes.c_int, ctypes.c_int,
                                        ctypes.c_int, ctypes.c_int, P(AugParams)]
         L.aeon_seed_slots.argtypes = [ctypes.c_uint32, ctypes.c_int, P(ctypes.c_uint32)]
+        L.aeon_unbiased_round.argtypes = [ctypes.c_float, P(ctypes.c_int64)]
+        L.aeon_calculate_scale.argtypes = [ctypes.c_int] * 4 + [P(ctypes.c_float)]
+        L.aeon_cropbox_max_proportional.argtypes = [ctypes.c_float] * 4 + [P(ctypes.c_float)] * 2
         L.aeon_hip_host_alloc.argtypes = [ctypes.c_size_t, P(vp)]
         L.aeon_hip_host_free.argtypes = [vp]
         L.aeon_decoder_create.argtypes = [ctypes.c_char_p, ctypes.c_int, P(vp)]
@@ -171,6 +174,27 @@ def seed_slots(seed, n):
     out = np.zeros(n, np.uint32)
     _check(lib().aeon_seed_slots(seed, n, out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))))
     return out
+
+
+def unbiased_round(x):
+    """nervana::unbiased_round (aeon src/util.cpp:212-239)."""
+    r = ctypes.c_int64()
+    _check(lib().aeon_unbiased_round(x, ctypes.byref(r)))
+    return r.value
+
+
+def calculate_scale(w, h, out_w, out_h):
+    """image::calculate_scale (aeon src/image.cpp:214-224)."""
+    s = ctypes.c_float()
+    _check(lib().aeon_calculate_scale(w, h, out_w, out_h, ctypes.byref(s)))
+    return s.value
+
+
+def cropbox_max_proportional(in_w, in_h, out_w, out_h):
+    """image::cropbox_max_proportional (aeon src/image.cpp:226-237) -> (width, height)."""
+    rw, rh = ctypes.c_float(), ctypes.c_float()
+    _check(lib().aeon_cropbox_max_proportional(in_w, in_h, out_w, out_h, ctypes.byref(rw), ctypes.byref(rh)))
+    return rw.value, rh.value
 
 
 def aug_params(**kw):

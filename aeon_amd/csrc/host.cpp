@@ -472,13 +472,7 @@ batch_decoder::batch_decoder(const Json& config, int device) : m_device(device)
     // decoder seed = random_seed + node_id (loader.cpp:174); deterministic when non-zero
     const uint32_t dseed = seed ? seed + node_id : 0;
     m_deterministic      = dseed != 0;
-    if (m_deterministic) {
-        // slot engines are seeded lazily per window size from one minstd_rand0(seed)
-        m_random.clear();
-        std::minstd_rand0 g(dseed);
-        m_random.resize(4096);
-        for (auto& e : m_random) e.seed(g());
-    }
+    if (m_deterministic) m_seed_gen.seed(dseed); // slot engines: see slot_engines()
     // the HIP context is created on the first window (configs validate without a GPU)
     m_dev_out.assign(m_provider->providers().size(), nullptr);
     m_dev_out_cap.assign(m_provider->providers().size(), 0);
@@ -498,14 +492,25 @@ batch_decoder::~batch_decoder()
             if (p) (void)hipFree(p);
 }
 
+// Deterministic mode: engine i of the decode window is seeded with the i-th output of
+// minstd_rand0(random_seed + node_id) (batch_decoder.cpp:47-54).  aeon seeds decode_size engines
+// up front; here the table grows with the largest window seen, continuing the same generator, so
+// the first N engines are aeon's for any N.
+void batch_decoder::grow_slot_engines(int n)
+{
+    while ((int)m_random.size() < n) {
+        m_random.emplace_back();
+        m_random.back().seed(m_seed_gen());
+    }
+}
+
 void batch_decoder::decode(int n, const decoded_element* records, void* const* outputs, bool on_device,
                            void* stream_)
 {
     if (n <= 0) return;
     if (!m_batch_major && n % m_batch_size != 0)
         invalid("batch_major=false needs whole batches per decode window");
-    if (m_deterministic && n > (int)m_random.size())
-        invalid("decode window larger than the deterministic slot table (4096)");
+    if (m_deterministic) grow_slot_engines(n);
     if (!m_ctx) check(aeon_hip_ctx_create(m_device, &m_ctx));
     hip_check(hipSetDevice(m_device), "hipSetDevice");
     hipStream_t   stream = (hipStream_t)stream_;

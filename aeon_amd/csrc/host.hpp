@@ -166,10 +166,12 @@ public:
     int            batch_size() const { return m_batch_size; }
 
 private:
+    void                           grow_slot_engines(int n);
     std::shared_ptr<provider_base> m_provider;
     int                            m_batch_size = 1;
     bool                           m_deterministic = false;
     std::vector<std::minstd_rand0> m_random; // one engine per decode slot (batch_decoder.cpp:47-54)
+    std::minstd_rand0              m_seed_gen; // seeds m_random[i] (grow_slot_engines)
     std::minstd_rand0              m_local_random; // non-deterministic mode (util.cpp:266)
     std::unique_ptr<thread_pool>   m_pool;
     aeon_hip_ctx*                  m_ctx = nullptr;

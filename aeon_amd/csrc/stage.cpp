@@ -511,6 +511,7 @@ struct aeon_hip_ctx {
     Slot       slots[kSlots];
     int        next = 0;
     int        done_every = 8;
+    size_t     table_cap = 0, partials_cap = 0, shifts_cap = 0; // per-slot capacities (ensure_ring)
     std::vector<int> open_slots; // used since the last completion event, on open_stream
     hipStream_t      open_stream = nullptr;
     // job tables go up on their own stream, so a call's H2D overlaps the previous call's kernels
@@ -552,6 +553,7 @@ struct aeon_hip_ctx {
 
 struct aeon_param_factory {
     param_factory f;
+    std::mutex    mu; // make_params calls are serialised (the lighting normal_distribution caches a draw)
     explicit aeon_param_factory(const Json& j) : f(j) {}
 };
 
@@ -567,6 +569,44 @@ void grow(uint8_t*& p, size_t& cap, size_t need, bool pinned)
     if (pinned) HIP_OK(hipHostMalloc((void**)&p, n, hipHostMallocDefault));
     else HIP_OK(hipMalloc((void**)&p, n));
     cap = n;
+}
+
+void close_slots(aeon_hip_ctx* ctx);
+
+// Wait until no kernel of any ring slot can still be running.
+void drain_ring(aeon_hip_ctx* ctx)
+{
+    close_slots(ctx);
+    for (Slot& q : ctx->slots)
+        if (q.pending) {
+            HIP_OK(hipEventSynchronize(ctx->slots[q.cover].done));
+            q.pending = false;
+        }
+}
+
+// Ring capacities are shared by all slots and grown for all of them at once (after draining the
+// ring), so the first call -- a warmup -- allocates everything the steady state needs and later
+// calls never pay an allocation when they rotate onto a slot they have not used before.
+void ensure_ring(aeon_hip_ctx* ctx, size_t table, size_t partials, size_t shifts)
+{
+    table = std::max<size_t>(table, 16);
+    if (table <= ctx->table_cap && partials <= ctx->partials_cap && shifts <= ctx->shifts_cap) return;
+    drain_ring(ctx);
+    const size_t tc = table > ctx->table_cap ? std::max(table, ctx->table_cap * 2) : ctx->table_cap;
+    const size_t pc = partials > ctx->partials_cap ? std::max(partials, ctx->partials_cap * 2) : ctx->partials_cap;
+    const size_t sc = shifts > ctx->shifts_cap ? std::max(shifts, ctx->shifts_cap * 2) : ctx->shifts_cap;
+    for (Slot& q : ctx->slots) {
+        grow(q.host, q.host_cap, tc, true);
+        HIP_OK(hipHostGetDevicePointer((void**)&q.host_dev, q.host, 0));
+        grow(q.dev, q.dev_cap, tc, false);
+        uint8_t* p = (uint8_t*)q.partials;
+        grow(p, q.partials_cap, pc, false);
+        q.partials = (uint32_t*)p;
+        uint8_t* r = (uint8_t*)q.shifts;
+        grow(r, q.shifts_cap, sc, false);
+        q.shifts = (double*)r;
+    }
+    ctx->table_cap = tc, ctx->partials_cap = pc, ctx->shifts_cap = sc;
 }
 
 // Device copy of the standardize LUT of output config `o` (uploaded the first time it is seen).
@@ -680,6 +720,10 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
              "Standardization (mean, stddev) is supported only for float or double 'output_type'.");
     if (o.bgr_to_rgb && o.channels != 3)
         fail(AEON_HIP_EINVAL, "invalid config: bgr_to_rgb can be 'true' only for channels set to '3'");
+    // pixel_mask / depthmap loaders never standardize or swap channels (etl_pixel_mask.cpp:94-105,
+    // etl_depthmap.cpp:98-134): refuse both, so rotated and unrotated masks agree
+    if (is_mask && (o.has_mean || o.bgr_to_rgb))
+        fail(AEON_HIP_EINVAL, "pixel masks / depth maps take no mean/stddev and no bgr_to_rgb");
     if (o.fixed_aspect_ratio) {
         // aeon's fixed-aspect loader views the canvas as CV_8U planes whatever the output type
         // (etl_image.cpp:263-305), so only uint8 output has a meaningful layout
@@ -779,21 +823,10 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
     }
     phase(3);
     const float* d_lut = resident_lut(ctx, o);
-    blob = std::max<size_t>(blob, 16);
-    if (blob > s.host_cap) {
-        grow(s.host, s.host_cap, blob, true);
-        HIP_OK(hipHostGetDevicePointer((void**)&s.host_dev, s.host, 0));
-    }
-    if (ctx->jobs_mode != 2) grow(s.dev, s.dev_cap, blob, false);
-    grow(s.scratch, s.scratch_cap, std::max<size_t>(scratch_bytes, 16), false);
-    {
-        uint8_t* p = (uint8_t*)s.partials;
-        grow(p, s.partials_cap, partial_words * 4, false);
-        s.partials = (uint32_t*)p;
-        uint8_t* q = (uint8_t*)s.shifts;
-        grow(q, s.shifts_cap, std::max<size_t>(1, pass1_all.jobs.size()) * 4 * sizeof(double), false);
-        s.shifts = (double*)q;
-    }
+    // job tables, contrast sums and shifts: one capacity for every slot of the ring (a call never
+    // allocates unless it needs more than any call before it); scratch per slot, on demand
+    ensure_ring(ctx, blob, partial_words * 4, std::max<size_t>(1, pass1_all.jobs.size()) * 4 * sizeof(double));
+    if (scratch_bytes > 0) grow(s.scratch, s.scratch_cap, scratch_bytes, false);
     for (RotJob& R : rot) R.out_ptr += (uint64_t)s.scratch;
     if (!rot.empty()) std::memcpy(s.host + rot_off, rot.data(), rot.size() * sizeof(RotJob));
     if (!m16.empty()) std::memcpy(s.host + m16_off, m16.data(), m16.size() * sizeof(Mask16Job));
@@ -951,6 +984,9 @@ int aeon_hip_ctx_create(int device, aeon_hip_ctx** out)
                 HIP_OK(hipEventCreateWithFlags(&s.copied, hipEventDisableTiming));
             }
             HIP_OK(hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
+            // the ring at the size a 512-record call needs (job tables of 128 KB), so steady-state
+            // calls of that size never allocate
+            ensure_ring(c, 128 * 1024, 64 * 1024, 8 * 1024);
             if (const char* e = std::getenv("AEON_HIP_HOST_PROFILE")) c->host_profile = std::atoi(e) != 0;
             if (const char* e = std::getenv("AEON_HIP_JOBS")) c->jobs_mode = std::min(3, std::max(0, std::atoi(e)));
             HIP_OK(hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, device));
@@ -1130,6 +1166,7 @@ int aeon_make_params(aeon_param_factory* f, uint32_t* state, int in_w, int in_h,
 {
     return guarded([&] {
         if (!f || !state || !out) fail(AEON_HIP_EINVAL, "null argument");
+        std::lock_guard<std::mutex> lock(f->mu);
         TrackedEngine eng(*state);
         f->f.make_params(eng, in_w, in_h, out_w, out_h, out);
         *state = eng.last;
@@ -1146,6 +1183,33 @@ int aeon_seed_slots(uint32_t seed, int n, uint32_t* states)
             uint32_t s = g() % 2147483647u;
             states[i]  = s == 0 ? 1 : s;
         }
+        return 0;
+    });
+}
+
+int aeon_unbiased_round(float x, int64_t* out)
+{
+    return guarded([&] {
+        if (!out) fail(AEON_HIP_EINVAL, "null out");
+        *out = unbiased_round(x);
+        return 0;
+    });
+}
+
+int aeon_calculate_scale(int width, int height, int output_width, int output_height, float* scale)
+{
+    return guarded([&] {
+        if (!scale) fail(AEON_HIP_EINVAL, "null out");
+        *scale = calculate_scale(width, height, output_width, output_height);
+        return 0;
+    });
+}
+
+int aeon_cropbox_max_proportional(float in_w, float in_h, float out_w, float out_h, float* res_w, float* res_h)
+{
+    return guarded([&] {
+        if (!res_w || !res_h) fail(AEON_HIP_EINVAL, "null out");
+        cropbox_max_proportional(in_w, in_h, out_w, out_h, res_w, res_h);
         return 0;
     });
 }

@@ -62,7 +62,7 @@ typedef struct aeon_aug_params {
     int32_t crop_x, crop_y, crop_w, crop_h; /* cropbox (cv::Rect) */
     int32_t resize_short_size;              /* 0 = off */
     int32_t out_w, out_h;                   /* output_size */
-    int32_t angle;                          /* rotation (degrees); only 0 supported here */
+    int32_t angle;                          /* rotation (degrees, image::rotate) */
     int32_t flip;                           /* horizontal flip after photometric */
     int32_t padding, pad_off_x, pad_off_y;  /* padding + padding_crop_offset */
     int32_t n_lighting;                     /* 0 or 3 */
@@ -147,11 +147,24 @@ int aeon_hip_kernel_times(aeon_hip_ctx* ctx, double* ms, double* bytes, long* co
 int aeon_param_factory_create(const char* aug_json, aeon_param_factory** out);
 int aeon_param_factory_destroy(aeon_param_factory* f);
 /* param_factory::make_params (src/augment_image.cpp:107-230) drawing from the minstd_rand0
- * engine whose state word is *engine_state (updated in place). */
+ * engine whose state word is *engine_state (updated in place).  Calls on one factory are
+ * serialised internally, but the lighting normal_distribution caches its second draw inside the
+ * factory (as aeon's shared, mutable one does), so reproducible lighting needs one calling thread
+ * making the calls in record order -- aeon's own deterministic order. */
 int aeon_make_params(aeon_param_factory* f, uint32_t* engine_state, int in_w, int in_h,
                      int out_w, int out_h, aeon_aug_params* out);
 /* batch_decoder deterministic mode (src/batch_decoder.cpp:47-54): slot engine state words. */
 int aeon_seed_slots(uint32_t seed, int n, uint32_t* states);
+
+/* Host geometry helpers make_params is built on (exported for callers that derive their own
+ * cropboxes, e.g. a localization provider, and for the reference's known-answer tests):
+ *   nervana::unbiased_round (src/util.cpp:212-239)
+ *   image::calculate_scale (src/image.cpp:214-224)
+ *   image::cropbox_max_proportional (src/image.cpp:226-237) */
+int aeon_unbiased_round(float x, int64_t* out);
+int aeon_calculate_scale(int width, int height, int output_width, int output_height, float* scale);
+int aeon_cropbox_max_proportional(float in_w, float in_h, float out_w, float out_h, float* res_w,
+                                  float* res_h);
 
 /* ---- decode stage: provider_factory + batch_decoder (host C++ above the kernels) --------------
  * aeon_decoder = batch_decoder (src/batch_decoder.cpp:24-99) over provider_factory::create

@@ -101,8 +101,17 @@ def lib():
         L.orc_batch_augment.argtypes = [ctypes.c_int, P(ctypes.c_void_p), P(ctypes.c_int),
                                         P(ctypes.c_int), P(Params), P(LoadConfig), ctypes.c_void_p,
                                         ctypes.c_size_t, ctypes.c_int]
+        L.orc_batch_image_mask.restype = ctypes.c_double
+        L.orc_batch_image_mask.argtypes = [ctypes.c_int, P(ctypes.c_void_p), P(ctypes.c_void_p), P(ctypes.c_int),
+                                           P(ctypes.c_int), P(Params), P(LoadConfig), ctypes.c_void_p,
+                                           ctypes.c_size_t, P(LoadConfig), ctypes.c_void_p, ctypes.c_size_t,
+                                           ctypes.c_int]
         L.orc_rotate.argtypes = [ctypes.c_void_p] + [ctypes.c_int] * 6 + [ctypes.c_void_p]
         L.orc_transpose.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int]
+        L.orc_unbiased_round.argtypes = [ctypes.c_float]
+        L.orc_calculate_scale.restype = ctypes.c_float
+        L.orc_calculate_scale.argtypes = [ctypes.c_int] * 4
+        L.orc_cropbox_max_proportional.argtypes = [ctypes.c_float] * 4 + [P(ctypes.c_float)] * 2
         L.orc_last_error.restype = ctypes.c_char_p
         _lib = L
     return _lib
@@ -161,6 +170,20 @@ def params(**kw):
         else:
             setattr(p, k, v)
     return p
+
+
+def unbiased_round(x):
+    return lib().orc_unbiased_round(x)
+
+
+def calculate_scale(w, h, ow, oh):
+    return lib().orc_calculate_scale(w, h, ow, oh)
+
+
+def cropbox_max_proportional(in_w, in_h, out_w, out_h):
+    rw, rh = ctypes.c_float(), ctypes.c_float()
+    lib().orc_cropbox_max_proportional(in_w, in_h, out_w, out_h, ctypes.byref(rw), ctypes.byref(rh))
+    return rw.value, rh.value
 
 
 def transform_image(src, p):
@@ -257,6 +280,25 @@ def batch_augment(srcs, params_list, lc, item_shape, threads):
     if secs < 0:
         raise RuntimeError("oracle: " + lib().orc_last_error().decode())
     return out, secs
+
+
+def batch_image_mask(srcs, masks, params_list, lc, item_shape, mlc, mask_shape, threads):
+    """CPU-baseline batch of image + pixelmask pairs sharing params; returns (img, mask, seconds)."""
+    n = len(srcs)
+    srcs = [np.ascontiguousarray(s, dtype=np.uint8) for s in srcs]
+    masks = [np.ascontiguousarray(m, dtype=np.uint8) for m in masks]
+    ptrs = (ctypes.c_void_p * n)(*[s.ctypes.data for s in srcs])
+    mptrs = (ctypes.c_void_p * n)(*[m.ctypes.data for m in masks])
+    ws = (ctypes.c_int * n)(*[s.shape[1] for s in srcs])
+    hs = (ctypes.c_int * n)(*[s.shape[0] for s in srcs])
+    ps = (Params * n)(*params_list)
+    out = np.zeros((n,) + tuple(item_shape), np.uint8 if lc.out_dtype == 0 else np.float32)
+    mout = np.zeros((n,) + tuple(mask_shape), np.uint8 if mlc.out_dtype == 0 else np.float32)
+    secs = lib().orc_batch_image_mask(n, ptrs, mptrs, ws, hs, ps, ctypes.byref(lc), out.ctypes.data, out[0].nbytes,
+                                      ctypes.byref(mlc), mout.ctypes.data, mout[0].nbytes, threads)
+    if secs < 0:
+        raise RuntimeError("oracle: " + lib().orc_last_error().decode())
+    return out, mout, secs
 
 
 def transpose(src, rows, cols, element_size):

@@ -773,6 +773,13 @@ int orc_make_params(void* f, uint32_t* state, int in_w, int in_h, int out_w, int
     });
 }
 
+int   orc_unbiased_round(float x) { return unbiased_round(x); }
+float orc_calculate_scale(int w, int h, int ow, int oh) { return calculate_scale(w, h, ow, oh); }
+void  orc_cropbox_max_proportional(float in_w, float in_h, float out_w, float out_h, float* rw, float* rh)
+{
+    cropbox_max_proportional(in_w, in_h, out_w, out_h, rw, rh);
+}
+
 void orc_seed_slots(uint32_t seed, int n, uint32_t* states)
 {
     // engine_i.seed(generator_seed()): minstd's seed(s) keeps s mod m (1 if that is 0),
@@ -873,6 +880,37 @@ double orc_batch_augment(int n, const uint8_t* const* srcs, const int* widths, c
                 load_image(o, *lc, (char*)out + (size_t)i * item_bytes);
             } catch (const std::exception& e) {
                 g_err = e.what();
+                failed = true;
+            }
+        }
+    };
+    auto t0 = std::chrono::steady_clock::now();
+    std::vector<std::thread> pool;
+    for (int t = 0; t < std::max(1, threads); t++) pool.emplace_back(work);
+    for (auto& t : pool) t.join();
+    auto t1 = std::chrono::steady_clock::now();
+    if (failed) return -1.0;
+    return std::chrono::duration<double>(t1 - t0).count();
+}
+
+double orc_batch_image_mask(int n, const uint8_t* const* srcs, const uint8_t* const* masks, const int* widths,
+                            const int* heights, const orc_params* params, const orc_load_config* lc,
+                            void* out, size_t item_bytes, const orc_load_config* mlc, void* mout,
+                            size_t mitem_bytes, int threads)
+{
+    std::atomic<int>  next{0};
+    std::atomic<bool> failed{false};
+    auto              work = [&] {
+        for (;;) {
+            int i = next.fetch_add(1);
+            if (i >= n) break;
+            try {
+                Img s = Img::view(srcs[i], widths[i], heights[i], lc->channels, widths[i] * lc->channels);
+                load_image(transform_single_image(s, params[i]), *lc, (char*)out + (size_t)i * item_bytes);
+                Img m = Img::view(masks[i], widths[i], heights[i], 1, widths[i]);
+                load_image(transform_mask(m, params[i]), *mlc, (char*)mout + (size_t)i * mitem_bytes);
+            } catch (const std::exception& e) {
+                g_err  = e.what();
                 failed = true;
             }
         }

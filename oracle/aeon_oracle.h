@@ -69,6 +69,12 @@ int   orc_make_params(void* f, uint32_t* engine_state, int in_w, int in_h, int o
 /* aeon deterministic-mode slot seeding (src/batch_decoder.cpp:47-54): n engine states. */
 void  orc_seed_slots(uint32_t seed, int n, uint32_t* states);
 
+/* geometry helpers: unbiased_round (src/util.cpp:212-239), calculate_scale (src/image.cpp:214-224),
+ * cropbox_max_proportional (src/image.cpp:226-237) */
+int   orc_unbiased_round(float x);
+float orc_calculate_scale(int w, int h, int ow, int oh);
+void  orc_cropbox_max_proportional(float in_w, float in_h, float out_w, float out_h, float* rw, float* rh);
+
 /* transform_single_image (src/etl_image.cpp:146-202) -> out_h x out_w x cn uint8 HWC BGR. */
 int orc_transform_image(const uint8_t* src, int w, int h, int cn, int src_stride,
                         const orc_params* p, uint8_t* out);
@@ -102,6 +108,13 @@ int orc_transpose(void* dest, const void* src, int64_t rows, int64_t cols, int e
 double orc_batch_augment(int n, const uint8_t* const* srcs, const int* widths, const int* heights,
                          const orc_params* params, const orc_load_config* lc, void* out,
                          size_t item_bytes, int threads);
+
+/* provider_base::provide of an image + pixelmask record pair (src/provider.cpp:109-119) over a
+ * batch on a thread pool: one params set per record for both -- the C5 CPU baseline. */
+double orc_batch_image_mask(int n, const uint8_t* const* srcs, const uint8_t* const* masks, const int* widths,
+                            const int* heights, const orc_params* params, const orc_load_config* lc,
+                            void* out, size_t item_bytes, const orc_load_config* mlc, void* mout,
+                            size_t mitem_bytes, int threads);
 
 const char* orc_last_error(void);
 

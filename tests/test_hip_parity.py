@@ -296,6 +296,52 @@ def test_full_batch_c3_properties(ctx):
     torch.cuda.synchronize()
 
 
+def test_full_batch_c2_all_records(ctx):
+    """BASELINE.json C2 at its headline size: 256 records of 256x256 -> 224x224 fp32 CHW is 1,792
+    tiles on a persistent grid of 768 workgroups, so every workgroup walks 2-3 tiles (the
+    multi-tile staging path every headline number runs).  All 256 records bit-exact against the
+    oracle (test/test_provider.cpp:96-177 semantics, per record); a rerun is bit-identical."""
+    n = 256
+    imgs = _synthetic(n)
+    params = H.draw_params(C.C2_AUG, [(256, 256)] * n, 224, 224, seed=1)
+    out = A.out_desc(**MEAN_OUT)
+    r1 = H.hip_records(ctx, imgs, params, out)
+    r2 = H.hip_records(ctx, imgs, params, out)
+    assert all(np.array_equal(a, b) for a, b in zip(r1, r2)), "C2 rerun differs"
+    _assert_same(r1, H.oracle_records(imgs, params, out), "C2 full batch")
+
+
+def test_full_batch_c5_all_records(ctx):
+    """BASELINE.json C5 at its size: 128 image + pixel-mask pairs, 640x480 sources -> 512x512
+    (image bilinear fp32 CHW, mask NEAREST uint8), shared params; every record of both against
+    the oracle, plus a bit-identical rerun."""
+    n = 128
+    rng = np.random.default_rng(55)
+    imgs = [A.synthetic_image(i, 640, 480, 3) for i in range(n)]
+    masks = [rng.integers(0, 21, (480, 640), dtype=np.uint8) for _ in range(n)]
+    params = H.draw_params(C.C5_AUG, [(640, 480)] * n, 512, 512, seed=1)
+    iout = C.out_desc_for(C.IMAGE_512, C.C5_AUG)
+    mout = C.out_desc_for(C.MASK_512, C.C5_AUG)
+    i1 = H.hip_records(ctx, imgs, params, iout)
+    m1 = H.hip_records(ctx, masks, params, mout, mask=True)
+    i2 = H.hip_records(ctx, imgs, params, iout)
+    m2 = H.hip_records(ctx, masks, params, mout, mask=True)
+    assert all(np.array_equal(a, b) for a, b in zip(i1 + m1, i2 + m2)), "C5 rerun differs"
+    _assert_same(i1, H.oracle_records(imgs, params, iout), "C5 image full batch")
+    _assert_same(m1, H.oracle_records(masks, params, mout, mask=True), "C5 mask full batch")
+
+
+def test_mask_rejects_standardize(ctx):
+    """pixel_mask's loader never standardizes (etl_pixel_mask.cpp:94-105): refused either way."""
+    m = A.synthetic_image(0, 64, 64, 1)
+    p = A.aug_params(crop_x=0, crop_y=0, crop_w=64, crop_h=64, out_w=32, out_h=32)
+    out = A.out_desc(channels=1, dtype="float32", mean=(0.5,), stddev=(0.2,), item_stride=32 * 32 * 4)
+    for angle in (0, 30):
+        p.angle = angle
+        with pytest.raises(A.AeonHipError, match="no mean/stddev"):
+            H.hip_records(ctx, [m], [p], out, mask=True)
+
+
 # ---- batch transpose (batch_major=false layout) ---------------------------------------------
 @pytest.mark.parametrize("rows,cols,esize", [(256, 150528, 4), (7, 1000, 4), (64, 64, 4), (1, 33, 4),
                                              (33, 1, 4), (5, 127, 1), (130, 70, 2), (3, 65, 8)])
