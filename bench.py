@@ -9,11 +9,18 @@ Augmentation parameters come from aeon's deterministic mode (random_seed 1 + nod
 one minstd_rand0 per decode slot) and are drawn on the host before the timed region.
 
 N GPUs: one process per GPU (torch.distributed.run), each an independent manifest slice
-(node_id = rank, node_count = N): no data-path collective; barrier + max-over-ranks timing.
+(node_id = rank, node_count = N, aeon src/manifest_file.cpp:278-295) with decoder seed
+random_seed + node_id (src/loader.cpp:174): no data-path collective; barrier + max-over-ranks
+timing.  `python bench.py --gpus N` with no torchrun environment starts torchrun itself as a
+child process (this parent never touches the GPU).  At N > 1 the line also carries C4 (the C3
+workload at per-GPU batch 1024 on every rank).  --dry-run rehearses the launcher, the slicing
+and the seeding with gloo on the CPU (no GPU work).
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -40,24 +47,80 @@ def parse():
     ap.add_argument("--streams", type=int, default=1, help="development: alternate batches over N streams")
     ap.add_argument("--timing-every", type=int, default=8,
                     help="bracket the kernels of one step in N with HIP events (0 = none)")
+    ap.add_argument("--cpu-extra-seconds", type=float, default=3.0,
+                    help="CPU-baseline sample budget of each of C1/C3/C5")
     ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
+    ap.add_argument("--share-device", action="store_true",
+                    help="development: ranks share the visible GPUs round-robin (gloo barrier), to run "
+                         "the N-rank path on a 1-GPU box")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="CPU rehearsal of the N-rank path (gloo, no GPU): slices, seeds, timing")
     return ap.parse_args()
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(args):
+    """--gpus N without a torchrun environment: run torchrun with N ranks as a CHILD process
+    (never exec: this parent has not initialised the GPU and does not) and exit with its code."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    return subprocess.call(cmd, env=env)
+
+
+def rank_slice(n_records, batch, rank, world):
+    """The record indices of this rank's manifest slice (aeon node slicing) and its decoder
+    seed (random_seed 1 + node_id)."""
+    import aeon_amd as A
+    return A.manifest_node_slice(n_records, batch, rank, world), 1 + rank
+
+
+def synthetic_pool(torch, records, w, h, cn=3, seed=0x5EED, chunk=64, device="cuda"):
+    """A.synthetic_image(g, w, h, cn) for every global record index g, computed on the device:
+    splitmix64 in int64 arithmetic (wrapping add/mul; logical shifts by masking)."""
+    n = len(records)
+    L = w * h * cn
+    out = torch.empty(n * L, dtype=torch.uint8, device=device)
+    idx = torch.arange(L, dtype=torch.int64, device=device)
+
+    def shr(z, k):
+        return (z >> k) & ((1 << (64 - k)) - 1)
+
+    def s64(v):  # uint64 constant as the int64 with the same bits
+        return v - (1 << 64) if v >= 1 << 63 else v
+
+    g = torch.as_tensor(records, dtype=torch.int64, device=device)
+    for a in range(0, n, chunk):
+        gg = g[a:a + chunk, None]
+        z = (seed ^ (gg << 32) ^ idx[None, :]) + s64(0x9E3779B97F4A7C15)
+        z = (z ^ shr(z, 30)) * s64(0xBF58476D1CE4E5B9)
+        z = (z ^ shr(z, 27)) * s64(0x94D049BB133111EB)
+        z = z ^ shr(z, 31)
+        out[a * L:(a + gg.shape[0]) * L] = (z & 0xFF).to(torch.uint8).reshape(-1)
+    return out
 
 
 class Workload:
     """Synthetic already-decoded sources in HBM + pre-drawn params for every step."""
 
-    def __init__(self, A, C, torch, cfg, batch, steps, rank, pool_mib, src_wh=(256, 256)):
+    def __init__(self, A, C, torch, cfg, batch, steps, rank, pool_mib, src_wh=(256, 256), world=1):
         self.batch = batch
         self.aug = {"C2": C.C2_AUG, "C3": C.C3_AUG}[cfg]
         w, h = src_wh
         img_bytes = w * h * 3
         per_batch = batch * img_bytes
         self.n_pool = max(1, (pool_mib << 20) // per_batch)
-        gen = torch.Generator(device="cuda")
-        gen.manual_seed(0x5EED + rank)
-        self.src = torch.randint(0, 256, (self.n_pool * per_batch,), dtype=torch.uint8,
-                                 device="cuda", generator=gen)
+        # this rank's records: its aeon node slice of a manifest of n_pool*batch*world records;
+        # pixels = A.synthetic_image(global record index) generated on the device
+        records, seed = rank_slice(self.n_pool * batch * world, batch, rank, world)
+        self.src = synthetic_pool(torch, records[:self.n_pool * batch], w, h)
         self.descs = [(A.ImgDesc * batch)(*[A.ImgDesc(offset=(b * batch + i) * img_bytes, width=w, height=h,
                                                       stride=w * 3, channels=3) for i in range(batch)])
                       for b in range(self.n_pool)]
@@ -67,7 +130,7 @@ class Workload:
         # aeon deterministic mode: decoder seed = random_seed + node_id (src/loader.cpp:174),
         # one engine per decode slot, persisting across windows (src/batch_decoder.cpp:47-70)
         f = A.ParamFactory(self.aug)
-        states = A.seed_slots(1 + rank, batch)
+        states = A.seed_slots(seed, batch)
         t0 = time.perf_counter()
         self.params = []
         for s in range(steps):
@@ -87,7 +150,7 @@ class Workload:
 
 def run_device(A, C, torch, cfg, batch, steps, warmup, rank, world, pool_mib, dist, timing=8, streams=1):
     ctx = A.Context(torch.cuda.current_device())
-    wl = Workload(A, C, torch, cfg, batch, steps + warmup, rank, pool_mib)
+    wl = Workload(A, C, torch, cfg, batch, steps + warmup, rank, pool_mib, world=world)
     # streams > 1 (development): consecutive batches alternate between caller streams, as a
     # loader double-buffering its output batches would
     strs = [torch.cuda.current_stream().cuda_stream] + [torch.cuda.Stream().cuda_stream for _ in range(streams - 1)]
@@ -106,12 +169,15 @@ def run_device(A, C, torch, cfg, batch, steps, warmup, rank, world, pool_mib, di
     wl.submit_s = time.perf_counter() - t0  # host time to plan + enqueue all steps
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    if dist:
+        dist.barrier()
     for st in strs:
         ctx.synchronize(st)
     kt = ctx.kernel_times()
     ctx.set_timing(False)
     if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     ctx.close()
@@ -226,34 +292,82 @@ def run_c5(A, C, torch, steps, warmup, pool_mib, src_wh=(640, 480)):
             "what": "image 512x512x3 f32 CHW (bilinear) + mask 512x512 u8 (nearest), shared params"}
 
 
-def cpu_baseline(A, C, budget_s):
-    """aeon's CPU path restated (oracle/, C++): thread pool of hc - min(2, hc/8) workers with a
-    dynamic atomic task counter (src/util.cpp:360-370, src/thread_pool.hpp:155-162)."""
-    import oracle as O
-    from tests import helpers as H
-    hc = int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
-    threads = max(1, hc - min(2, hc // 8))
-    n = 256
-    imgs = [A.synthetic_image(i, 256, 256, 3) for i in range(n)]
-    params = H.draw_params(C.C2_AUG, [(256, 256)] * n, 224, 224, seed=1)
-    q = [H.to_oracle_params(p) for p in params]
-    lc = H.oracle_load_config(C.out_desc_for(C.IMAGE_224, C.C2_AUG))
-    done, secs = 0, 0.0
-    while secs < budget_s:
-        _, dt = O.batch_augment(imgs, q, lc, (3, 224, 224), threads)
-        secs += dt
-        done += n
-    cpu = "unknown"
+def pool_threads():
+    """aeon's decode pool size, hc - min(2, hc/8) (src/util.cpp:360-370), over the CPUs this
+    process may use (OMP_NUM_THREADS on the GPU box, else the affinity mask)."""
+    visible = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    hc = int(os.environ.get("OMP_NUM_THREADS") or visible)
+    return max(1, hc - min(2, hc // 8)), hc, visible
+
+
+def cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
             if line.startswith("model name"):
-                cpu = line.split(":", 1)[1].strip()
-                break
+                return line.split(":", 1)[1].strip()
     except OSError:
         pass
-    return {"value": done / secs, "unit": "images/s", "cores": threads, "kind": "port",
-            "sample": f"C2 on {done} synthetic 256x256 records ({secs:.1f} s CPU wall), oracle/ C++ "
-                      f"restatement of aeon's transform+load on {threads} pool threads; CPU: {cpu}"}
+    return "unknown"
+
+
+def cpu_baseline(A, C, budget_s, cfg="C2"):
+    """aeon's CPU path restated (oracle/, C++): a pool of hc - min(2, hc/8) workers with a
+    dynamic atomic task counter (src/util.cpp:360-370, src/thread_pool.hpp:155-162) over
+    decode windows of the config's batch.  Scalar C++ with -ffp-contract=off, not OpenCV's SIMD
+    paths: a LOWER BOUND on aeon's own CPU rate."""
+    import numpy as np
+    import oracle as O
+    from tests import helpers as H
+    threads, hc, visible = pool_threads()
+    if cfg == "C5":
+        n, w, h = 128, 640, 480
+        imgs = [A.synthetic_image(i, w, h, 3) for i in range(n)]
+        rng = np.random.default_rng(5)
+        masks = [rng.integers(0, 21, (h, w), dtype=np.uint8) for _ in range(n)]
+        params = H.draw_params(C.C5_AUG, [(w, h)] * n, 512, 512, seed=1)
+        lc = H.oracle_load_config(C.out_desc_for(C.IMAGE_512, C.C5_AUG))
+        mlc = H.oracle_load_config(C.out_desc_for(C.MASK_512, C.C5_AUG))
+        q = [H.to_oracle_params(p) for p in params]
+        run = lambda: O.batch_image_mask(imgs, masks, q, lc, (3, 512, 512), mlc, (1, 512, 512), threads)[2]
+        what = f"C5 image+mask pairs, {w}x{h} -> 512x512"
+    else:
+        aug = {"C1": C.C1_AUG, "C2": C.C2_AUG, "C3": C.C3_AUG}[cfg]
+        # C1 = aeon's own eval config on decoded images of its golden record's size (480x360)
+        n, w, h = {"C1": (32, 480, 360), "C2": (256, 256, 256), "C3": (256, 256, 256)}[cfg]
+        imgs = [A.synthetic_image(i, w, h, 3) for i in range(n)]
+        params = H.draw_params(aug, [(w, h)] * n, 224, 224, seed=1)
+        lc = H.oracle_load_config(C.out_desc_for(C.IMAGE_224, aug))
+        q = [H.to_oracle_params(p) for p in params]
+        run = lambda: O.batch_augment(imgs, q, lc, (3, 224, 224), threads)[1]
+        what = f"{cfg} on {w}x{h} records -> 224x224 fp32 CHW"
+    done, secs = 0, 0.0
+    while secs < budget_s:
+        secs += run()
+        done += n
+    return {"value": done / secs, "unit": "images/s" if cfg != "C5" else "image+mask pairs/s", "cores": threads,
+            "kind": "port",
+            "sample": f"{what}: {done} records in windows of {n} ({secs:.1f} s CPU wall); oracle/ C++ restatement "
+                      f"of aeon's transform+load on {threads} pool threads (aeon's policy over {hc} usable CPUs; "
+                      f"{visible} in the affinity mask, {os.cpu_count()} on the machine; CPU: {cpu_model()}); "
+                      "scalar C++, a lower bound on aeon's OpenCV-SIMD path"}
+
+
+def run_c1_decoder(A, C, budget_s=2.0):
+    """C1 through the product's decode stage (aeon_decoder: provider_factory + batch_decoder,
+    host records in, host batch out): 32-record windows of 480x360 decoded records."""
+    cfg = dict(C.CONFIGS["C1"], random_seed=1)
+    d = A.Decoder(cfg)
+    recs = [(A.synthetic_image(i, 480, 360, 3),) for i in range(cfg["batch_size"])]
+    d.decode(recs)  # warmup (context, kernels, buffers)
+    done, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < budget_s:
+        d.decode(recs)
+        done += len(recs)
+    dt = time.perf_counter() - t0
+    d.close()
+    return {"value": done / dt, "unit": "images/s", "batch": cfg["batch_size"],
+            "what": "aeon_decoder_decode: host decoded 480x360 records -> pinned H2D -> resize_short 256 + "
+                    "center crop 224 -> fp32 CHW -> D2H, one decode window per call"}
 
 
 def load_traffic(path, cfg):
@@ -264,22 +378,66 @@ def load_traffic(path, cfg):
         return None
 
 
+def dry_run(args, world, rank):
+    """CPU rehearsal of the N-rank path with gloo: every rank takes its aeon node slice and decoder
+    seed, draws its first window of params, and times stub steps; rank 0 prints the line with each
+    rank's slice head / length and slot states, and the max-over-ranks time."""
+    import torch
+    import torch.distributed as dist
+    import aeon_amd as A
+    from aeon_amd import configs as C
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    batch = args.batch or C.CONFIGS[args.config]["batch_size"]
+    n_records = 16 * batch * world
+    records, seed = rank_slice(n_records, batch, rank, world)
+    states = A.seed_slots(seed, 4)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        time.sleep(0.0005)
+    elapsed = time.perf_counter() - t0
+    mine = {"rank": rank, "node_id": rank, "seed": seed, "slice_len": len(records),
+            "slice_head": [int(x) for x in records[:2 * batch]], "slot_states": [int(x) for x in states]}
+    allv = [None] * world
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        dist.all_gather_object(allv, mine)
+        dist.destroy_process_group()
+    else:
+        allv = [mine]
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "n_gpus": world, "steps": args.steps, "batch_per_rank": batch,
+                          "n_records": n_records, "elapsed_max_s": elapsed, "ranks": allv}), flush=True)
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dry_run:
+        return dry_run(args, world, rank)
     import torch
     import aeon_amd as A
     from aeon_amd import configs as C
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", rank=rank, world_size=world,
-                                device_id=torch.device("cuda", local))
+        if args.share_device:
+            torch.cuda.set_device(local % torch.cuda.device_count())
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+        else:
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", rank=rank, world_size=world,
+                                    device_id=torch.device("cuda", local))
     else:
         torch.cuda.set_device(0)
     batch = args.batch or C.CONFIGS[args.config]["batch_size"]
@@ -294,16 +452,25 @@ def main():
     # launch duration (HIP events on the launch stream, on every --timing-every-th step of the
     # timed region; one launch per step unless a batch mixes resize modes)
     achieved = k_bytes / (k_ms * 1e-3) / 1e9 if k_ms else 0.0
+    bytes_per_launch = k_bytes / max(k_n, 1)
 
     extra = {}
+    if world > 1 and not args.no_extra:
+        # C4 (BASELINE configs[3]): the full augment_image workload at per-GPU batch 1024 on every
+        # rank, each its own node slice and seed; global batch 1024 * N
+        st4 = max(5, args.steps // 5)
+        e4, kt4, _, _ = run_device(A, C, torch, "C3", 1024, st4, 2, rank, world, args.pool_mib, dist)
+        extra["C4"] = {"value": 1024 * st4 * world / e4, "unit": "images/s", "batch_per_gpu": 1024,
+                       "global_batch": 1024 * world, "steps": st4, "ms_per_step": e4 / st4 * 1e3,
+                       "what": "C3 workload on every rank (node slice + seed 1 + node_id), max over ranks"}
     if rank == 0 and world == 1 and not args.no_extra:
         if args.config == "C2":
-            e3, kt3, _, _ = run_device(A, C, torch, "C3", 1024, max(5, args.steps // 5), 2, 0, 1,
-                                       args.pool_mib, None)
             st3 = max(5, args.steps // 5)
+            e3, kt3, _, _ = run_device(A, C, torch, "C3", 1024, st3, 2, 0, 1, args.pool_mib, None)
             m3, b3, n3 = kt3["augment"]
             s3 = kt3["stats"]
             extra["C3"] = {"value": 1024 * st3 / e3, "unit": "images/s", "batch": 1024,
+                           "ms_per_step": e3 / st3 * 1e3,
                            "augment_kernel_avg_launch_ms": m3 / max(n3, 1),
                            "stats_kernel_avg_launch_ms": s3[0] / max(s3[2], 1),
                            "augment_kernel_gbs": b3 / (m3 * 1e-3) / 1e9 if m3 else 0}
@@ -319,6 +486,11 @@ def main():
         extra["C5"] = run_c5(A, C, torch, max(5, args.steps // 5), 2, args.pool_mib)
         extra["e2e_host_to_host"] = {"value": run_e2e(A, C, torch, 256, 20), "unit": "images/s",
                                      "what": "pinned H2D of decoded 256x256 u8 + kernel + D2H of fp32 CHW"}
+        extra["C1"] = {"decoder": run_c1_decoder(A, C)}
+        if not args.no_cpu_baseline:
+            extra["C1"]["cpu_baseline"] = cpu_baseline(A, C, args.cpu_extra_seconds, "C1")
+            extra["C3"]["cpu_baseline"] = cpu_baseline(A, C, args.cpu_extra_seconds, "C3") if "C3" in extra else None
+            extra["C5"]["cpu_baseline"] = cpu_baseline(A, C, args.cpu_extra_seconds, "C5")
 
     line = {
         "metric": METRIC,
@@ -331,25 +503,31 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
+        # integer pixel arithmetic (u8 fixed-point resize / photometric), f32 only in the final
+        # standardize of the 3x224x224 float32 CHW output
         "dtype": "u8",
-        "data": "synthetic: counter-free torch.randint HWC u8 256x256 sources resident in HBM",
+        "data": "synthetic: A.synthetic_image (splitmix64) HWC u8 256x256 sources of this rank's manifest "
+                "slice, resident in HBM",
         "config": {"workload": f"{args.config}: " + {
             "C2": "random crop + flip + bilinear resize to 224x224, standardize, CHW fp32",
             "C3": "full augment_image (brightness/contrast/saturation/hue/lighting), CHW fp32"}[args.config],
             "batch_per_gpu": batch, "global_batch": batch * world, "source": "256x256x3 u8 HWC",
-            "output": "3x224x224 float32 CHW", "parallelism": f"dp{world} (manifest node slices)"},
+            "output": "3x224x224 float32 CHW",
+            "parallelism": f"dp{world}: one aeon manifest node slice + seed per rank, no collective"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS,
                      "traffic": load_traffic(args.traffic_file, args.config),
                      "kernel": "augment_tiles<KM_FINAL,...>", "kernel_avg_launch_ms": k_ms / max(k_n, 1),
-                     "algorithmic_bytes_per_launch": k_bytes / max(k_n, 1), "timed_launches": k_n},
+                     "algorithmic_bytes_per_launch": bytes_per_launch, "timed_launches": k_n,
+                     # the same algorithmic bytes over the whole step (upload + kernel + host)
+                     "step_gbs": bytes_per_launch / (elapsed / args.steps) / 1e9 if k_n else None},
         "host_make_params_us_per_record": param_us,
         "host_submit_ms_per_step": submit_s / args.steps * 1e3,
     }
     if extra:
         line["extra"] = extra
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline(A, C, args.cpu_seconds)
+        line["cpu_baseline"] = cpu_baseline(A, C, args.cpu_seconds, args.config)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if dist:
