@@ -20,6 +20,7 @@
 #include "mask16.hpp"
 #include "json.hpp"
 #include "param_factory.hpp"
+#include "plan_record.hpp"
 
 namespace aeon_hip {
 hipError_t launch_tiles(int km, int rm, bool tail, bool photo, const LaunchArgs& a, int grid, hipStream_t stream,
@@ -33,6 +34,7 @@ hipError_t launch_rotate(const RotJob* jobs, int n_jobs, int max_pixels, hipStre
 hipError_t launch_nearest(const Mask16Job* jobs, int n_jobs, int max_h, int max_w, hipStream_t stream,
                           hipEvent_t start, hipEvent_t stop);
 hipError_t launch_upload_table(const void* host_dev, void* dst, size_t bytes, hipStream_t stream);
+hipError_t launch_plan_records(const void* host_records, void* jobs, const PlanArgs& a, hipStream_t stream);
 } // namespace aeon_hip
 
 using namespace aeon_hip;
@@ -62,74 +64,6 @@ constexpr size_t kUploadKernelMax = 128 * 1024; // job tables above this go up b
 // Per-image constants (aeon computes these on the host per record, too)
 // ---------------------------------------------------------------------------------------------
 
-// OpenCV 2.4 cv::resize dispatch for 8U: identity, INTER_NEAREST, 2x INTER_LINEAR -> area fast
-// path, generic INTER_LINEAR.
-// An identity resize (image::resize's same-size shortcut) is planned as LINEAR / NEAREST: with
-// scale 1 every LINEAR tap is (sx = dx, weights 2048/0), which reproduces the source exactly
-// through both OpenCV vertical formulas, so no separate copy launch is needed.
-int choose_mode(int sw, int sh, int dw, int dh, int interp, int cn)
-{
-    if (interp == AEON_INTERP_NEAREST) return RESIZE_NEAREST;
-    if (sw == dw && sh == dh) return RESIZE_LINEAR;
-    double sx = 1. / ((double)dw / sw), sy = 1. / ((double)dh / sh);
-    int    ix = cv_round(sx), iy = cv_round(sy);
-    bool   fast = std::abs(sx - ix) < DBL_EPSILON && std::abs(sy - iy) < DBL_EPSILON;
-    if (fast && ix == 2 && iy == 2 && (cn == 1 || cn == 3)) return RESIZE_AREA2X;
-    return RESIZE_LINEAR;
-}
-
-// First element of a W-element destination row handled by OpenCV's scalar tail after
-// VResizeLinearVec_32s8u (16-wide loop while x <= W-16, 4-wide while x < W-4).
-int simd_boundary(int W)
-{
-    int x = W >= 16 ? (W / 16) * 16 : 0;
-    while (x < W - 4) x += 4;
-    return x;
-}
-
-// photometric::cbsjitter brightness/saturation matrix (src/image.cpp:362-373) and the
-// cv::transform path OpenCV 2.4 picks for it.
-void plan_bs(AugJob& J, float brightness, float saturation)
-{
-    const float g[3] = {0.0820f, 0.6094f, 0.3086f};
-    float       M[9];
-    float       oms = 1 - saturation;
-    for (int i = 0; i < 3; i++)
-        for (int j = 0; j < 3; j++) {
-            float A = i == j ? saturation : 0.f;
-            float B = (float)((double)oms * (double)g[j]);
-            M[i * 3 + j] = brightness == 1.0f ? A + B
-                                              : (float)((double)A * brightness + (double)B * brightness + 0.0);
-        }
-    bool diag = true;
-    for (int i = 0; i < 3; i++)
-        for (int j = 0; j < 3; j++)
-            if (i != j && std::fabs((double)M[i * 3 + j]) > FLT_EPSILON) diag = false;
-    bool fixpt = true;
-    for (int k = 0; k < 9; k++)
-        if (!(std::fabs(M[k]) < 32.f)) fixpt = false;
-    for (int k = 0; k < 9; k++) {
-        J.bsm[k] = M[k];
-        J.bsq[k] = std::min(std::max(cv_roundf(M[k] * 1024), -32768), 32767);
-    }
-    J.bs_kind = diag ? BS_DIAG : (fixpt ? BS_FIXPT : BS_FLOAT);
-}
-
-// photometric::lighting (src/image.cpp:320-346): the PCA pixel and its (1+sigma) scaling.
-void plan_lighting(AugJob& J, const float* al, float sigma)
-{
-    static const float CPCA[3][3] = {{0.39731118f, 0.70119634f, -0.59200296f},
-                                     {-0.81698062f, -0.02354167f, -0.57618440f},
-                                     {0.41795513f, -0.71257945f, -0.56351045f}};
-    static const float CSTD[3]    = {19.72083305f, 37.09388853f, 121.78006099f};
-    float              v[3], px[3];
-    for (int k = 0; k < 3; k++) v[k] = CSTD[k] * al[k];
-    for (int i = 0; i < 3; i++) px[i] = CPCA[i][0] * v[0] + CPCA[i][1] * v[1] + CPCA[i][2] * v[2];
-    const double a = 1. / (1.0 + (double)sigma);
-    J.light_a      = (float)a;
-    for (int k = 0; k < 3; k++) J.light_add[k] = cv_round((double)px[k] * a);
-}
-
 // image::standardize arithmetic (src/image.cpp:129-174 over OpenCV 2.4 arithm_op: f64 work
 // type per op, rounded to f32 after each op) tabulated per channel and input value.
 void build_lut(const aeon_out_desc& o, float* lut)
@@ -150,8 +84,16 @@ void build_lut(const aeon_out_desc& o, float* lut)
     }
 }
 
+// What the launch planner needs to know of a job (the fields share AugJob's names, so the
+// templates below take either).
+struct JobGeom {
+    int32_t mode, cn, crop_w, crop_h, win_w, win_h, dst_w, dst_h, photo, stats_slot;
+    double  scale_x, scale_y;
+};
+
 // source-footprint bounds used to size the LDS staging area
-int stage_cols(const AugJob& J)
+template <typename J_>
+int stage_cols(const J_& J)
 {
     switch (J.mode) {
     // +1: the second tap column is staged even where its weight is 0
@@ -161,7 +103,8 @@ int stage_cols(const AugJob& J)
     default: return J.win_w;
     }
 }
-int stage_rows_for(const AugJob& J, int tr)
+template <typename J_>
+int stage_rows_for(const J_& J, int tr)
 {
     int rows = std::min(tr, J.win_h);
     switch (J.mode) {
@@ -183,11 +126,24 @@ struct LaunchPlan {
     bool                vec_ok = true;
     bool                has_hue = false, has_contrast = false;
 
+    // launch shape for this->jobs, and each job's tile count
     void finalize()
     {
         if (jobs.empty()) return;
+        shape(jobs);
+        max_tiles = 0;
+        for (AugJob& J : jobs) {
+            J.tiles   = (J.win_h + tr - 1) / tr;
+            max_tiles = std::max(max_tiles, J.tiles);
+        }
+    }
+
+    // workgroup size, rows per tile, LDS staging size for a set of jobs (AugJob or JobGeom)
+    template <typename J_>
+    void shape(const std::vector<J_>& jobs)
+    {
         int ww = 0;
-        for (const AugJob& J : jobs) ww = std::max(ww, J.win_w);
+        for (const J_& J : jobs) ww = std::max(ww, J.win_w);
         max_win_w = std::max(ww, 1);
         // workgroup = 256..512 lanes holding whole 4-pixel column groups (fewest idle lanes;
         // ties go to the larger group), row phases = lanes / column groups
@@ -218,7 +174,7 @@ struct LaunchPlan {
         if (const char* e = std::getenv("AEON_HIP_STAGE_KB")) budget = std::max(1, std::atoi(e)) * 1024;
         if (const char* e = std::getenv("AEON_HIP_TR")) tr_cap = std::min(64, std::max(1, std::atoi(e)));
         bool hue = false, contrast = false;
-        for (const AugJob& J : jobs) {
+        for (const J_& J : jobs) {
             hue |= (J.photo & PHOTO_HUE) != 0;
             contrast |= (J.photo & PHOTO_CONTRAST) != 0 && J.stats_slot >= 0;
         }
@@ -229,7 +185,7 @@ struct LaunchPlan {
                 // staged rows x whole 4-pixel groups, in whole DMA instructions (64 groups = 1 KiB
                 // for BGR, 64 gray pixels = 256 B)
                 long by = 0;
-                for (const AugJob& J : jobs) {
+                for (const J_& J : jobs) {
                     const long groups = (long)stage_rows_for(J, t) * ((stage_cols(J) + 3) / 4);
                     by = std::max(by, J.cn == 3 ? (groups + 63) / 64 * 1024 : (groups * 4 + 63) / 64 * 256);
                 }
@@ -246,11 +202,6 @@ struct LaunchPlan {
         if (lds > kMaxLds)
             fail(AEON_HIP_EUNSUPPORTED, "source crop too wide for LDS-staged row bands (" + std::to_string(lds) +
                                             " bytes)");
-        max_tiles = 0;
-        for (AugJob& J : jobs) {
-            J.tiles   = (J.win_h + tr - 1) / tr;
-            max_tiles = std::max(max_tiles, J.tiles);
-        }
     }
 };
 
@@ -312,11 +263,8 @@ void plan_mask16(const aeon_img_desc& d, const void* src_base, const aeon_aug_pa
     m16.push_back(M);
 }
 
-// Launch order: rot (image::rotate) -> pre (resize_short) -> pre2 (2x-area resize ahead of photometric stages) ->
-// pass1 (contrast statistics) -> main; each reads only what an earlier group wrote.
-void plan_image(const aeon_img_desc& d, const void* src_base, const aeon_aug_params& p,
-                const aeon_out_desc& o, uint8_t* out_item, bool is_mask, std::vector<RotJob>& rot,
-                LaunchPlan& pre, LaunchPlan& pre2, LaunchPlan& pass1, LaunchPlan& main, size_t& scratch_bytes)
+// Checks of one 8-bit record aeon's transformer would throw on (or that this stage refuses).
+void validate_record(const aeon_img_desc& d, const aeon_aug_params& p, const aeon_out_desc& o, bool is_mask)
 {
     const int cn = d.channels;
     if (cn != 1 && cn != 3) fail(AEON_HIP_EINVAL, "channels must be 1 or 3");
@@ -332,12 +280,28 @@ void plan_image(const aeon_img_desc& d, const void* src_base, const aeon_aug_par
         fail(AEON_HIP_EINVAL, "output item does not fit item_stride");
     if (o.fixed_aspect_ratio && (p.out_w > o.canvas_w || p.out_h > o.canvas_h))
         fail(AEON_HIP_EINVAL, "fixed_aspect_ratio: output_size larger than the image canvas");
+    int base_w = d.width, base_h = d.height;
+    if (!is_mask && p.resize_short_size > 0) get_resized_short_size(d.width, d.height, p.resize_short_size, &base_w, &base_h);
+    if (p.crop_x < 0 || p.crop_y < 0 || p.crop_w <= 0 || p.crop_h <= 0 || p.crop_x + p.crop_w > base_w ||
+        p.crop_y + p.crop_h > base_h)
+        fail(AEON_HIP_EINVAL, base_w == d.width && base_h == d.height ? "cropbox outside image"
+                                                                      : "cropbox outside the resize_short image");
+    if (!is_mask && photo_flags(p) && cn != 3) fail(AEON_HIP_EINVAL, "photometric augmentation needs a 3-channel image");
+    if (!is_mask && (p.n_lighting != 0 && p.n_lighting != 3)) fail(AEON_HIP_EINVAL, "lighting needs 3 values");
+}
 
-    AugJob J{};
-    J.src_ptr    = (uint64_t)((const uint8_t*)src_base + d.offset);
-    J.src_bytes  = (uint64_t)d.stride * d.height;
-    J.src_w      = d.width, J.src_h = d.height, J.src_stride = d.stride, J.cn = cn;
-    J.stats_slot = -1;
+OutGeom out_geom(const aeon_out_desc& o) { return OutGeom{o.fixed_aspect_ratio, o.canvas_w, o.canvas_h}; }
+
+// Launch order: rot (image::rotate) -> pre (resize_short) -> pre2 (2x-area resize ahead of photometric stages) ->
+// pass1 (contrast statistics) -> main; each reads only what an earlier group wrote.
+void plan_image(const aeon_img_desc& d, const void* src_base, const aeon_aug_params& p,
+                const aeon_out_desc& o, uint8_t* out_item, bool is_mask, std::vector<RotJob>& rot,
+                LaunchPlan& pre, LaunchPlan& pre2, LaunchPlan& pass1, LaunchPlan& main, size_t& scratch_bytes)
+{
+    validate_record(d, p, o, is_mask);
+    const int cn = d.channels;
+    AugJob    J;
+    plan_direct(d, (uint64_t)src_base, p, out_geom(o), (uint64_t)out_item, is_mask, J);
     if (p.angle != 0) {
         // image::rotate into scratch (interpolated for images, nearest + border 0 for pixel
         // masks, etl_pixel_mask.cpp:72-74); everything after reads the rotated record
@@ -355,18 +319,16 @@ void plan_image(const aeon_img_desc& d, const void* src_base, const aeon_aug_par
         J.src_bytes   = (uint64_t)d.width * d.height * cn;
         J.src_stride  = d.width * cn;
     }
-
-    int base_w = d.width, base_h = d.height;
     if (!is_mask && p.resize_short_size > 0) {
         // image::resize_short (image.cpp:118-127) into a device scratch, cropbox window only
         int rw, rh;
         get_resized_short_size(d.width, d.height, p.resize_short_size, &rw, &rh);
-        if (p.crop_x < 0 || p.crop_y < 0 || p.crop_w <= 0 || p.crop_h <= 0 ||
-            p.crop_x + p.crop_w > rw || p.crop_y + p.crop_h > rh)
-            fail(AEON_HIP_EINVAL, "cropbox outside the resize_short image");
         AugJob P = J;
+        P.photo   = 0;
+        P.flip    = 0;
+        P.shift_x = P.shift_y = P.padded = 0;
         P.crop_x = 0, P.crop_y = 0, P.crop_w = d.width, P.crop_h = d.height;
-        P.mode    = choose_mode(d.width, d.height, rw, rh, interp, cn);
+        P.mode    = choose_mode(d.width, d.height, rw, rh, p.interp, cn);
         P.scale_x = 1. / ((double)rw / d.width);
         P.scale_y = 1. / ((double)rh / d.height);
         P.dst_w = rw, P.dst_h = rh;
@@ -381,91 +343,50 @@ void plan_image(const aeon_img_desc& d, const void* src_base, const aeon_aug_par
         J.src_w = p.crop_w, J.src_h = p.crop_h, J.src_stride = p.crop_w * cn;
         J.crop_x = 0, J.crop_y = 0;
         J.src_scratch = 1; // relocated to the slot's scratch by the caller
-        base_w = p.crop_w, base_h = p.crop_h;
-    } else {
-        if (p.crop_x < 0 || p.crop_y < 0 || p.crop_w <= 0 || p.crop_h <= 0 ||
-            p.crop_x + p.crop_w > base_w || p.crop_y + p.crop_h > base_h)
-            fail(AEON_HIP_EINVAL, "cropbox outside image");
-        J.crop_x = p.crop_x, J.crop_y = p.crop_y;
     }
-    J.crop_w = p.crop_w, J.crop_h = p.crop_h;
-    if (!is_mask && !(p.padding == 0 || (p.pad_off_x == p.padding && p.pad_off_y == p.padding))) {
-        J.shift_x = p.pad_off_x - p.padding;
-        J.shift_y = p.pad_off_y - p.padding;
-        J.padded  = 1;
+    const int photo = J.photo;
+    if (photo && J.mode == RESIZE_AREA2X) {
+        // 2x-area resize first (resize-only pre-pass into scratch, unflipped), then the
+        // photometric stages as a copy pass over it
+        AugJob P      = J;
+        P.photo       = 0;
+        P.flip        = 0;
+        size_t off    = (scratch_bytes + 15) & ~(size_t)15;
+        scratch_bytes = off + (size_t)J.win_w * J.win_h * 3 + 16;
+        P.out_ptr     = off; // relocated to the slot's scratch by the caller
+        pre2.jobs.push_back(P);
+        J.src_ptr     = off;
+        J.src_scratch = 1;
+        J.src_bytes   = (uint64_t)J.win_w * J.win_h * 3;
+        J.src_w = J.win_w, J.src_h = J.win_h, J.src_stride = J.win_w * 3;
+        J.crop_x = J.crop_y = 0, J.crop_w = J.win_w, J.crop_h = J.win_h;
+        J.shift_x = J.shift_y = J.padded = 0;
+        J.mode    = RESIZE_COPY;
+        J.scale_x = J.scale_y = 1.0;
+        J.xv      = simd_boundary(J.win_w * 3);
     }
-    J.mode    = choose_mode(J.crop_w, J.crop_h, p.out_w, p.out_h, interp, cn);
-    J.scale_x = 1. / ((double)p.out_w / J.crop_w);
-    J.scale_y = 1. / ((double)p.out_h / J.crop_h);
-    J.dst_w = p.out_w, J.dst_h = p.out_h;
-    J.win_x = 0, J.win_y = 0, J.win_w = p.out_w, J.win_h = p.out_h;
-    J.xv      = simd_boundary(p.out_w * cn);
-    J.flip    = p.flip ? 1 : 0;
-    J.out_ptr = (uint64_t)out_item;
-    // image::loader::load (etl_image.cpp:258-306): planes of the record's own size, or with
-    // fixed_aspect_ratio the record at the top-left of the (zeroed) config-sized canvas
-    J.out_pitch = o.fixed_aspect_ratio ? o.canvas_w : p.out_w;
-    J.out_plane = o.fixed_aspect_ratio ? o.canvas_w * o.canvas_h : p.out_w * p.out_h;
-
-    if (!is_mask) {
-        int photo = 0;
-        if (p.brightness != 1.0 || p.saturation != 1.0) photo |= PHOTO_BS;
-        if (p.hue != 0) photo |= PHOTO_HUE;
-        if (p.contrast != 1.0) photo |= PHOTO_CONTRAST;
-        if (p.n_lighting > 0) photo |= PHOTO_LIGHTING;
-        if (photo && cn != 3)
-            fail(AEON_HIP_EINVAL, "photometric augmentation needs a 3-channel image");
-        if (photo & PHOTO_BS) plan_bs(J, p.brightness, p.saturation);
-        J.contrast = p.contrast;
-        J.hue      = p.hue;
-        if (photo & PHOTO_LIGHTING) {
-            if (p.n_lighting != 3) fail(AEON_HIP_EINVAL, "lighting needs 3 values");
-            plan_lighting(J, p.lighting, p.color_noise_std);
-        }
-        J.photo = photo;
-        if (photo && J.mode == RESIZE_AREA2X) {
-            // 2x-area resize first (resize-only pre-pass into scratch, unflipped), then the
-            // photometric stages as a copy pass over it
-            AugJob P      = J;
-            P.photo       = 0;
-            P.flip        = 0;
-            size_t off    = (scratch_bytes + 15) & ~(size_t)15;
-            scratch_bytes = off + (size_t)J.win_w * J.win_h * 3 + 16;
-            P.out_ptr     = off; // relocated to the slot's scratch by the caller
-            pre2.jobs.push_back(P);
-            J.src_ptr     = off;
-            J.src_scratch = 1;
-            J.src_bytes   = (uint64_t)J.win_w * J.win_h * 3;
-            J.src_w = J.win_w, J.src_h = J.win_h, J.src_stride = J.win_w * 3;
-            J.crop_x = J.crop_y = 0, J.crop_w = J.win_w, J.crop_h = J.win_h;
-            J.shift_x = J.shift_y = J.padded = 0;
-            J.mode    = RESIZE_COPY;
-            J.scale_x = J.scale_y = 1.0;
-            J.xv      = simd_boundary(J.win_w * 3);
-        }
-        if (photo & PHOTO_CONTRAST) {
-            // contrast needs the mean of the post-hue image: pass 1 writes that image (HWC
-            // uint8, unflipped) and its exact per-chunk sums; pass 2 (this job) reads it back
-            AugJob P1     = J;
-            P1.flip       = 0;
-            P1.photo      = photo & (PHOTO_BS | PHOTO_HUE | PHOTO_CONTRAST);
-            P1.stats_slot = (int)pass1.jobs.size();
-            size_t off    = (scratch_bytes + 15) & ~(size_t)15;
-            scratch_bytes = off + (size_t)J.win_w * J.win_h * 3 + 16;
-            P1.out_ptr    = off; // relocated to the slot's scratch by the caller
-            pass1.jobs.push_back(P1);
-            J.stats_slot  = P1.stats_slot;
-            J.src_ptr     = off;
-            J.src_scratch = 1;
-            J.src_bytes   = (uint64_t)J.win_w * J.win_h * 3;
-            J.src_w = J.win_w, J.src_h = J.win_h, J.src_stride = J.win_w * 3;
-            J.crop_x = J.crop_y = 0, J.crop_w = J.win_w, J.crop_h = J.win_h;
-            J.shift_x = J.shift_y = J.padded = 0;
-            J.mode    = RESIZE_COPY;
-            J.scale_x = J.scale_y = 1.0;
-            J.xv      = simd_boundary(J.win_w * 3);
-            J.photo   = photo & (PHOTO_CONTRAST | PHOTO_LIGHTING);
-        }
+    if (photo & PHOTO_CONTRAST) {
+        // contrast needs the mean of the post-hue image: pass 1 writes that image (HWC
+        // uint8, unflipped) and its exact per-chunk sums; pass 2 (this job) reads it back
+        AugJob P1     = J;
+        P1.flip       = 0;
+        P1.photo      = photo & (PHOTO_BS | PHOTO_HUE | PHOTO_CONTRAST);
+        P1.stats_slot = (int)pass1.jobs.size();
+        size_t off    = (scratch_bytes + 15) & ~(size_t)15;
+        scratch_bytes = off + (size_t)J.win_w * J.win_h * 3 + 16;
+        P1.out_ptr    = off; // relocated to the slot's scratch by the caller
+        pass1.jobs.push_back(P1);
+        J.stats_slot  = P1.stats_slot;
+        J.src_ptr     = off;
+        J.src_scratch = 1;
+        J.src_bytes   = (uint64_t)J.win_w * J.win_h * 3;
+        J.src_w = J.win_w, J.src_h = J.win_h, J.src_stride = J.win_w * 3;
+        J.crop_x = J.crop_y = 0, J.crop_w = J.win_w, J.crop_h = J.win_h;
+        J.shift_x = J.shift_y = J.padded = 0;
+        J.mode    = RESIZE_COPY;
+        J.scale_x = J.scale_y = 1.0;
+        J.xv      = simd_boundary(J.win_w * 3);
+        J.photo   = photo & (PHOTO_CONTRAST | PHOTO_LIGHTING);
     }
     if ((J.out_ptr & 15) != 0 || (J.win_w & 3) != 0 || o.fixed_aspect_ratio) main.vec_ok = false;
     main.jobs.push_back(J);
@@ -512,6 +433,10 @@ struct aeon_hip_ctx {
     int        next = 0;
     int        done_every = 8;
     size_t     table_cap = 0, partials_cap = 0, shifts_cap = 0; // per-slot capacities (ensure_ring)
+    // device planning (run_direct): calls whose records are one job each of one launch group
+    // upload the caller's descriptors + params and let plan_records build the jobs on the GPU
+    bool                 device_plan = true; // AEON_HIP_DEVICE_PLAN=0: always plan on the host
+    std::vector<JobGeom> geoms;              // reused per call
     std::vector<int> open_slots; // used since the last completion event, on open_stream
     hipStream_t      open_stream = nullptr;
     // job tables go up on their own stream, so a call's H2D overlaps the previous call's kernels
@@ -631,10 +556,11 @@ const float* resident_lut(aeon_hip_ctx* ctx, const aeon_out_desc& o)
 
 // Algorithmic bytes of one launch: the resampled u8 source footprint plus
 // the bytes written (KM_STATS / KM_RAW write an HWC uint8 intermediate).
-double launch_bytes(const LaunchPlan& L, int mode, size_t out_elem)
+template <typename J_>
+double launch_bytes(const std::vector<J_>& jobs, int mode, size_t out_elem)
 {
     double b = 0;
-    for (const AugJob& J : L.jobs) {
+    for (const J_& J : jobs) {
         double rd = (double)J.crop_w * J.crop_h * J.cn;
         if (J.mode == RESIZE_LINEAR || J.mode == RESIZE_NEAREST) {
             // a window of the resize target reads only its share of the source
@@ -704,6 +630,130 @@ void timed_launch(aeon_hip_ctx* ctx, int mode, const LaunchPlan& P, const Launch
     if (timed) ctx->timers.push_back(t);
 }
 
+// The next ring slot for a call on `stream`, once the kernels that last used it are done.
+Slot& take_slot(aeon_hip_ctx* ctx, hipStream_t stream, int& index)
+{
+    // calls on another stream than the open ones: close those with an event on their stream
+    if (!ctx->open_slots.empty() && ctx->open_stream != stream) close_slots(ctx);
+    index     = ctx->next;
+    Slot& s   = ctx->slots[index];
+    ctx->next = (ctx->next + 1) % aeon_hip_ctx::kSlots;
+    if (s.pending) {
+        HIP_OK(hipEventSynchronize(ctx->slots[s.cover].done));
+        s.pending = false;
+    }
+    return s;
+}
+
+// The call's launches are enqueued: its slot stays busy until a completion event covers it.
+void release_slot(aeon_hip_ctx* ctx, int index, hipStream_t stream)
+{
+    ctx->open_slots.push_back(index);
+    ctx->open_stream = stream;
+    if ((int)ctx->open_slots.size() >= ctx->done_every) close_slots(ctx);
+    ctx->host_calls++;
+}
+
+LaunchArgs launch_args(aeon_hip_ctx* ctx, const Slot& s, const uint8_t* table, const LaunchPlan& L, int n_jobs,
+                       const aeon_out_desc& o, const float* d_lut, int partial_stride)
+{
+    LaunchArgs a{};
+    a.jobs           = (const AugJob*)(table + L.blob_off);
+    a.lut            = d_lut; // [3][256]: standardized, or (float)x without mean
+    a.hsv_tables     = ctx->d_hsv;
+    a.partials       = s.partials;
+    a.shifts         = s.shifts;
+    a.partial_stride = partial_stride;
+    a.error          = ctx->d_error;
+    if (const char* e = std::getenv("AEON_HIP_TRACE_PTR")) a.trace = (uint32_t*)std::strtoull(e, nullptr, 0);
+    a.rows_per_tile = L.tr;
+    a.max_tiles     = L.max_tiles;
+    a.total_tiles   = L.max_tiles * n_jobs;
+    a.stage_bytes   = L.stage_bytes;
+    a.stage_buffers = L.buffers;
+    a.max_win_w     = L.max_win_w;
+    a.out_dtype     = o.dtype == AEON_DTYPE_F32 ? OUT_F32 : OUT_U8;
+    a.channel_major = o.channel_major;
+    a.bgr_to_rgb    = o.bgr_to_rgb;
+    a.vec_ok        = L.vec_ok && o.channel_major;
+    a.lds_bytes     = L.lds;
+    a.has_hue       = L.has_hue;
+    a.threads       = L.threads;
+    return a;
+}
+
+// Device-planned call (the common case: C2, C5's image, every record transformed straight from
+// its source in one launch group).  The host checks the records and sizes the launch from their
+// geometry; the caller's descriptors + params (128 B per record) go to the slot's pinned table and
+// plan_records -- on the launch stream, ahead of the tile kernel -- reads them over PCIe and
+// writes each record's AugJob with the same plan_direct the host planner uses.  Returns false
+// (nothing done) when some record needs the host planner: rotation, resize_short, contrast's two
+// passes, 2x-area + photometric, the mask gather pass, or records of several launch groups.
+template <typename Phase>
+bool run_direct(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* src_base,
+                const aeon_aug_params* params, const aeon_out_desc& o, void* out_dev, hipStream_t stream,
+                bool is_mask, Phase&& phase)
+{
+    std::vector<JobGeom>& geo = ctx->geoms;
+    geo.resize(n);
+    int  key = -1, max_h = 0;
+    bool vec_ok = !o.fixed_aspect_ratio;
+    for (int i = 0; i < n; i++) {
+        const aeon_img_desc&   d = descs[i];
+        const aeon_aug_params& p = params[i];
+        if (d.elem_bytes != 0 && d.elem_bytes != 1) return false;
+        if (is_mask && d.channels == 1 && o.channels == 1 && p.angle == 0) return false; // mask gather pass
+        if (p.angle != 0 || (!is_mask && p.resize_short_size > 0)) return false;
+        validate_record(d, p, o, is_mask);
+        const int photo = is_mask ? 0 : photo_flags(p);
+        const int mode  = choose_mode(p.crop_w, p.crop_h, p.out_w, p.out_h, is_mask ? AEON_INTERP_NEAREST : p.interp,
+                                      d.channels);
+        if ((photo & PHOTO_CONTRAST) || (photo && mode == RESIZE_AREA2X)) return false;
+        const bool tail = mode == RESIZE_LINEAR && simd_boundary(p.out_w * d.channels) < p.out_w * d.channels;
+        const int  k    = mode * 4 + (tail ? 2 : 0) + (photo ? 1 : 0);
+        if (key < 0) key = k;
+        else if (k != key) return false;
+        if ((((uint64_t)out_dev + (uint64_t)i * o.item_stride) & 15) != 0 || (p.out_w & 3) != 0) vec_ok = false;
+        JobGeom& g = geo[i];
+        g.mode = mode, g.cn = d.channels, g.crop_w = p.crop_w, g.crop_h = p.crop_h;
+        g.win_w = g.dst_w = p.out_w, g.win_h = g.dst_h = p.out_h, g.photo = photo, g.stats_slot = -1;
+        g.scale_x = 1. / ((double)p.out_w / p.crop_w);
+        g.scale_y = 1. / ((double)p.out_h / p.crop_h);
+        max_h     = std::max(max_h, p.out_h);
+    }
+    LaunchPlan P;
+    P.rm     = key >> 2;
+    P.tail   = (key & 2) != 0;
+    P.photo  = (key & 1) != 0;
+    P.vec_ok = vec_ok;
+    P.shape(geo);
+    P.max_tiles = (max_h + P.tr - 1) / P.tr;
+    phase(2);
+    int         slot;
+    Slot&       s     = take_slot(ctx, stream, slot);
+    phase(3);
+    const float* d_lut = resident_lut(ctx, o);
+    ensure_ring(ctx, (size_t)n * sizeof(AugJob), 16, 32);
+    PlanRecord* R = (PlanRecord*)s.host;
+    for (int i = 0; i < n; i++) {
+        std::memcpy(&R[i].desc, &descs[i], sizeof(aeon_img_desc));
+        std::memcpy(&R[i].params, &params[i], sizeof(aeon_aug_params));
+    }
+    phase(4);
+    const PlanArgs pa{(uint64_t)src_base, (uint64_t)out_dev, o.item_stride, out_geom(o), n, is_mask ? 1 : 0, P.tr, 0};
+    HIP_OK(launch_plan_records(s.host_dev, s.dev, pa, stream));
+    phase(5);
+    const bool timed = ctx->timing && (ctx->timing_calls++ % ctx->timing_every) == 0;
+    if (o.fixed_aspect_ratio) // std::fill_n of each item's canvas (etl_image.cpp:263)
+        HIP_OK(hipMemset2DAsync(out_dev, o.item_stride, 0, (size_t)o.canvas_w * o.canvas_h * o.channels, n, stream));
+    timed_launch(ctx, KM_FINAL, P, launch_args(ctx, s, s.dev, P, n, o, d_lut, 1), stream,
+                 launch_bytes(geo, KM_FINAL, o.dtype == AEON_DTYPE_F32 ? 4 : 1), timed);
+    phase(6);
+    release_slot(ctx, slot, stream);
+    phase(7);
+    return true;
+}
+
 int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* src_base,
               const aeon_aug_params* params, const aeon_out_desc* out, void* out_dev, void* stream_,
               bool is_mask)
@@ -746,6 +796,9 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
     };
     HIP_OK(hipSetDevice(ctx->device));
     phase(0);
+    if (ctx->device_plan && ctx->jobs_mode < 0 &&
+        run_direct(ctx, n, descs, src_base, params, o, out_dev, stream, is_mask, phase))
+        return 0;
 
     LaunchPlan             pre_all, pre2_all, pass1_all, main_all;
     std::vector<RotJob>    rot;
@@ -812,15 +865,8 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
     const size_t partial_words = std::max<size_t>(4, pass1_all.jobs.size() * partial_stride * 4);
 
     phase(2);
-    // calls on another stream than the open ones: close those with an event on their stream
-    if (!ctx->open_slots.empty() && ctx->open_stream != stream) close_slots(ctx);
-    const int slot = ctx->next;
-    Slot&     s    = ctx->slots[slot];
-    ctx->next      = (ctx->next + 1) % aeon_hip_ctx::kSlots;
-    if (s.pending) {
-        HIP_OK(hipEventSynchronize(ctx->slots[s.cover].done));
-        s.pending = false;
-    }
+    int   slot;
+    Slot& s = take_slot(ctx, stream, slot);
     phase(3);
     const float* d_lut = resident_lut(ctx, o);
     // job tables, contrast sums and shifts: one capacity for every slot of the ring (a call never
@@ -855,29 +901,7 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
     phase(5);
 
     auto args = [&](const LaunchPlan& L) {
-        LaunchArgs a{};
-        a.jobs          = (const AugJob*)(table + L.blob_off);
-        a.lut           = d_lut; // [3][256]: standardized, or (float)x without mean
-        a.hsv_tables    = ctx->d_hsv;
-        a.partials      = s.partials;
-        a.shifts        = s.shifts;
-        a.partial_stride = partial_stride;
-        a.error         = ctx->d_error;
-        if (const char* e = std::getenv("AEON_HIP_TRACE_PTR")) a.trace = (uint32_t*)std::strtoull(e, nullptr, 0);
-        a.rows_per_tile = L.tr;
-        a.max_tiles     = L.max_tiles;
-        a.total_tiles   = L.max_tiles * (int)L.jobs.size();
-        a.stage_bytes   = L.stage_bytes;
-        a.stage_buffers = L.buffers;
-        a.max_win_w     = L.max_win_w;
-        a.out_dtype     = o.dtype == AEON_DTYPE_F32 ? OUT_F32 : OUT_U8;
-        a.channel_major = o.channel_major;
-        a.bgr_to_rgb    = o.bgr_to_rgb;
-        a.vec_ok        = L.vec_ok && o.channel_major;
-        a.lds_bytes     = L.lds;
-        a.has_hue       = L.has_hue;
-        a.threads       = L.threads;
-        return a;
+        return launch_args(ctx, s, table, L, (int)L.jobs.size(), o, d_lut, partial_stride);
     };
     const size_t oelem = o.dtype == AEON_DTYPE_F32 ? 4 : 1;
     // timing events on one call in timing_every (each event pair costs GPU time between launches)
@@ -895,20 +919,17 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
         HIP_OK(launch_rotate((const RotJob*)(table + rot_off), (int)rot.size(), rot_max_px, stream));
     for (auto* v : {&pre, &pre2})
         for (LaunchPlan& P : *v)
-            if (!P.jobs.empty()) timed_launch(ctx, KM_RAW, P, args(P), stream, launch_bytes(P, KM_RAW, 1), timed);
+            if (!P.jobs.empty()) timed_launch(ctx, KM_RAW, P, args(P), stream, launch_bytes(P.jobs, KM_RAW, 1), timed);
     for (LaunchPlan& P : pass1)
-        if (!P.jobs.empty()) timed_launch(ctx, KM_STATS, P, args(P), stream, launch_bytes(P, KM_STATS, oelem), timed);
+        if (!P.jobs.empty()) timed_launch(ctx, KM_STATS, P, args(P), stream, launch_bytes(P.jobs, KM_STATS, oelem), timed);
     for (LaunchPlan& P : main) {
         if (P.jobs.empty()) continue;
         if (P.has_contrast) HIP_OK(launch_contrast_reduce(args(P), (int)P.jobs.size(), stream));
-        timed_launch(ctx, KM_FINAL, P, args(P), stream, launch_bytes(P, KM_FINAL, oelem), timed);
+        timed_launch(ctx, KM_FINAL, P, args(P), stream, launch_bytes(P.jobs, KM_FINAL, oelem), timed);
     }
     phase(6);
-    ctx->open_slots.push_back(slot);
-    ctx->open_stream = stream;
-    if ((int)ctx->open_slots.size() >= ctx->done_every) close_slots(ctx);
+    release_slot(ctx, slot, stream);
     phase(7);
-    ctx->host_calls++;
     return 0;
 }
 
@@ -989,6 +1010,7 @@ int aeon_hip_ctx_create(int device, aeon_hip_ctx** out)
             ensure_ring(c, 128 * 1024, 64 * 1024, 8 * 1024);
             if (const char* e = std::getenv("AEON_HIP_HOST_PROFILE")) c->host_profile = std::atoi(e) != 0;
             if (const char* e = std::getenv("AEON_HIP_JOBS")) c->jobs_mode = std::min(3, std::max(0, std::atoi(e)));
+            if (const char* e = std::getenv("AEON_HIP_DEVICE_PLAN")) c->device_plan = std::atoi(e) != 0;
             HIP_OK(hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, device));
             if (const char* e = std::getenv("AEON_HIP_WG_PER_CU")) c->wg_per_cu = std::atoi(e);
             if (const char* e = std::getenv("AEON_HIP_DONE_EVERY"))

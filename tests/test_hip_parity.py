@@ -331,6 +331,31 @@ def test_full_batch_c5_all_records(ctx):
     _assert_same(m1, H.oracle_records(masks, params, mout, mask=True), "C5 mask full batch")
 
 
+@pytest.mark.parametrize("aug_name", ["C2", "C3_no_contrast", "C5_image", "nearest_u8"])
+def test_device_planner_matches_host_planner(ctx, monkeypatch, aug_name):
+    """run_direct's device planner (plan_records -> plan_direct on the GPU) against the host planner
+    (AEON_HIP_DEVICE_PLAN=0) and the oracle: same outputs, bit for bit, for every single-pass
+    record shape (bilinear, photometric without contrast, nearest / uint8 HWC)."""
+    aug = {"C2": C.C2_AUG, "C3_no_contrast": dict(C.C3_AUG, contrast=[1.0, 1.0]), "C5_image": C.C5_AUG,
+           "nearest_u8": dict(C.C2_AUG, interpolation_method="NEAREST")}[aug_name]
+    ow, oh = (512, 512) if aug_name == "C5_image" else (224, 224)
+    rng = np.random.default_rng(77)
+    sizes = [(int(rng.integers(200, 700)), int(rng.integers(200, 700))) for _ in range(40)]
+    imgs = [A.synthetic_image(i, w, h, 3) for i, (w, h) in enumerate(sizes)]
+    params = H.draw_params(aug, sizes, ow, oh, seed=8)
+    if aug_name == "nearest_u8":
+        out = A.out_desc(channels=3, channel_major=False, dtype="uint8", item_stride=ow * oh * 3)
+    else:
+        out = A.out_desc(**dict(MEAN_OUT, item_stride=3 * ow * oh * 4))
+    dev = H.hip_records(ctx, imgs, params, out)
+    monkeypatch.setenv("AEON_HIP_DEVICE_PLAN", "0")
+    host_ctx = A.Context(0)
+    host = H.hip_records(host_ctx, imgs, params, out)
+    host_ctx.close()
+    _assert_same(dev, host, aug_name + " device vs host planner")
+    _assert_same(dev, H.oracle_records(imgs, params, out), aug_name)
+
+
 def test_mask_rejects_standardize(ctx):
     """pixel_mask's loader never standardizes (etl_pixel_mask.cpp:94-105): refused either way."""
     m = A.synthetic_image(0, 64, 64, 1)
