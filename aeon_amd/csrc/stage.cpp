@@ -181,7 +181,7 @@ struct LaunchPlan {
         has_hue = hue, has_contrast = contrast;
         for (int pass = 0; pass < 2; pass++) {
             for (int t = tr_cap; t >= 1; t--) {
-                if (t > nph && t % nph) continue;
+                if (buffers == 2 && t > nph && t % nph) continue; // whole row sets (counted vmcnt waits)
                 // staged rows x whole 4-pixel groups, in whole DMA instructions (64 groups = 1 KiB
                 // for BGR, 64 gray pixels = 256 B)
                 long by = 0;
