@@ -114,6 +114,8 @@ def lib():
         L.aeon_unbiased_round.argtypes = [ctypes.c_float, P(ctypes.c_int64)]
         L.aeon_calculate_scale.argtypes = [ctypes.c_int] * 4 + [P(ctypes.c_float)]
         L.aeon_cropbox_max_proportional.argtypes = [ctypes.c_float] * 4 + [P(ctypes.c_float)] * 2
+        L.aeon_jpeg_info.argtypes = [ctypes.c_char_p, ctypes.c_size_t] + [P(ctypes.c_int)] * 3
+        L.aeon_hip_decode_jpeg_batch.argtypes = [vp, ctypes.c_int, P(vp), P(ctypes.c_size_t), P(ImgDesc), vp, vp]
         L.aeon_hip_host_alloc.argtypes = [ctypes.c_size_t, P(vp)]
         L.aeon_hip_host_free.argtypes = [vp]
         L.aeon_decoder_create.argtypes = [ctypes.c_char_p, ctypes.c_int, P(vp)]
@@ -174,6 +176,13 @@ def seed_slots(seed, n):
     out = np.zeros(n, np.uint32)
     _check(lib().aeon_seed_slots(seed, n, out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))))
     return out
+
+
+def jpeg_info(data):
+    """(width, height, components) of a JPEG file (aeon_jpeg_info)."""
+    w, h, n = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    _check(lib().aeon_jpeg_info(bytes(data), len(data), ctypes.byref(w), ctypes.byref(h), ctypes.byref(n)))
+    return w.value, h.value, n.value
 
 
 def unbiased_round(x):
@@ -265,6 +274,17 @@ class Context:
     def depthmap_batch(self, descs, src_ptr, params, out, out_ptr, stream=0):
         """depthmap transform + load (aeon src/etl_depthmap.cpp) for len(descs) records."""
         self._batch(lib().aeon_hip_depthmap_batch, descs, src_ptr, params, out, out_ptr, stream)
+
+    def decode_jpeg_batch(self, files, descs, dst_ptr, stream=0):
+        """image::extractor::extract of JPEG files into device memory (aeon_hip_decode_jpeg_batch):
+        files = list of bytes, descs[i] = where record i goes (HWC, channels 3 = BGR / 1 = gray)."""
+        n = len(files)
+        bufs = [bytes(f) for f in files]
+        ptrs = (ctypes.c_void_p * n)(*[ctypes.cast(ctypes.c_char_p(b), ctypes.c_void_p) for b in bufs])
+        sizes = (ctypes.c_size_t * n)(*[len(b) for b in bufs])
+        d = descs if isinstance(descs, ctypes.Array) else (ImgDesc * n)(*descs)
+        _check(lib().aeon_hip_decode_jpeg_batch(self._h, n, ptrs, sizes, d, ctypes.c_void_p(dst_ptr),
+                                                ctypes.c_void_p(stream or 0)))
 
     def set_timing(self, every=1):
         """Time the launches of one call in `every` (0 = off) with HIP events on their stream."""

@@ -357,7 +357,7 @@ std::shared_ptr<provider_base> provider_factory::create(const Json& config)
 // ---- thread_pool ----------------------------------------------------------------------------------
 thread_pool::thread_pool(int nthreads)
 {
-    for (int i = 0; i < std::max(1, nthreads); i++) m_threads.emplace_back([this] { worker(); });
+    for (int i = 0; i < std::max(1, nthreads); i++) m_threads.emplace_back([this, i] { worker(i); });
 }
 
 thread_pool::~thread_pool()
@@ -370,11 +370,11 @@ thread_pool::~thread_pool()
     for (auto& t : m_threads) t.join();
 }
 
-void thread_pool::worker()
+void thread_pool::worker(int index)
 {
     long seen = 0;
     for (;;) {
-        const std::function<void(int)>* fn;
+        const std::function<void(int, int)>* fn;
         int                            n;
         {
             std::unique_lock<std::mutex> l(m_mu);
@@ -388,7 +388,7 @@ void thread_pool::worker()
             int i = m_next.fetch_add(1);
             if (i >= n) break;
             try {
-                (*fn)(i);
+                (*fn)(i, index);
             } catch (...) {
                 std::lock_guard<std::mutex> l(m_mu);
                 if (!m_error) m_error = std::current_exception();
@@ -402,6 +402,11 @@ void thread_pool::worker()
 }
 
 void thread_pool::run(int n, const std::function<void(int)>& fn)
+{
+    run_indexed(n, [&](int i, int) { fn(i); });
+}
+
+void thread_pool::run_indexed(int n, const std::function<void(int, int)>& fn)
 {
     {
         std::lock_guard<std::mutex> l(m_mu);

@@ -139,14 +139,16 @@ public:
     explicit thread_pool(int nthreads);
     ~thread_pool();
     void run(int n, const std::function<void(int)>& fn);
+    // fn(task, worker): worker in [0, size()) identifies the calling pool thread
+    void run_indexed(int n, const std::function<void(int, int)>& fn);
     int  size() const { return (int)m_threads.size(); }
 
 private:
-    void                           worker();
-    std::vector<std::thread>       m_threads;
-    std::mutex                     m_mu;
-    std::condition_variable        m_cv, m_done_cv;
-    const std::function<void(int)>* m_fn = nullptr;
+    void                                 worker(int index);
+    std::vector<std::thread>             m_threads;
+    std::mutex                           m_mu;
+    std::condition_variable              m_cv, m_done_cv;
+    const std::function<void(int, int)>* m_fn = nullptr;
     int                            m_n = 0, m_active = 0;
     long                           m_generation = 0;
     std::atomic<int>               m_next{0};

@@ -1,0 +1,551 @@
+// jpeg_host.cpp -- host half of the JPEG decode stage (see jpeg.hpp): header parsing, Huffman
+// entropy decoding into the sparse coefficient stream on the decode pool, the per-call device
+// layout, and the extern "C" entries aeon_jpeg_info / aeon_hip_decode_jpeg_batch.
+//
+// Follows libjpeg's baseline / extended-sequential decoder (ITU T.81 F.2: DHT/DQT/DRI/SOF0-1/SOS,
+// interleaved and non-interleaved scans, restart intervals, 0xFF00 stuffing), which is what
+// cv::imdecode runs under aeon's image::extractor::extract (src/etl_image.cpp:83-99).  Progressive,
+// arithmetic-coded, 12-bit and 4-component (CMYK / Adobe RGB) files are refused with
+// AEON_HIP_EUNSUPPORTED.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/aeon_hip.h"
+#include "host.hpp"
+#include "jpeg.hpp"
+
+namespace aeon_hip {
+hipError_t launch_jpeg(const JpegImage* imgs, const JpegChunk* chunks, int n_chunks, const JpegRows* rows, int n_rows,
+                       hipStream_t stream);
+
+namespace {
+
+[[noreturn]] void bad(const std::string& m) { throw jpeg_error(AEON_HIP_EINVAL, "JPEG: " + m); }
+[[noreturn]] void unsupported(const std::string& m) { throw jpeg_error(AEON_HIP_EUNSUPPORTED, "JPEG: " + m); }
+
+const uint8_t kZigzagToNatural[80] = {
+    0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,  12, 19, 26, 33, 40, 48, 41, 34, 27, 20, 13,
+    6,  7,  14, 21, 28, 35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51, 58, 59, 52, 45, 38, 31,
+    39, 46, 53, 60, 61, 54, 47, 55, 62, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63};
+
+// Canonical Huffman table with a 9-bit lookahead (libjpeg's jdhuff.c scheme).
+struct Huffman {
+    bool     set = false;
+    uint16_t look[512]; // (length << 8) | symbol for codes of <= 9 bits, 0 otherwise
+    int32_t  maxcode[18], valptr[17], mincode[17];
+    uint8_t  vals[256];
+
+    void build(const uint8_t* counts, const uint8_t* symbols, int n)
+    {
+        std::memcpy(vals, symbols, n);
+        std::memset(look, 0, sizeof(look));
+        int code = 0, k = 0;
+        for (int l = 1; l <= 16; l++) {
+            valptr[l]  = k;
+            mincode[l] = code;
+            for (int i = 0; i < counts[l - 1]; i++, k++, code++)
+                if (l <= 9)
+                    for (int f = 0; f < (1 << (9 - l)); f++) look[(code << (9 - l)) | f] = (uint16_t)((l << 8) | vals[k]);
+            maxcode[l] = counts[l - 1] ? code - 1 : -1;
+            if (code > (1 << l)) bad("bad Huffman table");
+            code <<= 1;
+        }
+        maxcode[17] = 0x7fffffff;
+        set         = true;
+    }
+};
+
+// Entropy-coded segment reader: 64-bit buffer, 0xFF00 unstuffing; a marker ends the supply (zeros
+// follow, as libjpeg's fill_bit_buffer does), running off the end of the file is an error.
+struct Bits {
+    const uint8_t* p;
+    const uint8_t* end;
+    uint64_t       buf    = 0;
+    int            n      = 0;
+    bool           marker = false;
+
+    void fill()
+    {
+        while (n <= 56) {
+            uint64_t b = 0;
+            if (!marker) {
+                if (p >= end) bad("truncated scan data");
+                b = *p;
+                if (b == 0xFF) {
+                    const int nx = p + 1 < end ? p[1] : 0xD9;
+                    if (nx == 0) p += 2;
+                    else marker = true, b = 0;
+                } else {
+                    p++;
+                }
+            }
+            buf |= b << (56 - n);
+            n += 8;
+        }
+    }
+    uint32_t get(int k) // k in 1..16
+    {
+        if (n < k) fill();
+        const uint32_t v = (uint32_t)(buf >> (64 - k));
+        buf <<= k;
+        n -= k;
+        return v;
+    }
+    int decode(const Huffman& t)
+    {
+        if (n < 16) fill();
+        const uint16_t e = t.look[buf >> 55];
+        if (e) {
+            buf <<= e >> 8;
+            n -= e >> 8;
+            return e & 0xff;
+        }
+        int l = 10;
+        while (l <= 16 && (int32_t)(buf >> (64 - l)) > t.maxcode[l]) l++;
+        if (l > 16) bad("corrupt Huffman code");
+        const int code = (int)(buf >> (64 - l));
+        buf <<= l;
+        n -= l;
+        return t.vals[t.valptr[l] + code - t.mincode[l]];
+    }
+    // RSTn: drop buffered bits, skip to just past the marker
+    void restart()
+    {
+        buf = 0, n = 0, marker = false;
+        while (p + 1 < end && !(p[0] == 0xFF && p[1] >= 0xD0 && p[1] <= 0xD7)) p++;
+        if (p + 1 < end) p += 2;
+    }
+};
+
+inline int extend(int v, int s) { return v < (1 << (s - 1)) ? v - (1 << s) + 1 : v; }
+
+struct Comp {
+    int id = 0, h = 1, v = 1, tq = 0, td = 0, ta = 0;
+    int bw = 0, bh = 0, dw = 0, dh = 0;
+    int pred = 0;
+};
+
+// Header of one file (and, once decoded, where its streams sit in the worker's arena).
+struct Frame {
+    int      W = 0, H = 0, ncomp = 0, hmax = 1, vmax = 1, mcux = 0, mcuy = 0;
+    Comp     c[3];
+    uint16_t q[4][64];
+    bool     qset[4] = {false, false, false, false};
+};
+
+// The worker's growable output: block records then values per image (16-byte aligned pieces).
+struct Arena {
+    std::vector<uint8_t> host; // pageable staging, copied into the set's pinned buffer
+    size_t               used = 0;
+    uint8_t*             reserve(size_t bytes)
+    {
+        used = (used + 15) & ~(size_t)15;
+        if (used + bytes > host.size()) host.resize(std::max(used + bytes, host.size() * 2));
+        uint8_t* r = host.data() + used;
+        used += bytes;
+        return r;
+    }
+};
+
+uint16_t be16(const uint8_t* p) { return (uint16_t)((p[0] << 8) | p[1]); }
+
+// Parse markers up to the frame header (SOF): size, components, sampling.
+void parse_frame(const uint8_t* d, size_t size, Frame& f, const uint8_t** after)
+{
+    const uint8_t* p   = d;
+    const uint8_t* end = d + size;
+    if (size < 4 || p[0] != 0xFF || p[1] != 0xD8) bad("not a JPEG file (no SOI marker)");
+    p += 2;
+    for (;;) {
+        while (p < end && *p != 0xFF) p++; // tolerate fill / garbage between segments
+        while (p < end && *p == 0xFF) p++;
+        if (p >= end) bad("no frame header");
+        const int m = *p++;
+        if (m == 0xD8 || (m >= 0xD0 && m <= 0xD7) || m == 0x01) continue;
+        if (m == 0xD9) bad("no frame header");
+        if (p + 2 > end) bad("truncated marker segment");
+        const int len = be16(p);
+        if (len < 2 || p + len > end) bad("truncated marker segment");
+        const uint8_t* s = p + 2;
+        if (m == 0xC0 || m == 0xC1) {
+            if (len < 8) bad("bad frame header");
+            if (s[0] != 8) unsupported("only 8-bit samples are supported");
+            f.H = be16(s + 1), f.W = be16(s + 3), f.ncomp = s[5];
+            if (f.W <= 0 || f.H <= 0) bad("bad image size");
+            if (f.ncomp != 1 && f.ncomp != 3) unsupported("only 1- and 3-component images are supported");
+            if (len < 8 + 3 * f.ncomp) bad("bad frame header");
+            for (int k = 0; k < f.ncomp; k++) {
+                Comp& c = f.c[k];
+                c.id = s[6 + 3 * k], c.h = s[7 + 3 * k] >> 4, c.v = s[7 + 3 * k] & 15, c.tq = s[8 + 3 * k];
+                if (c.h < 1 || c.h > 4 || c.v < 1 || c.v > 4 || c.tq > 3) bad("bad component parameters");
+                f.hmax = std::max(f.hmax, c.h), f.vmax = std::max(f.vmax, c.v);
+            }
+            for (int k = 0; k < f.ncomp; k++)
+                if (f.hmax % f.c[k].h || f.vmax % f.c[k].v) unsupported("fractional sampling factors");
+            f.mcux = (f.W + 8 * f.hmax - 1) / (8 * f.hmax);
+            f.mcuy = (f.H + 8 * f.vmax - 1) / (8 * f.vmax);
+            for (int k = 0; k < f.ncomp; k++) {
+                Comp& c = f.c[k];
+                c.dw = (f.W * c.h + f.hmax - 1) / f.hmax;
+                c.dh = (f.H * c.v + f.vmax - 1) / f.vmax;
+                c.bw = f.mcux * c.h, c.bh = f.mcuy * c.v;
+            }
+            *after = p + len;
+            return;
+        }
+        if (m >= 0xC2 && m <= 0xCF && m != 0xC4 && m != 0xC8 && m != 0xCC)
+            unsupported("only baseline / extended-sequential Huffman JPEGs are supported (no progressive, "
+                        "lossless or arithmetic coding)");
+        p += len;
+    }
+}
+
+// Decode one file: the frame's block records (per component, bh x bw, in the arena) and values.
+// Returns the byte offsets in `a` of each component's records and of the values.
+void decode_file(const uint8_t* d, size_t size, Frame& f, Arena& a, size_t blk_off[3], size_t* val_off, bool luma_only)
+{
+    const uint8_t* p = nullptr;
+    parse_frame(d, size, f, &p);
+    const uint8_t* end = d + size;
+    // re-walk the tables defined before the frame (DQT / DHT / DRI may precede SOF)
+    Huffman dc[4], ac[4];
+    int     restart = 0;
+    bool    adobe_rgb = false;
+    size_t  nblocks   = 0;
+    for (int k = 0; k < f.ncomp; k++) nblocks += (size_t)f.c[k].bw * f.c[k].bh;
+    // block records (zeroed: blocks a non-interleaved scan never codes stay empty), then values
+    for (int k = 0; k < f.ncomp; k++) {
+        uint8_t* b = a.reserve((size_t)f.c[k].bw * f.c[k].bh * sizeof(JpegBlock));
+        std::memset(b, 0, (size_t)f.c[k].bw * f.c[k].bh * sizeof(JpegBlock));
+        blk_off[k] = (size_t)(b - a.host.data());
+    }
+    // values: at most 64 per block
+    uint8_t* vbase = a.reserve(nblocks * 64 * sizeof(int16_t));
+    *val_off       = (size_t)(vbase - a.host.data());
+    uint32_t nvals = 0;
+    auto table_segment = [&](int m, const uint8_t* s, int len) {
+        const uint8_t* e = s + len - 2;
+        if (m == 0xC4) {
+            while (s < e) {
+                const int tc = s[0] >> 4, th = s[0] & 15;
+                if (tc > 1 || th > 3 || s + 17 > e) bad("bad Huffman table segment");
+                int tot = 0;
+                for (int i = 0; i < 16; i++) tot += s[1 + i];
+                if (tot > 256 || s + 17 + tot > e) bad("bad Huffman table segment");
+                (tc ? ac[th] : dc[th]).build(s + 1, s + 17, tot);
+                s += 17 + tot;
+            }
+        } else if (m == 0xDB) {
+            while (s < e) {
+                const int pq = s[0] >> 4, tq = s[0] & 15;
+                if (tq > 3 || pq > 1 || s + 1 + 64 * (pq + 1) > e) bad("bad quantisation table segment");
+                for (int i = 0; i < 64; i++)
+                    f.q[tq][kZigzagToNatural[i]] = pq ? be16(s + 1 + 2 * i) : s[1 + i];
+                f.qset[tq] = true;
+                s += 1 + 64 * (pq + 1);
+            }
+        } else if (m == 0xDD) {
+            if (len < 4) bad("bad restart interval segment");
+            restart = be16(s);
+        } else if (m == 0xEE) {
+            if (len >= 14 && std::memcmp(s, "Adobe", 5) == 0 && s[11] == 0) adobe_rgb = true;
+        }
+    };
+    {
+        // tables before SOF
+        const uint8_t* q = d + 2;
+        while (q < p) {
+            while (q < p && *q != 0xFF) q++;
+            while (q < p && *q == 0xFF) q++;
+            if (q >= p) break;
+            const int m = *q++;
+            if (m == 0xD8 || (m >= 0xD0 && m <= 0xD7) || m == 0x01) continue;
+            const int len = be16(q);
+            if (m == 0xC0 || m == 0xC1) break;
+            table_segment(m, q + 2, len);
+            q += len;
+        }
+    }
+    bool any_scan = false;
+    for (;;) {
+        while (p < end && *p != 0xFF) p++;
+        while (p < end && *p == 0xFF) p++;
+        if (p >= end) {
+            if (!any_scan) bad("no scan data");
+            break; // missing EOI: tolerated, as libjpeg does
+        }
+        const int m = *p++;
+        if (m == 0xD9) break;
+        if (m == 0xD8 || (m >= 0xD0 && m <= 0xD7) || m == 0x01) continue;
+        if (p + 2 > end) bad("truncated marker segment");
+        const int len = be16(p);
+        if (len < 2 || p + len > end) bad("truncated marker segment");
+        if (m != 0xDA) {
+            if ((m >= 0xC0 && m <= 0xCF && m != 0xC4 && m != 0xC8 && m != 0xCC)) bad("second frame header");
+            table_segment(m, p + 2, len);
+            p += len;
+            continue;
+        }
+        // SOS
+        const uint8_t* s  = p + 2;
+        const int      ns = s[0];
+        if (ns < 1 || ns > f.ncomp || len != 6 + 2 * ns) bad("bad scan header");
+        int sc[3];
+        for (int i = 0; i < ns; i++) {
+            const int cid = s[1 + 2 * i], t = s[2 + 2 * i];
+            int       k   = 0;
+            while (k < f.ncomp && f.c[k].id != cid) k++;
+            if (k == f.ncomp) bad("scan names an unknown component");
+            f.c[k].td = t >> 4, f.c[k].ta = t & 15;
+            if (f.c[k].td > 3 || f.c[k].ta > 3 || !dc[f.c[k].td].set || !ac[f.c[k].ta].set)
+                bad("scan uses an undefined Huffman table");
+            if (!f.qset[f.c[k].tq]) bad("component uses an undefined quantisation table");
+            sc[i] = k;
+        }
+        if (s[1 + 2 * ns] != 0 || s[2 + 2 * ns] != 63 || s[3 + 2 * ns] != 0)
+            unsupported("progressive scan parameters in a sequential file");
+        p += len;
+        any_scan = true;
+        Bits br{p, end};
+        for (int k = 0; k < f.ncomp; k++) f.c[k].pred = 0;
+        int16_t*  vals = (int16_t*)(a.host.data() + *val_off); // (no reallocation below: reserved)
+        auto      block = [&](Comp& c, JpegBlock* recs, int bx, int by) {
+            JpegBlock& R = recs[(size_t)by * c.bw + bx];
+            uint64_t   mask = 0;
+            const uint32_t first = nvals;
+            int        sdc  = br.decode(dc[c.td]);
+            if (sdc > 15) bad("corrupt DC coefficient");
+            c.pred += sdc ? extend((int)br.get(sdc), sdc) : 0;
+            const int16_t dcv = (int16_t)c.pred;
+            if (dcv) mask |= 1, vals[nvals++] = dcv;
+            for (int k = 1; k < 64;) {
+                const int rs = br.decode(ac[c.ta]), r = rs >> 4, sz = rs & 15;
+                if (sz) {
+                    k += r;
+                    const int16_t v  = (int16_t)extend((int)br.get(sz), sz);
+                    const int     kk = std::min(k, 63); // libjpeg's natural-order table clamps overruns
+                    if (mask >> kk & 1) vals[nvals - 1] = v; // (only kk = 63 can repeat: the last value)
+                    else {
+                        mask |= 1ull << kk;
+                        vals[nvals++] = v;
+                    }
+                    k++;
+                } else if (r == 15) {
+                    k += 16;
+                } else {
+                    break;
+                }
+            }
+            // a block coded twice (corrupt / duplicate scans) keeps the later values
+            R.mask    = mask;
+            R.val_off = first;
+        };
+        int done = 0;
+        if (ns == 1) {
+            Comp&      c    = f.c[sc[0]];
+            JpegBlock* recs = (JpegBlock*)(a.host.data() + blk_off[sc[0]]);
+            const int  nx = (c.dw + 7) / 8, ny = (c.dh + 7) / 8;
+            for (int by = 0; by < ny; by++)
+                for (int bx = 0; bx < nx; bx++) {
+                    if (restart && done && done % restart == 0) br.restart(), c.pred = 0;
+                    block(c, recs, bx, by);
+                    done++;
+                }
+        } else {
+            for (int my = 0; my < f.mcuy; my++)
+                for (int mx = 0; mx < f.mcux; mx++) {
+                    if (restart && done && done % restart == 0) {
+                        br.restart();
+                        for (int k = 0; k < f.ncomp; k++) f.c[k].pred = 0;
+                    }
+                    for (int i = 0; i < ns; i++) {
+                        Comp&      c    = f.c[sc[i]];
+                        JpegBlock* recs = (JpegBlock*)(a.host.data() + blk_off[sc[i]]);
+                        for (int y = 0; y < c.v; y++)
+                            for (int x = 0; x < c.h; x++) block(c, recs, mx * c.h + x, my * c.v + y);
+                    }
+                    done++;
+                }
+        }
+        if (nvals > nblocks * 64) bad("coefficient overflow");
+        // continue after the scan's data: the next marker that is not RSTn
+        p = br.p;
+        while (p + 1 < end && !(p[0] == 0xFF && p[1] != 0 && !(p[1] >= 0xD0 && p[1] <= 0xD7))) p++;
+    }
+    if (adobe_rgb && f.ncomp == 3) unsupported("RGB (Adobe transform 0) JPEGs");
+    (void)luma_only;
+    // give back the unused tail of the value reservation
+    a.used = *val_off + (size_t)nvals * sizeof(int16_t);
+}
+
+} // namespace
+
+// Per-context JPEG state: the decode pool, worker arenas, a two-deep ring of pinned staging +
+// device buffers (a call reuses a set once the copies and kernels of the call before last are done).
+struct JpegState {
+    std::unique_ptr<thread_pool> pool;
+    std::vector<Arena>           arenas;
+    struct Set {
+        hipEvent_t done    = nullptr;
+        bool       pending = false;
+        uint8_t*   pinned  = nullptr;
+        size_t     pinned_cap = 0;
+        uint8_t*   dev     = nullptr;
+        size_t     dev_cap = 0;
+        uint8_t*   planes  = nullptr;
+        size_t     planes_cap = 0;
+    } sets[2];
+    int        next = 0;
+    std::mutex mu;
+};
+
+namespace {
+
+void grow_buf(uint8_t*& p, size_t& cap, size_t need, bool pinned)
+{
+    if (need <= cap) return;
+    const size_t n = std::max(need, cap * 2);
+    if (p) (void)(pinned ? hipHostFree(p) : hipFree(p));
+    p = nullptr, cap = 0;
+    hipError_t e = pinned ? hipHostMalloc((void**)&p, n, hipHostMallocDefault) : hipMalloc((void**)&p, n);
+    if (e != hipSuccess) throw jpeg_error(AEON_HIP_ERUNTIME, std::string("JPEG staging allocation: ") + hipGetErrorString(e));
+    cap = n;
+}
+
+void hip_ok(hipError_t e, const char* what)
+{
+    if (e != hipSuccess) throw jpeg_error(AEON_HIP_ERUNTIME, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+} // namespace
+
+JpegState* jpeg_state_create()
+{
+    auto* s = new JpegState();
+    int   threads = aeon_thread_count("");
+    if (const char* e = std::getenv("AEON_HIP_JPEG_THREADS")) threads = std::max(1, std::atoi(e));
+    s->pool.reset(new thread_pool(threads));
+    s->arenas.resize(s->pool->size());
+    return s;
+}
+
+void jpeg_state_destroy(JpegState* s)
+{
+    if (!s) return;
+    for (auto& st : s->sets) {
+        if (st.pending) (void)hipEventSynchronize(st.done);
+        if (st.done) (void)hipEventDestroy(st.done);
+        if (st.pinned) (void)hipHostFree(st.pinned);
+        if (st.dev) (void)hipFree(st.dev);
+        if (st.planes) (void)hipFree(st.planes);
+    }
+    delete s;
+}
+
+// The decode call (aeon_hip_decode_jpeg_batch): entropy-decode every file on the pool, stage the
+// coefficient streams + tables in one pinned buffer, one H2D, IDCT and colour kernels on `stream`.
+void jpeg_decode_batch(JpegState* S, int n, const void* const* data, const size_t* sizes, const aeon_img_desc* descs,
+                       void* dst_base, hipStream_t stream)
+{
+    std::lock_guard<std::mutex> lock(S->mu);
+    for (auto& a : S->arenas) a.used = 0;
+    std::vector<Frame>  frames(n);
+    std::vector<int>    owner(n);
+    std::vector<size_t> blk(3 * (size_t)n), val(n);
+    S->pool->run_indexed(n, [&](int i, int w) {
+        try {
+            if (!data[i] || !sizes[i]) bad("empty file");
+            const aeon_img_desc& d = descs[i];
+            if (d.channels != 1 && d.channels != 3) bad("decoded channels must be 1 or 3");
+            decode_file((const uint8_t*)data[i], sizes[i], frames[i], S->arenas[w], &blk[3 * (size_t)i], &val[i],
+                        d.channels == 1);
+            owner[i] = w;
+            if (frames[i].W != d.width || frames[i].H != d.height)
+                bad("decoded size " + std::to_string(frames[i].W) + "x" + std::to_string(frames[i].H) +
+                    " does not match the record descriptor " + std::to_string(d.width) + "x" + std::to_string(d.height));
+            if (d.stride < d.width * d.channels) bad("record descriptor stride too small");
+        } catch (const jpeg_error& e) {
+            throw jpeg_error(e.code, std::string(e.what()) + " (record " + std::to_string(i) + ")");
+        }
+    });
+    // device layout of the call: [images][chunks][rows][arena 0][arena 1]...
+    std::vector<JpegChunk> chunks;
+    std::vector<JpegRows>  rows;
+    size_t                 plane_bytes = 0;
+    std::vector<size_t>    plane_off(3 * (size_t)n, 0);
+    for (int i = 0; i < n; i++) {
+        const Frame& f  = frames[i];
+        const int    nc = descs[i].channels == 1 ? 1 : f.ncomp; // grayscale output needs Y only
+        for (int k = 0; k < nc; k++) {
+            plane_off[3 * (size_t)i + k] = plane_bytes;
+            plane_bytes += ((size_t)f.c[k].bw * 8 * f.c[k].bh * 8 + 255) & ~(size_t)255;
+            const int nb = f.c[k].bw * f.c[k].bh;
+            for (int b = 0; b < nb; b += kJpegIdctLanes) chunks.push_back({i, k, b, std::min(kJpegIdctLanes, nb - b)});
+        }
+        for (int y = 0; y < f.H; y += kJpegRowsPerWg) rows.push_back({i, y, std::min(kJpegRowsPerWg, f.H - y), 0});
+    }
+    const size_t img_bytes = (size_t)n * sizeof(JpegImage);
+    const size_t chk_off   = img_bytes;
+    const size_t row_off   = chk_off + ((chunks.size() * sizeof(JpegChunk) + 255) & ~(size_t)255);
+    size_t       total     = row_off + ((rows.size() * sizeof(JpegRows) + 255) & ~(size_t)255);
+    std::vector<size_t> arena_off(S->arenas.size());
+    for (size_t w = 0; w < S->arenas.size(); w++) {
+        arena_off[w] = total;
+        total += (S->arenas[w].used + 255) & ~(size_t)255;
+    }
+    JpegState::Set& st = S->sets[S->next];
+    S->next ^= 1;
+    if (!st.done) hip_ok(hipEventCreateWithFlags(&st.done, hipEventDisableTiming), "hipEventCreate");
+    if (st.pending) hip_ok(hipEventSynchronize(st.done), "hipEventSynchronize");
+    st.pending = false;
+    grow_buf(st.pinned, st.pinned_cap, total, true);
+    grow_buf(st.dev, st.dev_cap, total, false);
+    grow_buf(st.planes, st.planes_cap, std::max<size_t>(plane_bytes, 256), false);
+    const uint64_t dev = (uint64_t)st.dev;
+    JpegImage*     imgs = (JpegImage*)st.pinned;
+    for (int i = 0; i < n; i++) {
+        const Frame& f = frames[i];
+        JpegImage&   J = imgs[i];
+        std::memset(&J, 0, sizeof(J));
+        const uint64_t base = dev + arena_off[owner[i]];
+        for (int k = 0; k < f.ncomp; k++) {
+            J.blocks[k] = base + blk[3 * (size_t)i + k];
+            J.planes[k] = (uint64_t)st.planes + plane_off[3 * (size_t)i + k];
+            J.bw[k] = f.c[k].bw, J.bh[k] = f.c[k].bh, J.dw[k] = f.c[k].dw, J.dh[k] = f.c[k].dh;
+            J.hs[k] = f.c[k].h, J.vs[k] = f.c[k].v;
+            std::memcpy(J.q[k], f.q[f.c[k].tq], sizeof(J.q[k]));
+        }
+        J.values     = base + val[i];
+        J.out        = (uint64_t)dst_base + descs[i].offset;
+        J.W          = f.W, J.H = f.H, J.ncomp = f.ncomp, J.out_cn = descs[i].channels, J.out_stride = descs[i].stride;
+        J.hmax       = f.hmax, J.vmax = f.vmax;
+    }
+    if (!chunks.empty()) std::memcpy(st.pinned + chk_off, chunks.data(), chunks.size() * sizeof(JpegChunk));
+    if (!rows.empty()) std::memcpy(st.pinned + row_off, rows.data(), rows.size() * sizeof(JpegRows));
+    S->pool->run((int)S->arenas.size(), [&](int w) {
+        if (S->arenas[w].used) std::memcpy(st.pinned + arena_off[w], S->arenas[w].host.data(), S->arenas[w].used);
+    });
+    hip_ok(hipMemcpyAsync(st.dev, st.pinned, total, hipMemcpyHostToDevice, stream), "hipMemcpyAsync");
+    hip_ok(launch_jpeg((const JpegImage*)st.dev, (const JpegChunk*)(st.dev + chk_off), (int)chunks.size(),
+                       (const JpegRows*)(st.dev + row_off), (int)rows.size(), stream),
+           "JPEG kernels");
+    hip_ok(hipEventRecord(st.done, stream), "hipEventRecord");
+    st.pending = true;
+}
+
+// aeon_jpeg_info's body.
+void jpeg_info(const void* data, size_t size, int* w, int* h, int* ncomp)
+{
+    Frame          f;
+    const uint8_t* after = nullptr;
+    parse_frame((const uint8_t*)data, size, f, &after);
+    *w = f.W, *h = f.H, *ncomp = f.ncomp;
+}
+
+} // namespace aeon_hip

@@ -17,6 +17,7 @@
 
 #include "../../include/aeon_hip.h"
 #include "aug_job.hpp"
+#include "jpeg.hpp"
 #include "mask16.hpp"
 #include "json.hpp"
 #include "param_factory.hpp"
@@ -35,6 +36,9 @@ hipError_t launch_nearest(const Mask16Job* jobs, int n_jobs, int max_h, int max_
                           hipEvent_t start, hipEvent_t stop);
 hipError_t launch_upload_table(const void* host_dev, void* dst, size_t bytes, hipStream_t stream);
 hipError_t launch_plan_records(const void* host_records, void* jobs, const PlanArgs& a, hipStream_t stream);
+void       jpeg_decode_batch(JpegState* S, int n, const void* const* data, const size_t* sizes,
+                             const aeon_img_desc* descs, void* dst_base, hipStream_t stream);
+void       jpeg_info(const void* data, size_t size, int* w, int* h, int* ncomp);
 } // namespace aeon_hip
 
 using namespace aeon_hip;
@@ -437,6 +441,7 @@ struct aeon_hip_ctx {
     // upload the caller's descriptors + params and let plan_records build the jobs on the GPU
     bool                 device_plan = true; // AEON_HIP_DEVICE_PLAN=0: always plan on the host
     std::vector<JobGeom> geoms;              // reused per call
+    JpegState*           jpeg = nullptr;     // JPEG decode stage (pool, staging ring), on first use
     std::vector<int> open_slots; // used since the last completion event, on open_stream
     hipStream_t      open_stream = nullptr;
     // job tables go up on their own stream, so a call's H2D overlaps the previous call's kernels
@@ -952,6 +957,9 @@ int guarded(F&& f)
     } catch (const aeon_error& e) {
         g_err = e.what();
         return e.code;
+    } catch (const jpeg_error& e) {
+        g_err = e.what();
+        return e.code;
     } catch (const std::invalid_argument& e) {
         g_err = e.what();
         return AEON_HIP_EINVAL;
@@ -1046,6 +1054,7 @@ int aeon_hip_ctx_destroy(aeon_hip_ctx* c)
             std::fprintf(stderr, "; mean total %.1f us\n", total / 1e3);
         }
         (void)hipSetDevice(c->device);
+        jpeg_state_destroy(c->jpeg);
         if (!c->open_slots.empty()) (void)hipStreamSynchronize(c->open_stream);
         for (Slot& s : c->slots)
             if (s.pending) (void)hipEventSynchronize(c->slots[s.cover].done);
@@ -1205,6 +1214,28 @@ int aeon_seed_slots(uint32_t seed, int n, uint32_t* states)
             uint32_t s = g() % 2147483647u;
             states[i]  = s == 0 ? 1 : s;
         }
+        return 0;
+    });
+}
+
+int aeon_jpeg_info(const void* data, size_t size, int* width, int* height, int* components)
+{
+    return guarded([&] {
+        if (!data || !width || !height || !components) fail(AEON_HIP_EINVAL, "null argument");
+        jpeg_info(data, size, width, height, components);
+        return 0;
+    });
+}
+
+int aeon_hip_decode_jpeg_batch(aeon_hip_ctx* ctx, int n, const void* const* data, const size_t* sizes,
+                               const aeon_img_desc* descs, void* dst_base, void* stream)
+{
+    return guarded([&] {
+        if (!ctx || n < 0 || (n > 0 && (!data || !sizes || !descs || !dst_base))) fail(AEON_HIP_EINVAL, "null argument");
+        if (n == 0) return 0;
+        HIP_OK(hipSetDevice(ctx->device));
+        if (!ctx->jpeg) ctx->jpeg = jpeg_state_create();
+        jpeg_decode_batch(ctx->jpeg, n, data, sizes, descs, dst_base, (hipStream_t)stream);
         return 0;
     });
 }

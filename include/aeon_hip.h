@@ -128,6 +128,20 @@ int aeon_hip_depthmap_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs
 int aeon_hip_transpose_batch(aeon_hip_ctx* ctx, const void* src_dev, void* dst_dev, int64_t rows,
                              int64_t cols, int element_size, void* stream);
 
+/* ---- decode (image::extractor::extract, src/etl_image.cpp:83-99) ---------------------------- */
+/* JPEG frame header: width, height, component count (1 or 3).  Host only, no context needed. */
+int aeon_jpeg_info(const void* data, size_t size, int* width, int* height, int* components);
+/* cv::imdecode(CV_LOAD_IMAGE_COLOR / GRAYSCALE) of n JPEG files (baseline / extended sequential
+ * Huffman, 8-bit, 1 or 3 components) as libjpeg decodes them (ISLOW IDCT, fancy upsampling),
+ * into device memory: record i as HWC uint8 (BGR if descs[i].channels == 3, the Y component if 1)
+ * at dst_base + descs[i].offset with descs[i].stride bytes per row; descs[i].width/height must be
+ * the file's (aeon_jpeg_info).  Huffman decoding runs on the context's host pool; the sparse
+ * coefficients go up in one H2D and the IDCT / upsampling / colour conversion run as kernels on
+ * `stream`.  The files may be released when the call returns; dst must stay valid until the stream
+ * reaches the work.  Progressive / arithmetic / 12-bit / CMYK files: AEON_HIP_EUNSUPPORTED. */
+int aeon_hip_decode_jpeg_batch(aeon_hip_ctx* ctx, int n, const void* const* data, const size_t* sizes,
+                               const aeon_img_desc* descs, void* dst_base, void* stream);
+
 /* Wait for `stream` and check the device error word of ctx. */
 int aeon_hip_synchronize(aeon_hip_ctx* ctx, void* stream);
 

@@ -112,6 +112,9 @@ def lib():
         L.orc_calculate_scale.restype = ctypes.c_float
         L.orc_calculate_scale.argtypes = [ctypes.c_int] * 4
         L.orc_cropbox_max_proportional.argtypes = [ctypes.c_float] * 4 + [P(ctypes.c_float)] * 2
+        L.orc_jpeg_info.argtypes = [ctypes.c_char_p, ctypes.c_size_t] + [P(ctypes.c_int)] * 3
+        L.orc_jpeg_decode.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p]
+        L.orc_jpeg_last_error.restype = ctypes.c_char_p
         L.orc_last_error.restype = ctypes.c_char_p
         _lib = L
     return _lib
@@ -184,6 +187,23 @@ def cropbox_max_proportional(in_w, in_h, out_w, out_h):
     rw, rh = ctypes.c_float(), ctypes.c_float()
     lib().orc_cropbox_max_proportional(in_w, in_h, out_w, out_h, ctypes.byref(rw), ctypes.byref(rh))
     return rw.value, rh.value
+
+
+def jpeg_info(data):
+    """(width, height, components) of a JPEG file's frame."""
+    w, h, n = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    if lib().orc_jpeg_info(bytes(data), len(data), ctypes.byref(w), ctypes.byref(h), ctypes.byref(n)) != 0:
+        raise RuntimeError("oracle: " + lib().orc_jpeg_last_error().decode())
+    return w.value, h.value, n.value
+
+
+def jpeg_decode(data, channels=3):
+    """cv::imdecode of a JPEG as aeon's extractor calls it: HWC BGR (channels 3) or gray (1)."""
+    w, h, _ = jpeg_info(data)
+    out = np.zeros((h, w, channels) if channels == 3 else (h, w), np.uint8)
+    if lib().orc_jpeg_decode(bytes(data), len(data), channels, out.ctypes.data) != 0:
+        raise RuntimeError("oracle: " + lib().orc_jpeg_last_error().decode())
+    return out
 
 
 def transform_image(src, p):

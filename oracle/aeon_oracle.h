@@ -116,6 +116,14 @@ double orc_batch_image_mask(int n, const uint8_t* const* srcs, const uint8_t* co
                             void* out, size_t item_bytes, const orc_load_config* mlc, void* mout,
                             size_t mitem_bytes, int threads);
 
+/* image::extractor::extract's JPEG decode (cv::imdecode -> libjpeg: baseline/extended Huffman,
+ * ISLOW IDCT, fancy upsampling, YCbCr->RGB, emitted as BGR) -- jpeg_oracle.cpp.
+ * orc_jpeg_info: frame size and component count.  orc_jpeg_decode: HWC uint8, channels 3 = BGR,
+ * 1 = grayscale (Y).  Both return 0, or -1 with orc_jpeg_last_error(). */
+int         orc_jpeg_info(const uint8_t* data, size_t size, int* w, int* h, int* ncomp);
+int         orc_jpeg_decode(const uint8_t* data, size_t size, int channels, uint8_t* out);
+const char* orc_jpeg_last_error(void);
+
 const char* orc_last_error(void);
 
 #ifdef __cplusplus
