@@ -70,6 +70,12 @@ class RecordElem(ctypes.Structure):
                 ("channels", ctypes.c_int32), ("stride", ctypes.c_int32)]
 
 
+class EncodedElem(ctypes.Structure):
+    """aeon_encoded_elem: an encoded JPEG file (width 0) or decoded HWC uint8 pixels."""
+    _fields_ = [("data", ctypes.c_void_p), ("size", ctypes.c_size_t), ("width", ctypes.c_int32),
+                ("height", ctypes.c_int32), ("channels", ctypes.c_int32), ("stride", ctypes.c_int32)]
+
+
 class AeonHipError(RuntimeError):
     def __init__(self, code, msg):
         super().__init__(f"aeon_hip error {code}: {msg}")
@@ -125,6 +131,9 @@ def lib():
                                                P(ctypes.c_int64), P(ctypes.c_int), P(ctypes.c_size_t),
                                                P(ctypes.c_int)]
         L.aeon_decoder_decode.argtypes = [vp, ctypes.c_int, P(RecordElem), P(vp), ctypes.c_int, vp]
+        L.aeon_decoder_decode_encoded.argtypes = [vp, ctypes.c_int, P(EncodedElem), P(vp), ctypes.c_int, vp]
+        L.aeon_decoder_submit.argtypes = [vp, ctypes.c_int, P(EncodedElem), P(vp), ctypes.c_int]
+        L.aeon_decoder_wait.argtypes = [vp]
         L.aeon_decoder_last_error.restype = ctypes.c_char_p
         L.aeon_manifest_node_slice.argtypes = [ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                                P(ctypes.c_int64), P(ctypes.c_int64)]
@@ -375,11 +384,37 @@ class Decoder:
         except Exception:
             pass
 
+    def _encoded(self, records):
+        """aeon_encoded_elem array for records whose elements are JPEG bytes or HWC uint8 arrays."""
+        n, ne = len(records), len(self.outputs)
+        keep = []
+        elems = (EncodedElem * (n * ne))()
+        for i, rec in enumerate(records):
+            for k in range(ne):
+                x = rec[k]
+                if isinstance(x, (bytes, bytearray, memoryview)):
+                    b = bytes(x)
+                    keep.append(b)
+                    elems[i * ne + k] = EncodedElem(ctypes.cast(ctypes.c_char_p(b), ctypes.c_void_p), len(b), 0, 0, 0, 0)
+                else:
+                    a = np.ascontiguousarray(x, dtype=np.uint8)
+                    keep.append(a)
+                    h, w = a.shape[:2]
+                    cn = 1 if a.ndim == 2 else a.shape[2]
+                    elems[i * ne + k] = EncodedElem(a.ctypes.data, a.nbytes, w, h, cn, w * cn)
+        return elems, keep
+
     def decode(self, records, stream=0):
-        """records: list of tuples of HWC uint8 arrays (one per ETL element).  Returns one numpy
-        array per output buffer, shape (n,) + item shape."""
+        """records: list of tuples, one element per ETL provider: HWC uint8 arrays or encoded JPEG
+        bytes.  Returns one numpy array per output buffer, shape (n,) + item shape."""
         n = len(records)
         ne = len(self.outputs)
+        outs = [np.zeros((n,) + o["shape"], o["dtype"]) for o in self.outputs]
+        ptrs = (ctypes.c_void_p * ne)(*[o.ctypes.data for o in outs])
+        if any(isinstance(x, (bytes, bytearray, memoryview)) for rec in records for x in rec):
+            elems, keep = self._encoded(records)
+            _check_host(lib().aeon_decoder_decode_encoded(self._h, n, elems, ptrs, 0, ctypes.c_void_p(stream or 0)))
+            return outs
         keep = []
         elems = (RecordElem * (n * ne))()
         for i, rec in enumerate(records):
@@ -389,10 +424,19 @@ class Decoder:
                 h, w = a.shape[:2]
                 cn = 1 if a.ndim == 2 else a.shape[2]
                 elems[i * ne + k] = RecordElem(a.ctypes.data, w, h, cn, w * cn)
-        outs = [np.zeros((n,) + o["shape"], o["dtype"]) for o in self.outputs]
-        ptrs = (ctypes.c_void_p * ne)(*[o.ctypes.data for o in outs])
         _check_host(lib().aeon_decoder_decode(self._h, n, elems, ptrs, 0, ctypes.c_void_p(stream or 0)))
         return outs
+
+    def submit(self, records, output_ptrs, on_device=False):
+        """Double-buffered window (aeon_decoder_submit): output_ptrs[k] = address of n items of
+        output k (pinned host memory, or device memory with on_device); complete after wait()."""
+        n, ne = len(records), len(self.outputs)
+        elems, keep = self._encoded(records)
+        ptrs = (ctypes.c_void_p * ne)(*output_ptrs)
+        _check_host(lib().aeon_decoder_submit(self._h, n, elems, ptrs, int(on_device)))
+
+    def wait(self):
+        _check_host(lib().aeon_decoder_wait(self._h))
 
 
 def manifest_node_slice(record_count, batch_size, node_id, node_count):

@@ -315,6 +315,7 @@ void provider_base::stage(int idx, const decoded_element* elems, decode_window& 
 {
     for (size_t k = 0; k < m_providers.size(); k++) {
         const decoded_element& e = elems[k];
+        if (e.encoded) continue; // decoded on the device, straight into the source arena
         const size_t row = (size_t)e.width * e.channels;
         uint8_t*     dst = w.arena + w.offset[k][idx];
         if ((size_t)e.stride == row) {
@@ -479,22 +480,24 @@ batch_decoder::batch_decoder(const Json& config, int device) : m_device(device)
     m_deterministic      = dseed != 0;
     if (m_deterministic) m_seed_gen.seed(dseed); // slot engines: see slot_engines()
     // the HIP context is created on the first window (configs validate without a GPU)
-    m_dev_out.assign(m_provider->providers().size(), nullptr);
-    m_dev_out_cap.assign(m_provider->providers().size(), 0);
-    m_dev_tmp.assign(m_provider->providers().size(), nullptr);
-    m_dev_tmp_cap.assign(m_provider->providers().size(), 0);
 }
 
 batch_decoder::~batch_decoder()
 {
     if (!m_ctx) return; // no window ran: nothing was allocated on the device
-    aeon_hip_ctx_destroy(m_ctx);
     (void)hipSetDevice(m_device);
-    if (m_pinned) (void)hipHostFree(m_pinned);
-    if (m_dev_src) (void)hipFree(m_dev_src);
-    for (auto* v : {&m_dev_out, &m_dev_tmp})
-        for (auto* p : *v)
-            if (p) (void)hipFree(p);
+    for (auto& ws : m_slots)
+        if (ws.pending) (void)hipEventSynchronize(ws.done);
+    aeon_hip_ctx_destroy(m_ctx);
+    for (auto& ws : m_slots) {
+        if (ws.done) (void)hipEventDestroy(ws.done);
+        if (ws.stream) (void)hipStreamDestroy(ws.stream);
+        if (ws.pinned) (void)hipHostFree(ws.pinned);
+        if (ws.dev_src) (void)hipFree(ws.dev_src);
+        for (auto* v : {&ws.dev_out, &ws.dev_tmp})
+            for (auto* p : *v)
+                if (p) (void)hipFree(p);
+    }
 }
 
 // Deterministic mode: engine i of the decode window is seeded with the i-th output of
@@ -509,85 +512,112 @@ void batch_decoder::grow_slot_engines(int n)
     }
 }
 
-void batch_decoder::decode(int n, const decoded_element* records, void* const* outputs, bool on_device,
-                           void* stream_)
+namespace {
+void grow_dev(uint8_t*& p, size_t& cap, size_t bytes)
 {
-    if (n <= 0) return;
-    if (!m_batch_major && n % m_batch_size != 0)
-        invalid("batch_major=false needs whole batches per decode window");
-    if (m_deterministic) grow_slot_engines(n);
-    if (!m_ctx) check(aeon_hip_ctx_create(m_device, &m_ctx));
-    hip_check(hipSetDevice(m_device), "hipSetDevice");
-    hipStream_t   stream = (hipStream_t)stream_;
-    const int     ne     = (int)m_provider->get_input_count();
+    if (bytes <= cap) return;
+    if (p) hip_check(hipFree(p), "hipFree");
+    p = nullptr;
+    hip_check(hipMalloc((void**)&p, bytes), "hipMalloc");
+    cap = bytes;
+}
+} // namespace
+
+// One decode window on `stream` using window slot ws (whose previous window has completed):
+// batch_decoder::filler (batch_decoder.cpp:73-99) with the per-record body split into
+//   host:   JPEG headers -> make_params (record order: aeon's deterministic draw order) ->
+//           decoded pixels staged into pinned memory on the pool -> JPEG entropy decode
+//   device: H2D of the staged pixels -> JPEG IDCT/colour into the source arena -> augmentation
+//           kernels (post_process) -> [batch transpose] -> [D2H into host outputs]
+void batch_decoder::enqueue(window_slot& ws, int n, const decoded_element* in, void* const* outputs, bool on_device,
+                            hipStream_t stream)
+{
+    const int ne = (int)m_provider->get_input_count();
+    // image::extractor::extract of encoded elements: the frame header gives the decoded size; the
+    // record is decoded with the provider's channel count (CV_LOAD_IMAGE_COLOR / GRAYSCALE)
+    std::vector<decoded_element> records(in, in + (size_t)n * ne);
+    for (int i = 0; i < n; i++)
+        for (int k = 0; k < ne; k++) {
+            decoded_element& e = records[(size_t)i * ne + k];
+            if (!e.encoded) continue;
+            if (m_provider->providers()[k]->is_mask())
+                throw std::runtime_error("encoded pixel masks are not decoded here (PNG): pass the decoded mask");
+            int comps = 0;
+            check(aeon_jpeg_info(e.data, e.size, &e.width, &e.height, &comps));
+            e.channels = m_provider->providers()[k]->out_desc().channels;
+            e.stride   = e.width * e.channels;
+        }
     decode_window w;
     w.n = n;
     w.descs.assign(ne, std::vector<aeon_img_desc>(n));
     w.params.assign(ne, std::vector<aeon_aug_params>(n));
     w.offset.assign(ne, std::vector<size_t>(n));
-    size_t total = 0;
-    for (int i = 0; i < n; i++)
-        for (int k = 0; k < ne; k++) {
-            const decoded_element& e = records[(size_t)i * ne + k];
-            const size_t           b = (size_t)std::max(e.width, 0) * std::max(e.height, 0) * std::max(e.channels, 0);
-            w.offset[k][i]           = total;
-            w.descs[k][i]            = aeon_img_desc{total, e.width, e.height, e.width * e.channels, e.channels};
-            total += (b + 15) & ~(size_t)15;
-        }
+    // source arena: decoded elements first (staged + one H2D), then the device-decoded JPEGs
+    size_t staged = 0, total = 0;
+    for (int pass = 0; pass < 2; pass++)
+        for (int i = 0; i < n; i++)
+            for (int k = 0; k < ne; k++) {
+                const decoded_element& e = records[(size_t)i * ne + k];
+                if (e.encoded != (pass == 1)) continue;
+                const size_t b = (size_t)std::max(e.width, 0) * std::max(e.height, 0) * std::max(e.channels, 0);
+                w.offset[k][i] = total;
+                w.descs[k][i]  = aeon_img_desc{total, e.width, e.height, e.width * e.channels, e.channels, 0, 0};
+                total += (b + 15) & ~(size_t)15;
+                if (pass == 0) staged = total;
+            }
     total = std::max<size_t>(total, 16);
-    if (total > m_pinned_cap) {
-        if (m_pinned) hip_check(hipHostFree(m_pinned), "hipHostFree");
-        m_pinned = nullptr;
-        hip_check(hipHostMalloc((void**)&m_pinned, total, hipHostMallocDefault), "hipHostMalloc");
-        m_pinned_cap = total;
+    if (staged > ws.pinned_cap) {
+        if (ws.pinned) hip_check(hipHostFree(ws.pinned), "hipHostFree");
+        ws.pinned = nullptr;
+        hip_check(hipHostMalloc((void**)&ws.pinned, staged, hipHostMallocDefault), "hipHostMalloc");
+        ws.pinned_cap = staged;
     }
-    if (total > m_dev_src_cap) {
-        if (m_dev_src) hip_check(hipFree(m_dev_src), "hipFree");
-        m_dev_src = nullptr;
-        hip_check(hipMalloc((void**)&m_dev_src, total), "hipMalloc");
-        m_dev_src_cap = total;
-    }
-    w.arena = m_pinned;
+    grow_dev(ws.dev_src, ws.dev_src_cap, total);
+    w.arena = ws.pinned;
     // batch_decoder::process: the slot engine of record i draws its params (deterministic mode
     // swaps the slot engine in and out, batch_decoder.cpp:62-71).  The draws run in record
     // order on this thread -- aeon's single-threaded order, the only reproducible one, since
     // the lighting normal_distribution caches a value inside the shared factory -- and the
     // pool threads stage the pixels into the pinned arena.
     for (int i = 0; i < n; i++)
-        m_provider->draw(i, records + (size_t)i * ne, w, m_deterministic ? m_random[i] : m_local_random);
-    m_pool->run(n, [&](int i) { m_provider->stage(i, records + (size_t)i * ne, w); });
-    hip_check(hipMemcpyAsync(m_dev_src, m_pinned, total, hipMemcpyHostToDevice, stream), "hipMemcpyAsync");
+        m_provider->draw(i, records.data() + (size_t)i * ne, w, m_deterministic ? m_random[i] : m_local_random);
+    if (staged) {
+        m_pool->run(n, [&](int i) { m_provider->stage(i, records.data() + (size_t)i * ne, w); });
+        hip_check(hipMemcpyAsync(ws.dev_src, ws.pinned, staged, hipMemcpyHostToDevice, stream), "hipMemcpyAsync");
+    }
+    for (int k = 0; k < ne; k++) {
+        std::vector<const void*> files;
+        std::vector<size_t>      sizes;
+        std::vector<aeon_img_desc> descs;
+        for (int i = 0; i < n; i++) {
+            const decoded_element& e = records[(size_t)i * ne + k];
+            if (!e.encoded) continue;
+            files.push_back(e.data), sizes.push_back(e.size), descs.push_back(w.descs[k][i]);
+        }
+        if (!files.empty())
+            check(aeon_hip_decode_jpeg_batch(m_ctx, (int)files.size(), files.data(), sizes.data(), descs.data(),
+                                             ws.dev_src, stream));
+    }
     std::vector<void*> outs(ne);
+    ws.dev_out.resize(ne, nullptr), ws.dev_out_cap.resize(ne, 0);
+    ws.dev_tmp.resize(ne, nullptr), ws.dev_tmp_cap.resize(ne, 0);
     for (int k = 0; k < ne; k++) {
         const size_t bytes = (size_t)n * m_provider->providers()[k]->shape().byte_size();
-        if (on_device) {
-            outs[k] = outputs[k];
-        } else {
-            if (bytes > m_dev_out_cap[k]) {
-                if (m_dev_out[k]) hip_check(hipFree(m_dev_out[k]), "hipFree");
-                m_dev_out[k] = nullptr;
-                hip_check(hipMalloc((void**)&m_dev_out[k], bytes), "hipMalloc");
-                m_dev_out_cap[k] = bytes;
-            }
-            outs[k] = m_dev_out[k];
+        if (on_device) outs[k] = outputs[k];
+        else {
+            grow_dev(ws.dev_out[k], ws.dev_out_cap[k], bytes);
+            outs[k] = ws.dev_out[k];
         }
     }
-    auto grow = [&](std::vector<uint8_t*>& v, std::vector<size_t>& cap, int k, size_t bytes) {
-        if (bytes <= cap[k]) return;
-        if (v[k]) hip_check(hipFree(v[k]), "hipFree");
-        v[k] = nullptr;
-        hip_check(hipMalloc((void**)&v[k], bytes), "hipMalloc");
-        cap[k] = bytes;
-    };
     if (m_batch_major) {
-        m_provider->post_process(m_ctx, w, m_dev_src, outs.data(), stream);
+        m_provider->post_process(m_ctx, w, ws.dev_src, outs.data(), stream);
     } else {
         std::vector<void*> tmp(ne);
         for (int k = 0; k < ne; k++) {
-            grow(m_dev_tmp, m_dev_tmp_cap, k, (size_t)n * m_provider->providers()[k]->shape().byte_size());
-            tmp[k] = m_dev_tmp[k];
+            grow_dev(ws.dev_tmp[k], ws.dev_tmp_cap[k], (size_t)n * m_provider->providers()[k]->shape().byte_size());
+            tmp[k] = ws.dev_tmp[k];
         }
-        m_provider->post_process(m_ctx, w, m_dev_src, tmp.data(), stream);
+        m_provider->post_process(m_ctx, w, ws.dev_src, tmp.data(), stream);
         for (int k = 0; k < ne; k++) {
             const shape_type& sh    = m_provider->providers()[k]->shape();
             const size_t      esize = sh.otype.size;
@@ -604,8 +634,55 @@ void batch_decoder::decode(int n, const decoded_element* records, void* const* o
             hip_check(hipMemcpyAsync(outputs[k], outs[k], (size_t)n * m_provider->providers()[k]->shape().byte_size(),
                                      hipMemcpyDeviceToHost, stream),
                       "hipMemcpyAsync");
+    if (!ws.done) hip_check(hipEventCreateWithFlags(&ws.done, hipEventDisableTiming), "hipEventCreate");
+    hip_check(hipEventRecord(ws.done, stream), "hipEventRecord");
+    ws.pending = true;
+}
+
+void batch_decoder::decode(int n, const decoded_element* records, void* const* outputs, bool on_device, void* stream_)
+{
+    if (n <= 0) return;
+    if (!m_batch_major && n % m_batch_size != 0) invalid("batch_major=false needs whole batches per decode window");
+    while (!m_queue.empty()) wait(); // windows are completed in submission order
+    if (m_deterministic) grow_slot_engines(n);
+    if (!m_ctx) check(aeon_hip_ctx_create(m_device, &m_ctx));
+    hip_check(hipSetDevice(m_device), "hipSetDevice");
+    window_slot& ws = m_slots[m_next];
+    m_next ^= 1;
+    if (ws.pending) hip_check(hipEventSynchronize(ws.done), "hipEventSynchronize");
+    ws.pending = false;
+    enqueue(ws, n, records, outputs, on_device, (hipStream_t)stream_);
     // the pinned arena and the window's params must outlive the copies: finish the window
-    check(aeon_hip_synchronize(m_ctx, stream));
+    check(aeon_hip_synchronize(m_ctx, stream_));
+    ws.pending = false;
+}
+
+void batch_decoder::submit(int n, const decoded_element* records, void* const* outputs, bool on_device)
+{
+    if (n <= 0) invalid("empty decode window");
+    if (!m_batch_major && n % m_batch_size != 0) invalid("batch_major=false needs whole batches per decode window");
+    if (m_queue.size() >= 2) invalid("two windows are in flight: wait() for the oldest before submitting another");
+    if (m_deterministic) grow_slot_engines(n);
+    if (!m_ctx) check(aeon_hip_ctx_create(m_device, &m_ctx));
+    hip_check(hipSetDevice(m_device), "hipSetDevice");
+    const int    slot = m_next;
+    window_slot& ws   = m_slots[slot];
+    m_next ^= 1;
+    if (!ws.stream) hip_check(hipStreamCreateWithFlags(&ws.stream, hipStreamNonBlocking), "hipStreamCreate");
+    if (ws.pending) hip_check(hipEventSynchronize(ws.done), "hipEventSynchronize");
+    ws.pending = false;
+    enqueue(ws, n, records, outputs, on_device, ws.stream);
+    m_queue.push_back(slot);
+}
+
+void batch_decoder::wait()
+{
+    if (m_queue.empty()) invalid("no decode window in flight");
+    const int slot = m_queue.front();
+    m_queue.erase(m_queue.begin());
+    window_slot& ws = m_slots[slot];
+    check(aeon_hip_synchronize(m_ctx, ws.stream));
+    ws.pending = false;
 }
 
 // ---- manifest_file node slicing ------------------------------------------------------------------
@@ -722,6 +799,56 @@ int aeon_decoder_decode(aeon_decoder* d, int n, const aeon_record_elem* elems, v
                                                 elems[i].channels,
                                                 elems[i].stride ? elems[i].stride : elems[i].width * elems[i].channels};
         d->d->decode(n, recs.data(), outputs, outputs_on_device != 0, stream);
+    });
+}
+
+namespace {
+std::vector<aeon_hip::decoded_element> to_elements(aeon_decoder* d, int n, const aeon_encoded_elem* elems)
+{
+    const int ne = (int)d->d->provider().get_input_count();
+    std::vector<aeon_hip::decoded_element> recs((size_t)n * ne);
+    for (size_t i = 0; i < recs.size(); i++) {
+        const aeon_encoded_elem& e = elems[i];
+        aeon_hip::decoded_element& r = recs[i];
+        r.data = (const uint8_t*)e.data;
+        if (e.width > 0) {
+            r.width = e.width, r.height = e.height, r.channels = e.channels;
+            r.stride = e.stride ? e.stride : e.width * e.channels;
+        } else {
+            if (!e.data || !e.size) throw std::runtime_error("received encoded image with size 0, at idx " +
+                                                             std::to_string(i / ne));
+            r.encoded = true, r.size = e.size;
+        }
+    }
+    return recs;
+}
+} // namespace
+
+int aeon_decoder_decode_encoded(aeon_decoder* d, int n, const aeon_encoded_elem* elems, void* const* outputs,
+                                int outputs_on_device, void* stream)
+{
+    return host_guarded([&] {
+        if (!d || (n > 0 && (!elems || !outputs))) throw std::invalid_argument("null argument");
+        auto recs = to_elements(d, n, elems);
+        d->d->decode(n, recs.data(), outputs, outputs_on_device != 0, stream);
+    });
+}
+
+int aeon_decoder_submit(aeon_decoder* d, int n, const aeon_encoded_elem* elems, void* const* outputs,
+                        int outputs_on_device)
+{
+    return host_guarded([&] {
+        if (!d || n <= 0 || !elems || !outputs) throw std::invalid_argument("null argument");
+        auto recs = to_elements(d, n, elems);
+        d->d->submit(n, recs.data(), outputs, outputs_on_device != 0);
+    });
+}
+
+int aeon_decoder_wait(aeon_decoder* d)
+{
+    return host_guarded([&] {
+        if (!d) throw std::invalid_argument("null argument");
+        d->d->wait();
     });
 }
 

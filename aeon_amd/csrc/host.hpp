@@ -9,9 +9,10 @@
 //   batch_decoder            src/batch_decoder.cpp:24-99        (thread pool + deterministic slots)
 //   thread_pool              src/thread_pool.hpp:82-175         (dynamic atomic task counter)
 //   manifest node slicing    src/manifest_file.cpp:278-295
-// Decoding (image::extractor::extract = cv::imdecode) stays with the caller: records arrive as
-// decoded HWC uint8 pixels.  Per record, the pool threads draw the augmentation params and
-// stage the pixels into pinned memory; one flush per decode window runs the HIP kernels.
+// Records arrive as encoded JPEG files (image::extractor::extract's cv::imdecode runs in the
+// JPEG stage: host Huffman + GPU IDCT/colour, jpeg_host.cpp) or as decoded HWC uint8 pixels (staged
+// into pinned memory by the pool).  One flush per decode window runs the HIP kernels; windows are
+// double-buffered like async_manager's two containers (submit / wait).
 #pragma once
 #include <atomic>
 #include <condition_variable>
@@ -24,6 +25,8 @@
 #include <thread>
 #include <utility>
 #include <vector>
+
+#include <hip/hip_runtime_api.h>
 
 #include "../../include/aeon_hip.h"
 #include "json.hpp"
@@ -58,10 +61,13 @@ struct image_config {
     explicit image_config(const Json& js);
 };
 
-// A decoded element of a record (what image::extractor::extract returns, as plain pixels).
+// An element of a record: an encoded JPEG file (size > 0; width/height/channels filled in from
+// its header by the decoder) or decoded HWC uint8 pixels (what image::extractor::extract returns).
 struct decoded_element {
     const uint8_t* data = nullptr;
     int            width = 0, height = 0, channels = 0, stride = 0;
+    size_t         size    = 0;     // encoded bytes
+    bool           encoded = false; // JPEG file: decoded on the device (jpeg_host.cpp)
 };
 
 // Per-window staging shared by the providers (filled concurrently by the pool threads).
@@ -157,17 +163,39 @@ private:
 };
 
 // batch_decoder: decode windows of records on the pool, flush each window to the GPU.
+// Two window slots (async_manager's two containers, src/async_manager.hpp:203-204), each with its
+// own pinned staging, device buffers, stream and completion event: submit() stages window k+1 and
+// enqueues its copies and kernels while window k's are still running; wait() completes the oldest.
 class batch_decoder {
 public:
     batch_decoder(const Json& config, int device);
     ~batch_decoder();
-    // n records x input_count elements (row-major); outputs[k] per provider buffer
+    // n records x input_count elements (row-major); outputs[k] per provider buffer.  Synchronous,
+    // on `stream` (batch_decoder::filler, src/batch_decoder.cpp:73-99).
     void decode(int n, const decoded_element* records, void* const* outputs, bool outputs_on_device,
                 void* stream);
+    // Asynchronous window on the decoder's own streams: returns once the records' bytes are
+    // consumed (drawn, staged, entropy-decoded); outputs are complete after the matching wait().
+    void submit(int n, const decoded_element* records, void* const* outputs, bool outputs_on_device);
+    void wait(); // oldest submitted window
+    int  outstanding() const { return (int)m_queue.size(); }
     provider_base& provider() { return *m_provider; }
     int            batch_size() const { return m_batch_size; }
 
 private:
+    struct window_slot {
+        hipStream_t           stream  = nullptr;
+        hipEvent_t            done    = nullptr;
+        bool                  pending = false;
+        uint8_t*              pinned = nullptr;
+        size_t                pinned_cap = 0;
+        uint8_t*              dev_src = nullptr;
+        size_t                dev_src_cap = 0;
+        std::vector<uint8_t*> dev_out, dev_tmp;
+        std::vector<size_t>   dev_out_cap, dev_tmp_cap;
+    };
+    void enqueue(window_slot& ws, int n, const decoded_element* records, void* const* outputs, bool on_device,
+                 hipStream_t stream);
     void                           grow_slot_engines(int n);
     std::shared_ptr<provider_base> m_provider;
     int                            m_batch_size = 1;
@@ -178,17 +206,12 @@ private:
     std::unique_ptr<thread_pool>   m_pool;
     aeon_hip_ctx*                  m_ctx = nullptr;
     int                            m_device = 0;
-    uint8_t*                       m_pinned = nullptr;
-    size_t                         m_pinned_cap = 0;
-    uint8_t*                       m_dev_src = nullptr;
-    size_t                         m_dev_src_cap = 0;
-    std::vector<uint8_t*>          m_dev_out;
-    std::vector<size_t>            m_dev_out_cap;
-    // batch_major=false (loader.hpp:63): outputs are produced batch-major into m_dev_tmp and
+    window_slot                    m_slots[2];
+    int                            m_next = 0;
+    std::vector<int>               m_queue; // submitted, not yet waited (slot indices, oldest first)
+    // batch_major=false (loader.hpp:63): outputs are produced batch-major into dev_tmp and
     // transposed per batch into the caller's layout (batch_iterator.cpp:125-136)
     bool                           m_batch_major = true;
-    std::vector<uint8_t*>          m_dev_tmp;
-    std::vector<size_t>            m_dev_tmp_cap;
 };
 
 // manifest_file node slicing (generate_blocks, src/manifest_file.cpp:278-295)

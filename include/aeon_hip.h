@@ -206,6 +206,28 @@ int aeon_decoder_output_info(aeon_decoder* d, int index, char* name, size_t name
  * the window is complete (batch_decoder::filler, src/batch_decoder.cpp:73-99). */
 int aeon_decoder_decode(aeon_decoder* d, int n, const aeon_record_elem* elems, void* const* outputs,
                         int outputs_on_device, void* stream);
+/* A record element as aeon's encoded_record holds it (src/buffer_batch.hpp:45-152): an encoded
+ * JPEG file (width == 0: data/size, decoded by the JPEG stage with the provider's channel count),
+ * or -- width > 0 -- decoded HWC uint8 pixels as in aeon_record_elem (pixel masks must be). */
+typedef struct aeon_encoded_elem {
+    const void* data;
+    size_t      size;
+    int32_t     width, height, channels;
+    int32_t     stride; /* decoded pixels only; 0 = width*channels */
+} aeon_encoded_elem;
+
+/* As aeon_decoder_decode, from encoded records: extract (JPEG) + transform + load per record. */
+int aeon_decoder_decode_encoded(aeon_decoder* d, int n, const aeon_encoded_elem* elems, void* const* outputs,
+                                int outputs_on_device, void* stream);
+/* Double-buffered decode windows (async_manager's two containers, src/async_manager.hpp:91-114,
+ * 162-204): submit returns once the window's input bytes are consumed (params drawn, pixels staged,
+ * JPEGs entropy-decoded) with its copies and kernels queued on the decoder's own stream; at most two
+ * windows are in flight, and outputs[k] must stay valid until aeon_decoder_wait returns for that
+ * window (windows complete in submission order).  Host outputs should be pinned
+ * (aeon_hip_host_alloc) for the D2H to overlap the next window. */
+int aeon_decoder_submit(aeon_decoder* d, int n, const aeon_encoded_elem* elems, void* const* outputs,
+                        int outputs_on_device);
+int aeon_decoder_wait(aeon_decoder* d);
 const char* aeon_decoder_last_error(void);
 
 /* manifest_file node slicing (src/manifest_file.cpp:278-295): the record indices of node

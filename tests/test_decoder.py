@@ -101,3 +101,67 @@ def test_decoder_fixed_aspect_ratio_uint8():
     od = C.out_desc_for(etl, aug)
     ref = np.stack([H.place_canvas(r, od) for r in H.oracle_records([r[0] for r in recs], params, od)])
     assert np.array_equal(out, ref)
+
+
+def _jpeg_files():
+    import os
+    fx = np.load(os.path.join(os.path.dirname(__file__), "golden", "jpeg_fixtures.npz"))
+    names = sorted({k.rsplit(".", 1)[0] for k in fx.files})
+    return [fx[n + ".jpg"].tobytes() for n in names]
+
+
+def test_decoder_encoded_jpeg_records_c1():
+    """provider::image::provide end to end from encoded records (image::extractor::extract ->
+    transform -> load): JPEG files through the JPEG stage and the C1 eval transform, against the
+    oracle's decode + transform + load of the same files (the golden img_2112_70.jpg among them)."""
+    import oracle as O
+    files = _jpeg_files()
+    files = [f for f in files if min(O.jpeg_info(f)[:2]) >= 8]  # resize_short of the smallest is degenerate
+    cfg = dict(batch_size=len(files), random_seed=7, etl=[C.IMAGE_224], augmentation=[C.C1_AUG])
+    (out,) = A.Decoder(cfg).decode([(f,) for f in files])
+    dec = [O.jpeg_decode(f, 3) for f in files]
+    params = H.draw_params(C.C1_AUG, [(d.shape[1], d.shape[0]) for d in dec], 224, 224, seed=7)
+    (ref,) = _oracle([(d,) for d in dec], params, [C.IMAGE_224], C.C1_AUG)
+    assert np.array_equal(out, ref)
+
+
+def test_decoder_encoded_and_decoded_elements_mix():
+    """An encoded JPEG image element next to a decoded pixel-mask element (C5 shape): the mask
+    shares the image's params, and the JPEG record equals its pre-decoded twin."""
+    import oracle as O
+    files = [f for f in _jpeg_files() if min(O.jpeg_info(f)[:2]) >= 32][:6]
+    dec = [O.jpeg_decode(f, 3) for f in files]
+    masks = [((A.synthetic_image(70 + i, d.shape[1], d.shape[0], 1) > 127) * 255).astype(np.uint8)
+             for i, d in enumerate(dec)]
+    cfg = dict(batch_size=len(files), random_seed=3, etl=[C.IMAGE_512, C.MASK_512], augmentation=[C.C5_AUG])
+    img_a, msk_a = A.Decoder(cfg).decode([(f, m) for f, m in zip(files, masks)])
+    img_b, msk_b = A.Decoder(cfg).decode([(d, m) for d, m in zip(dec, masks)])
+    assert np.array_equal(img_a, img_b) and np.array_equal(msk_a, msk_b)
+
+
+def test_decoder_submit_wait_double_buffered():
+    """aeon_decoder_submit / wait: two windows in flight on the decoder's streams (async_manager's
+    two containers) give exactly the synchronous decode's outputs, window by window; a third submit
+    before a wait is refused."""
+    import torch
+    files = _jpeg_files()
+    files = [f for f in files if min(A.jpeg_info(f)[:2]) >= 8]
+    cfg = dict(batch_size=len(files), random_seed=11, etl=[C.IMAGE_224], augmentation=[C.C2_AUG])
+    windows = [[(files[(i + w) % len(files)],) for i in range(len(files))] for w in range(4)]
+    sync = A.Decoder(cfg)
+    want = [sync.decode(win)[0] for win in windows]
+    d = A.Decoder(cfg)
+    item = 3 * 224 * 224 * 4
+    bufs = [torch.empty(len(files) * item, dtype=torch.uint8).pin_memory() for _ in range(2)]
+    got = []
+    d.submit(windows[0], [bufs[0].data_ptr()])
+    d.submit(windows[1], [bufs[1].data_ptr()])
+    with pytest.raises(A.AeonHipError, match="in flight"):
+        d.submit(windows[2], [bufs[0].data_ptr()])
+    for w in range(4):
+        d.wait()
+        got.append(bufs[w % 2].numpy().view(np.float32).reshape(want[w].shape).copy())
+        if w + 2 < 4:
+            d.submit(windows[w + 2], [bufs[w % 2].data_ptr()])
+    for w in range(4):
+        assert np.array_equal(got[w], want[w]), w
