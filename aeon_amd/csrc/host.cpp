@@ -2,6 +2,7 @@
 #include "host.hpp"
 
 #include <hip/hip_runtime.h>
+#include <sched.h>
 
 #include <algorithm>
 #include <cstring>
@@ -444,7 +445,14 @@ int aeon_thread_count(const std::string& cpu_list)
         }
         return std::max<int>(1, (int)cpus.size());
     }
+    // hardware_concurrency, capped by the CPUs this process may run on (affinity mask) and by
+    // OMP_NUM_THREADS when the launcher sets it (a container's CPU share: the GPU box gives each
+    // job 16 of its 256 CPUs, and 254 pool threads would only contend for them)
     int hc = (int)std::thread::hardware_concurrency();
+    cpu_set_t set;
+    if (sched_getaffinity(0, sizeof(set), &set) == 0) hc = std::min(hc, std::max(1, CPU_COUNT(&set)));
+    if (const char* e = std::getenv("OMP_NUM_THREADS"))
+        if (std::atoi(e) > 0) hc = std::min(hc, std::atoi(e));
     return std::max(1, hc - std::min(2, hc / 8));
 }
 

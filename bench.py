@@ -352,22 +352,117 @@ def cpu_baseline(A, C, budget_s, cfg="C2"):
                       "scalar C++, a lower bound on aeon's OpenCV-SIMD path"}
 
 
-def run_c1_decoder(A, C, budget_s=2.0):
-    """C1 through the product's decode stage (aeon_decoder: provider_factory + batch_decoder,
-    host records in, host batch out): 32-record windows of 480x360 decoded records."""
-    cfg = dict(C.CONFIGS["C1"], random_seed=1)
+def jpeg_files(batch):
+    """Encoded records of a decode window: aeon's own JPEG fixtures (test/test_data/img_2112_70.jpg
+    480x360 and flowers.jpg 600x800, 4:2:0 baseline; committed in tests/golden), cycled."""
+    import numpy as np
+    fx = np.load(os.path.join(ROOT, "tests", "golden", "jpeg_fixtures.npz"))
+    files = [fx["img_2112_70.jpg"].tobytes(), fx["flowers.jpg"].tobytes()]
+    return [files[i % 2] for i in range(batch)]
+
+
+def run_e2e_jpeg(A, C, torch, batch=256, windows=12, on_device=False):
+    """The product's whole decode stage from encoded records, double-buffered (aeon_decoder_submit /
+    wait over two windows): JPEG entropy decode on the host pool, sparse coefficients H2D, GPU IDCT
+    + colour into the source arena, C2 augmentation, and (host outputs) D2H into pinned buffers."""
+    cfg = dict(C.CONFIGS["C2"], random_seed=1)
+    files = jpeg_files(batch)
+    recs = [(f,) for f in files]
     d = A.Decoder(cfg)
-    recs = [(A.synthetic_image(i, 480, 360, 3),) for i in range(cfg["batch_size"])]
-    d.decode(recs)  # warmup (context, kernels, buffers)
-    done, t0 = 0, time.perf_counter()
-    while time.perf_counter() - t0 < budget_s:
-        d.decode(recs)
-        done += len(recs)
+    item = 3 * 224 * 224 * 4
+    if on_device:
+        bufs = [torch.empty(batch * item, dtype=torch.uint8, device="cuda") for _ in range(2)]
+    else:
+        bufs = [torch.empty(batch * item, dtype=torch.uint8).pin_memory() for _ in range(2)]
+    for w in range(2):  # warmup: contexts, staging, kernels
+        d.submit(recs, [bufs[w].data_ptr()], on_device)
+    d.wait()
+    d.wait()
+    t0 = time.perf_counter()
+    for w in range(windows):
+        if w >= 2:
+            d.wait()
+        d.submit(recs, [bufs[w % 2].data_ptr()], on_device)
+    d.wait()
+    d.wait()
     dt = time.perf_counter() - t0
     d.close()
-    return {"value": done / dt, "unit": "images/s", "batch": cfg["batch_size"],
-            "what": "aeon_decoder_decode: host decoded 480x360 records -> pinned H2D -> resize_short 256 + "
-                    "center crop 224 -> fp32 CHW -> D2H, one decode window per call"}
+    return batch * windows / dt
+
+
+def run_jpeg_stage(A, torch, batch=256, reps=10):
+    """aeon_hip_decode_jpeg_batch alone (extract of a window of JPEG files into device memory)."""
+    files = jpeg_files(batch)
+    ctx = A.Context(torch.cuda.current_device())
+    infos = [A.jpeg_info(f) for f in files]
+    descs, off = [], 0
+    for (w, h, _) in infos:
+        descs.append(A.ImgDesc(offset=off, width=w, height=h, stride=w * 3, channels=3))
+        off += (w * h * 3 + 15) // 16 * 16
+    descs = (A.ImgDesc * batch)(*descs)
+    dst = torch.empty(off, dtype=torch.uint8, device="cuda")
+    stream = torch.cuda.current_stream().cuda_stream
+    ctx.decode_jpeg_batch(files, descs, dst.data_ptr(), stream)
+    ctx.synchronize(stream)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        ctx.decode_jpeg_batch(files, descs, dst.data_ptr(), stream)
+    ctx.synchronize(stream)
+    dt = time.perf_counter() - t0
+    ctx.close()
+    mp = sum(w * h for (w, h, _) in infos) / batch / 1e6
+    return {"value": batch * reps / dt, "unit": "images/s", "megapixels_per_image": mp,
+            "what": "aeon_hip_decode_jpeg_batch: host Huffman decode on the pool, sparse coefficients H2D, "
+                    "GPU ISLOW IDCT + fancy upsampling + YCbCr->BGR into device memory"}
+
+
+def cpu_baseline_jpeg(A, C, budget_s):
+    """aeon's full CPU path per record (imdecode -> transform -> load) restated by the oracle, on the
+    same encoded files and C2 params, aeon's pool policy: a lower bound (scalar decode, no SIMD)."""
+    import oracle as O
+    from tests import helpers as H
+    threads, hc, visible = pool_threads()
+    files = jpeg_files(256)
+    sizes = [O.jpeg_info(f)[:2] for f in files]
+    params = [H.to_oracle_params(p) for p in H.draw_params(C.C2_AUG, sizes, 224, 224, seed=1)]
+    lc = H.oracle_load_config(C.out_desc_for(C.IMAGE_224, C.C2_AUG))
+    done, secs = 0, 0.0
+    while secs < budget_s:
+        secs += O.batch_decode_augment(files, params, lc, (3, 224, 224), threads)[1]
+        done += len(files)
+    return {"value": done / secs, "unit": "images/s", "cores": threads, "kind": "port",
+            "sample": f"{done} JPEG records (img_2112_70.jpg / flowers.jpg) decoded + C2-augmented by the oracle "
+                      f"on {threads} pool threads ({secs:.1f} s); scalar C++, a lower bound on aeon's "
+                      "libjpeg-turbo + OpenCV-SIMD path"}
+
+
+def run_c1_decoder(A, C, torch, budget_s=2.0):
+    """C1 through the product's decode stage (aeon_decoder: provider_factory + batch_decoder,
+    host records in, host batch out): 32-record windows of 480x360 decoded records, two windows in
+    flight (submit / wait) into pinned host batches."""
+    cfg = dict(C.CONFIGS["C1"], random_seed=1)
+    d = A.Decoder(cfg)
+    n = cfg["batch_size"]
+    recs = [(A.synthetic_image(i, 480, 360, 3),) for i in range(n)]
+    bufs = [torch.empty(n * 3 * 224 * 224 * 4, dtype=torch.uint8).pin_memory() for _ in range(2)]
+    for w in range(2):  # warmup (context, kernels, buffers)
+        d.submit(recs, [bufs[w].data_ptr()])
+    d.wait()
+    d.wait()
+    done, w, t0 = 0, 0, time.perf_counter()
+    while time.perf_counter() - t0 < budget_s:
+        if w >= 2:
+            d.wait()
+        d.submit(recs, [bufs[w % 2].data_ptr()])
+        w += 1
+        done += n
+    d.wait()
+    d.wait()
+    dt = time.perf_counter() - t0
+    d.close()
+    return {"value": done / dt, "unit": "images/s", "batch": n,
+            "what": "aeon_decoder submit/wait: host decoded 480x360 records -> pinned H2D -> resize_short 256 + "
+                    "center crop 224 -> fp32 CHW -> D2H into pinned batches, two 32-record windows in flight"}
 
 
 def load_traffic(path, cfg):
@@ -486,7 +581,15 @@ def main():
         extra["C5"] = run_c5(A, C, torch, max(5, args.steps // 5), 2, args.pool_mib)
         extra["e2e_host_to_host"] = {"value": run_e2e(A, C, torch, 256, 20), "unit": "images/s",
                                      "what": "pinned H2D of decoded 256x256 u8 + kernel + D2H of fp32 CHW"}
-        extra["C1"] = {"decoder": run_c1_decoder(A, C)}
+        extra["C1"] = {"decoder": run_c1_decoder(A, C, torch)}
+        extra["e2e_jpeg_decoder"] = {
+            "host_outputs": {"value": run_e2e_jpeg(A, C, torch, on_device=False), "unit": "images/s"},
+            "device_outputs": {"value": run_e2e_jpeg(A, C, torch, on_device=True), "unit": "images/s"},
+            "jpeg_stage": run_jpeg_stage(A, torch),
+            "what": "encoded JPEG records (aeon's img_2112_70.jpg / flowers.jpg) -> aeon_decoder submit/wait "
+                    "(two windows in flight): extract on the JPEG stage + C2 augmentation, 256-record windows"}
+        if not args.no_cpu_baseline:
+            extra["e2e_jpeg_decoder"]["cpu_baseline"] = cpu_baseline_jpeg(A, C, args.cpu_extra_seconds)
         if not args.no_cpu_baseline:
             extra["C1"]["cpu_baseline"] = cpu_baseline(A, C, args.cpu_extra_seconds, "C1")
             extra["C3"]["cpu_baseline"] = cpu_baseline(A, C, args.cpu_extra_seconds, "C3") if "C3" in extra else None

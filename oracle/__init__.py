@@ -115,6 +115,9 @@ def lib():
         L.orc_jpeg_info.argtypes = [ctypes.c_char_p, ctypes.c_size_t] + [P(ctypes.c_int)] * 3
         L.orc_jpeg_decode.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p]
         L.orc_jpeg_last_error.restype = ctypes.c_char_p
+        L.orc_batch_decode_augment.restype = ctypes.c_double
+        L.orc_batch_decode_augment.argtypes = [ctypes.c_int, P(ctypes.c_void_p), P(ctypes.c_size_t), P(Params),
+                                               P(LoadConfig), ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
         L.orc_last_error.restype = ctypes.c_char_p
         _lib = L
     return _lib
@@ -319,6 +322,20 @@ def batch_image_mask(srcs, masks, params_list, lc, item_shape, mlc, mask_shape, 
     if secs < 0:
         raise RuntimeError("oracle: " + lib().orc_last_error().decode())
     return out, mout, secs
+
+
+def batch_decode_augment(files, params_list, lc, item_shape, threads):
+    """aeon's CPU path (JPEG decode + transform + load) over encoded files; returns (out, seconds)."""
+    n = len(files)
+    bufs = [bytes(f) for f in files]
+    ptrs = (ctypes.c_void_p * n)(*[ctypes.cast(ctypes.c_char_p(b), ctypes.c_void_p) for b in bufs])
+    sizes = (ctypes.c_size_t * n)(*[len(b) for b in bufs])
+    ps = (Params * n)(*params_list)
+    out = np.zeros((n,) + tuple(item_shape), np.uint8 if lc.out_dtype == 0 else np.float32)
+    secs = lib().orc_batch_decode_augment(n, ptrs, sizes, ps, ctypes.byref(lc), out.ctypes.data, out[0].nbytes, threads)
+    if secs < 0:
+        raise RuntimeError("oracle: " + lib().orc_last_error().decode())
+    return out, secs
 
 
 def transpose(src, rows, cols, element_size):

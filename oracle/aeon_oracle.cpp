@@ -924,6 +924,49 @@ double orc_batch_image_mask(int n, const uint8_t* const* srcs, const uint8_t* co
     return std::chrono::duration<double>(t1 - t0).count();
 }
 
+// aeon's whole CPU path per record -- image::extractor::extract (JPEG decode, jpeg_oracle.cpp) ->
+// transform_single_image -> loader::load -- over a batch of encoded files on a thread pool: the CPU
+// baseline of the end-to-end decode stage.  params[i] must be drawn for file i's decoded size.
+double orc_batch_decode_augment(int n, const uint8_t* const* files, const size_t* sizes, const orc_params* params,
+                                const orc_load_config* lc, void* out, size_t item_bytes, int threads)
+{
+    std::atomic<int>  next{0};
+    std::atomic<bool> failed{false};
+    auto              work = [&] {
+        std::vector<uint8_t> px;
+        for (;;) {
+            int i = next.fetch_add(1);
+            if (i >= n) break;
+            int w, h, nc;
+            if (orc_jpeg_info(files[i], sizes[i], &w, &h, &nc) != 0) {
+                g_err  = orc_jpeg_last_error();
+                failed = true;
+                continue;
+            }
+            px.resize((size_t)w * h * lc->channels);
+            if (orc_jpeg_decode(files[i], sizes[i], lc->channels, px.data()) != 0) {
+                g_err  = orc_jpeg_last_error();
+                failed = true;
+                continue;
+            }
+            try {
+                Img o = transform_single_image(Img::view(px.data(), w, h, lc->channels, w * lc->channels), params[i]);
+                load_image(o, *lc, (char*)out + (size_t)i * item_bytes);
+            } catch (const std::exception& e) {
+                g_err  = e.what();
+                failed = true;
+            }
+        }
+    };
+    auto t0 = std::chrono::steady_clock::now();
+    std::vector<std::thread> pool;
+    for (int t = 0; t < std::max(1, threads); t++) pool.emplace_back(work);
+    for (auto& t : pool) t.join();
+    auto t1 = std::chrono::steady_clock::now();
+    if (failed) return -1.0;
+    return std::chrono::duration<double>(t1 - t0).count();
+}
+
 int orc_transpose(void* dest, const void* src, int64_t rows, int64_t cols, int element_size)
 {
     switch (element_size) {

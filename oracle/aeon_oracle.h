@@ -123,6 +123,9 @@ double orc_batch_image_mask(int n, const uint8_t* const* srcs, const uint8_t* co
 int         orc_jpeg_info(const uint8_t* data, size_t size, int* w, int* h, int* ncomp);
 int         orc_jpeg_decode(const uint8_t* data, size_t size, int channels, uint8_t* out);
 const char* orc_jpeg_last_error(void);
+/* the whole CPU path per record (extract -> transform -> load) over n JPEG files on a pool. */
+double orc_batch_decode_augment(int n, const uint8_t* const* files, const size_t* sizes, const orc_params* params,
+                                const orc_load_config* lc, void* out, size_t item_bytes, int threads);
 
 const char* orc_last_error(void);
 
