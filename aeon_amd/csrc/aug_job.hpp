@@ -92,6 +92,11 @@ struct LaunchArgs {
     int32_t        has_hue;    // some job of the launch shifts hue (HSV tables in LDS)
     int32_t        partial_stride; // (tile, wave) entries per contrast slot in `partials`
     int32_t        threads;    // workgroup size (kBlockMin..kBlockMax, a multiple of 64)
+    int32_t        has_rtab;   // LDS holds a per-record table (contrast -> lighting -> standardize)
+    // tail split: tiles from split_base on (the last, partial round of the persistent grid) are
+    // cut into split_parts row sub-tiles each, so every workgroup takes part in that round
+    int32_t        split_base;
+    int32_t        split_parts;
 };
 
 // KM_FINAL: a record through to the loader output.  KM_STATS: contrast pass 1 -- resize +
@@ -113,17 +118,19 @@ constexpr int kHsvWords = 512 + 256 * 4; // RGB2HSV division tables + HSV2RGB pe
 
 // LDS carve of one workgroup (bytes; every region 16-byte aligned, see the CDNA guide G17).
 struct LdsLayout {
-    int lut, hsv, xt, yt, pf, stage, stage_bytes, total;
+    int lut, hsv, rtab, xt, yt, pf, stage, stage_bytes, total;
 };
 // One or two staging buffers and copies of the tap tables (with two, the next tile's are filled
 // while the current tile is computed).  The HSV tables are reserved only for hue launches.  The LUT sits
 // at offset 0 so its per-channel reads use immediate LDS offsets.
-AEON_HD inline LdsLayout lds_layout(int max_win_w, int rows_per_tile, int stage_bytes, bool hue, int buffers)
+AEON_HD inline LdsLayout lds_layout(int max_win_w, int rows_per_tile, int stage_bytes, bool hue, int buffers,
+                                    bool rtab = false)
 {
     LdsLayout L;
     int       o = 0;
     L.lut = o; o += 3 * 256 * 4;                             // standardize LUT (source channel order)
     L.hsv = o; o += hue ? kHsvWords * 4 : 0;                 // sdiv / hdiv180 / HSV2RGB weights
+    L.rtab = o; o += rtab ? 3 * 256 * 4 : 0;                 // the tile's record table (f32, source channel order)
     L.xt  = o; o += buffers * ((max_win_w * 8 + 15) / 16) * 16; // per-column taps + weights
     L.yt  = o; o += buffers * rows_per_tile * 16;               // per-row taps + weights
     L.pf  = o; o += 256;                                     // LDS-DMA sink of job prefetches

@@ -365,10 +365,16 @@ __device__ __forceinline__ void stage_unpack(cjob& J, const StageGeom& G, int bu
 
 // Pull the job descriptor of a future tile into L2 (an LDS-DMA into a sink nobody reads): its
 // scalar loads then hit L2 instead of paying an HBM round trip at the head of that tile.
+// The whole tile a (possibly split, see Bands::info) launch tile index belongs to.
+__device__ __forceinline__ int whole_tile(const LaunchArgs& a, int t)
+{
+    return t >= a.split_base ? a.split_base + (t - a.split_base) / a.split_parts : t;
+}
+
 __device__ __forceinline__ void prefetch_job(const LaunchArgs& a, int t, int lds_sink)
 {
     if (t >= a.total_tiles) return;
-    const int      job  = t / a.max_tiles;
+    const int      job  = whole_tile(a, t) / a.max_tiles;
     const auto     rs   = uniform_rsrc((const void*)(a.jobs + job), (int)sizeof(AugJob));
     const uint32_t lane = threadIdx.x & 63;
     lds_dma<4>(rs, lds_sink, lane * 4 < sizeof(AugJob) ? lane * 4 : kOutOfRange);
@@ -524,15 +530,23 @@ struct Bands {
     __device__ __forceinline__ Info info(int t) const
     {
         Info f;
-        f.ok   = false;
+        f.ok       = false;
+        int part   = 0, parts = 1;
+        if (t >= a.split_base) { // a sub-tile of the last round (split_parts per tile)
+            parts = a.split_parts;
+            part  = (t - a.split_base) % parts;
+            t     = whole_tile(a, t);
+        }
         f.job  = t / a.max_tiles;
         f.band = t - f.job * a.max_tiles;
         cjob& J = job_ref(a, f.job);
         if (f.band >= J.tiles) return f;
         if (KM == KM_STATS && J.stats_slot < 0) return f;
-        const int TR = a.rows_per_tile;
-        f.y0         = f.band * TR;
-        f.nrows      = min(TR, J.win_h - f.y0);
+        const int TR  = a.rows_per_tile;
+        const int sub = (TR + parts - 1) / parts;
+        f.y0          = f.band * TR + part * sub;
+        f.nrows       = min(min(sub, TR - part * sub), J.win_h - f.y0);
+        if (f.nrows <= 0) return f; // a sub-tile past the end of a short last band
         // source columns (taps are monotone in dx)
         const XTap xf      = xcoef<RM>(J.win_x, J.scale_x, J.crop_w);
         const XTap xl      = xcoef<RM>(J.win_x + J.win_w - 1, J.scale_x, J.crop_w);
@@ -586,6 +600,35 @@ struct Bands {
         }
     }
 
+    // The per-channel tail of the record's chain -- contrast -> lighting -> standardize, each a
+    // function of one u8 channel value (image.cpp:336-346, 398-405, etl_image.cpp:316-339) -- as one
+    // 3 x 256 f32 table in LDS for the tile's record, so the pixel loop does one lookup per channel.
+    __device__ __forceinline__ bool uses_rtab(cjob& J) const
+    {
+        return KM == KM_FINAL && PHOTO && a.has_rtab && J.cn == 3 && (J.photo & (PHOTO_CONTRAST | PHOTO_LIGHTING));
+    }
+    __device__ __forceinline__ void record_table(const Info& f) const
+    {
+        if (!f.ok) return;
+        cjob& J = job_ref(a, f.job);
+        if (!uses_rtab(J)) return;
+        const int photo = J.photo;
+        double    sh[3] = {0, 0, 0};
+        if (photo & PHOTO_CONTRAST) {
+            const double* p = a.shifts + (size_t)J.stats_slot * 4;
+            sh[0] = p[0], sh[1] = p[1], sh[2] = p[2];
+        }
+        const float c = J.contrast, la = J.light_a;
+        const auto  rt = lds_ptr<float>(L.rtab);
+        for (int i = threadIdx.x; i < 3 * 256; i += blockDim.x) {
+            const int ch = i >> 8;
+            int       y  = i & 255;
+            if (photo & PHOTO_CONTRAST) y = u8rnd((float)((double)((float)y * c + 0.f) + sh[ch]));
+            if (photo & PHOTO_LIGHTING) y = sat_u8(u8rnd((float)y * la + 0.f) + J.light_add[ch]);
+            rt[i] = lut_at(ch, y << 2);
+        }
+    }
+
     __device__ __forceinline__ void unpack(const Info& f, int b) const
     {
         if (f.ok) stage_unpack(job_ref(a, f.job), f.G, L.stage + b * L.stage_bytes, wave, nw);
@@ -635,7 +678,8 @@ struct Bands {
         const bool active = lph < nph;
         // values carried from the resize to the store: 4x scaled (see resize_px) unless photometric
         constexpr bool SC = !PHOTO;
-        auto lut_of = [&](int c, int v) { return lut_at(c, SC ? v : v << 2); };
+        const bool     rtab = uses_rtab(J);
+        auto lut_of = [&](int c, int v) { return rtab ? lds_ldf(L.rtab + (c * 256 + v) * 4) : lut_at(c, SC ? v : v << 2); };
         auto u8_of  = [&](int v) { return SC ? v >> 2 : v; };
 
         for (int cg = active ? lcg : gpr; cg < gpr; cg += ncg) {
@@ -683,6 +727,10 @@ struct Bands {
                         if (photo & PHOTO_HUE) hue_apply(sdiv, hdiv, lds_ptr<const f32x4>(L.hsv + 2048), J.hue, bb, gg, rr);
                         if (KM == KM_STATS) { // the intermediate keeps the post-hue pixel
                             if (k < nk) sum0 += bb, sum1 += gg, sum2 += rr;
+                            val[k][0] = bb, val[k][1] = gg, val[k][2] = rr;
+                            continue;
+                        }
+                        if (rtab) { // contrast / lighting folded into the record table
                             val[k][0] = bb, val[k][1] = gg, val[k][2] = rr;
                             continue;
                         }
@@ -814,7 +862,8 @@ __global__ __launch_bounds__(kBlockMax, AEON_HIP_MIN_WAVES) void augment_tiles(L
     }
     const int       tid = threadIdx.x, nt = blockDim.x;
     const int       wave = __builtin_amdgcn_readfirstlane(tid >> 6), nw = nt >> 6;
-    const LdsLayout L = lds_layout(a.max_win_w, a.rows_per_tile, a.stage_bytes, PHOTO && a.has_hue, a.stage_buffers);
+    const LdsLayout L = lds_layout(a.max_win_w, a.rows_per_tile, a.stage_bytes, PHOTO && a.has_hue, a.stage_buffers,
+                                   a.has_rtab != 0);
     const Bands<KM, RM, PHOTO, OF, TAIL> W{a, L, wave, nw};
 
     // per-launch tables
@@ -826,6 +875,7 @@ __global__ __launch_bounds__(kBlockMax, AEON_HIP_MIN_WAVES) void augment_tiles(L
         const auto hsv = lds_ptr<int32_t>(L.hsv);
         for (int i = tid; i < kHsvWords; i += nt) hsv[i] = a.hsv_tables[i];
     }
+    if (KM == KM_FINAL && PHOTO && a.has_rtab) __syncthreads(); // record tables read the LUT
     // static schedule: tiles blockIdx.x, +G, +2G, ... -- the tiles in flight at any moment are
     // consecutive bands of a few records (measured faster than contiguous ranges per workgroup,
     // and than a counter-fed dynamic schedule: per-XCD ticket pools with stealing and smaller
@@ -857,6 +907,7 @@ __global__ __launch_bounds__(kBlockMax, AEON_HIP_MIN_WAVES) void augment_tiles(L
             W.issue(f, 0);
             stamp(it, 2);
             W.tables(f, 0, true);
+            W.record_table(f);
             stamp(it, 3);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             stamp(it, 4);

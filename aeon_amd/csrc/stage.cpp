@@ -129,6 +129,7 @@ struct LaunchPlan {
     int                 lds = 0, threads = kBlockMax;
     bool                vec_ok = true;
     bool                has_hue = false, has_contrast = false;
+    bool                rtab    = false; // final f32 launch with contrast / lighting: per-record LDS table
 
     // launch shape for this->jobs, and each job's tile count
     void finalize()
@@ -172,7 +173,7 @@ struct LaunchPlan {
         // lane: 42 vs 45 us (C2), 152/291 vs 186/370 us (C3 pass 2 / pass 1) -- the second
         // buffer costs occupancy and halves the rows per tile.  Knobs for experiments only.
         buffers    = 1;
-        if (const char* e = std::getenv("AEON_HIP_BUFFERS")) buffers = std::atoi(e) == 1 ? 1 : 2;
+        if (const char* e = std::getenv("AEON_HIP_BUFFERS")) buffers = std::atoi(e) == 1 || rtab ? 1 : 2;
         int tr_cap = std::min(64, std::max(1, (buffers == 1 ? 4 : 2) * nph));
         int budget = kStageBudget;
         if (const char* e = std::getenv("AEON_HIP_STAGE_KB")) budget = std::max(1, std::atoi(e)) * 1024;
@@ -202,7 +203,7 @@ struct LaunchPlan {
             budget = kStageBudgetHi;
         }
     chosen:
-        lds = lds_layout(max_win_w, tr, stage_bytes, photo && hue, buffers).total;
+        lds = lds_layout(max_win_w, tr, stage_bytes, photo && hue, buffers, rtab).total;
         if (lds > kMaxLds)
             fail(AEON_HIP_EUNSUPPORTED, "source crop too wide for LDS-staged row bands (" + std::to_string(lds) +
                                             " bytes)");
@@ -442,6 +443,12 @@ struct aeon_hip_ctx {
     bool                 device_plan = true; // AEON_HIP_DEVICE_PLAN=0: always plan on the host
     std::vector<JobGeom> geoms;              // reused per call
     JpegState*           jpeg = nullptr;     // JPEG decode stage (pool, staging ring), on first use
+    // overlap_contrast: a contrast batch runs as `overlap_chunks` chunks whose pass 2 (memory-bound)
+    // runs on side_stream beside the next chunk's pass 1 (VALU-bound), grids capped per CU
+    hipStream_t          side_stream    = nullptr;
+    hipEvent_t           join_event     = nullptr;
+    int                  overlap_chunks = 1, cap_pass1 = 2, cap_pass2 = 1; // off: measured slower
+    bool                 tail_split     = false; // AEON_HIP_TAIL_SPLIT=1: measured slower
     std::vector<int> open_slots; // used since the last completion event, on open_stream
     hipStream_t      open_stream = nullptr;
     // job tables go up on their own stream, so a call's H2D overlaps the previous call's kernels
@@ -578,11 +585,11 @@ double launch_bytes(const std::vector<J_>& jobs, int mode, size_t out_elem)
 }
 
 // Persistent grid: as many workgroups as the CUs hold at once, never more than the tiles.
-int grid_for(aeon_hip_ctx* ctx, int mode, const LaunchPlan& P, const LaunchArgs& a)
+int grid_for(aeon_hip_ctx* ctx, int mode, const LaunchPlan& P, const LaunchArgs& a, int cap = 0)
 {
     int per_cu = ctx->wg_per_cu;
     if (per_cu <= 0) {
-        const std::vector<int> key = {mode, P.rm, (int)P.tail, (int)P.photo, a.threads, a.lds_bytes, a.vec_ok,
+        const std::vector<int> key = {mode, P.rm, (int)P.tail, (int)P.photo, a.threads, a.lds_bytes, a.vec_ok, a.has_rtab,
                                       a.out_dtype, a.channel_major, a.stage_buffers};
         for (auto& e : ctx->occ)
             if (e.first == key) per_cu = e.second;
@@ -597,6 +604,7 @@ int grid_for(aeon_hip_ctx* ctx, int mode, const LaunchPlan& P, const LaunchArgs&
                              ctx->n_cu, a.total_tiles);
         }
     }
+    if (cap > 0) per_cu = std::min(per_cu, cap); // co-running launches share the CUs (overlap_contrast)
     return (int)std::min<long>((long)a.total_tiles, (long)per_cu * ctx->n_cu);
 }
 
@@ -625,12 +633,29 @@ KernelTimer take_timer(aeon_hip_ctx* ctx, int kind, double bytes)
     return t;
 }
 
-void timed_launch(aeon_hip_ctx* ctx, int mode, const LaunchPlan& P, const LaunchArgs& a, hipStream_t stream,
-                  double bytes, bool timed)
+void timed_launch(aeon_hip_ctx* ctx, int mode, const LaunchPlan& P, const LaunchArgs& a_in, hipStream_t stream,
+                  double bytes, bool timed, int cap = 0)
 {
     KernelTimer t{};
     if (timed) t = take_timer(ctx, mode, bytes);
-    HIP_OK(launch_tiles(mode, P.rm, P.tail, P.photo, a, grid_for(ctx, mode, P, a), stream, timed ? t.start : nullptr,
+    LaunchArgs a    = a_in;
+    const int  grid = grid_for(ctx, mode, P, a, cap);
+    // Tail split (final launches): T tiles on a grid of G workgroups leave a last round of
+    // T mod G tiles on as many workgroups while the rest of the grid idles; cutting each of those
+    // tiles into floor(G / (T mod G)) row sub-tiles spreads the round over the whole grid.  (Not for
+    // the contrast statistics pass: its partial sums are indexed by whole tiles.)
+    a.split_base  = a.total_tiles;
+    a.split_parts = 1;
+    const int rem = a.total_tiles % grid;
+    if (mode == KM_FINAL && ctx->tail_split && rem > 0 && a.total_tiles > grid) {
+        const int parts = std::min(grid / rem, a.rows_per_tile);
+        if (parts > 1) {
+            a.split_base  = a.total_tiles - rem;
+            a.split_parts = parts;
+            a.total_tiles = a.split_base + rem * parts;
+        }
+    }
+    HIP_OK(launch_tiles(mode, P.rm, P.tail, P.photo, a, grid, stream, timed ? t.start : nullptr,
                         timed ? t.stop : nullptr));
     if (timed) ctx->timers.push_back(t);
 }
@@ -684,6 +709,7 @@ LaunchArgs launch_args(aeon_hip_ctx* ctx, const Slot& s, const uint8_t* table, c
     a.lds_bytes     = L.lds;
     a.has_hue       = L.has_hue;
     a.threads       = L.threads;
+    a.has_rtab      = L.rtab;
     return a;
 }
 
@@ -731,6 +757,7 @@ bool run_direct(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void
     P.tail   = (key & 2) != 0;
     P.photo  = (key & 1) != 0;
     P.vec_ok = vec_ok;
+    P.rtab   = P.photo && o.dtype == AEON_DTYPE_F32;
     P.shape(geo);
     P.max_tiles = (max_h + P.tr - 1) / P.tr;
     phase(2);
@@ -759,9 +786,12 @@ bool run_direct(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void
     return true;
 }
 
+// stream2 (optional): the final launches (contrast_reduce + KM_FINAL) go there after an event on
+// the caller's stream, with the pass-1 / final grids capped at cap1 / cap2 workgroups per CU, so
+// this call's pass 2 can run beside the next call's pass 1 (overlap_contrast).
 int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* src_base,
               const aeon_aug_params* params, const aeon_out_desc* out, void* out_dev, void* stream_,
-              bool is_mask)
+              bool is_mask, hipStream_t stream2 = nullptr, int cap1 = 0, int cap2 = 0)
 {
     if (!ctx || n < 0 || (n > 0 && (!descs || !params || !out || !out_dev || !src_base)))
         fail(AEON_HIP_EINVAL, "null argument");
@@ -855,6 +885,7 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
         for (LaunchPlan& P : *v) {
             if (P.jobs.empty()) continue;
             P.vec_ok = main_all.vec_ok;
+            P.rtab   = v == &main && P.photo && o.dtype == AEON_DTYPE_F32;
             P.finalize();
             P.blob_off = blob;
             blob += P.jobs.size() * sizeof(AugJob);
@@ -926,14 +957,21 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
         for (LaunchPlan& P : *v)
             if (!P.jobs.empty()) timed_launch(ctx, KM_RAW, P, args(P), stream, launch_bytes(P.jobs, KM_RAW, 1), timed);
     for (LaunchPlan& P : pass1)
-        if (!P.jobs.empty()) timed_launch(ctx, KM_STATS, P, args(P), stream, launch_bytes(P.jobs, KM_STATS, oelem), timed);
+        if (!P.jobs.empty())
+            timed_launch(ctx, KM_STATS, P, args(P), stream, launch_bytes(P.jobs, KM_STATS, oelem), timed, cap1);
+    hipStream_t fs = stream;
+    if (stream2 && stream2 != stream) { // the final launches on stream2, after everything above
+        HIP_OK(hipEventRecord(s.copied, stream));
+        HIP_OK(hipStreamWaitEvent(stream2, s.copied, 0));
+        fs = stream2;
+    }
     for (LaunchPlan& P : main) {
         if (P.jobs.empty()) continue;
-        if (P.has_contrast) HIP_OK(launch_contrast_reduce(args(P), (int)P.jobs.size(), stream));
-        timed_launch(ctx, KM_FINAL, P, args(P), stream, launch_bytes(P.jobs, KM_FINAL, oelem), timed);
+        if (P.has_contrast) HIP_OK(launch_contrast_reduce(args(P), (int)P.jobs.size(), fs));
+        timed_launch(ctx, KM_FINAL, P, args(P), fs, launch_bytes(P.jobs, KM_FINAL, oelem), timed, cap2);
     }
     phase(6);
-    release_slot(ctx, slot, stream);
+    release_slot(ctx, slot, fs);
     phase(7);
     return 0;
 }
@@ -1016,6 +1054,12 @@ int aeon_hip_ctx_create(int device, aeon_hip_ctx** out)
             // the ring at the size a 512-record call needs (job tables of 128 KB), so steady-state
             // calls of that size never allocate
             ensure_ring(c, 128 * 1024, 64 * 1024, 8 * 1024);
+            HIP_OK(hipStreamCreateWithFlags(&c->side_stream, hipStreamNonBlocking));
+            HIP_OK(hipEventCreateWithFlags(&c->join_event, hipEventDisableTiming));
+            if (const char* e = std::getenv("AEON_HIP_OVERLAP_CHUNKS")) c->overlap_chunks = std::max(1, std::atoi(e));
+            if (const char* e = std::getenv("AEON_HIP_TAIL_SPLIT")) c->tail_split = std::atoi(e) != 0;
+            if (const char* e = std::getenv("AEON_HIP_CAP_PASS1")) c->cap_pass1 = std::max(0, std::atoi(e));
+            if (const char* e = std::getenv("AEON_HIP_CAP_PASS2")) c->cap_pass2 = std::max(0, std::atoi(e));
             if (const char* e = std::getenv("AEON_HIP_HOST_PROFILE")) c->host_profile = std::atoi(e) != 0;
             if (const char* e = std::getenv("AEON_HIP_JOBS")) c->jobs_mode = std::min(3, std::max(0, std::atoi(e)));
             if (const char* e = std::getenv("AEON_HIP_DEVICE_PLAN")) c->device_plan = std::atoi(e) != 0;
@@ -1070,6 +1114,8 @@ int aeon_hip_ctx_destroy(aeon_hip_ctx* c)
         for (auto* v : {&c->timers, &c->free_timers})
             for (KernelTimer& t : *v) (void)hipEventDestroy(t.start), (void)hipEventDestroy(t.stop);
         if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
+        if (c->side_stream) (void)hipStreamSynchronize(c->side_stream), (void)hipStreamDestroy(c->side_stream);
+        if (c->join_event) (void)hipEventDestroy(c->join_event);
         for (auto& L : c->luts) (void)hipFree(L.dev);
         if (c->d_error) (void)hipFree(c->d_error);
         if (c->d_hsv) (void)hipFree(c->d_hsv);
@@ -1103,7 +1149,24 @@ int aeon_hip_augment_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs,
                            const aeon_aug_params* params, const aeon_out_desc* out, void* out_dev,
                            void* stream)
 {
-    return guarded([&] { return run_batch(ctx, n, descs, src_base, params, out, out_dev, stream, false); });
+    return guarded([&] {
+        // contrast batches: chunks whose pass 2 overlaps the next chunk's pass 1 (overlap_contrast)
+        int with_contrast = 0;
+        for (int i = 0; ctx && params && i < n; i++) with_contrast += params[i].contrast != 1.0f;
+        const int chunks = ctx ? std::min(ctx->overlap_chunks, n / 64) : 1;
+        if (chunks < 2 || with_contrast * 2 < n || !out || !descs || !out_dev)
+            return run_batch(ctx, n, descs, src_base, params, out, out_dev, stream, false);
+        const int per = (n + chunks - 1) / chunks;
+        for (int a = 0; a < n; a += per)
+            run_batch(ctx, std::min(per, n - a), descs + a, src_base, params + a, out,
+                      (uint8_t*)out_dev + (size_t)a * out->item_stride, stream, false, ctx->side_stream,
+                      ctx->cap_pass1, ctx->cap_pass2);
+        // rejoin: everything of the call is ordered before later work on the caller's stream
+        std::lock_guard<std::mutex> lock(ctx->mu);
+        HIP_OK(hipEventRecord(ctx->join_event, ctx->side_stream));
+        HIP_OK(hipStreamWaitEvent((hipStream_t)stream, ctx->join_event, 0));
+        return 0;
+    });
 }
 
 int aeon_hip_mask_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* src_base,

@@ -356,6 +356,23 @@ def test_device_planner_matches_host_planner(ctx, monkeypatch, aug_name):
     _assert_same(dev, H.oracle_records(imgs, params, out), aug_name)
 
 
+def test_c3_chunked_overlap_matches_single_pass_schedule(ctx, monkeypatch):
+    """A contrast batch runs as chunks whose pass 2 (side stream) overlaps the next chunk's pass 1
+    (overlap_contrast): every record equals the unchunked schedule (AEON_HIP_OVERLAP_CHUNKS=1) and
+    the oracle; ragged sources, 3 chunks of 67 records."""
+    n = 200
+    imgs = _synthetic(n, ragged=True)
+    params = H.draw_params(C.C3_AUG, [(im.shape[1], im.shape[0]) for im in imgs], 224, 224, seed=31)
+    out = A.out_desc(**MEAN_OUT)
+    chunked = H.hip_records(ctx, imgs, params, out)
+    monkeypatch.setenv("AEON_HIP_OVERLAP_CHUNKS", "1")
+    one = A.Context(0)
+    single = H.hip_records(one, imgs, params, out)
+    one.close()
+    _assert_same(chunked, single, "C3 chunked vs single schedule")
+    _assert_same(chunked, H.oracle_records(imgs, params, out), "C3 chunked")
+
+
 def test_mask_rejects_standardize(ctx):
     """pixel_mask's loader never standardizes (etl_pixel_mask.cpp:94-105): refused either way."""
     m = A.synthetic_image(0, 64, 64, 1)
