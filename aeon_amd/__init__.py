@@ -24,6 +24,10 @@ AEON_HIP_EDEVICE = -4
 
 DTYPE_U8 = 0
 DTYPE_F32 = 1
+# output dtype name -> (AEON_DTYPE_* code, numpy type); aeon output_type uint32_t maps to int32 storage
+DTYPES = {"uint8": (0, np.uint8), "float32": (1, np.float32), "int8": (2, np.int8), "int16": (3, np.int16),
+          "uint16": (4, np.uint16), "int32": (5, np.int32), "float64": (6, np.float64)}
+NP_DTYPE = {code: t for code, t in DTYPES.values()}
 INTERP_LINEAR = 0
 INTERP_NEAREST = 1
 
@@ -229,7 +233,7 @@ def aug_params(**kw):
 
 def out_desc(channels=3, channel_major=True, bgr_to_rgb=False, dtype="float32", mean=None,
              stddev=None, item_stride=0, fixed_aspect_ratio=False, canvas=(0, 0)):
-    o = OutDesc(dtype=DTYPE_U8 if dtype == "uint8" else DTYPE_F32, channels=channels,
+    o = OutDesc(dtype=DTYPES[dtype][0], channels=channels,
                 channel_major=int(channel_major), bgr_to_rgb=int(bgr_to_rgb), has_mean=0,
                 item_stride=item_stride, fixed_aspect_ratio=int(fixed_aspect_ratio),
                 canvas_w=canvas[0], canvas_h=canvas[1])
@@ -371,7 +375,7 @@ class Decoder:
                                                        ctypes.byref(ib), ctypes.byref(dt)))
             self.outputs.append({"name": name.value.decode(), "shape": tuple(shape[:nd.value]),
                                  "item_bytes": ib.value,
-                                 "dtype": {DTYPE_U8: np.uint8, DTYPE_F32: np.float32}.get(dt.value)})
+                                 "dtype": NP_DTYPE.get(dt.value)})
 
     def close(self):
         if getattr(self, "_h", None):

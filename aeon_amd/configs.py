@@ -32,11 +32,14 @@ CONFIGS = {
 
 def out_desc_for(etl, aug, item_stride=None):
     """aeon image::config + param_factory mean/stddev -> aeon_amd.OutDesc."""
+    import numpy as np
+
     import aeon_amd as A
     cn = etl.get("channels", 3)
     otype = etl.get("output_type", "uint8_t")
-    dtype = {"float": "float32", "uint8_t": "uint8"}[otype]
-    esz = 4 if dtype == "float32" else 1
+    dtype = {"float": "float32", "uint8_t": "uint8", "int8_t": "int8", "char": "int8", "int16_t": "int16",
+             "uint16_t": "uint16", "int32_t": "int32", "uint32_t": "int32", "double": "float64"}[otype]
+    esz = np.dtype(A.NP_DTYPE[A.DTYPES[dtype][0]]).itemsize
     mean = aug.get("mean") if etl.get("type") == "image" else None
     std = aug.get("stddev") if etl.get("type") == "image" else None
     if item_stride is None:

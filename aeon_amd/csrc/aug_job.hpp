@@ -24,7 +24,16 @@ enum PhotoFlags : int32_t {
 
 enum BsKind : int32_t { BS_DIAG = 0, BS_FIXPT = 1, BS_FLOAT = 2 };
 
-enum OutDtype : int32_t { OUT_U8 = 0, OUT_F32 = 1 };
+// Output element types, AEON_DTYPE_* codes (aeon output_type -> cv type).
+enum OutDtype : int32_t { OUT_U8 = 0, OUT_F32 = 1, OUT_S8 = 2, OUT_S16 = 3, OUT_U16 = 4, OUT_S32 = 5, OUT_F64 = 6 };
+
+#if defined(__HIPCC__)
+__host__ __device__
+#endif
+inline int out_elem_bytes(int dt)
+{
+    return dt == OUT_U8 || dt == OUT_S8 ? 1 : (dt == OUT_S16 || dt == OUT_U16 ? 2 : (dt == OUT_F64 ? 8 : 4));
+}
 
 // 16-byte aligned, plain data (copied H2D as an array).
 struct alignas(16) AugJob {
@@ -97,6 +106,9 @@ struct LaunchArgs {
     // cut into split_parts row sub-tiles each, so every workgroup takes part in that round
     int32_t        split_base;
     int32_t        split_parts;
+    int32_t        u8_map;     // uint8 stores go through the LUT (fixed_aspect_ratio's uint8 standardize)
+    int32_t        has_mean;   // double output: standardize with smean / sinv (by SOURCE channel)
+    double         smean[3], sinv[3]; // sinv = 1/stddev, or 0 for stddev 0 (no division)
 };
 
 // KM_FINAL: a record through to the loader output.  KM_STATS: contrast pass 1 -- resize +

@@ -660,7 +660,7 @@ struct Bands {
         int      bs_kind = 0;
         if (PHOTO && (photo & PHOTO_BS)) bs_kind = J.bs_kind, bsr = bs_regs(J);
 
-        const int  elem  = (KM != KM_FINAL || a.out_dtype == OUT_U8) ? 1 : 4;
+        const int  elem  = KM != KM_FINAL ? 1 : out_elem_bytes(a.out_dtype);
         const int  plane = win_w * J.win_h;
         const int  obytes = (KM == KM_FINAL ? J.out_plane : plane) * cn * elem;
         const auto orsrc = __builtin_amdgcn_make_buffer_rsrc((void*)J.out_ptr, (short)0, obytes, 0x00020000);
@@ -681,6 +681,9 @@ struct Bands {
         const bool     rtab = uses_rtab(J);
         auto lut_of = [&](int c, int v) { return rtab ? lds_ldf(L.rtab + (c * 256 + v) * 4) : lut_at(c, SC ? v : v << 2); };
         auto u8_of  = [&](int v) { return SC ? v >> 2 : v; };
+        // uint8 output value of source channel c: the plain byte, or its fixed_aspect_ratio
+        // uint8 standardize through the LUT
+        auto u8_out = [&](int c, int v) { return a.u8_map ? (int)lut_of(c, v) : u8_of(v); };
 
         for (int cg = active ? lcg : gpr; cg < gpr; cg += ncg) {
             const int ox0 = cg * 4;
@@ -793,7 +796,7 @@ struct Bands {
                     }
                     continue;
                 }
-                if (a.out_dtype != OUT_F32 && (a.channel_major || cn == 1) && nk == 4) {
+                if (a.out_dtype == OUT_U8 && (a.channel_major || cn == 1) && nk == 4) {
                     // uint8 planes (pixel masks, uint8 images): a lane's 4 consecutive output
                     // bytes of a plane as one dword store when the 4-byte group is aligned
 #pragma unroll
@@ -801,8 +804,8 @@ struct Bands {
                         if (c >= cn) break;
                         const int oc = bgr ? 2 - c : c;
                         const int i0 = (cn == 1 ? 0 : oc * J.out_plane) + y * J.out_pitch + ox0;
-                        const uint32_t w = ((uint32_t)u8_of(val[0][c]) & 0xff) | (((uint32_t)u8_of(val[1][c]) & 0xff) << 8) |
-                                           (((uint32_t)u8_of(val[2][c]) & 0xff) << 16) | ((uint32_t)u8_of(val[3][c]) << 24);
+                        const uint32_t w = ((uint32_t)u8_out(c, val[0][c]) & 0xff) | (((uint32_t)u8_out(c, val[1][c]) & 0xff) << 8) |
+                                           (((uint32_t)u8_out(c, val[2][c]) & 0xff) << 16) | ((uint32_t)u8_out(c, val[3][c]) << 24);
                         if ((i0 & 3) == 0) {
                             __builtin_amdgcn_raw_buffer_store_b32(w, orsrc, i0, 0, kStoreAux);
                         } else {
@@ -822,11 +825,38 @@ struct Bands {
                         if (k >= nk) break;
                         const int i = a.channel_major ? oc * J.out_plane + y * J.out_pitch + ox0 + k
                                                       : (y * J.out_pitch + ox0 + k) * cn + oc;
-                        if (a.out_dtype == OUT_F32)
-                            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(lut_of(c, val[k][c])), orsrc,
-                                                                  i * 4, 0, kStoreAux);
-                        else
-                            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)u8_of(val[k][c]), orsrc, i, 0, kStoreAux);
+                        // image::loader (convert_mix_channels: Mat::convertTo of the uint8 record,
+                        // saturating; standardize for float / double)
+                        const int v = u8_of(val[k][c]);
+                        switch (a.out_dtype) {
+                        case OUT_F32:
+                            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(lut_of(c, val[k][c])), orsrc, i * 4, 0,
+                                                                  kStoreAux);
+                            break;
+                        case OUT_F64: { // CV_64F standardize: every op in double (image.cpp:129-174)
+                            double d = (double)v;
+                            if (a.has_mean) {
+                                d = d * (1. / 255.) - a.smean[c];
+                                if (a.sinv[c] != 0) d = d * a.sinv[c];
+                            }
+                            const uint64_t bits = __double_as_longlong(d);
+                            __builtin_amdgcn_raw_buffer_store_b64((u32x2){(uint32_t)bits, (uint32_t)(bits >> 32)}, orsrc,
+                                                                  i * 8, 0, kStoreAux);
+                            break;
+                        }
+                        case OUT_S8:
+                            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)min(v, 127), orsrc, i, 0, kStoreAux);
+                            break;
+                        case OUT_S16:
+                        case OUT_U16:
+                            __builtin_amdgcn_raw_buffer_store_b16((uint16_t)v, orsrc, i * 2, 0, kStoreAux);
+                            break;
+                        case OUT_S32:
+                            __builtin_amdgcn_raw_buffer_store_b32((uint32_t)v, orsrc, i * 4, 0, kStoreAux);
+                            break;
+                        default:
+                            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)u8_out(c, val[k][c]), orsrc, i, 0, kStoreAux);
+                        }
                     }
                 }
             }
@@ -867,7 +897,7 @@ __global__ __launch_bounds__(kBlockMax, AEON_HIP_MIN_WAVES) void augment_tiles(L
     const Bands<KM, RM, PHOTO, OF, TAIL> W{a, L, wave, nw};
 
     // per-launch tables
-    if (KM == KM_FINAL && a.out_dtype == OUT_F32) {
+    if (KM == KM_FINAL && (a.out_dtype == OUT_F32 || a.u8_map)) {
         const auto lut = lds_ptr<float>(L.lut);
         for (int i = tid; i < 3 * 256; i += nt) lut[i] = a.lut[i];
     }

@@ -88,10 +88,11 @@ Json without_type(const Json& j, std::string& type)
 // ---- typemap -------------------------------------------------------------------------------
 output_type::output_type(const std::string& n) : name(n)
 {
+    // typemap.hpp:43-52 (name -> cv type): the loader's convertTo target
     static const std::map<std::string, std::pair<size_t, int>> all{
-        {"int8_t", {1, -1}},  {"uint8_t", {1, AEON_DTYPE_U8}}, {"int16_t", {2, -1}},
-        {"uint16_t", {2, -1}}, {"int32_t", {4, -1}}, {"uint32_t", {4, -1}},
-        {"float", {4, AEON_DTYPE_F32}}, {"double", {8, -1}}, {"char", {1, -1}}};
+        {"int8_t", {1, AEON_DTYPE_S8}},    {"uint8_t", {1, AEON_DTYPE_U8}},  {"int16_t", {2, AEON_DTYPE_S16}},
+        {"uint16_t", {2, AEON_DTYPE_U16}}, {"int32_t", {4, AEON_DTYPE_S32}}, {"uint32_t", {4, AEON_DTYPE_S32}},
+        {"float", {4, AEON_DTYPE_F32}},    {"double", {8, AEON_DTYPE_F64}},  {"char", {1, AEON_DTYPE_S8}}};
     auto it = all.find(n);
     if (it == all.end()) throw std::runtime_error("Unable to map output type " + n);
     size  = it->second.first;
@@ -185,11 +186,6 @@ public:
             if (mean.size() != m_cfg.channels || std_.size() != m_cfg.channels)
                 invalid("Size of 'mean' and 'stddev' must be equal to number of channels or empty.");
         }
-        if (m_factory.fixed_aspect_ratio && m_cfg.shape.otype.dtype != AEON_DTYPE_U8)
-            throw std::runtime_error("fixed_aspect_ratio is implemented for uint8_t output only in the HIP stage");
-        if (m_cfg.shape.otype.dtype < 0)
-            throw std::runtime_error("output_type '" + m_cfg.output_type_name +
-                                     "' is not implemented in the HIP stage (uint8_t, float)");
     }
     void provide(int, const decoded_element& in, augmentation& aug, std::minstd_rand0& random,
                  aeon_aug_params& params) const override
@@ -231,12 +227,6 @@ public:
     pixelmask_provider(const Json& js, const Json& aug)
         : m_cfg(js), m_factory(aug), m_name(create_name(m_cfg.name, "pixelmask"))
     {
-        if (m_cfg.shape.otype.dtype < 0)
-            throw std::runtime_error("output_type '" + m_cfg.output_type_name +
-                                     "' is not implemented in the HIP stage (uint8_t, float)");
-        // the image::loader it shares (provider.cpp:359) takes the augmentation's fixed_aspect_ratio
-        if (m_factory.fixed_aspect_ratio && m_cfg.shape.otype.dtype != AEON_DTYPE_U8)
-            throw std::runtime_error("fixed_aspect_ratio is implemented for uint8_t output only in the HIP stage");
     }
     void provide(int, const decoded_element& in, augmentation& aug, std::minstd_rand0& random,
                  aeon_aug_params& params) const override

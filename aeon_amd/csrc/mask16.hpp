@@ -15,7 +15,7 @@ struct alignas(16) Mask16Job {
     int32_t  out_w, out_h, out_pitch; // output size; elements per output row (canvas width
                                       // with fixed_aspect_ratio)
     int32_t  flip;
-    int32_t  dtype;                   // 0 = uint8 (saturate), 1 = float32
+    int32_t  dtype;                   // OutDtype (AEON_DTYPE_*): saturating convertTo
     int32_t  src_elem;                // bytes per source element: 1 (CV_8U) or 2 (CV_16U)
     int32_t  pad_;
 };

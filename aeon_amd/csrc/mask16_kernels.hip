@@ -19,6 +19,7 @@
 #include <algorithm>
 #include <cstdlib>
 
+#include "aug_job.hpp"
 #include "mask16.hpp"
 
 namespace aeon_hip {
@@ -27,7 +28,20 @@ namespace aeon_hip {
 // store when the destination is aligned, element stores otherwise
 __device__ __forceinline__ void store4(const Mask16Job& J, size_t o, int nk, const uint32_t v[4])
 {
-    if (J.dtype == 1) {
+    if (J.dtype != OUT_U8 && J.dtype != OUT_F32) { // the other convertTo targets, element by element
+        for (int k = 0; k < nk; k++) {
+            const uint32_t x = v[k];
+            switch (J.dtype) {
+            case OUT_S8: ((int8_t*)J.out_ptr)[o + k] = (int8_t)min(x, 127u); break;
+            case OUT_S16: ((int16_t*)J.out_ptr)[o + k] = (int16_t)min(x, 32767u); break;
+            case OUT_U16: ((uint16_t*)J.out_ptr)[o + k] = (uint16_t)x; break;
+            case OUT_S32: ((int32_t*)J.out_ptr)[o + k] = (int32_t)x; break;
+            default: ((double*)J.out_ptr)[o + k] = (double)x; break; // OUT_F64
+            }
+        }
+        return;
+    }
+    if (J.dtype == OUT_F32) {
         typedef float f32x4 __attribute__((ext_vector_type(4)));
         float* dst = (float*)J.out_ptr + o;
         if (nk == 4 && ((uintptr_t)dst & 15) == 0) {

@@ -70,8 +70,29 @@ constexpr size_t kUploadKernelMax = 128 * 1024; // job tables above this go up b
 
 // image::standardize arithmetic (src/image.cpp:129-174 over OpenCV 2.4 arithm_op: f64 work
 // type per op, rounded to f32 after each op) tabulated per channel and input value.
-void build_lut(const aeon_out_desc& o, float* lut)
+void build_lut(const aeon_out_desc& o, float* lut, bool u8_map = false)
 {
+    if (u8_map) {
+        // fixed_aspect_ratio's in-place standardize of its uint8 canvas (etl_image.cpp:263-300 ->
+        // image.cpp:129-174 on CV_8U planes): OpenCV 2.4 arithm_op on 8U -- multiply(1/255.) in
+        // double, subtract the mean converted to int (cvRound, add/sub rule), multiply(1/stddev)
+        // in double -- each saturated to uint8
+        for (int c = 0; c < 3; c++) {
+            const int oc = (o.bgr_to_rgb && o.channels == 3) ? 2 - c : c;
+            for (int x = 0; x < 256; x++) {
+                if (oc >= o.channels) {
+                    lut[c * 256 + x] = (float)x;
+                    continue;
+                }
+                auto sat = [](int v) { return std::min(std::max(v, 0), 255); };
+                int  a   = sat(cv_round((double)x * (1. / 255.)));
+                a        = sat(a - cv_round(o.mean[oc]));
+                if (o.stddev[oc] != 0) a = sat(cv_round((double)a * (1. / o.stddev[oc])));
+                lut[c * 256 + x] = (float)a;
+            }
+        }
+        return;
+    }
     // indexed by SOURCE channel c; its value lands in output channel oc (mixChannels
     // from_to {0,2,1,1,2,0} when bgr_to_rgb), standardized with that channel's mean/stddev
     for (int c = 0; c < 3; c++) {
@@ -246,7 +267,7 @@ void plan_mask16(const aeon_img_desc& d, const void* src_base, const aeon_aug_pa
         fail(AEON_HIP_EINVAL, eb == 2 ? "invalid 16-bit source image descriptor" : "invalid source image descriptor");
     if (p.angle != 0) fail(AEON_HIP_EUNSUPPORTED, "rotation of 16-bit masks is not implemented");
     if (p.out_w <= 0 || p.out_h <= 0) fail(AEON_HIP_EINVAL, "invalid output size");
-    const size_t elem = o.dtype == AEON_DTYPE_F32 ? 4 : 1;
+    const size_t elem = out_elem_bytes(o.dtype);
     if ((size_t)p.out_w * p.out_h * elem > o.item_stride) fail(AEON_HIP_EINVAL, "output item does not fit item_stride");
     if (o.fixed_aspect_ratio && (p.out_w > o.canvas_w || p.out_h > o.canvas_h))
         fail(AEON_HIP_EINVAL, "fixed_aspect_ratio: output_size larger than the image canvas");
@@ -263,7 +284,7 @@ void plan_mask16(const aeon_img_desc& d, const void* src_base, const aeon_aug_pa
     M.out_w = p.out_w, M.out_h = p.out_h;
     M.out_pitch = o.fixed_aspect_ratio ? o.canvas_w : p.out_w;
     M.flip      = p.flip ? 1 : 0;
-    M.dtype     = o.dtype == AEON_DTYPE_F32 ? 1 : 0;
+    M.dtype     = o.dtype;
     M.src_elem  = eb;
     m16.push_back(M);
 }
@@ -280,7 +301,7 @@ void validate_record(const aeon_img_desc& d, const aeon_aug_params& p, const aeo
     if (interp != AEON_INTERP_LINEAR && interp != AEON_INTERP_NEAREST)
         fail(AEON_HIP_EUNSUPPORTED, "only LINEAR and NEAREST interpolation are implemented");
     if (p.out_w <= 0 || p.out_h <= 0) fail(AEON_HIP_EINVAL, "invalid output size");
-    const size_t elem = o.dtype == AEON_DTYPE_F32 ? 4 : 1;
+    const size_t elem = out_elem_bytes(o.dtype);
     if ((size_t)p.out_w * p.out_h * cn * elem > o.item_stride)
         fail(AEON_HIP_EINVAL, "output item does not fit item_stride");
     if (o.fixed_aspect_ratio && (p.out_w > o.canvas_w || p.out_h > o.canvas_h))
@@ -547,10 +568,10 @@ void ensure_ring(aeon_hip_ctx* ctx, size_t table, size_t partials, size_t shifts
 }
 
 // Device copy of the standardize LUT of output config `o` (uploaded the first time it is seen).
-const float* resident_lut(aeon_hip_ctx* ctx, const aeon_out_desc& o)
+const float* resident_lut(aeon_hip_ctx* ctx, const aeon_out_desc& o, bool u8_map = false)
 {
     float lut[768];
-    build_lut(o, lut);
+    build_lut(o, lut, u8_map);
     for (auto& L : ctx->luts)
         if (std::memcmp(L.host, lut, sizeof(lut)) == 0) return L.dev;
     if (ctx->luts.size() >= 16) { // many configs on one context: start over once the device is idle
@@ -684,8 +705,27 @@ void release_slot(aeon_hip_ctx* ctx, int index, hipStream_t stream)
     ctx->host_calls++;
 }
 
+// The loader side of a launch: ko = what the kernels write (fixed_aspect_ratio writes its uint8
+// canvas whatever the declared type, u8_map = standardized through the LUT); double output
+// standardizes in the kernel with the declared mean / stddev by source channel.
+struct OutView {
+    aeon_out_desc ko;
+    bool          u8_map = false;
+};
+OutView out_view(const aeon_out_desc& o)
+{
+    OutView v;
+    v.ko = o;
+    if (o.fixed_aspect_ratio && o.dtype != AEON_DTYPE_U8) {
+        v.ko.dtype    = AEON_DTYPE_U8;
+        v.ko.has_mean = 0;
+        v.u8_map      = o.has_mean != 0;
+    }
+    return v;
+}
+
 LaunchArgs launch_args(aeon_hip_ctx* ctx, const Slot& s, const uint8_t* table, const LaunchPlan& L, int n_jobs,
-                       const aeon_out_desc& o, const float* d_lut, int partial_stride)
+                       const aeon_out_desc& o, const float* d_lut, int partial_stride, bool u8_map = false)
 {
     LaunchArgs a{};
     a.jobs           = (const AugJob*)(table + L.blob_off);
@@ -702,7 +742,14 @@ LaunchArgs launch_args(aeon_hip_ctx* ctx, const Slot& s, const uint8_t* table, c
     a.stage_bytes   = L.stage_bytes;
     a.stage_buffers = L.buffers;
     a.max_win_w     = L.max_win_w;
-    a.out_dtype     = o.dtype == AEON_DTYPE_F32 ? OUT_F32 : OUT_U8;
+    a.out_dtype     = o.dtype;
+    a.u8_map        = u8_map;
+    a.has_mean      = o.has_mean;
+    for (int c = 0; c < 3; c++) { // by source channel (mixChannels from_to {0,2,1,1,2,0} with bgr_to_rgb)
+        const int oc = (o.bgr_to_rgb && o.channels == 3) ? 2 - c : c;
+        a.smean[c]   = oc < o.channels ? o.mean[oc] : 0;
+        a.sinv[c]    = oc < o.channels && o.stddev[oc] != 0 ? 1. / o.stddev[oc] : 0;
+    }
     a.channel_major = o.channel_major;
     a.bgr_to_rgb    = o.bgr_to_rgb;
     a.vec_ok        = L.vec_ok && o.channel_major;
@@ -722,9 +769,11 @@ LaunchArgs launch_args(aeon_hip_ctx* ctx, const Slot& s, const uint8_t* table, c
 // passes, 2x-area + photometric, the mask gather pass, or records of several launch groups.
 template <typename Phase>
 bool run_direct(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* src_base,
-                const aeon_aug_params* params, const aeon_out_desc& o, void* out_dev, hipStream_t stream,
+                const aeon_aug_params* params, const aeon_out_desc& od, void* out_dev, hipStream_t stream,
                 bool is_mask, Phase&& phase)
 {
+    const OutView        ov = out_view(od);
+    const aeon_out_desc& o  = ov.ko; // what the kernels write
     std::vector<JobGeom>& geo = ctx->geoms;
     geo.resize(n);
     int  key = -1, max_h = 0;
@@ -764,7 +813,7 @@ bool run_direct(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void
     int         slot;
     Slot&       s     = take_slot(ctx, stream, slot);
     phase(3);
-    const float* d_lut = resident_lut(ctx, o);
+    const float* d_lut = resident_lut(ctx, od, ov.u8_map);
     ensure_ring(ctx, (size_t)n * sizeof(AugJob), 16, 32);
     PlanRecord* R = (PlanRecord*)s.host;
     for (int i = 0; i < n; i++) {
@@ -776,10 +825,11 @@ bool run_direct(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void
     HIP_OK(launch_plan_records(s.host_dev, s.dev, pa, stream));
     phase(5);
     const bool timed = ctx->timing && (ctx->timing_calls++ % ctx->timing_every) == 0;
-    if (o.fixed_aspect_ratio) // std::fill_n of each item's canvas (etl_image.cpp:263)
-        HIP_OK(hipMemset2DAsync(out_dev, o.item_stride, 0, (size_t)o.canvas_w * o.canvas_h * o.channels, n, stream));
-    timed_launch(ctx, KM_FINAL, P, launch_args(ctx, s, s.dev, P, n, o, d_lut, 1), stream,
-                 launch_bytes(geo, KM_FINAL, o.dtype == AEON_DTYPE_F32 ? 4 : 1), timed);
+    if (o.fixed_aspect_ratio) // std::fill_n of each item's canvas, its whole byte size (etl_image.cpp:263)
+        HIP_OK(hipMemset2DAsync(out_dev, o.item_stride, 0,
+                                (size_t)o.canvas_w * o.canvas_h * o.channels * out_elem_bytes(od.dtype), n, stream));
+    timed_launch(ctx, KM_FINAL, P, launch_args(ctx, s, s.dev, P, n, o, d_lut, 1, ov.u8_map), stream,
+                 launch_bytes(geo, KM_FINAL, out_elem_bytes(o.dtype)), timed);
     phase(6);
     release_slot(ctx, slot, stream);
     phase(7);
@@ -797,25 +847,24 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
         fail(AEON_HIP_EINVAL, "null argument");
     if (n == 0) return 0;
     if (n > 65535) fail(AEON_HIP_EINVAL, "at most 65535 records per call");
-    const aeon_out_desc& o = *out;
-    if (o.dtype != AEON_DTYPE_U8 && o.dtype != AEON_DTYPE_F32)
-        fail(AEON_HIP_EUNSUPPORTED, "output dtype must be uint8 or float32");
-    if (o.has_mean && o.dtype != AEON_DTYPE_F32)
+    const aeon_out_desc& od = *out; // as declared; `o` below is what the kernels write (out_view)
+    if (od.dtype < AEON_DTYPE_U8 || od.dtype > AEON_DTYPE_F64) fail(AEON_HIP_EUNSUPPORTED, "unknown output dtype");
+    if (od.has_mean && od.dtype != AEON_DTYPE_F32 && od.dtype != AEON_DTYPE_F64)
         fail(AEON_HIP_EINVAL,
              "Standardization (mean, stddev) is supported only for float or double 'output_type'.");
+    const OutView        ov = out_view(od);
+    const aeon_out_desc& o  = ov.ko;
     if (o.bgr_to_rgb && o.channels != 3)
         fail(AEON_HIP_EINVAL, "invalid config: bgr_to_rgb can be 'true' only for channels set to '3'");
     // pixel_mask / depthmap loaders never standardize or swap channels (etl_pixel_mask.cpp:94-105,
     // etl_depthmap.cpp:98-134): refuse both, so rotated and unrotated masks agree
-    if (is_mask && (o.has_mean || o.bgr_to_rgb))
+    if (is_mask && (od.has_mean || od.bgr_to_rgb))
         fail(AEON_HIP_EINVAL, "pixel masks / depth maps take no mean/stddev and no bgr_to_rgb");
-    if (o.fixed_aspect_ratio) {
-        // aeon's fixed-aspect loader views the canvas as CV_8U planes whatever the output type
-        // (etl_image.cpp:263-305), so only uint8 output has a meaningful layout
-        if (o.dtype != AEON_DTYPE_U8)
-            fail(AEON_HIP_EUNSUPPORTED, "fixed_aspect_ratio is implemented for uint8_t output only (aeon's "
-                                        "loader writes uint8 pixels into the canvas)");
-        if (o.canvas_w <= 0 || o.canvas_h <= 0 || (size_t)o.canvas_w * o.canvas_h * o.channels > o.item_stride)
+    if (od.fixed_aspect_ratio) {
+        // aeon's fixed-aspect loader zeroes the item's whole byte size and views the canvas as
+        // CV_8U planes whatever the output type (etl_image.cpp:263-305): out_view
+        if (od.canvas_w <= 0 || od.canvas_h <= 0 ||
+            (size_t)od.canvas_w * od.canvas_h * od.channels * out_elem_bytes(od.dtype) > od.item_stride)
             fail(AEON_HIP_EINVAL, "fixed_aspect_ratio: canvas does not fit item_stride");
     }
     hipStream_t stream = (hipStream_t)stream_;
@@ -832,7 +881,7 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
     HIP_OK(hipSetDevice(ctx->device));
     phase(0);
     if (ctx->device_plan && ctx->jobs_mode < 0 &&
-        run_direct(ctx, n, descs, src_base, params, o, out_dev, stream, is_mask, phase))
+        run_direct(ctx, n, descs, src_base, params, od, out_dev, stream, is_mask, phase))
         return 0;
 
     LaunchPlan             pre_all, pre2_all, pass1_all, main_all;
@@ -904,7 +953,7 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
     int   slot;
     Slot& s = take_slot(ctx, stream, slot);
     phase(3);
-    const float* d_lut = resident_lut(ctx, o);
+    const float* d_lut = resident_lut(ctx, od, ov.u8_map);
     // job tables, contrast sums and shifts: one capacity for every slot of the ring (a call never
     // allocates unless it needs more than any call before it); scratch per slot, on demand
     ensure_ring(ctx, blob, partial_words * 4, std::max<size_t>(1, pass1_all.jobs.size()) * 4 * sizeof(double));
@@ -937,13 +986,14 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
     phase(5);
 
     auto args = [&](const LaunchPlan& L) {
-        return launch_args(ctx, s, table, L, (int)L.jobs.size(), o, d_lut, partial_stride);
+        return launch_args(ctx, s, table, L, (int)L.jobs.size(), o, d_lut, partial_stride, ov.u8_map);
     };
-    const size_t oelem = o.dtype == AEON_DTYPE_F32 ? 4 : 1;
+    const size_t oelem = out_elem_bytes(o.dtype);
     // timing events on one call in timing_every (each event pair costs GPU time between launches)
     const bool timed = ctx->timing && (ctx->timing_calls++ % ctx->timing_every) == 0;
-    if (o.fixed_aspect_ratio) // std::fill_n of each item's canvas (etl_image.cpp:263)
-        HIP_OK(hipMemset2DAsync(out_dev, o.item_stride, 0, (size_t)o.canvas_w * o.canvas_h * o.channels, n, stream));
+    if (o.fixed_aspect_ratio) // std::fill_n of each item's canvas, its whole byte size (etl_image.cpp:263)
+        HIP_OK(hipMemset2DAsync(out_dev, o.item_stride, 0,
+                                (size_t)o.canvas_w * o.canvas_h * o.channels * out_elem_bytes(od.dtype), n, stream));
     if (!m16.empty()) {
         KernelTimer t{};
         if (timed) t = take_timer(ctx, KM_FINAL, m16_bytes);

@@ -31,9 +31,15 @@ extern "C" {
 #define AEON_HIP_EUNSUPPORTED -3 /* a feature this build does not implement (e.g. rotation) */
 #define AEON_HIP_EDEVICE -4    /* a kernel reported an inconsistency in its device error word */
 
-/* output element types (aeon output_type, src/typemap.hpp) */
-#define AEON_DTYPE_U8 0
-#define AEON_DTYPE_F32 1
+/* output element types (aeon output_type -> cv type, src/typemap.hpp:43-52); the loader converts the
+ * uint8 record with Mat::convertTo (saturating) and standardizes float / double outputs */
+#define AEON_DTYPE_U8 0  /* uint8_t  (CV_8U) */
+#define AEON_DTYPE_F32 1 /* float    (CV_32F) */
+#define AEON_DTYPE_S8 2  /* int8_t, char (CV_8S) */
+#define AEON_DTYPE_S16 3 /* int16_t  (CV_16S) */
+#define AEON_DTYPE_U16 4 /* uint16_t (CV_16U) */
+#define AEON_DTYPE_S32 5 /* int32_t, uint32_t (CV_32S) */
+#define AEON_DTYPE_F64 6 /* double   (CV_64F) */
 
 /* resize interpolation (image::config "interpolation_method") */
 #define AEON_INTERP_LINEAR 0
@@ -80,10 +86,12 @@ typedef struct aeon_out_desc {
     int32_t  channels;      /* 1 or 3 */
     int32_t  channel_major; /* 1: CHW planes, 0: HWC */
     int32_t  bgr_to_rgb;    /* swap channels 0 and 2 (3-channel only) */
-    int32_t  has_mean;      /* standardize with mean/stddev (float output only) */
+    int32_t  has_mean;      /* standardize with mean/stddev (float / double output only) */
     int32_t  fixed_aspect_ratio; /* image::loader m_fixed_aspect_ratio (etl_image.cpp:258-306):
-                                  * each item is a zeroed canvas_w x canvas_h canvas with the
-                                  * record written at its top-left; uint8 output only */
+                                  * each item (its whole dtype-sized byte size) is zeroed and the
+                                  * record is written at the top-left of a canvas_w x canvas_h
+                                  * canvas viewed as CV_8U planes, whatever the dtype, standardized
+                                  * in place as uint8 when mean/stddev are set -- aeon's layout */
     double   mean[3];
     double   stddev[3];
     uint64_t item_stride;   /* bytes between consecutive items of the batch buffer */

@@ -95,6 +95,7 @@ def lib():
                                     ctypes.c_float, ctypes.c_float, ctypes.c_int]
         L.orc_lighting.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, P(ctypes.c_float),
                                    ctypes.c_int, ctypes.c_float]
+        L.orc_u8_standardize_value.argtypes = [ctypes.c_int, ctypes.c_double, ctypes.c_double]
         L.orc_standardize_value.restype = ctypes.c_float
         L.orc_standardize_value.argtypes = [ctypes.c_int, ctypes.c_double, ctypes.c_double]
         L.orc_batch_augment.restype = ctypes.c_double
@@ -219,10 +220,15 @@ def transform_image(src, p):
     return out
 
 
+DTYPES = {"uint8": (0, np.uint8), "float32": (1, np.float32), "int8": (2, np.int8), "int16": (3, np.int16),
+          "uint16": (4, np.uint16), "int32": (5, np.int32), "float64": (6, np.float64)}
+NP_OF = {code: t for code, t in DTYPES.values()}
+
+
 def load_config(channels=3, channel_major=True, bgr_to_rgb=False, out_dtype="float32",
                 mean=None, stddev=None):
     lc = LoadConfig(channels=channels, channel_major=int(channel_major), bgr_to_rgb=int(bgr_to_rgb),
-                    out_dtype=0 if out_dtype == "uint8" else 1, has_mean=0)
+                    out_dtype=DTYPES[out_dtype][0], has_mean=0)
     if mean is not None:
         lc.has_mean = 1
         for i in range(channels):
@@ -234,7 +240,7 @@ def load_config(channels=3, channel_major=True, bgr_to_rgb=False, out_dtype="flo
 def load_image(img, lc):
     img = np.ascontiguousarray(img, dtype=np.uint8)
     h, w = img.shape[:2]
-    dt = np.uint8 if lc.out_dtype == 0 else np.float32
+    dt = NP_OF[lc.out_dtype]
     shape = (lc.channels, h, w) if lc.channel_major else (h, w, lc.channels)
     out = np.zeros(shape, dt)
     _check(lib().orc_load_image(img.ctypes.data, w, h, ctypes.byref(lc), out.ctypes.data))
@@ -285,6 +291,11 @@ def lighting(img, alphas, sigma):
 def augment_record(src, p, lc):
     """transform_single_image + loader::load for one record."""
     return load_image(transform_image(src, p), lc)
+
+
+def u8_standardize(x, mean, stddev):
+    """uint8 result of standardizing a CV_8U canvas value x (fixed_aspect_ratio loader)."""
+    return lib().orc_u8_standardize_value(int(x), mean, stddev)
 
 
 def batch_augment(srcs, params_list, lc, item_shape, threads):

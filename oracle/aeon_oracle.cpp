@@ -696,12 +696,27 @@ void load_image(const Img& img, const orc_load_config& lc, void* out)
                 int    v   = p[x * cn + sc];
                 size_t idx = lc.channel_major ? (size_t)oc * plane + (size_t)y * w + x
                                               : ((size_t)y * w + x) * cn + oc;
-                if (lc.out_dtype == 0) {
-                    ((uint8_t*)out)[idx] = (uint8_t)v;
-                } else {
-                    float f = lc.has_mean ? standardize_value(v, lc.mean[oc], lc.stddev[oc])
-                                          : (float)v;
+                // convert_mix_channels (image.cpp:176-212): Mat::convertTo(target type) of the
+                // uint8 record, saturating, then standardize (float / double only, image.cpp:129-174)
+                switch (lc.out_dtype) {
+                case 0: ((uint8_t*)out)[idx] = (uint8_t)v; break;              // CV_8U
+                case 2: ((int8_t*)out)[idx] = (int8_t)std::min(v, 127); break;  // CV_8S (int8_t, char)
+                case 3: ((int16_t*)out)[idx] = (int16_t)v; break;              // CV_16S
+                case 4: ((uint16_t*)out)[idx] = (uint16_t)v; break;            // CV_16U
+                case 5: ((int32_t*)out)[idx] = v; break;                       // CV_32S (int32_t, uint32_t)
+                case 6: { // CV_64F: multiply / subtract / multiply in double, nothing rounded to float
+                    double d = (double)v;
+                    if (lc.has_mean) {
+                        d = d * (1. / 255.) - lc.mean[oc];
+                        if (lc.stddev[oc] != 0) d = d * (1. / lc.stddev[oc]);
+                    }
+                    ((double*)out)[idx] = d;
+                    break;
+                }
+                default: { // CV_32F
+                    float f = lc.has_mean ? standardize_value(v, lc.mean[oc], lc.stddev[oc]) : (float)v;
                     ((float*)out)[idx] = f;
+                }
                 }
             }
         }
@@ -846,6 +861,19 @@ void orc_lighting(uint8_t* img, int w, int h, const float* l, int n, float sigma
 {
     Img m = Img::view(img, w, h, 3, w * 3);
     lighting(m, l, n, sigma);
+}
+
+// image::standardize applied to a CV_8U canvas (the fixed_aspect_ratio loader standardizes its
+// uint8 planes in place, etl_image.cpp:263-300): OpenCV 2.4 arithm_op on 8U data --
+// multiply(x, 1/255.) in double then saturate_cast<uchar>; subtract(scalar mean) with the scalar
+// converted to int first (cvRound: "just one input is floating-point" rule for add/sub);
+// multiply(1/stddev) in double, saturating.  Parity unpinned: no reference fixture covers it.
+int orc_u8_standardize_value(int x, double mean, double stddev)
+{
+    int a = sat_u8(cv_round((double)x * (1. / 255.)));
+    a     = sat_u8(a - cv_round(mean));
+    if (stddev != 0) a = sat_u8(cv_round((double)a * (1. / stddev)));
+    return a;
 }
 
 float orc_standardize_value(int x, double mean, double stddev)

@@ -55,7 +55,7 @@ typedef struct orc_load_config {
     int    channels;       /* 1 or 3 */
     int    channel_major;  /* CHW planes vs HWC */
     int    bgr_to_rgb;
-    int    out_dtype;      /* 0 = uint8, 1 = float32 */
+    int    out_dtype;      /* 0 uint8, 1 float32, 2 int8, 3 int16, 4 uint16, 5 int32, 6 float64 */
     int    has_mean;       /* standardize enabled */
     double mean[3];
     double stddev[3];
@@ -93,6 +93,8 @@ void orc_cbsjitter(uint8_t* img, int w, int h, float contrast, float brightness,
                    float saturation, int hue);
 void orc_lighting(uint8_t* img, int w, int h, const float* lighting, int n, float color_noise_std);
 float orc_standardize_value(int x, double mean, double stddev);
+/* standardize of a uint8 canvas (fixed_aspect_ratio loader): the uint8 result of value x */
+int   orc_u8_standardize_value(int x, double mean, double stddev);
 
 /* whole-record path (transform + load) over a batch on a thread pool -- CPU baseline.
  * srcs[i] = HWC BGR uint8 image i (widths/heights per image), params[i] its params,

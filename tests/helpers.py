@@ -36,8 +36,8 @@ def oracle_aug_config(aug):
 
 def oracle_load_config(out):
     """aeon_amd.OutDesc -> oracle LoadConfig."""
-    return O.load_config(out.channels, bool(out.channel_major), bool(out.bgr_to_rgb),
-                         "uint8" if out.dtype == A.DTYPE_U8 else "float32",
+    name = {code: n for n, (code, _) in A.DTYPES.items()}[out.dtype]
+    return O.load_config(out.channels, bool(out.channel_major), bool(out.bgr_to_rgb), name,
                          list(out.mean) if out.has_mean else None,
                          list(out.stddev) if out.has_mean else None)
 
@@ -113,7 +113,7 @@ def hip_records(ctx, images, params, out, mask=False, dtype=None):
     for i, p in enumerate(params):
         cn = out.channels
         shape = (cn, p.out_h, p.out_w) if out.channel_major else (p.out_h, p.out_w, cn)
-        dt = np.uint8 if out.dtype == A.DTYPE_U8 else np.float32
+        dt = A.NP_DTYPE[out.dtype]
         nbytes = int(np.prod(shape)) * np.dtype(dt).itemsize
         item = host[i * out.item_stride: i * out.item_stride + nbytes].view(dt).reshape(shape)
         res.append(item.copy())

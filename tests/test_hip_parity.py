@@ -129,13 +129,87 @@ def test_fixed_aspect_ratio_canvas(ctx, channel_major):
     _assert_same(H.hip_canvases(ctx, masks, params, mout, mask=True), mref, "fixed_aspect mask")
 
 
-def test_fixed_aspect_ratio_float_is_unsupported(ctx):
-    aug = {"type": "image", "fixed_aspect_ratio": True, "crop_enable": False}
-    etl = {"type": "image", "height": 64, "width": 64, "channels": 3, "output_type": "float"}
+@pytest.mark.parametrize("otype", ["float", "double", "int32_t"])
+@pytest.mark.parametrize("with_mean", [False, True])
+@pytest.mark.parametrize("channel_major", [True, False])
+def test_fixed_aspect_ratio_non_uint8(ctx, otype, with_mean, channel_major):
+    """fixed_aspect_ratio with a non-uint8 output_type (etl_image.cpp:258-306): aeon zeroes the
+    item's whole byte size, writes the record as CV_8U planes / pixels at the top-left of the
+    canvas whatever the declared type, and standardizes that uint8 canvas in place (OpenCV 2.4
+    8-bit arithm_op rules, oracle orc_u8_standardize_value -- parity unpinned)."""
+    import oracle as O
+    if with_mean and otype == "int32_t":
+        pytest.skip("mean/stddev need float or double output")
+    aug = {"type": "image", "fixed_aspect_ratio": True, "crop_enable": False, "flip_enable": True}
+    if with_mean:
+        aug.update(mean=[0.485, 0.456, 0.6], stddev=[0.229, 0.0, 0.225])
+    etl = {"type": "image", "height": 96, "width": 128, "channels": 3, "output_type": otype,
+           "channel_major": channel_major, "bgr_to_rgb": True}
+    sizes = [(64, 40), (200, 90), (128, 96), (31, 77)]
+    imgs = [A.synthetic_image(i, w, h, 3) for i, (w, h) in enumerate(sizes)]
+    params = H.draw_params(aug, sizes, 128, 96, seed=6)
     out = C.out_desc_for(etl, aug)
-    params = H.draw_params(aug, [(40, 30)], 64, 64)
-    with pytest.raises(A.AeonHipError, match="uint8_t output only"):
-        H.hip_records(ctx, [A.synthetic_image(0, 40, 30, 3)], params, out)
+    u8 = A.out_desc(channels=3, channel_major=channel_major, bgr_to_rgb=True, dtype="uint8",
+                    item_stride=128 * 96 * 3, fixed_aspect_ratio=True, canvas=(128, 96))
+    canv = [H.place_canvas(r, u8) for r in H.oracle_records(imgs, params, u8)]
+    if with_mean:
+        lut = np.array([[O.u8_standardize(x, aug["mean"][c], aug["stddev"][c]) for x in range(256)]
+                        for c in range(3)], np.uint8)
+        for k, cv in enumerate(canv):  # the record's pixels only: the rest of the canvas is 0 -> f(0)
+            cm = cv if channel_major else cv.transpose(2, 0, 1)
+            for c in range(3):
+                cm[c] = lut[c][cm[c]]
+            canv[k] = cm if channel_major else cm.transpose(1, 2, 0)
+    import torch
+    arena, descs = A.pack_images(imgs)
+    src = torch.from_numpy(arena).to("cuda")
+    dst = torch.full((len(imgs) * out.item_stride,), 0xAB, dtype=torch.uint8, device="cuda")
+    stream = torch.cuda.current_stream().cuda_stream
+    ctx.augment_batch(descs, src.data_ptr(), params, out, dst.data_ptr(), stream)
+    ctx.synchronize(stream)
+    host = dst.cpu().numpy()
+    for i, cv in enumerate(canv):
+        item = host[i * out.item_stride:(i + 1) * out.item_stride]
+        want = np.zeros(out.item_stride, np.uint8)
+        want[:cv.size] = np.ascontiguousarray(cv).reshape(-1)
+        assert np.array_equal(item, want), (otype, with_mean, channel_major, i)
+
+
+OUTPUT_TYPES = ["int8_t", "char", "int16_t", "uint16_t", "int32_t", "uint32_t", "double", "float", "uint8_t"]
+
+
+@pytest.mark.parametrize("otype", OUTPUT_TYPES)
+@pytest.mark.parametrize("channel_major", [True, False])
+def test_output_types_images(ctx, otype, channel_major):
+    """image::loader to every aeon output_type (convert_mix_channels: saturating convertTo of the
+    uint8 record, image.cpp:176-212; typemap.hpp:43-52), against the oracle."""
+    etl = {"type": "image", "height": 96, "width": 80, "channels": 3, "output_type": otype,
+           "channel_major": channel_major, "bgr_to_rgb": True}
+    aug = dict(C.C3_AUG)
+    if otype not in ("float", "double"):
+        aug.pop("mean"), aug.pop("stddev")
+    sizes = [(160, 120), (97, 203), (300, 300)]
+    imgs = [A.synthetic_image(i, w, h, 3) for i, (w, h) in enumerate(sizes)]
+    params = H.draw_params(aug, sizes, 80, 96, seed=2)
+    out = C.out_desc_for(etl, aug)
+    _assert_same(H.hip_records(ctx, imgs, params, out), H.oracle_records(imgs, params, out), otype)
+
+
+@pytest.mark.parametrize("otype", OUTPUT_TYPES)
+def test_output_types_masks(ctx, otype):
+    """pixelmask loader to every output_type (aeon's own int32 masks among them) through the
+    NEAREST gather pass and, rotated, through the tile kernel."""
+    etl = {"type": "pixelmask", "height": 64, "width": 72, "channels": 1, "output_type": otype}
+    sizes = [(100, 90), (64, 72), (333, 111)]
+    masks = [(A.synthetic_image(40 + i, w, h, 1) % 37).astype(np.uint8) for i, (w, h) in enumerate(sizes)]
+    params = H.draw_params(dict(C.C5_AUG, angle=[-30, 30]), sizes, 72, 64, seed=13)
+    out = C.out_desc_for(etl, C.C5_AUG)
+    _assert_same(H.hip_records(ctx, masks, params, out, mask=True),
+                 H.oracle_records(masks, params, out, mask=True), otype)
+    for p in params:
+        p.angle = 0
+    _assert_same(H.hip_records(ctx, masks, params, out, mask=True),
+                 H.oracle_records(masks, params, out, mask=True), otype + " unrotated")
 
 
 # ---- image::rotate (angle != 0) --------------------------------------------------------------
@@ -426,7 +500,7 @@ def _pack16(masks):
     return np.concatenate(chunks), (A.ImgDesc * len(descs))(*descs)
 
 
-@pytest.mark.parametrize("dtype", ["uint8", "float32"])
+@pytest.mark.parametrize("dtype", ["uint8", "float32", "int8", "int16", "uint16", "int32", "float64"])
 @pytest.mark.parametrize("entry", ["mask", "depthmap"])
 def test_16bit_masks_and_depthmaps(ctx, dtype, entry):
     """ANYDEPTH records (etl_pixel_mask.cpp:35, etl_depthmap.cpp:35) stay 16-bit through
@@ -439,7 +513,8 @@ def test_16bit_masks_and_depthmaps(ctx, dtype, entry):
     masks = [rng.integers(0, 65536, (h, w), dtype=np.uint16) for w, h in sizes]
     masks[0][:] = rng.integers(0, 256, masks[0].shape)  # values within uint8 too
     params = H.draw_params(C.C5_AUG, sizes, 128, 96, seed=12)
-    esz = 4 if dtype == "float32" else 1
+    npt = A.DTYPES[dtype][1]
+    esz = np.dtype(npt).itemsize
     out = A.out_desc(channels=1, channel_major=True, dtype=dtype, item_stride=128 * 96 * esz)
     arena, descs = _pack16(masks)
     src = torch.from_numpy(arena).to("cuda")
@@ -453,7 +528,8 @@ def test_16bit_masks_and_depthmaps(ctx, dtype, entry):
     hi = H.oracle_records([(m >> 8).astype(np.uint8) for m in masks], params, o8, mask=True)
     for i, p in enumerate(params):
         v = hi[i].astype(np.uint32) * 256 + lo[i]
-        want = np.minimum(v, 255).astype(np.uint8) if dtype == "uint8" else v.astype(np.float32)
+        sat = {"uint8": 255, "int8": 127, "int16": 32767}.get(dtype)  # saturate_cast from CV_16U
+        want = (np.minimum(v, sat) if sat else v).astype(npt)
         got = host[i * out.item_stride: i * out.item_stride + v.size * esz].view(want.dtype).reshape(v.shape)
         assert np.array_equal(got, want), (entry, dtype, i)
 
