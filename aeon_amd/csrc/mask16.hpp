@@ -17,7 +17,8 @@ struct alignas(16) Mask16Job {
     int32_t  flip;
     int32_t  dtype;                   // OutDtype (AEON_DTYPE_*): saturating convertTo
     int32_t  src_elem;                // bytes per source element: 1 (CV_8U) or 2 (CV_16U)
-    int32_t  pad_;
+    int32_t  src_scratch;             // host bookkeeping: src_ptr is an offset in the slot scratch
+                                      // (the record's image::rotate pre-pass output)
 };
 
 } // namespace aeon_hip

@@ -257,15 +257,17 @@ void rotation_inverse_map(int w, int h, int angle, double M[6])
 // A single-channel pixel-mask / depth-map record, 16-bit (CV_16U, ANYDEPTH) or rotation-free
 // 8-bit: crop -> INTER_NEAREST -> flip -> convertTo (etl_pixel_mask.cpp:65-92,
 // etl_depthmap.cpp:65-96, image.cpp:176-212), one gather pass (mask16_kernels.hip).
+void rotation_inverse_map(int w, int h, int angle, double M[6]);
+
 void plan_mask16(const aeon_img_desc& d, const void* src_base, const aeon_aug_params& p, const aeon_out_desc& o,
-                 uint8_t* out_item, bool is_mask, std::vector<Mask16Job>& m16)
+                 uint8_t* out_item, bool is_mask, std::vector<Mask16Job>& m16, std::vector<RotJob>& rot,
+                 size_t& scratch_bytes)
 {
     const int eb = d.elem_bytes == 2 ? 2 : 1;
     if (!is_mask) fail(AEON_HIP_EUNSUPPORTED, "16-bit sources are implemented for pixel masks / depth maps only");
     if (d.channels != 1 || o.channels != 1) fail(AEON_HIP_EINVAL, "16-bit masks must have one channel");
     if (d.width <= 0 || d.height <= 0 || d.stride < d.width * eb || (eb == 2 && ((d.stride & 1) || (d.offset & 1))))
         fail(AEON_HIP_EINVAL, eb == 2 ? "invalid 16-bit source image descriptor" : "invalid source image descriptor");
-    if (p.angle != 0) fail(AEON_HIP_EUNSUPPORTED, "rotation of 16-bit masks is not implemented");
     if (p.out_w <= 0 || p.out_h <= 0) fail(AEON_HIP_EINVAL, "invalid output size");
     const size_t elem = out_elem_bytes(o.dtype);
     if ((size_t)p.out_w * p.out_h * elem > o.item_stride) fail(AEON_HIP_EINVAL, "output item does not fit item_stride");
@@ -286,6 +288,23 @@ void plan_mask16(const aeon_img_desc& d, const void* src_base, const aeon_aug_pa
     M.flip      = p.flip ? 1 : 0;
     M.dtype     = o.dtype;
     M.src_elem  = eb;
+    if (p.angle != 0) {
+        // image::rotate(..., interpolate = false, border 0) (etl_pixel_mask.cpp:72-74,
+        // etl_depthmap.cpp:72-73): nearest moves whole elements, so a 16-bit record rotates as a
+        // 2-byte-per-pixel one; the gather pass then reads the rotated copy in the slot scratch
+        RotJob R{};
+        rotation_inverse_map(d.width, d.height, p.angle, R.M);
+        R.src_ptr = M.src_ptr;
+        R.w = d.width, R.h = d.height, R.stride = d.stride, R.cn = eb;
+        R.interp      = AEON_INTERP_NEAREST;
+        size_t off    = (scratch_bytes + 15) & ~(size_t)15;
+        scratch_bytes = off + (size_t)d.width * d.height * eb + 16;
+        R.out_ptr     = off; // relocated to the slot's scratch by the caller
+        rot.push_back(R);
+        M.src_ptr     = off;
+        M.src_scratch = 1;
+        M.src_stride  = d.width * eb;
+    }
     m16.push_back(M);
 }
 
@@ -894,7 +913,7 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
         const bool gather = descs[i].elem_bytes == 2 ||
                             (is_mask && descs[i].channels == 1 && o.channels == 1 && params[i].angle == 0 &&
                              (descs[i].elem_bytes == 0 || descs[i].elem_bytes == 1));
-        if (gather) plan_mask16(descs[i], src_base, params[i], o, item, is_mask, m16);
+        if (gather) plan_mask16(descs[i], src_base, params[i], o, item, is_mask, m16, rot, scratch_bytes);
         else if (descs[i].elem_bytes == 0 || descs[i].elem_bytes == 1)
             plan_image(descs[i], src_base, params[i], o, item, is_mask, rot, pre_all, pre2_all, pass1_all, main_all,
                        scratch_bytes);
@@ -959,6 +978,8 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
     ensure_ring(ctx, blob, partial_words * 4, std::max<size_t>(1, pass1_all.jobs.size()) * 4 * sizeof(double));
     if (scratch_bytes > 0) grow(s.scratch, s.scratch_cap, scratch_bytes, false);
     for (RotJob& R : rot) R.out_ptr += (uint64_t)s.scratch;
+    for (Mask16Job& M : m16)
+        if (M.src_scratch) M.src_ptr += (uint64_t)s.scratch;
     if (!rot.empty()) std::memcpy(s.host + rot_off, rot.data(), rot.size() * sizeof(RotJob));
     if (!m16.empty()) std::memcpy(s.host + m16_off, m16.data(), m16.size() * sizeof(Mask16Job));
     for (auto* v : {&pre, &pre2, &pass1, &main})
@@ -994,6 +1015,8 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
     if (o.fixed_aspect_ratio) // std::fill_n of each item's canvas, its whole byte size (etl_image.cpp:263)
         HIP_OK(hipMemset2DAsync(out_dev, o.item_stride, 0,
                                 (size_t)o.canvas_w * o.canvas_h * o.channels * out_elem_bytes(od.dtype), n, stream));
+    if (!rot.empty()) // image::rotate pre-pass first: the gather and tile passes read its output
+        HIP_OK(launch_rotate((const RotJob*)(table + rot_off), (int)rot.size(), rot_max_px, stream));
     if (!m16.empty()) {
         KernelTimer t{};
         if (timed) t = take_timer(ctx, KM_FINAL, m16_bytes);
@@ -1001,8 +1024,6 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
                               timed ? t.start : nullptr, timed ? t.stop : nullptr));
         if (timed) ctx->timers.push_back(t);
     }
-    if (!rot.empty())
-        HIP_OK(launch_rotate((const RotJob*)(table + rot_off), (int)rot.size(), rot_max_px, stream));
     for (auto* v : {&pre, &pre2})
         for (LaunchPlan& P : *v)
             if (!P.jobs.empty()) timed_launch(ctx, KM_RAW, P, args(P), stream, launch_bytes(P.jobs, KM_RAW, 1), timed);

@@ -502,7 +502,8 @@ def _pack16(masks):
 
 @pytest.mark.parametrize("dtype", ["uint8", "float32", "int8", "int16", "uint16", "int32", "float64"])
 @pytest.mark.parametrize("entry", ["mask", "depthmap"])
-def test_16bit_masks_and_depthmaps(ctx, dtype, entry):
+@pytest.mark.parametrize("rotated", [False, True])
+def test_16bit_masks_and_depthmaps(ctx, dtype, entry, rotated):
     """ANYDEPTH records (etl_pixel_mask.cpp:35, etl_depthmap.cpp:35) stay 16-bit through
     crop -> NEAREST -> flip and are converted by the loader (saturate_cast<uchar> / exact float).
     NEAREST is a pure gather, so the oracle reference is its 8-bit transform of the low and high
@@ -512,7 +513,8 @@ def test_16bit_masks_and_depthmaps(ctx, dtype, entry):
     sizes = [(int(rng.integers(40, 300)), int(rng.integers(40, 300))) for _ in range(9)]
     masks = [rng.integers(0, 65536, (h, w), dtype=np.uint16) for w, h in sizes]
     masks[0][:] = rng.integers(0, 256, masks[0].shape)  # values within uint8 too
-    params = H.draw_params(C.C5_AUG, sizes, 128, 96, seed=12)
+    params = H.draw_params(dict(C.C5_AUG, angle=[-40, 40]) if rotated else C.C5_AUG, sizes, 128, 96, seed=12)
+    assert rotated == any(p.angle != 0 for p in params)
     npt = A.DTYPES[dtype][1]
     esz = np.dtype(npt).itemsize
     out = A.out_desc(channels=1, channel_major=True, dtype=dtype, item_stride=128 * 96 * esz)
@@ -544,6 +546,4 @@ def test_16bit_errors(ctx):
     (p,) = H.draw_params(C.C5_AUG, [(30, 20)], 64, 64)
     with pytest.raises(A.AeonHipError, match="pixel masks / depth maps only"):
         ctx.augment_batch(descs, src.data_ptr(), [p], out, dst.data_ptr())
-    p.angle = 90
-    with pytest.raises(A.AeonHipError, match="rotation of 16-bit"):
-        ctx.mask_batch(descs, src.data_ptr(), [p], out, dst.data_ptr())
+
