@@ -52,6 +52,8 @@ class AugParams(ctypes.Structure):
         ("contrast", ctypes.c_float), ("brightness", ctypes.c_float),
         ("saturation", ctypes.c_float), ("hue", ctypes.c_int32),
         ("interp", ctypes.c_int32),
+        ("expand_ratio", ctypes.c_float), ("expand_x", ctypes.c_int32), ("expand_y", ctypes.c_int32),
+        ("expand_w", ctypes.c_int32), ("expand_h", ctypes.c_int32),
     ]
 
     def as_dict(self):
@@ -120,6 +122,10 @@ def lib():
         L.aeon_param_factory_destroy.argtypes = [vp]
         L.aeon_make_params.argtypes = [vp, P(ctypes.c_uint32), ctypes.c_int, ctypes.c_int,
                                        ctypes.c_int, ctypes.c_int, P(AugParams)]
+        L.aeon_make_ssd_params.argtypes = [vp, P(ctypes.c_uint32), ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                           ctypes.c_int, P(ctypes.c_float), ctypes.c_int, P(AugParams)]
+        L.aeon_batch_sample_patches.argtypes = [vp, ctypes.c_int, P(ctypes.c_uint32), P(ctypes.c_float),
+                                                ctypes.c_int, P(ctypes.c_float), ctypes.c_int, P(ctypes.c_int)]
         L.aeon_seed_slots.argtypes = [ctypes.c_uint32, ctypes.c_int, P(ctypes.c_uint32)]
         L.aeon_unbiased_round.argtypes = [ctypes.c_float, P(ctypes.c_int64)]
         L.aeon_calculate_scale.argtypes = [ctypes.c_int] * 4 + [P(ctypes.c_float)]
@@ -180,6 +186,29 @@ class ParamFactory:
         p = AugParams()
         st = ctypes.c_uint32(int(state[0]))
         _check(lib().aeon_make_params(self._h, ctypes.byref(st), in_w, in_h, out_w, out_h, ctypes.byref(p)))
+        state[0] = st.value
+        return p
+
+    def sample_patches(self, sampler, state, nboxes, cap=4096):
+        """batch_sampler::sample_patches of batch_samplers[sampler] (aeon src/augment_image.cpp:567-586)
+        over normalized boxes; returns the sampled normalized boxes."""
+        st = ctypes.c_uint32(int(state[0]))
+        flat = (ctypes.c_float * max(1, 4 * len(nboxes)))(*[float(v) for b in nboxes for v in b])
+        out = (ctypes.c_float * (4 * cap))()
+        n = ctypes.c_int()
+        _check(lib().aeon_batch_sample_patches(self._h, sampler, ctypes.byref(st), flat, len(nboxes), out, cap,
+                                               ctypes.byref(n)))
+        state[0] = st.value
+        return [tuple(out[4 * i:4 * i + 4]) for i in range(min(n.value, cap))]
+
+    def make_ssd_params(self, state, in_w, in_h, out_w, out_h, boxes=()):
+        """param_factory::make_ssd_params (aeon src/augment_image.cpp:232-310); boxes are
+        boundingbox::box pixel coordinates (xmin, ymin, xmax, ymax), xmax/ymax inclusive."""
+        p = AugParams()
+        st = ctypes.c_uint32(int(state[0]))
+        flat = (ctypes.c_float * max(1, 4 * len(boxes)))(*[float(v) for b in boxes for v in b])
+        _check(lib().aeon_make_ssd_params(self._h, ctypes.byref(st), in_w, in_h, out_w, out_h, flat, len(boxes),
+                                          ctypes.byref(p)))
         state[0] = st.value
         return p
 

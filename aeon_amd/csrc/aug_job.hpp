@@ -77,6 +77,17 @@ struct alignas(16) RotJob {
     int32_t  pad_;
 };
 
+// image::expand pre-pass of one record (rotate_kernels.hip): the record at (ox, oy) of a zeroed
+// ew x eh canvas in the slot scratch (src/image.cpp:276-303).
+struct alignas(16) ExpandJob {
+    uint64_t src_ptr;     // HWC uint8 record (its original, or its rotated copy in scratch)
+    uint64_t out_ptr;     // HWC uint8 canvas, ew * cn bytes per row
+    int32_t  w, h, stride, cn;
+    int32_t  ew, eh, ox, oy;
+    int32_t  src_scratch; // host bookkeeping: src_ptr / out_ptr are slot-scratch offsets until relocated
+    int32_t  pad_[3];
+};
+
 // Per-launch uniform arguments.
 struct LaunchArgs {
     const AugJob*  jobs;

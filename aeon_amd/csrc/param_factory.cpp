@@ -4,6 +4,7 @@
 
 #include <algorithm>
 #include <cctype>
+#include <cfloat>
 #include <cmath>
 
 namespace aeon_hip {
@@ -101,10 +102,13 @@ param_factory::param_factory(const Json& js_in)
             !(expand_ratio.a() >= 1 && expand_ratio.a() <= expand_ratio.b()))
             out_of_range("expand_ratio");
         if (ipair("hue", hue) && !(hue.a() <= hue.b())) out_of_range("hue");
-        if (js.has("batch_samplers") && crop_enable && !js.at("batch_samplers").array().empty())
+        if (js.has("batch_samplers"))
+            for (const Json& b : js.at("batch_samplers").array()) batch_samplers.emplace_back(b);
+        if (crop_enable && !batch_samplers.empty())
             throw std::invalid_argument(
                 "'Cannot use 'batch_samplers' with 'crop_enable'. Please use only one cropping "
                 "method in augmentations.");
+        number("emit_constraint_min_overlap", emit_constraint_min_overlap);
 
         // derived (augment_image.cpp:70-85)
         if (flip_enable) flip_distribution = std::bernoulli_distribution{0.5};
@@ -117,6 +121,106 @@ param_factory::param_factory(const Json& js_in)
         std::transform(e.begin(), e.end(), e.begin(), ::tolower);
         if (!(e == "center" || e == "min_overlap" || e.empty()))
             throw std::invalid_argument("Invalid emit constraint type");
+        emit_constraint_type = e;
+    }
+}
+
+// ---- SSD patch sampling geometry ------------------------------------------------------------
+namespace {
+constexpr float kEps = 0.00001f; // nervana::epsilon (util.hpp:32)
+bool normalized(float x) { return x >= 0.0f - kEps && x <= 1.0f + kEps; } // almost_equal_or_*
+} // namespace
+
+nbox::nbox(float x0, float y0, float x1, float y1) : xmin(x0), ymin(y0), xmax(x1), ymax(y1)
+{
+    if (!(normalized(xmin) && normalized(xmax) && normalized(ymin) && normalized(ymax)))
+        throw std::invalid_argument("bounding box is not properly normalized");
+}
+
+nbox nbox::intersect(const nbox& b) const // normalized_box.cpp:75-88
+{
+    if (b.xmin > xmax || b.xmax < xmin || b.ymin > ymax || b.ymax < ymin) return nbox();
+    return nbox(std::max(xmin, b.xmin), std::max(ymin, b.ymin), std::min(xmax, b.xmax), std::min(ymax, b.ymax));
+}
+
+float nbox::jaccard_overlap(const nbox& b) const // normalized_box.cpp:47-57
+{
+    const float i = intersect(b).size();
+    if (i == 0.f) return 0.f;
+    return i / (size() + b.size() - i);
+}
+
+float nbox::coverage(const nbox& b) const // normalized_box.cpp:59-73
+{
+    const float i = intersect(b).size();
+    return i > 0 ? i / size() : 0.f;
+}
+
+bool sample_constraint::satisfies(const nbox& s, const std::vector<nbox>& objects) const // :404-474
+{
+    auto has = [](float v) { return !std::isnan(v); };
+    const bool jac = has(min_jaccard_overlap) || has(max_jaccard_overlap);
+    const bool sc  = has(min_sample_coverage) || has(max_sample_coverage);
+    const bool oc  = has(min_object_coverage) || has(max_object_coverage);
+    if (!jac && !sc && !oc) return true;
+    bool found = false;
+    for (const nbox& o : objects) {
+        if (jac) {
+            const float v = s.jaccard_overlap(o);
+            if (has(min_jaccard_overlap) && v < min_jaccard_overlap) continue;
+            if (has(max_jaccard_overlap) && v > max_jaccard_overlap) continue;
+            found = true;
+        }
+        if (sc) {
+            const float v = s.coverage(o);
+            if (has(min_sample_coverage) && v < min_sample_coverage) continue;
+            if (has(max_sample_coverage) && v > max_sample_coverage) continue;
+            found = true;
+        }
+        if (oc) {
+            const float v = o.coverage(s);
+            if (has(min_object_coverage) && v < min_object_coverage) continue;
+            if (has(max_object_coverage) && v > max_object_coverage) continue;
+            found = true;
+        }
+        if (found) return true;
+    }
+    return found;
+}
+
+// batch_sampler / sampler / sample_constraint JSON (augment_image.hpp:262-420 config lists)
+batch_sampler::batch_sampler(const Json& js)
+{
+    if (js.is_null()) return;
+    if (js.has("max_sample")) {
+        max_sample = (int)js.at("max_sample").number();
+        if (max_sample < 0) out_of_range("max_sample");
+    }
+    if (js.has("max_trials")) max_trials = (unsigned)js.at("max_trials").number();
+    if (js.has("sampler") && !js.at("sampler").is_null()) {
+        const Json& sj = js.at("sampler");
+        if (sj.has("scale")) {
+            auto p = pair_of(sj, "scale");
+            if (!(p[0] <= p[1] && p[0] > 0. && p[1] <= 1.)) out_of_range("scale");
+            scale = std::uniform_real_distribution<float>{(float)p[0], (float)p[1]};
+        }
+        if (sj.has("aspect_ratio")) {
+            auto p = pair_of(sj, "aspect_ratio");
+            if (!(p[0] <= p[1] && p[0] > 0. && p[1] < FLT_MAX)) out_of_range("aspect_ratio");
+            aspect_ratio = std::uniform_real_distribution<float>{(float)p[0], (float)p[1]};
+        }
+    }
+    if (js.has("sample_constraint") && !js.at("sample_constraint").is_null()) {
+        const Json& cj = js.at("sample_constraint");
+        auto        f  = [&](const char* k, float& v) {
+            if (cj.has(k)) v = (float)cj.at(k).number();
+        };
+        f("min_jaccard_overlap", constraint.min_jaccard_overlap);
+        f("max_jaccard_overlap", constraint.max_jaccard_overlap);
+        f("min_sample_coverage", constraint.min_sample_coverage);
+        f("max_sample_coverage", constraint.max_sample_coverage);
+        f("min_object_coverage", constraint.min_object_coverage);
+        f("max_object_coverage", constraint.max_object_coverage);
     }
 }
 

@@ -5,7 +5,9 @@
 // same minstd_rand0 state gets the same params as in aeon.  Parameter sampling stays on the
 // host (µs per record); the pixel work it parameterises runs on the GPU.
 #pragma once
+#include <cmath>
 #include <random>
+#include <stdexcept>
 #include <string>
 #include <vector>
 
@@ -13,6 +15,40 @@
 #include "json.hpp"
 
 namespace aeon_hip {
+
+// normalized_box::box (src/normalized_box.hpp:24-67): coordinates in [0, 1] (within aeon's 1e-5
+// epsilon, src/util.cpp:246-254), width = xmax - xmin.  Constructing an improperly normalized box
+// throws std::invalid_argument, as aeon's constructor does.
+struct nbox {
+    float xmin = 0, ymin = 0, xmax = 0, ymax = 0;
+    nbox() = default;
+    nbox(float x0, float y0, float x1, float y1);
+    float size() const { return (xmax < xmin || ymax < ymin) ? 0.0f : (xmax - xmin) * (ymax - ymin); }
+    nbox  intersect(const nbox& b) const;
+    float jaccard_overlap(const nbox& b) const;
+    float coverage(const nbox& b) const;
+};
+
+// sample_constraint (src/augment_image.cpp:404-474): NaN = bound not configured
+struct sample_constraint {
+    float min_jaccard_overlap = NAN, max_jaccard_overlap = NAN;
+    float min_sample_coverage = NAN, max_sample_coverage = NAN;
+    float min_object_coverage = NAN, max_object_coverage = NAN;
+    bool  satisfies(const nbox& sampled, const std::vector<nbox>& objects) const;
+};
+
+// sampler + batch_sampler (src/augment_image.cpp:355-402, 556-586)
+struct batch_sampler {
+    int                                           max_sample = -1;
+    unsigned                                      max_trials = 100;
+    mutable std::uniform_real_distribution<float> scale{1.0f, 1.0f}, aspect_ratio{1.0f, 1.0f};
+    sample_constraint                             constraint;
+    explicit batch_sampler(const Json& js);
+    template <typename URNG>
+    nbox sample_patch(URNG& random) const;
+    template <typename URNG>
+    void sample_patches(URNG& random, const std::vector<nbox>& objects, std::vector<nbox>& out) const;
+};
 
 class param_factory {
 public:
@@ -50,6 +86,16 @@ public:
     mutable std::uniform_int_distribution<int>    padding_crop_offset_distribution{0, 0};
 
     int interp_code() const; // AEON_INTERP_* (or -1 for CUBIC/AREA/LANCZOS4)
+
+    // src/augment_image.cpp:232-301 (boxes: n x (xmin, ymin, xmax, ymax) boundingbox::box)
+    template <typename URNG>
+    void make_ssd_params(URNG& random, int in_w, int in_h, int out_w, int out_h, const float* boxes, int n_boxes,
+                         aeon_aug_params* p) const;
+
+    std::vector<batch_sampler>                    batch_samplers;
+    mutable std::uniform_real_distribution<float> expand_distribution{0.0f, 1.0f};
+    std::string                                   emit_constraint_type;
+    float                                         emit_constraint_min_overlap = 0.0f;
 };
 
 // ---- geometry helpers (src/image.cpp:108-273, src/util.cpp:212-239) ---------------------------
@@ -135,6 +181,79 @@ void param_factory::make_params(URNG& random, int in_w, int in_h, int out_w, int
         for (int i = 0; i < 3; i++) p->lighting[i] = lighting(random);
         p->n_lighting      = 3;
         p->color_noise_std = lighting.stddev();
+    }
+}
+
+// sampler::sample_patch (src/augment_image.cpp:355-384): float scale, aspect ratio bounded by
+// scale^2 (pow in double, then float), box of scale * sqrt(ar) x scale / sqrt(ar) at a uniform offset
+template <typename URNG>
+nbox batch_sampler::sample_patch(URNG& random) const
+{
+    const float s      = scale(random);
+    const float min_ar = std::max<float>(aspect_ratio.min(), std::pow(s, 2.));
+    const float max_ar = std::min<float>(aspect_ratio.max(), 1 / std::pow(s, 2.));
+    const float ar     = std::uniform_real_distribution<float>(min_ar, max_ar)(random);
+    const float bw = s * std::sqrt(ar), bh = s / std::sqrt(ar);
+    const float w_off  = std::uniform_real_distribution<float>(0.f, 1.f - bw)(random);
+    const float h_off  = std::uniform_real_distribution<float>(0.f, 1.f - bh)(random);
+    return nbox(w_off, h_off, w_off + bw, h_off + bh);
+}
+
+// batch_sampler::sample_patches (src/augment_image.cpp:568-586)
+template <typename URNG>
+void batch_sampler::sample_patches(URNG& random, const std::vector<nbox>& objects, std::vector<nbox>& out) const
+{
+    int found = 0;
+    for (unsigned i = 0; i < max_trials; ++i) {
+        if (max_sample != -1 && found >= max_sample) break;
+        const nbox sampled = sample_patch(random);
+        if (constraint.satisfies(sampled, objects)) {
+            ++found;
+            out.push_back(sampled);
+        }
+    }
+}
+
+template <typename URNG>
+void param_factory::make_ssd_params(URNG& random, int in_w, int in_h, int out_w, int out_h, const float* boxes,
+                                    int n_boxes, aeon_aug_params* p) const
+{
+    make_params(random, in_w, in_h, out_w, out_h, p);
+    p->out_w = out_w, p->out_h = out_h; // "use warping"
+    float     ratio   = expand_ratio(random);
+    const bool enabled = expand_distribution(random) < expand_probability;
+    if (ratio < 1.) throw std::invalid_argument("Expand ratio must be greater than 1.");
+    int ox = 0, oy = 0, ew = in_w, eh = in_h;
+    if (enabled) {
+        const float fw = ratio * (float)(size_t)in_w, fh = ratio * (float)(size_t)in_h;
+        ew = (int)std::floor(fw), eh = (int)std::floor(fh);
+        const float mw = fw - (float)(size_t)in_w, mh = fh - (float)(size_t)in_h;
+        const float w_off = expand_distribution(random) * mw;
+        const float h_off = expand_distribution(random) * mh;
+        ox = (int)std::floor(w_off), oy = (int)std::floor(h_off);
+    } else {
+        ratio = 1.0f;
+    }
+    p->expand_ratio = ratio, p->expand_x = ox, p->expand_y = oy, p->expand_w = ew, p->expand_h = eh;
+    // boundingbox::expand then normalize (boundingbox.cpp:88-105, 150-163)
+    std::vector<nbox> objects;
+    for (int i = 0; i < n_boxes; i++) {
+        const float* b = boxes + 4 * i;
+        if (b[2] + ox > ew || b[3] + oy > eh) throw std::invalid_argument("Invalid parameters to expand boundingbox");
+        const float x0 = b[0] + ox, y0 = b[1] + oy, x1 = b[2] + ox, y1 = b[3] + oy;
+        objects.emplace_back(x0 / ew, y0 / eh, (x1 + 1) / ew, (y1 + 1) / eh);
+    }
+    if (!crop_enable) {
+        // param_factory::sample_patch (src/augment_image.cpp:303-322)
+        std::vector<nbox> samples;
+        for (const batch_sampler& bs : batch_samplers) bs.sample_patches(random, objects, samples);
+        nbox patch(0, 0, 1, 1);
+        if (!samples.empty()) patch = samples[std::uniform_int_distribution<int>(0, (int)samples.size() - 1)(random)];
+        // unnormalize (normalized_box.hpp:59-63) -> boundingbox rect() (box.hpp:53-57)
+        const float x0 = patch.xmin * (float)ew, y0 = patch.ymin * (float)eh;
+        const float x1 = patch.xmax * (float)ew - 1, y1 = patch.ymax * (float)eh - 1;
+        p->crop_x = (int)std::round(x0), p->crop_y = (int)std::round(y0);
+        p->crop_w = (int)std::round(x1 - x0 + 1), p->crop_h = (int)std::round(y1 - y0 + 1);
     }
 }
 

@@ -12,8 +12,8 @@ namespace aeon_hip {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-// A workgroup of 128 lanes plans 16 records: every lane brings one 16-byte piece of the records'
-// 2 KiB over PCIe (many lanes and workgroups keep many reads in flight: with one lane reading a
+// A workgroup of 128 lanes plans 16 records: the lanes bring the records' 16-byte pieces (2.25 KiB)
+// over PCIe (many lanes and workgroups keep many reads in flight: with one lane reading a
 // whole record the kernel took 11.8 us for 256 records, against 5.2 us for a 64 KiB table upload);
 // lanes 0-15 plan one record each into LDS; all 128 lanes store the 16 jobs (4 KiB) 16 bytes apiece.
 constexpr int kPlanPerBlock = 16;
@@ -21,7 +21,7 @@ constexpr int kPlanPerBlock = 16;
 __global__ __launch_bounds__(128) void plan_records(const PlanRecord* host_records, AugJob* __restrict__ jobs,
                                                     PlanArgs a)
 {
-    __shared__ u32x4 recs[kPlanPerBlock * 8];
+    __shared__ u32x4 recs[kPlanPerBlock * kPlanRecordPieces];
     __shared__ u32x4 out[kPlanPerBlock * 16];
     const int tid = threadIdx.x;
     const int r0  = blockIdx.x * kPlanPerBlock;
@@ -29,11 +29,12 @@ __global__ __launch_bounds__(128) void plan_records(const PlanRecord* host_recor
     // sc0 sc1: read through to host memory (the slot was written by the host since its last use)
     const auto src = __builtin_amdgcn_make_buffer_rsrc((void*)host_records, (short)0, a.n * (int)sizeof(PlanRecord),
                                                        0x00020000);
-    if (tid < nr * 8) recs[tid] = __builtin_amdgcn_raw_buffer_load_b128(src, r0 * 128 + tid * 16, 0, 1 | 16);
+    for (int i = tid; i < nr * kPlanRecordPieces; i += 128)
+        recs[i] = __builtin_amdgcn_raw_buffer_load_b128(src, r0 * (int)sizeof(PlanRecord) + i * 16, 0, 1 | 16);
     __syncthreads();
     if (tid < nr) {
         PlanRecord R;
-        __builtin_memcpy(&R, &recs[tid * 8], sizeof(R));
+        __builtin_memcpy(&R, &recs[tid * kPlanRecordPieces], sizeof(R));
         const int i = r0 + tid;
         AugJob    J;
         plan_direct(R.desc, a.src_base, R.params, a.out, a.out_base + (uint64_t)i * a.item_stride, a.is_mask != 0, J);

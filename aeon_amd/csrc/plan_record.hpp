@@ -99,6 +99,9 @@ struct OutGeom {
     int32_t fixed_aspect_ratio, canvas_w, canvas_h;
 };
 
+// The record goes through image::expand (etl_image.cpp:155-159: expand_ratio > 1), a pre-pass.
+AEON_HD inline bool expands(const aeon_aug_params& p) { return p.expand_ratio > 1.0f; }
+
 // transform_single_image (src/etl_image.cpp:146-202) of one record read straight from its
 // decoded source: crop [+ add_padding] -> resize -> [cbsjitter -> lighting] -> flip -> load, as ONE
 // job.  Callers handle rotation / resize_short (pre-passes) and contrast (two passes) by patching
@@ -144,10 +147,10 @@ AEON_HD inline void plan_direct(const aeon_img_desc& d, uint64_t src_base, const
 // Compact per-record input of the device planner: what the caller handed over for the record.
 struct alignas(16) PlanRecord {
     aeon_img_desc   desc;   // 32 B
-    aeon_aug_params params; // 88 B
-    uint64_t        pad_;   // -> 128 B
+    aeon_aug_params params; // 108 B (-> 144 with the alignment)
 };
-static_assert(sizeof(PlanRecord) == 128, "PlanRecord is 128 bytes (8 x 16-byte loads)");
+constexpr int kPlanRecordPieces = (int)sizeof(PlanRecord) / 16;
+static_assert(sizeof(PlanRecord) == 144, "PlanRecord is 144 bytes (9 x 16-byte loads)");
 
 // Per-call uniform arguments of the device planner.
 struct PlanArgs {

@@ -55,6 +55,28 @@ __global__ __launch_bounds__(256) void rotate_records(const RotJob* __restrict__
     }
 }
 
+// image::expand: every canvas pixel is the record's pixel (x - ox, y - oy) or 0 outside it.
+__global__ __launch_bounds__(256) void expand_records(const ExpandJob* __restrict__ jobs)
+{
+    const ExpandJob E  = jobs[blockIdx.y];
+    const int       px = blockIdx.x * 256 + threadIdx.x;
+    if (px >= E.ew * E.eh) return;
+    const int      y = px / E.ew, x = px - y * E.ew;
+    const int      sx = x - E.ox, sy = y - E.oy;
+    const bool     in = sx >= 0 && sx < E.w && sy >= 0 && sy < E.h;
+    const uint8_t* S  = (const uint8_t*)E.src_ptr + (size_t)sy * E.stride + (size_t)sx * E.cn;
+    uint8_t*       D  = (uint8_t*)E.out_ptr + (size_t)px * E.cn;
+    for (int c = 0; c < E.cn; c++) D[c] = in ? S[c] : 0;
+}
+
+hipError_t launch_expand(const ExpandJob* jobs, int n_jobs, int max_pixels, hipStream_t stream)
+{
+    if (n_jobs <= 0) return hipSuccess;
+    const dim3 grid((unsigned)((max_pixels + 255) / 256), (unsigned)n_jobs), block(256);
+    hipLaunchKernelGGL(expand_records, grid, block, 0, stream, jobs);
+    return hipGetLastError();
+}
+
 hipError_t launch_rotate(const RotJob* jobs, int n_jobs, int max_pixels, hipStream_t stream)
 {
     if (n_jobs <= 0) return hipSuccess;

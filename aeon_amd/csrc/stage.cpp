@@ -32,6 +32,7 @@ hipError_t set_kernel_lds_limit(int bytes);
 hipError_t launch_transpose(const void* src, void* dst, int64_t rows, int64_t cols, int element_size,
                             hipStream_t stream);
 hipError_t launch_rotate(const RotJob* jobs, int n_jobs, int max_pixels, hipStream_t stream);
+hipError_t launch_expand(const ExpandJob* jobs, int n_jobs, int max_pixels, hipStream_t stream);
 hipError_t launch_nearest(const Mask16Job* jobs, int n_jobs, int max_h, int max_w, hipStream_t stream,
                           hipEvent_t start, hipEvent_t stop);
 hipError_t launch_upload_table(const void* host_dev, void* dst, size_t bytes, hipStream_t stream);
@@ -326,11 +327,17 @@ void validate_record(const aeon_img_desc& d, const aeon_aug_params& p, const aeo
     if (o.fixed_aspect_ratio && (p.out_w > o.canvas_w || p.out_h > o.canvas_h))
         fail(AEON_HIP_EINVAL, "fixed_aspect_ratio: output_size larger than the image canvas");
     int base_w = d.width, base_h = d.height;
-    if (!is_mask && p.resize_short_size > 0) get_resized_short_size(d.width, d.height, p.resize_short_size, &base_w, &base_h);
+    if (!is_mask && expands(p)) { // image::expand throws on a record that does not fit the canvas
+        if (p.expand_x < 0 || p.expand_y < 0 || p.expand_x + d.width > p.expand_w || p.expand_y + d.height > p.expand_h)
+            fail(AEON_HIP_EINVAL, "Invalid parameters to expand image");
+        base_w = p.expand_w, base_h = p.expand_h;
+    }
+    if (!is_mask && p.resize_short_size > 0) get_resized_short_size(base_w, base_h, p.resize_short_size, &base_w, &base_h);
     if (p.crop_x < 0 || p.crop_y < 0 || p.crop_w <= 0 || p.crop_h <= 0 || p.crop_x + p.crop_w > base_w ||
         p.crop_y + p.crop_h > base_h)
-        fail(AEON_HIP_EINVAL, base_w == d.width && base_h == d.height ? "cropbox outside image"
-                                                                      : "cropbox outside the resize_short image");
+        fail(AEON_HIP_EINVAL, (is_mask || p.resize_short_size <= 0) && !(!is_mask && expands(p))
+                                  ? "cropbox outside image"
+                                  : "cropbox outside the expanded / resize_short image");
     if (!is_mask && photo_flags(p) && cn != 3) fail(AEON_HIP_EINVAL, "photometric augmentation needs a 3-channel image");
     if (!is_mask && (p.n_lighting != 0 && p.n_lighting != 3)) fail(AEON_HIP_EINVAL, "lighting needs 3 values");
 }
@@ -341,7 +348,8 @@ OutGeom out_geom(const aeon_out_desc& o) { return OutGeom{o.fixed_aspect_ratio, 
 // pass1 (contrast statistics) -> main; each reads only what an earlier group wrote.
 void plan_image(const aeon_img_desc& d, const void* src_base, const aeon_aug_params& p,
                 const aeon_out_desc& o, uint8_t* out_item, bool is_mask, std::vector<RotJob>& rot,
-                LaunchPlan& pre, LaunchPlan& pre2, LaunchPlan& pass1, LaunchPlan& main, size_t& scratch_bytes)
+                std::vector<ExpandJob>& exp, LaunchPlan& pre, LaunchPlan& pre2, LaunchPlan& pass1, LaunchPlan& main,
+                size_t& scratch_bytes)
 {
     validate_record(d, p, o, is_mask);
     const int cn = d.channels;
@@ -364,18 +372,36 @@ void plan_image(const aeon_img_desc& d, const void* src_base, const aeon_aug_par
         J.src_bytes   = (uint64_t)d.width * d.height * cn;
         J.src_stride  = d.width * cn;
     }
+    if (!is_mask && expands(p)) {
+        // image::expand (image.cpp:276-303) into scratch: a zeroed expand_w x expand_h canvas with the
+        // (rotated) record at (expand_x, expand_y); everything after reads the canvas
+        ExpandJob E{};
+        E.src_ptr     = J.src_ptr;
+        E.src_scratch = J.src_scratch;
+        E.w = J.src_w, E.h = J.src_h, E.stride = J.src_stride, E.cn = cn;
+        E.ew = p.expand_w, E.eh = p.expand_h, E.ox = p.expand_x, E.oy = p.expand_y;
+        size_t off    = (scratch_bytes + 15) & ~(size_t)15;
+        scratch_bytes = off + (size_t)E.ew * E.eh * cn + 16;
+        E.out_ptr     = off; // relocated to the slot's scratch by the caller
+        exp.push_back(E);
+        J.src_ptr     = off;
+        J.src_scratch = 1;
+        J.src_bytes   = (uint64_t)E.ew * E.eh * cn;
+        J.src_w = E.ew, J.src_h = E.eh, J.src_stride = E.ew * cn;
+    }
     if (!is_mask && p.resize_short_size > 0) {
         // image::resize_short (image.cpp:118-127) into a device scratch, cropbox window only
-        int rw, rh;
-        get_resized_short_size(d.width, d.height, p.resize_short_size, &rw, &rh);
+        const int bw = J.src_w, bh = J.src_h; // the (rotated, expanded) record
+        int       rw, rh;
+        get_resized_short_size(bw, bh, p.resize_short_size, &rw, &rh);
         AugJob P = J;
         P.photo   = 0;
         P.flip    = 0;
         P.shift_x = P.shift_y = P.padded = 0;
-        P.crop_x = 0, P.crop_y = 0, P.crop_w = d.width, P.crop_h = d.height;
-        P.mode    = choose_mode(d.width, d.height, rw, rh, p.interp, cn);
-        P.scale_x = 1. / ((double)rw / d.width);
-        P.scale_y = 1. / ((double)rh / d.height);
+        P.crop_x = 0, P.crop_y = 0, P.crop_w = bw, P.crop_h = bh;
+        P.mode    = choose_mode(bw, bh, rw, rh, p.interp, cn);
+        P.scale_x = 1. / ((double)rw / bw);
+        P.scale_y = 1. / ((double)rh / bh);
         P.dst_w = rw, P.dst_h = rh;
         P.win_x = p.crop_x, P.win_y = p.crop_y, P.win_w = p.crop_w, P.win_h = p.crop_h;
         P.xv      = simd_boundary(rw * cn);
@@ -802,7 +828,7 @@ bool run_direct(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void
         const aeon_aug_params& p = params[i];
         if (d.elem_bytes != 0 && d.elem_bytes != 1) return false;
         if (is_mask && d.channels == 1 && o.channels == 1 && p.angle == 0) return false; // mask gather pass
-        if (p.angle != 0 || (!is_mask && p.resize_short_size > 0)) return false;
+        if (p.angle != 0 || (!is_mask && (p.resize_short_size > 0 || expands(p)))) return false;
         validate_record(d, p, o, is_mask);
         const int photo = is_mask ? 0 : photo_flags(p);
         const int mode  = choose_mode(p.crop_w, p.crop_h, p.out_w, p.out_h, is_mask ? AEON_INTERP_NEAREST : p.interp,
@@ -905,6 +931,7 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
 
     LaunchPlan             pre_all, pre2_all, pass1_all, main_all;
     std::vector<RotJob>    rot;
+    std::vector<ExpandJob> exp;
     std::vector<Mask16Job> m16;
     size_t     scratch_bytes = 0;
     for (int i = 0; i < n; i++) {
@@ -915,8 +942,8 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
                              (descs[i].elem_bytes == 0 || descs[i].elem_bytes == 1));
         if (gather) plan_mask16(descs[i], src_base, params[i], o, item, is_mask, m16, rot, scratch_bytes);
         else if (descs[i].elem_bytes == 0 || descs[i].elem_bytes == 1)
-            plan_image(descs[i], src_base, params[i], o, item, is_mask, rot, pre_all, pre2_all, pass1_all, main_all,
-                       scratch_bytes);
+            plan_image(descs[i], src_base, params[i], o, item, is_mask, rot, exp, pre_all, pre2_all, pass1_all,
+                       main_all, scratch_bytes);
         else fail(AEON_HIP_EINVAL, "elem_bytes must be 1 (CV_8U) or 2 (CV_16U)");
     }
 
@@ -938,7 +965,10 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
     for (const AugJob& J : main_all.jobs) main[J.mode * 4 + has_tail(J) * 2 + (J.photo ? 1 : 0)].jobs.push_back(J);
     const size_t     rot_off   = 0;
     const size_t     m16_off   = rot_off + rot.size() * sizeof(RotJob);
-    size_t           blob      = m16_off + m16.size() * sizeof(Mask16Job);
+    const size_t     exp_off   = m16_off + m16.size() * sizeof(Mask16Job);
+    size_t           blob      = exp_off + exp.size() * sizeof(ExpandJob);
+    int              exp_max_px = 0;
+    for (const ExpandJob& E : exp) exp_max_px = std::max(exp_max_px, E.ew * E.eh);
     int              m16_max_h = 0, m16_max_w = 0;
     double           m16_bytes = 0; // algorithmic: crop read once + output written once
     for (const Mask16Job& M : m16) {
@@ -980,6 +1010,11 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
     for (RotJob& R : rot) R.out_ptr += (uint64_t)s.scratch;
     for (Mask16Job& M : m16)
         if (M.src_scratch) M.src_ptr += (uint64_t)s.scratch;
+    for (ExpandJob& E : exp) {
+        E.out_ptr += (uint64_t)s.scratch;
+        if (E.src_scratch) E.src_ptr += (uint64_t)s.scratch;
+    }
+    if (!exp.empty()) std::memcpy(s.host + exp_off, exp.data(), exp.size() * sizeof(ExpandJob));
     if (!rot.empty()) std::memcpy(s.host + rot_off, rot.data(), rot.size() * sizeof(RotJob));
     if (!m16.empty()) std::memcpy(s.host + m16_off, m16.data(), m16.size() * sizeof(Mask16Job));
     for (auto* v : {&pre, &pre2, &pass1, &main})
@@ -1017,6 +1052,8 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
                                 (size_t)o.canvas_w * o.canvas_h * o.channels * out_elem_bytes(od.dtype), n, stream));
     if (!rot.empty()) // image::rotate pre-pass first: the gather and tile passes read its output
         HIP_OK(launch_rotate((const RotJob*)(table + rot_off), (int)rot.size(), rot_max_px, stream));
+    if (!exp.empty()) // then image::expand (etl_image.cpp:155-159)
+        HIP_OK(launch_expand((const ExpandJob*)(table + exp_off), (int)exp.size(), exp_max_px, stream));
     if (!m16.empty()) {
         KernelTimer t{};
         if (timed) t = take_timer(ctx, KM_FINAL, m16_bytes);
@@ -1334,6 +1371,42 @@ int aeon_make_params(aeon_param_factory* f, uint32_t* state, int in_w, int in_h,
         std::lock_guard<std::mutex> lock(f->mu);
         TrackedEngine eng(*state);
         f->f.make_params(eng, in_w, in_h, out_w, out_h, out);
+        *state = eng.last;
+        return 0;
+    });
+}
+
+int aeon_make_ssd_params(aeon_param_factory* f, uint32_t* state, int in_w, int in_h, int out_w, int out_h,
+                         const float* boxes, int n_boxes, aeon_aug_params* out)
+{
+    return guarded([&] {
+        if (!f || !state || !out || n_boxes < 0 || (n_boxes > 0 && !boxes)) fail(AEON_HIP_EINVAL, "null argument");
+        std::lock_guard<std::mutex> lock(f->mu);
+        TrackedEngine eng(*state);
+        f->f.make_ssd_params(eng, in_w, in_h, out_w, out_h, boxes, n_boxes, out);
+        *state = eng.last;
+        return 0;
+    });
+}
+
+int aeon_batch_sample_patches(aeon_param_factory* f, int sampler, uint32_t* state, const float* nboxes, int n,
+                              float* out, int cap, int* n_out)
+{
+    return guarded([&] {
+        if (!f || !state || !n_out || n < 0 || (n > 0 && !nboxes) || cap < 0 || (cap > 0 && !out))
+            fail(AEON_HIP_EINVAL, "null argument");
+        std::lock_guard<std::mutex> lock(f->mu);
+        if (sampler < 0 || sampler >= (int)f->f.batch_samplers.size()) fail(AEON_HIP_EINVAL, "sampler index out of range");
+        TrackedEngine     eng(*state);
+        std::vector<nbox> objects, samples;
+        for (int i = 0; i < n; i++)
+            objects.emplace_back(nboxes[4 * i], nboxes[4 * i + 1], nboxes[4 * i + 2], nboxes[4 * i + 3]);
+        f->f.batch_samplers[sampler].sample_patches(eng, objects, samples);
+        *n_out = (int)samples.size();
+        for (int i = 0; i < (int)samples.size() && i < cap; i++) {
+            out[4 * i] = samples[i].xmin, out[4 * i + 1] = samples[i].ymin;
+            out[4 * i + 2] = samples[i].xmax, out[4 * i + 3] = samples[i].ymax;
+        }
         *state = eng.last;
         return 0;
     });

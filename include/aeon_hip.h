@@ -77,6 +77,11 @@ typedef struct aeon_aug_params {
     float   contrast, brightness, saturation;
     int32_t hue;
     int32_t interp;                         /* AEON_INTERP_* */
+    /* image::expand (src/image.cpp:276-303; make_ssd_params, src/augment_image.cpp:246-273): with
+     * expand_ratio > 1 the (rotated) record is placed at (expand_x, expand_y) of a zeroed
+     * expand_w x expand_h canvas before resize_short / crop; 0 or 1 = no expand */
+    float   expand_ratio;
+    int32_t expand_x, expand_y, expand_w, expand_h;
 } aeon_aug_params;
 
 /* image::loader configuration (src/etl_image.cpp:204-244) plus the batch-buffer geometry of
@@ -175,6 +180,22 @@ int aeon_param_factory_destroy(aeon_param_factory* f);
  * making the calls in record order -- aeon's own deterministic order. */
 int aeon_make_params(aeon_param_factory* f, uint32_t* engine_state, int in_w, int in_h,
                      int out_w, int out_h, aeon_aug_params* out);
+/* param_factory::make_ssd_params (src/augment_image.cpp:232-301): make_params, then expand
+ * (expand_ratio / expand_probability) and -- crop_enable false -- a patch from the configured
+ * batch_samplers (sampler scale / aspect_ratio, sample_constraint jaccard / coverage bounds, max_sample,
+ * max_trials; src/augment_image.cpp:303-586) as the cropbox of the expanded image.  boxes: n_boxes
+ * object boxes (xmin, ymin, xmax, ymax; boundingbox::box pixel coordinates, xmax inclusive), may be
+ * NULL when n_boxes is 0.  Same engine and draw order as aeon, so the same state gives aeon's params. */
+int aeon_make_ssd_params(aeon_param_factory* f, uint32_t* engine_state, int in_w, int in_h, int out_w, int out_h,
+                         const float* boxes, int n_boxes, aeon_aug_params* out);
+
+/* batch_sampler::sample_patches (src/augment_image.cpp:567-586) of the factory's batch_samplers[sampler]
+ * over n normalized object boxes (xmin, ymin, xmax, ymax in [0, 1]) -- what aeon's tests call as
+ * factory.m_batch_samplers[i].sample_patches (test/test_augmentation.cpp:347-443).  Writes up to cap
+ * boxes to out (4 floats each) and the number of samples found to *n_out. */
+int aeon_batch_sample_patches(aeon_param_factory* f, int sampler, uint32_t* engine_state, const float* nboxes, int n,
+                              float* out, int cap, int* n_out);
+
 /* batch_decoder deterministic mode (src/batch_decoder.cpp:47-54): slot engine state words. */
 int aeon_seed_slots(uint32_t seed, int n, uint32_t* states);
 

@@ -14,6 +14,24 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "liboracle.so")
 
 
+class BatchSampler(ctypes.Structure):
+    _fields_ = [("max_sample", ctypes.c_int), ("max_trials", ctypes.c_int),
+                ("scale_min", ctypes.c_float), ("scale_max", ctypes.c_float),
+                ("ar_min", ctypes.c_float), ("ar_max", ctypes.c_float),
+                ("min_jaccard", ctypes.c_float), ("max_jaccard", ctypes.c_float),
+                ("min_sample_cov", ctypes.c_float), ("max_sample_cov", ctypes.c_float),
+                ("min_object_cov", ctypes.c_float), ("max_object_cov", ctypes.c_float)]
+
+
+def batch_sampler(max_sample=-1, max_trials=100, scale=(1.0, 1.0), aspect_ratio=(1.0, 1.0), **constraint):
+    nan = float("nan")
+    b = BatchSampler(max_sample=max_sample, max_trials=max_trials, scale_min=scale[0], scale_max=scale[1],
+                     ar_min=aspect_ratio[0], ar_max=aspect_ratio[1])
+    for k in ("min_jaccard", "max_jaccard", "min_sample_cov", "max_sample_cov", "min_object_cov", "max_object_cov"):
+        setattr(b, k, constraint.get(k, nan))
+    return b
+
+
 class AugConfig(ctypes.Structure):
     _fields_ = [
         ("scale_min", ctypes.c_float), ("scale_max", ctypes.c_float),
@@ -29,6 +47,9 @@ class AugConfig(ctypes.Structure):
         ("resize_short_size", ctypes.c_int), ("padding", ctypes.c_int),
         ("fixed_scaling_factor", ctypes.c_float),
         ("interp", ctypes.c_int),
+        ("expand_probability", ctypes.c_float), ("expand_ratio_min", ctypes.c_float),
+        ("expand_ratio_max", ctypes.c_float),
+        ("n_samplers", ctypes.c_int), ("samplers", BatchSampler * 4),
     ]
 
 
@@ -45,6 +66,8 @@ class Params(ctypes.Structure):
         ("contrast", ctypes.c_float), ("brightness", ctypes.c_float),
         ("saturation", ctypes.c_float), ("hue", ctypes.c_int),
         ("interp", ctypes.c_int),
+        ("expand_ratio", ctypes.c_float), ("expand_x", ctypes.c_int), ("expand_y", ctypes.c_int),
+        ("expand_w", ctypes.c_int), ("expand_h", ctypes.c_int),
     ]
 
     def as_dict(self):
@@ -81,6 +104,10 @@ def lib():
         L.orc_factory_destroy.argtypes = [ctypes.c_void_p]
         L.orc_make_params.argtypes = [ctypes.c_void_p, P(ctypes.c_uint32), ctypes.c_int, ctypes.c_int,
                                       ctypes.c_int, ctypes.c_int, P(Params)]
+        L.orc_make_ssd_params.argtypes = [ctypes.c_void_p, P(ctypes.c_uint32), ctypes.c_int, ctypes.c_int,
+                                          ctypes.c_int, ctypes.c_int, P(ctypes.c_float), ctypes.c_int, P(Params)]
+        L.orc_sample_patches.argtypes = [ctypes.c_void_p, ctypes.c_int, P(ctypes.c_uint32), P(ctypes.c_float),
+                                         ctypes.c_int, P(ctypes.c_float), ctypes.c_int, P(ctypes.c_int)]
         L.orc_seed_slots.argtypes = [ctypes.c_uint32, ctypes.c_int, P(ctypes.c_uint32)]
         L.orc_transform_image.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                           ctypes.c_int, P(Params), ctypes.c_void_p]
@@ -136,9 +163,15 @@ def aug_config(**kw):
                   contrast_min=1.0, contrast_max=1.0, brightness_min=1.0, brightness_max=1.0,
                   saturation_min=1.0, saturation_max=1.0, hue_min=0, hue_max=0,
                   flip_enable=0, center=1, crop_enable=1, do_area_scale=0,
-                  resize_short_size=0, padding=0, fixed_scaling_factor=-1.0, interp=0)
+                  resize_short_size=0, padding=0, fixed_scaling_factor=-1.0, interp=0,
+                  expand_probability=0.0, expand_ratio_min=1.0, expand_ratio_max=1.0, n_samplers=0)
     for k, v in kw.items():
-        setattr(c, k, v)
+        if k == "samplers":
+            c.n_samplers = len(v)
+            for i, b in enumerate(v):
+                c.samplers[i] = b
+        else:
+            setattr(c, k, v)
     return c
 
 
@@ -159,6 +192,29 @@ class Factory:
                                      ctypes.byref(p)))
         state[0] = st.value
         return p
+
+
+def make_ssd_params(factory, state, in_w, in_h, out_w, out_h, boxes=()):
+    """param_factory::make_ssd_params; boxes: (xmin, ymin, xmax, ymax) per object."""
+    p = Params()
+    st = ctypes.c_uint32(int(state[0]))
+    flat = (ctypes.c_float * max(1, 4 * len(boxes)))(*[v for b in boxes for v in b])
+    _check(lib().orc_make_ssd_params(factory._f, ctypes.byref(st), in_w, in_h, out_w, out_h, flat, len(boxes),
+                                     ctypes.byref(p)))
+    state[0] = st.value
+    return p
+
+
+def sample_patches(factory, sampler, state, nboxes, cap=4096):
+    """batch_sampler::sample_patches -> list of (xmin, ymin, xmax, ymax) normalized boxes."""
+    st = ctypes.c_uint32(int(state[0]))
+    flat = (ctypes.c_float * max(1, 4 * len(nboxes)))(*[v for b in nboxes for v in b])
+    out = (ctypes.c_float * (4 * cap))()
+    n = ctypes.c_int()
+    _check(lib().orc_sample_patches(factory._f, sampler, ctypes.byref(st), flat, len(nboxes), out, cap,
+                                    ctypes.byref(n)))
+    state[0] = st.value
+    return [tuple(out[4 * i:4 * i + 4]) for i in range(min(n.value, cap))]
 
 
 def seed_slots(seed, n):

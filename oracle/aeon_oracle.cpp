@@ -207,6 +207,65 @@ void make_params(const Factory& fc, Engine& eng, int in_w, int in_h, int out_w, 
     }
 }
 
+// ---- make_ssd_params (src/augment_image.cpp:232-586, normalized_box.cpp, boundingbox.cpp) ------
+// normalized_box::box: constructor rejects coordinates outside [0, 1] +- nervana::epsilon
+struct NBox {
+    float x0, y0, x1, y1;
+};
+NBox make_nbox(float x0, float y0, float x1, float y1)
+{
+    const float e  = 0.00001f;
+    auto        ok = [&](float v) { return v >= 0.0f - e && v <= 1.0f + e; };
+    if (!(ok(x0) && ok(x1) && ok(y0) && ok(y1))) throw std::invalid_argument("bounding box is not properly normalized");
+    return NBox{x0, y0, x1, y1};
+}
+float nbox_size(const NBox& b) { return (b.x1 < b.x0 || b.y1 < b.y0) ? 0.0f : (b.x1 - b.x0) * (b.y1 - b.y0); }
+NBox  nbox_intersect(const NBox& a, const NBox& b)
+{
+    if (b.x0 > a.x1 || b.x1 < a.x0 || b.y0 > a.y1 || b.y1 < a.y0) return NBox{0, 0, 0, 0};
+    return make_nbox(std::max(a.x0, b.x0), std::max(a.y0, b.y0), std::min(a.x1, b.x1), std::min(a.y1, b.y1));
+}
+float jaccard(const NBox& a, const NBox& b)
+{
+    float i = nbox_size(nbox_intersect(a, b));
+    return i == 0.f ? 0.f : i / (nbox_size(a) + nbox_size(b) - i);
+}
+float coverage_of(const NBox& own, const NBox& other)
+{
+    float i = nbox_size(nbox_intersect(own, other));
+    return i > 0 ? i / nbox_size(own) : 0.f;
+}
+bool satisfies(const orc_batch_sampler& bs, const NBox& s, const std::vector<NBox>& objs)
+{
+    auto       has = [](float v) { return v == v; };
+    const bool jac = has(bs.min_jaccard) || has(bs.max_jaccard);
+    const bool sc  = has(bs.min_sample_cov) || has(bs.max_sample_cov);
+    const bool oc  = has(bs.min_object_cov) || has(bs.max_object_cov);
+    if (!jac && !sc && !oc) return true;
+    bool found = false; // not reset per object: a partial pass on one object carries over
+    for (const NBox& o : objs) {
+        if (jac) {
+            float v = jaccard(s, o);
+            if ((has(bs.min_jaccard) && v < bs.min_jaccard) || (has(bs.max_jaccard) && v > bs.max_jaccard)) continue;
+            found = true;
+        }
+        if (sc) {
+            float v = coverage_of(s, o);
+            if ((has(bs.min_sample_cov) && v < bs.min_sample_cov) || (has(bs.max_sample_cov) && v > bs.max_sample_cov))
+                continue;
+            found = true;
+        }
+        if (oc) {
+            float v = coverage_of(o, s);
+            if ((has(bs.min_object_cov) && v < bs.min_object_cov) || (has(bs.max_object_cov) && v > bs.max_object_cov))
+                continue;
+            found = true;
+        }
+        if (found) return true;
+    }
+    return found;
+}
+
 // ---- a light u8 image view ------------------------------------------------------------------
 struct Img {
     int                  w = 0, h = 0, cn = 0, stride = 0;
@@ -635,10 +694,19 @@ Img transform_single_image(const Img& src, const orc_params& p)
         rot  = rotate(base, p.angle, true);
         base = Img::view(rot.data, rot.w, rot.h, rot.cn, rot.stride);
     }
+    Img ex;
+    if (p.expand_ratio > 1.0f) { // image::expand (image.cpp:276-303), etl_image.cpp:155-159
+        if (p.expand_x < 0 || p.expand_y < 0 || base.w + p.expand_x > p.expand_w || base.h + p.expand_y > p.expand_h)
+            throw std::invalid_argument("Invalid parameters to expand image");
+        ex = Img::alloc(p.expand_w, p.expand_h, base.cn);
+        for (int y = 0; y < base.h; y++)
+            std::memcpy(ex.row(y + p.expand_y) + (size_t)p.expand_x * base.cn, base.row(y), (size_t)base.w * base.cn);
+        base = Img::view(ex.data, ex.w, ex.h, ex.cn, ex.stride);
+    }
     Img rs;
     if (p.resize_short_size != 0) {
         int rw, rh;
-        resized_short_size(src.w, src.h, p.resize_short_size, &rw, &rh);
+        resized_short_size(base.w, base.h, p.resize_short_size, &rw, &rh);
         rs = Img::alloc(rw, rh, src.cn);
         if (p.interp == 1) resize_nearest(base, rs);
         else resize_linear(base, rs);
@@ -777,6 +845,87 @@ extern "C" {
 
 void* orc_factory_create(const orc_aug_config* cfg) { return new Factory(*cfg); }
 void  orc_factory_destroy(void* f) { delete (Factory*)f; }
+
+// sampler::sample_patch + batch_sampler::sample_patches (src/augment_image.cpp:359-395, 567-586)
+void sample_patches(const orc_batch_sampler& bs, Engine& e, const std::vector<NBox>& objs, std::vector<NBox>& samples)
+{
+    std::uniform_real_distribution<float> sd{bs.scale_min, bs.scale_max};
+    int found = 0;
+    for (unsigned t = 0; t < (unsigned)bs.max_trials; t++) {
+        if (bs.max_sample != -1 && found >= bs.max_sample) break;
+        float s   = sd(e);
+        float amn = std::max<float>(bs.ar_min, std::pow(s, 2.));
+        float amx = std::min<float>(bs.ar_max, 1 / std::pow(s, 2.));
+        float ar  = std::uniform_real_distribution<float>(amn, amx)(e);
+        float bw = s * std::sqrt(ar), bh = s / std::sqrt(ar);
+        float wo = std::uniform_real_distribution<float>(0.f, 1.f - bw)(e);
+        float ho = std::uniform_real_distribution<float>(0.f, 1.f - bh)(e);
+        NBox  nb = make_nbox(wo, ho, wo + bw, ho + bh);
+        if (satisfies(bs, nb, objs)) found++, samples.push_back(nb);
+    }
+}
+
+int orc_sample_patches(void* fp, int sampler, uint32_t* state, const float* nboxes, int n, float* out, int cap,
+                       int* n_out)
+{
+    return guarded([&] {
+        Factory& f = *(Factory*)fp;
+        if (sampler < 0 || sampler >= f.c.n_samplers) throw std::invalid_argument("sampler index");
+        Engine            e(*state);
+        std::vector<NBox> objs, samples;
+        for (int i = 0; i < n; i++) objs.push_back(make_nbox(nboxes[4 * i], nboxes[4 * i + 1], nboxes[4 * i + 2], nboxes[4 * i + 3]));
+        sample_patches(f.c.samplers[sampler], e, objs, samples);
+        *n_out = (int)samples.size();
+        for (int i = 0; i < (int)samples.size() && i < cap; i++) {
+            out[4 * i] = samples[i].x0, out[4 * i + 1] = samples[i].y0;
+            out[4 * i + 2] = samples[i].x1, out[4 * i + 3] = samples[i].y1;
+        }
+        *state = e.last;
+    });
+}
+
+int orc_make_ssd_params(void* fp, uint32_t* state, int in_w, int in_h, int out_w, int out_h, const float* boxes,
+                        int n_boxes, orc_params* out)
+{
+    return guarded([&] {
+        Factory& f = *(Factory*)fp;
+        Engine   e(*state);
+        make_params(f, e, in_w, in_h, out_w, out_h, out);
+        out->out_w = out_w, out->out_h = out_h;
+        std::uniform_real_distribution<float> ratio_d{f.c.expand_ratio_min, f.c.expand_ratio_max}, unit{0.0f, 1.0f};
+        float      ratio   = ratio_d(e);
+        const bool enabled = unit(e) < f.c.expand_probability;
+        if (ratio < 1.) throw std::invalid_argument("Expand ratio must be greater than 1.");
+        int ox = 0, oy = 0, ew = in_w, eh = in_h;
+        if (enabled) {
+            float fw = ratio * (float)in_w, fh = ratio * (float)in_h;
+            ew = (int)std::floor(fw), eh = (int)std::floor(fh);
+            float wo = unit(e) * (fw - (float)in_w);
+            float ho = unit(e) * (fh - (float)in_h);
+            ox = (int)std::floor(wo), oy = (int)std::floor(ho);
+        } else {
+            ratio = 1.0f;
+        }
+        out->expand_ratio = ratio, out->expand_x = ox, out->expand_y = oy, out->expand_w = ew, out->expand_h = eh;
+        std::vector<NBox> objs;
+        for (int i = 0; i < n_boxes; i++) {
+            const float* b = boxes + 4 * i;
+            if (b[2] + ox > ew || b[3] + oy > eh) throw std::invalid_argument("Invalid parameters to expand boundingbox");
+            objs.push_back(make_nbox((b[0] + ox) / ew, (b[1] + oy) / eh, (b[2] + ox + 1) / ew, (b[3] + oy + 1) / eh));
+        }
+        if (!f.c.crop_enable) {
+            std::vector<NBox> samples;
+            for (int k = 0; k < f.c.n_samplers; k++) sample_patches(f.c.samplers[k], e, objs, samples);
+            NBox patch{0, 0, 1, 1};
+            if (!samples.empty()) patch = samples[std::uniform_int_distribution<int>(0, (int)samples.size() - 1)(e)];
+            float x0 = patch.x0 * (float)ew, y0 = patch.y0 * (float)eh;
+            float x1 = patch.x1 * (float)ew - 1, y1 = patch.y1 * (float)eh - 1;
+            out->crop_x = (int)std::round(x0), out->crop_y = (int)std::round(y0);
+            out->crop_w = (int)std::round(x1 - x0 + 1), out->crop_h = (int)std::round(y1 - y0 + 1);
+        }
+        *state = e.last;
+    });
+}
 
 int orc_make_params(void* f, uint32_t* state, int in_w, int in_h, int out_w, int out_h,
                     orc_params* out)

@@ -20,6 +20,13 @@
 extern "C" {
 #endif
 
+/* batch_sampler (src/augment_image.hpp:343-378): sampler + sample_constraint (NaN = unset) */
+typedef struct orc_batch_sampler {
+    int   max_sample, max_trials;
+    float scale_min, scale_max, ar_min, ar_max;
+    float min_jaccard, max_jaccard, min_sample_cov, max_sample_cov, min_object_cov, max_object_cov;
+} orc_batch_sampler;
+
 /* augment::image::param_factory configuration (src/augment_image.hpp:141-246). */
 typedef struct orc_aug_config {
     float scale_min, scale_max;           /* "scale"                 */
@@ -34,6 +41,9 @@ typedef struct orc_aug_config {
     int   resize_short_size, padding;
     float fixed_scaling_factor;           /* -1 = unset */
     int   interp;                         /* 0 LINEAR, 1 NEAREST */
+    float expand_probability, expand_ratio_min, expand_ratio_max; /* make_ssd_params */
+    int   n_samplers;
+    orc_batch_sampler samplers[4];
 } orc_aug_config;
 
 /* augment::image::params (src/augment_image.hpp:99-119), the fields the image path reads. */
@@ -48,6 +58,8 @@ typedef struct orc_params {
     float contrast, brightness, saturation;
     int   hue;
     int   interp;
+    float expand_ratio;                   /* image::expand (> 1 = on) */
+    int   expand_x, expand_y, expand_w, expand_h;
 } orc_params;
 
 /* image::loader configuration (src/etl_image.cpp:204-244). */
@@ -66,6 +78,13 @@ void* orc_factory_create(const orc_aug_config* cfg);
 void  orc_factory_destroy(void* f);
 int   orc_make_params(void* f, uint32_t* engine_state, int in_w, int in_h, int out_w, int out_h,
                       orc_params* out);
+/* param_factory::make_ssd_params: boxes = n x (xmin, ymin, xmax, ymax) boundingbox::box. */
+int   orc_make_ssd_params(void* f, uint32_t* engine_state, int in_w, int in_h, int out_w, int out_h,
+                          const float* boxes, int n_boxes, orc_params* out);
+/* batch_sampler::sample_patches of configured sampler `sampler` over n normalized boxes
+ * (xmin, ymin, xmax, ymax); writes up to cap boxes to out, the count to *n_out. */
+int   orc_sample_patches(void* f, int sampler, uint32_t* engine_state, const float* nboxes, int n, float* out,
+                         int cap, int* n_out);
 /* aeon deterministic-mode slot seeding (src/batch_decoder.cpp:47-54): n engine states. */
 void  orc_seed_slots(uint32_t seed, int n, uint32_t* states);
 

@@ -31,6 +31,23 @@ def oracle_aug_config(aug):
         kw["fixed_scaling_factor"] = aug["fixed_scaling_factor"]
     if aug.get("interpolation_method", "LINEAR").upper() == "NEAREST":
         kw["interp"] = 1
+    if "expand_ratio" in aug:
+        kw["expand_ratio_min"], kw["expand_ratio_max"] = aug["expand_ratio"]
+    if "expand_probability" in aug:
+        kw["expand_probability"] = aug["expand_probability"]
+    samplers = []
+    for bs in aug.get("batch_samplers", []):
+        bs = bs or {}
+        sm, sc = bs.get("sampler") or {}, bs.get("sample_constraint") or {}
+        samplers.append(O.batch_sampler(max_sample=bs.get("max_sample", -1), max_trials=bs.get("max_trials", 100),
+                                        scale=tuple(sm.get("scale", (1.0, 1.0))),
+                                        aspect_ratio=tuple(sm.get("aspect_ratio", (1.0, 1.0))),
+                                        **{k + "_" + v: sc[k + "_" + w] for k in ("min", "max")
+                                           for v, w in (("jaccard", "jaccard_overlap"), ("sample_cov", "sample_coverage"),
+                                                        ("object_cov", "object_coverage"))
+                                           if k + "_" + w in sc}))
+    if samplers:
+        kw["samplers"] = samplers
     return O.aug_config(**kw)
 
 

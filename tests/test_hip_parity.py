@@ -547,3 +547,58 @@ def test_16bit_errors(ctx):
     with pytest.raises(A.AeonHipError, match="pixel masks / depth maps only"):
         ctx.augment_batch(descs, src.data_ptr(), [p], out, dst.data_ptr())
 
+
+
+def test_ssd_expand_records(ctx):
+    """make_ssd_params records (expand + batch-sampler crop + photometric, "use warping" 300x300):
+    image::expand (image.cpp:276-303) runs as a pre-pass before the crop/resize job."""
+    from tests.test_ssd import SSD_AUG, random_boxes
+    rng = np.random.default_rng(21)
+    f = A.ParamFactory(SSD_AUG)
+    states = A.seed_slots(5, 24)
+    imgs, params = [], []
+    for i in range(24):
+        w, h = int(rng.integers(40, 400)), int(rng.integers(40, 400))
+        imgs.append(A.synthetic_image(i, w, h, 3))
+        st = states[i:i + 1].copy()
+        params.append(f.make_ssd_params(st, w, h, 300, 300, random_boxes(rng, w, h, 3)))
+    assert any(p.expand_ratio > 1 for p in params) and any(p.expand_ratio == 1 for p in params)
+    for otype in ("uint8", "float32"):
+        out = A.out_desc(channels=3, channel_major=True, dtype=otype, item_stride=3 * 300 * 300 * 4)
+        _assert_same(H.hip_records(ctx, imgs, params, out), H.oracle_records(imgs, params, out), "ssd " + otype)
+
+
+@pytest.mark.parametrize("angle,rss", [(0, 0), (30, 0), (0, 200), (-90, 160)])
+def test_expand_with_rotation_and_resize_short(ctx, angle, rss):
+    """rotate -> expand -> resize_short -> crop (etl_image.cpp:146-170) with hand-built params;
+    masks of the same params ignore the expand (etl_pixel_mask.cpp:65-90)."""
+    rng = np.random.default_rng(angle + rss)
+    imgs, masks, params = [], [], []
+    for i in range(8):
+        w, h = int(rng.integers(60, 300)), int(rng.integers(60, 300))
+        imgs.append(A.synthetic_image(i, w, h, 3))
+        masks.append(A.synthetic_image(50 + i, w, h, 1))
+        ew, eh = int(w * 2.5), int(h * 2.5)
+        ox, oy = int(rng.integers(0, ew - w + 1)), int(rng.integers(0, eh - h + 1))
+        bw, bh = (ew, eh)
+        if rss:
+            s = rss / min(ew, eh)
+            bw, bh = (rss, int(round(eh * s))) if ew <= eh else (int(round(ew * s)), rss)
+        bw, bh = bw - 2, bh - 2  # margin for resize_short's rounding
+        cw, ch = int(rng.integers(16, min(bw, w) + 1)), int(rng.integers(16, min(bh, h) + 1))
+        params.append(A.aug_params(crop_x=int(rng.integers(0, bw - cw + 1)), crop_y=int(rng.integers(0, bh - ch + 1)),
+                                   crop_w=cw, crop_h=ch, out_w=96, out_h=80, angle=angle, flip=i % 2,
+                                   resize_short_size=rss, expand_ratio=2.5, expand_x=ox, expand_y=oy,
+                                   expand_w=ew, expand_h=eh))
+    out = A.out_desc(channels=3, channel_major=False, dtype="uint8", item_stride=3 * 96 * 80)
+    _assert_same(H.hip_records(ctx, imgs, params, out), H.oracle_records(imgs, params, out), "expand")
+    mparams = []
+    for m, p in zip(masks, params):  # mask crops must fit the un-expanded (rotated) record
+        q = A.aug_params(**{k: v for k, v in p.as_dict().items() if k != "lighting"})
+        q.crop_x, q.crop_y = 0, 0
+        q.crop_w, q.crop_h = min(p.crop_w, m.shape[1]), min(p.crop_h, m.shape[0])
+        q.resize_short_size = 0
+        mparams.append(q)
+    mout = A.out_desc(channels=1, channel_major=True, dtype="uint8", item_stride=96 * 80)
+    _assert_same(H.hip_records(ctx, masks, mparams, mout, mask=True),
+                 H.oracle_records(masks, mparams, mout, mask=True), "expand mask")
