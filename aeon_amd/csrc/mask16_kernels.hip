@@ -18,11 +18,20 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <string>
 
 #include "aug_job.hpp"
 #include "mask16.hpp"
 
 namespace aeon_hip {
+
+// Global (not flat) memory operations: a flat access also counts on the LDS counter, so waiting
+// for an LDS read (say, the address a load needs) would wait for every flat load in flight too.
+template <typename T>
+__device__ __forceinline__ __attribute__((address_space(1))) T* gptr(uint64_t a)
+{
+    return (__attribute__((address_space(1))) T*)a;
+}
 
 // 4 consecutive output elements of a row: one dword (uint8, saturated) or one 16-byte (float32)
 // store when the destination is aligned, element stores otherwise
@@ -32,32 +41,32 @@ __device__ __forceinline__ void store4(const Mask16Job& J, size_t o, int nk, con
         for (int k = 0; k < nk; k++) {
             const uint32_t x = v[k];
             switch (J.dtype) {
-            case OUT_S8: ((int8_t*)J.out_ptr)[o + k] = (int8_t)min(x, 127u); break;
-            case OUT_S16: ((int16_t*)J.out_ptr)[o + k] = (int16_t)min(x, 32767u); break;
-            case OUT_U16: ((uint16_t*)J.out_ptr)[o + k] = (uint16_t)x; break;
-            case OUT_S32: ((int32_t*)J.out_ptr)[o + k] = (int32_t)x; break;
-            default: ((double*)J.out_ptr)[o + k] = (double)x; break; // OUT_F64
+            case OUT_S8: gptr<int8_t>(J.out_ptr)[o + k] = (int8_t)min(x, 127u); break;
+            case OUT_S16: gptr<int16_t>(J.out_ptr)[o + k] = (int16_t)min(x, 32767u); break;
+            case OUT_U16: gptr<uint16_t>(J.out_ptr)[o + k] = (uint16_t)x; break;
+            case OUT_S32: gptr<int32_t>(J.out_ptr)[o + k] = (int32_t)x; break;
+            default: gptr<double>(J.out_ptr)[o + k] = (double)x; break; // OUT_F64
             }
         }
         return;
     }
     if (J.dtype == OUT_F32) {
         typedef float f32x4 __attribute__((ext_vector_type(4)));
-        float* dst = (float*)J.out_ptr + o;
-        if (nk == 4 && ((uintptr_t)dst & 15) == 0) {
+        const uint64_t dst = J.out_ptr + o * 4;
+        if (nk == 4 && (dst & 15) == 0) {
             const f32x4 q = {(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
-            __builtin_nontemporal_store(q, (f32x4*)dst);
+            __builtin_nontemporal_store(q, gptr<f32x4>(dst));
         } else {
-            for (int k = 0; k < nk; k++) dst[k] = (float)v[k];
+            for (int k = 0; k < nk; k++) gptr<float>(dst)[k] = (float)v[k];
         }
     } else {
-        uint8_t*       dst = (uint8_t*)J.out_ptr + o;
+        const uint64_t dst = J.out_ptr + o;
         const uint32_t b0 = min(v[0], 255u), b1 = min(v[1], 255u), b2 = min(v[2], 255u), b3 = min(v[3], 255u);
-        if (nk == 4 && ((uintptr_t)dst & 3) == 0) {
-            __builtin_nontemporal_store(b0 | (b1 << 8) | (b2 << 16) | (b3 << 24), (uint32_t*)dst);
+        if (nk == 4 && (dst & 3) == 0) {
+            __builtin_nontemporal_store(b0 | (b1 << 8) | (b2 << 16) | (b3 << 24), gptr<uint32_t>(dst));
         } else {
             const uint32_t b[4] = {b0, b1, b2, b3};
-            for (int k = 0; k < nk; k++) dst[k] = (uint8_t)b[k];
+            for (int k = 0; k < nk; k++) gptr<uint8_t>(dst)[k] = (uint8_t)b[k];
         }
     }
 }
@@ -85,7 +94,7 @@ __device__ __forceinline__ void nearest_rows(const Mask16Job& J, int y0, int y1)
             for (int r = 0; r < 8; r++) {
                 const int y   = min(yc + r, y1 - 1);
                 const int sy  = min((int)floor(y * J.scale_y), J.crop_h - 1);
-                const T*  row = (const T*)(src + (size_t)(J.crop_y + sy) * J.src_stride) + J.crop_x;
+                const auto row = gptr<const T>((uint64_t)(src + (size_t)(J.crop_y + sy) * J.src_stride)) + J.crop_x;
 #pragma unroll
                 for (int k = 0; k < 4; k++) v[r][k] = row[sx[k]];
             }
@@ -99,6 +108,186 @@ __device__ __forceinline__ void nearest_rows(const Mask16Job& J, int y0, int y1)
     }
 }
 
+// LDS-staged gather (the default): a workgroup owns `rows` output rows of one record.  Wave 0 maps
+// them to their source rows (sy = min(floor(y * ify), crop_h - 1), monotonic in y) and numbers the
+// distinct ones; the workgroup copies each distinct row's crop segment into LDS with aligned
+// 16-byte loads (a 16-byte-aligned block that holds one byte of the segment never leaves that
+// byte's page, so the over-read at both ends is always mapped), and every lane then gathers its 16
+// output columns from LDS and stores them as one 16-byte row piece.  Compared with the direct
+// gather above, the texture path sees one 16-byte load per 16 source bytes instead of one byte load
+// per output element, and one 16-byte store per 16 output bytes.
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+constexpr int kLoadsPerLane = 8; // 16-byte loads a lane keeps in flight before their LDS writes
+
+// The source rows of one block of output rows, as wave 0 numbered them.
+struct RowMap {
+    uint64_t addr[64]; // 16-byte-aligned start of each distinct row's segment
+    int      shift[64]; // segment start - addr
+    int      slot[64];  // output row -> distinct row
+    int      nslots, nrows, rec, y0;
+};
+
+// wave 0: rows [y0, y0 + nrows) of record `rec`
+__device__ __forceinline__ void map_rows(const Mask16Job& J, int rec, int y0, int nrows, RowMap& M)
+{
+    const int  tid   = threadIdx.x;
+    const int  eb    = J.src_elem;
+    const bool valid = tid < nrows;
+    const int  sy    = valid ? min((int)floor((y0 + tid) * J.scale_y), J.crop_h - 1) : -1;
+    const int  prev  = __shfl_up(sy, 1);
+    const bool fresh = valid && (tid == 0 || sy != prev);
+    const unsigned long long m    = __ballot(fresh);
+    const unsigned long long upto = tid == 63 ? ~0ull : ((2ull << tid) - 1);
+    const int                slot = __popcll(m & upto) - 1;
+    if (valid) M.slot[tid] = slot;
+    if (fresh) {
+        const uint64_t a = J.src_ptr + (uint64_t)(J.crop_y + sy) * J.src_stride + (uint64_t)J.crop_x * eb;
+        M.addr[slot]     = a & ~(uint64_t)15;
+        M.shift[slot]    = (int)(a & 15);
+    }
+    if (tid == 0) M.nslots = __popcll(m), M.nrows = nrows, M.rec = rec, M.y0 = y0;
+}
+
+__device__ __forceinline__ int seg_blocks(const Mask16Job& J) { return (15 + J.crop_w * J.src_elem + 15) >> 4; }
+
+// Source-row copy: thread t moves 16-byte blocks t, t + blockDim, ... of the concatenated row
+// segments (block i = row i / nblk, block i % nblk, the quotient through a float reciprocal: exact
+// while i / nblk < 2^12 as (i + 0.5) / nblk stays > 0.5 / nblk from an integer).  Each thread
+// issues kLoadsPerLane loads before their LDS writes; the loads are unconditional (clamped to the
+// last block) because a branch around each would make the compiler wait for it at the join.
+__device__ __forceinline__ void copy_rows(const RowMap& M, int nblk, int pitch, uint8_t* lds)
+{
+    const int   total = M.nslots * nblk;
+    const float rcp   = 1.0f / (float)nblk;
+    if (total <= 0) return;
+    for (int i0 = threadIdx.x; i0 < total; i0 += kLoadsPerLane * blockDim.x) {
+        u32x4 v[kLoadsPerLane];
+        int   at[kLoadsPerLane];
+#pragma unroll
+        for (int u = 0; u < kLoadsPerLane; u++) {
+            const int i = min(i0 + u * (int)blockDim.x, total - 1);
+            const int s = (int)(((float)i + 0.5f) * rcp), b = i - s * nblk;
+            v[u]        = __builtin_nontemporal_load(gptr<const u32x4>(M.addr[s] + (uint64_t)b * 16));
+            at[u]       = s * pitch + b * 16;
+        }
+#pragma unroll
+        for (int u = 0; u < kLoadsPerLane; u++)
+            if (i0 + u * (int)blockDim.x < total) *(u32x4*)(lds + at[u]) = v[u];
+    }
+}
+
+// 8-bit source, 8-bit output, and every 4 consecutive output columns of the lane drawn from 5
+// consecutive source bytes (horizontal scale < 4/3): per 4 outputs, one 8-byte LDS read pair and one
+// v_perm_b32 (selector = the 4 source bytes' positions in the pair) instead of 4 byte reads, 4
+// saturations and the packing.  Returns false when a lane's columns do not qualify.
+__device__ __forceinline__ bool gather_u8_perm(const Mask16Job& J, const RowMap& M, int pitch, const uint8_t* lds,
+                                               int x0, int r0, int rstep, const int (&sx)[16])
+{
+    int      lo[4];
+    uint32_t rel[4];
+    bool     ok = true;
+#pragma unroll
+    for (int w = 0; w < 4; w++) {
+        const int a = sx[4 * w], d = sx[4 * w + 3]; // ascending, or descending when flipped
+        lo[w]       = min(a, d);
+        ok          = ok && (max(a, d) - lo[w] <= 4);
+        rel[w]      = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) rel[w] |= (uint32_t)(sx[4 * w + k] - lo[w]) << (8 * k);
+    }
+    if (!ok) return false;
+    const uint32_t* lds32 = (const uint32_t*)lds;
+    for (int r = r0; r < M.nrows; r += rstep) {
+        const int s    = M.slot[r];
+        const int rowb = s * pitch + M.shift[s];
+        u32x4     q;
+#pragma unroll
+        for (int w = 0; w < 4; w++) {
+            const int      a   = rowb + lo[w];
+            const uint32_t sel = rel[w] + (uint32_t)(a & 3) * 0x01010101u;
+            q[w]               = __builtin_amdgcn_perm(lds32[(a >> 2) + 1], lds32[a >> 2], sel);
+        }
+        __builtin_nontemporal_store(q, gptr<u32x4>(J.out_ptr + (size_t)(M.y0 + r) * J.out_pitch + x0));
+    }
+    return true;
+}
+
+template <typename T>
+__device__ __forceinline__ void gather_rows(const Mask16Job& J, const RowMap& M, int pitch, const uint8_t* lds,
+                                            bool perm_ok)
+{
+    constexpr int eb    = sizeof(T);
+    constexpr int C     = 16; // output columns per lane
+    const int     tid   = threadIdx.x;
+    const int     nrows = M.nrows, y0 = M.y0;
+    const int     ng    = (J.out_w + C - 1) / C;
+    const int     per   = min(ng, (int)blockDim.x);
+    const int     rstep = blockDim.x / per;
+    const int     r0    = tid / per;
+    if (r0 >= rstep) return;
+    const bool u8out = J.dtype == OUT_U8;
+    for (int g = tid % per; g < ng; g += per) {
+        const int x0 = g * C;
+        const int nk = min(C, J.out_w - x0);
+        int       off[C];
+#pragma unroll
+        for (int k = 0; k < C; k++) {
+            const int x  = min(x0 + k, J.out_w - 1);
+            const int dx = J.flip ? J.out_w - 1 - x : x; // cv::flip(.., 1) after the resize
+            off[k]       = min((int)floor(dx * J.scale_x), J.crop_w - 1) * eb;
+        }
+        if (eb == 1 && u8out && nk == C && perm_ok && ((J.out_ptr + (size_t)y0 * J.out_pitch + x0) & 15) == 0 &&
+            (J.out_pitch & 15) == 0 && gather_u8_perm(J, M, pitch, lds, x0, r0, rstep, off))
+            continue;
+        for (int r = r0; r < nrows; r += rstep) {
+            const int      s    = M.slot[r];
+            const uint8_t* base = lds + s * pitch + M.shift[s];
+            uint32_t       v[C];
+#pragma unroll
+            for (int k = 0; k < C; k++) v[k] = *(const T*)(base + off[k]);
+            const size_t o = (size_t)(y0 + r) * J.out_pitch + x0;
+            if (u8out) {
+                const uint64_t dst = J.out_ptr + o;
+                if (nk == C && (dst & 15) == 0) {
+                    u32x4 q;
+#pragma unroll
+                    for (int w = 0; w < 4; w++)
+                        q[w] = min(v[4 * w], 255u) | (min(v[4 * w + 1], 255u) << 8) | (min(v[4 * w + 2], 255u) << 16) |
+                               (min(v[4 * w + 3], 255u) << 24);
+                    __builtin_nontemporal_store(q, gptr<u32x4>(dst));
+                    continue;
+                }
+            }
+#pragma unroll
+            for (int w = 0; w < 4; w++)
+                if (4 * w < nk) store4(J, o + 4 * w, min(4, nk - 4 * w), v + 4 * w);
+        }
+    }
+}
+
+__device__ __forceinline__ void gather_any(const Mask16Job& J, const RowMap& M, int pitch, const uint8_t* lds,
+                                           bool perm_ok)
+{
+    if (J.src_elem == 2) gather_rows<uint16_t>(J, M, pitch, lds, false);
+    else gather_rows<uint8_t>(J, M, pitch, lds, perm_ok);
+}
+
+// one block of rows per workgroup: grid (row blocks, records)
+__global__ __launch_bounds__(256) void nearest_staged(const Mask16Job* __restrict__ jobs, int rows_per_block, int pitch,
+                                                      int perm_ok)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds_rows[];
+    __shared__ RowMap M;
+    const Mask16Job& J  = jobs[blockIdx.y];
+    const int        y0 = blockIdx.x * rows_per_block;
+    if (y0 >= J.out_h) return;
+    if (threadIdx.x < 64) map_rows(J, blockIdx.y, y0, min(rows_per_block, J.out_h - y0), M);
+    __syncthreads();
+    copy_rows(M, seg_blocks(J), pitch, lds_rows);
+    __syncthreads();
+    gather_any(J, M, pitch, lds_rows, perm_ok != 0);
+}
+
 __global__ __launch_bounds__(256) void nearest_records(const Mask16Job* __restrict__ jobs, int rows_per_block)
 {
     const Mask16Job& J  = jobs[blockIdx.y];
@@ -109,10 +298,30 @@ __global__ __launch_bounds__(256) void nearest_records(const Mask16Job* __restri
     else nearest_rows<uint8_t>(J, y0, y1);
 }
 
-hipError_t launch_nearest(const Mask16Job* jobs, int n_jobs, int max_h, int max_w, hipStream_t stream,
-                          hipEvent_t start, hipEvent_t stop)
+hipError_t launch_nearest(const Mask16Job* jobs, int n_jobs, int max_h, int max_w, int max_seg_bytes,
+                          hipStream_t stream, hipEvent_t start, hipEvent_t stop)
 {
     if (n_jobs <= 0) return hipSuccess;
+    const int   pitch = (max_seg_bytes + 15 + 15) & ~15;
+    const char* env   = std::getenv("AEON_HIP_MASK_GATHER"); // experiments: "direct" = the old gather
+    const std::string mode = env ? env : "staged";
+    // staged: up to 64 output rows / ~32K output elements per workgroup, LDS <= 64 KB (C5 A/B:
+    // 64 rows 15.8 us, 32 rows 16.7, 16 rows 20.5, 8 rows 29.9; the direct gather 26.3)
+    int srows = std::min({64, 65536 / pitch, std::max(1, 32768 / std::max(1, max_w))});
+    if (srows >= 1 && mode != "direct") {
+        if (const char* e = std::getenv("AEON_HIP_NEAREST_ROWS")) srows = std::max(1, std::min(std::atoi(e), 64));
+        srows           = std::min(srows, std::max(1, 65536 / pitch));
+        const dim3 grid((max_h + srows - 1) / srows, n_jobs);
+        const size_t lds = (size_t)srows * pitch;
+        int perm = 1;
+        if (const char* e = std::getenv("AEON_HIP_MASK_PERM")) perm = std::atoi(e);
+        if (start || stop) {
+            void* args[4] = {(void*)&jobs, (void*)&srows, (void*)&pitch, (void*)&perm};
+            return hipExtLaunchKernel((const void*)nearest_staged, grid, dim3(256), args, lds, stream, start, stop, 0);
+        }
+        hipLaunchKernelGGL(nearest_staged, grid, dim3(256), lds, stream, jobs, srows, pitch, perm);
+        return hipGetLastError();
+    }
     // lanes = the widest record's 4-column groups (64..256); ~8K output pixels per workgroup
     const int groups  = (max_w + 3) / 4;
     const int threads = std::min(256, std::max(64, (groups + 63) / 64 * 64));

@@ -33,7 +33,7 @@ hipError_t launch_transpose(const void* src, void* dst, int64_t rows, int64_t co
                             hipStream_t stream);
 hipError_t launch_rotate(const RotJob* jobs, int n_jobs, int max_pixels, hipStream_t stream);
 hipError_t launch_expand(const ExpandJob* jobs, int n_jobs, int max_pixels, hipStream_t stream);
-hipError_t launch_nearest(const Mask16Job* jobs, int n_jobs, int max_h, int max_w, hipStream_t stream,
+hipError_t launch_nearest(const Mask16Job* jobs, int n_jobs, int max_h, int max_w, int max_seg_bytes, hipStream_t stream,
                           hipEvent_t start, hipEvent_t stop);
 hipError_t launch_upload_table(const void* host_dev, void* dst, size_t bytes, hipStream_t stream);
 hipError_t launch_plan_records(const void* host_records, void* jobs, const PlanArgs& a, hipStream_t stream);
@@ -969,11 +969,12 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
     size_t           blob      = exp_off + exp.size() * sizeof(ExpandJob);
     int              exp_max_px = 0;
     for (const ExpandJob& E : exp) exp_max_px = std::max(exp_max_px, E.ew * E.eh);
-    int              m16_max_h = 0, m16_max_w = 0;
+    int              m16_max_h = 0, m16_max_w = 0, m16_max_seg = 0;
     double           m16_bytes = 0; // algorithmic: crop read once + output written once
     for (const Mask16Job& M : m16) {
         m16_max_h = std::max(m16_max_h, M.out_h), m16_max_w = std::max(m16_max_w, M.out_w);
-        m16_bytes += (double)M.crop_w * M.crop_h * M.src_elem + (double)M.out_w * M.out_h * (M.dtype == 1 ? 4 : 1);
+        m16_max_seg = std::max(m16_max_seg, M.crop_w * M.src_elem);
+        m16_bytes += (double)M.crop_w * M.crop_h * M.src_elem + (double)M.out_w * M.out_h * out_elem_bytes(M.dtype);
     }
     int              rot_max_px = 0;
     for (const RotJob& R : rot) rot_max_px = std::max(rot_max_px, R.w * R.h);
@@ -1057,7 +1058,7 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
     if (!m16.empty()) {
         KernelTimer t{};
         if (timed) t = take_timer(ctx, KM_FINAL, m16_bytes);
-        HIP_OK(launch_nearest((const Mask16Job*)(table + m16_off), (int)m16.size(), m16_max_h, m16_max_w, stream,
+        HIP_OK(launch_nearest((const Mask16Job*)(table + m16_off), (int)m16.size(), m16_max_h, m16_max_w, m16_max_seg, stream,
                               timed ? t.start : nullptr, timed ? t.stop : nullptr));
         if (timed) ctx->timers.push_back(t);
     }
