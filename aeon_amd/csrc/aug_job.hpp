@@ -122,6 +122,16 @@ struct LaunchArgs {
     double         smean[3], sinv[3]; // sinv = 1/stddev, or 0 for stddev 0 (no division)
 };
 
+// Arguments of augment_contrast_fused (both passes of contrast records in one launch).
+struct FusedArgs {
+    LaunchArgs s, f;   // pass 1 (KM_STATS, LINEAR) and pass 2 (KM_FINAL, COPY + record table)
+    uint32_t*  done;   // per record (stats slot): pass-1 tiles published; zeroed before every launch
+    int32_t    n_rec;  // records = pass-1 jobs = pass-2 jobs, pass-2 job i reading stats slot i
+    int32_t    lag;    // records between a record's pass-1 and pass-2 tiles in the task order
+    int32_t    total;  // tasks = n_rec * (s.max_tiles + f.max_tiles)
+    int32_t    max_win_w, rows_per_tile, stage_bytes; // the shared LDS layout (max of both passes)
+};
+
 // KM_FINAL: a record through to the loader output.  KM_STATS: contrast pass 1 -- resize +
 // brightness/saturation + hue into an HWC uint8 intermediate plus exact per-chunk channel sums
 // (the mean cv::mean needs).  KM_RAW: resize only, HWC uint8 (resize_short pre-pass).

@@ -184,30 +184,54 @@ __device__ __forceinline__ void bs_apply(int kind, const BsRegs& R, int& b, int&
 // built on the host with HSV2RGB_f's own float operations, gives every t exactly (s*0 = 0,
 // s*1 = s, and 1-f rounded once as OpenCV does).  With s == 0 every t equals v exactly, so
 // OpenCV's s == 0 branch needs no special case.
-template <typename TAB, typename WTAB>
-__device__ __forceinline__ void hue_apply(TAB sdiv, TAB hdiv, WTAB wtab, int hue, int& b, int& g, int& r)
+#ifndef AEON_HIP_HUE_BATCH
+#define AEON_HIP_HUE_BATCH 2
+#endif
+constexpr int kHueBatch = AEON_HIP_HUE_BATCH; // pixels per hue_apply_n (1, 2 or 4)
+// Over N of a lane's 4 pixels at once: the 2N division-table reads (sdiv[v], hdiv[diff]) and
+// then the N weight-table reads are issued back to back, so one LDS latency is waited for per
+// group of reads instead of one per read (the per-pixel form waited three times per pixel).
+// `hue_small` = |hue| < 180 (uniform; the wrap is then one conditional subtraction).
+template <int N, int K0, typename TAB, typename WTAB>
+__device__ __forceinline__ void hue_apply_n(TAB sdiv, TAB hdiv, WTAB wtab, int hue, bool hue_small, int (&pxs)[4][3])
 {
-    int v = max(b, max(g, r)), vmin = min(b, min(g, r));
-    int diff = v - vmin;
-    int vr = v == r ? -1 : 0, vg = v == g ? -1 : 0;
-    // operands < 2^23 in magnitude (sdiv <= 255<<12, hdiv <= 30<<12, |h| <= 5*255)
-    int s = mad_i24(diff, sdiv[v], 1 << 11) >> 12;
-    int h = (vr & (g - b)) + (~vr & ((vg & (b - r + 2 * diff)) + ((~vg) & (r - g + 4 * diff))));
-    h = mad_i24(h, hdiv[diff], 1 << 11) >> 12;
-    h += h < 0 ? 180 : 0;
-    const int x = sat_u8(h) + hue; // H in [0, 180]
-    // C's % (truncating) then the uchar store; for |hue| < 180, x is in (-180, 360)
-    const int H = (hue > -180 && hue < 180 ? (x >= 180 ? x - 180 : x) : x % 180) & 0xff;
-
-    const f32x4 w  = wtab[H];
-    const float sf = (float)s * (1.f / 255), vf = (float)v * (1.f / 255);
-    const float bb = vf * (1.f - sf * w[0]);
-    const float gg = vf * (1.f - sf * w[1]);
-    const float rr = vf * (1.f - sf * w[2]);
-    // v, s in [0, 1] and w in [0, 1]: every product is in [0, 255], no saturation needed
-    b = u8rnd(bb * 255.f);
-    g = u8rnd(gg * 255.f);
-    r = u8rnd(rr * 255.f);
+    int (*px)[3] = pxs + K0; // pixels K0 .. K0 + N - 1
+    int v[N], diff[N], sd[N], hd[N];
+#pragma unroll
+    for (int k = 0; k < N; k++) {
+        const int b = px[k][0], g = px[k][1], r = px[k][2];
+        v[k]        = max(b, max(g, r));
+        diff[k]     = v[k] - min(b, min(g, r));
+    }
+#pragma unroll
+    for (int k = 0; k < N; k++) sd[k] = sdiv[v[k]], hd[k] = hdiv[diff[k]];
+    int   H[N];
+    float sf[N];
+#pragma unroll
+    for (int k = 0; k < N; k++) {
+        const int b = px[k][0], g = px[k][1], r = px[k][2];
+        const int vr = v[k] == r ? -1 : 0, vg = v[k] == g ? -1 : 0;
+        // operands < 2^23 in magnitude (sdiv <= 255<<12, hdiv <= 30<<12, |h| <= 5*255)
+        const int s = mad_i24(diff[k], sd[k], 1 << 11) >> 12;
+        int h = (vr & (g - b)) + (~vr & ((vg & (b - r + 2 * diff[k])) + ((~vg) & (r - g + 4 * diff[k]))));
+        h = mad_i24(h, hd[k], 1 << 11) >> 12;
+        h += h < 0 ? 180 : 0;
+        const int x = sat_u8(h) + hue; // H in [0, 180]
+        // C's % (truncating) then the uchar store; for |hue| < 180, x is in (-180, 360)
+        H[k]  = (hue_small ? (x >= 180 ? x - 180 : x) : x % 180) & 0xff;
+        sf[k] = (float)s * (1.f / 255);
+    }
+    f32x4 w[N];
+#pragma unroll
+    for (int k = 0; k < N; k++) w[k] = wtab[H[k]];
+#pragma unroll
+    for (int k = 0; k < N; k++) {
+        const float vf = (float)v[k] * (1.f / 255);
+        // v, s in [0, 1] and w in [0, 1]: every product is in [0, 255], no saturation needed
+        px[k][0] = u8rnd(vf * (1.f - sf[k] * w[k][0]) * 255.f);
+        px[k][1] = u8rnd(vf * (1.f - sf[k] * w[k][1]) * 255.f);
+        px[k][2] = u8rnd(vf * (1.f - sf[k] * w[k][2]) * 255.f);
+    }
 }
 
 // ---- source staging (LDS-DMA) ------------------------------------------------------------------
@@ -515,7 +539,10 @@ enum OutForm : int { OF_F32_CHW_VEC = 0, OF_GENERIC = 1 };
 // launch has OpenCV scalar-tail columns (3*dst_w not covered by the SIMD loops).
 
 
-template <int KM, int RM, bool PHOTO, int OF, bool TAIL>
+// IAUX: cache-policy bits of the uint8 intermediate's stores and of the contrast partial sums (16 =
+// sc1, write-through, when another workgroup of the same launch consumes them: the fused contrast
+// kernel below).
+template <int KM, int RM, bool PHOTO, int OF, bool TAIL, int IAUX = 0>
 struct Bands {
     const LaunchArgs& a;
     const LdsLayout&  L;
@@ -607,14 +634,18 @@ struct Bands {
     {
         return KM == KM_FINAL && PHOTO && a.has_rtab && J.cn == 3 && (J.photo & (PHOTO_CONTRAST | PHOTO_LIGHTING));
     }
-    __device__ __forceinline__ void record_table(const Info& f) const
+    // lds_shifts: the record's (1-c)*mean per channel in LDS (null: from a.shifts, contrast_reduce's)
+    __device__ __forceinline__ void record_table(const Info& f,
+                                                 const __attribute__((address_space(3))) double* lds_shifts = nullptr) const
     {
         if (!f.ok) return;
         cjob& J = job_ref(a, f.job);
         if (!uses_rtab(J)) return;
         const int photo = J.photo;
         double    sh[3] = {0, 0, 0};
-        if (photo & PHOTO_CONTRAST) {
+        if ((photo & PHOTO_CONTRAST) && lds_shifts) {
+            sh[0] = lds_shifts[0], sh[1] = lds_shifts[1], sh[2] = lds_shifts[2];
+        } else if (photo & PHOTO_CONTRAST) {
             const double* p = a.shifts + (size_t)J.stats_slot * 4;
             sh[0] = p[0], sh[1] = p[1], sh[2] = p[2];
         }
@@ -656,6 +687,9 @@ struct Bands {
             sh0 = sh[0], sh1 = sh[1], sh2 = sh[2];
         }
         uint32_t sum0 = 0, sum1 = 0, sum2 = 0;
+        const auto wtab      = lds_ptr<const f32x4>(L.hsv + 2048);
+        const int  hue       = (photo & PHOTO_HUE) ? J.hue : 0;
+        const bool hue_small = hue > -180 && hue < 180;
         BsRegs   bsr{};
         int      bs_kind = 0;
         if (PHOTO && (photo & PHOTO_BS)) bs_kind = J.bs_kind, bsr = bs_regs(J);
@@ -723,11 +757,21 @@ struct Bands {
                         }
                 }
                 if (PHOTO && photo) {
+                    if (photo & PHOTO_BS) {
+#pragma unroll
+                        for (int k = 0; k < 4; k++) bs_apply(bs_kind, bsr, val[k][0], val[k][1], val[k][2]);
+                    }
+                    if (photo & PHOTO_HUE) { // two pixels at a time: four cost 14 VGPRs (a wave per SIMD)
+                        hue_apply_n<kHueBatch, 0>(sdiv, hdiv, wtab, hue, hue_small, val);
+                        if (kHueBatch < 4) hue_apply_n<kHueBatch, kHueBatch % 4>(sdiv, hdiv, wtab, hue, hue_small, val);
+                        if (kHueBatch == 1) {
+                            hue_apply_n<1, 2>(sdiv, hdiv, wtab, hue, hue_small, val);
+                            hue_apply_n<1, 3>(sdiv, hdiv, wtab, hue, hue_small, val);
+                        }
+                    }
 #pragma unroll
                     for (int k = 0; k < 4; k++) {
                         int bb = val[k][0], gg = val[k][1], rr = val[k][2];
-                        if (photo & PHOTO_BS) bs_apply(bs_kind, bsr, bb, gg, rr);
-                        if (photo & PHOTO_HUE) hue_apply(sdiv, hdiv, lds_ptr<const f32x4>(L.hsv + 2048), J.hue, bb, gg, rr);
                         if (KM == KM_STATS) { // the intermediate keeps the post-hue pixel
                             if (k < nk) sum0 += bb, sum1 += gg, sum2 += rr;
                             val[k][0] = bb, val[k][1] = gg, val[k][2] = rr;
@@ -764,7 +808,7 @@ struct Bands {
                     const uint32_t w1 = v[1][1] | (v[1][2] << 8) | (v[2][0] << 16) | ((uint32_t)v[2][1] << 24);
                     const uint32_t w2 = v[2][2] | (v[3][0] << 8) | (v[3][1] << 16) | ((uint32_t)v[3][2] << 24);
                     const u32x3    q  = {w0, w1, w2};
-                    __builtin_amdgcn_raw_buffer_store_b96(q, orsrc, (y * win_w + ox0) * 3, 0, 0);
+                    __builtin_amdgcn_raw_buffer_store_b96(q, orsrc, (y * win_w + ox0) * 3, 0, IAUX);
                     continue;
                 }
                 if (KM == KM_RAW || KM == KM_STATS) { // HWC uint8, source channel order
@@ -775,7 +819,7 @@ struct Bands {
                         for (int c = 0; c < 3; c++)
                             if (k < nk && c < cn)
                                 __builtin_amdgcn_raw_buffer_store_b8((uint8_t)u8_of(val[k][c]), orsrc, base + k * cn + c,
-                                                                     0, 0);
+                                                                     0, IAUX);
                     continue;
                 }
                 // image::loader::load: source channel c goes to output channel oc (mixChannels
@@ -870,8 +914,12 @@ struct Bands {
             }
             const int lane = tid & 63;
             uint32_t* p    = a.partials + ((size_t)J.stats_slot * a.partial_stride + (size_t)band * 8) * 4;
-            if (lane == 0) p[wave * 4 + 0] = sum0, p[wave * 4 + 1] = sum1, p[wave * 4 + 2] = sum2;
-            if (wave == 0 && lane >= nw && lane < 8) p[lane * 4 + 0] = p[lane * 4 + 1] = p[lane * 4 + 2] = 0;
+            auto put = [&](uint32_t* q, uint32_t v) {
+                if (IAUX) __hip_atomic_store(q, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                else *q = v;
+            };
+            if (lane == 0) put(p + wave * 4 + 0, sum0), put(p + wave * 4 + 1, sum1), put(p + wave * 4 + 2, sum2);
+            if (wave == 0 && lane >= nw && lane < 8) put(p + lane * 4 + 0, 0), put(p + lane * 4 + 1, 0), put(p + lane * 4 + 2, 0);
         }
         // stores per wave when every lane is busy on whole rows of whole 4-pixel groups (one row
         // set of nrows / nph rows per lane): 3 per row for float32 planes, 1 (a 12-byte group)
@@ -882,8 +930,14 @@ struct Bands {
     }
 };
 
+// The contrast pass 1 with photometric stages (VALU-bound) is held to 80 VGPRs: 6 waves per SIMD =
+// three 512-lane workgroups per CU (at 85 VGPRs it gets two).
 template <int KM, int RM, bool PHOTO, int OF, bool TAIL>
-__global__ __launch_bounds__(kBlockMax, AEON_HIP_MIN_WAVES) void augment_tiles(LaunchArgs a)
+constexpr int kMinWaves = (KM == KM_STATS && PHOTO && !TAIL) ? 6 : AEON_HIP_MIN_WAVES;
+
+template <int KM, int RM, bool PHOTO, int OF, bool TAIL>
+__global__ __launch_bounds__(kBlockMax) __attribute__((amdgpu_waves_per_eu(kMinWaves<KM, RM, PHOTO, OF, TAIL>)))
+void augment_tiles(LaunchArgs a)
 {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     if ((uint32_t)(size_t)(__attribute__((address_space(3))) char*)smem != 0u) { // see lds_ld
@@ -1018,6 +1072,131 @@ __global__ __launch_bounds__(64) void contrast_reduce(LaunchArgs a, int n_jobs)
     }
 }
 
+// ---- contrast records in one launch -----------------------------------------------------------
+// Contrast needs the mean of the whole post-hue record, so a contrast record is two passes: pass 1
+// (STATS, VALU-bound: resize + brightness/saturation + hue into an HWC uint8 intermediate + exact
+// channel sums) and pass 2 (FINAL, memory-bound: record table + float32 CHW stores).  As two
+// launches they run back to back; here one persistent launch takes both kinds of tile from one
+// static task order in which record j's pass-2 tiles come `lag` records after its pass-1 tiles, so
+// at any moment some workgroups compute pass 1 while others stream pass 2.  Hand-off (placement-
+// independent, cdna_hip_programming.md Guideline 16): pass 1 stores the intermediate and the
+// partial sums write-through (sc1), every wave drains them, then one lane adds to the record's
+// counter; a pass-2 tile's wave 0 polls that counter (relaxed, bounded, s_sleep), one agent-scope
+// acquire, then the workgroup reduces the sums and reads the intermediate.  Progress: a workgroup
+// takes its tasks in increasing order and a pass-2 task depends only on lower-numbered pass-1
+// tasks, so with every workgroup resident the lowest unfinished task can always run.
+// task q -> (pass 2?, record, band)
+__device__ __forceinline__ void fused_task(const FusedArgs& A, int q, bool& second, int& rec, int& band)
+{
+    const int ms = A.s.max_tiles, mf = A.f.max_tiles, L = A.lag, n = A.n_rec;
+    const int head = L * ms;                 // records 0..L-1: pass 1 only
+    const int mid  = (n - L) * (ms + mf);    // then per record: pass 1 of j, pass 2 of j - L
+    if (q < head) {
+        second = false, rec = q / ms, band = q - rec * ms;
+    } else if (q < head + mid) {
+        const int r = q - head, blk = r / (ms + mf), off = r - blk * (ms + mf);
+        if (off < ms) second = false, rec = L + blk, band = off;
+        else second = true, rec = blk, band = off - ms;
+    } else {
+        const int r = q - head - mid;
+        second = true, rec = n - L + r / mf, band = r - (r / mf) * mf;
+    }
+}
+
+template <int OF2>
+__global__ __launch_bounds__(kBlockMax) __attribute__((amdgpu_waves_per_eu(6)))
+void augment_contrast_fused(FusedArgs A)
+{
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    if ((uint32_t)(size_t)(__attribute__((address_space(3))) char*)smem != 0u) { // see lds_ld
+        if (threadIdx.x == 0) atomicOr(A.s.error, 4);
+        return;
+    }
+    const int       tid = threadIdx.x, nt = blockDim.x;
+    const int       wave = __builtin_amdgcn_readfirstlane(tid >> 6), nw = nt >> 6;
+    // the record table sits in the staging area past pass 2's own staging footprint (pass-2 tiles
+    // stage fewer bytes than pass-1 tiles), which keeps three workgroups per CU
+    LdsLayout L = lds_layout(A.max_win_w, A.rows_per_tile, A.stage_bytes, true, 1, false);
+    L.rtab      = L.stage + A.f.stage_bytes;
+    const Bands<KM_STATS, RESIZE_LINEAR, true, OF_GENERIC, false, 16> WS{A.s, L, wave, nw};
+    const Bands<KM_FINAL, RESIZE_COPY, true, OF2, false>               WF{A.f, L, wave, nw};
+    const auto sh = lds_ptr<double>(L.pf); // the record's (1-c)*mean (the job-prefetch sink is unused here)
+    {
+        const auto lut = lds_ptr<float>(L.lut);
+        for (int i = tid; i < 3 * 256; i += nt) lut[i] = A.f.lut[i];
+        const auto hsv = lds_ptr<int32_t>(L.hsv);
+        for (int i = tid; i < kHsvWords; i += nt) hsv[i] = A.s.hsv_tables[i];
+    }
+    __syncthreads();
+    for (int q = blockIdx.x; q < A.total; q += gridDim.x) {
+        bool second;
+        int  rec, band;
+        fused_task(A, q, second, rec, band);
+        if (!second) {
+            const auto f = WS.info(rec * A.s.max_tiles + band);
+            __builtin_amdgcn_s_setprio(kComputePrio);
+            WS.issue(f, 0);
+            WS.tables(f, 0, true);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            WS.unpack(f, 0);
+            __syncthreads();
+            __builtin_amdgcn_s_setprio(kStagePrio);
+            WS.compute(f, 0);
+            // publish: every wave's write-through stores drained, then one counter add
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (tid == 0 && f.ok)
+                __hip_atomic_fetch_add(A.done + rec, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            continue;
+        }
+        const auto f = WF.info(rec * A.f.max_tiles + band);
+        if (f.ok) {
+            cjob& JF = job_ref(A.f, f.job);
+            cjob& JS = job_ref(A.s, JF.stats_slot);
+            if (tid == 0) {
+                const uint32_t need = (uint32_t)JS.tiles;
+                uint32_t       spins = 0;
+                while (__hip_atomic_load(A.done + JF.stats_slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
+                    __builtin_amdgcn_s_sleep(2);
+                    if (++spins > (1u << 24)) { // ~0.5 s: give up, flag it (never expected)
+                        atomicOr(A.s.error, 8);
+                        break;
+                    }
+                }
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            __syncthreads();
+            if (wave == 0) { // contrast_reduce for this record, into LDS
+                unsigned long long s0 = 0, s1 = 0, s2 = 0;
+                const uint32_t*    base = A.s.partials + (size_t)JF.stats_slot * A.s.partial_stride * 4;
+                for (int e = tid; e < JS.tiles * 8; e += 64) s0 += base[e * 4], s1 += base[e * 4 + 1], s2 += base[e * 4 + 2];
+                for (int o = 32; o > 0; o >>= 1) {
+                    s0 += __shfl_xor(s0, o);
+                    s1 += __shfl_xor(s1, o);
+                    s2 += __shfl_xor(s2, o);
+                }
+                if (tid == 0) {
+                    const double inv_n = 1. / (double)(JS.win_w * JS.win_h);
+                    const double k     = 1.0 - (double)JS.contrast;
+                    sh[0] = k * ((double)s0 * inv_n), sh[1] = k * ((double)s1 * inv_n), sh[2] = k * ((double)s2 * inv_n);
+                }
+            }
+            __syncthreads();
+        }
+        __builtin_amdgcn_s_setprio(kStagePrio);
+        WF.issue(f, 0);
+        WF.tables(f, 0, true);
+        WF.record_table(f, sh);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        WF.unpack(f, 0);
+        __syncthreads();
+        __builtin_amdgcn_s_setprio(kComputePrio);
+        WF.compute(f, 0);
+        lds_barrier();
+    }
+}
+
 // ---- host-side launch helpers (stage.cpp) ----------------------------------------------------
 typedef void (*KernelFn)(LaunchArgs);
 
@@ -1079,6 +1258,23 @@ hipError_t launch_contrast_reduce(const LaunchArgs& a, int n_jobs, hipStream_t s
 {
     hipLaunchKernelGGL(contrast_reduce, dim3(n_jobs), dim3(64), 0, stream, a, n_jobs);
     return hipGetLastError();
+}
+
+static const void* fused_fn(int of) { return of == OF_F32_CHW_VEC ? (const void*)augment_contrast_fused<OF_F32_CHW_VEC>
+                                                                   : (const void*)augment_contrast_fused<OF_GENERIC>; }
+
+hipError_t launch_contrast_fused(const FusedArgs& A, int grid, int threads, int lds_bytes, hipStream_t stream,
+                                 hipEvent_t start, hipEvent_t stop)
+{
+    void* args[1] = {(void*)&A};
+    if (start || stop)
+        return hipExtLaunchKernel(fused_fn(out_form(A.f)), dim3(grid), dim3(threads), args, lds_bytes, stream, start, stop, 0);
+    return hipLaunchKernel(fused_fn(out_form(A.f)), dim3(grid), dim3(threads), args, lds_bytes, stream);
+}
+
+hipError_t contrast_fused_occupancy(const FusedArgs& A, int threads, int lds_bytes, int* blocks)
+{
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, fused_fn(out_form(A.f)), threads, lds_bytes);
 }
 
 // Workgroups of this kernel form one CU holds at once (persistent grid sizing).

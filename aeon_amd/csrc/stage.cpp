@@ -28,6 +28,9 @@ hipError_t launch_tiles(int km, int rm, bool tail, bool photo, const LaunchArgs&
                         hipEvent_t start, hipEvent_t stop);
 hipError_t launch_contrast_reduce(const LaunchArgs& a, int n_jobs, hipStream_t stream);
 hipError_t kernel_occupancy(int km, int rm, bool tail, bool photo, const LaunchArgs& a, int* blocks);
+hipError_t launch_contrast_fused(const FusedArgs& A, int grid, int threads, int lds_bytes, hipStream_t stream,
+                                 hipEvent_t start, hipEvent_t stop);
+hipError_t contrast_fused_occupancy(const FusedArgs& A, int threads, int lds_bytes, int* blocks);
 hipError_t set_kernel_lds_limit(int bytes);
 hipError_t launch_transpose(const void* src, void* dst, int64_t rows, int64_t cols, int element_size,
                             hipStream_t stream);
@@ -152,6 +155,7 @@ struct LaunchPlan {
     bool                vec_ok = true;
     bool                has_hue = false, has_contrast = false;
     bool                rtab    = false; // final f32 launch with contrast / lighting: per-record LDS table
+    int                 force_threads = 0; // workgroup size imposed (the fused contrast launch)
 
     // launch shape for this->jobs, and each job's tile count
     void finalize()
@@ -186,6 +190,7 @@ struct LaunchPlan {
         // contrast pass 2 (photometric over the u8 intermediate, no resize): full workgroups
         // beat the fewest-idle-lanes choice (C3: 140 vs 158 us at 512 vs 448 lanes)
         if (rm == RESIZE_COPY && photo) threads = kBlockMax;
+        if (force_threads) threads = force_threads; // one launch with another plan's workgroups
         if (const char* e = std::getenv("AEON_HIP_THREADS"))
             threads = std::min(kBlockMax, std::max(kBlockMin, std::atoi(e) / 64 * 64));
         const int nph = threads / ncg;
@@ -515,6 +520,11 @@ struct aeon_hip_ctx {
     hipEvent_t           join_event     = nullptr;
     int                  overlap_chunks = 1, cap_pass1 = 2, cap_pass2 = 1; // off: measured slower
     bool                 tail_split     = false; // AEON_HIP_TAIL_SPLIT=1: measured slower
+    // contrast records' two passes in one launch (augment_contrast_fused, AEON_HIP_FUSED=1): measured
+    // slower than the pass-1 / reduce / pass-2 launches, so off.  fused_lag = records
+    // between a record's two passes in its task order.
+    int                  fused = 0, fused_lag = 256;
+    bool                 fused_reported = false;
     std::vector<int> open_slots; // used since the last completion event, on open_stream
     hipStream_t      open_stream = nullptr;
     // job tables go up on their own stream, so a call's H2D overlaps the previous call's kernels
@@ -980,11 +990,29 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
     for (const RotJob& R : rot) rot_max_px = std::max(rot_max_px, R.w * R.h);
     std::vector<int> slot_tiles(pass1_all.jobs.size(), 0);
     int              partial_stride = 1;
+    // both passes of the contrast records in one launch: every record a contrast record, one pass-1
+    // group (LINEAR, no scalar tail) and one pass-2 group (COPY with the record table), pass-2 job i
+    // reading stats slot i, and no second stream
+    LaunchPlan* f1 = nullptr;
+    LaunchPlan* f2 = nullptr;
+    {
+        int g1 = 0, g2 = 0;
+        for (LaunchPlan& P : pass1)
+            if (!P.jobs.empty()) g1++, f1 = &P;
+        for (LaunchPlan& P : main)
+            if (!P.jobs.empty()) g2++, f2 = &P;
+        bool ok = ctx->fused && !stream2 && g1 == 1 && g2 == 1 && f1->rm == RESIZE_LINEAR && !f1->tail &&
+                  f2->rm == RESIZE_COPY && f2->photo && o.dtype == AEON_DTYPE_F32 &&
+                  f1->jobs.size() == (size_t)n && f2->jobs.size() == (size_t)n;
+        for (int i = 0; ok && i < n; i++) ok = f2->jobs[i].stats_slot == i && f1->jobs[i].stats_slot == i;
+        if (!ok) f1 = f2 = nullptr;
+    }
     for (auto* v : {&pre, &pre2, &pass1, &main})
         for (LaunchPlan& P : *v) {
             if (P.jobs.empty()) continue;
             P.vec_ok = main_all.vec_ok;
             P.rtab   = v == &main && P.photo && o.dtype == AEON_DTYPE_F32;
+            if (&P == f2) P.force_threads = f1->threads;
             P.finalize();
             P.blob_off = blob;
             blob += P.jobs.size() * sizeof(AugJob);
@@ -1065,6 +1093,41 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
     for (auto* v : {&pre, &pre2})
         for (LaunchPlan& P : *v)
             if (!P.jobs.empty()) timed_launch(ctx, KM_RAW, P, args(P), stream, launch_bytes(P.jobs, KM_RAW, 1), timed);
+    if (f1) { // augment_contrast_fused: both passes, one launch
+        FusedArgs A{};
+        A.s = args(*f1), A.f = args(*f2);
+        A.s.split_base = A.s.total_tiles, A.s.split_parts = 1; // no tail split
+        A.f.split_base = A.f.total_tiles, A.f.split_parts = 1;
+        A.done  = (uint32_t*)s.shifts; // unused as shifts here: the per-record publish counters
+        A.n_rec = n;
+        A.lag   = std::min(n, ctx->fused_lag);
+        A.total = n * (A.s.max_tiles + A.f.max_tiles);
+        A.max_win_w     = std::max(f1->max_win_w, f2->max_win_w);
+        A.rows_per_tile = std::max(f1->tr, f2->tr);
+        A.stage_bytes   = std::max(f1->stage_bytes, f2->stage_bytes);
+        const LdsLayout FL = lds_layout(A.max_win_w, A.rows_per_tile, A.stage_bytes, true, 1, false);
+        const int lds = std::max(FL.total, FL.stage + f2->stage_bytes + 3 * 256 * 4); // + the record table
+        if (lds > kMaxLds) fail(AEON_HIP_EUNSUPPORTED, "fused contrast launch: LDS layout too large");
+        if (f1->threads != f2->threads) fail(AEON_HIP_ERUNTIME, "fused contrast launch: workgroup sizes differ");
+        int per_cu = 0;
+        HIP_OK(contrast_fused_occupancy(A, f1->threads, lds, &per_cu));
+        if (per_cu < 1) fail(AEON_HIP_ERUNTIME, "fused contrast launch does not fit a CU");
+        const int grid = std::min(A.total, per_cu * ctx->n_cu); // every workgroup resident (progress)
+        if (ctx->host_profile && !ctx->fused_reported) {
+            ctx->fused_reported = true;
+            std::fprintf(stderr, "[aeon_hip] fused contrast: %d threads, %d B LDS, TR %d/%d, %d workgroups/CU, %d tasks\n",
+                         f1->threads, lds, f1->tr, f2->tr, per_cu, A.total);
+        }
+        HIP_OK(hipMemsetAsync(A.done, 0, ((size_t)n * 4 + 15) & ~(size_t)15, stream));
+        KernelTimer t{};
+        if (timed) t = take_timer(ctx, KM_FINAL, launch_bytes(f1->jobs, KM_STATS, oelem) + launch_bytes(f2->jobs, KM_FINAL, oelem));
+        HIP_OK(launch_contrast_fused(A, grid, f1->threads, lds, stream, timed ? t.start : nullptr, timed ? t.stop : nullptr));
+        if (timed) ctx->timers.push_back(t);
+        phase(6);
+        release_slot(ctx, slot, stream);
+        phase(7);
+        return 0;
+    }
     for (LaunchPlan& P : pass1)
         if (!P.jobs.empty())
             timed_launch(ctx, KM_STATS, P, args(P), stream, launch_bytes(P.jobs, KM_STATS, oelem), timed, cap1);
@@ -1167,6 +1230,8 @@ int aeon_hip_ctx_create(int device, aeon_hip_ctx** out)
             HIP_OK(hipEventCreateWithFlags(&c->join_event, hipEventDisableTiming));
             if (const char* e = std::getenv("AEON_HIP_OVERLAP_CHUNKS")) c->overlap_chunks = std::max(1, std::atoi(e));
             if (const char* e = std::getenv("AEON_HIP_TAIL_SPLIT")) c->tail_split = std::atoi(e) != 0;
+            if (const char* e = std::getenv("AEON_HIP_FUSED")) c->fused = std::atoi(e);
+            if (const char* e = std::getenv("AEON_HIP_FUSED_LAG")) c->fused_lag = std::max(1, std::atoi(e));
             if (const char* e = std::getenv("AEON_HIP_CAP_PASS1")) c->cap_pass1 = std::max(0, std::atoi(e));
             if (const char* e = std::getenv("AEON_HIP_CAP_PASS2")) c->cap_pass2 = std::max(0, std::atoi(e));
             if (const char* e = std::getenv("AEON_HIP_HOST_PROFILE")) c->host_profile = std::atoi(e) != 0;
@@ -1306,7 +1371,8 @@ int aeon_hip_synchronize(aeon_hip_ctx* ctx, void* stream)
         if (err != 0) {
             HIP_OK(hipMemset(ctx->d_error, 0, sizeof(int32_t)));
             fail(AEON_HIP_EDEVICE, "device error word " + std::to_string(err) +
-                                       " (LDS staging footprint exceeded)");
+                                       ((err & 8) ? " (fused contrast launch: a pass-2 tile gave up waiting for pass 1)"
+                                                  : " (LDS staging footprint exceeded)"));
         }
         return 0;
     });

@@ -602,3 +602,23 @@ def test_expand_with_rotation_and_resize_short(ctx, angle, rss):
     mout = A.out_desc(channels=1, channel_major=True, dtype="uint8", item_stride=96 * 80)
     _assert_same(H.hip_records(ctx, masks, mparams, mout, mask=True),
                  H.oracle_records(masks, mparams, mout, mask=True), "expand mask")
+
+
+def test_c3_fused_launch_matches_oracle(ctx, monkeypatch):
+    """AEON_HIP_FUSED=1 (augment_contrast_fused: both contrast passes in one launch, pass-2 tiles
+    waiting on per-record counters): every record of a 1024-record C3 batch equals the oracle."""
+    monkeypatch.setenv("AEON_HIP_FUSED", "1")
+    monkeypatch.setenv("AEON_HIP_FUSED_LAG", "64")
+    c = A.Context(0)
+    try:
+        imgs = _synthetic(64)
+        idx = np.random.default_rng(2).integers(0, len(imgs), 1024)
+        srcs = [imgs[i] for i in idx]
+        params = H.draw_params(C.C3_AUG, [(256, 256)] * len(srcs), 224, 224, seed=17)
+        out = A.out_desc(**MEAN_OUT)
+        hip = H.hip_records(c, srcs, params, out)
+        sel = list(range(0, 1024, 7)) + [1023]
+        _assert_same([hip[i] for i in sel], H.oracle_records([srcs[i] for i in sel], [params[i] for i in sel], out),
+                     "C3 fused")
+    finally:
+        c.close()
