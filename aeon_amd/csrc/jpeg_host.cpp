@@ -34,12 +34,21 @@ const uint8_t kZigzagToNatural[80] = {
     6,  7,  14, 21, 28, 35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51, 58, 59, 52, 45, 38, 31,
     39, 46, 53, 60, 61, 54, 47, 55, 62, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63};
 
+inline int extend(int v, int s) { return v < (1 << (s - 1)) ? v - (1 << s) + 1 : v; }
+
+// AC fast table (10-bit lookahead): a code of L bits whose symbol (run r, size z) and value bits fit
+// in the 10 (L + z <= 10) decodes in one lookup.  Entry: bits 0-4 bits consumed, 5-8 run, 9-10 kind
+// (kAcValue: value in bits 16-31; kAcEob; kAcZrl), 0 = take the general path.
+constexpr int      kAcFastBits = 10;
+constexpr uint32_t kAcValue = 1u << 9, kAcEob = 2u << 9, kAcZrl = 3u << 9;
+
 // Canonical Huffman table with a 9-bit lookahead (libjpeg's jdhuff.c scheme).
 struct Huffman {
     bool     set = false;
     uint16_t look[512]; // (length << 8) | symbol for codes of <= 9 bits, 0 otherwise
     int32_t  maxcode[18], valptr[17], mincode[17];
     uint8_t  vals[256];
+    uint32_t fast[1 << kAcFastBits]; // AC tables: see kAcFastBits
 
     void build(const uint8_t* counts, const uint8_t* symbols, int n)
     {
@@ -57,12 +66,36 @@ struct Huffman {
             code <<= 1;
         }
         maxcode[17] = 0x7fffffff;
-        set         = true;
+        // AC fast entries: every 10-bit window starting with a code of <= 10 bits
+        std::memset(fast, 0, sizeof(fast));
+        code = 0, k = 0;
+        for (int l = 1; l <= kAcFastBits; l++) {
+            for (int i = 0; i < counts[l - 1]; i++, k++, code++) {
+                const int sym = vals[k], r = sym >> 4, z = sym & 15;
+                for (int f = 0; f < (1 << (kAcFastBits - l)); f++) {
+                    uint32_t e = 0;
+                    if (sym == 0x00) e = kAcEob | (uint32_t)l;
+                    else if (sym == 0xF0) e = kAcZrl | (uint32_t)l;
+                    else if (z && l + z <= kAcFastBits) {
+                        const int bits = (f >> (kAcFastBits - l - z)) & ((1 << z) - 1);
+                        e = kAcValue | (uint32_t)(l + z) | ((uint32_t)r << 5) |
+                            ((uint32_t)(uint16_t)(int16_t)extend(bits, z) << 16);
+                    }
+                    fast[(code << (kAcFastBits - l)) | f] = e;
+                }
+            }
+            code <<= 1;
+        }
+        set = true;
     }
 };
 
 // Entropy-coded segment reader: 64-bit buffer, 0xFF00 unstuffing; a marker ends the supply (zeros
-// follow, as libjpeg's fill_bit_buffer does), running off the end of the file is an error.
+// follow, as libjpeg's fill_bit_buffer does), running off the end of the file is an error.  fill()
+// tops the buffer up to at least 57 bits once fewer than 32 are left, so one symbol (<= 16 bits)
+// and its value bits (<= 16) follow without another check; eight bytes free of 0xFF go in with
+// one load.  Every member that touches the
+// state is inlined (nothing takes the reader's address), so a scan keeps it in registers.
 struct Bits {
     const uint8_t* p;
     const uint8_t* end;
@@ -70,9 +103,24 @@ struct Bits {
     int            n      = 0;
     bool           marker = false;
 
-    void fill()
+    [[gnu::always_inline]] void fill()
     {
-        while (n <= 56) {
+        if (n >= 32) return; // enough for one symbol and its value bits
+        if (!marker && end - p >= 8) {
+            uint64_t w;
+            std::memcpy(&w, p, 8);
+            w                = __builtin_bswap64(w); // the next 8 bytes, first in the top byte
+            const uint64_t x = ~w;                   // a 0xFF byte of w = a zero byte of x
+            if (__builtin_expect(!((x - 0x0101010101010101ull) & ~x & 0x8080808080808080ull), 1)) {
+                const int      k   = (64 - n) >> 3; // whole bytes that fit
+                const uint64_t top = k == 8 ? w : (w >> (64 - 8 * k)) << (64 - 8 * k);
+                buf |= top >> n;
+                n += 8 * k;
+                p += k;
+                return;
+            }
+        }
+        while (n <= 56) { // byte by byte: stuffing, markers, the end of the data
             uint64_t b = 0;
             if (!marker) {
                 if (p >= end) bad("truncated scan data");
@@ -89,33 +137,34 @@ struct Bits {
             n += 8;
         }
     }
-    uint32_t get(int k) // k in 1..16
+    // k in 1..16 bits; the caller has filled since the last symbol
+    [[gnu::always_inline]] uint32_t get(int k)
     {
-        if (n < k) fill();
         const uint32_t v = (uint32_t)(buf >> (64 - k));
         buf <<= k;
         n -= k;
         return v;
     }
-    int decode(const Huffman& t)
+    // codes longer than 9 bits (the lookahead's miss): (symbol, length)
+    [[gnu::noinline]] static uint32_t decode_long(const Huffman& t, uint64_t buf)
     {
-        if (n < 16) fill();
-        const uint16_t e = t.look[buf >> 55];
-        if (e) {
-            buf <<= e >> 8;
-            n -= e >> 8;
-            return e & 0xff;
-        }
         int l = 10;
         while (l <= 16 && (int32_t)(buf >> (64 - l)) > t.maxcode[l]) l++;
         if (l > 16) bad("corrupt Huffman code");
         const int code = (int)(buf >> (64 - l));
-        buf <<= l;
-        n -= l;
-        return t.vals[t.valptr[l] + code - t.mincode[l]];
+        return (uint32_t)t.vals[t.valptr[l] + code - t.mincode[l]] | ((uint32_t)l << 8);
+    }
+    [[gnu::always_inline]] int decode(const Huffman& t)
+    {
+        fill();
+        uint32_t e = t.look[buf >> 55];
+        if (!e) e = decode_long(t, buf);
+        buf <<= e >> 8;
+        n -= e >> 8;
+        return e & 0xff;
     }
     // RSTn: drop buffered bits, skip to just past the marker
-    void restart()
+    [[gnu::always_inline]] void restart()
     {
         buf = 0, n = 0, marker = false;
         while (p + 1 < end && !(p[0] == 0xFF && p[1] >= 0xD0 && p[1] <= 0xD7)) p++;
@@ -123,12 +172,9 @@ struct Bits {
     }
 };
 
-inline int extend(int v, int s) { return v < (1 << (s - 1)) ? v - (1 << s) + 1 : v; }
-
 struct Comp {
     int id = 0, h = 1, v = 1, tq = 0, td = 0, ta = 0;
     int bw = 0, bh = 0, dw = 0, dh = 0;
-    int pred = 0;
 };
 
 // Header of one file (and, once decoded, where its streams sit in the worker's arena).
@@ -208,6 +254,59 @@ void parse_frame(const uint8_t* d, size_t size, Frame& f, const uint8_t** after)
 
 // Decode one file: the frame's block records (per component, bh x bw, in the arena) and values.
 // Returns the byte offsets in `a` of each component's records and of the values.
+// One 8x8 block of a Huffman scan: its non-zero coefficients appended to vals (zigzag order) and
+// their zigzag positions as the returned mask.  Inlined into the scan loops with the reader a
+// local there, so the bit buffer stays in registers.
+[[gnu::always_inline]] inline uint64_t decode_block(Bits& b, const Huffman& dct, const Huffman& act, int& pred,
+                                                    int16_t* vals, uint32_t& nv)
+{
+    uint64_t  mask = 0;
+    const int sdc  = b.decode(dct);
+    if (sdc > 15) bad("corrupt DC coefficient");
+    pred += sdc ? extend((int)b.get(sdc), sdc) : 0;
+    const int16_t dcv = (int16_t)pred;
+    if (dcv) mask |= 1, vals[nv++] = dcv;
+    for (int k = 1; k < 64;) {
+        b.fill();
+        const uint32_t e    = act.fast[b.buf >> (64 - kAcFastBits)];
+        const uint32_t kind = e & (3u << 9);
+        int            v;
+        if (kind == kAcValue) { // code + value bits in one lookup
+            const int used = e & 31;
+            b.buf <<= used;
+            b.n -= used;
+            k += (e >> 5) & 15;
+            v = (int16_t)(e >> 16);
+        } else if (e) { // EOB / ZRL
+            b.buf <<= (e & 31);
+            b.n -= (e & 31);
+            if (kind == kAcEob) break;
+            k += 16;
+            continue;
+        } else {
+            const int rs = b.decode(act), r = rs >> 4, sz = rs & 15;
+            if (!sz) {
+                if (r != 15) break;
+                k += 16;
+                continue;
+            }
+            k += r;
+            v = extend((int)b.get(sz), sz);
+        }
+        if (k < 63) {
+            mask |= 1ull << k;
+            vals[nv++] = (int16_t)v;
+        } else if (mask >> 63 & 1) { // libjpeg's natural-order table clamps overruns to 63:
+            vals[nv - 1] = (int16_t)v; // only that last value can repeat
+        } else {
+            mask |= 1ull << 63;
+            vals[nv++] = (int16_t)v;
+        }
+        k++;
+    }
+    return mask;
+}
+
 void decode_file(const uint8_t* d, size_t size, Frame& f, Arena& a, size_t blk_off[3], size_t* val_off, bool luma_only)
 {
     const uint8_t* p = nullptr;
@@ -313,66 +412,50 @@ void decode_file(const uint8_t* d, size_t size, Frame& f, Arena& a, size_t blk_o
         p += len;
         any_scan = true;
         Bits br{p, end};
-        for (int k = 0; k < f.ncomp; k++) f.c[k].pred = 0;
         int16_t*  vals = (int16_t*)(a.host.data() + *val_off); // (no reallocation below: reserved)
-        auto      block = [&](Comp& c, JpegBlock* recs, int bx, int by) {
-            JpegBlock& R = recs[(size_t)by * c.bw + bx];
-            uint64_t   mask = 0;
-            const uint32_t first = nvals;
-            int        sdc  = br.decode(dc[c.td]);
-            if (sdc > 15) bad("corrupt DC coefficient");
-            c.pred += sdc ? extend((int)br.get(sdc), sdc) : 0;
-            const int16_t dcv = (int16_t)c.pred;
-            if (dcv) mask |= 1, vals[nvals++] = dcv;
-            for (int k = 1; k < 64;) {
-                const int rs = br.decode(ac[c.ta]), r = rs >> 4, sz = rs & 15;
-                if (sz) {
-                    k += r;
-                    const int16_t v  = (int16_t)extend((int)br.get(sz), sz);
-                    const int     kk = std::min(k, 63); // libjpeg's natural-order table clamps overruns
-                    if (mask >> kk & 1) vals[nvals - 1] = v; // (only kk = 63 can repeat: the last value)
-                    else {
-                        mask |= 1ull << kk;
-                        vals[nvals++] = v;
-                    }
-                    k++;
-                } else if (r == 15) {
-                    k += 16;
-                } else {
-                    break;
-                }
-            }
-            // a block coded twice (corrupt / duplicate scans) keeps the later values
-            R.mask    = mask;
-            R.val_off = first;
-        };
-        int done = 0;
+        // a block coded twice (corrupt / duplicate scans) keeps the later values
+        uint32_t nv   = nvals;
+        int      done = 0, left = restart; // MCUs until the next restart marker
         if (ns == 1) {
-            Comp&      c    = f.c[sc[0]];
-            JpegBlock* recs = (JpegBlock*)(a.host.data() + blk_off[sc[0]]);
-            const int  nx = (c.dw + 7) / 8, ny = (c.dh + 7) / 8;
+            Comp&          c    = f.c[sc[0]];
+            JpegBlock*     recs = (JpegBlock*)(a.host.data() + blk_off[sc[0]]);
+            const Huffman& dct = dc[c.td];
+            const Huffman& act = ac[c.ta];
+            const int      nx = (c.dw + 7) / 8, ny = (c.dh + 7) / 8;
+            int            pred = 0;
             for (int by = 0; by < ny; by++)
                 for (int bx = 0; bx < nx; bx++) {
-                    if (restart && done && done % restart == 0) br.restart(), c.pred = 0;
-                    block(c, recs, bx, by);
-                    done++;
+                    if (restart && done && left == 0) br.restart(), pred = 0, left = restart;
+                    JpegBlock& R = recs[(size_t)by * c.bw + bx];
+                    R.val_off    = nv;
+                    R.mask       = decode_block(br, dct, act, pred, vals, nv);
+                    done++, left--;
                 }
         } else {
+            int pred[3] = {0, 0, 0};
             for (int my = 0; my < f.mcuy; my++)
                 for (int mx = 0; mx < f.mcux; mx++) {
-                    if (restart && done && done % restart == 0) {
+                    if (restart && done && left == 0) {
                         br.restart();
-                        for (int k = 0; k < f.ncomp; k++) f.c[k].pred = 0;
+                        pred[0] = pred[1] = pred[2] = 0;
+                        left = restart;
                     }
                     for (int i = 0; i < ns; i++) {
-                        Comp&      c    = f.c[sc[i]];
-                        JpegBlock* recs = (JpegBlock*)(a.host.data() + blk_off[sc[i]]);
+                        Comp&          c    = f.c[sc[i]];
+                        JpegBlock*     recs = (JpegBlock*)(a.host.data() + blk_off[sc[i]]);
+                        const Huffman& dct = dc[c.td];
+                        const Huffman& act = ac[c.ta];
                         for (int y = 0; y < c.v; y++)
-                            for (int x = 0; x < c.h; x++) block(c, recs, mx * c.h + x, my * c.v + y);
+                            for (int x = 0; x < c.h; x++) {
+                                JpegBlock& R = recs[(size_t)(my * c.v + y) * c.bw + mx * c.h + x];
+                                R.val_off    = nv;
+                                R.mask       = decode_block(br, dct, act, pred[i], vals, nv);
+                            }
                     }
-                    done++;
+                    done++, left--;
                 }
         }
+        nvals = nv;
         if (nvals > nblocks * 64) bad("coefficient overflow");
         // continue after the scan's data: the next marker that is not RSTn
         p = br.p;
