@@ -6,30 +6,30 @@
 // scalar loads.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "plan_record.hpp"
 
 namespace aeon_hip {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-// A workgroup of 128 lanes plans 16 records: the lanes bring the records' 16-byte pieces (2.25 KiB)
-// over PCIe (many lanes and workgroups keep many reads in flight: with one lane reading a
-// whole record the kernel took 11.8 us for 256 records, against 5.2 us for a 64 KiB table upload);
-// lanes 0-15 plan one record each into LDS; all 128 lanes store the 16 jobs (4 KiB) 16 bytes apiece.
-constexpr int kPlanPerBlock = 16;
-
-__global__ __launch_bounds__(128) void plan_records(const PlanRecord* host_records, AugJob* __restrict__ jobs,
-                                                    PlanArgs a)
+// A workgroup plans PER records: its lanes bring the records' 16-byte pieces over PCIe (many lanes
+// and workgroups keep many reads in flight: with one lane reading a whole record the kernel took
+// 11.8 us for 256 records, against 5.2 us for a 64 KiB table upload); lanes 0..PER-1 plan one record
+// each into LDS; all lanes store the jobs 16 bytes apiece.
+template <int PER, int LANES>
+__global__ __launch_bounds__(LANES) void plan_records(const PlanRecord* host_records, AugJob* __restrict__ jobs, PlanArgs a)
 {
-    __shared__ u32x4 recs[kPlanPerBlock * kPlanRecordPieces];
-    __shared__ u32x4 out[kPlanPerBlock * 16];
+    __shared__ u32x4 recs[PER * kPlanRecordPieces];
+    __shared__ u32x4 out[PER * 16];
     const int tid = threadIdx.x;
-    const int r0  = blockIdx.x * kPlanPerBlock;
-    const int nr  = min(kPlanPerBlock, a.n - r0);
+    const int r0  = blockIdx.x * PER;
+    const int nr  = min(PER, a.n - r0);
     // sc0 sc1: read through to host memory (the slot was written by the host since its last use)
     const auto src = __builtin_amdgcn_make_buffer_rsrc((void*)host_records, (short)0, a.n * (int)sizeof(PlanRecord),
                                                        0x00020000);
-    for (int i = tid; i < nr * kPlanRecordPieces; i += 128)
+    for (int i = tid; i < nr * kPlanRecordPieces; i += LANES)
         recs[i] = __builtin_amdgcn_raw_buffer_load_b128(src, r0 * (int)sizeof(PlanRecord) + i * 16, 0, 1 | 16);
     __syncthreads();
     if (tid < nr) {
@@ -43,13 +43,24 @@ __global__ __launch_bounds__(128) void plan_records(const PlanRecord* host_recor
     }
     __syncthreads();
     u32x4* dst = (u32x4*)(jobs + r0);
-    for (int k = tid; k < nr * 16; k += 128) dst[k] = out[k];
+    for (int k = tid; k < nr * 16; k += LANES) dst[k] = out[k];
 }
 
 hipError_t launch_plan_records(const void* host_records, void* jobs, const PlanArgs& a, hipStream_t stream)
 {
-    hipLaunchKernelGGL(plan_records, dim3((a.n + kPlanPerBlock - 1) / kPlanPerBlock), dim3(128), 0, stream,
-                       (const PlanRecord*)host_records, (AugJob*)jobs, a);
+    static int per = 0;
+    if (!per) {
+        per = 16;
+        if (const char* e = std::getenv("AEON_HIP_PLAN_PER_BLOCK")) per = std::atoi(e); // experiments
+    }
+    const PlanRecord* r = (const PlanRecord*)host_records;
+    AugJob*           j = (AugJob*)jobs;
+    switch (per) {
+    case 1: hipLaunchKernelGGL((plan_records<1, 64>), dim3(a.n), dim3(64), 0, stream, r, j, a); break;
+    case 4: hipLaunchKernelGGL((plan_records<4, 64>), dim3((a.n + 3) / 4), dim3(64), 0, stream, r, j, a); break;
+    case 8: hipLaunchKernelGGL((plan_records<8, 128>), dim3((a.n + 7) / 8), dim3(128), 0, stream, r, j, a); break;
+    default: hipLaunchKernelGGL((plan_records<16, 128>), dim3((a.n + 15) / 16), dim3(128), 0, stream, r, j, a); break;
+    }
     return hipGetLastError();
 }
 

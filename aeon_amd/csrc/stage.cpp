@@ -512,6 +512,7 @@ struct aeon_hip_ctx {
     // device planning (run_direct): calls whose records are one job each of one launch group
     // upload the caller's descriptors + params and let plan_records build the jobs on the GPU
     bool                 device_plan = true; // AEON_HIP_DEVICE_PLAN=0: always plan on the host
+    bool                 plan_async  = false; // AEON_HIP_PLAN_ASYNC=1: plan_records on copy_stream
     std::vector<JobGeom> geoms;              // reused per call
     JpegState*           jpeg = nullptr;     // JPEG decode stage (pool, staging ring), on first use
     // overlap_contrast: a contrast batch runs as `overlap_chunks` chunks whose pass 2 (memory-bound)
@@ -877,7 +878,13 @@ bool run_direct(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void
     }
     phase(4);
     const PlanArgs pa{(uint64_t)src_base, (uint64_t)out_dev, o.item_stride, out_geom(o), n, is_mask ? 1 : 0, P.tr, 0};
-    HIP_OK(launch_plan_records(s.host_dev, s.dev, pa, stream));
+    if (ctx->plan_async) { // experiments: planned on the copy stream beside the previous call's kernels
+        HIP_OK(launch_plan_records(s.host_dev, s.dev, pa, ctx->copy_stream));
+        HIP_OK(hipEventRecord(s.copied, ctx->copy_stream));
+        HIP_OK(hipStreamWaitEvent(stream, s.copied, 0));
+    } else {
+        HIP_OK(launch_plan_records(s.host_dev, s.dev, pa, stream));
+    }
     phase(5);
     const bool timed = ctx->timing && (ctx->timing_calls++ % ctx->timing_every) == 0;
     if (o.fixed_aspect_ratio) // std::fill_n of each item's canvas, its whole byte size (etl_image.cpp:263)
@@ -1230,6 +1237,7 @@ int aeon_hip_ctx_create(int device, aeon_hip_ctx** out)
             HIP_OK(hipEventCreateWithFlags(&c->join_event, hipEventDisableTiming));
             if (const char* e = std::getenv("AEON_HIP_OVERLAP_CHUNKS")) c->overlap_chunks = std::max(1, std::atoi(e));
             if (const char* e = std::getenv("AEON_HIP_TAIL_SPLIT")) c->tail_split = std::atoi(e) != 0;
+            if (const char* e = std::getenv("AEON_HIP_PLAN_ASYNC")) c->plan_async = std::atoi(e) != 0;
             if (const char* e = std::getenv("AEON_HIP_FUSED")) c->fused = std::atoi(e);
             if (const char* e = std::getenv("AEON_HIP_FUSED_LAG")) c->fused_lag = std::max(1, std::atoi(e));
             if (const char* e = std::getenv("AEON_HIP_CAP_PASS1")) c->cap_pass1 = std::max(0, std::atoi(e));
