@@ -131,6 +131,9 @@ def lib():
         L.aeon_calculate_scale.argtypes = [ctypes.c_int] * 4 + [P(ctypes.c_float)]
         L.aeon_cropbox_max_proportional.argtypes = [ctypes.c_float] * 4 + [P(ctypes.c_float)] * 2
         L.aeon_jpeg_info.argtypes = [ctypes.c_char_p, ctypes.c_size_t] + [P(ctypes.c_int)] * 3
+        L.aeon_png_info.argtypes = [ctypes.c_char_p, ctypes.c_size_t] + [P(ctypes.c_int)] * 4
+        L.aeon_decode_png.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int, vp, ctypes.c_size_t,
+                                      P(ctypes.c_int)]
         L.aeon_hip_decode_jpeg_batch.argtypes = [vp, ctypes.c_int, P(vp), P(ctypes.c_size_t), P(ImgDesc), vp, vp]
         L.aeon_hip_host_alloc.argtypes = [ctypes.c_size_t, P(vp)]
         L.aeon_hip_host_free.argtypes = [vp]
@@ -225,6 +228,29 @@ def jpeg_info(data):
     w, h, n = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
     _check(lib().aeon_jpeg_info(bytes(data), len(data), ctypes.byref(w), ctypes.byref(h), ctypes.byref(n)))
     return w.value, h.value, n.value
+
+
+PNG_BGR8, PNG_GRAY8, PNG_ANYDEPTH = 0, 1, 2
+
+
+def png_info(data):
+    """(width, height, bit depth, PNG colour type) of a PNG file (aeon_png_info)."""
+    w, h, d, c = ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    _check(lib().aeon_png_info(bytes(data), len(data), ctypes.byref(w), ctypes.byref(h), ctypes.byref(d),
+                               ctypes.byref(c)))
+    return w.value, h.value, d.value, c.value
+
+
+def decode_png(data, mode=PNG_BGR8):
+    """cv::imdecode of a PNG file as aeon's extractors ask for it (aeon_decode_png): HxWx3 uint8 BGR
+    (PNG_BGR8), HxW uint8 (PNG_GRAY8), or HxW uint8 / uint16 at the file's depth (PNG_ANYDEPTH)."""
+    w, h, d, c = png_info(data)
+    wide = mode == PNG_ANYDEPTH and d == 16 and c != 3
+    cn = 3 if mode == PNG_BGR8 else 1
+    out = np.zeros((h, w, cn) if cn == 3 else (h, w), np.uint16 if wide else np.uint8)
+    eb = ctypes.c_int()
+    _check(lib().aeon_decode_png(bytes(data), len(data), mode, out.ctypes.data, out.strides[0], ctypes.byref(eb)))
+    return out
 
 
 def unbiased_round(x):

@@ -307,9 +307,11 @@ void provider_base::stage(int idx, const decoded_element* elems, decode_window& 
     for (size_t k = 0; k < m_providers.size(); k++) {
         const decoded_element& e = elems[k];
         if (e.encoded) continue; // decoded on the device, straight into the source arena
-        const size_t row = (size_t)e.width * e.channels;
+        const size_t row = (size_t)e.width * e.channels * e.elem_bytes;
         uint8_t*     dst = w.arena + w.offset[k][idx];
-        if ((size_t)e.stride == row) {
+        if (e.png_mode >= 0) { // extract on this pool thread, straight into the pinned arena
+            check(aeon_decode_png(e.data, e.size, e.png_mode, dst, row, nullptr));
+        } else if ((size_t)e.stride == row) {
             std::memcpy(dst, e.data, row * e.height);
         } else {
             for (int y = 0; y < e.height; y++) std::memcpy(dst + y * row, e.data + (size_t)y * e.stride, row);
@@ -533,16 +535,32 @@ void batch_decoder::enqueue(window_slot& ws, int n, const decoded_element* in, v
     const int ne = (int)m_provider->get_input_count();
     // image::extractor::extract of encoded elements: the frame header gives the decoded size; the
     // record is decoded with the provider's channel count (CV_LOAD_IMAGE_COLOR / GRAYSCALE)
+    // (CV_LOAD_IMAGE_COLOR / GRAYSCALE for images, CV_LOAD_IMAGE_ANYDEPTH for pixel masks).  PNG
+    // files are decoded on the host pool while staging (png_host.cpp), JPEG files on the device.
     std::vector<decoded_element> records(in, in + (size_t)n * ne);
+    static const uint8_t kPngSig[8] = {0x89, 'P', 'N', 'G', 0x0D, 0x0A, 0x1A, 0x0A};
     for (int i = 0; i < n; i++)
         for (int k = 0; k < ne; k++) {
             decoded_element& e = records[(size_t)i * ne + k];
             if (!e.encoded) continue;
-            if (m_provider->providers()[k]->is_mask())
-                throw std::runtime_error("encoded pixel masks are not decoded here (PNG): pass the decoded mask");
+            const bool mask = m_provider->providers()[k]->is_mask();
+            const int  cn   = m_provider->providers()[k]->out_desc().channels;
+            if (e.size >= 8 && std::memcmp(e.data, kPngSig, 8) == 0) {
+                int depth = 0, ctype = 0;
+                check(aeon_png_info(e.data, e.size, &e.width, &e.height, &depth, &ctype));
+                e.encoded    = false;
+                e.png_mode   = mask ? AEON_PNG_ANYDEPTH : (cn == 3 ? AEON_PNG_BGR8 : AEON_PNG_GRAY8);
+                e.channels   = mask ? 1 : cn;
+                e.elem_bytes = (mask && depth == 16 && ctype != 3) ? 2 : 1;
+                e.stride     = e.width * e.channels * e.elem_bytes;
+                continue;
+            }
+            if (mask)
+                throw std::runtime_error("encoded pixel masks are decoded from PNG files only (JPEG masks: pass the "
+                                         "decoded mask)");
             int comps = 0;
             check(aeon_jpeg_info(e.data, e.size, &e.width, &e.height, &comps));
-            e.channels = m_provider->providers()[k]->out_desc().channels;
+            e.channels = cn;
             e.stride   = e.width * e.channels;
         }
     decode_window w;
@@ -557,9 +575,11 @@ void batch_decoder::enqueue(window_slot& ws, int n, const decoded_element* in, v
             for (int k = 0; k < ne; k++) {
                 const decoded_element& e = records[(size_t)i * ne + k];
                 if (e.encoded != (pass == 1)) continue;
-                const size_t b = (size_t)std::max(e.width, 0) * std::max(e.height, 0) * std::max(e.channels, 0);
+                const size_t b = (size_t)std::max(e.width, 0) * std::max(e.height, 0) * std::max(e.channels, 0) *
+                                 e.elem_bytes;
                 w.offset[k][i] = total;
-                w.descs[k][i]  = aeon_img_desc{total, e.width, e.height, e.width * e.channels, e.channels, 0, 0};
+                w.descs[k][i]  = aeon_img_desc{total, e.width, e.height, e.width * e.channels * e.elem_bytes, e.channels,
+                                              e.elem_bytes == 2 ? 2 : 0, 0};
                 total += (b + 15) & ~(size_t)15;
                 if (pass == 0) staged = total;
             }
@@ -734,6 +754,28 @@ int host_guarded(F&& f)
 }
 } // namespace
 
+namespace {
+std::vector<aeon_hip::decoded_element> to_elements(aeon_decoder* d, int n, const aeon_encoded_elem* elems)
+{
+    const int ne = (int)d->d->provider().get_input_count();
+    std::vector<aeon_hip::decoded_element> recs((size_t)n * ne);
+    for (size_t i = 0; i < recs.size(); i++) {
+        const aeon_encoded_elem& e = elems[i];
+        aeon_hip::decoded_element& r = recs[i];
+        r.data = (const uint8_t*)e.data;
+        if (e.width > 0) {
+            r.width = e.width, r.height = e.height, r.channels = e.channels;
+            r.stride = e.stride ? e.stride : e.width * e.channels;
+        } else {
+            if (!e.data || !e.size) throw std::runtime_error("received encoded image with size 0, at idx " +
+                                                             std::to_string(i / ne));
+            r.encoded = true, r.size = e.size;
+        }
+    }
+    return recs;
+}
+} // namespace
+
 extern "C" {
 
 int aeon_decoder_create(const char* config_json, int device, aeon_decoder** out)
@@ -800,27 +842,6 @@ int aeon_decoder_decode(aeon_decoder* d, int n, const aeon_record_elem* elems, v
     });
 }
 
-namespace {
-std::vector<aeon_hip::decoded_element> to_elements(aeon_decoder* d, int n, const aeon_encoded_elem* elems)
-{
-    const int ne = (int)d->d->provider().get_input_count();
-    std::vector<aeon_hip::decoded_element> recs((size_t)n * ne);
-    for (size_t i = 0; i < recs.size(); i++) {
-        const aeon_encoded_elem& e = elems[i];
-        aeon_hip::decoded_element& r = recs[i];
-        r.data = (const uint8_t*)e.data;
-        if (e.width > 0) {
-            r.width = e.width, r.height = e.height, r.channels = e.channels;
-            r.stride = e.stride ? e.stride : e.width * e.channels;
-        } else {
-            if (!e.data || !e.size) throw std::runtime_error("received encoded image with size 0, at idx " +
-                                                             std::to_string(i / ne));
-            r.encoded = true, r.size = e.size;
-        }
-    }
-    return recs;
-}
-} // namespace
 
 int aeon_decoder_decode_encoded(aeon_decoder* d, int n, const aeon_encoded_elem* elems, void* const* outputs,
                                 int outputs_on_device, void* stream)

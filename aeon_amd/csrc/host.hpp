@@ -68,6 +68,8 @@ struct decoded_element {
     int            width = 0, height = 0, channels = 0, stride = 0;
     size_t         size    = 0;     // encoded bytes
     bool           encoded = false; // JPEG file: decoded on the device (jpeg_host.cpp)
+    int            png_mode   = -1; // PNG file: AEON_PNG_* decode on the host while staging
+    int            elem_bytes = 1;  // bytes per sample (2: a 16-bit mask / depth map)
 };
 
 // Per-window staging shared by the providers (filled concurrently by the pool threads).

@@ -43,6 +43,8 @@ hipError_t launch_plan_records(const void* host_records, void* jobs, const PlanA
 void       jpeg_decode_batch(JpegState* S, int n, const void* const* data, const size_t* sizes,
                              const aeon_img_desc* descs, void* dst_base, hipStream_t stream);
 void       jpeg_info(const void* data, size_t size, int* w, int* h, int* ncomp);
+void       png_header(const void* data, size_t size, int* w, int* h, int* depth, int* ctype);
+void       png_decode(const void* data, size_t size, int mode, void* dst, size_t stride, int* out_elem_bytes);
 } // namespace aeon_hip
 
 using namespace aeon_hip;
@@ -1460,6 +1462,29 @@ int aeon_make_ssd_params(aeon_param_factory* f, uint32_t* state, int in_w, int i
         TrackedEngine eng(*state);
         f->f.make_ssd_params(eng, in_w, in_h, out_w, out_h, boxes, n_boxes, out);
         *state = eng.last;
+        return 0;
+    });
+}
+
+int aeon_png_info(const void* data, size_t size, int* width, int* height, int* bit_depth, int* color_type)
+{
+    return guarded([&] {
+        if (!data || !width || !height || !bit_depth || !color_type) fail(AEON_HIP_EINVAL, "null argument");
+        png_header(data, size, width, height, bit_depth, color_type);
+        return 0;
+    });
+}
+
+int aeon_decode_png(const void* data, size_t size, int mode, void* dst, size_t stride, int* elem_bytes)
+{
+    return guarded([&] {
+        if (!data || !dst) fail(AEON_HIP_EINVAL, "null argument");
+        if (mode < AEON_PNG_BGR8 || mode > AEON_PNG_ANYDEPTH) fail(AEON_HIP_EINVAL, "unknown PNG decode mode");
+        int w, h, depth, ctype;
+        png_header(data, size, &w, &h, &depth, &ctype);
+        const size_t eb = (mode == AEON_PNG_ANYDEPTH && depth == 16 && ctype != 3) ? 2 : 1;
+        if (stride < (size_t)w * (mode == AEON_PNG_BGR8 ? 3 : 1) * eb) fail(AEON_HIP_EINVAL, "stride too small");
+        png_decode(data, size, mode, dst, stride, elem_bytes);
         return 0;
     });
 }

@@ -189,6 +189,19 @@ int aeon_make_params(aeon_param_factory* f, uint32_t* engine_state, int in_w, in
 int aeon_make_ssd_params(aeon_param_factory* f, uint32_t* engine_state, int in_w, int in_h, int out_w, int out_h,
                          const float* boxes, int n_boxes, aeon_aug_params* out);
 
+/* PNG decode -- image::extractor::extract / pixel_mask::extractor::extract on PNG files
+ * (src/etl_image.cpp:83-99, src/etl_pixel_mask.cpp:30-53: cv::imdecode over libpng), on the host.
+ * Modes: AEON_PNG_BGR8 = CV_LOAD_IMAGE_COLOR (8-bit BGR), AEON_PNG_GRAY8 = CV_LOAD_IMAGE_GRAYSCALE,
+ * AEON_PNG_ANYDEPTH = CV_LOAD_IMAGE_ANYDEPTH (gray at the file's depth: 16-bit files give native
+ * uint16 samples).  aeon_png_info: size, bit depth and PNG colour type from the header.
+ * aeon_decode_png writes height rows of `stride` bytes to dst and the element size (1 or 2) to
+ * *elem_bytes (may be NULL). */
+#define AEON_PNG_BGR8     0
+#define AEON_PNG_GRAY8    1
+#define AEON_PNG_ANYDEPTH 2
+int aeon_png_info(const void* data, size_t size, int* width, int* height, int* bit_depth, int* color_type);
+int aeon_decode_png(const void* data, size_t size, int mode, void* dst, size_t stride, int* elem_bytes);
+
 /* batch_sampler::sample_patches (src/augment_image.cpp:567-586) of the factory's batch_samplers[sampler]
  * over n normalized object boxes (xmin, ymin, xmax, ymax in [0, 1]) -- what aeon's tests call as
  * factory.m_batch_samplers[i].sample_patches (test/test_augmentation.cpp:347-443).  Writes up to cap

@@ -165,3 +165,55 @@ def test_decoder_submit_wait_double_buffered():
             d.submit(windows[w + 2], [bufs[w % 2].data_ptr()])
     for w in range(4):
         assert np.array_equal(got[w], want[w]), w
+
+
+def test_decoder_png_image_and_mask():
+    """Encoded PNG records (image::extractor / pixel_mask::extractor over cv::imdecode, decoded on
+    the host pool while staging): an RGB image and gray / palette / 16-bit gray masks, against the
+    oracle's PNG decode (oracle/png_oracle.py) and transforms."""
+    import io
+
+    from PIL import Image
+
+    from oracle import png_oracle as PO
+
+    def png_of(arr, mode=None, palette=None):
+        im = Image.fromarray(arr, mode) if mode else Image.fromarray(arr)
+        if palette is not None:
+            im.putpalette(palette)
+        buf = io.BytesIO()
+        im.save(buf, "PNG")
+        return buf.getvalue()
+
+    rng = np.random.default_rng(11)
+    recs, decoded = [], []
+    for i in range(6):
+        w, h = int(rng.integers(200, 360)), int(rng.integers(160, 300))
+        img = A.synthetic_image(700 + i, w, h, 3)
+        cls = (A.synthetic_image(900 + i, w, h, 1) % 5).astype(np.uint8)
+        if i % 3 == 0:
+            mpng = png_of(cls * 40)
+        elif i % 3 == 1:
+            mpng = png_of(cls, "P", [v for c in range(5) for v in (c * 30, c * 50, 255 - c * 40)])
+        else:
+            mpng = png_of((cls.astype(np.uint16) * 97 + (i * 13)).astype(np.uint16))
+        recs.append((png_of(img[:, :, ::-1].copy()), mpng))
+        decoded.append((PO.decode(recs[-1][0], PO.BGR8), PO.decode(mpng, PO.ANYDEPTH)))
+    assert np.array_equal(decoded[0][0], A.decode_png(recs[0][0]))
+    cfg = dict(batch_size=6, random_seed=4, etl=[C.IMAGE_512, C.MASK_512], augmentation=[C.C5_AUG])
+    d = A.Decoder(cfg)
+    img, msk = d.decode(recs)
+    params = H.draw_params(C.C5_AUG, [(r[0].shape[1], r[0].shape[0]) for r in decoded], 512, 512, seed=4)
+    iod = C.out_desc_for(C.IMAGE_512, C.C5_AUG)
+    ref_img = np.stack(H.oracle_records([r[0] for r in decoded], params, iod))
+    assert np.array_equal(img, ref_img)
+    mod = C.out_desc_for(C.MASK_512, C.C5_AUG)
+    for i, (r, p) in enumerate(zip(decoded, params)):
+        m = r[1]
+        if m.dtype == np.uint16:  # saturate_cast<uchar> of the 16-bit NEAREST result
+            lo = H.oracle_records([(m & 0xff).astype(np.uint8)], [p], mod, mask=True)[0]
+            hi = H.oracle_records([(m >> 8).astype(np.uint8)], [p], mod, mask=True)[0]
+            want = np.minimum(hi.astype(np.uint32) * 256 + lo, 255).astype(np.uint8)
+        else:
+            want = H.oracle_records([m], [p], mod, mask=True)[0]
+        assert np.array_equal(msk[i], want.reshape(msk[i].shape)), i
