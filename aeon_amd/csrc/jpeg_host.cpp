@@ -2,11 +2,11 @@
 // entropy decoding into the sparse coefficient stream on the decode pool, the per-call device
 // layout, and the extern "C" entries aeon_jpeg_info / aeon_hip_decode_jpeg_batch.
 //
-// Follows libjpeg's baseline / extended-sequential decoder (ITU T.81 F.2: DHT/DQT/DRI/SOF0-1/SOS,
-// interleaved and non-interleaved scans, restart intervals, 0xFF00 stuffing), which is what
-// cv::imdecode runs under aeon's image::extractor::extract (src/etl_image.cpp:83-99).  Progressive,
-// arithmetic-coded, 12-bit and 4-component (CMYK / Adobe RGB) files are refused with
-// AEON_HIP_EUNSUPPORTED.
+// Follows libjpeg's Huffman decoders (ITU T.81 F.2 / G.1.2: DHT/DQT/DRI/SOF0-2/SOS, interleaved and
+// non-interleaved scans, restart intervals, 0xFF00 stuffing; progressive files through spectral
+// selection and successive approximation, jdphuff.c), which is what cv::imdecode runs under aeon's
+// image::extractor::extract (src/etl_image.cpp:83-99).  Arithmetic-coded, lossless, 12-bit and
+// 4-component (CMYK / Adobe RGB) files are refused with AEON_HIP_EUNSUPPORTED.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -180,6 +180,7 @@ struct Comp {
 // Header of one file (and, once decoded, where its streams sit in the worker's arena).
 struct Frame {
     int      W = 0, H = 0, ncomp = 0, hmax = 1, vmax = 1, mcux = 0, mcuy = 0;
+    bool     progressive = false; // SOF2
     Comp     c[3];
     uint16_t q[4][64];
     bool     qset[4] = {false, false, false, false};
@@ -189,6 +190,7 @@ struct Frame {
 struct Arena {
     std::vector<uint8_t> host; // pageable staging, copied into the set's pinned buffer
     size_t               used = 0;
+    std::vector<int16_t> coef; // progressive files: every block's 64 coefficients (zigzag order)
     uint8_t*             reserve(size_t bytes)
     {
         used = (used + 15) & ~(size_t)15;
@@ -219,7 +221,8 @@ void parse_frame(const uint8_t* d, size_t size, Frame& f, const uint8_t** after)
         const int len = be16(p);
         if (len < 2 || p + len > end) bad("truncated marker segment");
         const uint8_t* s = p + 2;
-        if (m == 0xC0 || m == 0xC1) {
+        if (m == 0xC0 || m == 0xC1 || m == 0xC2) {
+            f.progressive = m == 0xC2;
             if (len < 8) bad("bad frame header");
             if (s[0] != 8) unsupported("only 8-bit samples are supported");
             f.H = be16(s + 1), f.W = be16(s + 3), f.ncomp = s[5];
@@ -245,9 +248,9 @@ void parse_frame(const uint8_t* d, size_t size, Frame& f, const uint8_t** after)
             *after = p + len;
             return;
         }
-        if (m >= 0xC2 && m <= 0xCF && m != 0xC4 && m != 0xC8 && m != 0xCC)
-            unsupported("only baseline / extended-sequential Huffman JPEGs are supported (no progressive, "
-                        "lossless or arithmetic coding)");
+        if (m >= 0xC3 && m <= 0xCF && m != 0xC4 && m != 0xC8 && m != 0xCC)
+            unsupported("only Huffman-coded baseline / extended-sequential / progressive JPEGs are supported (no "
+                        "lossless, hierarchical or arithmetic coding)");
         p += len;
     }
 }
@@ -307,6 +310,122 @@ void parse_frame(const uint8_t* d, size_t size, Frame& f, const uint8_t** after)
     return mask;
 }
 
+// One scan of a progressive file (ITU T.81 G.1.2.1-2; libjpeg's jdphuff.c): DC first / refine
+// (interleaved or not) and AC first / refine (one component) over the dense coefficients.
+struct ProgScan {
+    int Ss, Se, Ah, Al;
+};
+
+[[gnu::always_inline]] inline void refine_bit(Bits& b, int16_t& c, int p1, int m1)
+{
+    b.fill();
+    if (b.get(1) && (c & p1) == 0) c = (int16_t)(c + (c >= 0 ? p1 : m1));
+}
+
+void decode_progressive_scan(Bits& br, const Frame& f, const int* sc, int ns, const ProgScan& S, const Huffman* dc,
+                             const Huffman* ac, int restart, int16_t* const coef_of[3])
+{
+    const int p1 = 1 << S.Al, m1 = -p1;
+    int       pred[3] = {0, 0, 0};
+    int       eobrun  = 0;
+    // block (bx, by) of scan component i
+    auto dc_block = [&](int i, int16_t* blk) {
+        const Comp& c = f.c[sc[i]];
+        if (S.Ah == 0) {
+            br.fill();
+            const int t = br.decode(dc[c.td]);
+            if (t > 15) bad("corrupt DC coefficient");
+            br.fill();
+            pred[i] += t ? extend((int)br.get(t), t) : 0;
+            blk[0] = (int16_t)(pred[i] * (1 << S.Al));
+        } else {
+            br.fill();
+            if (br.get(1)) blk[0] = (int16_t)(blk[0] | p1);
+        }
+    };
+    auto ac_block = [&](int16_t* blk) {
+        const Huffman& t = ac[f.c[sc[0]].ta];
+        int            k = S.Ss;
+        if (S.Ah == 0) { // AC first
+            if (eobrun > 0) {
+                eobrun--;
+                return;
+            }
+            for (; k <= S.Se; k++) {
+                const int rs = br.decode(t), r = rs >> 4, z = rs & 15;
+                if (z) {
+                    k += r;
+                    br.fill();
+                    // libjpeg's natural-order table clamps a corrupt run past 63 to 63
+                    blk[std::min(k, 63)] = (int16_t)(extend((int)br.get(z), z) * (1 << S.Al));
+                } else if (r == 15) {
+                    k += 15;
+                } else {
+                    eobrun = (1 << r) - 1;
+                    if (r) br.fill(), eobrun += (int)br.get(r);
+                    break;
+                }
+            }
+            return;
+        }
+        // AC refine
+        if (eobrun == 0) {
+            for (; k <= S.Se; k++) {
+                const int rs = br.decode(t);
+                int       r = rs >> 4, z = rs & 15, v = 0;
+                if (z) { // (size 1 by construction; libjpeg only warns otherwise)
+                    br.fill();
+                    v = br.get(1) ? p1 : m1;
+                } else if (r != 15) {
+                    eobrun = 1 << r;
+                    if (r) br.fill(), eobrun += (int)br.get(r);
+                    break;
+                }
+                // past the coefficients already non-zero (refining each) and r zero ones
+                for (; k <= S.Se; k++) {
+                    int16_t& c = blk[k];
+                    if (c != 0) refine_bit(br, c, p1, m1);
+                    else if (--r < 0) break;
+                }
+                if (v) blk[std::min(k, 63)] = (int16_t)v;
+            }
+        }
+        if (eobrun > 0) { // the band's remaining non-zero coefficients get their refinement bits
+            for (; k <= S.Se; k++)
+                if (blk[k] != 0) refine_bit(br, blk[k], p1, m1);
+            eobrun--;
+        }
+    };
+    int done = 0, left = restart;
+    auto at_restart = [&]() {
+        if (restart && done && left == 0) br.restart(), pred[0] = pred[1] = pred[2] = 0, eobrun = 0, left = restart;
+    };
+    if (ns == 1) { // non-interleaved: the component's own block grid
+        const Comp& c  = f.c[sc[0]];
+        const int   nx = (c.dw + 7) / 8, ny = (c.dh + 7) / 8;
+        for (int by = 0; by < ny; by++)
+            for (int bx = 0; bx < nx; bx++) {
+                at_restart();
+                int16_t* blk = coef_of[sc[0]] + ((size_t)by * c.bw + bx) * 64;
+                if (S.Ss == 0) dc_block(0, blk);
+                else ac_block(blk);
+                done++, left--;
+            }
+        return;
+    }
+    for (int my = 0; my < f.mcuy; my++)
+        for (int mx = 0; mx < f.mcux; mx++) {
+            at_restart();
+            for (int i = 0; i < ns; i++) {
+                const Comp& c = f.c[sc[i]];
+                for (int y = 0; y < c.v; y++)
+                    for (int x = 0; x < c.h; x++)
+                        dc_block(i, coef_of[sc[i]] + ((size_t)(my * c.v + y) * c.bw + mx * c.h + x) * 64);
+            }
+            done++, left--;
+        }
+}
+
 void decode_file(const uint8_t* d, size_t size, Frame& f, Arena& a, size_t blk_off[3], size_t* val_off, bool luma_only)
 {
     const uint8_t* p = nullptr;
@@ -328,6 +447,12 @@ void decode_file(const uint8_t* d, size_t size, Frame& f, Arena& a, size_t blk_o
     uint8_t* vbase = a.reserve(nblocks * 64 * sizeof(int16_t));
     *val_off       = (size_t)(vbase - a.host.data());
     uint32_t nvals = 0;
+    int16_t* coef_of[3] = {nullptr, nullptr, nullptr};
+    if (f.progressive) { // scans refine a dense coefficient image; the sparse records come at the end
+        a.coef.assign(nblocks * 64, 0);
+        size_t o = 0;
+        for (int k = 0; k < f.ncomp; k++) coef_of[k] = a.coef.data() + o, o += (size_t)f.c[k].bw * f.c[k].bh * 64;
+    }
     auto table_segment = [&](int m, const uint8_t* s, int len) {
         const uint8_t* e = s + len - 2;
         if (m == 0xC4) {
@@ -366,7 +491,7 @@ void decode_file(const uint8_t* d, size_t size, Frame& f, Arena& a, size_t blk_o
             const int m = *q++;
             if (m == 0xD8 || (m >= 0xD0 && m <= 0xD7) || m == 0x01) continue;
             const int len = be16(q);
-            if (m == 0xC0 || m == 0xC1) break;
+            if (m == 0xC0 || m == 0xC1 || m == 0xC2) break;
             table_segment(m, q + 2, len);
             q += len;
         }
@@ -402,12 +527,32 @@ void decode_file(const uint8_t* d, size_t size, Frame& f, Arena& a, size_t blk_o
             while (k < f.ncomp && f.c[k].id != cid) k++;
             if (k == f.ncomp) bad("scan names an unknown component");
             f.c[k].td = t >> 4, f.c[k].ta = t & 15;
-            if (f.c[k].td > 3 || f.c[k].ta > 3 || !dc[f.c[k].td].set || !ac[f.c[k].ta].set)
-                bad("scan uses an undefined Huffman table");
+            if (f.c[k].td > 3 || f.c[k].ta > 3) bad("bad Huffman table selector");
             if (!f.qset[f.c[k].tq]) bad("component uses an undefined quantisation table");
             sc[i] = k;
         }
-        if (s[1 + 2 * ns] != 0 || s[2 + 2 * ns] != 63 || s[3 + 2 * ns] != 0)
+        const ProgScan S{s[1 + 2 * ns], s[2 + 2 * ns], s[3 + 2 * ns] >> 4, s[3 + 2 * ns] & 15};
+        if (f.progressive) {
+            // jdphuff.c start_pass_phuff_decoder's checks
+            const bool ok = (S.Ss == 0 ? S.Se == 0 : (S.Se >= S.Ss && S.Se <= 63 && ns == 1)) && S.Al <= 13 &&
+                            (S.Ah == 0 || S.Al == S.Ah - 1);
+            if (!ok) bad("bad progressive scan parameters");
+            for (int i = 0; i < ns; i++) {
+                const Comp& c = f.c[sc[i]];
+                if ((S.Ss == 0 && S.Ah == 0 && !dc[c.td].set) || (S.Ss > 0 && !ac[c.ta].set))
+                    bad("scan uses an undefined Huffman table");
+            }
+            p += len;
+            any_scan = true;
+            Bits br{p, end};
+            decode_progressive_scan(br, f, sc, ns, S, dc, ac, restart, coef_of);
+            p = br.p;
+            while (p + 1 < end && !(p[0] == 0xFF && p[1] != 0 && !(p[1] >= 0xD0 && p[1] <= 0xD7))) p++;
+            continue;
+        }
+        for (int i = 0; i < ns; i++)
+            if (!dc[f.c[sc[i]].td].set || !ac[f.c[sc[i]].ta].set) bad("scan uses an undefined Huffman table");
+        if (S.Ss != 0 || S.Se != 63 || S.Ah != 0 || S.Al != 0)
             unsupported("progressive scan parameters in a sequential file");
         p += len;
         any_scan = true;
@@ -426,6 +571,7 @@ void decode_file(const uint8_t* d, size_t size, Frame& f, Arena& a, size_t blk_o
             for (int by = 0; by < ny; by++)
                 for (int bx = 0; bx < nx; bx++) {
                     if (restart && done && left == 0) br.restart(), pred = 0, left = restart;
+                    if (nv + 64 > nblocks * 64) bad("coefficient overflow (a block coded twice)");
                     JpegBlock& R = recs[(size_t)by * c.bw + bx];
                     R.val_off    = nv;
                     R.mask       = decode_block(br, dct, act, pred, vals, nv);
@@ -447,6 +593,7 @@ void decode_file(const uint8_t* d, size_t size, Frame& f, Arena& a, size_t blk_o
                         const Huffman& act = ac[c.ta];
                         for (int y = 0; y < c.v; y++)
                             for (int x = 0; x < c.h; x++) {
+                                if (nv + 64 > nblocks * 64) bad("coefficient overflow (a block coded twice)");
                                 JpegBlock& R = recs[(size_t)(my * c.v + y) * c.bw + mx * c.h + x];
                                 R.val_off    = nv;
                                 R.mask       = decode_block(br, dct, act, pred[i], vals, nv);
@@ -462,6 +609,20 @@ void decode_file(const uint8_t* d, size_t size, Frame& f, Arena& a, size_t blk_o
         while (p + 1 < end && !(p[0] == 0xFF && p[1] != 0 && !(p[1] >= 0xD0 && p[1] <= 0xD7))) p++;
     }
     if (adobe_rgb && f.ncomp == 3) unsupported("RGB (Adobe transform 0) JPEGs");
+    if (f.progressive) { // the dense coefficients as the sparse stream the kernels read
+        int16_t* vals = (int16_t*)(a.host.data() + *val_off);
+        for (int k = 0; k < f.ncomp; k++) {
+            JpegBlock*     recs = (JpegBlock*)(a.host.data() + blk_off[k]);
+            const int16_t* cb   = coef_of[k];
+            for (size_t b = 0; b < (size_t)f.c[k].bw * f.c[k].bh; b++, cb += 64) {
+                uint64_t mask = 0;
+                recs[b].val_off = nvals;
+                for (int z = 0; z < 64; z++)
+                    if (cb[z]) mask |= 1ull << z, vals[nvals++] = cb[z];
+                recs[b].mask = mask;
+            }
+        }
+    }
     (void)luma_only;
     // give back the unused tail of the value reservation
     a.used = *val_off + (size_t)nvals * sizeof(int16_t);

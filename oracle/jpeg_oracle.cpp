@@ -188,6 +188,100 @@ struct Decoder {
         while (p + 1 < end && !(p[0] == 0xFF && p[1] != 0 && !(p[1] >= 0xD0 && p[1] <= 0xD7))) p++;
     }
 
+    // progressive scans (ITU T.81 G.1.2; libjpeg jdphuff.c), coefficients in natural order
+    bool progressive = false;
+    int  eobrun      = 0;
+    void refine(int16_t& c, int p1, int m1)
+    {
+        if (bit() && (c & p1) == 0) c = (int16_t)(c >= 0 ? c + p1 : c + m1);
+    }
+    void prog_block(Comp& c, int bx, int by, int Ss, int Se, int Ah, int Al)
+    {
+        int16_t*  blk = &c.coef[((size_t)by * c.bw + bx) * 64];
+        const int p1 = 1 << Al, m1 = -p1;
+        if (Ss == 0) { // DC (first: Huffman-coded difference; refine: one raw bit)
+            if (Ah == 0) {
+                int s = decode(dc[c.td]);
+                c.pred += s ? extend(receive(s), s) : 0;
+                blk[0] = (int16_t)(c.pred * p1);
+            } else if (bit()) {
+                blk[0] = (int16_t)(blk[0] | p1);
+            }
+            return;
+        }
+        int k = Ss;
+        if (Ah == 0) { // AC first
+            if (eobrun) {
+                eobrun--;
+                return;
+            }
+            while (k <= Se) {
+                int rs = decode(ac[c.ta]), r = rs >> 4, s = rs & 15;
+                if (s) {
+                    k += r;
+                    blk[kNatural[k]] = (int16_t)(extend(receive(s), s) * p1);
+                } else if (r < 15) {
+                    eobrun = (1 << r) - 1 + (r ? receive(r) : 0);
+                    return;
+                } else {
+                    k += 15;
+                }
+                k++;
+            }
+            return;
+        }
+        if (!eobrun) { // AC refine
+            while (k <= Se) {
+                int rs = decode(ac[c.ta]), r = rs >> 4, s = rs & 15, v = 0;
+                if (s) v = bit() ? p1 : m1;
+                else if (r < 15) {
+                    eobrun = (1 << r) + (r ? receive(r) : 0);
+                    break;
+                }
+                while (k <= Se) {
+                    int16_t& x = blk[kNatural[k]];
+                    if (x) refine(x, p1, m1);
+                    else if (r-- == 0) break;
+                    k++;
+                }
+                if (v) blk[kNatural[k]] = (int16_t)v;
+                k++;
+            }
+        }
+        if (eobrun) {
+            for (; k <= Se; k++)
+                if (blk[kNatural[k]]) refine(blk[kNatural[k]], p1, m1);
+            eobrun--;
+        }
+    }
+    void prog_scan(const std::vector<int>& sc, int Ss, int Se, int Ah, int Al)
+    {
+        if ((Ss == 0 && Se != 0) || (Ss > 0 && (Se < Ss || Se > 63 || sc.size() != 1)) || Al > 13 ||
+            (Ah && Al != Ah - 1))
+            bad("bad progressive scan");
+        nbits = 0, hit_marker = false, eobrun = 0;
+        for (auto& c : comps) c.pred = 0;
+        int done = 0;
+        auto rst = [&] {
+            if (restart && done && done % restart == 0) restart_marker(), eobrun = 0;
+        };
+        if (sc.size() == 1) {
+            Comp& c = comps[sc[0]];
+            for (int by = 0; by < (c.dh + 7) / 8; by++)
+                for (int bx = 0; bx < (c.dw + 7) / 8; bx++, done++) rst(), prog_block(c, bx, by, Ss, Se, Ah, Al);
+        } else {
+            for (int my = 0; my < mcuy; my++)
+                for (int mx = 0; mx < mcux; mx++, done++) {
+                    rst();
+                    for (int ci : sc)
+                        for (int y = 0; y < comps[ci].v; y++)
+                            for (int x = 0; x < comps[ci].h; x++)
+                                prog_block(comps[ci], mx * comps[ci].h + x, my * comps[ci].v + y, Ss, Se, Ah, Al);
+                }
+        }
+        while (p + 1 < end && !(p[0] == 0xFF && p[1] != 0 && !(p[1] >= 0xD0 && p[1] <= 0xD7))) p++;
+    }
+
     void parse()
     {
         if (u8() != 0xFF || u8() != 0xD8) bad("not a JPEG (no SOI)");
@@ -200,7 +294,8 @@ struct Decoder {
             int len = u16();
             const uint8_t* seg = p;
             if (len < 2 || p + len - 2 > end) bad("bad segment length");
-            if (m == 0xC0 || m == 0xC1) {
+            if (m == 0xC0 || m == 0xC1 || m == 0xC2) {
+                progressive = m == 0xC2;
                 if (u8() != 8) bad("only 8-bit precision");
                 H = u16(), W = u16();
                 int n = u8();
@@ -222,8 +317,8 @@ struct Decoder {
                     c.coef.assign((size_t)c.bw * c.bh * 64, 0);
                 }
                 sof = true;
-            } else if (m >= 0xC2 && m <= 0xCF && m != 0xC4 && m != 0xC8 && m != 0xCC) {
-                bad("only baseline / extended sequential Huffman JPEGs");
+            } else if (m >= 0xC3 && m <= 0xCF && m != 0xC4 && m != 0xC8 && m != 0xCC) {
+                bad("only Huffman baseline / extended sequential / progressive JPEGs");
             } else if (m == 0xC4) {
                 while (p < seg + len - 2) {
                     int tc = u8(), th = tc & 15;
@@ -259,8 +354,10 @@ struct Decoder {
                     comps[k].td = t >> 4, comps[k].ta = t & 15;
                     sc.push_back(k);
                 }
+                const int Ss = u8(), Se = u8(), AhAl = u8();
                 p = seg + len - 2;
-                scan(sc);
+                if (progressive) prog_scan(sc, Ss, Se, AhAl >> 4, AhAl & 15);
+                else scan(sc);
                 continue;
             } else {
                 p = seg + len - 2;

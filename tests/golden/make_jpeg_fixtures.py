@@ -14,7 +14,8 @@ jpeg_fixtures.npz, per fixture <name>:
   <name>.bgr_px  the full BGR decode, for the small synthetic fixtures only
 Fixtures: aeon's own test/test_data/img_2112_70.jpg and flowers.jpg (4:2:0 baseline), and files
 Pillow encodes from seeded smooth-noise images: 4:4:4 / 4:2:2 / 4:2:0 / 4:1:1, grayscale, restart
-intervals, sizes from 1x1 up, qualities 10..100.
+intervals, sizes from 1x1 up, qualities 10..100, and progressive files (synthetic ones and aeon's two
+images re-encoded progressive).
 """
 import hashlib
 import io
@@ -51,6 +52,10 @@ def synthetic():
         ("tiny_1x1", 1, 1, "RGB", "4:2:0", 90, 0), ("tiny_3x2", 3, 2, "RGB", "4:2:0", 90, 0),
         ("narrow_5x300", 5, 300, "RGB", "4:2:0", 60, 0), ("wide_301x4", 301, 4, "RGB", "4:2:2", 60, 0),
         ("q100", 80, 72, "RGB", "4:2:0", 100, 0), ("q10", 88, 56, "RGB", "4:2:0", 10, 0),
+        # progressive (SOF2: spectral selection + successive approximation scans)
+        ("prog_s420", 150, 110, "RGB", "4:2:0", 85, 0), ("prog_s444_rst", 90, 70, "RGB", "4:4:4", 90, 2),
+        ("prog_gray", 77, 51, "L", None, 75, 0), ("prog_s422_q30", 131, 67, "RGB", "4:2:2", 30, 0),
+        ("prog_q100", 64, 48, "RGB", "4:2:0", 100, 0), ("prog_tiny_5x3", 5, 3, "RGB", "4:2:0", 90, 0),
     ]
     out = []
     for name, w, h, mode, sub, q, rst in cases:
@@ -63,6 +68,8 @@ def synthetic():
             kw["subsampling"] = sub
         if rst:
             kw["restart_marker_blocks"] = rst
+        if name.startswith("prog_"):
+            kw["progressive"] = True
         bio = io.BytesIO()
         im.save(bio, "JPEG", **kw)
         out.append((name, bio.getvalue(), True))
@@ -72,6 +79,12 @@ def synthetic():
 def main():
     files = [(n[:-4], open(os.path.join(REF, n), "rb").read(), False) for n in ("img_2112_70.jpg", "flowers.jpg")]
     files += synthetic()
+    # aeon's two test images re-encoded progressive (from their baseline decode, Pillow quality 90)
+    from PIL import Image
+    for n, (_, src, _) in zip(("img_2112_70", "flowers"), files[:2]):
+        bio = io.BytesIO()
+        Image.open(io.BytesIO(src)).save(bio, "JPEG", quality=90, progressive=True)
+        files.append(("prog_" + n, bio.getvalue(), False))
     fx = {}
     for name, b, keep in files:
         bgr, gray = _decode(b)
