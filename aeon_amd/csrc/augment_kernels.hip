@@ -30,6 +30,7 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 typedef float    f32x4 __attribute__((ext_vector_type(4)));
 typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
+typedef int16_t  i16x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
 typedef int32_t  i32x4 __attribute__((ext_vector_type(4)));
 typedef int32_t  i32x2 __attribute__((ext_vector_type(2)));
@@ -146,12 +147,22 @@ __device__ __forceinline__ uint32_t to_vgpr(uint32_t s)
     asm("v_mov_b32 %0, %1" : "=v"(v) : "s"(s));
     return v;
 }
+// BS_FIXPT keeps the coefficients of B and G as int16 pairs, (q0, q1), (q3, q4), (q6, q7), for
+// v_dot2_i32_i16, and the R ones (q2, q5, q8) as plain words.
 __device__ __forceinline__ BsRegs bs_regs(cjob& J)
 {
     BsRegs R;
-    const bool fix = J.bs_kind == BS_FIXPT;
+    if (J.bs_kind == BS_FIXPT) {
 #pragma unroll
-    for (int k = 0; k < 9; k++) R.w[k] = to_vgpr(fix ? (uint32_t)J.bsq[k] : __float_as_uint(J.bsm[k]));
+        for (int i = 0; i < 3; i++) {
+            R.w[i]     = to_vgpr(((uint32_t)J.bsq[3 * i] & 0xffffu) | ((uint32_t)J.bsq[3 * i + 1] << 16));
+            R.w[3 + i] = to_vgpr((uint32_t)J.bsq[3 * i + 2]);
+        }
+        R.w[6] = R.w[7] = R.w[8] = 0;
+    } else {
+#pragma unroll
+        for (int k = 0; k < 9; k++) R.w[k] = to_vgpr(__float_as_uint(J.bsm[k]));
+    }
     return R;
 }
 __device__ __forceinline__ void bs_apply(int kind, const BsRegs& R, int& b, int& g, int& r)
@@ -162,11 +173,13 @@ __device__ __forceinline__ void bs_apply(int kind, const BsRegs& R, int& b, int&
         g = u8rnd(m(4) * (float)g + 0.f);
         r = u8rnd(m(8) * (float)r + 0.f);
     } else if (kind == BS_FIXPT) { // transform_8u, 10-bit fixed point
-        const auto q = [&](int k) { return (int)R.w[k]; };
-        // |q| < 2^15, x < 2^8: full-rate 24-bit multiply-adds
-        int t0 = mad_i24(q(0), b, mad_i24(q(1), g, mad_i24(q(2), r, 512))) >> 10;
-        int t1 = mad_i24(q(3), b, mad_i24(q(4), g, mad_i24(q(5), r, 512))) >> 10;
-        int t2 = mad_i24(q(6), b, mad_i24(q(7), g, mad_i24(q(8), r, 512))) >> 10;
+        // |q| < 2^15, x < 2^8: exact in int32 in any order.  q_B*b + q_G*g as one v_dot2_i32_i16
+        // on the (b, g) pair, + q_R*r + 512 as a full-rate 24-bit multiply-add.
+        const i16x2 bg = __builtin_bit_cast(i16x2, (uint32_t)b | ((uint32_t)g << 16));
+        const auto  dq = [&](int i, int acc) { return __builtin_amdgcn_sdot2(bg, __builtin_bit_cast(i16x2, R.w[i]), acc, false); };
+        int t0 = dq(0, mad_i24((int)R.w[3], r, 512)) >> 10;
+        int t1 = dq(1, mad_i24((int)R.w[4], r, 512)) >> 10;
+        int t2 = dq(2, mad_i24((int)R.w[5], r, 512)) >> 10;
         b = sat_u8(t0), g = sat_u8(t1), r = sat_u8(t2);
     } else { // transform_<uchar,float>
         float fb = (float)b, fg = (float)g, fr = (float)r;
@@ -191,7 +204,10 @@ constexpr int kHueBatch = AEON_HIP_HUE_BATCH; // pixels per hue_apply_n (1, 2 or
 // Over N of a lane's 4 pixels at once: the 2N division-table reads (sdiv[v], hdiv[diff]) and
 // then the N weight-table reads are issued back to back, so one LDS latency is waited for per
 // group of reads instead of one per read (the per-pixel form waited three times per pixel).
-// `hue_small` = |hue| < 180 (uniform; the wrap is then one conditional subtraction).
+// The H byte: OpenCV's h (h12 below, in [-30, 150] for every BGR triple, tools/hue_range.py) +180
+// if negative -- min_u32(h12, h12 + 180) --, so in [0, 179] and its saturate_cast is a no-op; then
+// (H + hue) % 180 stored as uchar.  `hue_small` = |hue| < 180 (uniform): x = H + hue is in
+// (-180, 360) and C's truncating % is one conditional subtraction.
 template <int N, int K0, typename TAB, typename WTAB>
 __device__ __forceinline__ void hue_apply_n(TAB sdiv, TAB hdiv, WTAB wtab, int hue, bool hue_small, int (&pxs)[4][3])
 {
@@ -214,11 +230,9 @@ __device__ __forceinline__ void hue_apply_n(TAB sdiv, TAB hdiv, WTAB wtab, int h
         // operands < 2^23 in magnitude (sdiv <= 255<<12, hdiv <= 30<<12, |h| <= 5*255)
         const int s = mad_i24(diff[k], sd[k], 1 << 11) >> 12;
         int h = (vr & (g - b)) + (~vr & ((vg & (b - r + 2 * diff[k])) + ((~vg) & (r - g + 4 * diff[k]))));
-        h = mad_i24(h, hd[k], 1 << 11) >> 12;
-        h += h < 0 ? 180 : 0;
-        const int x = sat_u8(h) + hue; // H in [0, 180]
-        // C's % (truncating) then the uchar store; for |hue| < 180, x is in (-180, 360)
-        H[k]  = (hue_small ? (x >= 180 ? x - 180 : x) : x % 180) & 0xff;
+        const int h12 = mad_i24(h, hd[k], 1 << 11) >> 12;
+        const int x   = (int)min((uint32_t)h12, (uint32_t)(h12 + 180)) + hue; // h12 < 0 ? h12 + 180 : h12
+        H[k]          = (hue_small ? (x >= 180 ? x - 180 : x) : x % 180) & 0xff;
         sf[k] = (float)s * (1.f / 255);
     }
     f32x4 w[N];
@@ -227,10 +241,14 @@ __device__ __forceinline__ void hue_apply_n(TAB sdiv, TAB hdiv, WTAB wtab, int h
 #pragma unroll
     for (int k = 0; k < N; k++) {
         const float vf = (float)v[k] * (1.f / 255);
+#if defined(AEON_HIP_EXP_HUE_NOTAIL) // development ablation: no HSV2RGB float chain (wrong values)
+        px[k][0] = (int)w[k][0] + v[k], px[k][1] = (int)w[k][1] + (int)sf[k], px[k][2] = (int)w[k][2];
+#else
         // v, s in [0, 1] and w in [0, 1]: every product is in [0, 255], no saturation needed
         px[k][0] = u8rnd(vf * (1.f - sf[k] * w[k][0]) * 255.f);
         px[k][1] = u8rnd(vf * (1.f - sf[k] * w[k][1]) * 255.f);
         px[k][2] = u8rnd(vf * (1.f - sf[k] * w[k][2]) * 255.f);
+#endif
     }
 }
 
@@ -705,6 +723,7 @@ struct Bands {
         const int  bgr   = a.bgr_to_rgb && cn == 3;
         // Lane -> (column group, row phase), fixed for the tile
         const int  gpr    = (win_w + 3) >> 2;
+        const bool full4  = (win_w & 3) == 0; // every lane's group is 4 pixels of the window
         const int  ncg    = min(gpr, nt);
         const int  nph    = nt / ncg;
         const int  lph    = tid / ncg;
@@ -757,11 +776,17 @@ struct Bands {
                         }
                 }
                 if (PHOTO && photo) {
+#ifndef AEON_HIP_EXP_NOBS // development ablation: no brightness/saturation (wrong values)
                     if (photo & PHOTO_BS) {
 #pragma unroll
                         for (int k = 0; k < 4; k++) bs_apply(bs_kind, bsr, val[k][0], val[k][1], val[k][2]);
                     }
-                    if (photo & PHOTO_HUE) { // two pixels at a time: four cost 14 VGPRs (a wave per SIMD)
+#endif
+#ifdef AEON_HIP_EXP_NOHUE // development ablation: no hue (wrong values)
+                    if (false) {
+#else
+                    if (photo & PHOTO_HUE) {
+#endif // two pixels at a time: four cost 14 VGPRs (a wave per SIMD)
                         hue_apply_n<kHueBatch, 0>(sdiv, hdiv, wtab, hue, hue_small, val);
                         if (kHueBatch < 4) hue_apply_n<kHueBatch, kHueBatch % 4>(sdiv, hdiv, wtab, hue, hue_small, val);
                         if (kHueBatch == 1) {
@@ -773,7 +798,7 @@ struct Bands {
                     for (int k = 0; k < 4; k++) {
                         int bb = val[k][0], gg = val[k][1], rr = val[k][2];
                         if (KM == KM_STATS) { // the intermediate keeps the post-hue pixel
-                            if (k < nk) sum0 += bb, sum1 += gg, sum2 += rr;
+                            if (full4 || k < nk) sum0 += bb, sum1 += gg, sum2 += rr;
                             val[k][0] = bb, val[k][1] = gg, val[k][2] = rr;
                             continue;
                         }

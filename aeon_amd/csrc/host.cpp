@@ -5,6 +5,7 @@
 #include <sched.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <numeric>
@@ -513,6 +514,29 @@ void batch_decoder::grow_slot_engines(int n)
 }
 
 namespace {
+// Device address through which the kernels can store straight into host buffer p (pinned and
+// mapped: hipHostMalloc / hipHostRegister), or null for pageable memory.  Such host outputs are
+// written over PCIe by the augmentation (or transpose) kernels themselves -- zero-copy --, which
+// measured 81.6 K against 54 K records/s host->host for C2 with a D2H copy behind the kernels
+// (tools/e2e_probe.py): the kernels' store stream uses both PCIe directions' worth of requests in
+// flight where the copy engine does not.  AEON_HIP_ZERO_COPY=0 keeps the device staging + D2H (the
+// kernels then occupy the CUs only for their HBM-speed run; zero-copy holds them for the PCIe time).
+void* zero_copy_view(void* p)
+{
+    static const bool on = [] {
+        const char* e = std::getenv("AEON_HIP_ZERO_COPY");
+        return !(e && std::atoi(e) == 0);
+    }();
+    if (!on || !p) return nullptr;
+    hipPointerAttribute_t a{};
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError(); // pageable memory: not an error
+        return nullptr;
+    }
+    if (a.type != hipMemoryTypeHost || !a.devicePointer || !a.hostPointer) return nullptr;
+    return (uint8_t*)a.devicePointer + ((uint8_t*)p - (uint8_t*)a.hostPointer);
+}
+
 void grow_dev(uint8_t*& p, size_t& cap, size_t bytes)
 {
     if (bytes <= cap) return;
@@ -528,7 +552,8 @@ void grow_dev(uint8_t*& p, size_t& cap, size_t bytes)
 //   host:   JPEG headers -> make_params (record order: aeon's deterministic draw order) ->
 //           decoded pixels staged into pinned memory on the pool -> JPEG entropy decode
 //   device: H2D of the staged pixels -> JPEG IDCT/colour into the source arena -> augmentation
-//           kernels (post_process) -> [batch transpose] -> [D2H into host outputs]
+//           kernels (post_process) -> [batch transpose] -> host outputs: stored there directly
+//           when pinned (zero_copy_view), else staged on the device + one D2H
 void batch_decoder::enqueue(window_slot& ws, int n, const decoded_element* in, void* const* outputs, bool on_device,
                             hipStream_t stream)
 {
@@ -617,14 +642,17 @@ void batch_decoder::enqueue(window_slot& ws, int n, const decoded_element* in, v
                                              ws.dev_src, stream));
     }
     std::vector<void*> outs(ne);
+    std::vector<bool>  copy_out(ne, false); // staged on the device, then one D2H into outputs[k]
     ws.dev_out.resize(ne, nullptr), ws.dev_out_cap.resize(ne, 0);
     ws.dev_tmp.resize(ne, nullptr), ws.dev_tmp_cap.resize(ne, 0);
     for (int k = 0; k < ne; k++) {
         const size_t bytes = (size_t)n * m_provider->providers()[k]->shape().byte_size();
         if (on_device) outs[k] = outputs[k];
+        else if (void* v = zero_copy_view(outputs[k])) outs[k] = v;
         else {
             grow_dev(ws.dev_out[k], ws.dev_out_cap[k], bytes);
-            outs[k] = ws.dev_out[k];
+            outs[k]     = ws.dev_out[k];
+            copy_out[k] = true;
         }
     }
     if (m_batch_major) {
@@ -647,8 +675,8 @@ void batch_decoder::enqueue(window_slot& ws, int n, const decoded_element* in, v
             }
         }
     }
-    if (!on_device)
-        for (int k = 0; k < ne; k++)
+    for (int k = 0; k < ne; k++)
+        if (copy_out[k])
             hip_check(hipMemcpyAsync(outputs[k], outs[k], (size_t)n * m_provider->providers()[k]->shape().byte_size(),
                                      hipMemcpyDeviceToHost, stream),
                       "hipMemcpyAsync");

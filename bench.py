@@ -184,9 +184,10 @@ def run_device(A, C, torch, cfg, batch, steps, warmup, rank, world, pool_mib, di
     return elapsed, kt, wl.param_us, wl.submit_s
 
 
-def run_e2e(A, C, torch, batch, steps):
+def run_e2e(A, C, torch, batch, steps, zero_copy=False):
     """Host->host rate: pinned decoded pixels -> H2D -> kernel -> D2H into a pinned batch
-    buffer, with copies and kernels on separate streams (PCIe-inclusive)."""
+    buffer, with copies and kernels on separate streams (PCIe-inclusive).  zero_copy:
+    the kernel stores straight into the pinned batch buffer over PCIe (no device output, no D2H)."""
     ctx = A.Context(torch.cuda.current_device())
     w = h = 256
     img_bytes = w * h * 3
@@ -214,9 +215,11 @@ def run_e2e(A, C, torch, batch, steps):
             ev_in[j].record(s_h2d)
         s_k.wait_event(ev_in[j])
         s_k.wait_event(ev_out[j])  # previous D2H of this buffer done
-        ctx.augment_batch(descs, dev_src[j].data_ptr(), params[s % 4], out, dev_dst[j].data_ptr(),
-                          s_k.cuda_stream)
+        dst = host_dst[j].data_ptr() if zero_copy else dev_dst[j].data_ptr()
+        ctx.augment_batch(descs, dev_src[j].data_ptr(), params[s % 4], out, dst, s_k.cuda_stream)
         ev_k[j].record(s_k)
+        if zero_copy:
+            return
         with torch.cuda.stream(s_d2h):
             s_d2h.wait_event(ev_k[j])
             host_dst[j].copy_(dev_dst[j], non_blocking=True)
@@ -581,6 +584,9 @@ def main():
         extra["C5"] = run_c5(A, C, torch, max(5, args.steps // 5), 2, args.pool_mib)
         extra["e2e_host_to_host"] = {"value": run_e2e(A, C, torch, 256, 20), "unit": "images/s",
                                      "what": "pinned H2D of decoded 256x256 u8 + kernel + D2H of fp32 CHW"}
+        extra["e2e_zero_copy"] = {"value": run_e2e(A, C, torch, 256, 20, zero_copy=True), "unit": "images/s",
+                                  "what": "pinned H2D of decoded 256x256 u8 + kernel storing fp32 CHW straight "
+                                          "into the pinned host batch (zero-copy over PCIe, no D2H)"}
         extra["C1"] = {"decoder": run_c1_decoder(A, C, torch)}
         extra["e2e_jpeg_decoder"] = {
             "host_outputs": {"value": run_e2e_jpeg(A, C, torch, on_device=False), "unit": "images/s"},

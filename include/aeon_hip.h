@@ -112,7 +112,10 @@ int aeon_hip_ctx_destroy(aeon_hip_ctx* ctx);
 /* The per-record body of provider::image::provide after extract + make_params, for n records
  * at once: transform_single_image + image::loader::load of record i into
  * out_dev + i*out->item_stride.  Asynchronous on `stream`; src/out must stay valid until the
- * stream reaches this work.  descs/params are host arrays, consumed before return. */
+ * stream reaches this work.  descs/params are host arrays, consumed before return.
+ * src_base / out_dev are device addresses: HBM, or pinned device-mapped host memory
+ * (aeon_hip_host_alloc), which the kernels then read / store over PCIe directly (zero-copy: the
+ * fastest host->host path). */
 int aeon_hip_augment_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs,
                            const void* src_base, const aeon_aug_params* params,
                            const aeon_out_desc* out, void* out_dev, void* stream);

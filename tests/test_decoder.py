@@ -217,3 +217,36 @@ def test_decoder_png_image_and_mask():
         else:
             want = H.oracle_records([m], [p], mod, mask=True)[0]
         assert np.array_equal(msk[i], want.reshape(msk[i].shape)), i
+
+
+def _decode_pinned(d, recs):
+    """One window through submit/wait into pinned host buffers: the kernels store there directly
+    (zero-copy host outputs)."""
+    import torch
+    bufs = [torch.full((len(recs) * o["item_bytes"],), 0xCD, dtype=torch.uint8).pin_memory() for o in d.outputs]
+    d.submit(recs, [b.data_ptr() for b in bufs])
+    d.wait()
+    return [b.numpy().view(o["dtype"]).reshape((len(recs),) + o["shape"]).copy() for b, o in zip(bufs, d.outputs)]
+
+
+@pytest.mark.parametrize("case", ["c5", "batch_major_false", "fixed_aspect_ratio"])
+def test_decoder_zero_copy_outputs_match_staged(case):
+    """Pinned host outputs are written by the kernels themselves (zero_copy_view, host.cpp); pageable
+    ones are staged on the device and copied: the same bytes, including the transposed
+    (batch_major=false) layout and fixed_aspect_ratio's zeroed canvases."""
+    if case == "c5":
+        cfg = dict(batch_size=6, random_seed=3, etl=[C.IMAGE_512, C.MASK_512], augmentation=[C.C5_AUG])
+        recs = _records(6, seed=2, mask=True)
+    elif case == "batch_major_false":
+        cfg = dict(batch_size=4, random_seed=9, batch_major=False, etl=[C.IMAGE_224], augmentation=[C.C3_AUG])
+        recs = _records(8, seed=4)
+    else:
+        aug = {"type": "image", "fixed_aspect_ratio": True, "crop_enable": False, "flip_enable": True}
+        etl = {"type": "image", "height": 256, "width": 256, "channels": 3, "output_type": "float",
+               "channel_major": True, "bgr_to_rgb": True}
+        cfg = dict(batch_size=6, random_seed=9, etl=[etl], augmentation=[aug])
+        recs = _records(6, seed=4)
+    want = A.Decoder(cfg).decode(recs)
+    got = _decode_pinned(A.Decoder(cfg), recs)
+    for w, g in zip(want, got):
+        assert w.dtype == g.dtype and np.array_equal(w.view(np.uint8), g.view(np.uint8)), case

@@ -274,6 +274,14 @@ EDGE_CASES = [
                                                out_h=224, saturation=40.0), {}),
     ("hue_neg", (256, 256), dict(crop_x=0, crop_y=0, crop_w=256, crop_h=256, out_w=224, out_h=224, hue=-179), {}),
     ("hue_pos", (256, 256), dict(crop_x=0, crop_y=0, crop_w=256, crop_h=256, out_w=224, out_h=224, hue=180), {}),
+    # hue wraps: |hue| < 180 (one conditional subtraction, negative H stored as uchar) and the rest
+    ("hue_179", (256, 256), dict(crop_x=0, crop_y=0, crop_w=256, crop_h=256, out_w=224, out_h=224, hue=179), {}),
+    ("hue_m1_sat", (256, 256), dict(crop_x=0, crop_y=0, crop_w=256, crop_h=256, out_w=224, out_h=224, hue=-1,
+                                    saturation=1.7), {}),
+    ("hue_m180_contrast", (256, 256), dict(crop_x=0, crop_y=0, crop_w=256, crop_h=256, out_w=224, out_h=224,
+                                           hue=-180, contrast=0.8), {}),
+    ("hue_401", (256, 256), dict(crop_x=0, crop_y=0, crop_w=256, crop_h=256, out_w=224, out_h=224, hue=401), {}),
+    ("hue_m397", (256, 256), dict(crop_x=0, crop_y=0, crop_w=256, crop_h=256, out_w=224, out_h=224, hue=-397), {}),
     ("contrast_only", (256, 256), dict(crop_x=0, crop_y=0, crop_w=256, crop_h=256, out_w=224, out_h=224,
                                        contrast=0.3), {}),
     ("lighting_only", (256, 256), dict(crop_x=0, crop_y=0, crop_w=256, crop_h=256, out_w=224, out_h=224,
@@ -403,6 +411,47 @@ def test_full_batch_c5_all_records(ctx):
     assert all(np.array_equal(a, b) for a, b in zip(i1 + m1, i2 + m2)), "C5 rerun differs"
     _assert_same(i1, H.oracle_records(imgs, params, iout), "C5 image full batch")
     _assert_same(m1, H.oracle_records(masks, params, mout, mask=True), "C5 mask full batch")
+
+
+@pytest.mark.parametrize("cfg", ["C2", "C3", "C5_mask", "fixed_u8"])
+def test_zero_copy_host_buffers(ctx, cfg):
+    """Outputs stored straight into pinned host memory by the kernels (out_dev = a device-mapped
+    pinned buffer: the zero-copy host->host path, tools/e2e_probe.py), and sources read from pinned
+    host memory, give exactly the device-resident call's bytes -- single-pass, contrast two-pass,
+    the mask gather pass, and fixed_aspect_ratio (whose canvas fill is a memset on the host buffer)."""
+    import torch
+    n = 24
+    mask = cfg == "C5_mask"
+    if mask:
+        rng = np.random.default_rng(3)
+        imgs = [rng.integers(0, 21, (480, 640), dtype=np.uint8) for _ in range(n)]
+        params = H.draw_params(C.C5_AUG, [(640, 480)] * n, 512, 512, seed=2)
+        out = C.out_desc_for(C.MASK_512, C.C5_AUG)
+    elif cfg == "fixed_u8":
+        aug = {"type": "image", "fixed_aspect_ratio": True, "crop_enable": False, "flip_enable": True}
+        etl = {"type": "image", "height": 96, "width": 128, "channels": 3, "output_type": "uint8_t",
+               "channel_major": True}
+        sizes = [(64 + 7 * i, 40 + 5 * i) for i in range(n)]
+        imgs = [A.synthetic_image(i, w, h, 3) for i, (w, h) in enumerate(sizes)]
+        params = H.draw_params(aug, sizes, 128, 96, seed=6)
+        out = C.out_desc_for(etl, aug)
+    else:
+        aug = C.C2_AUG if cfg == "C2" else C.C3_AUG
+        imgs = _synthetic(n)
+        params = H.draw_params(aug, [(256, 256)] * n, 224, 224, seed=4)
+        out = C.out_desc_for(C.IMAGE_224, aug)
+    arena, descs = A.pack_images(imgs)
+    run = ctx.mask_batch if mask else ctx.augment_batch
+    stream = torch.cuda.current_stream().cuda_stream
+    src_dev = torch.from_numpy(arena).to("cuda")
+    dst_dev = torch.full((n * out.item_stride,), 0xAB, dtype=torch.uint8, device="cuda")
+    run(descs, src_dev.data_ptr(), params, out, dst_dev.data_ptr(), stream)
+    src_host = torch.from_numpy(arena).pin_memory()
+    for src in (src_dev, src_host):
+        dst_host = torch.full((n * out.item_stride,), 0xCD, dtype=torch.uint8).pin_memory()
+        run(descs, src.data_ptr(), params, out, dst_host.data_ptr(), stream)
+        ctx.synchronize(stream)
+        assert torch.equal(dst_host, dst_dev.cpu()), (cfg, "host source" if src is src_host else "device source")
 
 
 @pytest.mark.parametrize("aug_name", ["C2", "C3_no_contrast", "C5_image", "nearest_u8"])
