@@ -71,10 +71,12 @@ struct alignas(16) AugJob {
 struct alignas(16) RotJob {
     double   M[6];     // warpAffine's inverted affine map (output -> source), as OpenCV computes it
     uint64_t src_ptr;  // HWC uint8 source
-    uint64_t out_ptr;  // HWC uint8 rotated image (w * cn bytes per row)
-    int32_t  w, h, stride, cn;
+    uint64_t out_ptr;  // HWC uint8 window [ox, ox+ow) x [oy, oy+oh) of the rotated image (ow * cn bytes per row)
+    int32_t  w, h, stride, cn; // the source (= rotated image) size; cn = bytes per pixel (1..4)
     int32_t  interp;   // AEON_INTERP_LINEAR (images) or AEON_INTERP_NEAREST (pixel masks)
-    int32_t  pad_;
+    int32_t  ox, oy, ow, oh; // the window of the rotated image later stages read (the cropbox, or all)
+    int32_t  angle;          // degrees (sizes the launch's LDS source box)
+    int32_t  pad_[2];
 };
 
 // image::expand pre-pass of one record (rotate_kernels.hip): the record at (ox, oy) of a zeroed

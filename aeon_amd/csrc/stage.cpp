@@ -34,7 +34,8 @@ hipError_t contrast_fused_occupancy(const FusedArgs& A, int threads, int lds_byt
 hipError_t set_kernel_lds_limit(int bytes);
 hipError_t launch_transpose(const void* src, void* dst, int64_t rows, int64_t cols, int element_size,
                             hipStream_t stream);
-hipError_t launch_rotate(const RotJob* jobs, int n_jobs, int max_pixels, hipStream_t stream);
+hipError_t launch_rotate(const RotJob* jobs, int n_jobs, int max_tiles, int words, int cn, hipStream_t stream);
+int        rot_box_words(int angle);
 hipError_t launch_expand(const ExpandJob* jobs, int n_jobs, int max_pixels, hipStream_t stream);
 hipError_t launch_nearest(const Mask16Job* jobs, int n_jobs, int max_h, int max_w, int max_seg_bytes, hipStream_t stream,
                           hipEvent_t start, hipEvent_t stop);
@@ -300,18 +301,22 @@ void plan_mask16(const aeon_img_desc& d, const void* src_base, const aeon_aug_pa
         // image::rotate(..., interpolate = false, border 0) (etl_pixel_mask.cpp:72-74,
         // etl_depthmap.cpp:72-73): nearest moves whole elements, so a 16-bit record rotates as a
         // 2-byte-per-pixel one; the gather pass then reads the rotated copy in the slot scratch
+        // only the cropbox window of the rotated record is produced (the gather reads nothing else)
         RotJob R{};
         rotation_inverse_map(d.width, d.height, p.angle, R.M);
         R.src_ptr = M.src_ptr;
         R.w = d.width, R.h = d.height, R.stride = d.stride, R.cn = eb;
         R.interp      = AEON_INTERP_NEAREST;
+        R.ox = p.crop_x, R.oy = p.crop_y, R.ow = p.crop_w, R.oh = p.crop_h;
         size_t off    = (scratch_bytes + 15) & ~(size_t)15;
-        scratch_bytes = off + (size_t)d.width * d.height * eb + 16;
+        scratch_bytes = off + (size_t)R.ow * R.oh * eb + 16;
         R.out_ptr     = off; // relocated to the slot's scratch by the caller
+        R.angle       = p.angle;
         rot.push_back(R);
         M.src_ptr     = off;
         M.src_scratch = 1;
-        M.src_stride  = d.width * eb;
+        M.src_stride  = R.ow * eb;
+        M.crop_x = M.crop_y = 0;
     }
     m16.push_back(M);
 }
@@ -365,19 +370,27 @@ void plan_image(const aeon_img_desc& d, const void* src_base, const aeon_aug_par
     if (p.angle != 0) {
         // image::rotate into scratch (interpolated for images, nearest + border 0 for pixel
         // masks, etl_pixel_mask.cpp:72-74); everything after reads the rotated record
+        // Only the cropbox window is produced when nothing before the crop needs the whole rotated
+        // record (no expand canvas, no resize_short of it); the job then crops it at (0, 0).
         RotJob R{};
         rotation_inverse_map(d.width, d.height, p.angle, R.M);
         R.src_ptr = J.src_ptr;
         R.w = d.width, R.h = d.height, R.stride = d.stride, R.cn = cn;
-        R.interp      = is_mask ? AEON_INTERP_NEAREST : AEON_INTERP_LINEAR;
+        R.interp = is_mask ? AEON_INTERP_NEAREST : AEON_INTERP_LINEAR;
+        const bool window = is_mask || (!expands(p) && p.resize_short_size <= 0);
+        R.ox = window ? p.crop_x : 0, R.oy = window ? p.crop_y : 0;
+        R.ow = window ? p.crop_w : d.width, R.oh = window ? p.crop_h : d.height;
         size_t off    = (scratch_bytes + 15) & ~(size_t)15;
-        scratch_bytes = off + (size_t)d.width * d.height * cn + 16;
+        scratch_bytes = off + (size_t)R.ow * R.oh * cn + 16;
         R.out_ptr     = off; // relocated to the slot's scratch by the caller
+        R.angle       = p.angle;
         rot.push_back(R);
         J.src_ptr     = off;
         J.src_scratch = 1;
-        J.src_bytes   = (uint64_t)d.width * d.height * cn;
-        J.src_stride  = d.width * cn;
+        J.src_w = R.ow, J.src_h = R.oh;
+        J.src_bytes   = (uint64_t)R.ow * R.oh * cn;
+        J.src_stride  = R.ow * cn;
+        J.crop_x -= R.ox, J.crop_y -= R.oy;
     }
     if (!is_mask && expands(p)) {
         // image::expand (image.cpp:276-303) into scratch: a zeroed expand_w x expand_h canvas with the
@@ -995,8 +1008,13 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
         m16_max_seg = std::max(m16_max_seg, M.crop_w * M.src_elem);
         m16_bytes += (double)M.crop_w * M.crop_h * M.src_elem + (double)M.out_w * M.out_h * out_elem_bytes(M.dtype);
     }
-    int              rot_max_px = 0;
-    for (const RotJob& R : rot) rot_max_px = std::max(rot_max_px, R.w * R.h);
+    int              rot_max_tiles = 0, rot_words = 0, rot_cn = rot.empty() ? 0 : rot[0].cn; // (rotate_tiles)
+    for (size_t r = 0; r < rot.size(); r++) {
+        const RotJob& R = rot[r];
+        if (R.cn != rot_cn) rot_cn = 0;
+        rot_max_tiles   = std::max(rot_max_tiles, ((R.ow + 63) / 64) * ((R.oh + 31) / 32));
+        rot_words       = std::max(rot_words, rot_box_words(R.angle));
+    }
     std::vector<int> slot_tiles(pass1_all.jobs.size(), 0);
     int              partial_stride = 1;
     // both passes of the contrast records in one launch: every record a contrast record, one pass-1
@@ -1089,7 +1107,7 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
         HIP_OK(hipMemset2DAsync(out_dev, o.item_stride, 0,
                                 (size_t)o.canvas_w * o.canvas_h * o.channels * out_elem_bytes(od.dtype), n, stream));
     if (!rot.empty()) // image::rotate pre-pass first: the gather and tile passes read its output
-        HIP_OK(launch_rotate((const RotJob*)(table + rot_off), (int)rot.size(), rot_max_px, stream));
+        HIP_OK(launch_rotate((const RotJob*)(table + rot_off), (int)rot.size(), rot_max_tiles, rot_words, rot_cn, stream));
     if (!exp.empty()) // then image::expand (etl_image.cpp:155-159)
         HIP_OK(launch_expand((const ExpandJob*)(table + exp_off), (int)exp.size(), exp_max_px, stream));
     if (!m16.empty()) {
