@@ -111,6 +111,7 @@ void param_factory::make_params(URNG& random, int in_w, int in_h, int out_w, int
                                 aeon_aug_params* p) const
 {
     *p            = aeon_aug_params{};
+    p->expand_ratio = 1.0f; // augment::image::params default (augment_image.hpp:99): make_params leaves it
     p->out_w      = out_w;
     p->out_h      = out_h;
     p->angle      = angle(random);

@@ -128,6 +128,7 @@ void make_params(const Factory& fc, Engine& eng, int in_w, int in_h, int out_w, 
     Factory&              f = const_cast<Factory&>(fc); // distributions are `mutable` in aeon
     const orc_aug_config& c = f.c;
     std::memset(p, 0, sizeof(*p));
+    p->expand_ratio = 1.0f; // augment::image::params default (augment_image.hpp:99)
     p->out_w      = out_w;
     p->out_h      = out_h;
     p->angle      = f.angle(eng);

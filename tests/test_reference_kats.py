@@ -1,0 +1,135 @@
+"""aeon's own image-transform known-answer tests (test/test_image.cpp) that earlier rounds had not
+restated: expand, expand + crop + flip + resize, the SSD "warp" resize, the fixed-aspect flip and
+the param factory's expand / fixed_scaling_factor rules.  Pixel cases run through the oracle (CPU)
+and the HIP stage (GPU) on the reference's own synthetic inputs and assert the reference's own
+expectations; param cases run through the product's param factory (C ABI) and the oracle's."""
+import numpy as np
+import pytest
+
+import aeon_amd as A
+from tests import helpers as H
+
+
+def _indexed(rows, cols):
+    """generate_indexed_image (test_image.cpp:42-57): b = col, g = row, r = 0."""
+    img = np.zeros((rows, cols, 3), np.uint8)
+    img[:, :, 0] = np.arange(cols, dtype=np.uint8)[None, :]
+    img[:, :, 1] = np.arange(rows, dtype=np.uint8)[:, None]
+    return img
+
+
+def _striped(width, height, left, right):
+    """generate_stripped_image (test_image.cpp:59-84): colours as 0xRRGGBB in B, G, R byte order."""
+    img = np.zeros((height, width, 3), np.uint8)
+    for half, col in ((slice(0, width // 2), left), (slice(width // 2, width), right)):
+        img[:, half] = (col & 0xFF, (col >> 8) & 0xFF, (col >> 16) & 0xFF)
+    return img
+
+
+def _u8(w, h):
+    return A.out_desc(channels=3, channel_major=False, dtype="uint8", item_stride=3 * w * h)
+
+
+def _run(runner, ctx, img, p, out):
+    rec = H.hip_records(ctx, [img], [p], out) if runner == "gpu" else H.oracle_records([img], [p], out)
+    return rec[0].reshape(p.out_h, p.out_w, 3) if not out.fixed_aspect_ratio else rec[0]
+
+
+RUNNERS = ["oracle", pytest.param("gpu", marks=pytest.mark.gpu)]
+
+
+@pytest.fixture(scope="module")
+def gpu_ctx():
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need a GPU"
+    c = A.Context(0)
+    yield c
+    c.close()
+
+
+@pytest.fixture
+def ctx_for(request):
+    def get(runner):
+        return request.getfixturevalue("gpu_ctx") if runner == "gpu" else None
+    return get
+
+
+@pytest.mark.parametrize("runner", RUNNERS)
+def test_kat_expand(runner, ctx_for):
+    """image.expand (test_image.cpp:1254-1291): a 200x300 (0, 0, 255) record, expand_ratio 4 with
+    probability 1, no crop: the output is a zeroed 800x1200 canvas holding the record at the drawn
+    expand_offset."""
+    img = np.zeros((300, 200, 3), np.uint8)
+    img[:] = (0, 0, 255)
+    aug = {"type": "image", "expand_probability": 1.0, "expand_ratio": [4.0, 4.0], "crop_enable": False}
+    p = A.ParamFactory(aug).make_ssd_params(np.array([7], np.uint32), 200, 300, 800, 1200, [])
+    assert (p.expand_w, p.expand_h) == (800, 1200) and p.expand_ratio == 4.0
+    want = np.zeros((1200, 800, 3), np.uint8)
+    want[p.expand_y:p.expand_y + 300, p.expand_x:p.expand_x + 200] = (0, 0, 255)
+    assert np.array_equal(_run(runner, ctx_for(runner), img, p, _u8(800, 1200)), want)
+
+
+@pytest.mark.parametrize("runner", RUNNERS)
+def test_kat_transform_expand_crop_flip_resize(runner, ctx_for):
+    """image.transform_expand_crop_flip_resize (test_image.cpp:495-562): a 25x25 (0xFF, 0, 0)
+    record expanded to 100x100 at (50, 0), cropped to (50, 0, 50, 50), flipped and resized to
+    100x100: the record fills the top-right quarter, zeros elsewhere (5-pixel blur band)."""
+    img = np.zeros((25, 25, 3), np.uint8)
+    img[:] = (0xFF, 0, 0)
+    p = A.aug_params(crop_x=50, crop_y=0, crop_w=50, crop_h=50, out_w=100, out_h=100, flip=1, expand_ratio=4.0,
+                     expand_x=50, expand_y=0, expand_w=100, expand_h=100)
+    got = _run(runner, ctx_for(runner), img, p, _u8(100, 100))
+    i, j = np.meshgrid(np.arange(100), np.arange(100), indexing="ij")
+    blue = (j >= 55) & (i < 45)
+    zero = (j < 45) | (i >= 55)
+    assert (got[blue] == (0xFF, 0, 0)).all() and (got[zero] == 0).all()
+
+
+@pytest.mark.parametrize("runner", RUNNERS)
+def test_kat_warp_resize(runner, ctx_for):
+    """image.warp_resize (test_image.cpp:1138-1206): make_ssd_params of a 100x200 left-blue /
+    right-green striped record to 400x400 (aspect not kept): every row is blue then green outside
+    the 10-pixel blur band around the middle."""
+    img = _striped(100, 200, 0xFF, 0xFF00)
+    p = A.ParamFactory({"type": "image"}).make_ssd_params(np.array([1], np.uint32), 100, 200, 400, 400, [])
+    got = _run(runner, ctx_for(runner), img, p, _u8(400, 400))
+    assert (got[:, :195] == (0xFF, 0, 0)).all()
+    assert (got[:, 205:] == (0, 0xFF, 0)).all()
+
+
+@pytest.mark.parametrize("runner", RUNNERS)
+def test_kat_var_transform_flip(runner, ctx_for):
+    """image.var_transform_flip (test_image.cpp:1293-1323): the 256x256 indexed record with
+    fixed_aspect_ratio, no crop, flip forced: output pixel (x, y) has b = 255 - x, g = y."""
+    aug = {"type": "image", "fixed_aspect_ratio": True, "crop_enable": False}
+    p = A.ParamFactory(aug).make_params(np.array([3], np.uint32), 256, 256, 256, 256)
+    p.flip = 1
+    out = A.out_desc(channels=3, channel_major=False, dtype="uint8", item_stride=3 * 256 * 256,
+                     fixed_aspect_ratio=True, canvas=(256, 256))
+    got = _run(runner, ctx_for(runner), _indexed(256, 256), p, out)
+    got = got.reshape(256, 256, 3)
+    assert tuple(got[0, 0, :2]) == (255, 0)
+    assert tuple(got[100, 100, :2]) == (255 - 100, 100)
+
+
+def test_kat_var_resize_fixed_scale(oracle):
+    """image.var_resize_fixed_scale (test_image.cpp:1102-1136): fixed_aspect_ratio with
+    fixed_scaling_factor 1.0 keeps a 300x200 record at 300x200 inside a 400x400 config."""
+    aug = {"type": "image", "fixed_aspect_ratio": True, "crop_enable": False, "fixed_scaling_factor": 1.0}
+    p = A.ParamFactory(aug).make_params(np.array([1], np.uint32), 300, 200, 400, 400)
+    q = oracle.Factory(H.oracle_aug_config(aug)).make_params(np.array([1], np.uint32), 300, 200, 400, 400)
+    for r in (p, q):
+        assert (r.out_w, r.out_h) == (300, 200)
+
+
+def test_kat_expand_not_and_invalid_ratio():
+    """image.expand_not / expand_ratio_invalid (test_image.cpp:1208-1252): expand_probability 0
+    leaves expand_ratio at 1; an expand_ratio range below 1 is refused by the factory."""
+    aug = {"type": "image", "expand_probability": 0.0, "expand_ratio": [5, 10], "crop_enable": False}
+    p = A.ParamFactory(aug).make_params(np.array([1], np.uint32), 300, 300, 300, 300)
+    assert p.expand_ratio == 1.0
+    q = H.O.Factory(H.oracle_aug_config(aug)).make_params(np.array([1], np.uint32), 300, 300, 300, 300)
+    assert q.expand_ratio == 1.0
+    with pytest.raises(A.AeonHipError):
+        A.ParamFactory({"type": "image", "expand_probability": 1.0, "expand_ratio": [0.01, 0.99],
+                        "crop_enable": False})
