@@ -133,3 +133,37 @@ def test_kat_expand_not_and_invalid_ratio():
     with pytest.raises(A.AeonHipError):
         A.ParamFactory({"type": "image", "expand_probability": 1.0, "expand_ratio": [0.01, 0.99],
                         "crop_enable": False})
+
+
+CONVERT_CASES = [  # test_image.cpp: noconvert_nosplit 686-720, noconvert_split 722-757,
+    ("noconvert_nosplit", "uint8", False),  # convert_nosplit 759-792, convert_split 794-829
+    ("noconvert_split", "uint8", True),
+    ("convert_nosplit", "int32", False),
+    ("convert_split", "int32", True),
+]
+
+
+@pytest.mark.parametrize("runner", RUNNERS)
+@pytest.mark.parametrize("name,dtype,channel_major", CONVERT_CASES)
+def test_kat_loader_convert_split(runner, ctx_for, name, dtype, channel_major):
+    """image.{no,}convert_{no,}split: a constant 100x100 BGR record loaded untransformed as uint8 /
+    uint32_t (int32 planes), interleaved or channel-major: every element is its channel's value."""
+    img = np.zeros((100, 100, 3), np.uint8)
+    img[:] = (50, 100, 150) if channel_major else (50, 100, 200)
+    p = A.aug_params(crop_x=0, crop_y=0, crop_w=100, crop_h=100, out_w=100, out_h=100)
+    es = 1 if dtype == "uint8" else 4
+    out = A.out_desc(channels=3, channel_major=channel_major, dtype=dtype, item_stride=3 * 100 * 100 * es)
+    rec = (H.hip_records(ctx_for(runner), [img], [p], out) if runner == "gpu" else
+           H.oracle_records([img], [p], out))[0]
+    flat = np.frombuffer(np.ascontiguousarray(rec).tobytes(), np.uint8 if es == 1 else np.int32)
+    if channel_major:
+        want = np.concatenate([np.full(100 * 100, 50 * (c + 1)) for c in range(3)])
+    else:
+        want = np.tile([50, 100, 200], 100 * 100)
+    assert np.array_equal(flat, want), name
+
+
+def test_kat_config_bad_scale():
+    """image.config_bad_scale (test_image.cpp:978-993): a scale range reaching above 1 is refused."""
+    with pytest.raises(A.AeonHipError):
+        A.ParamFactory({"type": "image", "horizontal_distortion": [2, 2], "scale": [0.5, 1.5], "flip_enable": False})
