@@ -204,12 +204,11 @@ constexpr int kHueBatch = AEON_HIP_HUE_BATCH; // pixels per hue_apply_n (1, 2 or
 // Over N of a lane's 4 pixels at once: the 2N division-table reads (sdiv[v], hdiv[diff]) and
 // then the N weight-table reads are issued back to back, so one LDS latency is waited for per
 // group of reads instead of one per read (the per-pixel form waited three times per pixel).
-// The H byte: OpenCV's h (h12 below, in [-30, 150] for every BGR triple, tools/hue_range.py) +180
-// if negative -- min_u32(h12, h12 + 180) --, so in [0, 179] and its saturate_cast is a no-op; then
-// (H + hue) % 180 stored as uchar.  `hue_small` = |hue| < 180 (uniform): x = H + hue is in
-// (-180, 360) and C's truncating % is one conditional subtraction.
+// htab = the tile's hue table at h12 = 0 (kHueTabBytes): OpenCV's h (h12 below, in [-30, 150] for
+// every BGR triple, tools/hue_range.py) -> its +180 wrap, + hue, % 180 stored as uchar, -> the
+// HSV2RGB weights of that H, all folded into the one lookup.
 template <int N, int K0, typename TAB, typename WTAB>
-__device__ __forceinline__ void hue_apply_n(TAB sdiv, TAB hdiv, WTAB wtab, int hue, bool hue_small, int (&pxs)[4][3])
+__device__ __forceinline__ void hue_apply_n(TAB sdiv, TAB hdiv, WTAB htab, int (&pxs)[4][3])
 {
     int (*px)[3] = pxs + K0; // pixels K0 .. K0 + N - 1
     int v[N], diff[N], sd[N], hd[N];
@@ -221,7 +220,7 @@ __device__ __forceinline__ void hue_apply_n(TAB sdiv, TAB hdiv, WTAB wtab, int h
     }
 #pragma unroll
     for (int k = 0; k < N; k++) sd[k] = sdiv[v[k]], hd[k] = hdiv[diff[k]];
-    int   H[N];
+    int   h12[N];
     float sf[N];
 #pragma unroll
     for (int k = 0; k < N; k++) {
@@ -230,14 +229,12 @@ __device__ __forceinline__ void hue_apply_n(TAB sdiv, TAB hdiv, WTAB wtab, int h
         // operands < 2^23 in magnitude (sdiv <= 255<<12, hdiv <= 30<<12, |h| <= 5*255)
         const int s = mad_i24(diff[k], sd[k], 1 << 11) >> 12;
         int h = (vr & (g - b)) + (~vr & ((vg & (b - r + 2 * diff[k])) + ((~vg) & (r - g + 4 * diff[k]))));
-        const int h12 = mad_i24(h, hd[k], 1 << 11) >> 12;
-        const int x   = (int)min((uint32_t)h12, (uint32_t)(h12 + 180)) + hue; // h12 < 0 ? h12 + 180 : h12
-        H[k]          = (hue_small ? (x >= 180 ? x - 180 : x) : x % 180) & 0xff;
+        h12[k] = mad_i24(h, hd[k], 1 << 11) >> 12;
         sf[k] = (float)s * (1.f / 255);
     }
     f32x4 w[N];
 #pragma unroll
-    for (int k = 0; k < N; k++) w[k] = wtab[H[k]];
+    for (int k = 0; k < N; k++) w[k] = htab[h12[k]];
 #pragma unroll
     for (int k = 0; k < N; k++) {
         const float vf = (float)v[k] * (1.f / 255);
@@ -638,6 +635,16 @@ struct Bands {
                 xt[x]        = (i32x2){c.sx - G.u_lo, (c.a0 & 0xffff) | (c.a1 << 16)};
             }
         }
+        if (PHOTO && KM != KM_RAW && a.has_hue && J.cn == 3 && (J.photo & PHOTO_HUE)) {
+            // the record's hue table (kHueTabBytes): cvtColor's H of h12, + hue, % 180 as uchar
+            const auto    ht  = lds_ptr<f32x4>(L.hsv + kHsvDivWords * 4 + b * kHueTabBytes);
+            const f32x4*  wt  = reinterpret_cast<const f32x4*>(a.hsv_tables + kHsvDivWords);
+            const int     hue = J.hue;
+            for (int i = tid; i < kHueTabEntries; i += nt) {
+                const int h12 = i - 30;
+                ht[i]         = wt[(((h12 < 0 ? h12 + 180 : h12) + hue) % 180) & 0xff];
+            }
+        }
         const auto yt = lds_ptr<i32x4>(L.yt) + b * a.rows_per_tile;
         for (int r = tid; r < f.nrows; r += nt) {
             const YTap y = ycoef<RM>(J.win_y + f.y0 + r, J.scale_y, J.crop_h);
@@ -683,34 +690,55 @@ struct Bands {
         if (f.ok) stage_unpack(job_ref(a, f.job), f.G, L.stage + b * L.stage_bytes, wave, nw);
     }
 
+    // SPEC_BS_HUE: the tile's record is known (fast_photo) to be 3-channel, 4-pixel-aligned, with
+    // brightness/saturation in the 10-bit fixed-point cv::transform and a hue shift:
+    // the pixel loop then carries no per-pixel branches on those run-time choices (their merged
+    // paths cost ~7 VALU per pixel: conversions and moves the compiler hoists out of the branches).
+    enum : int { SPEC_NONE = 0, SPEC_BS_HUE = 1 };
+    static constexpr bool kHasSpec = KM == KM_STATS && PHOTO && RM == RESIZE_LINEAR && !TAIL && IAUX == 0;
+    __device__ __forceinline__ bool fast_photo(const Info& f) const
+    {
+        if (!kHasSpec || !f.ok) return false;
+        cjob& J = job_ref(a, f.job);
+        return J.cn == 3 && (J.photo & (PHOTO_BS | PHOTO_HUE)) == (PHOTO_BS | PHOTO_HUE) && J.bs_kind == BS_FIXPT &&
+               (J.win_w & 3) == 0;
+    }
+    __device__ __forceinline__ int compute_any(const Info& f, int b) const
+    {
+        if constexpr (kHasSpec)
+            if (fast_photo(f)) return compute<SPEC_BS_HUE>(f, b);
+        return compute<SPEC_NONE>(f, b);
+    }
+
     // Compute and store tile t from buffer b.  Returns a lower bound on the vector-memory
     // instructions this wave issued (its stores): all younger than the next tile's staging loads.
+    template <int SPEC = SPEC_NONE>
     __device__ __forceinline__ int compute(const Info& f, int b) const
     {
         if (!f.ok) return 0;
+        constexpr bool SP = SPEC == SPEC_BS_HUE;
         const int  band = f.band, y0 = f.y0, nrows = f.nrows;
         cjob&      J     = job_ref(a, f.job);
         const int  tid   = threadIdx.x;
         const int  nt    = blockDim.x;
-        const int  cn    = J.cn;
+        const int  cn    = SP ? 3 : J.cn;
         const int  win_w = J.win_w;
         const auto xt    = lds_ptr<const i32x2>(L.xt) + b * a.max_win_w;
         const auto yt    = lds_ptr<const i32x4>(L.yt) + b * a.rows_per_tile;
         const auto sdiv  = lds_ptr<const int32_t>(L.hsv);
         const auto hdiv  = sdiv + 256;
-        const int  photo = (PHOTO && KM != KM_RAW && cn == 3) ? J.photo : 0;
+        // (a STATS tile's chain ends at the intermediate: only BS and HUE matter to it)
+        const int  photo = SP ? (PHOTO_BS | PHOTO_HUE) : (PHOTO && KM != KM_RAW && cn == 3) ? J.photo : 0;
         double     sh0 = 0, sh1 = 0, sh2 = 0;
         if (KM == KM_FINAL && (photo & PHOTO_CONTRAST)) {
             const double* sh = a.shifts + (size_t)J.stats_slot * 4;
             sh0 = sh[0], sh1 = sh[1], sh2 = sh[2];
         }
         uint32_t sum0 = 0, sum1 = 0, sum2 = 0;
-        const auto wtab      = lds_ptr<const f32x4>(L.hsv + 2048);
-        const int  hue       = (photo & PHOTO_HUE) ? J.hue : 0;
-        const bool hue_small = hue > -180 && hue < 180;
+        const auto htab = lds_ptr<const f32x4>(L.hsv + kHsvDivWords * 4 + b * kHueTabBytes) + 30; // at h12 = 0
         BsRegs   bsr{};
         int      bs_kind = 0;
-        if (PHOTO && (photo & PHOTO_BS)) bs_kind = J.bs_kind, bsr = bs_regs(J);
+        if (PHOTO && (photo & PHOTO_BS)) bs_kind = SP ? (int)BS_FIXPT : J.bs_kind, bsr = bs_regs(J);
 
         const int  elem  = KM != KM_FINAL ? 1 : out_elem_bytes(a.out_dtype);
         const int  plane = win_w * J.win_h;
@@ -723,7 +751,7 @@ struct Bands {
         const int  bgr   = a.bgr_to_rgb && cn == 3;
         // Lane -> (column group, row phase), fixed for the tile
         const int  gpr    = (win_w + 3) >> 2;
-        const bool full4  = (win_w & 3) == 0; // every lane's group is 4 pixels of the window
+        const bool full4  = SP || (win_w & 3) == 0; // every lane's group is 4 pixels of the window
         const int  ncg    = min(gpr, nt);
         const int  nph    = nt / ncg;
         const int  lph    = tid / ncg;
@@ -740,7 +768,7 @@ struct Bands {
 
         for (int cg = active ? lcg : gpr; cg < gpr; cg += ncg) {
             const int ox0 = cg * 4;
-            const int nk  = min(4, win_w - ox0);
+            const int nk  = SP ? 4 : min(4, win_w - ox0);
             int       col[4];
             uint32_t  wxk[4];
             int       tmask = 0;
@@ -787,11 +815,11 @@ struct Bands {
 #else
                     if (photo & PHOTO_HUE) {
 #endif // two pixels at a time: four cost 14 VGPRs (a wave per SIMD)
-                        hue_apply_n<kHueBatch, 0>(sdiv, hdiv, wtab, hue, hue_small, val);
-                        if (kHueBatch < 4) hue_apply_n<kHueBatch, kHueBatch % 4>(sdiv, hdiv, wtab, hue, hue_small, val);
+                        hue_apply_n<kHueBatch, 0>(sdiv, hdiv, htab, val);
+                        if (kHueBatch < 4) hue_apply_n<kHueBatch, kHueBatch % 4>(sdiv, hdiv, htab, val);
                         if (kHueBatch == 1) {
-                            hue_apply_n<1, 2>(sdiv, hdiv, wtab, hue, hue_small, val);
-                            hue_apply_n<1, 3>(sdiv, hdiv, wtab, hue, hue_small, val);
+                            hue_apply_n<1, 2>(sdiv, hdiv, htab, val);
+                            hue_apply_n<1, 3>(sdiv, hdiv, htab, val);
                         }
                     }
 #pragma unroll
@@ -982,7 +1010,7 @@ void augment_tiles(LaunchArgs a)
     }
     if (PHOTO && KM != KM_RAW && a.has_hue) {
         const auto hsv = lds_ptr<int32_t>(L.hsv);
-        for (int i = tid; i < kHsvWords; i += nt) hsv[i] = a.hsv_tables[i];
+        for (int i = tid; i < kHsvDivWords; i += nt) hsv[i] = a.hsv_tables[i];
     }
     if (KM == KM_FINAL && PHOTO && a.has_rtab) __syncthreads(); // record tables read the LUT
     // static schedule: tiles blockIdx.x, +G, +2G, ... -- the tiles in flight at any moment are
@@ -1025,7 +1053,7 @@ void augment_tiles(LaunchArgs a)
             __syncthreads();
             stamp(it, 6);
             __builtin_amdgcn_s_setprio(KM == KM_STATS ? kStagePrio : kComputePrio);
-            W.compute(f, 0);
+            W.compute_any(f, 0);
             stamp(it, 7);
             lds_barrier(); // everyone is done reading the buffer before it is refilled
             stamp(it, 8);
@@ -1150,7 +1178,7 @@ void augment_contrast_fused(FusedArgs A)
         const auto lut = lds_ptr<float>(L.lut);
         for (int i = tid; i < 3 * 256; i += nt) lut[i] = A.f.lut[i];
         const auto hsv = lds_ptr<int32_t>(L.hsv);
-        for (int i = tid; i < kHsvWords; i += nt) hsv[i] = A.s.hsv_tables[i];
+        for (int i = tid; i < kHsvDivWords; i += nt) hsv[i] = A.s.hsv_tables[i];
     }
     __syncthreads();
     for (int q = blockIdx.x; q < A.total; q += gridDim.x) {
