@@ -144,7 +144,10 @@ enum KernelMode : int { KM_FINAL = 0, KM_STATS = 1, KM_RAW = 2 };
 constexpr int kBlockMin = 256;
 constexpr int kBlockMax = 512;
 constexpr int kHsvWords = 512 + 256 * 4; // RGB2HSV division tables + HSV2RGB per-H weights (global copy)
-constexpr int kHsvDivWords = 512;         // ... of which LDS holds the division tables
+constexpr int kHsvDivWords = 512;         // ... of which the division tables (sdiv, hdiv180)
+// In LDS: per v {sdiv[v], bits of (float)v * (1.f / 255)} (8 B, one read gives the HSV2RGB v too),
+// then hdiv180[256], then the per-tile hue tables.
+constexpr int kHsvLdsDivBytes = 256 * 8 + 256 * 4;
 // Per tile of a hue record, in LDS: the HSV2RGB weights of the record's shifted H for every
 // OpenCV h before its +180 wrap, h12 in [-30, 150] (tools/hue_range.py): entry h12 + 30 holds
 // weights[((h12 < 0 ? h12 + 180 : h12) + hue) % 180 as uchar], so the pixel loop does one lookup.
@@ -170,7 +173,7 @@ AEON_HD inline LdsLayout lds_layout(int max_win_w, int rows_per_tile, int stage_
     LdsLayout L;
     int       o = 0;
     L.lut = o; o += 3 * 256 * 4;                             // standardize LUT (source channel order)
-    L.hsv = o; o += hue ? kHsvDivWords * 4 + buffers * kHueTabBytes : 0; // sdiv / hdiv180, per-tile hue tables
+    L.hsv = o; o += hue ? kHsvLdsDivBytes + buffers * kHueTabBytes : 0; // sdiv + v/255 / hdiv180, per-tile hue tables
     L.rtab = o; o += rtab ? 3 * 256 * 4 : 0;                 // the tile's record table (f32, source channel order)
     L.xt  = o; o += buffers * ((max_win_w * 8 + 15) / 16) * 16; // per-column taps + weights
     L.yt  = o; o += buffers * rows_per_tile * 16;               // per-row taps + weights

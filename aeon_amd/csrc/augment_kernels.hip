@@ -207,8 +207,8 @@ constexpr int kHueBatch = AEON_HIP_HUE_BATCH; // pixels per hue_apply_n (1, 2 or
 // htab = the tile's hue table at h12 = 0 (kHueTabBytes): OpenCV's h (h12 below, in [-30, 150] for
 // every BGR triple, tools/hue_range.py) -> its +180 wrap, + hue, % 180 stored as uchar, -> the
 // HSV2RGB weights of that H, all folded into the one lookup.
-template <int N, int K0, typename TAB, typename WTAB>
-__device__ __forceinline__ void hue_apply_n(TAB sdiv, TAB hdiv, WTAB htab, int (&pxs)[4][3])
+template <int N, int K0, typename STAB, typename TAB, typename WTAB>
+__device__ __forceinline__ void hue_apply_n(STAB sdv, TAB hdiv, WTAB htab, int (&pxs)[4][3])
 {
     int (*px)[3] = pxs + K0; // pixels K0 .. K0 + N - 1
     int v[N], diff[N], sd[N], hd[N];
@@ -219,7 +219,7 @@ __device__ __forceinline__ void hue_apply_n(TAB sdiv, TAB hdiv, WTAB htab, int (
         diff[k]     = v[k] - min(b, min(g, r));
     }
 #pragma unroll
-    for (int k = 0; k < N; k++) sd[k] = sdiv[v[k]], hd[k] = hdiv[diff[k]];
+    for (int k = 0; k < N; k++) sd[k] = sdv[v[k]].x, hd[k] = hdiv[diff[k]];
     int   h12[N];
     float sf[N];
 #pragma unroll
@@ -246,6 +246,62 @@ __device__ __forceinline__ void hue_apply_n(TAB sdiv, TAB hdiv, WTAB htab, int (
         px[k][1] = u8rnd(vf * (1.f - sf[k] * w[k][1]) * 255.f);
         px[k][2] = u8rnd(vf * (1.f - sf[k] * w[k][2]) * 255.f);
 #endif
+    }
+}
+
+// The division tables in LDS (kHsvLdsDivBytes): {sdiv[v], (float)v * (1.f / 255)} pairs, hdiv180.
+__device__ __forceinline__ void hsv_div_tables(const LdsLayout& L, const int32_t* g)
+{
+    const auto sdv = lds_ptr<i32x2>(L.hsv);
+    const auto hd  = lds_ptr<int32_t>(L.hsv + 256 * 8);
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) {
+        sdv[i] = (i32x2){g[i], (int)__float_as_uint((float)i * (1.f / 255))};
+        hd[i]  = g[256 + i];
+    }
+}
+
+// hue_apply_n for the SPEC_BS_HUE pass-1 loop, the result packed as one dword (B, G, R, 0) per
+// pixel.  In every HSV2RGB_f sector one output channel is t0 = v (w = 0: v/255*255 rounds back to
+// v for all 256 v), one is t1 = v(1-s) (w = 1, s*1 == s) and one is v(1 - s*w) with w in {f, 1-f}:
+// the tile's table entry (htab8 at h12) = {bits of that w, v_perm selector placing (v, t1, t_w)
+// in the channel order}; the two float chains are OpenCV's own operations, so every byte equals
+// hue_apply_n's.
+template <int N, int K0, typename STAB, typename TAB, typename ETAB>
+__device__ __forceinline__ void hue_pack_n(STAB sdv, TAB hdiv, ETAB htab8, const int (&pxs)[4][3], uint32_t (&pk)[4])
+{
+    const int (*px)[3] = pxs + K0;
+    int   v[N], diff[N], hd[N];
+    i32x2 sv[N];
+#pragma unroll
+    for (int k = 0; k < N; k++) {
+        const int b = px[k][0], g = px[k][1], r = px[k][2];
+        v[k]        = max(b, max(g, r));
+        diff[k]     = v[k] - min(b, min(g, r));
+    }
+#pragma unroll
+    for (int k = 0; k < N; k++) sv[k] = sdv[v[k]], hd[k] = hdiv[diff[k]];
+    int   h12[N];
+    float sf[N];
+#pragma unroll
+    for (int k = 0; k < N; k++) {
+        const int b = px[k][0], g = px[k][1], r = px[k][2];
+        const int vr = v[k] == r ? -1 : 0, vg = v[k] == g ? -1 : 0;
+        const int s = mad_i24(diff[k], sv[k].x, 1 << 11) >> 12;
+        int h = (vr & (g - b)) + (~vr & ((vg & (b - r + 2 * diff[k])) + ((~vg) & (r - g + 4 * diff[k]))));
+        h12[k] = mad_i24(h, hd[k], 1 << 11) >> 12;
+        sf[k]  = (float)s * (1.f / 255);
+    }
+    i32x2 e[N];
+#pragma unroll
+    for (int k = 0; k < N; k++) e[k] = htab8[h12[k]];
+#pragma unroll
+    for (int k = 0; k < N; k++) {
+        const float vf = __uint_as_float((uint32_t)sv[k].y);
+        const float c1 = vf * (1.f - sf[k]) * 255.f;
+        const float cw = vf * (1.f - sf[k] * __uint_as_float((uint32_t)e[k].x)) * 255.f;
+        uint32_t    q  = __builtin_amdgcn_cvt_pk_u8_f32(c1, 1u, (uint32_t)v[k]);
+        q              = __builtin_amdgcn_cvt_pk_u8_f32(cw, 2u, q);
+        pk[K0 + k]     = __builtin_amdgcn_perm(0u, q, (uint32_t)e[k].y);
     }
 }
 
@@ -637,12 +693,28 @@ struct Bands {
         }
         if (PHOTO && KM != KM_RAW && a.has_hue && J.cn == 3 && (J.photo & PHOTO_HUE)) {
             // the record's hue table (kHueTabBytes): cvtColor's H of h12, + hue, % 180 as uchar
-            const auto    ht  = lds_ptr<f32x4>(L.hsv + kHsvDivWords * 4 + b * kHueTabBytes);
+            const int     tab = L.hsv + kHsvLdsDivBytes + b * kHueTabBytes;
             const f32x4*  wt  = reinterpret_cast<const f32x4*>(a.hsv_tables + kHsvDivWords);
             const int     hue = J.hue;
+            const bool    sp  = fast_photo(f);
             for (int i = tid; i < kHueTabEntries; i += nt) {
-                const int h12 = i - 30;
-                ht[i]         = wt[(((h12 < 0 ? h12 + 180 : h12) + hue) % 180) & 0xff];
+                const int   h12 = i - 30;
+                const f32x4 w   = wt[(((h12 < 0 ? h12 + 180 : h12) + hue) % 180) & 0xff];
+                if (!sp) {
+                    lds_ptr<f32x4>(tab)[i] = w;
+                    continue;
+                }
+                // hue_pack_n's entry: a channel with w == 0 takes v (byte 0), another with w == 1
+                // takes t1 (byte 1), the third t_w (byte 2) with its w
+                const int iv = w[0] == 0.f ? 0 : (w[1] == 0.f ? 1 : 2);
+                int       i1 = -1;
+                for (int c = 0; c < 3; c++)
+                    if (c != iv && i1 < 0 && w[c] == 1.f) i1 = c;
+                if (i1 < 0) i1 = iv == 0 ? 1 : 0, atomicOr(a.error, 16); // impossible (every sector has t1)
+                const int iw  = 3 - iv - i1;
+                uint32_t  sel = 0x0c000000u;
+                for (int c = 0; c < 3; c++) sel |= (uint32_t)(c == iv ? 0 : (c == i1 ? 1 : 2)) << (8 * c);
+                lds_ptr<i32x2>(tab)[i] = (i32x2){(int)__float_as_uint(w[iw]), (int)sel};
             }
         }
         const auto yt = lds_ptr<i32x4>(L.yt) + b * a.rows_per_tile;
@@ -725,8 +797,8 @@ struct Bands {
         const int  win_w = J.win_w;
         const auto xt    = lds_ptr<const i32x2>(L.xt) + b * a.max_win_w;
         const auto yt    = lds_ptr<const i32x4>(L.yt) + b * a.rows_per_tile;
-        const auto sdiv  = lds_ptr<const int32_t>(L.hsv);
-        const auto hdiv  = sdiv + 256;
+        const auto sdv   = lds_ptr<const i32x2>(L.hsv);
+        const auto hdiv  = lds_ptr<const int32_t>(L.hsv + 256 * 8);
         // (a STATS tile's chain ends at the intermediate: only BS and HUE matter to it)
         const int  photo = SP ? (PHOTO_BS | PHOTO_HUE) : (PHOTO && KM != KM_RAW && cn == 3) ? J.photo : 0;
         double     sh0 = 0, sh1 = 0, sh2 = 0;
@@ -735,7 +807,8 @@ struct Bands {
             sh0 = sh[0], sh1 = sh[1], sh2 = sh[2];
         }
         uint32_t sum0 = 0, sum1 = 0, sum2 = 0;
-        const auto htab = lds_ptr<const f32x4>(L.hsv + kHsvDivWords * 4 + b * kHueTabBytes) + 30; // at h12 = 0
+        const auto htab  = lds_ptr<const f32x4>(L.hsv + kHsvLdsDivBytes + b * kHueTabBytes) + 30; // at h12 = 0
+        const auto htab8 = lds_ptr<const i32x2>(L.hsv + kHsvLdsDivBytes + b * kHueTabBytes) + 30; // SPEC_BS_HUE form
         BsRegs   bsr{};
         int      bs_kind = 0;
         if (PHOTO && (photo & PHOTO_BS)) bs_kind = SP ? (int)BS_FIXPT : J.bs_kind, bsr = bs_regs(J);
@@ -803,6 +876,26 @@ struct Bands {
                             tail_fix<SC>(ytr, col[k], wxk[k], (wx0 + x) * cn, xv, val[k]);
                         }
                 }
+                if constexpr (SP) {
+                    // fixed-point brightness/saturation -> hue, packed (B, G, R, 0) per pixel ->
+                    // exact channel sums (v_dot4 byte picks) -> 12 bytes of HWC uint8
+#pragma unroll
+                    for (int k = 0; k < 4; k++) bs_apply(BS_FIXPT, bsr, val[k][0], val[k][1], val[k][2]);
+                    uint32_t pk[4];
+                    hue_pack_n<2, 0>(sdv, hdiv, htab8, val, pk);
+                    hue_pack_n<2, 2>(sdv, hdiv, htab8, val, pk);
+#pragma unroll
+                    for (int k = 0; k < 4; k++) {
+                        sum0 = __builtin_amdgcn_udot4(pk[k], 0x1u, sum0, false);
+                        sum1 = __builtin_amdgcn_udot4(pk[k], 0x100u, sum1, false);
+                        sum2 = __builtin_amdgcn_udot4(pk[k], 0x10000u, sum2, false);
+                    }
+                    const u32x3 q = {__builtin_amdgcn_perm(pk[1], pk[0], 0x04020100u),
+                                     __builtin_amdgcn_perm(pk[2], pk[1], 0x05040201u),
+                                     __builtin_amdgcn_perm(pk[3], pk[2], 0x06050402u)};
+                    __builtin_amdgcn_raw_buffer_store_b96(q, orsrc, (y * win_w + ox0) * 3, 0, IAUX);
+                    continue;
+                }
                 if (PHOTO && photo) {
 #ifndef AEON_HIP_EXP_NOBS // development ablation: no brightness/saturation (wrong values)
                     if (photo & PHOTO_BS) {
@@ -815,11 +908,11 @@ struct Bands {
 #else
                     if (photo & PHOTO_HUE) {
 #endif // two pixels at a time: four cost 14 VGPRs (a wave per SIMD)
-                        hue_apply_n<kHueBatch, 0>(sdiv, hdiv, htab, val);
-                        if (kHueBatch < 4) hue_apply_n<kHueBatch, kHueBatch % 4>(sdiv, hdiv, htab, val);
+                        hue_apply_n<kHueBatch, 0>(sdv, hdiv, htab, val);
+                        if (kHueBatch < 4) hue_apply_n<kHueBatch, kHueBatch % 4>(sdv, hdiv, htab, val);
                         if (kHueBatch == 1) {
-                            hue_apply_n<1, 2>(sdiv, hdiv, htab, val);
-                            hue_apply_n<1, 3>(sdiv, hdiv, htab, val);
+                            hue_apply_n<1, 2>(sdv, hdiv, htab, val);
+                            hue_apply_n<1, 3>(sdv, hdiv, htab, val);
                         }
                     }
 #pragma unroll
@@ -1009,8 +1102,7 @@ void augment_tiles(LaunchArgs a)
         for (int i = tid; i < 3 * 256; i += nt) lut[i] = a.lut[i];
     }
     if (PHOTO && KM != KM_RAW && a.has_hue) {
-        const auto hsv = lds_ptr<int32_t>(L.hsv);
-        for (int i = tid; i < kHsvDivWords; i += nt) hsv[i] = a.hsv_tables[i];
+        hsv_div_tables(L, a.hsv_tables);
     }
     if (KM == KM_FINAL && PHOTO && a.has_rtab) __syncthreads(); // record tables read the LUT
     // static schedule: tiles blockIdx.x, +G, +2G, ... -- the tiles in flight at any moment are
@@ -1177,8 +1269,7 @@ void augment_contrast_fused(FusedArgs A)
     {
         const auto lut = lds_ptr<float>(L.lut);
         for (int i = tid; i < 3 * 256; i += nt) lut[i] = A.f.lut[i];
-        const auto hsv = lds_ptr<int32_t>(L.hsv);
-        for (int i = tid; i < kHsvDivWords; i += nt) hsv[i] = A.s.hsv_tables[i];
+        hsv_div_tables(L, A.s.hsv_tables);
     }
     __syncthreads();
     for (int q = blockIdx.x; q < A.total; q += gridDim.x) {

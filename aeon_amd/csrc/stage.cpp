@@ -901,7 +901,7 @@ bool run_direct(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void
         HIP_OK(launch_plan_records(s.host_dev, s.dev, pa, stream));
     }
     phase(5);
-    const bool timed = ctx->timing && (ctx->timing_calls++ % ctx->timing_every) == 0;
+    const bool timed = ctx->timing && (ctx->timing_calls++ % ctx->timing_every) == ctx->timing_every - 1;
     if (o.fixed_aspect_ratio) // std::fill_n of each item's canvas, its whole byte size (etl_image.cpp:263)
         HIP_OK(hipMemset2DAsync(out_dev, o.item_stride, 0,
                                 (size_t)o.canvas_w * o.canvas_h * o.channels * out_elem_bytes(od.dtype), n, stream));
@@ -1102,7 +1102,7 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
     };
     const size_t oelem = out_elem_bytes(o.dtype);
     // timing events on one call in timing_every (each event pair costs GPU time between launches)
-    const bool timed = ctx->timing && (ctx->timing_calls++ % ctx->timing_every) == 0;
+    const bool timed = ctx->timing && (ctx->timing_calls++ % ctx->timing_every) == ctx->timing_every - 1;
     if (o.fixed_aspect_ratio) // std::fill_n of each item's canvas, its whole byte size (etl_image.cpp:263)
         HIP_OK(hipMemset2DAsync(out_dev, o.item_stride, 0,
                                 (size_t)o.canvas_w * o.canvas_h * o.channels * out_elem_bytes(od.dtype), n, stream));

@@ -162,9 +162,10 @@ int aeon_hip_decode_jpeg_batch(aeon_hip_ctx* ctx, int n, const void* const* data
 int aeon_hip_synchronize(aeon_hip_ctx* ctx, void* stream);
 
 /* ---- measurement ---------------------------------------------------------------------------- */
-/* every > 0: the kernel launches of one augment/mask call in `every` are bracketed by HIP events
- * on their own stream (an event pair costs GPU time between launches, so benchmarks sample);
- * 0 disables timing. */
+/* every > 0: the kernel launches of one augment/mask call in `every` -- the every-th, 2*every-th,
+ * ... call after this one, so never the first launch after an idle GPU -- are bracketed by HIP
+ * events on their own stream (an event pair costs GPU time between launches, so benchmarks
+ * sample); 0 disables timing. */
 int aeon_hip_set_timing(aeon_hip_ctx* ctx, int every);
 /* Drain the timers: per kernel kind [0]=augment (final), [1]=contrast statistics,
  * [2]=resize_short pre-pass: total ms, total algorithmic bytes, launches. Resets the totals. */
