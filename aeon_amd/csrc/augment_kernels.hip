@@ -882,8 +882,12 @@ struct Bands {
 #pragma unroll
                     for (int k = 0; k < 4; k++) bs_apply(BS_FIXPT, bsr, val[k][0], val[k][1], val[k][2]);
                     uint32_t pk[4];
+#if AEON_HIP_HUE_PACK4
+                    hue_pack_n<4, 0>(sdv, hdiv, htab8, val, pk);
+#else
                     hue_pack_n<2, 0>(sdv, hdiv, htab8, val, pk);
                     hue_pack_n<2, 2>(sdv, hdiv, htab8, val, pk);
+#endif
 #pragma unroll
                     for (int k = 0; k < 4; k++) {
                         sum0 = __builtin_amdgcn_udot4(pk[k], 0x1u, sum0, false);
