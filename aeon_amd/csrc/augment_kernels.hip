@@ -677,7 +677,7 @@ struct Bands {
     {
         if (f.ok) stage_issue(job_ref(a, f.job), f.G, L.stage + b * L.stage_bytes, wave, nw);
     }
-    __device__ __forceinline__ void tables(const Info& f, int b, bool build_xt) const
+    __device__ __forceinline__ void tables(const Info& f, int b, bool build_xt, bool build_rec = true) const
     {
         if (!f.ok) return;
         cjob&      J     = job_ref(a, f.job);
@@ -691,7 +691,7 @@ struct Bands {
                 xt[x]        = (i32x2){c.sx - G.u_lo, (c.a0 & 0xffff) | (c.a1 << 16)};
             }
         }
-        if (PHOTO && KM != KM_RAW && a.has_hue && J.cn == 3 && (J.photo & PHOTO_HUE)) {
+        if (PHOTO && KM != KM_RAW && a.has_hue && build_rec && J.cn == 3 && (J.photo & PHOTO_HUE)) {
             // the record's hue table (kHueTabBytes): cvtColor's H of h12, + hue, % 180 as uchar
             const int     tab = L.hsv + kHsvLdsDivBytes + b * kHueTabBytes;
             const f32x4*  wt  = reinterpret_cast<const f32x4*>(a.hsv_tables + kHsvDivWords);
@@ -1083,7 +1083,10 @@ struct Bands {
 // The contrast pass 1 with photometric stages (VALU-bound) is held to 80 VGPRs: 6 waves per SIMD =
 // three 512-lane workgroups per CU (at 85 VGPRs it gets two).
 template <int KM, int RM, bool PHOTO, int OF, bool TAIL>
-constexpr int kMinWaves = (KM == KM_STATS && PHOTO && !TAIL) ? 6 : AEON_HIP_MIN_WAVES;
+#ifndef AEON_HIP_STATS_MIN_WAVES
+#define AEON_HIP_STATS_MIN_WAVES 6
+#endif
+constexpr int kMinWaves = (KM == KM_STATS && PHOTO && !TAIL) ? AEON_HIP_STATS_MIN_WAVES : AEON_HIP_MIN_WAVES;
 
 template <int KM, int RM, bool PHOTO, int OF, bool TAIL>
 __global__ __launch_bounds__(kBlockMax) __attribute__((amdgpu_waves_per_eu(kMinWaves<KM, RM, PHOTO, OF, TAIL>)))
@@ -1127,7 +1130,13 @@ void augment_tiles(LaunchArgs a)
     if (a.stage_buffers == 1) {
         // one buffer (compute-heavy photometric launches, more rows per tile): stage, wait,
         // compute; the CU's other workgroups cover the latency
-        for (int it = 0; t < T; t += G, it++) {
+        int t_end = T, t_step = G, prev_job = -1;
+        if (a.contig) { // contiguous tile ranges: a record's consecutive bands keep its tables
+            t     = (int)((long)T * blockIdx.x / G);
+            t_end = (int)((long)T * (blockIdx.x + 1) / G);
+            t_step = 1;
+        }
+        for (int it = 0; t < t_end; t += t_step, it++) {
             // the staging phases (job loads, LDS-DMA issue, tap tables, unpack) at a raised wave
             // priority: they are this workgroup's critical path while the CU's other workgroups
             // stream stores (measured 38.8 -> 37.7 us on C2)
@@ -1136,10 +1145,12 @@ void augment_tiles(LaunchArgs a)
             stamp(it, 0);
             const Info f = W.info(t);
             stamp(it, 1);
-            if (wave == 0) prefetch_job(a, t + G, L.pf);
+            if (wave == 0) prefetch_job(a, t + t_step, L.pf);
             W.issue(f, 0);
             stamp(it, 2);
-            W.tables(f, 0, true);
+            const bool same = f.ok && f.job == prev_job; // the LDS tables still hold this record's
+            prev_job        = f.ok ? f.job : -1;
+            W.tables(f, 0, !same, !same);
             W.record_table(f);
             stamp(it, 3);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
