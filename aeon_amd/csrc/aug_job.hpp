@@ -121,6 +121,7 @@ struct LaunchArgs {
     int32_t        split_parts;
     int32_t        u8_map;     // uint8 stores go through the LUT (fixed_aspect_ratio's uint8 standardize)
     int32_t        has_mean;   // double output: standardize with smean / sinv (by SOURCE channel)
+    int32_t        l2_prefetch; // single-buffer launches: touch the next tile's source lines (L2) during compute
     int32_t        contig;     // single-buffer launches: workgroup b takes the contiguous tile range
                                // [T*b/G, T*(b+1)/G) (consecutive bands of a record reuse its tables)
     double         smean[3], sinv[3]; // sinv = 1/stddev, or 0 for stddev 0 (no division)

@@ -388,6 +388,29 @@ __device__ __forceinline__ void stage_issue(cjob& J, const StageGeom& G, int buf
     }
 }
 
+// L2 warm-up of a later tile's source rows: this wave's share of one 4-byte LDS-DMA per 128-byte
+// line of the rows (into the 256-byte sink; nothing reads it), so that tile's staging loads hit L2.
+__device__ __forceinline__ void stage_prefetch(cjob& J, const StageGeom& G, int sink, int wave, int nw)
+{
+    const int   lane = threadIdx.x & 63;
+    const auto  rsrc = uniform_rsrc((const void*)J.src_ptr, (int)J.src_bytes);
+    const int   row  = G.nc * J.cn;
+    const int   lpr  = (row + 127) / 128 + 1; // lines a row segment can touch
+    const int   Q    = G.nr * lpr;
+    const float inv  = 1.f / (float)lpr;
+    for (int i = wave; i * 64 < Q; i += nw) {
+        const int q    = i * 64 + lane;
+        uint32_t  voff = kOutOfRange;
+        if (q < Q) {
+            const int j = (int)(((float)q + 0.5f) * inv), k = q - j * lpr;
+            const int b = src_off(J, G, j, 0);
+            const int a = (max(b, 0) & ~127) + k * 128;
+            if (b >= 0 && a < b + row) voff = (uint32_t)a;
+        }
+        lds_dma<4>(rsrc, sink, voff);
+    }
+}
+
 // (2) After this wave's loads landed: unpack its BGR slots in place; zero border of a padded job;
 // re-read loads that crossed the end of the buffer (rare; uniformly skipped otherwise for gray).
 __device__ __forceinline__ void stage_unpack(cjob& J, const StageGeom& G, int buf, int wave, int nw)
@@ -672,6 +695,10 @@ struct Bands {
     {
         issue(f, b);
         tables(f, b, build_xt);
+    }
+    __device__ __forceinline__ void prefetch_src(const Info& f) const
+    {
+        if (f.ok) stage_prefetch(job_ref(a, f.job), f.G, L.pf, wave, nw);
     }
     __device__ __forceinline__ void issue(const Info& f, int b) const
     {
@@ -1160,6 +1187,7 @@ void augment_tiles(LaunchArgs a)
             __syncthreads();
             stamp(it, 6);
             __builtin_amdgcn_s_setprio(KM == KM_STATS ? kStagePrio : kComputePrio);
+            if (a.l2_prefetch && t + t_step < t_end) W.prefetch_src(W.info(t + t_step));
             W.compute_any(f, 0);
             stamp(it, 7);
             lds_barrier(); // everyone is done reading the buffer before it is refilled
