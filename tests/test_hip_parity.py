@@ -309,6 +309,12 @@ EDGE_CASES = [
     ("u8_chw_c3_odd", (256, 256), dict(crop_x=0, crop_y=0, crop_w=256, crop_h=256, out_w=223, out_h=31,
                                       brightness=0.8, saturation=1.3, contrast=0.7, hue=-12),
      dict(dtype="uint8", mean=None, stddev=None, item_stride=223 * 31 * 3)),
+] + [
+    # contrast pass 1's specialised loop (fixed-point brightness/saturation + hue, packed HSV2RGB
+    # with the per-H channel selector): every hue wrap, sector boundaries included
+    (f"spec_bs_hue_{hue}", (256, 256), dict(crop_x=3, crop_y=1, crop_w=250, crop_h=241, out_w=224, out_h=224,
+                                            flip=hue & 1, brightness=0.75, saturation=1.8, contrast=0.65, hue=hue),
+     {}) for hue in (-397, -180, -179, -91, -30, -1, 1, 29, 30, 90, 150, 179, 180, 401)
 ]
 
 
@@ -671,3 +677,23 @@ def test_c3_fused_launch_matches_oracle(ctx, monkeypatch):
                      "C3 fused")
     finally:
         c.close()
+
+
+def test_spec_bs_hue_primary_colours_and_greys(ctx):
+    """Contrast pass 1's specialised loop on pixels at HSV sector boundaries (pure and mixed
+    primaries: f = 0, two channels with the same weight) and on greys (s = 0, diff = 0)."""
+    w, h = 240, 200
+    img = np.zeros((h, w, 3), np.uint8)
+    levels = np.arange(0, 256, 17, dtype=np.uint8)
+    combos = [(1, 0, 0), (0, 1, 0), (0, 0, 1), (1, 1, 0), (0, 1, 1), (1, 0, 1), (1, 1, 1), (2, 1, 0), (0, 2, 1)]
+    for y in range(h):
+        for x in range(w):
+            c = combos[(x // 8) % len(combos)]
+            v = int(levels[(y // 4) % len(levels)])
+            img[y, x] = [min(255, v * k // 2 + (v if k else 0)) for k in c]
+    params = [A.aug_params(crop_x=0, crop_y=0, crop_w=w, crop_h=h, out_w=224, out_h=224, flip=i & 1,
+                           brightness=b, saturation=s, contrast=0.7, hue=hue)
+              for i, (b, s, hue) in enumerate([(0.9, 1.5, 30), (0.6, 0.5, -60), (1.0, 2.0, 179), (0.8, 1.2, -1)])]
+    imgs = [img] * len(params)
+    out = A.out_desc(**MEAN_OUT)
+    _assert_same(H.hip_records(ctx, imgs, params, out), H.oracle_records(imgs, params, out), "spec primaries")
