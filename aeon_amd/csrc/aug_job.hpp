@@ -122,6 +122,7 @@ struct LaunchArgs {
     int32_t        u8_map;     // uint8 stores go through the LUT (fixed_aspect_ratio's uint8 standardize)
     int32_t        has_mean;   // double output: standardize with smean / sinv (by SOURCE channel)
     int32_t        l2_prefetch; // single-buffer launches: touch the next tile's source lines (L2) during compute
+    int32_t        info_ahead; // single-buffer launches: one wave derives the next tile's geometry during compute
     int32_t        contig;     // single-buffer launches: workgroup b takes the contiguous tile range
                                // [T*b/G, T*(b+1)/G) (consecutive bands of a record reuse its tables)
     double         smean[3], sinv[3]; // sinv = 1/stddev, or 0 for stddev 0 (no division)
@@ -165,7 +166,7 @@ constexpr int kHueTabBytes   = 184 * 16;
 
 // LDS carve of one workgroup (bytes; every region 16-byte aligned, see the CDNA guide G17).
 struct LdsLayout {
-    int lut, hsv, rtab, xt, yt, pf, stage, stage_bytes, total;
+    int lut, hsv, rtab, xt, yt, pf, info, stage, stage_bytes, total;
 };
 // One or two staging buffers and copies of the tap tables (with two, the next tile's are filled
 // while the current tile is computed).  The HSV tables are reserved only for hue launches.  The LUT sits
@@ -181,6 +182,7 @@ AEON_HD inline LdsLayout lds_layout(int max_win_w, int rows_per_tile, int stage_
     L.xt  = o; o += buffers * ((max_win_w * 8 + 15) / 16) * 16; // per-column taps + weights
     L.yt  = o; o += buffers * rows_per_tile * 16;               // per-row taps + weights
     L.pf  = o; o += 256;                                     // LDS-DMA sink of job prefetches
+    L.info = o; o += 64;                                     // the next tile's geometry (one wave computes it)
     L.stage_bytes = stage_bytes;                             // source pixels, 4 B each (B,G,R,x)
     L.stage = o; o += buffers * stage_bytes;
     L.total = o;

@@ -682,10 +682,29 @@ struct Bands {
         // whole DMA instructions: 64 groups (1 KiB) or 64 gray pixels (256 B)
         const int need = J.cn == 3 ? (G.nr * G.ng + 63) / 64 * 1024 : (G.nr * G.pitch + 63) / 64 * 256;
         if (need > L.stage_bytes || J.win_w > a.max_win_w || f.nrows <= 0) {
-            if (threadIdx.x == 0) atomicOr(a.error, 2);
+            if ((threadIdx.x & 63) == 0) atomicOr(a.error, 2); // (lane 0 of whichever wave derives it)
             return f;
         }
         f.ok = true;
+        return f;
+    }
+
+    // The next tile's Info through LDS: derived by one wave (its f64 tap bounds are uniform
+    // work every wave would otherwise repeat) while the tile before it is computed.
+    __device__ __forceinline__ void put_info(const Info& f) const
+    {
+        if ((threadIdx.x & 63) != 0) return;
+        const auto p = lds_ptr<int32_t>(L.info);
+        p[0] = f.ok, p[1] = f.job, p[2] = f.band, p[3] = f.y0, p[4] = f.nrows;
+        p[5] = f.G.v_lo, p[6] = f.G.nr, p[7] = f.G.u_lo, p[8] = f.G.nc, p[9] = f.G.ng, p[10] = f.G.pitch;
+    }
+    __device__ __forceinline__ Info get_info() const
+    {
+        const auto p  = lds_ptr<const int32_t>(L.info);
+        const auto rf = [&](int i) { return __builtin_amdgcn_readfirstlane(p[i]); };
+        Info       f;
+        f.ok = rf(0) != 0, f.job = rf(1), f.band = rf(2), f.y0 = rf(3), f.nrows = rf(4);
+        f.G.v_lo = rf(5), f.G.nr = rf(6), f.G.u_lo = rf(7), f.G.nc = rf(8), f.G.ng = rf(9), f.G.pitch = rf(10);
         return f;
     }
 
@@ -1163,6 +1182,7 @@ void augment_tiles(LaunchArgs a)
             t_end = (int)((long)T * (blockIdx.x + 1) / G);
             t_step = 1;
         }
+        Info f = W.info(t < t_end ? t : 0);
         for (int it = 0; t < t_end; t += t_step, it++) {
             // the staging phases (job loads, LDS-DMA issue, tap tables, unpack) at a raised wave
             // priority: they are this workgroup's critical path while the CU's other workgroups
@@ -1170,7 +1190,7 @@ void augment_tiles(LaunchArgs a)
             // (the VALU-bound contrast pass 1 prefers the reverse: 293 -> 283 us on C3)
             __builtin_amdgcn_s_setprio(KM == KM_STATS ? kComputePrio : kStagePrio);
             stamp(it, 0);
-            const Info f = W.info(t);
+            const bool more = t + t_step < t_end;
             stamp(it, 1);
             if (wave == 0) prefetch_job(a, t + t_step, L.pf);
             W.issue(f, 0);
@@ -1187,11 +1207,13 @@ void augment_tiles(LaunchArgs a)
             __syncthreads();
             stamp(it, 6);
             __builtin_amdgcn_s_setprio(KM == KM_STATS ? kStagePrio : kComputePrio);
-            if (a.l2_prefetch && t + t_step < t_end) W.prefetch_src(W.info(t + t_step));
+            if (a.l2_prefetch && more) W.prefetch_src(W.info(t + t_step));
+            if (a.info_ahead && more && wave == nw - 1) W.put_info(W.info(t + t_step));
             W.compute_any(f, 0);
             stamp(it, 7);
             lds_barrier(); // everyone is done reading the buffer before it is refilled
             stamp(it, 8);
+            if (more) f = a.info_ahead ? W.get_info() : W.info(t + t_step);
         }
         if (a.trace && tid == 0) a.trace[(blockIdx.x * 16 + 1) * 16 + 15] = (uint32_t)__builtin_amdgcn_s_memrealtime();
         return;

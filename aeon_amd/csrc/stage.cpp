@@ -558,6 +558,7 @@ struct aeon_hip_ctx {
     int         n_cu      = 0;
     int         wg_per_cu = 0; // AEON_HIP_WG_PER_CU: experiments only (0 = occupancy API)
     int         l2_prefetch = 0; // AEON_HIP_L2_PREFETCH: warm L2 with the next tile's source rows (experiment)
+    int         info_ahead  = 1; // AEON_HIP_INFO_AHEAD=0: every wave derives each tile's geometry itself
     int         contig    = 0; // AEON_HIP_CONTIG: 1 = contiguous tile ranges for contrast pass 1, 2 = every launch
     std::vector<std::pair<std::vector<int>, int>> occ; // launch shape -> workgroups per CU
     // standardize LUTs stay resident per distinct output config (a new one is uploaded once)
@@ -736,6 +737,7 @@ void timed_launch(aeon_hip_ctx* ctx, int mode, const LaunchPlan& P, const Launch
     const int  grid = grid_for(ctx, mode, P, a, cap);
     a.contig        = a.stage_buffers == 1 && ((ctx->contig == 1 && mode == KM_STATS) || ctx->contig == 2);
     a.l2_prefetch   = ctx->l2_prefetch;
+    a.info_ahead    = ctx->info_ahead;
     // Tail split (final launches): T tiles on a grid of G workgroups leave a last round of
     // T mod G tiles on as many workgroups while the rest of the grid idles; cutting each of those
     // tiles into floor(G / (T mod G)) row sub-tiles spreads the round over the whole grid.  (Not for
@@ -1273,6 +1275,7 @@ int aeon_hip_ctx_create(int device, aeon_hip_ctx** out)
             if (const char* e = std::getenv("AEON_HIP_WG_PER_CU")) c->wg_per_cu = std::atoi(e);
             if (const char* e = std::getenv("AEON_HIP_CONTIG")) c->contig = std::atoi(e);
             if (const char* e = std::getenv("AEON_HIP_L2_PREFETCH")) c->l2_prefetch = std::atoi(e);
+            if (const char* e = std::getenv("AEON_HIP_INFO_AHEAD")) c->info_ahead = std::atoi(e);
             if (const char* e = std::getenv("AEON_HIP_DONE_EVERY"))
                 c->done_every = std::min(aeon_hip_ctx::kSlots / 2, std::max(1, std::atoi(e)));
         } catch (...) {
