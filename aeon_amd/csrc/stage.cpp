@@ -535,6 +535,7 @@ struct aeon_hip_ctx {
     hipStream_t          side_stream    = nullptr;
     hipEvent_t           join_event     = nullptr;
     int                  overlap_chunks = 1, cap_pass1 = 2, cap_pass2 = 1; // off: measured slower
+    int                  caps_always = 0; // AEON_HIP_CAPS: apply cap_pass1/2 to every contrast call
     bool                 tail_split     = false; // AEON_HIP_TAIL_SPLIT=1: measured slower
     // contrast records' two passes in one launch (augment_contrast_fused, AEON_HIP_FUSED=1): measured
     // slower than the pass-1 / reduce / pass-2 launches, so off.  fused_lag = records
@@ -1267,6 +1268,7 @@ int aeon_hip_ctx_create(int device, aeon_hip_ctx** out)
             if (const char* e = std::getenv("AEON_HIP_FUSED")) c->fused = std::atoi(e);
             if (const char* e = std::getenv("AEON_HIP_FUSED_LAG")) c->fused_lag = std::max(1, std::atoi(e));
             if (const char* e = std::getenv("AEON_HIP_CAP_PASS1")) c->cap_pass1 = std::max(0, std::atoi(e));
+            if (const char* e = std::getenv("AEON_HIP_CAPS")) c->caps_always = std::atoi(e) != 0;
             if (const char* e = std::getenv("AEON_HIP_CAP_PASS2")) c->cap_pass2 = std::max(0, std::atoi(e));
             if (const char* e = std::getenv("AEON_HIP_HOST_PROFILE")) c->host_profile = std::atoi(e) != 0;
             if (const char* e = std::getenv("AEON_HIP_JOBS")) c->jobs_mode = std::min(3, std::max(0, std::atoi(e)));
@@ -1365,8 +1367,13 @@ int aeon_hip_augment_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs,
         int with_contrast = 0;
         for (int i = 0; ctx && params && i < n; i++) with_contrast += params[i].contrast != 1.0f;
         const int chunks = ctx ? std::min(ctx->overlap_chunks, n / 64) : 1;
-        if (chunks < 2 || with_contrast * 2 < n || !out || !descs || !out_dev)
-            return run_batch(ctx, n, descs, src_base, params, out, out_dev, stream, false);
+        if (chunks < 2 || with_contrast * 2 < n || !out || !descs || !out_dev) {
+            // AEON_HIP_CAPS (experiment): the pass grids capped per CU even without chunking, so
+            // consecutive calls on two caller streams can share the CUs
+            const bool caps = ctx && ctx->caps_always && with_contrast * 2 >= n;
+            return run_batch(ctx, n, descs, src_base, params, out, out_dev, stream, false, nullptr,
+                             caps ? ctx->cap_pass1 : 0, caps ? ctx->cap_pass2 : 0);
+        }
         const int per = (n + chunks - 1) / chunks;
         for (int a = 0; a < n; a += per)
             run_batch(ctx, std::min(per, n - a), descs + a, src_base, params + a, out,
