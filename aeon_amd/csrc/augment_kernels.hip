@@ -1132,7 +1132,14 @@ template <int KM, int RM, bool PHOTO, int OF, bool TAIL>
 #ifndef AEON_HIP_STATS_MIN_WAVES
 #define AEON_HIP_STATS_MIN_WAVES 6
 #endif
-constexpr int kMinWaves = (KM == KM_STATS && PHOTO && !TAIL) ? AEON_HIP_STATS_MIN_WAVES : AEON_HIP_MIN_WAVES;
+// Contrast pass 2 (the photometric copy pass, 512-lane workgroups) likewise: at 82 VGPRs it held
+// two workgroups per CU, at 80 three (C3 pass 2 131-132 -> 127 us).
+#ifndef AEON_HIP_PASS2_MIN_WAVES
+#define AEON_HIP_PASS2_MIN_WAVES 6
+#endif
+constexpr int kMinWaves = (KM == KM_STATS && PHOTO && !TAIL) ? AEON_HIP_STATS_MIN_WAVES
+                          : (KM == KM_FINAL && RM == RESIZE_COPY && PHOTO) ? AEON_HIP_PASS2_MIN_WAVES
+                                                                          : AEON_HIP_MIN_WAVES;
 
 template <int KM, int RM, bool PHOTO, int OF, bool TAIL>
 __global__ __launch_bounds__(kBlockMax) __attribute__((amdgpu_waves_per_eu(kMinWaves<KM, RM, PHOTO, OF, TAIL>)))
