@@ -305,6 +305,25 @@ __device__ __forceinline__ void hue_pack_n(STAB sdv, TAB hdiv, ETAB htab8, const
     }
 }
 
+// Sum over the 64 lanes of a full wave with DPP adds (no LDS permutes), uniform result: quad
+// permutes and row mirrors give every lane its row's sum, row_bcast:15 / :31 carry rows 0..2
+// into rows 1..3, lane 63 holds the total.  Integer adds: exact in any order.
+template <int CTRL, int ROWS = 0xf>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t v)
+{
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROWS, 0xf, false);
+}
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v)
+{
+    v += dpp_u32<0xb1>(v);       // quad_perm [1, 0, 3, 2]
+    v += dpp_u32<0x4e>(v);       // quad_perm [2, 3, 0, 1]
+    v += dpp_u32<0x141>(v);      // row_half_mirror
+    v += dpp_u32<0x140>(v);      // row_mirror
+    v += dpp_u32<0x142, 0xa>(v); // row_bcast:15 -> rows 1, 3
+    v += dpp_u32<0x143, 0xc>(v); // row_bcast:31 -> rows 2, 3
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+
 // ---- source staging (LDS-DMA) ------------------------------------------------------------------
 // A tile (a band of TR output rows of one record) needs source rows [v_lo, v_lo+nr) x cols
 // [u_lo, u_lo+nc), staged as one 32-bit word per pixel (B, G, R, x), rows `pitch` = 4*ng words
@@ -1103,11 +1122,7 @@ struct Bands {
         }
 
         if (KM == KM_STATS) { // exact per-(tile, wave) sums; unused wave slots are zeroed
-            for (int o = 32; o > 0; o >>= 1) {
-                sum0 += __shfl_xor(sum0, o);
-                sum1 += __shfl_xor(sum1, o);
-                sum2 += __shfl_xor(sum2, o);
-            }
+            sum0 = wave_sum(sum0), sum1 = wave_sum(sum1), sum2 = wave_sum(sum2);
             const int lane = tid & 63;
             uint32_t* p    = a.partials + ((size_t)J.stats_slot * a.partial_stride + (size_t)band * 8) * 4;
             auto put = [&](uint32_t* q, uint32_t v) {
