@@ -339,8 +339,11 @@ def cpu_baseline(A, C, budget_s, cfg="C2"):
         what = f"C5 image+mask pairs, {w}x{h} -> 512x512"
     else:
         aug = {"C1": C.C1_AUG, "C2": C.C2_AUG, "C3": C.C3_AUG}[cfg]
-        # C1 = aeon's own eval config on decoded images of its golden record's size (480x360)
-        n, w, h = {"C1": (32, 480, 360), "C2": (256, 256, 256), "C3": (256, 256, 256)}[cfg]
+        # C1 = aeon's own eval config on decoded images of its golden record's size (480x360), in
+        # aeon's decode_size windows (batch 32 -> the smallest multiple giving each thread 8 records,
+        # src/loader.cpp:162-164); C2 / C3 in 256-record windows
+        n, w, h = {"C1": (32 * ((threads * 8 - 1) // 32 + 1), 480, 360), "C2": (256, 256, 256),
+                   "C3": (256, 256, 256)}[cfg]
         imgs = [A.synthetic_image(i, w, h, 3) for i in range(n)]
         params = H.draw_params(aug, [(w, h)] * n, 224, 224, seed=1)
         lc = H.oracle_load_config(C.out_desc_for(C.IMAGE_224, aug))
@@ -445,11 +448,15 @@ def cpu_baseline_jpeg(A, C, budget_s):
 
 def run_c1_decoder(A, C, torch, budget_s=2.0):
     """C1 through the product's decode stage (aeon_decoder: provider_factory + batch_decoder,
-    host records in, host batch out): 32-record windows of 480x360 decoded records, two windows in
-    flight (submit / wait) into pinned host batches."""
+    host records in, host batch out): decode windows of 480x360 decoded records, two windows in
+    flight (submit / wait) into pinned host batches.  The window is aeon's decode_size, the smallest
+    multiple of batch_size giving every pool thread 8 records (src/loader.cpp:162-164,
+    m_input_multiplier src/loader.hpp:237): 128 records for batch 32 on 14 threads."""
     cfg = dict(C.CONFIGS["C1"], random_seed=1)
     d = A.Decoder(cfg)
-    n = cfg["batch_size"]
+    batch = cfg["batch_size"]
+    threads = pool_threads()[0]
+    n = batch * ((threads * 8 - 1) // batch + 1)
     recs = [(A.synthetic_image(i, 480, 360, 3),) for i in range(n)]
     bufs = [torch.empty(n * 3 * 224 * 224 * 4, dtype=torch.uint8).pin_memory() for _ in range(2)]
     for w in range(2):  # warmup (context, kernels, buffers)
@@ -467,9 +474,10 @@ def run_c1_decoder(A, C, torch, budget_s=2.0):
     d.wait()
     dt = time.perf_counter() - t0
     d.close()
-    return {"value": done / dt, "unit": "images/s", "batch": n,
+    return {"value": done / dt, "unit": "images/s", "batch": batch, "decode_size": n,
             "what": "aeon_decoder submit/wait: host decoded 480x360 records -> pinned H2D -> resize_short 256 + "
-                    "center crop 224 -> fp32 CHW -> D2H into pinned batches, two 32-record windows in flight"}
+                    f"center crop 224 -> fp32 CHW -> D2H into pinned batches, two {n}-record windows (aeon's "
+                    "decode_size) in flight"}
 
 
 def load_traffic(path, cfg):
