@@ -297,8 +297,18 @@ __device__ __forceinline__ void hue_pack_n(STAB sdv, TAB hdiv, ETAB htab8, const
 #pragma unroll
     for (int k = 0; k < N; k++) {
         const float vf = __uint_as_float((uint32_t)sv[k].y);
+#ifndef AEON_HIP_HUE_PK_F32
+#define AEON_HIP_HUE_PK_F32 1
+#endif
+#if AEON_HIP_HUE_PK_F32 // both chains as packed f32 (s*1 == s exactly; separate IEEE mul/add, no FMA)
+        typedef float f32x2 __attribute__((ext_vector_type(2)));
+        f32x2       t  = (f32x2){sf[k], sf[k]} * (f32x2){1.f, __uint_as_float((uint32_t)e[k].x)};
+        t              = ((1.f - t) * vf) * 255.f;
+        const float c1 = t.x, cw = t.y;
+#else
         const float c1 = vf * (1.f - sf[k]) * 255.f;
         const float cw = vf * (1.f - sf[k] * __uint_as_float((uint32_t)e[k].x)) * 255.f;
+#endif
         uint32_t    q  = __builtin_amdgcn_cvt_pk_u8_f32(c1, 1u, (uint32_t)v[k]);
         q              = __builtin_amdgcn_cvt_pk_u8_f32(cw, 2u, q);
         pk[K0 + k]     = __builtin_amdgcn_perm(0u, q, (uint32_t)e[k].y);
