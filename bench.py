@@ -577,8 +577,8 @@ def main():
         if args.config == "C2":
             # rate untimed (an event pair between a step's launches costs ~10 us of GPU time there),
             # the kernel durations from a second run timing every launch
-            st3 = max(10, args.steps // 2)
-            e3, _, _, _ = run_device(A, C, torch, "C3", 1024, st3, 2, 0, 1, args.pool_mib, None, 0)
+            st3 = max(30, args.steps)
+            e3, _, _, _ = run_device(A, C, torch, "C3", 1024, st3, 3, 0, 1, args.pool_mib, None, 0)
             _, kt3, _, _ = run_device(A, C, torch, "C3", 1024, 6, 2, 0, 1, args.pool_mib, None, 1)
             m3, b3, n3 = kt3["augment"]
             s3 = kt3["stats"]
@@ -596,7 +596,7 @@ def main():
             extra["two_streams"] = {"value": batch * args.steps / e2, "unit": "images/s",
                                     "ms_per_step": e2 / args.steps * 1e3,
                                     "what": "same workload, consecutive batches on two streams"}
-        extra["C5"] = run_c5(A, C, torch, max(5, args.steps // 5), 2, args.pool_mib)
+        extra["C5"] = run_c5(A, C, torch, max(20, args.steps), 3, args.pool_mib)
         extra["e2e_host_to_host"] = {"value": run_e2e(A, C, torch, 256, 20), "unit": "images/s",
                                      "what": "pinned H2D of decoded 256x256 u8 + kernel + D2H of fp32 CHW"}
         extra["e2e_zero_copy"] = {"value": run_e2e(A, C, torch, 256, 20, zero_copy=True), "unit": "images/s",
