@@ -21,4 +21,16 @@ struct alignas(16) Mask16Job {
                                       // (the record's image::rotate pre-pass output)
 };
 
+// LDS-staged gather (nearest_staged) geometry, shared by the host and the launch: bytes per
+// staged source row (a 16-byte-aligned window around the crop segment) and output rows per
+// workgroup (up to 64 rows / ~32K output elements per workgroup, LDS <= 64 KB).
+inline int mask16_pitch(int max_seg_bytes) { return (max_seg_bytes + 15 + 15) & ~15; }
+inline int mask16_rows(int max_w, int max_seg_bytes)
+{
+    const int pitch = mask16_pitch(max_seg_bytes);
+    int       r     = 64 < 65536 / pitch ? 64 : 65536 / pitch;
+    const int by_w  = 32768 / (max_w > 1 ? max_w : 1);
+    return r < (by_w > 1 ? by_w : 1) ? r : (by_w > 1 ? by_w : 1);
+}
+
 } // namespace aeon_hip

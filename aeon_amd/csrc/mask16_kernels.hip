@@ -120,15 +120,19 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 constexpr int kLoadsPerLane = 8; // 16-byte loads a lane keeps in flight before their LDS writes
 
 // The source rows of one block of output rows, as wave 0 numbered them.
+// Kept small (336 B of static LDS): with the staged rows sized to the distinct rows a block can
+// touch, C5's 512-row masks fit four workgroups per CU, i.e. their 1,024 blocks in one round.
 struct RowMap {
-    uint64_t addr[64]; // 16-byte-aligned start of each distinct row's segment
-    int      shift[64]; // segment start - addr
-    int      slot[64];  // output row -> distinct row
+    uint32_t off[64];  // byte offset from src_ptr of each distinct row's crop segment
+    uint8_t  slot[64]; // output row -> distinct row
     int      nslots, nrows, rec, y0;
 };
+__device__ __forceinline__ uint64_t seg_start(const Mask16Job& J, const RowMap& M, int s) { return J.src_ptr + M.off[s]; }
 
 // wave 0: rows [y0, y0 + nrows) of record `rec`
-__device__ __forceinline__ void map_rows(const Mask16Job& J, int rec, int y0, int nrows, RowMap& M)
+// (max_slots: the staged rows the launch's LDS holds -- the host's exact bound on the distinct
+// rows of any block, so the clamp never applies)
+__device__ __forceinline__ void map_rows(const Mask16Job& J, int rec, int y0, int nrows, int max_slots, RowMap& M)
 {
     const int  tid   = threadIdx.x;
     const int  eb    = J.src_elem;
@@ -139,13 +143,9 @@ __device__ __forceinline__ void map_rows(const Mask16Job& J, int rec, int y0, in
     const unsigned long long m    = __ballot(fresh);
     const unsigned long long upto = tid == 63 ? ~0ull : ((2ull << tid) - 1);
     const int                slot = __popcll(m & upto) - 1;
-    if (valid) M.slot[tid] = slot;
-    if (fresh) {
-        const uint64_t a = J.src_ptr + (uint64_t)(J.crop_y + sy) * J.src_stride + (uint64_t)J.crop_x * eb;
-        M.addr[slot]     = a & ~(uint64_t)15;
-        M.shift[slot]    = (int)(a & 15);
-    }
-    if (tid == 0) M.nslots = __popcll(m), M.nrows = nrows, M.rec = rec, M.y0 = y0;
+    if (valid) M.slot[tid] = (uint8_t)slot;
+    if (fresh) M.off[slot] = (uint32_t)((uint64_t)(J.crop_y + sy) * J.src_stride + (uint64_t)J.crop_x * eb);
+    if (tid == 0) M.nslots = min(__popcll(m), max_slots), M.nrows = nrows, M.rec = rec, M.y0 = y0;
 }
 
 __device__ __forceinline__ int seg_blocks(const Mask16Job& J) { return (15 + J.crop_w * J.src_elem + 15) >> 4; }
@@ -155,7 +155,7 @@ __device__ __forceinline__ int seg_blocks(const Mask16Job& J) { return (15 + J.c
 // while i / nblk < 2^12 as (i + 0.5) / nblk stays > 0.5 / nblk from an integer).  Each thread
 // issues kLoadsPerLane loads before their LDS writes; the loads are unconditional (clamped to the
 // last block) because a branch around each would make the compiler wait for it at the join.
-__device__ __forceinline__ void copy_rows(const RowMap& M, int nblk, int pitch, uint8_t* lds)
+__device__ __forceinline__ void copy_rows(const Mask16Job& J, const RowMap& M, int nblk, int pitch, uint8_t* lds)
 {
     const int   total = M.nslots * nblk;
     const float rcp   = 1.0f / (float)nblk;
@@ -167,7 +167,7 @@ __device__ __forceinline__ void copy_rows(const RowMap& M, int nblk, int pitch, 
         for (int u = 0; u < kLoadsPerLane; u++) {
             const int i = min(i0 + u * (int)blockDim.x, total - 1);
             const int s = (int)(((float)i + 0.5f) * rcp), b = i - s * nblk;
-            v[u]        = __builtin_nontemporal_load(gptr<const u32x4>(M.addr[s] + (uint64_t)b * 16));
+            v[u]        = __builtin_nontemporal_load(gptr<const u32x4>((seg_start(J, M, s) & ~(uint64_t)15) + (uint64_t)b * 16));
             at[u]       = s * pitch + b * 16;
         }
 #pragma unroll
@@ -199,7 +199,7 @@ __device__ __forceinline__ bool gather_u8_perm(const Mask16Job& J, const RowMap&
     const uint32_t* lds32 = (const uint32_t*)lds;
     for (int r = r0; r < M.nrows; r += rstep) {
         const int s    = M.slot[r];
-        const int rowb = s * pitch + M.shift[s];
+        const int rowb = s * pitch + (int)(seg_start(J, M, s) & 15);
         u32x4     q;
 #pragma unroll
         for (int w = 0; w < 4; w++) {
@@ -241,7 +241,7 @@ __device__ __forceinline__ void gather_rows(const Mask16Job& J, const RowMap& M,
             continue;
         for (int r = r0; r < nrows; r += rstep) {
             const int      s    = M.slot[r];
-            const uint8_t* base = lds + s * pitch + M.shift[s];
+            const uint8_t* base = lds + s * pitch + (int)(seg_start(J, M, s) & 15);
             uint32_t       v[C];
 #pragma unroll
             for (int k = 0; k < C; k++) v[k] = *(const T*)(base + off[k]);
@@ -274,16 +274,16 @@ __device__ __forceinline__ void gather_any(const Mask16Job& J, const RowMap& M, 
 
 // one block of rows per workgroup: grid (row blocks, records)
 __global__ __launch_bounds__(256) void nearest_staged(const Mask16Job* __restrict__ jobs, int rows_per_block, int pitch,
-                                                      int perm_ok)
+                                                      int perm_ok, int max_slots)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds_rows[];
     __shared__ RowMap M;
     const Mask16Job& J  = jobs[blockIdx.y];
     const int        y0 = blockIdx.x * rows_per_block;
     if (y0 >= J.out_h) return;
-    if (threadIdx.x < 64) map_rows(J, blockIdx.y, y0, min(rows_per_block, J.out_h - y0), M);
+    if (threadIdx.x < 64) map_rows(J, blockIdx.y, y0, min(rows_per_block, J.out_h - y0), max_slots, M);
     __syncthreads();
-    copy_rows(M, seg_blocks(J), pitch, lds_rows);
+    copy_rows(J, M, seg_blocks(J), pitch, lds_rows);
     __syncthreads();
     gather_any(J, M, pitch, lds_rows, perm_ok != 0);
 }
@@ -298,28 +298,32 @@ __global__ __launch_bounds__(256) void nearest_records(const Mask16Job* __restri
     else nearest_rows<uint8_t>(J, y0, y1);
 }
 
-hipError_t launch_nearest(const Mask16Job* jobs, int n_jobs, int max_h, int max_w, int max_seg_bytes,
+hipError_t launch_nearest(const Mask16Job* jobs, int n_jobs, int max_h, int max_w, int max_seg_bytes, int max_slots,
                           hipStream_t stream, hipEvent_t start, hipEvent_t stop)
 {
     if (n_jobs <= 0) return hipSuccess;
-    const int   pitch = (max_seg_bytes + 15 + 15) & ~15;
+    const int   pitch = mask16_pitch(max_seg_bytes);
     const char* env   = std::getenv("AEON_HIP_MASK_GATHER"); // experiments: "direct" = the old gather
     const std::string mode = env ? env : "staged";
     // staged: up to 64 output rows / ~32K output elements per workgroup, LDS <= 64 KB (C5 A/B:
-    // 64 rows 15.8 us, 32 rows 16.7, 16 rows 20.5, 8 rows 29.9; the direct gather 26.3)
-    int srows = std::min({64, 65536 / pitch, std::max(1, 32768 / std::max(1, max_w))});
+    // 64 rows 15.8 us, 32 rows 16.7, 16 rows 20.5, 8 rows 29.9; the direct gather 26.3); the LDS
+    // holds max_slots staged rows (the host's bound on the distinct source rows of one block)
+    int srows = mask16_rows(max_w, max_seg_bytes);
     if (srows >= 1 && mode != "direct") {
-        if (const char* e = std::getenv("AEON_HIP_NEAREST_ROWS")) srows = std::max(1, std::min(std::atoi(e), 64));
-        srows           = std::min(srows, std::max(1, 65536 / pitch));
+        if (const char* e = std::getenv("AEON_HIP_NEAREST_ROWS")) { // experiments: LDS for every row
+            srows = std::max(1, std::min(std::min(std::atoi(e), 64), 65536 / pitch));
+            max_slots = srows;
+        }
+        max_slots       = std::max(1, std::min(max_slots, srows));
         const dim3 grid((max_h + srows - 1) / srows, n_jobs);
-        const size_t lds = (size_t)srows * pitch;
+        const size_t lds = (size_t)max_slots * pitch;
         int perm = 1;
         if (const char* e = std::getenv("AEON_HIP_MASK_PERM")) perm = std::atoi(e);
         if (start || stop) {
-            void* args[4] = {(void*)&jobs, (void*)&srows, (void*)&pitch, (void*)&perm};
+            void* args[5] = {(void*)&jobs, (void*)&srows, (void*)&pitch, (void*)&perm, (void*)&max_slots};
             return hipExtLaunchKernel((const void*)nearest_staged, grid, dim3(256), args, lds, stream, start, stop, 0);
         }
-        hipLaunchKernelGGL(nearest_staged, grid, dim3(256), lds, stream, jobs, srows, pitch, perm);
+        hipLaunchKernelGGL(nearest_staged, grid, dim3(256), lds, stream, jobs, srows, pitch, perm, max_slots);
         return hipGetLastError();
     }
     // lanes = the widest record's 4-column groups (64..256); ~8K output pixels per workgroup

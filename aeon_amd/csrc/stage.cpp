@@ -37,7 +37,7 @@ hipError_t launch_transpose(const void* src, void* dst, int64_t rows, int64_t co
 hipError_t launch_rotate(const RotJob* jobs, int n_jobs, int max_tiles, int words, int cn, hipStream_t stream);
 int        rot_box_words(int angle);
 hipError_t launch_expand(const ExpandJob* jobs, int n_jobs, int max_pixels, hipStream_t stream);
-hipError_t launch_nearest(const Mask16Job* jobs, int n_jobs, int max_h, int max_w, int max_seg_bytes, hipStream_t stream,
+hipError_t launch_nearest(const Mask16Job* jobs, int n_jobs, int max_h, int max_w, int max_seg_bytes, int max_slots, hipStream_t stream,
                           hipEvent_t start, hipEvent_t stop);
 hipError_t launch_upload_table(const void* host_dev, void* dst, size_t bytes, hipStream_t stream);
 hipError_t launch_plan_records(const void* host_records, void* jobs, const PlanArgs& a, hipStream_t stream);
@@ -1015,6 +1015,18 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
         m16_max_seg = std::max(m16_max_seg, M.crop_w * M.src_elem);
         m16_bytes += (double)M.crop_w * M.crop_h * M.src_elem + (double)M.out_w * M.out_h * out_elem_bytes(M.dtype);
     }
+    // distinct source rows of any block of the gather pass: the kernel's own row map
+    // (sy = min(floor(y * ify), crop_h - 1), monotonic in y), evaluated at each block's ends
+    int m16_max_slots = 1;
+    if (!m16.empty()) {
+        const int srows = mask16_rows(m16_max_w, m16_max_seg);
+        for (const Mask16Job& M : m16)
+            for (int y0 = 0; y0 < M.out_h; y0 += srows) {
+                const auto sy = [&](int y) { return std::min((int)std::floor(y * M.scale_y), M.crop_h - 1); };
+                const int  y1 = std::min(y0 + srows, M.out_h) - 1;
+                m16_max_slots = std::max(m16_max_slots, std::min(y1 - y0 + 1, sy(y1) - sy(y0) + 1));
+            }
+    }
     int              rot_max_tiles = 0, rot_words = 0, rot_cn = rot.empty() ? 0 : rot[0].cn; // (rotate_tiles)
     for (size_t r = 0; r < rot.size(); r++) {
         const RotJob& R = rot[r];
@@ -1120,7 +1132,8 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
     if (!m16.empty()) {
         KernelTimer t{};
         if (timed) t = take_timer(ctx, KM_FINAL, m16_bytes);
-        HIP_OK(launch_nearest((const Mask16Job*)(table + m16_off), (int)m16.size(), m16_max_h, m16_max_w, m16_max_seg, stream,
+        HIP_OK(launch_nearest((const Mask16Job*)(table + m16_off), (int)m16.size(), m16_max_h, m16_max_w, m16_max_seg,
+                              m16_max_slots, stream,
                               timed ? t.start : nullptr, timed ? t.stop : nullptr));
         if (timed) ctx->timers.push_back(t);
     }
