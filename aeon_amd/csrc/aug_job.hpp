@@ -123,6 +123,9 @@ struct LaunchArgs {
     int32_t        has_mean;   // double output: standardize with smean / sinv (by SOURCE channel)
     int32_t        l2_prefetch; // single-buffer launches: touch the next tile's source lines (L2) during compute
     int32_t        info_ahead; // single-buffer launches: one wave derives the next tile's geometry during compute
+    uint32_t*      tail_ctr;   // non-null: the partial last round of tiles is handed out by this counter
+                               // (zero on entry; the launch's last draw resets it)
+    int32_t        tail_rounds; // ... and this many full rounds before it
     int32_t        contig;     // single-buffer launches: workgroup b takes the contiguous tile range
                                // [T*b/G, T*(b+1)/G) (consecutive bands of a record reuse its tables)
     double         smean[3], sinv[3]; // sinv = 1/stddev, or 0 for stddev 0 (no division)

@@ -1214,15 +1214,38 @@ void augment_tiles(LaunchArgs a)
             t_end = (int)((long)T * (blockIdx.x + 1) / G);
             t_step = 1;
         }
+        // dynamic tail: the tiles of the partial last round go to whichever workgroups finish their
+        // static rounds first (one counter draw per tile, one failing draw per workgroup)
+        const int  t_tail = (a.tail_ctr && !a.contig) ? min(T % G + a.tail_rounds * G, T - T % G == 0 ? T : T - G) : 0;
+        const int  t_dyn  = T - t_tail; // first dynamically handed-out tile
+        if (t_tail) t_end = t_dyn;
         Info f = W.info(t < t_end ? t : 0);
-        for (int it = 0; t < t_end; t += t_step, it++) {
+        int  it = 0;
+        auto draw = [&]() -> int { // the next dynamic tile, or -1
+            const auto slot = lds_ptr<uint32_t>(L.info + 60);
+            if (tid == 0) {
+                const uint32_t k = atomicAdd(a.tail_ctr, 1u);
+                if (k == (uint32_t)(t_tail + G - 1)) atomicExch(a.tail_ctr, 0u); // the last draw of the launch
+                *slot = k;
+            }
+            __syncthreads();
+            const int k = (int)__builtin_amdgcn_readfirstlane(*slot);
+            return k < t_tail ? t_dyn + k : -1;
+        };
+        bool live = t < t_end;
+        if (t_tail && !live) { // no static tile: start with a drawn one
+            t    = draw();
+            live = t >= 0;
+            if (live) f = W.info(t);
+        }
+        for (; live; it++) {
             // the staging phases (job loads, LDS-DMA issue, tap tables, unpack) at a raised wave
             // priority: they are this workgroup's critical path while the CU's other workgroups
             // stream stores (measured 38.8 -> 37.7 us on C2)
             // (the VALU-bound contrast pass 1 prefers the reverse: 293 -> 283 us on C3)
             __builtin_amdgcn_s_setprio(KM == KM_STATS ? kComputePrio : kStagePrio);
             stamp(it, 0);
-            const bool more = t + t_step < t_end;
+            const bool more = t < t_end && t + t_step < t_end; // a static next tile
             stamp(it, 1);
             if (wave == 0) prefetch_job(a, t + t_step, L.pf);
             W.issue(f, 0);
@@ -1245,7 +1268,16 @@ void augment_tiles(LaunchArgs a)
             stamp(it, 7);
             lds_barrier(); // everyone is done reading the buffer before it is refilled
             stamp(it, 8);
-            if (more) f = a.info_ahead ? W.get_info() : W.info(t + t_step);
+            if (more) {
+                f = a.info_ahead ? W.get_info() : W.info(t + t_step);
+                t += t_step;
+            } else if (t_tail) {
+                t    = draw();
+                live = t >= 0;
+                if (live) f = W.info(t);
+            } else {
+                break;
+            }
         }
         if (a.trace && tid == 0) a.trace[(blockIdx.x * 16 + 1) * 16 + 15] = (uint32_t)__builtin_amdgcn_s_memrealtime();
         return;

@@ -515,6 +515,7 @@ struct KernelTimer {
 struct aeon_hip_ctx {
     int        device = 0;
     int32_t*   d_error = nullptr;
+    uint32_t*  d_tail  = nullptr; // per ring slot: dynamic-tail tile counters (zero between launches)
     int32_t*   d_hsv   = nullptr;
     // staging ring: a slot (job table, scratch) is reused only after the kernels that read it
     // finished.  A completion event is recorded once per `done_every` calls on a stream and
@@ -560,6 +561,7 @@ struct aeon_hip_ctx {
     int         wg_per_cu = 0; // AEON_HIP_WG_PER_CU: experiments only (0 = occupancy API)
     int         l2_prefetch = 0; // AEON_HIP_L2_PREFETCH: warm L2 with the next tile's source rows (experiment)
     int         info_ahead  = 1; // AEON_HIP_INFO_AHEAD=0: every wave derives each tile's geometry itself
+    int         dyn_tail    = 3; // AEON_HIP_DYN_TAIL: 0 = static schedule; n = the last partial + (n-1) full rounds of tiles handed out by a counter
     int         contig    = 0; // AEON_HIP_CONTIG: 1 = contiguous tile ranges for contrast pass 1, 2 = every launch
     std::vector<std::pair<std::vector<int>, int>> occ; // launch shape -> workgroups per CU
     // standardize LUTs stay resident per distinct output config (a new one is uploaded once)
@@ -806,6 +808,10 @@ LaunchArgs launch_args(aeon_hip_ctx* ctx, const Slot& s, const uint8_t* table, c
                        const aeon_out_desc& o, const float* d_lut, int partial_stride, bool u8_map = false)
 {
     LaunchArgs a{};
+    if (ctx->dyn_tail > 0) { // the slot's own counter: launches of calls in flight never share one
+        a.tail_ctr    = ctx->d_tail + (&s - ctx->slots);
+        a.tail_rounds = ctx->dyn_tail - 1;
+    }
     a.jobs           = (const AugJob*)(table + L.blob_off);
     a.lut            = d_lut; // [3][256]: standardized, or (float)x without mean
     a.hsv_tables     = ctx->d_hsv;
@@ -1241,6 +1247,9 @@ int aeon_hip_ctx_create(int device, aeon_hip_ctx** out)
             HIP_OK(set_kernel_lds_limit(kMaxLds));
             HIP_OK(hipMalloc((void**)&c->d_error, sizeof(int32_t)));
             HIP_OK(hipMemset(c->d_error, 0, sizeof(int32_t)));
+            HIP_OK(hipMalloc((void**)&c->d_tail, aeon_hip_ctx::kSlots * sizeof(uint32_t)));
+            HIP_OK(hipMemset(c->d_tail, 0, aeon_hip_ctx::kSlots * sizeof(uint32_t)));
+            HIP_OK(hipDeviceSynchronize());
             // RGB2HSV_b division tables (hsv_shift = 12), as OpenCV builds them, then per uchar H
             // HSV2RGB_f's sector fraction f (its own float operations) turned into the weight w of
             // each output channel in t = v*(1 - s*w): t0 w=0, t1 w=1, t2 w=f, t3 w=1-f
@@ -1291,6 +1300,7 @@ int aeon_hip_ctx_create(int device, aeon_hip_ctx** out)
             if (const char* e = std::getenv("AEON_HIP_CONTIG")) c->contig = std::atoi(e);
             if (const char* e = std::getenv("AEON_HIP_L2_PREFETCH")) c->l2_prefetch = std::atoi(e);
             if (const char* e = std::getenv("AEON_HIP_INFO_AHEAD")) c->info_ahead = std::atoi(e);
+            if (const char* e = std::getenv("AEON_HIP_DYN_TAIL")) c->dyn_tail = std::atoi(e);
             if (const char* e = std::getenv("AEON_HIP_DONE_EVERY"))
                 c->done_every = std::min(aeon_hip_ctx::kSlots / 2, std::max(1, std::atoi(e)));
         } catch (...) {
@@ -1344,6 +1354,7 @@ int aeon_hip_ctx_destroy(aeon_hip_ctx* c)
         if (c->join_event) (void)hipEventDestroy(c->join_event);
         for (auto& L : c->luts) (void)hipFree(L.dev);
         if (c->d_error) (void)hipFree(c->d_error);
+        if (c->d_tail) (void)hipFree(c->d_tail);
         if (c->d_hsv) (void)hipFree(c->d_hsv);
         delete c;
         return 0;
