@@ -126,6 +126,7 @@ struct LaunchArgs {
     uint32_t*      tail_ctr;   // non-null: the partial last round of tiles is handed out by this counter
                                // (zero on entry; the launch's last draw resets it)
     int32_t        tail_rounds; // ... and this many full rounds before it
+    int32_t        head_split;  // final single-buffer launches: each workgroup's first tile in two halves
     int32_t        contig;     // single-buffer launches: workgroup b takes the contiguous tile range
                                // [T*b/G, T*(b+1)/G) (consecutive bands of a record reuse its tables)
     double         smean[3], sinv[3]; // sinv = 1/stddev, or 0 for stddev 0 (no division)

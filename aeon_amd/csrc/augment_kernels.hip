@@ -677,12 +677,13 @@ struct Bands {
         int       job, band, y0, nrows;
         StageGeom G;
     };
-    __device__ __forceinline__ Info info(int t) const
+    // (hparts > 1: part hpart of tile t cut into hparts row sub-tiles -- the head split)
+    __device__ __forceinline__ Info info(int t, int hpart = 0, int hparts = 1) const
     {
         Info f;
         f.ok       = false;
-        int part   = 0, parts = 1;
-        if (t >= a.split_base) { // a sub-tile of the last round (split_parts per tile)
+        int part   = hpart, parts = hparts;
+        if (hparts == 1 && t >= a.split_base) { // a sub-tile of the last round (split_parts per tile)
             parts = a.split_parts;
             part  = (t - a.split_base) % parts;
             t     = whole_tile(a, t);
@@ -1232,6 +1233,10 @@ void augment_tiles(LaunchArgs a)
             const int k = (int)__builtin_amdgcn_readfirstlane(*slot);
             return k < t_tail ? t_dyn + k : -1;
         };
+        // head split (final launches): a workgroup's first tile as two half-height sub-tiles, so the
+        // chip's first stores start after half a tile's staging
+        int hp = (KM == KM_FINAL && a.head_split && t < t_end) ? 0 : -1;
+        if (hp == 0) f = W.info(t, 0, 2);
         bool live = t < t_end;
         if (t_tail && !live) { // no static tile: start with a drawn one
             t    = draw();
@@ -1245,7 +1250,7 @@ void augment_tiles(LaunchArgs a)
             // (the VALU-bound contrast pass 1 prefers the reverse: 293 -> 283 us on C3)
             __builtin_amdgcn_s_setprio(KM == KM_STATS ? kComputePrio : kStagePrio);
             stamp(it, 0);
-            const bool more = t < t_end && t + t_step < t_end; // a static next tile
+            const bool more = hp == 0 || (t < t_end && t + t_step < t_end); // a static next (sub-)tile
             stamp(it, 1);
             if (wave == 0) prefetch_job(a, t + t_step, L.pf);
             W.issue(f, 0);
@@ -1262,15 +1267,21 @@ void augment_tiles(LaunchArgs a)
             __syncthreads();
             stamp(it, 6);
             __builtin_amdgcn_s_setprio(KM == KM_STATS ? kStagePrio : kComputePrio);
-            if (a.l2_prefetch && more) W.prefetch_src(W.info(t + t_step));
-            if (a.info_ahead && more && wave == nw - 1) W.put_info(W.info(t + t_step));
+            if (a.l2_prefetch && more && hp != 0) W.prefetch_src(W.info(t + t_step));
+            if (a.info_ahead && more && wave == nw - 1) W.put_info(hp == 0 ? W.info(t, 1, 2) : W.info(t + t_step));
             W.compute_any(f, 0);
             stamp(it, 7);
             lds_barrier(); // everyone is done reading the buffer before it is refilled
             stamp(it, 8);
             if (more) {
-                f = a.info_ahead ? W.get_info() : W.info(t + t_step);
-                t += t_step;
+                if (hp == 0) {
+                    f  = a.info_ahead ? W.get_info() : W.info(t, 1, 2);
+                    hp = 1;
+                } else {
+                    f = a.info_ahead ? W.get_info() : W.info(t + t_step);
+                    t += t_step;
+                    hp = -1;
+                }
             } else if (t_tail) {
                 t    = draw();
                 live = t >= 0;

@@ -561,6 +561,7 @@ struct aeon_hip_ctx {
     int         wg_per_cu = 0; // AEON_HIP_WG_PER_CU: experiments only (0 = occupancy API)
     int         l2_prefetch = 0; // AEON_HIP_L2_PREFETCH: warm L2 with the next tile's source rows (experiment)
     int         info_ahead  = 1; // AEON_HIP_INFO_AHEAD=0: every wave derives each tile's geometry itself
+    int         head_split  = 0; // AEON_HIP_HEAD_SPLIT: first tile of each workgroup in two halves (experiment)
     int         dyn_tail    = 3; // AEON_HIP_DYN_TAIL: 0 = static schedule; n = the last partial + (n-1) full rounds of tiles handed out by a counter
     int         contig    = 0; // AEON_HIP_CONTIG: 1 = contiguous tile ranges for contrast pass 1, 2 = every launch
     std::vector<std::pair<std::vector<int>, int>> occ; // launch shape -> workgroups per CU
@@ -808,6 +809,7 @@ LaunchArgs launch_args(aeon_hip_ctx* ctx, const Slot& s, const uint8_t* table, c
                        const aeon_out_desc& o, const float* d_lut, int partial_stride, bool u8_map = false)
 {
     LaunchArgs a{};
+    a.head_split = ctx->head_split;
     if (ctx->dyn_tail > 0) { // the slot's own counter: launches of calls in flight never share one
         a.tail_ctr    = ctx->d_tail + (&s - ctx->slots);
         a.tail_rounds = ctx->dyn_tail - 1;
@@ -1301,6 +1303,7 @@ int aeon_hip_ctx_create(int device, aeon_hip_ctx** out)
             if (const char* e = std::getenv("AEON_HIP_L2_PREFETCH")) c->l2_prefetch = std::atoi(e);
             if (const char* e = std::getenv("AEON_HIP_INFO_AHEAD")) c->info_ahead = std::atoi(e);
             if (const char* e = std::getenv("AEON_HIP_DYN_TAIL")) c->dyn_tail = std::atoi(e);
+            if (const char* e = std::getenv("AEON_HIP_HEAD_SPLIT")) c->head_split = std::atoi(e);
             if (const char* e = std::getenv("AEON_HIP_DONE_EVERY"))
                 c->done_every = std::min(aeon_hip_ctx::kSlots / 2, std::max(1, std::atoi(e)));
         } catch (...) {
