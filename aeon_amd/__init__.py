@@ -131,6 +131,8 @@ def lib():
         L.aeon_calculate_scale.argtypes = [ctypes.c_int] * 4 + [P(ctypes.c_float)]
         L.aeon_cropbox_max_proportional.argtypes = [ctypes.c_float] * 4 + [P(ctypes.c_float)] * 2
         L.aeon_jpeg_info.argtypes = [ctypes.c_char_p, ctypes.c_size_t] + [P(ctypes.c_int)] * 3
+        L.aeon_jpeg_entropy_decode.argtypes = ([ctypes.c_char_p, ctypes.c_size_t] + [P(ctypes.c_int)] * 3 +
+                                               [P(ctypes.c_int64)] * 2 + [P(ctypes.c_uint64)])
         L.aeon_png_info.argtypes = [ctypes.c_char_p, ctypes.c_size_t] + [P(ctypes.c_int)] * 4
         L.aeon_decode_png.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int, vp, ctypes.c_size_t,
                                       P(ctypes.c_int)]
@@ -228,6 +230,16 @@ def jpeg_info(data):
     w, h, n = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
     _check(lib().aeon_jpeg_info(bytes(data), len(data), ctypes.byref(w), ctypes.byref(h), ctypes.byref(n)))
     return w.value, h.value, n.value
+
+
+def jpeg_entropy_decode(data):
+    """Host-only Huffman decode of a JPEG file (aeon_jpeg_entropy_decode): (width, height,
+    components, blocks, non-zero values, FNV-1a hash of the sparse coefficient stream)."""
+    w, h, n = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    nb, nv, hv = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_uint64()
+    _check(lib().aeon_jpeg_entropy_decode(bytes(data), len(data), ctypes.byref(w), ctypes.byref(h), ctypes.byref(n),
+                                          ctypes.byref(nb), ctypes.byref(nv), ctypes.byref(hv)))
+    return w.value, h.value, n.value, nb.value, nv.value, hv.value
 
 
 PNG_BGR8, PNG_GRAY8, PNG_ANYDEPTH = 0, 1, 2

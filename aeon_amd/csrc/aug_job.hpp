@@ -104,7 +104,6 @@ struct LaunchArgs {
     int32_t        max_tiles;      // tiles per job (tile t = band t % max_tiles of job t / max_tiles)
     int32_t        total_tiles;    // jobs * max_tiles
     int32_t        stage_bytes;    // capacity of one LDS staging buffer (multiple of 1 KiB)
-    int32_t        stage_buffers;  // 2: the next tile's staging overlaps this tile's compute; 1: serial
     int32_t        max_win_w;  // capacity of the column-tap tables
     int32_t        out_dtype;  // OutDtype
     int32_t        channel_major;
@@ -115,31 +114,12 @@ struct LaunchArgs {
     int32_t        partial_stride; // (tile, wave) entries per contrast slot in `partials`
     int32_t        threads;    // workgroup size (kBlockMin..kBlockMax, a multiple of 64)
     int32_t        has_rtab;   // LDS holds a per-record table (contrast -> lighting -> standardize)
-    // tail split: tiles from split_base on (the last, partial round of the persistent grid) are
-    // cut into split_parts row sub-tiles each, so every workgroup takes part in that round
-    int32_t        split_base;
-    int32_t        split_parts;
     int32_t        u8_map;     // uint8 stores go through the LUT (fixed_aspect_ratio's uint8 standardize)
     int32_t        has_mean;   // double output: standardize with smean / sinv (by SOURCE channel)
-    int32_t        l2_prefetch; // single-buffer launches: touch the next tile's source lines (L2) during compute
-    int32_t        info_ahead; // single-buffer launches: one wave derives the next tile's geometry during compute
     uint32_t*      tail_ctr;   // non-null: the partial last round of tiles is handed out by this counter
                                // (zero on entry; the launch's last draw resets it)
     int32_t        tail_rounds; // ... and this many full rounds before it
-    int32_t        head_split;  // final single-buffer launches: each workgroup's first tile in two halves
-    int32_t        contig;     // single-buffer launches: workgroup b takes the contiguous tile range
-                               // [T*b/G, T*(b+1)/G) (consecutive bands of a record reuse its tables)
     double         smean[3], sinv[3]; // sinv = 1/stddev, or 0 for stddev 0 (no division)
-};
-
-// Arguments of augment_contrast_fused (both passes of contrast records in one launch).
-struct FusedArgs {
-    LaunchArgs s, f;   // pass 1 (KM_STATS, LINEAR) and pass 2 (KM_FINAL, COPY + record table)
-    uint32_t*  done;   // per record (stats slot): pass-1 tiles published; zeroed before every launch
-    int32_t    n_rec;  // records = pass-1 jobs = pass-2 jobs, pass-2 job i reading stats slot i
-    int32_t    lag;    // records between a record's pass-1 and pass-2 tiles in the task order
-    int32_t    total;  // tasks = n_rec * (s.max_tiles + f.max_tiles)
-    int32_t    max_win_w, rows_per_tile, stage_bytes; // the shared LDS layout (max of both passes)
 };
 
 // KM_FINAL: a record through to the loader output.  KM_STATS: contrast pass 1 -- resize +
@@ -172,23 +152,21 @@ constexpr int kHueTabBytes   = 184 * 16;
 struct LdsLayout {
     int lut, hsv, rtab, xt, yt, pf, info, stage, stage_bytes, total;
 };
-// One or two staging buffers and copies of the tap tables (with two, the next tile's are filled
-// while the current tile is computed).  The HSV tables are reserved only for hue launches.  The LUT sits
-// at offset 0 so its per-channel reads use immediate LDS offsets.
-AEON_HD inline LdsLayout lds_layout(int max_win_w, int rows_per_tile, int stage_bytes, bool hue, int buffers,
-                                    bool rtab = false)
+// One staging buffer and the tap tables.  The HSV tables are reserved only for hue launches.  The
+// LUT sits at offset 0 so its per-channel reads use immediate LDS offsets.
+AEON_HD inline LdsLayout lds_layout(int max_win_w, int rows_per_tile, int stage_bytes, bool hue, bool rtab = false)
 {
     LdsLayout L;
     int       o = 0;
     L.lut = o; o += 3 * 256 * 4;                             // standardize LUT (source channel order)
-    L.hsv = o; o += hue ? kHsvLdsDivBytes + buffers * kHueTabBytes : 0; // sdiv + v/255 / hdiv180, per-tile hue tables
+    L.hsv = o; o += hue ? kHsvLdsDivBytes + kHueTabBytes : 0; // sdiv + v/255 / hdiv180, per-tile hue tables
     L.rtab = o; o += rtab ? 3 * 256 * 4 : 0;                 // the tile's record table (f32, source channel order)
-    L.xt  = o; o += buffers * ((max_win_w * 8 + 15) / 16) * 16; // per-column taps + weights
-    L.yt  = o; o += buffers * rows_per_tile * 16;               // per-row taps + weights
+    L.xt  = o; o += ((max_win_w * 8 + 15) / 16) * 16; // per-column taps + weights
+    L.yt  = o; o += rows_per_tile * 16;               // per-row taps + weights
     L.pf  = o; o += 256;                                     // LDS-DMA sink of job prefetches
     L.info = o; o += 64;                                     // the next tile's geometry (one wave computes it)
     L.stage_bytes = stage_bytes;                             // source pixels, 4 B each (B,G,R,x)
-    L.stage = o; o += buffers * stage_bytes;
+    L.stage = o; o += stage_bytes;
     L.total = o;
     return L;
 }

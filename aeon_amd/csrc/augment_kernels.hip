@@ -417,29 +417,6 @@ __device__ __forceinline__ void stage_issue(cjob& J, const StageGeom& G, int buf
     }
 }
 
-// L2 warm-up of a later tile's source rows: this wave's share of one 4-byte LDS-DMA per 128-byte
-// line of the rows (into the 256-byte sink; nothing reads it), so that tile's staging loads hit L2.
-__device__ __forceinline__ void stage_prefetch(cjob& J, const StageGeom& G, int sink, int wave, int nw)
-{
-    const int   lane = threadIdx.x & 63;
-    const auto  rsrc = uniform_rsrc((const void*)J.src_ptr, (int)J.src_bytes);
-    const int   row  = G.nc * J.cn;
-    const int   lpr  = (row + 127) / 128 + 1; // lines a row segment can touch
-    const int   Q    = G.nr * lpr;
-    const float inv  = 1.f / (float)lpr;
-    for (int i = wave; i * 64 < Q; i += nw) {
-        const int q    = i * 64 + lane;
-        uint32_t  voff = kOutOfRange;
-        if (q < Q) {
-            const int j = (int)(((float)q + 0.5f) * inv), k = q - j * lpr;
-            const int b = src_off(J, G, j, 0);
-            const int a = (max(b, 0) & ~127) + k * 128;
-            if (b >= 0 && a < b + row) voff = (uint32_t)a;
-        }
-        lds_dma<4>(rsrc, sink, voff);
-    }
-}
-
 // (2) After this wave's loads landed: unpack its BGR slots in place; zero border of a padded job;
 // re-read loads that crossed the end of the buffer (rare; uniformly skipped otherwise for gray).
 __device__ __forceinline__ void stage_unpack(cjob& J, const StageGeom& G, int buf, int wave, int nw)
@@ -512,16 +489,10 @@ __device__ __forceinline__ void stage_unpack(cjob& J, const StageGeom& G, int bu
 
 // Pull the job descriptor of a future tile into L2 (an LDS-DMA into a sink nobody reads): its
 // scalar loads then hit L2 instead of paying an HBM round trip at the head of that tile.
-// The whole tile a (possibly split, see Bands::info) launch tile index belongs to.
-__device__ __forceinline__ int whole_tile(const LaunchArgs& a, int t)
-{
-    return t >= a.split_base ? a.split_base + (t - a.split_base) / a.split_parts : t;
-}
-
 __device__ __forceinline__ void prefetch_job(const LaunchArgs& a, int t, int lds_sink)
 {
-    if (t >= a.total_tiles) return;
-    const int      job  = whole_tile(a, t) / a.max_tiles;
+    if (t < 0 || t >= a.total_tiles) return;
+    const int      job  = t / a.max_tiles;
     const auto     rs   = uniform_rsrc((const void*)(a.jobs + job), (int)sizeof(AugJob));
     const uint32_t lane = threadIdx.x & 63;
     lds_dma<4>(rs, lds_sink, lane * 4 < sizeof(AugJob) ? lane * 4 : kOutOfRange);
@@ -646,10 +617,10 @@ enum OutForm : int { OF_F32_CHW_VEC = 0, OF_GENERIC = 1 };
 // A launch covers n_jobs x max_tiles tiles: tile t = band (t % max_tiles) of job (t / max_tiles),
 // a band being TR consecutive output rows of the job's window.  Workgroups are persistent (the
 // host sizes the grid to what the CUs hold at once) and take tiles blockIdx.x, +gridDim.x, ...
-// Per tile, with two LDS staging buffers:
-//   issue the LDS-DMA staging of the NEXT tile (and build its row / column tap tables) ->
-//   compute and store the current tile from LDS -> counted vmcnt wait that retires the next
-//   tile's loads but not this tile's stores -> unpack own slots -> barrier.
+// for the static rounds, the last rounds from a counter (dynamic tail).  Per tile, one LDS
+// staging buffer: LDS-DMA of the tile's source rows + row / column tap tables -> wait -> unpack
+// own slots -> barrier -> compute and store -> barrier; the CU's other workgroups cover the
+// staging latency, one wave derives the next tile's geometry during the compute.
 // A workgroup = 256..512 lanes holding whole 4-pixel column groups of the window (448 = 8 x 56
 // for 224-wide outputs); a lane keeps the same four output columns for the whole tile, so their
 // resize taps, LDS byte offsets, flip and scalar-tail masks stay in registers, and writes each
@@ -662,10 +633,7 @@ enum OutForm : int { OF_F32_CHW_VEC = 0, OF_GENERIC = 1 };
 // launch has OpenCV scalar-tail columns (3*dst_w not covered by the SIMD loops).
 
 
-// IAUX: cache-policy bits of the uint8 intermediate's stores and of the contrast partial sums (16 =
-// sc1, write-through, when another workgroup of the same launch consumes them: the fused contrast
-// kernel below).
-template <int KM, int RM, bool PHOTO, int OF, bool TAIL, int IAUX = 0>
+template <int KM, int RM, bool PHOTO, int OF, bool TAIL>
 struct Bands {
     const LaunchArgs& a;
     const LdsLayout&  L;
@@ -677,27 +645,19 @@ struct Bands {
         int       job, band, y0, nrows;
         StageGeom G;
     };
-    // (hparts > 1: part hpart of tile t cut into hparts row sub-tiles -- the head split)
-    __device__ __forceinline__ Info info(int t, int hpart = 0, int hparts = 1) const
+    __device__ __forceinline__ Info info(int t) const
     {
         Info f;
-        f.ok       = false;
-        int part   = hpart, parts = hparts;
-        if (hparts == 1 && t >= a.split_base) { // a sub-tile of the last round (split_parts per tile)
-            parts = a.split_parts;
-            part  = (t - a.split_base) % parts;
-            t     = whole_tile(a, t);
-        }
+        f.ok   = false;
         f.job  = t / a.max_tiles;
         f.band = t - f.job * a.max_tiles;
         cjob& J = job_ref(a, f.job);
         if (f.band >= J.tiles) return f;
         if (KM == KM_STATS && J.stats_slot < 0) return f;
-        const int TR  = a.rows_per_tile;
-        const int sub = (TR + parts - 1) / parts;
-        f.y0          = f.band * TR + part * sub;
-        f.nrows       = min(min(sub, TR - part * sub), J.win_h - f.y0);
-        if (f.nrows <= 0) return f; // a sub-tile past the end of a short last band
+        const int TR = a.rows_per_tile;
+        f.y0         = f.band * TR;
+        f.nrows      = min(TR, J.win_h - f.y0);
+        if (f.nrows <= 0) return f;
         // source columns (taps are monotone in dx)
         const XTap xf      = xcoef<RM>(J.win_x, J.scale_x, J.crop_w);
         const XTap xl      = xcoef<RM>(J.win_x + J.win_w - 1, J.scale_x, J.crop_w);
@@ -738,30 +698,22 @@ struct Bands {
         return f;
     }
 
-    // Stage a tile into buffer b (loads in flight on return) and build its row taps; its column
-    // taps too unless buffer b already holds this job's (consecutive tiles of one record).
-    __device__ __forceinline__ void prep(const Info& f, int b, bool build_xt) const
+    // Issue the tile's LDS-DMA staging (loads in flight on return).
+    __device__ __forceinline__ void issue(const Info& f) const
     {
-        issue(f, b);
-        tables(f, b, build_xt);
+        if (f.ok) stage_issue(job_ref(a, f.job), f.G, L.stage, wave, nw);
     }
-    __device__ __forceinline__ void prefetch_src(const Info& f) const
-    {
-        if (f.ok) stage_prefetch(job_ref(a, f.job), f.G, L.pf, wave, nw);
-    }
-    __device__ __forceinline__ void issue(const Info& f, int b) const
-    {
-        if (f.ok) stage_issue(job_ref(a, f.job), f.G, L.stage + b * L.stage_bytes, wave, nw);
-    }
-    __device__ __forceinline__ void tables(const Info& f, int b, bool build_xt, bool build_rec = true) const
+    // The tile's row taps; its column taps and hue table too unless the LDS still holds this
+    // record's (build_xt / build_rec false: the workgroup's previous tile was of the same record).
+    __device__ __forceinline__ void tables(const Info& f, bool build_xt, bool build_rec = true) const
     {
         if (!f.ok) return;
         cjob&      J     = job_ref(a, f.job);
         const StageGeom& G = f.G;
-        const int  stage = L.stage + b * L.stage_bytes;
+        const int  stage = L.stage;
         const int  tid = threadIdx.x, nt = blockDim.x;
         if (build_xt) {
-            const auto xt = lds_ptr<i32x2>(L.xt) + b * a.max_win_w;
+            const auto xt = lds_ptr<i32x2>(L.xt);
             for (int x = tid; x < J.win_w; x += nt) {
                 const XTap c = xcoef<RM>(J.win_x + x, J.scale_x, J.crop_w);
                 xt[x]        = (i32x2){c.sx - G.u_lo, (c.a0 & 0xffff) | (c.a1 << 16)};
@@ -769,7 +721,7 @@ struct Bands {
         }
         if (PHOTO && KM != KM_RAW && a.has_hue && build_rec && J.cn == 3 && (J.photo & PHOTO_HUE)) {
             // the record's hue table (kHueTabBytes): cvtColor's H of h12, + hue, % 180 as uchar
-            const int     tab = L.hsv + kHsvLdsDivBytes + b * kHueTabBytes;
+            const int     tab = L.hsv + kHsvLdsDivBytes;
             const f32x4*  wt  = reinterpret_cast<const f32x4*>(a.hsv_tables + kHsvDivWords);
             const int     hue = J.hue;
             const bool    sp  = fast_photo(f);
@@ -793,7 +745,7 @@ struct Bands {
                 lds_ptr<i32x2>(tab)[i] = (i32x2){(int)__float_as_uint(w[iw]), (int)sel};
             }
         }
-        const auto yt = lds_ptr<i32x4>(L.yt) + b * a.rows_per_tile;
+        const auto yt = lds_ptr<i32x4>(L.yt);
         for (int r = tid; r < f.nrows; r += nt) {
             const YTap y = ycoef<RM>(J.win_y + f.y0 + r, J.scale_y, J.crop_h);
             yt[r]        = (i32x4){stage + (y.r0 - G.v_lo) * G.pitch * 4, stage + (y.r1 - G.v_lo) * G.pitch * 4, y.b0, y.b1};
@@ -833,9 +785,9 @@ struct Bands {
         }
     }
 
-    __device__ __forceinline__ void unpack(const Info& f, int b) const
+    __device__ __forceinline__ void unpack(const Info& f) const
     {
-        if (f.ok) stage_unpack(job_ref(a, f.job), f.G, L.stage + b * L.stage_bytes, wave, nw);
+        if (f.ok) stage_unpack(job_ref(a, f.job), f.G, L.stage, wave, nw);
     }
 
     // SPEC_BS_HUE: the tile's record is known (fast_photo) to be 3-channel, 4-pixel-aligned, with
@@ -843,7 +795,7 @@ struct Bands {
     // the pixel loop then carries no per-pixel branches on those run-time choices (their merged
     // paths cost ~7 VALU per pixel: conversions and moves the compiler hoists out of the branches).
     enum : int { SPEC_NONE = 0, SPEC_BS_HUE = 1 };
-    static constexpr bool kHasSpec = KM == KM_STATS && PHOTO && RM == RESIZE_LINEAR && !TAIL && IAUX == 0;
+    static constexpr bool kHasSpec = KM == KM_STATS && PHOTO && RM == RESIZE_LINEAR && !TAIL;
     __device__ __forceinline__ bool fast_photo(const Info& f) const
     {
         if (!kHasSpec || !f.ok) return false;
@@ -851,17 +803,17 @@ struct Bands {
         return J.cn == 3 && (J.photo & (PHOTO_BS | PHOTO_HUE)) == (PHOTO_BS | PHOTO_HUE) && J.bs_kind == BS_FIXPT &&
                (J.win_w & 3) == 0;
     }
-    __device__ __forceinline__ int compute_any(const Info& f, int b) const
+    __device__ __forceinline__ int compute_any(const Info& f) const
     {
         if constexpr (kHasSpec)
-            if (fast_photo(f)) return compute<SPEC_BS_HUE>(f, b);
-        return compute<SPEC_NONE>(f, b);
+            if (fast_photo(f)) return compute<SPEC_BS_HUE>(f);
+        return compute<SPEC_NONE>(f);
     }
 
     // Compute and store tile t from buffer b.  Returns a lower bound on the vector-memory
     // instructions this wave issued (its stores): all younger than the next tile's staging loads.
     template <int SPEC = SPEC_NONE>
-    __device__ __forceinline__ int compute(const Info& f, int b) const
+    __device__ __forceinline__ int compute(const Info& f) const
     {
         if (!f.ok) return 0;
         constexpr bool SP = SPEC == SPEC_BS_HUE;
@@ -871,8 +823,8 @@ struct Bands {
         const int  nt    = blockDim.x;
         const int  cn    = SP ? 3 : J.cn;
         const int  win_w = J.win_w;
-        const auto xt    = lds_ptr<const i32x2>(L.xt) + b * a.max_win_w;
-        const auto yt    = lds_ptr<const i32x4>(L.yt) + b * a.rows_per_tile;
+        const auto xt    = lds_ptr<const i32x2>(L.xt);
+        const auto yt    = lds_ptr<const i32x4>(L.yt);
         const auto sdv   = lds_ptr<const i32x2>(L.hsv);
         const auto hdiv  = lds_ptr<const int32_t>(L.hsv + 256 * 8);
         // (a STATS tile's chain ends at the intermediate: only BS and HUE matter to it)
@@ -883,8 +835,8 @@ struct Bands {
             sh0 = sh[0], sh1 = sh[1], sh2 = sh[2];
         }
         uint32_t sum0 = 0, sum1 = 0, sum2 = 0;
-        const auto htab  = lds_ptr<const f32x4>(L.hsv + kHsvLdsDivBytes + b * kHueTabBytes) + 30; // at h12 = 0
-        const auto htab8 = lds_ptr<const i32x2>(L.hsv + kHsvLdsDivBytes + b * kHueTabBytes) + 30; // SPEC_BS_HUE form
+        const auto htab  = lds_ptr<const f32x4>(L.hsv + kHsvLdsDivBytes) + 30; // at h12 = 0
+        const auto htab8 = lds_ptr<const i32x2>(L.hsv + kHsvLdsDivBytes) + 30; // SPEC_BS_HUE form
         BsRegs   bsr{};
         int      bs_kind = 0;
         if (PHOTO && (photo & PHOTO_BS)) bs_kind = SP ? (int)BS_FIXPT : J.bs_kind, bsr = bs_regs(J);
@@ -973,7 +925,7 @@ struct Bands {
                     const u32x3 q = {__builtin_amdgcn_perm(pk[1], pk[0], 0x04020100u),
                                      __builtin_amdgcn_perm(pk[2], pk[1], 0x05040201u),
                                      __builtin_amdgcn_perm(pk[3], pk[2], 0x06050402u)};
-                    __builtin_amdgcn_raw_buffer_store_b96(q, orsrc, (y * win_w + ox0) * 3, 0, IAUX);
+                    __builtin_amdgcn_raw_buffer_store_b96(q, orsrc, (y * win_w + ox0) * 3, 0, 0);
                     continue;
                 }
                 if (PHOTO && photo) {
@@ -1034,7 +986,7 @@ struct Bands {
                     const uint32_t w1 = v[1][1] | (v[1][2] << 8) | (v[2][0] << 16) | ((uint32_t)v[2][1] << 24);
                     const uint32_t w2 = v[2][2] | (v[3][0] << 8) | (v[3][1] << 16) | ((uint32_t)v[3][2] << 24);
                     const u32x3    q  = {w0, w1, w2};
-                    __builtin_amdgcn_raw_buffer_store_b96(q, orsrc, (y * win_w + ox0) * 3, 0, IAUX);
+                    __builtin_amdgcn_raw_buffer_store_b96(q, orsrc, (y * win_w + ox0) * 3, 0, 0);
                     continue;
                 }
                 if (KM == KM_RAW || KM == KM_STATS) { // HWC uint8, source channel order
@@ -1045,7 +997,7 @@ struct Bands {
                         for (int c = 0; c < 3; c++)
                             if (k < nk && c < cn)
                                 __builtin_amdgcn_raw_buffer_store_b8((uint8_t)u8_of(val[k][c]), orsrc, base + k * cn + c,
-                                                                     0, IAUX);
+                                                                     0, 0);
                     continue;
                 }
                 // image::loader::load: source channel c goes to output channel oc (mixChannels
@@ -1136,10 +1088,7 @@ struct Bands {
             sum0 = wave_sum(sum0), sum1 = wave_sum(sum1), sum2 = wave_sum(sum2);
             const int lane = tid & 63;
             uint32_t* p    = a.partials + ((size_t)J.stats_slot * a.partial_stride + (size_t)band * 8) * 4;
-            auto put = [&](uint32_t* q, uint32_t v) {
-                if (IAUX) __hip_atomic_store(q, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                else *q = v;
-            };
+            auto put = [&](uint32_t* q, uint32_t v) { *q = v; };
             if (lane == 0) put(p + wave * 4 + 0, sum0), put(p + wave * 4 + 1, sum1), put(p + wave * 4 + 2, sum2);
             if (wave == 0 && lane >= nw && lane < 8) put(p + lane * 4 + 0, 0), put(p + lane * 4 + 1, 0), put(p + lane * 4 + 2, 0);
         }
@@ -1178,8 +1127,7 @@ void augment_tiles(LaunchArgs a)
     }
     const int       tid = threadIdx.x, nt = blockDim.x;
     const int       wave = __builtin_amdgcn_readfirstlane(tid >> 6), nw = nt >> 6;
-    const LdsLayout L = lds_layout(a.max_win_w, a.rows_per_tile, a.stage_bytes, PHOTO && a.has_hue, a.stage_buffers,
-                                   a.has_rtab != 0);
+    const LdsLayout L = lds_layout(a.max_win_w, a.rows_per_tile, a.stage_bytes, PHOTO && a.has_hue, a.has_rtab != 0);
     const Bands<KM, RM, PHOTO, OF, TAIL> W{a, L, wave, nw};
 
     // per-launch tables
@@ -1191,13 +1139,6 @@ void augment_tiles(LaunchArgs a)
         hsv_div_tables(L, a.hsv_tables);
     }
     if (KM == KM_FINAL && PHOTO && a.has_rtab) __syncthreads(); // record tables read the LUT
-    // static schedule: tiles blockIdx.x, +G, +2G, ... -- the tiles in flight at any moment are
-    // consecutive bands of a few records (measured faster than contiguous ranges per workgroup,
-    // and than a counter-fed dynamic schedule: per-XCD ticket pools with stealing and smaller
-    // tiles at the end measured 41-47 us against 39 us, pools of contiguous records 48 us)
-    const int T   = a.total_tiles, G = gridDim.x;
-    int       t   = blockIdx.x;
-    int       buf = 0;
     // development: s_memtime stamps per (workgroup, iteration, phase) when a.trace is set;
     // s_memrealtime (chip-wide 100 MHz) at entry and exit
     auto stamp = [&](int it, int ph) {
@@ -1206,126 +1147,79 @@ void augment_tiles(LaunchArgs a)
     };
     if (a.trace && tid == 0) a.trace[(blockIdx.x * 16) * 16 + 15] = (uint32_t)__builtin_amdgcn_s_memrealtime();
     using Info = typename Bands<KM, RM, PHOTO, OF, TAIL>::Info;
-    if (a.stage_buffers == 1) {
-        // one buffer (compute-heavy photometric launches, more rows per tile): stage, wait,
-        // compute; the CU's other workgroups cover the latency
-        int t_end = T, t_step = G, prev_job = -1;
-        if (a.contig) { // contiguous tile ranges: a record's consecutive bands keep its tables
-            t     = (int)((long)T * blockIdx.x / G);
-            t_end = (int)((long)T * (blockIdx.x + 1) / G);
-            t_step = 1;
+    // Schedule: static rounds, tiles blockIdx.x, +G, +2G, ... (the tiles in flight at any moment are
+    // consecutive bands of a few records: measured faster than contiguous ranges per workgroup and
+    // than a fully counter-fed schedule), then a dynamic tail: the tiles of the partial last round
+    // plus tail_rounds full rounds before it go to whichever workgroups finish their static tiles
+    // first, one counter draw per tile and one failing draw per workgroup -- exactly t_tail + G draws,
+    // the last of which resets the ring slot's counter for its next launch.
+    const int T      = a.total_tiles, G = gridDim.x;
+    const int t_tail = a.tail_ctr ? min(T % G + a.tail_rounds * G, T - T % G == 0 ? T : T - G) : 0;
+    const int t_dyn  = T - t_tail; // first dynamically handed-out tile
+    auto draw = [&]() -> int { // the next dynamic tile, or -1
+        const auto slot = lds_ptr<uint32_t>(L.info + 60);
+        if (tid == 0) {
+            const uint32_t k = atomicAdd(a.tail_ctr, 1u);
+            if (k == (uint32_t)(t_tail + G - 1)) atomicExch(a.tail_ctr, 0u); // the last draw of the launch
+            if (k >= (uint32_t)(t_tail + G)) atomicOr(a.error, 32);        // a counter left over by a launch
+            *slot = k;
         }
-        // dynamic tail: the tiles of the partial last round go to whichever workgroups finish their
-        // static rounds first (one counter draw per tile, one failing draw per workgroup)
-        const int  t_tail = (a.tail_ctr && !a.contig) ? min(T % G + a.tail_rounds * G, T - T % G == 0 ? T : T - G) : 0;
-        const int  t_dyn  = T - t_tail; // first dynamically handed-out tile
-        if (t_tail) t_end = t_dyn;
-        Info f = W.info(t < t_end ? t : 0);
-        int  it = 0;
-        auto draw = [&]() -> int { // the next dynamic tile, or -1
-            const auto slot = lds_ptr<uint32_t>(L.info + 60);
-            if (tid == 0) {
-                const uint32_t k = atomicAdd(a.tail_ctr, 1u);
-                if (k == (uint32_t)(t_tail + G - 1)) atomicExch(a.tail_ctr, 0u); // the last draw of the launch
-                *slot = k;
-            }
-            __syncthreads();
-            const int k = (int)__builtin_amdgcn_readfirstlane(*slot);
-            return k < t_tail ? t_dyn + k : -1;
-        };
-        // head split (final launches): a workgroup's first tile as two half-height sub-tiles, so the
-        // chip's first stores start after half a tile's staging
-        int hp = (KM == KM_FINAL && a.head_split && t < t_end) ? 0 : -1;
-        if (hp == 0) f = W.info(t, 0, 2);
-        bool live = t < t_end;
-        if (t_tail && !live) { // no static tile: start with a drawn one
+        __syncthreads();
+        const int k = (int)__builtin_amdgcn_readfirstlane(*slot);
+        return k < t_tail ? t_dyn + k : -1;
+    };
+    int  t        = blockIdx.x;
+    int  prev_job = -1;
+    bool live     = t < t_dyn;
+    if (t_tail && !live) { // no static tile: start with a drawn one
+        t    = draw();
+        live = t >= 0;
+    }
+    Info f = W.info(live ? t : 0);
+    for (int it = 0; live; it++) {
+        // the staging phases (job loads, LDS-DMA issue, tap tables, unpack) at a raised wave
+        // priority: they are this workgroup's critical path while the CU's other workgroups
+        // stream stores (measured 38.8 -> 37.7 us on C2); the VALU-bound contrast pass 1 prefers
+        // the reverse (293 -> 283 us on C3)
+        __builtin_amdgcn_s_setprio(KM == KM_STATS ? kComputePrio : kStagePrio);
+        stamp(it, 0);
+        const bool more = t + G < t_dyn; // a static next tile
+        if (wave == 0) prefetch_job(a, more ? t + G : -1, L.pf);
+        W.issue(f);
+        stamp(it, 2);
+        const bool same = f.ok && f.job == prev_job; // the LDS tables still hold this record's
+        prev_job        = f.ok ? f.job : -1;
+        W.tables(f, !same, !same);
+        W.record_table(f);
+        stamp(it, 3);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        stamp(it, 4);
+        W.unpack(f);
+        stamp(it, 5);
+        __syncthreads();
+        stamp(it, 6);
+        __builtin_amdgcn_s_setprio(KM == KM_STATS ? kStagePrio : kComputePrio);
+        // the next static tile's geometry: derived by one wave (its f64 tap bounds are uniform work
+        // every wave would otherwise repeat) during the compute, handed over through LDS
+        if (more && wave == nw - 1) W.put_info(W.info(t + G));
+        W.compute_any(f);
+        stamp(it, 7);
+        lds_barrier(); // everyone is done reading the buffer before it is refilled
+        stamp(it, 8);
+        if (more) {
+            f = W.get_info();
+            t += G;
+        } else if (t_tail) {
             t    = draw();
             live = t >= 0;
             if (live) f = W.info(t);
+        } else {
+            break;
         }
-        for (; live; it++) {
-            // the staging phases (job loads, LDS-DMA issue, tap tables, unpack) at a raised wave
-            // priority: they are this workgroup's critical path while the CU's other workgroups
-            // stream stores (measured 38.8 -> 37.7 us on C2)
-            // (the VALU-bound contrast pass 1 prefers the reverse: 293 -> 283 us on C3)
-            __builtin_amdgcn_s_setprio(KM == KM_STATS ? kComputePrio : kStagePrio);
-            stamp(it, 0);
-            const bool more = hp == 0 || (t < t_end && t + t_step < t_end); // a static next (sub-)tile
-            stamp(it, 1);
-            if (wave == 0) prefetch_job(a, t + t_step, L.pf);
-            W.issue(f, 0);
-            stamp(it, 2);
-            const bool same = f.ok && f.job == prev_job; // the LDS tables still hold this record's
-            prev_job        = f.ok ? f.job : -1;
-            W.tables(f, 0, !same, !same);
-            W.record_table(f);
-            stamp(it, 3);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            stamp(it, 4);
-            W.unpack(f, 0);
-            stamp(it, 5);
-            __syncthreads();
-            stamp(it, 6);
-            __builtin_amdgcn_s_setprio(KM == KM_STATS ? kStagePrio : kComputePrio);
-            if (a.l2_prefetch && more && hp != 0) W.prefetch_src(W.info(t + t_step));
-            if (a.info_ahead && more && wave == nw - 1) W.put_info(hp == 0 ? W.info(t, 1, 2) : W.info(t + t_step));
-            W.compute_any(f, 0);
-            stamp(it, 7);
-            lds_barrier(); // everyone is done reading the buffer before it is refilled
-            stamp(it, 8);
-            if (more) {
-                if (hp == 0) {
-                    f  = a.info_ahead ? W.get_info() : W.info(t, 1, 2);
-                    hp = 1;
-                } else {
-                    f = a.info_ahead ? W.get_info() : W.info(t + t_step);
-                    t += t_step;
-                    hp = -1;
-                }
-            } else if (t_tail) {
-                t    = draw();
-                live = t >= 0;
-                if (live) f = W.info(t);
-            } else {
-                break;
-            }
-        }
-        if (a.trace && tid == 0) a.trace[(blockIdx.x * 16 + 1) * 16 + 15] = (uint32_t)__builtin_amdgcn_s_memrealtime();
-        return;
-    }
-    Info cur = W.info(t < T ? t : 0);
-    if (t < T) {
-        if (wave == 0) prefetch_job(a, t + G, L.pf);
-        W.prep(cur, 0, true);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        W.unpack(cur, 0);
-    }
-    __syncthreads();
-    for (int it = 0; t < T; t += G, it++) {
-        const bool more = t + G < T;
-        Info       nxt  = cur;
-        stamp(it, 0);
-        if (more) {
-            if (wave == 0) prefetch_job(a, t + 2 * G, L.pf);
-            nxt = W.info(t + G);
-            W.prep(nxt, buf ^ 1, true); // lands during this tile's compute
-        }
-        stamp(it, 1);
-        const int stores = W.compute(cur, buf);
-        stamp(it, 2);
-        if (!more) break;
-        // the next tile's loads were issued before this tile's stores: retire them, not the stores
-        wait_vm_upto(stores);
-        stamp(it, 3);
-        W.unpack(nxt, buf ^ 1);
-        stamp(it, 4);
-        lds_barrier();
-        stamp(it, 5);
-        buf ^= 1;
-        cur = nxt;
     }
     if (a.trace && tid == 0) a.trace[(blockIdx.x * 16 + 1) * 16 + 15] = (uint32_t)__builtin_amdgcn_s_memrealtime();
 }
+
 
 // Contrast pass 2 prologue: per stats slot, (1-c)*mean per channel from the exact per-(tile,
 // wave) sums of pass 1 (cv::mean = sum * (1./N), kept in f64).  One 64-lane workgroup per job
@@ -1354,130 +1248,6 @@ __global__ __launch_bounds__(64) void contrast_reduce(LaunchArgs a, int n_jobs)
         sh[0] = k * ((double)s0 * inv_n);
         sh[1] = k * ((double)s1 * inv_n);
         sh[2] = k * ((double)s2 * inv_n);
-    }
-}
-
-// ---- contrast records in one launch -----------------------------------------------------------
-// Contrast needs the mean of the whole post-hue record, so a contrast record is two passes: pass 1
-// (STATS, VALU-bound: resize + brightness/saturation + hue into an HWC uint8 intermediate + exact
-// channel sums) and pass 2 (FINAL, memory-bound: record table + float32 CHW stores).  As two
-// launches they run back to back; here one persistent launch takes both kinds of tile from one
-// static task order in which record j's pass-2 tiles come `lag` records after its pass-1 tiles, so
-// at any moment some workgroups compute pass 1 while others stream pass 2.  Hand-off (placement-
-// independent, cdna_hip_programming.md Guideline 16): pass 1 stores the intermediate and the
-// partial sums write-through (sc1), every wave drains them, then one lane adds to the record's
-// counter; a pass-2 tile's wave 0 polls that counter (relaxed, bounded, s_sleep), one agent-scope
-// acquire, then the workgroup reduces the sums and reads the intermediate.  Progress: a workgroup
-// takes its tasks in increasing order and a pass-2 task depends only on lower-numbered pass-1
-// tasks, so with every workgroup resident the lowest unfinished task can always run.
-// task q -> (pass 2?, record, band)
-__device__ __forceinline__ void fused_task(const FusedArgs& A, int q, bool& second, int& rec, int& band)
-{
-    const int ms = A.s.max_tiles, mf = A.f.max_tiles, L = A.lag, n = A.n_rec;
-    const int head = L * ms;                 // records 0..L-1: pass 1 only
-    const int mid  = (n - L) * (ms + mf);    // then per record: pass 1 of j, pass 2 of j - L
-    if (q < head) {
-        second = false, rec = q / ms, band = q - rec * ms;
-    } else if (q < head + mid) {
-        const int r = q - head, blk = r / (ms + mf), off = r - blk * (ms + mf);
-        if (off < ms) second = false, rec = L + blk, band = off;
-        else second = true, rec = blk, band = off - ms;
-    } else {
-        const int r = q - head - mid;
-        second = true, rec = n - L + r / mf, band = r - (r / mf) * mf;
-    }
-}
-
-template <int OF2>
-__global__ __launch_bounds__(kBlockMax) __attribute__((amdgpu_waves_per_eu(6)))
-void augment_contrast_fused(FusedArgs A)
-{
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    if ((uint32_t)(size_t)(__attribute__((address_space(3))) char*)smem != 0u) { // see lds_ld
-        if (threadIdx.x == 0) atomicOr(A.s.error, 4);
-        return;
-    }
-    const int       tid = threadIdx.x, nt = blockDim.x;
-    const int       wave = __builtin_amdgcn_readfirstlane(tid >> 6), nw = nt >> 6;
-    // the record table sits in the staging area past pass 2's own staging footprint (pass-2 tiles
-    // stage fewer bytes than pass-1 tiles), which keeps three workgroups per CU
-    LdsLayout L = lds_layout(A.max_win_w, A.rows_per_tile, A.stage_bytes, true, 1, false);
-    L.rtab      = L.stage + A.f.stage_bytes;
-    const Bands<KM_STATS, RESIZE_LINEAR, true, OF_GENERIC, false, 16> WS{A.s, L, wave, nw};
-    const Bands<KM_FINAL, RESIZE_COPY, true, OF2, false>               WF{A.f, L, wave, nw};
-    const auto sh = lds_ptr<double>(L.pf); // the record's (1-c)*mean (the job-prefetch sink is unused here)
-    {
-        const auto lut = lds_ptr<float>(L.lut);
-        for (int i = tid; i < 3 * 256; i += nt) lut[i] = A.f.lut[i];
-        hsv_div_tables(L, A.s.hsv_tables);
-    }
-    __syncthreads();
-    for (int q = blockIdx.x; q < A.total; q += gridDim.x) {
-        bool second;
-        int  rec, band;
-        fused_task(A, q, second, rec, band);
-        if (!second) {
-            const auto f = WS.info(rec * A.s.max_tiles + band);
-            __builtin_amdgcn_s_setprio(kComputePrio);
-            WS.issue(f, 0);
-            WS.tables(f, 0, true);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            WS.unpack(f, 0);
-            __syncthreads();
-            __builtin_amdgcn_s_setprio(kStagePrio);
-            WS.compute(f, 0);
-            // publish: every wave's write-through stores drained, then one counter add
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();
-            if (tid == 0 && f.ok)
-                __hip_atomic_fetch_add(A.done + rec, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            continue;
-        }
-        const auto f = WF.info(rec * A.f.max_tiles + band);
-        if (f.ok) {
-            cjob& JF = job_ref(A.f, f.job);
-            cjob& JS = job_ref(A.s, JF.stats_slot);
-            if (tid == 0) {
-                const uint32_t need = (uint32_t)JS.tiles;
-                uint32_t       spins = 0;
-                while (__hip_atomic_load(A.done + JF.stats_slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
-                    __builtin_amdgcn_s_sleep(2);
-                    if (++spins > (1u << 24)) { // ~0.5 s: give up, flag it (never expected)
-                        atomicOr(A.s.error, 8);
-                        break;
-                    }
-                }
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            }
-            __syncthreads();
-            if (wave == 0) { // contrast_reduce for this record, into LDS
-                unsigned long long s0 = 0, s1 = 0, s2 = 0;
-                const uint32_t*    base = A.s.partials + (size_t)JF.stats_slot * A.s.partial_stride * 4;
-                for (int e = tid; e < JS.tiles * 8; e += 64) s0 += base[e * 4], s1 += base[e * 4 + 1], s2 += base[e * 4 + 2];
-                for (int o = 32; o > 0; o >>= 1) {
-                    s0 += __shfl_xor(s0, o);
-                    s1 += __shfl_xor(s1, o);
-                    s2 += __shfl_xor(s2, o);
-                }
-                if (tid == 0) {
-                    const double inv_n = 1. / (double)(JS.win_w * JS.win_h);
-                    const double k     = 1.0 - (double)JS.contrast;
-                    sh[0] = k * ((double)s0 * inv_n), sh[1] = k * ((double)s1 * inv_n), sh[2] = k * ((double)s2 * inv_n);
-                }
-            }
-            __syncthreads();
-        }
-        __builtin_amdgcn_s_setprio(kStagePrio);
-        WF.issue(f, 0);
-        WF.tables(f, 0, true);
-        WF.record_table(f, sh);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        WF.unpack(f, 0);
-        __syncthreads();
-        __builtin_amdgcn_s_setprio(kComputePrio);
-        WF.compute(f, 0);
-        lds_barrier();
     }
 }
 
@@ -1542,23 +1312,6 @@ hipError_t launch_contrast_reduce(const LaunchArgs& a, int n_jobs, hipStream_t s
 {
     hipLaunchKernelGGL(contrast_reduce, dim3(n_jobs), dim3(64), 0, stream, a, n_jobs);
     return hipGetLastError();
-}
-
-static const void* fused_fn(int of) { return of == OF_F32_CHW_VEC ? (const void*)augment_contrast_fused<OF_F32_CHW_VEC>
-                                                                   : (const void*)augment_contrast_fused<OF_GENERIC>; }
-
-hipError_t launch_contrast_fused(const FusedArgs& A, int grid, int threads, int lds_bytes, hipStream_t stream,
-                                 hipEvent_t start, hipEvent_t stop)
-{
-    void* args[1] = {(void*)&A};
-    if (start || stop)
-        return hipExtLaunchKernel(fused_fn(out_form(A.f)), dim3(grid), dim3(threads), args, lds_bytes, stream, start, stop, 0);
-    return hipLaunchKernel(fused_fn(out_form(A.f)), dim3(grid), dim3(threads), args, lds_bytes, stream);
-}
-
-hipError_t contrast_fused_occupancy(const FusedArgs& A, int threads, int lds_bytes, int* blocks)
-{
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, fused_fn(out_form(A.f)), threads, lds_bytes);
 }
 
 // Workgroups of this kernel form one CU holds at once (persistent grid sizing).

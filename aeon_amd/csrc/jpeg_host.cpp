@@ -52,6 +52,17 @@ struct Huffman {
 
     void build(const uint8_t* counts, const uint8_t* symbols, int n)
     {
+        // validate the code space before any table entry is written (jdhuff.c
+        // jpeg_make_d_derived_tbl: the code after the last one of length l must be < 2^l, so an
+        // over-full length or an all-ones code is rejected)
+        {
+            int64_t code = 0;
+            for (int l = 1; l <= 16; l++) {
+                code += counts[l - 1];
+                if (code >= ((int64_t)1 << l)) bad("bad Huffman table");
+                code <<= 1;
+            }
+        }
         std::memcpy(vals, symbols, n);
         std::memset(look, 0, sizeof(look));
         int code = 0, k = 0;
@@ -62,7 +73,6 @@ struct Huffman {
                 if (l <= 9)
                     for (int f = 0; f < (1 << (9 - l)); f++) look[(code << (9 - l)) | f] = (uint16_t)((l << 8) | vals[k]);
             maxcode[l] = counts[l - 1] ? code - 1 : -1;
-            if (code > (1 << l)) bad("bad Huffman table");
             code <<= 1;
         }
         maxcode[17] = 0x7fffffff;
@@ -227,6 +237,9 @@ void parse_frame(const uint8_t* d, size_t size, Frame& f, const uint8_t** after)
             if (s[0] != 8) unsupported("only 8-bit samples are supported");
             f.H = be16(s + 1), f.W = be16(s + 3), f.ncomp = s[5];
             if (f.W <= 0 || f.H <= 0) bad("bad image size");
+            // (libjpeg would allocate whatever the header asks for; a bound keeps a corrupt header
+            // from reserving gigabytes of coefficient staging)
+            if ((int64_t)f.W * f.H > ((int64_t)1 << 28)) unsupported("images above 2^28 pixels");
             if (f.ncomp != 1 && f.ncomp != 3) unsupported("only 1- and 3-component images are supported");
             if (len < 8 + 3 * f.ncomp) bad("bad frame header");
             for (int k = 0; k < f.ncomp; k++) {
@@ -517,6 +530,7 @@ void decode_file(const uint8_t* d, size_t size, Frame& f, Arena& a, size_t blk_o
             continue;
         }
         // SOS
+        if (len < 6) bad("bad scan header"); // (ns, the selectors and Ss/Se/Ah-Al need >= 4 bytes)
         const uint8_t* s  = p + 2;
         const int      ns = s[0];
         if (ns < 1 || ns > f.ncomp || len != 6 + 2 * ns) bad("bad scan header");
@@ -790,6 +804,35 @@ void jpeg_info(const void* data, size_t size, int* w, int* h, int* ncomp)
     const uint8_t* after = nullptr;
     parse_frame((const uint8_t*)data, size, f, &after);
     *w = f.W, *h = f.H, *ncomp = f.ncomp;
+}
+
+// aeon_jpeg_entropy_decode's body: the host half of the stage alone (headers, tables, every scan's
+// Huffman decoding into the sparse block stream) on the calling thread -- no device needed.  The
+// stream is summarised as its block and value counts and an FNV-1a hash of (mask, values) per block
+// in component / raster order.
+void jpeg_entropy_only(const void* data, size_t size, int* w, int* h, int* ncomp, int64_t* n_blocks,
+                       int64_t* n_values, uint64_t* hash)
+{
+    Frame  f;
+    Arena  a;
+    size_t blk_off[3] = {0, 0, 0}, val_off = 0;
+    decode_file((const uint8_t*)data, size, f, a, blk_off, &val_off, false);
+    uint64_t  hv = 1469598103934665603ull;
+    auto      mix = [&](uint64_t x) {
+        for (int k = 0; k < 8; k++) hv = (hv ^ ((x >> (8 * k)) & 0xff)) * 1099511628211ull;
+    };
+    int64_t         nb = 0, nv = 0;
+    const int16_t*  vals = (const int16_t*)(a.host.data() + val_off);
+    for (int k = 0; k < f.ncomp; k++) {
+        const JpegBlock* recs = (const JpegBlock*)(a.host.data() + blk_off[k]);
+        for (size_t b = 0; b < (size_t)f.c[k].bw * f.c[k].bh; b++) {
+            const int cnt = __builtin_popcountll(recs[b].mask);
+            mix(recs[b].mask);
+            for (int i = 0; i < cnt; i++) mix((uint64_t)(uint16_t)vals[recs[b].val_off + i]);
+            nb++, nv += cnt;
+        }
+    }
+    *w = f.W, *h = f.H, *ncomp = f.ncomp, *n_blocks = nb, *n_values = nv, *hash = hv;
 }
 
 } // namespace aeon_hip

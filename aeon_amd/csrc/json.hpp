@@ -19,7 +19,7 @@ public:
     static Json parse(const std::string& text)
     {
         size_t i = 0;
-        Json   v = parse_value(text, i);
+        Json   v = parse_value(text, i, 0);
         skip_ws(text, i);
         if (i != text.size()) throw std::invalid_argument("json: trailing characters");
         return v;
@@ -98,8 +98,12 @@ private:
         i++;
         return out;
     }
-    static Json parse_value(const std::string& s, size_t& i)
+    // Nesting deeper than any configuration needs is refused (recursive descent: the untrusted text
+    // must not be able to exhaust the stack).
+    static constexpr int kMaxDepth = 256;
+    static Json parse_value(const std::string& s, size_t& i, int depth)
     {
+        if (depth > kMaxDepth) throw std::invalid_argument("json: nesting too deep");
         skip_ws(s, i);
         if (i >= s.size()) throw std::invalid_argument("json: unexpected end");
         Json v;
@@ -116,7 +120,7 @@ private:
                 skip_ws(s, i);
                 if (i >= s.size() || s[i] != ':') throw std::invalid_argument("json: expected ':'");
                 i++;
-                v.m_obj[k] = parse_value(s, i);
+                v.m_obj[k] = parse_value(s, i, depth + 1);
                 skip_ws(s, i);
                 if (i < s.size() && s[i] == ',') { i++; continue; }
                 if (i < s.size() && s[i] == '}') { i++; break; }
@@ -128,7 +132,7 @@ private:
             skip_ws(s, i);
             if (i < s.size() && s[i] == ']') return i++, v;
             for (;;) {
-                v.m_arr.push_back(parse_value(s, i));
+                v.m_arr.push_back(parse_value(s, i, depth + 1));
                 skip_ws(s, i);
                 if (i < s.size() && s[i] == ',') { i++; continue; }
                 if (i < s.size() && s[i] == ']') { i++; break; }

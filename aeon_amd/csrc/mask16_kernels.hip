@@ -302,23 +302,17 @@ hipError_t launch_nearest(const Mask16Job* jobs, int n_jobs, int max_h, int max_
                           hipStream_t stream, hipEvent_t start, hipEvent_t stop)
 {
     if (n_jobs <= 0) return hipSuccess;
-    const int   pitch = mask16_pitch(max_seg_bytes);
-    const char* env   = std::getenv("AEON_HIP_MASK_GATHER"); // experiments: "direct" = the old gather
-    const std::string mode = env ? env : "staged";
+    const int pitch = mask16_pitch(max_seg_bytes);
     // staged: up to 64 output rows / ~32K output elements per workgroup, LDS <= 64 KB (C5 A/B:
     // 64 rows 15.8 us, 32 rows 16.7, 16 rows 20.5, 8 rows 29.9; the direct gather 26.3); the LDS
-    // holds max_slots staged rows (the host's bound on the distinct source rows of one block)
-    int srows = mask16_rows(max_w, max_seg_bytes);
-    if (srows >= 1 && mode != "direct") {
-        if (const char* e = std::getenv("AEON_HIP_NEAREST_ROWS")) { // experiments: LDS for every row
-            srows = std::max(1, std::min(std::min(std::atoi(e), 64), 65536 / pitch));
-            max_slots = srows;
-        }
+    // holds max_slots staged rows (the host's bound on the distinct source rows of one block).
+    // Rows longer than the staging holds (srows < 1) take the direct gather.
+    const int srows = mask16_rows(max_w, max_seg_bytes);
+    if (srows >= 1) {
         max_slots       = std::max(1, std::min(max_slots, srows));
         const dim3 grid((max_h + srows - 1) / srows, n_jobs);
         const size_t lds = (size_t)max_slots * pitch;
-        int perm = 1;
-        if (const char* e = std::getenv("AEON_HIP_MASK_PERM")) perm = std::atoi(e);
+        int perm = 1; // gather_u8_perm where the columns qualify
         if (start || stop) {
             void* args[5] = {(void*)&jobs, (void*)&srows, (void*)&pitch, (void*)&perm, (void*)&max_slots};
             return hipExtLaunchKernel((const void*)nearest_staged, grid, dim3(256), args, lds, stream, start, stop, 0);
@@ -330,7 +324,6 @@ hipError_t launch_nearest(const Mask16Job* jobs, int n_jobs, int max_h, int max_
     const int groups  = (max_w + 3) / 4;
     const int threads = std::min(256, std::max(64, (groups + 63) / 64 * 64));
     int       rows    = std::max(1, std::min(64, 8192 / std::max(1, max_w)));
-    if (const char* e = std::getenv("AEON_HIP_NEAREST_ROWS")) rows = std::max(1, std::atoi(e)); // experiments
     const dim3 grid((max_h + rows - 1) / rows, n_jobs);
     if (start || stop) { // dispatch-stamped timing events, as the tile kernels
         void* args[2] = {(void*)&jobs, (void*)&rows};

@@ -48,19 +48,9 @@ __global__ __launch_bounds__(LANES) void plan_records(const PlanRecord* host_rec
 
 hipError_t launch_plan_records(const void* host_records, void* jobs, const PlanArgs& a, hipStream_t stream)
 {
-    static int per = 0;
-    if (!per) {
-        per = 16;
-        if (const char* e = std::getenv("AEON_HIP_PLAN_PER_BLOCK")) per = std::atoi(e); // experiments
-    }
-    const PlanRecord* r = (const PlanRecord*)host_records;
-    AugJob*           j = (AugJob*)jobs;
-    switch (per) {
-    case 1: hipLaunchKernelGGL((plan_records<1, 64>), dim3(a.n), dim3(64), 0, stream, r, j, a); break;
-    case 4: hipLaunchKernelGGL((plan_records<4, 64>), dim3((a.n + 3) / 4), dim3(64), 0, stream, r, j, a); break;
-    case 8: hipLaunchKernelGGL((plan_records<8, 128>), dim3((a.n + 7) / 8), dim3(128), 0, stream, r, j, a); break;
-    default: hipLaunchKernelGGL((plan_records<16, 128>), dim3((a.n + 15) / 16), dim3(128), 0, stream, r, j, a); break;
-    }
+    // 16 records per 128-lane workgroup (measured against 1, 4 and 8 per workgroup)
+    hipLaunchKernelGGL((plan_records<16, 128>), dim3((a.n + 15) / 16), dim3(128), 0, stream,
+                       (const PlanRecord*)host_records, (AugJob*)jobs, a);
     return hipGetLastError();
 }
 

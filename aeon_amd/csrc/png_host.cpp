@@ -150,7 +150,11 @@ inline uint32_t sample(const uint8_t* row, size_t s, int depth)
     }
 }
 
-// libpng png_do_rgb_to_gray without gamma tables (png_set_rgb_to_gray(1, 0.299, 0.587))
+// libpng png_do_rgb_to_gray without gamma tables (png_set_rgb_to_gray(1, 0.299, 0.587)), as libpng
+// 1.2 computes it at both depths: truncating >> 15.  (libpng 1.2.x is what the OpenCV 2.4.9 of
+// aeon's README platform -- Ubuntu 16.04, libpng12 -- links; libpng >= 1.5.5 rounds the 16-bit case,
+// + 16384 before the shift, which can differ by 1 in a 16-bit gray value.  Parity unpinned: no
+// reference output holds a colour 16-bit PNG read as gray.)
 constexpr uint32_t kRc = 29900u * 32768u / 100000u, kGc = 58700u * 32768u / 100000u, kBc = 32768u - kRc - kGc;
 inline uint32_t rgb_to_gray(uint32_t r, uint32_t g, uint32_t b)
 {

@@ -47,7 +47,7 @@ struct RotMap {
 // words: the launch's LDS capacity for the box (rot_box_words of its steepest angle).  CN: bytes per
 // pixel of every job of the launch (1, 2 or 3: unrolled channel loops), 0 = each job's own.
 template <int CN>
-__global__ __launch_bounds__(256) void rotate_tiles(const RotJob* __restrict__ jobs, int words)
+__global__ __launch_bounds__(256) void rotate_tiles(const RotJob* __restrict__ jobs, int words, int32_t* error)
 {
     extern __shared__ uint32_t st[];
     __shared__ int box[4];
@@ -75,7 +75,10 @@ __global__ __launch_bounds__(256) void rotate_tiles(const RotJob* __restrict__ j
     }
     bx1 += m.linear, by1 += m.linear;
     const int bw = bx1 - bx0 + 1, bh = by1 - by0 + 1, pitch = (bw + 3) & ~3; // pitch: whole 16-byte groups
-    if (pitch * bh > words) return; // cannot happen: the host sizes `words` for the launch's angles
+    if (pitch * bh > words) { // cannot happen (the host sizes `words` for the launch's angles): flag it
+        if (tid == 0) atomicOr(error, 64);
+        return;
+    }
     // stage: the box's 4-pixel groups, lane-strided.  Every load of a lane is issued before any is
     // used (buffer loads at kOOB return 0: the predication costs no branch): one 12-byte load per
     // group inside the image (BGR), byte loads for groups straddling its left / right edge (and for
@@ -231,17 +234,17 @@ int rot_box_words(int angle)
 
 // max_tiles: the most output tiles of any job's window; words: max rot_box_words of its angles;
 // cn: the jobs' common bytes per pixel, 0 if they differ
-hipError_t launch_rotate(const RotJob* jobs, int n_jobs, int max_tiles, int words, int cn, hipStream_t stream)
+hipError_t launch_rotate(const RotJob* jobs, int n_jobs, int max_tiles, int words, int cn, int32_t* error, hipStream_t stream)
 {
     if (n_jobs <= 0) return hipSuccess;
     if (words > kRotMaxWords) return hipErrorInvalidValue;
     const dim3   grid((unsigned)max_tiles, (unsigned)n_jobs), block(256);
     const size_t lds = (size_t)words * 4;
     switch (cn) {
-    case 3: hipLaunchKernelGGL(rotate_tiles<3>, grid, block, lds, stream, jobs, words); break;
-    case 1: hipLaunchKernelGGL(rotate_tiles<1>, grid, block, lds, stream, jobs, words); break;
-    case 2: hipLaunchKernelGGL(rotate_tiles<2>, grid, block, lds, stream, jobs, words); break;
-    default: hipLaunchKernelGGL(rotate_tiles<0>, grid, block, lds, stream, jobs, words); break;
+    case 3: hipLaunchKernelGGL(rotate_tiles<3>, grid, block, lds, stream, jobs, words, error); break;
+    case 1: hipLaunchKernelGGL(rotate_tiles<1>, grid, block, lds, stream, jobs, words, error); break;
+    case 2: hipLaunchKernelGGL(rotate_tiles<2>, grid, block, lds, stream, jobs, words, error); break;
+    default: hipLaunchKernelGGL(rotate_tiles<0>, grid, block, lds, stream, jobs, words, error); break;
     }
     return hipGetLastError();
 }

@@ -28,13 +28,11 @@ hipError_t launch_tiles(int km, int rm, bool tail, bool photo, const LaunchArgs&
                         hipEvent_t start, hipEvent_t stop);
 hipError_t launch_contrast_reduce(const LaunchArgs& a, int n_jobs, hipStream_t stream);
 hipError_t kernel_occupancy(int km, int rm, bool tail, bool photo, const LaunchArgs& a, int* blocks);
-hipError_t launch_contrast_fused(const FusedArgs& A, int grid, int threads, int lds_bytes, hipStream_t stream,
-                                 hipEvent_t start, hipEvent_t stop);
-hipError_t contrast_fused_occupancy(const FusedArgs& A, int threads, int lds_bytes, int* blocks);
 hipError_t set_kernel_lds_limit(int bytes);
 hipError_t launch_transpose(const void* src, void* dst, int64_t rows, int64_t cols, int element_size,
                             hipStream_t stream);
-hipError_t launch_rotate(const RotJob* jobs, int n_jobs, int max_tiles, int words, int cn, hipStream_t stream);
+hipError_t launch_rotate(const RotJob* jobs, int n_jobs, int max_tiles, int words, int cn, int32_t* error,
+                         hipStream_t stream);
 int        rot_box_words(int angle);
 hipError_t launch_expand(const ExpandJob* jobs, int n_jobs, int max_pixels, hipStream_t stream);
 hipError_t launch_nearest(const Mask16Job* jobs, int n_jobs, int max_h, int max_w, int max_seg_bytes, int max_slots, hipStream_t stream,
@@ -44,6 +42,8 @@ hipError_t launch_plan_records(const void* host_records, void* jobs, const PlanA
 void       jpeg_decode_batch(JpegState* S, int n, const void* const* data, const size_t* sizes,
                              const aeon_img_desc* descs, void* dst_base, hipStream_t stream);
 void       jpeg_info(const void* data, size_t size, int* w, int* h, int* ncomp);
+void       jpeg_entropy_only(const void* data, size_t size, int* w, int* h, int* ncomp, int64_t* n_blocks,
+                             int64_t* n_values, uint64_t* hash);
 void       png_header(const void* data, size_t size, int* w, int* h, int* depth, int* ctype);
 void       png_decode(const void* data, size_t size, int mode, void* dst, size_t stride, int* out_elem_bytes);
 } // namespace aeon_hip
@@ -60,6 +60,23 @@ struct aeon_error : std::runtime_error {
 };
 [[noreturn]] void fail(int code, const std::string& msg) { throw aeon_error(code, msg); }
 
+// The device error word's bits (kernels atomicOr them; aeon_hip_synchronize reports and clears).
+std::string device_error_text(int err)
+{
+    static const struct {
+        int         bit;
+        const char* what;
+    } bits[] = {{2, "LDS staging footprint exceeded"},
+                {4, "dynamic LDS not at address 0"},
+                {16, "hue table without a t1 channel"},
+                {32, "dynamic-tail counter left over by an earlier launch"},
+                {64, "rotation source box exceeds the launch's LDS"}};
+    std::string s;
+    for (const auto& b : bits)
+        if (err & b.bit) s += (s.empty() ? "" : "; ") + std::string(b.what);
+    return s.empty() ? "unknown" : s;
+}
+
 #define HIP_OK(expr)                                                                           \
     do {                                                                                       \
         hipError_t e_ = (expr);                                                                \
@@ -67,9 +84,9 @@ struct aeon_error : std::runtime_error {
     } while (0)
 
 constexpr int kMaxLds        = 160 * 1024;
-constexpr int kStageBudget   = 48 * 1024;   // preferred LDS bytes of the two staging buffers
+constexpr int kStageBudget   = 48 * 1024;   // preferred LDS bytes of the staging buffer
 constexpr int kStageBudgetHi = 140 * 1024;  // fallback for very wide crops
-constexpr size_t kUploadKernelMax = 128 * 1024; // job tables above this go up by SDMA (jobs_mode)
+constexpr size_t kUploadKernelMax = 128 * 1024; // job tables above this go up by SDMA (run_batch)
 
 // ---------------------------------------------------------------------------------------------
 // Per-image constants (aeon computes these on the host per record, too)
@@ -153,12 +170,11 @@ struct LaunchPlan {
     bool                tail  = false; // LINEAR jobs with OpenCV scalar-tail columns
     size_t              blob_off = 0;     // byte offset of this group's jobs in the slot blob
     std::vector<AugJob> jobs;
-    int                 tr = 1, stage_bytes = 0, max_win_w = 0, max_tiles = 0, buffers = 2;
+    int                 tr = 1, stage_bytes = 0, max_win_w = 0, max_tiles = 0;
     int                 lds = 0, threads = kBlockMax;
     bool                vec_ok = true;
     bool                has_hue = false, has_contrast = false;
     bool                rtab    = false; // final f32 launch with contrast / lighting: per-record LDS table
-    int                 force_threads = 0; // workgroup size imposed (the fused contrast launch)
 
     // launch shape for this->jobs, and each job's tile count
     void finalize()
@@ -193,21 +209,14 @@ struct LaunchPlan {
         // contrast pass 2 (photometric over the u8 intermediate, no resize): full workgroups
         // beat the fewest-idle-lanes choice (C3: 140 vs 158 us at 512 vs 448 lanes)
         if (rm == RESIZE_COPY && photo) threads = kBlockMax;
-        if (force_threads) threads = force_threads; // one launch with another plan's workgroups
-        if (const char* e = std::getenv("AEON_HIP_THREADS"))
-            threads = std::min(kBlockMax, std::max(kBlockMin, std::atoi(e) / 64 * 64));
         const int nph = threads / ncg;
         // one staging buffer and four rows per lane (a multiple of the row phases): the CU's other
         // workgroups cover a tile's staging latency.  Measured on C2/C3 against two buffers
         // (the next tile's loads in flight during the current tile's compute) at two rows per
         // lane: 42 vs 45 us (C2), 152/291 vs 186/370 us (C3 pass 2 / pass 1) -- the second
-        // buffer costs occupancy and halves the rows per tile.  Knobs for experiments only.
-        buffers    = 1;
-        if (const char* e = std::getenv("AEON_HIP_BUFFERS")) buffers = std::atoi(e) == 1 || rtab ? 1 : 2;
-        int tr_cap = std::min(64, std::max(1, (buffers == 1 ? 4 : 2) * nph));
-        int budget = kStageBudget;
-        if (const char* e = std::getenv("AEON_HIP_STAGE_KB")) budget = std::max(1, std::atoi(e)) * 1024;
-        if (const char* e = std::getenv("AEON_HIP_TR")) tr_cap = std::min(64, std::max(1, std::atoi(e)));
+        // buffer costs occupancy and halves the rows per tile (rejected).
+        const int tr_cap = std::min(64, std::max(1, 4 * nph));
+        int       budget = kStageBudget;
         bool hue = false, contrast = false;
         for (const J_& J : jobs) {
             hue |= (J.photo & PHOTO_HUE) != 0;
@@ -216,7 +225,6 @@ struct LaunchPlan {
         has_hue = hue, has_contrast = contrast;
         for (int pass = 0; pass < 2; pass++) {
             for (int t = tr_cap; t >= 1; t--) {
-                if (buffers == 2 && t > nph && t % nph) continue; // whole row sets (counted vmcnt waits)
                 // staged rows x whole 4-pixel groups, in whole DMA instructions (64 groups = 1 KiB
                 // for BGR, 64 gray pixels = 256 B)
                 long by = 0;
@@ -225,7 +233,7 @@ struct LaunchPlan {
                     by = std::max(by, J.cn == 3 ? (groups + 63) / 64 * 1024 : (groups * 4 + 63) / 64 * 256);
                 }
                 by = (by + 1023) / 1024 * 1024;
-                if (buffers * by <= budget || (t == 1 && pass == 1)) {
+                if (by <= budget || (t == 1 && pass == 1)) {
                     tr = t, stage_bytes = (int)by;
                     goto chosen;
                 }
@@ -233,7 +241,7 @@ struct LaunchPlan {
             budget = kStageBudgetHi;
         }
     chosen:
-        lds = lds_layout(max_win_w, tr, stage_bytes, photo && hue, buffers, rtab).total;
+        lds = lds_layout(max_win_w, tr, stage_bytes, photo && hue, rtab).total;
         if (lds > kMaxLds)
             fail(AEON_HIP_EUNSUPPORTED, "source crop too wide for LDS-staged row bands (" + std::to_string(lds) +
                                             " bytes)");
@@ -528,42 +536,14 @@ struct aeon_hip_ctx {
     // device planning (run_direct): calls whose records are one job each of one launch group
     // upload the caller's descriptors + params and let plan_records build the jobs on the GPU
     bool                 device_plan = true; // AEON_HIP_DEVICE_PLAN=0: always plan on the host
-    bool                 plan_async  = false; // AEON_HIP_PLAN_ASYNC=1: plan_records on copy_stream
     std::vector<JobGeom> geoms;              // reused per call
     JpegState*           jpeg = nullptr;     // JPEG decode stage (pool, staging ring), on first use
-    // overlap_contrast: a contrast batch runs as `overlap_chunks` chunks whose pass 2 (memory-bound)
-    // runs on side_stream beside the next chunk's pass 1 (VALU-bound), grids capped per CU
-    hipStream_t          side_stream    = nullptr;
-    hipEvent_t           join_event     = nullptr;
-    int                  overlap_chunks = 1, cap_pass1 = 2, cap_pass2 = 1; // off: measured slower
-    int                  caps_always = 0; // AEON_HIP_CAPS: apply cap_pass1/2 to every contrast call
-    bool                 tail_split     = false; // AEON_HIP_TAIL_SPLIT=1: measured slower
-    // contrast records' two passes in one launch (augment_contrast_fused, AEON_HIP_FUSED=1): measured
-    // slower than the pass-1 / reduce / pass-2 launches, so off.  fused_lag = records
-    // between a record's two passes in its task order.
-    int                  fused = 0, fused_lag = 256;
-    bool                 fused_reported = false;
     std::vector<int> open_slots; // used since the last completion event, on open_stream
     hipStream_t      open_stream = nullptr;
     // job tables go up on their own stream, so a call's H2D overlaps the previous call's kernels
     // instead of queueing between them on the caller's stream
     hipStream_t copy_stream = nullptr;
-    // job-table transport: 3 (default) = an upload kernel on the launch stream reads the pinned
-    // table over PCIe (kernel-to-kernel order, no cross-queue wait: 43.5 vs 44.2 us per C2
-    // step); 0 = SDMA H2D on copy_stream + cross-stream event (a ~6.6 us dispatch gap per
-    // step); 1 = H2D on the launch stream; 2 = kernels read the pinned table in place
-    // (AEON_HIP_JOBS for experiments).  -1 (default) = 3 for tables up to kUploadKernelMax,
-    // 0 above: the upload kernel reads PCIe at ~34 GB/s while an SDMA copy of a large table
-    // overlaps the previous call's kernels (C3, 512 KB: 347 vs 357 us per step; C2, 64 KB:
-    // the kernel wins)
-    int         jobs_mode = -1;
     int         n_cu      = 0;
-    int         wg_per_cu = 0; // AEON_HIP_WG_PER_CU: experiments only (0 = occupancy API)
-    int         l2_prefetch = 0; // AEON_HIP_L2_PREFETCH: warm L2 with the next tile's source rows (experiment)
-    int         info_ahead  = 1; // AEON_HIP_INFO_AHEAD=0: every wave derives each tile's geometry itself
-    int         head_split  = 0; // AEON_HIP_HEAD_SPLIT: first tile of each workgroup in two halves (experiment)
-    int         dyn_tail    = 3; // AEON_HIP_DYN_TAIL: 0 = static schedule; n = the last partial + (n-1) full rounds of tiles handed out by a counter
-    int         contig    = 0; // AEON_HIP_CONTIG: 1 = contiguous tile ranges for contrast pass 1, 2 = every launch
     std::vector<std::pair<std::vector<int>, int>> occ; // launch shape -> workgroups per CU
     // standardize LUTs stay resident per distinct output config (a new one is uploaded once)
     struct Lut {
@@ -684,12 +664,12 @@ double launch_bytes(const std::vector<J_>& jobs, int mode, size_t out_elem)
 }
 
 // Persistent grid: as many workgroups as the CUs hold at once, never more than the tiles.
-int grid_for(aeon_hip_ctx* ctx, int mode, const LaunchPlan& P, const LaunchArgs& a, int cap = 0)
+int grid_for(aeon_hip_ctx* ctx, int mode, const LaunchPlan& P, const LaunchArgs& a)
 {
-    int per_cu = ctx->wg_per_cu;
-    if (per_cu <= 0) {
+    int per_cu = 0;
+    {
         const std::vector<int> key = {mode, P.rm, (int)P.tail, (int)P.photo, a.threads, a.lds_bytes, a.vec_ok, a.has_rtab,
-                                      a.out_dtype, a.channel_major, a.stage_buffers};
+                                      a.out_dtype, a.channel_major};
         for (auto& e : ctx->occ)
             if (e.first == key) per_cu = e.second;
         if (per_cu <= 0) {
@@ -703,7 +683,6 @@ int grid_for(aeon_hip_ctx* ctx, int mode, const LaunchPlan& P, const LaunchArgs&
                              ctx->n_cu, a.total_tiles);
         }
     }
-    if (cap > 0) per_cu = std::min(per_cu, cap); // co-running launches share the CUs (overlap_contrast)
     return (int)std::min<long>((long)a.total_tiles, (long)per_cu * ctx->n_cu);
 }
 
@@ -732,31 +711,12 @@ KernelTimer take_timer(aeon_hip_ctx* ctx, int kind, double bytes)
     return t;
 }
 
-void timed_launch(aeon_hip_ctx* ctx, int mode, const LaunchPlan& P, const LaunchArgs& a_in, hipStream_t stream,
-                  double bytes, bool timed, int cap = 0)
+void timed_launch(aeon_hip_ctx* ctx, int mode, const LaunchPlan& P, const LaunchArgs& a, hipStream_t stream,
+                  double bytes, bool timed)
 {
     KernelTimer t{};
     if (timed) t = take_timer(ctx, mode, bytes);
-    LaunchArgs a    = a_in;
-    const int  grid = grid_for(ctx, mode, P, a, cap);
-    a.contig        = a.stage_buffers == 1 && ((ctx->contig == 1 && mode == KM_STATS) || ctx->contig == 2);
-    a.l2_prefetch   = ctx->l2_prefetch;
-    a.info_ahead    = ctx->info_ahead;
-    // Tail split (final launches): T tiles on a grid of G workgroups leave a last round of
-    // T mod G tiles on as many workgroups while the rest of the grid idles; cutting each of those
-    // tiles into floor(G / (T mod G)) row sub-tiles spreads the round over the whole grid.  (Not for
-    // the contrast statistics pass: its partial sums are indexed by whole tiles.)
-    a.split_base  = a.total_tiles;
-    a.split_parts = 1;
-    const int rem = a.total_tiles % grid;
-    if (mode == KM_FINAL && ctx->tail_split && rem > 0 && a.total_tiles > grid) {
-        const int parts = std::min(grid / rem, a.rows_per_tile);
-        if (parts > 1) {
-            a.split_base  = a.total_tiles - rem;
-            a.split_parts = parts;
-            a.total_tiles = a.split_base + rem * parts;
-        }
-    }
+    const int grid = grid_for(ctx, mode, P, a);
     HIP_OK(launch_tiles(mode, P.rm, P.tail, P.photo, a, grid, stream, timed ? t.start : nullptr,
                         timed ? t.stop : nullptr));
     if (timed) ctx->timers.push_back(t);
@@ -809,11 +769,11 @@ LaunchArgs launch_args(aeon_hip_ctx* ctx, const Slot& s, const uint8_t* table, c
                        const aeon_out_desc& o, const float* d_lut, int partial_stride, bool u8_map = false)
 {
     LaunchArgs a{};
-    a.head_split = ctx->head_split;
-    if (ctx->dyn_tail > 0) { // the slot's own counter: launches of calls in flight never share one
-        a.tail_ctr    = ctx->d_tail + (&s - ctx->slots);
-        a.tail_rounds = ctx->dyn_tail - 1;
-    }
+    // dynamic tail: the partial last round plus two full rounds before it drawn from a counter (one
+    // or four full rounds measured within noise or slower), the slot's own counter so
+    // launches of calls in flight never share one
+    a.tail_ctr    = ctx->d_tail + (&s - ctx->slots);
+    a.tail_rounds = 2;
     a.jobs           = (const AugJob*)(table + L.blob_off);
     a.lut            = d_lut; // [3][256]: standardized, or (float)x without mean
     a.hsv_tables     = ctx->d_hsv;
@@ -826,7 +786,6 @@ LaunchArgs launch_args(aeon_hip_ctx* ctx, const Slot& s, const uint8_t* table, c
     a.max_tiles     = L.max_tiles;
     a.total_tiles   = L.max_tiles * n_jobs;
     a.stage_bytes   = L.stage_bytes;
-    a.stage_buffers = L.buffers;
     a.max_win_w     = L.max_win_w;
     a.out_dtype     = o.dtype;
     a.u8_map        = u8_map;
@@ -908,13 +867,7 @@ bool run_direct(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void
     }
     phase(4);
     const PlanArgs pa{(uint64_t)src_base, (uint64_t)out_dev, o.item_stride, out_geom(o), n, is_mask ? 1 : 0, P.tr, 0};
-    if (ctx->plan_async) { // experiments: planned on the copy stream beside the previous call's kernels
-        HIP_OK(launch_plan_records(s.host_dev, s.dev, pa, ctx->copy_stream));
-        HIP_OK(hipEventRecord(s.copied, ctx->copy_stream));
-        HIP_OK(hipStreamWaitEvent(stream, s.copied, 0));
-    } else {
-        HIP_OK(launch_plan_records(s.host_dev, s.dev, pa, stream));
-    }
+    HIP_OK(launch_plan_records(s.host_dev, s.dev, pa, stream));
     phase(5);
     const bool timed = ctx->timing && (ctx->timing_calls++ % ctx->timing_every) == ctx->timing_every - 1;
     if (o.fixed_aspect_ratio) // std::fill_n of each item's canvas, its whole byte size (etl_image.cpp:263)
@@ -928,12 +881,9 @@ bool run_direct(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void
     return true;
 }
 
-// stream2 (optional): the final launches (contrast_reduce + KM_FINAL) go there after an event on
-// the caller's stream, with the pass-1 / final grids capped at cap1 / cap2 workgroups per CU, so
-// this call's pass 2 can run beside the next call's pass 1 (overlap_contrast).
 int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* src_base,
               const aeon_aug_params* params, const aeon_out_desc* out, void* out_dev, void* stream_,
-              bool is_mask, hipStream_t stream2 = nullptr, int cap1 = 0, int cap2 = 0)
+              bool is_mask)
 {
     if (!ctx || n < 0 || (n > 0 && (!descs || !params || !out || !out_dev || !src_base)))
         fail(AEON_HIP_EINVAL, "null argument");
@@ -972,7 +922,7 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
     };
     HIP_OK(hipSetDevice(ctx->device));
     phase(0);
-    if (ctx->device_plan && ctx->jobs_mode < 0 &&
+    if (ctx->device_plan &&
         run_direct(ctx, n, descs, src_base, params, od, out_dev, stream, is_mask, phase))
         return 0;
 
@@ -1044,29 +994,11 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
     }
     std::vector<int> slot_tiles(pass1_all.jobs.size(), 0);
     int              partial_stride = 1;
-    // both passes of the contrast records in one launch: every record a contrast record, one pass-1
-    // group (LINEAR, no scalar tail) and one pass-2 group (COPY with the record table), pass-2 job i
-    // reading stats slot i, and no second stream
-    LaunchPlan* f1 = nullptr;
-    LaunchPlan* f2 = nullptr;
-    {
-        int g1 = 0, g2 = 0;
-        for (LaunchPlan& P : pass1)
-            if (!P.jobs.empty()) g1++, f1 = &P;
-        for (LaunchPlan& P : main)
-            if (!P.jobs.empty()) g2++, f2 = &P;
-        bool ok = ctx->fused && !stream2 && g1 == 1 && g2 == 1 && f1->rm == RESIZE_LINEAR && !f1->tail &&
-                  f2->rm == RESIZE_COPY && f2->photo && o.dtype == AEON_DTYPE_F32 &&
-                  f1->jobs.size() == (size_t)n && f2->jobs.size() == (size_t)n;
-        for (int i = 0; ok && i < n; i++) ok = f2->jobs[i].stats_slot == i && f1->jobs[i].stats_slot == i;
-        if (!ok) f1 = f2 = nullptr;
-    }
     for (auto* v : {&pre, &pre2, &pass1, &main})
         for (LaunchPlan& P : *v) {
             if (P.jobs.empty()) continue;
             P.vec_ok = main_all.vec_ok;
             P.rtab   = v == &main && P.photo && o.dtype == AEON_DTYPE_F32;
-            if (&P == f2) P.force_threads = f1->threads;
             P.finalize();
             P.blob_off = blob;
             blob += P.jobs.size() * sizeof(AugJob);
@@ -1109,18 +1041,18 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
             if (!P.jobs.empty()) std::memcpy(s.host + P.blob_off, P.jobs.data(), P.jobs.size() * sizeof(AugJob));
         }
     phase(4);
+    // Job-table transport: tables up to kUploadKernelMax go up by a small kernel on the launch
+    // stream that reads the pinned slot over PCIe (kernel-to-kernel order, no cross-queue wait:
+    // 43.5 vs 44.2 us per C2 step against an SDMA copy + event, which costs a ~6.6 us dispatch gap);
+    // larger ones by SDMA on copy_stream, which overlaps the previous call's kernels while the
+    // upload kernel would read PCIe at ~34 GB/s (C3, 512 KB: 347 vs 357 us per step).
     const uint8_t* table = s.dev;
-    const int      jobs_mode = ctx->jobs_mode >= 0 ? ctx->jobs_mode : (blob > kUploadKernelMax ? 0 : 3);
-    if (jobs_mode == 0) {
+    if (blob > kUploadKernelMax) {
         HIP_OK(hipMemcpyAsync(s.dev, s.host, blob, hipMemcpyHostToDevice, ctx->copy_stream));
         HIP_OK(hipEventRecord(s.copied, ctx->copy_stream));
         HIP_OK(hipStreamWaitEvent(stream, s.copied, 0));
-    } else if (jobs_mode == 3) {
-        HIP_OK(launch_upload_table(s.host_dev, s.dev, blob, stream));
-    } else if (jobs_mode == 1) {
-        HIP_OK(hipMemcpyAsync(s.dev, s.host, blob, hipMemcpyHostToDevice, stream));
     } else {
-        table = s.host_dev;
+        HIP_OK(launch_upload_table(s.host_dev, s.dev, blob, stream));
     }
     phase(5);
 
@@ -1134,7 +1066,8 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
         HIP_OK(hipMemset2DAsync(out_dev, o.item_stride, 0,
                                 (size_t)o.canvas_w * o.canvas_h * o.channels * out_elem_bytes(od.dtype), n, stream));
     if (!rot.empty()) // image::rotate pre-pass first: the gather and tile passes read its output
-        HIP_OK(launch_rotate((const RotJob*)(table + rot_off), (int)rot.size(), rot_max_tiles, rot_words, rot_cn, stream));
+        HIP_OK(launch_rotate((const RotJob*)(table + rot_off), (int)rot.size(), rot_max_tiles, rot_words, rot_cn, ctx->d_error,
+                             stream));
     if (!exp.empty()) // then image::expand (etl_image.cpp:155-159)
         HIP_OK(launch_expand((const ExpandJob*)(table + exp_off), (int)exp.size(), exp_max_px, stream));
     if (!m16.empty()) {
@@ -1148,57 +1081,16 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
     for (auto* v : {&pre, &pre2})
         for (LaunchPlan& P : *v)
             if (!P.jobs.empty()) timed_launch(ctx, KM_RAW, P, args(P), stream, launch_bytes(P.jobs, KM_RAW, 1), timed);
-    if (f1) { // augment_contrast_fused: both passes, one launch
-        FusedArgs A{};
-        A.s = args(*f1), A.f = args(*f2);
-        A.s.split_base = A.s.total_tiles, A.s.split_parts = 1; // no tail split
-        A.f.split_base = A.f.total_tiles, A.f.split_parts = 1;
-        A.done  = (uint32_t*)s.shifts; // unused as shifts here: the per-record publish counters
-        A.n_rec = n;
-        A.lag   = std::min(n, ctx->fused_lag);
-        A.total = n * (A.s.max_tiles + A.f.max_tiles);
-        A.max_win_w     = std::max(f1->max_win_w, f2->max_win_w);
-        A.rows_per_tile = std::max(f1->tr, f2->tr);
-        A.stage_bytes   = std::max(f1->stage_bytes, f2->stage_bytes);
-        const LdsLayout FL = lds_layout(A.max_win_w, A.rows_per_tile, A.stage_bytes, true, 1, false);
-        const int lds = std::max(FL.total, FL.stage + f2->stage_bytes + 3 * 256 * 4); // + the record table
-        if (lds > kMaxLds) fail(AEON_HIP_EUNSUPPORTED, "fused contrast launch: LDS layout too large");
-        if (f1->threads != f2->threads) fail(AEON_HIP_ERUNTIME, "fused contrast launch: workgroup sizes differ");
-        int per_cu = 0;
-        HIP_OK(contrast_fused_occupancy(A, f1->threads, lds, &per_cu));
-        if (per_cu < 1) fail(AEON_HIP_ERUNTIME, "fused contrast launch does not fit a CU");
-        const int grid = std::min(A.total, per_cu * ctx->n_cu); // every workgroup resident (progress)
-        if (ctx->host_profile && !ctx->fused_reported) {
-            ctx->fused_reported = true;
-            std::fprintf(stderr, "[aeon_hip] fused contrast: %d threads, %d B LDS, TR %d/%d, %d workgroups/CU, %d tasks\n",
-                         f1->threads, lds, f1->tr, f2->tr, per_cu, A.total);
-        }
-        HIP_OK(hipMemsetAsync(A.done, 0, ((size_t)n * 4 + 15) & ~(size_t)15, stream));
-        KernelTimer t{};
-        if (timed) t = take_timer(ctx, KM_FINAL, launch_bytes(f1->jobs, KM_STATS, oelem) + launch_bytes(f2->jobs, KM_FINAL, oelem));
-        HIP_OK(launch_contrast_fused(A, grid, f1->threads, lds, stream, timed ? t.start : nullptr, timed ? t.stop : nullptr));
-        if (timed) ctx->timers.push_back(t);
-        phase(6);
-        release_slot(ctx, slot, stream);
-        phase(7);
-        return 0;
-    }
     for (LaunchPlan& P : pass1)
         if (!P.jobs.empty())
-            timed_launch(ctx, KM_STATS, P, args(P), stream, launch_bytes(P.jobs, KM_STATS, oelem), timed, cap1);
-    hipStream_t fs = stream;
-    if (stream2 && stream2 != stream) { // the final launches on stream2, after everything above
-        HIP_OK(hipEventRecord(s.copied, stream));
-        HIP_OK(hipStreamWaitEvent(stream2, s.copied, 0));
-        fs = stream2;
-    }
+            timed_launch(ctx, KM_STATS, P, args(P), stream, launch_bytes(P.jobs, KM_STATS, oelem), timed);
     for (LaunchPlan& P : main) {
         if (P.jobs.empty()) continue;
-        if (P.has_contrast) HIP_OK(launch_contrast_reduce(args(P), (int)P.jobs.size(), fs));
-        timed_launch(ctx, KM_FINAL, P, args(P), fs, launch_bytes(P.jobs, KM_FINAL, oelem), timed, cap2);
+        if (P.has_contrast) HIP_OK(launch_contrast_reduce(args(P), (int)P.jobs.size(), stream));
+        timed_launch(ctx, KM_FINAL, P, args(P), stream, launch_bytes(P.jobs, KM_FINAL, oelem), timed);
     }
     phase(6);
-    release_slot(ctx, slot, fs);
+    release_slot(ctx, slot, stream);
     phase(7);
     return 0;
 }
@@ -1284,28 +1176,10 @@ int aeon_hip_ctx_create(int device, aeon_hip_ctx** out)
             // the ring at the size a 512-record call needs (job tables of 128 KB), so steady-state
             // calls of that size never allocate
             ensure_ring(c, 128 * 1024, 64 * 1024, 8 * 1024);
-            HIP_OK(hipStreamCreateWithFlags(&c->side_stream, hipStreamNonBlocking));
-            HIP_OK(hipEventCreateWithFlags(&c->join_event, hipEventDisableTiming));
-            if (const char* e = std::getenv("AEON_HIP_OVERLAP_CHUNKS")) c->overlap_chunks = std::max(1, std::atoi(e));
-            if (const char* e = std::getenv("AEON_HIP_TAIL_SPLIT")) c->tail_split = std::atoi(e) != 0;
-            if (const char* e = std::getenv("AEON_HIP_PLAN_ASYNC")) c->plan_async = std::atoi(e) != 0;
-            if (const char* e = std::getenv("AEON_HIP_FUSED")) c->fused = std::atoi(e);
-            if (const char* e = std::getenv("AEON_HIP_FUSED_LAG")) c->fused_lag = std::max(1, std::atoi(e));
-            if (const char* e = std::getenv("AEON_HIP_CAP_PASS1")) c->cap_pass1 = std::max(0, std::atoi(e));
-            if (const char* e = std::getenv("AEON_HIP_CAPS")) c->caps_always = std::atoi(e) != 0;
-            if (const char* e = std::getenv("AEON_HIP_CAP_PASS2")) c->cap_pass2 = std::max(0, std::atoi(e));
+            // diagnostics: host time per phase (printed at destroy); the host planner for every call
             if (const char* e = std::getenv("AEON_HIP_HOST_PROFILE")) c->host_profile = std::atoi(e) != 0;
-            if (const char* e = std::getenv("AEON_HIP_JOBS")) c->jobs_mode = std::min(3, std::max(0, std::atoi(e)));
             if (const char* e = std::getenv("AEON_HIP_DEVICE_PLAN")) c->device_plan = std::atoi(e) != 0;
             HIP_OK(hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, device));
-            if (const char* e = std::getenv("AEON_HIP_WG_PER_CU")) c->wg_per_cu = std::atoi(e);
-            if (const char* e = std::getenv("AEON_HIP_CONTIG")) c->contig = std::atoi(e);
-            if (const char* e = std::getenv("AEON_HIP_L2_PREFETCH")) c->l2_prefetch = std::atoi(e);
-            if (const char* e = std::getenv("AEON_HIP_INFO_AHEAD")) c->info_ahead = std::atoi(e);
-            if (const char* e = std::getenv("AEON_HIP_DYN_TAIL")) c->dyn_tail = std::atoi(e);
-            if (const char* e = std::getenv("AEON_HIP_HEAD_SPLIT")) c->head_split = std::atoi(e);
-            if (const char* e = std::getenv("AEON_HIP_DONE_EVERY"))
-                c->done_every = std::min(aeon_hip_ctx::kSlots / 2, std::max(1, std::atoi(e)));
         } catch (...) {
             delete c;
             throw;
@@ -1353,8 +1227,6 @@ int aeon_hip_ctx_destroy(aeon_hip_ctx* c)
         for (auto* v : {&c->timers, &c->free_timers})
             for (KernelTimer& t : *v) (void)hipEventDestroy(t.start), (void)hipEventDestroy(t.stop);
         if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
-        if (c->side_stream) (void)hipStreamSynchronize(c->side_stream), (void)hipStreamDestroy(c->side_stream);
-        if (c->join_event) (void)hipEventDestroy(c->join_event);
         for (auto& L : c->luts) (void)hipFree(L.dev);
         if (c->d_error) (void)hipFree(c->d_error);
         if (c->d_tail) (void)hipFree(c->d_tail);
@@ -1389,29 +1261,7 @@ int aeon_hip_augment_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs,
                            const aeon_aug_params* params, const aeon_out_desc* out, void* out_dev,
                            void* stream)
 {
-    return guarded([&] {
-        // contrast batches: chunks whose pass 2 overlaps the next chunk's pass 1 (overlap_contrast)
-        int with_contrast = 0;
-        for (int i = 0; ctx && params && i < n; i++) with_contrast += params[i].contrast != 1.0f;
-        const int chunks = ctx ? std::min(ctx->overlap_chunks, n / 64) : 1;
-        if (chunks < 2 || with_contrast * 2 < n || !out || !descs || !out_dev) {
-            // AEON_HIP_CAPS (experiment): the pass grids capped per CU even without chunking, so
-            // consecutive calls on two caller streams can share the CUs
-            const bool caps = ctx && ctx->caps_always && with_contrast * 2 >= n;
-            return run_batch(ctx, n, descs, src_base, params, out, out_dev, stream, false, nullptr,
-                             caps ? ctx->cap_pass1 : 0, caps ? ctx->cap_pass2 : 0);
-        }
-        const int per = (n + chunks - 1) / chunks;
-        for (int a = 0; a < n; a += per)
-            run_batch(ctx, std::min(per, n - a), descs + a, src_base, params + a, out,
-                      (uint8_t*)out_dev + (size_t)a * out->item_stride, stream, false, ctx->side_stream,
-                      ctx->cap_pass1, ctx->cap_pass2);
-        // rejoin: everything of the call is ordered before later work on the caller's stream
-        std::lock_guard<std::mutex> lock(ctx->mu);
-        HIP_OK(hipEventRecord(ctx->join_event, ctx->side_stream));
-        HIP_OK(hipStreamWaitEvent((hipStream_t)stream, ctx->join_event, 0));
-        return 0;
-    });
+    return guarded([&] { return run_batch(ctx, n, descs, src_base, params, out, out_dev, stream, false); });
 }
 
 int aeon_hip_mask_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* src_base,
@@ -1441,9 +1291,7 @@ int aeon_hip_synchronize(aeon_hip_ctx* ctx, void* stream)
         HIP_OK(hipMemcpy(&err, ctx->d_error, sizeof(err), hipMemcpyDeviceToHost));
         if (err != 0) {
             HIP_OK(hipMemset(ctx->d_error, 0, sizeof(int32_t)));
-            fail(AEON_HIP_EDEVICE, "device error word " + std::to_string(err) +
-                                       ((err & 8) ? " (fused contrast launch: a pass-2 tile gave up waiting for pass 1)"
-                                                  : " (LDS staging footprint exceeded)"));
+            fail(AEON_HIP_EDEVICE, "device error word " + std::to_string(err) + " (" + device_error_text(err) + ")");
         }
         return 0;
     });
@@ -1591,6 +1439,17 @@ int aeon_jpeg_info(const void* data, size_t size, int* width, int* height, int* 
     return guarded([&] {
         if (!data || !width || !height || !components) fail(AEON_HIP_EINVAL, "null argument");
         jpeg_info(data, size, width, height, components);
+        return 0;
+    });
+}
+
+int aeon_jpeg_entropy_decode(const void* data, size_t size, int* width, int* height, int* components,
+                             int64_t* n_blocks, int64_t* n_values, uint64_t* hash)
+{
+    return guarded([&] {
+        if (!data || !width || !height || !components || !n_blocks || !n_values || !hash)
+            fail(AEON_HIP_EINVAL, "null argument");
+        jpeg_entropy_only(data, size, width, height, components, n_blocks, n_values, hash);
         return 0;
     });
 }

@@ -28,7 +28,7 @@ extern "C" {
 #define AEON_HIP_OK 0
 #define AEON_HIP_EINVAL -1     /* invalid argument / configuration (aeon: std::invalid_argument) */
 #define AEON_HIP_ERUNTIME -2   /* HIP runtime failure (aeon: std::runtime_error) */
-#define AEON_HIP_EUNSUPPORTED -3 /* a feature this build does not implement (e.g. rotation) */
+#define AEON_HIP_EUNSUPPORTED -3 /* input this build refuses (e.g. arithmetic-coded / 12-bit JPEG, CMYK) */
 #define AEON_HIP_EDEVICE -4    /* a kernel reported an inconsistency in its device error word */
 
 /* output element types (aeon output_type -> cv type, src/typemap.hpp:43-52); the loader converts the
@@ -147,18 +147,27 @@ int aeon_hip_transpose_batch(aeon_hip_ctx* ctx, const void* src_dev, void* dst_d
 /* ---- decode (image::extractor::extract, src/etl_image.cpp:83-99) ---------------------------- */
 /* JPEG frame header: width, height, component count (1 or 3).  Host only, no context needed. */
 int aeon_jpeg_info(const void* data, size_t size, int* width, int* height, int* components);
-/* cv::imdecode(CV_LOAD_IMAGE_COLOR / GRAYSCALE) of n JPEG files (baseline / extended sequential
- * Huffman, 8-bit, 1 or 3 components) as libjpeg decodes them (ISLOW IDCT, fancy upsampling),
+/* The host half of the JPEG stage alone (headers, Huffman tables, every scan's entropy decoding into
+ * the sparse coefficient stream aeon_hip_decode_jpeg_batch uploads), on the calling thread, no device:
+ * the stream's block / non-zero value counts and an FNV-1a hash of it.  For robustness tests of the
+ * untrusted-input parser (sanitizer builds, malformed-file corpora).  Same error codes as the batch
+ * decode. */
+int aeon_jpeg_entropy_decode(const void* data, size_t size, int* width, int* height, int* components,
+                             int64_t* n_blocks, int64_t* n_values, uint64_t* hash);
+/* cv::imdecode(CV_LOAD_IMAGE_COLOR / GRAYSCALE) of n JPEG files (baseline / extended sequential /
+ * progressive Huffman, 8-bit, 1 or 3 components) as libjpeg decodes them (ISLOW IDCT, fancy upsampling),
  * into device memory: record i as HWC uint8 (BGR if descs[i].channels == 3, the Y component if 1)
  * at dst_base + descs[i].offset with descs[i].stride bytes per row; descs[i].width/height must be
  * the file's (aeon_jpeg_info).  Huffman decoding runs on the context's host pool; the sparse
  * coefficients go up in one H2D and the IDCT / upsampling / colour conversion run as kernels on
  * `stream`.  The files may be released when the call returns; dst must stay valid until the stream
- * reaches the work.  Progressive / arithmetic / 12-bit / CMYK files: AEON_HIP_EUNSUPPORTED. */
+ * reaches the work.  Arithmetic-coded / lossless / 12-bit / CMYK files: AEON_HIP_EUNSUPPORTED. */
 int aeon_hip_decode_jpeg_batch(aeon_hip_ctx* ctx, int n, const void* const* data, const size_t* sizes,
                                const aeon_img_desc* descs, void* dst_base, void* stream);
 
-/* Wait for `stream` and check the device error word of ctx. */
+/* Wait for `stream` and check the device error word of ctx: AEON_HIP_EDEVICE (the word cleared) when a
+ * kernel flagged an inconsistency -- an LDS footprint the host sized too small, a dynamic-tail counter
+ * not reset by an earlier launch, a rotation source box over its LDS.  None is expected. */
 int aeon_hip_synchronize(aeon_hip_ctx* ctx, void* stream);
 
 /* ---- measurement ---------------------------------------------------------------------------- */

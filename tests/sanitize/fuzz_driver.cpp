@@ -1,0 +1,108 @@
+// fuzz_driver.cpp -- runs the host-side parsers of untrusted bytes over a corpus of files, for the
+// sanitizer build (aeon_amd/csrc/Makefile target `sanitize`: -fsanitize=address,undefined,
+// aeon's SANITIZER_TYPE builds, /root/reference/CMakeLists.txt:80-101).  No device is touched: the
+// JPEG entropy decoder (jpeg_host.cpp), the PNG decoder (png_host.cpp) and the JSON reader +
+// param_factory (json.hpp, param_factory.cpp) are called directly.
+//
+// Usage: fuzz_driver FILE...   (*.jpg, *.png, *.json).  One line per file: the outcome, "ok ..." or
+// "error <code> <message>"; a sanitizer finding aborts the run with a non-zero exit status.
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <iterator>
+#include <new>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../aeon_amd/csrc/jpeg.hpp"
+#include "../../aeon_amd/csrc/param_factory.hpp"
+#include "../../include/aeon_hip.h"
+
+namespace aeon_hip {
+void jpeg_info(const void* data, size_t size, int* w, int* h, int* ncomp);
+void jpeg_entropy_only(const void* data, size_t size, int* w, int* h, int* ncomp, int64_t* n_blocks,
+                       int64_t* n_values, uint64_t* hash);
+void png_header(const void* data, size_t size, int* w, int* h, int* depth, int* ctype);
+void png_decode(const void* data, size_t size, int mode, void* dst, size_t stride, int* out_elem_bytes);
+} // namespace aeon_hip
+
+using namespace aeon_hip;
+
+namespace {
+
+bool ends_with(const std::string& s, const char* suf)
+{
+    const size_t n = std::strlen(suf);
+    return s.size() >= n && s.compare(s.size() - n, n, suf) == 0;
+}
+
+std::string run_jpeg(const std::vector<uint8_t>& d)
+{
+    int w, h, n;
+    jpeg_info(d.data(), d.size(), &w, &h, &n);
+    int64_t  nb, nv;
+    uint64_t hv;
+    jpeg_entropy_only(d.data(), d.size(), &w, &h, &n, &nb, &nv, &hv);
+    char buf[128];
+    std::snprintf(buf, sizeof(buf), "ok %dx%dx%d blocks %lld values %lld", w, h, n, (long long)nb, (long long)nv);
+    return buf;
+}
+
+std::string run_png(const std::vector<uint8_t>& d)
+{
+    int w, h, depth, ctype;
+    png_header(d.data(), d.size(), &w, &h, &depth, &ctype);
+    if ((int64_t)w * h > (1 << 22)) return "ok header only (large)";
+    for (int mode = AEON_PNG_BGR8; mode <= AEON_PNG_ANYDEPTH; mode++) {
+        const size_t         stride = (size_t)w * (mode == AEON_PNG_BGR8 ? 3 : 1) * 2;
+        std::vector<uint8_t> dst(stride * h);
+        int                  eb = 0;
+        png_decode(d.data(), d.size(), mode, dst.data(), stride, &eb);
+    }
+    char buf[96];
+    std::snprintf(buf, sizeof(buf), "ok %dx%d depth %d type %d", w, h, depth, ctype);
+    return buf;
+}
+
+std::string run_json(const std::vector<uint8_t>& d)
+{
+    const Json    j = Json::parse(std::string(d.begin(), d.end()));
+    param_factory f(j);
+    std::minstd_rand0 eng(1);
+    const int sizes[][2] = {{256, 256}, {1, 1}, {640, 480}, {3, 4000}};
+    for (const auto& s : sizes) {
+        aeon_aug_params p{};
+        f.make_params(eng, s[0], s[1], 224, 224, &p);
+    }
+    return "ok";
+}
+
+} // namespace
+
+int main(int argc, char** argv)
+{
+    for (int i = 1; i < argc; i++) {
+        const std::string    name = argv[i];
+        std::ifstream        in(name, std::ios::binary);
+        std::vector<uint8_t> d((std::istreambuf_iterator<char>(in)), std::istreambuf_iterator<char>());
+        std::string          r;
+        try {
+            if (ends_with(name, ".jpg")) r = run_jpeg(d);
+            else if (ends_with(name, ".png")) r = run_png(d);
+            else if (ends_with(name, ".json")) r = run_json(d);
+            else r = "skipped";
+        } catch (const jpeg_error& e) {
+            r = "error " + std::to_string(e.code) + " " + e.what();
+        } catch (const std::invalid_argument& e) {
+            r = std::string("error -1 ") + e.what();
+        } catch (const std::bad_alloc&) {
+            r = "error -2 allocation";
+        } catch (const std::exception& e) {
+            r = std::string("error -2 ") + e.what();
+        }
+        std::printf("%s\t%s\n", name.c_str(), r.c_str());
+    }
+    return 0;
+}

@@ -1,0 +1,95 @@
+"""CPU: the host parsers of untrusted bytes under AddressSanitizer + UndefinedBehaviorSanitizer.
+
+`make -C aeon_amd/csrc sanitize` builds tests/sanitize/fuzz_driver.cpp with the JPEG entropy decoder,
+the PNG decoder and the JSON reader + param_factory (aeon's SANITIZER_TYPE builds,
+/root/reference/CMakeLists.txt:80-101); it runs over tests/sanitize/corpus.npz (1,749 truncated,
+bit-flipped, over-full-table, oversized and deeply nested inputs, tests/sanitize/make_corpus.py).
+Every input must end in a clean result or a refused-input error, with no sanitizer report; the
+product library (non-sanitized, through the C ABI) must give the same outcome per input.
+"""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import aeon_amd as A
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+DRIVER = os.path.join(ROOT, "aeon_amd", "csrc", "build_sanitize", "fuzz_driver")
+
+
+@pytest.fixture(scope="module")
+def corpus_run(tmp_path_factory):
+    clang = "/opt/rocm/llvm/bin/clang++"
+    if not os.path.exists(clang):
+        pytest.skip("no clang with sanitizer runtimes")
+    subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "aeon_amd", "csrc"), "sanitize"])
+    d = tmp_path_factory.mktemp("corpus")
+    corpus = np.load(os.path.join(ROOT, "tests", "sanitize", "corpus.npz"))
+    names = sorted(corpus.keys())
+    for k in names:
+        (d / k).write_bytes(corpus[k].tobytes())
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0:exitcode=86",
+               UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1:exitcode=87")
+    env.pop("LD_PRELOAD", None) if "asan" in env.get("LD_PRELOAD", "") else None
+    r = subprocess.run([DRIVER] + [str(d / k) for k in names], capture_output=True, text=True, env=env,
+                       timeout=600)
+    results = {}
+    for line in r.stdout.splitlines():
+        path, res = line.split("\t", 1)
+        results[os.path.basename(path)] = res
+    return r, results, corpus
+
+
+def test_corpus_runs_clean_under_asan_ubsan(corpus_run):
+    r, results, corpus = corpus_run
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "Sanitizer" not in r.stderr and "runtime error" not in r.stderr, r.stderr[-3000:]
+    assert set(results) == set(corpus.keys())
+    for k, res in results.items():
+        assert res.startswith("ok") or res.startswith("error -1 ") or res.startswith("error -3 "), (k, res)
+
+
+def test_corpus_expected_outcomes(corpus_run):
+    _, results, _ = corpus_run
+    for k, res in results.items():
+        if k.startswith("seed__"):
+            assert res.startswith("ok"), (k, res)
+        if "__dht_overfull" in k or "__dht_allones" in k:  # jdhuff.c's code-space check
+            assert res == "error -1 JPEG: bad Huffman table", (k, res)
+        if "__deep_" in k:
+            assert res == "error -1 json: nesting too deep", (k, res)
+        if k.endswith("__sos_len2_eof.jpg"):
+            assert res.startswith("error -1"), (k, res)
+    assert sum(r.startswith("ok") for r in results.values()) > 60  # mutations that still decode
+
+
+def test_product_library_agrees_with_sanitized_driver(corpus_run):
+    """The shipped library (aeon_jpeg_entropy_decode / aeon_png_info + aeon_decode_png through the C
+    ABI) on the same JPEG / PNG inputs: same accept / refuse decision and error code."""
+    _, results, corpus = corpus_run
+    checked = 0
+    for k in sorted(corpus.keys()):
+        data = corpus[k].tobytes()
+        want = results[k]
+        if k.endswith(".jpg"):
+            try:
+                w, h, n, nb, nv, _ = A.jpeg_entropy_decode(data)
+                got = f"ok {w}x{h}x{n} blocks {nb} values {nv}"
+            except A.AeonHipError as e:
+                got = f"error {e.code}"
+            assert got == want if got.startswith("ok") else want.startswith(got + " "), (k, got, want)
+            checked += 1
+        elif k.endswith(".png"):
+            try:
+                w, h, depth, ctype = A.png_info(data)
+                if w * h <= (1 << 22):
+                    for mode in (A.PNG_BGR8, A.PNG_GRAY8, A.PNG_ANYDEPTH):
+                        A.decode_png(data, mode)
+                got = "ok"
+            except A.AeonHipError as e:
+                got = f"error {e.code}"
+            assert want.startswith(got), (k, got, want)
+            checked += 1
+    assert checked > 1000
