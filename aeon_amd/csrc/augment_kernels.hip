@@ -68,6 +68,38 @@ __device__ __forceinline__ __attribute__((address_space(3))) T* lds_ptr(int byte
 }
 __device__ __forceinline__ float    lds_ldf(int byte_addr) { return *(const lds_f32*)(size_t)(uint32_t)byte_addr; }
 
+// The job of a tile.  AEON_HIP_LDSJOB (default): a copy of the AugJob in one of the workgroup's two
+// LDS job slots, brought in by one LDS-DMA a tile ahead, its fields read as uniform values
+// (ds_read + readfirstlane: no scalar-cache round trip at the head of a tile); otherwise the
+// launch's job table through constant-address scalar loads.
+#ifndef AEON_HIP_LDSJOB
+#define AEON_HIP_LDSJOB 1
+#endif
+struct JobRef {
+    cjob* c;   // the job in the launch's table
+    int   lds; // byte address of its LDS copy (AEON_HIP_LDSJOB)
+};
+template <typename T>
+__device__ __forceinline__ T job_get(const JobRef& J, int off)
+{
+    if constexpr (sizeof(T) == 8) {
+        const uint64_t lo = __builtin_amdgcn_readfirstlane(lds_ld(J.lds + off));
+        const uint64_t hi = __builtin_amdgcn_readfirstlane(lds_ld(J.lds + off + 4));
+        return __builtin_bit_cast(T, lo | (hi << 32));
+    } else {
+        return __builtin_bit_cast(T, (uint32_t)__builtin_amdgcn_readfirstlane(lds_ld(J.lds + off)));
+    }
+}
+#if AEON_HIP_LDSJOB
+#define JF(J, field) job_get<decltype(AugJob::field)>(J, (int)__builtin_offsetof(AugJob, field))
+#define JFA(J, field, i)                                                                                     \
+    job_get<__remove_extent(decltype(AugJob::field))>(J, (int)__builtin_offsetof(AugJob, field) +           \
+                                                             (int)sizeof(AugJob::field[0]) * (i))
+#else
+#define JF(J, field) ((J).c->field)
+#define JFA(J, field, i) ((J).c->field[i])
+#endif
+
 // ---- resize coefficients (OpenCV 2.4 resizeGeneric_ / resizeNN) -----------------------------
 // Taps are (sx, sx+1) and (r0, r1); a weight of 0 marks a single-tap column / row.
 struct XTap {
@@ -149,19 +181,19 @@ __device__ __forceinline__ uint32_t to_vgpr(uint32_t s)
 }
 // BS_FIXPT keeps the coefficients of B and G as int16 pairs, (q0, q1), (q3, q4), (q6, q7), for
 // v_dot2_i32_i16, and the R ones (q2, q5, q8) as plain words.
-__device__ __forceinline__ BsRegs bs_regs(cjob& J)
+__device__ __forceinline__ BsRegs bs_regs(const JobRef& J)
 {
     BsRegs R;
-    if (J.bs_kind == BS_FIXPT) {
+    if (JF(J, bs_kind) == BS_FIXPT) {
 #pragma unroll
         for (int i = 0; i < 3; i++) {
-            R.w[i]     = to_vgpr(((uint32_t)J.bsq[3 * i] & 0xffffu) | ((uint32_t)J.bsq[3 * i + 1] << 16));
-            R.w[3 + i] = to_vgpr((uint32_t)J.bsq[3 * i + 2]);
+            R.w[i]     = to_vgpr(((uint32_t)JFA(J, bsq, 3 * i) & 0xffffu) | ((uint32_t)JFA(J, bsq, 3 * i + 1) << 16));
+            R.w[3 + i] = to_vgpr((uint32_t)JFA(J, bsq, 3 * i + 2));
         }
         R.w[6] = R.w[7] = R.w[8] = 0;
     } else {
 #pragma unroll
-        for (int k = 0; k < 9; k++) R.w[k] = to_vgpr(__float_as_uint(J.bsm[k]));
+        for (int k = 0; k < 9; k++) R.w[k] = to_vgpr(__float_as_uint(JFA(J, bsm, k)));
     }
     return R;
 }
@@ -382,100 +414,112 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* p, in
 }
 
 struct StageGeom { // uniform: the staged source of one tile
-    int v_lo, nr, u_lo, nc, ng, pitch;
+    int v_lo, nr, u_lo, nc, ng, pitch; // rows [v_lo, v_lo + nr), columns [u_lo, u_lo + nc), pitch = 4 * ng
+    int rp, ipr;                       // LDS bytes per staged row, DMA instructions per staged row
 };
+
+// The LDS image of a tile's staged rows (stage_bytes_for, aug_job.hpp): row j at j * rp, each
+// row's units (BGR groups of 4 pixels as 16-byte slots, or gray pixels as words) in ipr whole
+// DMA instructions of 64 units, so a DMA instruction never straddles two source rows and its
+// lanes' source offsets are one row base + lane * unit bytes.
+__device__ __forceinline__ void stage_layout(int cn, StageGeom& G)
+{
+    const int upr = cn == 3 ? G.ng : G.pitch;
+    G.ipr         = (upr + 63) >> 6;
+    G.rp          = G.ipr * (cn == 3 ? 1024 : 256);
+}
+__device__ __forceinline__ int stage_need(const StageGeom& G) { return G.nr * G.rp; }
 
 // byte offset in the source buffer of staged pixel (row j, column u); negative above/left of a
 // padded crop
-__device__ __forceinline__ int src_off(cjob& J, const StageGeom& G, int j, int u)
+__device__ __forceinline__ int src_off(const JobRef& J, const StageGeom& G, int j, int u)
 {
-    return (J.crop_y + G.v_lo + J.shift_y + j) * J.src_stride + (J.crop_x + G.u_lo + J.shift_x + u) * J.cn;
+    return (JF(J, crop_y) + G.v_lo + JF(J, shift_y) + j) * JF(J, src_stride) + (JF(J, crop_x) + G.u_lo + JF(J, shift_x) + u) * JF(J, cn);
 }
 
-// Units (BGR groups or gray pixels) per staged row, and their count.
-__device__ __forceinline__ int stage_units_per_row(cjob& J, const StageGeom& G) { return J.cn == 3 ? G.ng : G.pitch; }
+// Units (BGR groups or gray pixels) per staged row.
+__device__ __forceinline__ int stage_units_per_row(const JobRef& J, const StageGeom& G) { return JF(J, cn) == 3 ? G.ng : G.pitch; }
 
-// (1) This wave's share of the tile's LDS-DMA loads: instructions wave, wave + nw, ...
-__device__ __forceinline__ void stage_issue(cjob& J, const StageGeom& G, int buf, int wave, int nw)
+// (1) This wave's share of the tile's LDS-DMA loads: instructions wave, wave + nw, ... of the
+// nr * ipr; instruction i = part s of row j (i = j * ipr + s) loads units s * 64 + lane.
+__device__ __forceinline__ void stage_issue(const JobRef& J, const StageGeom& G, int buf, int wave, int nw)
 {
-    const int   lane = threadIdx.x & 63;
-    const int   cn   = J.cn;
-    const auto  rsrc = uniform_rsrc((const void*)J.src_ptr, (int)J.src_bytes);
-    const int   upr  = stage_units_per_row(J, G);
-    const int   Q    = G.nr * upr;
-    const float inv  = 1.f / (float)upr;
-    for (int i = wave; i * 64 < Q; i += nw) {
-        const int q    = i * 64 + lane;
-        uint32_t  voff = kOutOfRange;
-        if (q < Q) {
-            const int j = (int)(((float)q + 0.5f) * inv); // exact in f32 for q < 2^20
-            const int b = src_off(J, G, j, (q - j * upr) * (cn == 3 ? 4 : 1));
-            voff        = b >= 0 ? (uint32_t)b : kOutOfRange; // (padded jobs: fixed in stage_unpack)
-        }
+    const int  lane = threadIdx.x & 63;
+    const int  cn   = JF(J, cn);
+    const auto rsrc = uniform_rsrc((const void*)JF(J, src_ptr), (int)JF(J, src_bytes));
+    const int  upr  = stage_units_per_row(J, G);
+    const int  ub   = cn == 3 ? 12 : 1;          // source bytes per unit
+    const int  row0 = src_off(J, G, 0, 0);        // (padded jobs: fixed in stage_unpack)
+    const int  rs   = JF(J, src_stride);
+    int        j = 0, sp = wave;                   // instruction wave = (row j, part sp)
+    while (sp >= G.ipr) sp -= G.ipr, j++;
+    for (int i = wave; i < G.nr * G.ipr; i += nw) {
+        const int u    = sp * 64 + lane;
+        const int b    = row0 + j * rs + u * ub;
+        const uint32_t voff = (u < upr && b >= 0) ? (uint32_t)b : kOutOfRange;
         if (cn == 3) lds_dma<12>(rsrc, buf + i * 1024, voff);
         else lds_dma<4>(rsrc, buf + i * 256, voff);
+        sp += nw;
+        while (sp >= G.ipr) sp -= G.ipr, j++;
     }
 }
 
 // (2) After this wave's loads landed: unpack its BGR slots in place; zero border of a padded job;
 // re-read loads that crossed the end of the buffer (rare; uniformly skipped otherwise for gray).
-__device__ __forceinline__ void stage_unpack(cjob& J, const StageGeom& G, int buf, int wave, int nw)
+__device__ __forceinline__ u32x4 unpack_bgr(u32x4 w) // 12 bytes BGR BGR BGR BGR -> four (B, G, R, 0) words
+{
+    return (u32x4){w.x & 0xffffffu, __builtin_amdgcn_perm(w.y, w.x, 0x0C050403u),
+                   __builtin_amdgcn_perm(w.z, w.y, 0x0C040302u), w.z >> 8};
+}
+__device__ __forceinline__ void stage_unpack(const JobRef& J, const StageGeom& G, int buf, int wave, int nw)
 {
     const int  lane      = threadIdx.x & 63;
-    const int  cn        = J.cn;
-    const int  src_bytes = (int)J.src_bytes;
-    const bool padded    = J.padded != 0;
+    const int  cn        = JF(J, cn);
+    const int  src_bytes = (int)JF(J, src_bytes);
+    const bool padded    = JF(J, padded) != 0;
     const bool at_end    = src_off(J, G, G.nr - 1, G.pitch) + 12 > src_bytes;
     if (cn != 3 && !padded && !at_end) return;
-    const int   upr = stage_units_per_row(J, G);
-    const int   Q   = G.nr * upr;
+    const int NI = G.nr * G.ipr; // DMA instructions of the tile
     if (cn == 3 && !padded && !at_end) {
-        // common case: in-place unpack of this wave's slots, reads of several instructions in
-        // flight before their writes
+        // common case: in-place unpack of every slot of this wave's instructions (slots past a
+        // row's units are never read), reads of several instructions in flight before their writes
         int i = wave;
-        for (; (i + 2 * nw) * 64 < Q; i += 3 * nw) {
+        for (; i + 2 * nw < NI; i += 3 * nw) {
             u32x4 w[3];
 #pragma unroll
             for (int k = 0; k < 3; k++) w[k] = *lds_ptr<const u32x4>(buf + ((i + k * nw) * 64 + lane) * 16);
 #pragma unroll
-            for (int k = 0; k < 3; k++) {
-                const int q = (i + k * nw) * 64 + lane;
-                if (q < Q)
-                    *lds_ptr<u32x4>(buf + q * 16) =
-                        (u32x4){w[k].x & 0xffffffu, __builtin_amdgcn_perm(w[k].y, w[k].x, 0x0C050403u),
-                                __builtin_amdgcn_perm(w[k].z, w[k].y, 0x0C040302u), w[k].z >> 8};
-            }
+            for (int k = 0; k < 3; k++) *lds_ptr<u32x4>(buf + ((i + k * nw) * 64 + lane) * 16) = unpack_bgr(w[k]);
         }
-        for (; i * 64 < Q; i += nw) {
-            const int q = i * 64 + lane;
-            if (q >= Q) continue;
-            const auto  slot = lds_ptr<u32x4>(buf + q * 16);
-            const u32x4 w    = *slot;
-            *slot = (u32x4){w.x & 0xffffffu, __builtin_amdgcn_perm(w.y, w.x, 0x0C050403u),
-                            __builtin_amdgcn_perm(w.z, w.y, 0x0C040302u), w.z >> 8};
+        for (; i < NI; i += nw) {
+            const auto slot = lds_ptr<u32x4>(buf + (i * 64 + lane) * 16);
+            *slot           = unpack_bgr(*slot);
         }
         return;
     }
-    const float inv = 1.f / (float)upr;
-    for (int i = wave; i * 64 < Q; i += nw) {
-        const int q = i * 64 + lane;
-        if (q >= Q) continue;
-        const int j  = (int)(((float)q + 0.5f) * inv);
-        const int u0 = (q - j * upr) * (cn == 3 ? 4 : 1); // first staged column of this unit
-        const int np = cn == 3 ? 4 : 1;                   // pixels of this unit
-        const int b  = src_off(J, G, j, u0);
+    const int upr = stage_units_per_row(J, G);
+    int       j = 0, sp = wave;
+    while (sp >= G.ipr) sp -= G.ipr, j++;
+    for (int i = wave; i < NI; i += nw) {
+        const int u  = sp * 64 + lane; // unit of this lane's slot
+        const int q  = i * 64 + lane;  // the slot
+        sp += nw;
+        const int jj = j;
+        while (sp >= G.ipr) sp -= G.ipr, j++;
+        if (u >= upr) continue;
+        const int u0 = u * (cn == 3 ? 4 : 1); // first staged column of this unit
+        const int np = cn == 3 ? 4 : 1;       // pixels of this unit
+        const int b  = src_off(J, G, jj, u0);
         const bool slow = padded || b < 0 || (at_end && b + (cn == 3 ? 12 : 4) > src_bytes);
         if (cn == 3 && !slow) {
             const auto slot = lds_ptr<u32x4>(buf + q * 16);
-            const u32x4 w   = *slot; // 12 bytes BGR BGR BGR BGR -> four (B, G, R, 0) words
-            *slot = (u32x4){w.x & 0xffffffu, __builtin_amdgcn_perm(w.y, w.x, 0x0C050403u),
-                            __builtin_amdgcn_perm(w.z, w.y, 0x0C040302u), w.z >> 8};
+            *slot           = unpack_bgr(*slot);
         } else if (slow) {
-            const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)J.src_ptr, (short)0, src_bytes, 0x00020000);
+            const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)JF(J, src_ptr), (short)0, src_bytes, 0x00020000);
             for (int k = 0; k < np; k++) {
-                const int cy = G.v_lo + j + J.shift_y, cx = G.u_lo + u0 + k + J.shift_x;
+                const int cy = G.v_lo + jj + JF(J, shift_y), cx = G.u_lo + u0 + k + JF(J, shift_x);
                 uint32_t  p  = 0;
-                if (!padded || (cy >= 0 && cy < J.crop_h && cx >= 0 && cx < J.crop_w)) {
+                if (!padded || (cy >= 0 && cy < JF(J, crop_h) && cx >= 0 && cx < JF(J, crop_w))) {
                     const int bb = b + k * cn;
                     if (bb >= 0)
                         for (int c = 0; c < cn; c++)
@@ -487,9 +531,9 @@ __device__ __forceinline__ void stage_unpack(cjob& J, const StageGeom& G, int bu
     }
 }
 
-// Pull the job descriptor of a future tile into L2 (an LDS-DMA into a sink nobody reads): its
-// scalar loads then hit L2 instead of paying an HBM round trip at the head of that tile.
-__device__ __forceinline__ void prefetch_job(const LaunchArgs& a, int t, int lds_sink)
+// The job descriptor of tile t into an LDS job slot (one 64-lane LDS-DMA of its 256 bytes): the
+// tile's copy with AEON_HIP_LDSJOB, otherwise an L2 warm-up for its scalar loads.
+__device__ __forceinline__ void fetch_job(const LaunchArgs& a, int t, int lds_sink)
 {
     if (t < 0 || t >= a.total_tiles) return;
     const int      job  = t / a.max_tiles;
@@ -520,6 +564,10 @@ __device__ __forceinline__ void lds_barrier()
     asm volatile("" ::: "memory");
 }
 
+// Lane -> output column mapping of the f32 CHW store path (Bands::compute): 1 = strided columns.
+#ifndef AEON_HIP_STRIDED
+#define AEON_HIP_STRIDED 0
+#endif
 // Output cache policy: streaming stores (written once, read by the consumer of the batch).
 #ifndef AEON_HIP_STORE_AUX
 #define AEON_HIP_STORE_AUX 2 // nt
@@ -643,35 +691,42 @@ struct Bands {
     struct Info {
         bool      ok;
         int       job, band, y0, nrows;
+        int       jl; // LDS byte address of the job's copy (AEON_HIP_LDSJOB)
         StageGeom G;
     };
-    __device__ __forceinline__ Info info(int t) const
+    __device__ __forceinline__ JobRef jref(const Info& f) const
+    {
+        return JobRef{&job_ref(a, f.job), f.jl};
+    }
+    // tile t -> Info; jl: the LDS slot holding the tile's job (AEON_HIP_LDSJOB)
+    __device__ __forceinline__ Info info(int t, int jl) const
     {
         Info f;
         f.ok   = false;
         f.job  = t / a.max_tiles;
         f.band = t - f.job * a.max_tiles;
-        cjob& J = job_ref(a, f.job);
-        if (f.band >= J.tiles) return f;
-        if (KM == KM_STATS && J.stats_slot < 0) return f;
+        f.jl   = jl;
+        const JobRef J = jref(f);
+        if (f.band >= JF(J, tiles)) return f;
+        if (KM == KM_STATS && JF(J, stats_slot) < 0) return f;
         const int TR = a.rows_per_tile;
         f.y0         = f.band * TR;
-        f.nrows      = min(TR, J.win_h - f.y0);
+        f.nrows      = min(TR, JF(J, win_h) - f.y0);
         if (f.nrows <= 0) return f;
         // source columns (taps are monotone in dx)
-        const XTap xf      = xcoef<RM>(J.win_x, J.scale_x, J.crop_w);
-        const XTap xl      = xcoef<RM>(J.win_x + J.win_w - 1, J.scale_x, J.crop_w);
+        const XTap xf      = xcoef<RM>(JF(J, win_x), JF(J, scale_x), JF(J, crop_w));
+        const XTap xl      = xcoef<RM>(JF(J, win_x) + JF(J, win_w) - 1, JF(J, scale_x), JF(J, crop_w));
         const int  two_tap = (RM == RESIZE_LINEAR || RM == RESIZE_AREA2X) ? 1 : 0;
         StageGeom& G       = f.G;
         G.u_lo  = xf.sx;
         G.nc    = xl.sx + two_tap - G.u_lo + 1;
         G.ng    = (G.nc + 3) >> 2;
         G.pitch = 4 * G.ng;
-        G.v_lo  = ycoef<RM>(J.win_y + f.y0, J.scale_y, J.crop_h).r0;
-        G.nr    = ycoef<RM>(J.win_y + f.y0 + f.nrows - 1, J.scale_y, J.crop_h).r1 - G.v_lo + 1;
-        // whole DMA instructions: 64 groups (1 KiB) or 64 gray pixels (256 B)
-        const int need = J.cn == 3 ? (G.nr * G.ng + 63) / 64 * 1024 : (G.nr * G.pitch + 63) / 64 * 256;
-        if (need > L.stage_bytes || J.win_w > a.max_win_w || f.nrows <= 0) {
+        G.v_lo  = ycoef<RM>(JF(J, win_y) + f.y0, JF(J, scale_y), JF(J, crop_h)).r0;
+        G.nr    = ycoef<RM>(JF(J, win_y) + f.y0 + f.nrows - 1, JF(J, scale_y), JF(J, crop_h)).r1 - G.v_lo + 1;
+        stage_layout(JF(J, cn), G);
+        const int need = stage_need(G);
+        if (need > L.stage_bytes || JF(J, win_w) > a.max_win_w || f.nrows <= 0) {
             if ((threadIdx.x & 63) == 0) atomicOr(a.error, 2); // (lane 0 of whichever wave derives it)
             return f;
         }
@@ -687,6 +742,7 @@ struct Bands {
         const auto p = lds_ptr<int32_t>(L.info);
         p[0] = f.ok, p[1] = f.job, p[2] = f.band, p[3] = f.y0, p[4] = f.nrows;
         p[5] = f.G.v_lo, p[6] = f.G.nr, p[7] = f.G.u_lo, p[8] = f.G.nc, p[9] = f.G.ng, p[10] = f.G.pitch;
+        p[11] = f.G.rp, p[12] = f.G.ipr, p[13] = f.jl;
     }
     __device__ __forceinline__ Info get_info() const
     {
@@ -695,35 +751,36 @@ struct Bands {
         Info       f;
         f.ok = rf(0) != 0, f.job = rf(1), f.band = rf(2), f.y0 = rf(3), f.nrows = rf(4);
         f.G.v_lo = rf(5), f.G.nr = rf(6), f.G.u_lo = rf(7), f.G.nc = rf(8), f.G.ng = rf(9), f.G.pitch = rf(10);
+        f.G.rp = rf(11), f.G.ipr = rf(12), f.jl = rf(13);
         return f;
     }
 
     // Issue the tile's LDS-DMA staging (loads in flight on return).
     __device__ __forceinline__ void issue(const Info& f) const
     {
-        if (f.ok) stage_issue(job_ref(a, f.job), f.G, L.stage, wave, nw);
+        if (f.ok) stage_issue(jref(f), f.G, L.stage, wave, nw);
     }
     // The tile's row taps; its column taps and hue table too unless the LDS still holds this
     // record's (build_xt / build_rec false: the workgroup's previous tile was of the same record).
     __device__ __forceinline__ void tables(const Info& f, bool build_xt, bool build_rec = true) const
     {
         if (!f.ok) return;
-        cjob&      J     = job_ref(a, f.job);
+        const JobRef J = jref(f);
         const StageGeom& G = f.G;
         const int  stage = L.stage;
         const int  tid = threadIdx.x, nt = blockDim.x;
         if (build_xt) {
             const auto xt = lds_ptr<i32x2>(L.xt);
-            for (int x = tid; x < J.win_w; x += nt) {
-                const XTap c = xcoef<RM>(J.win_x + x, J.scale_x, J.crop_w);
+            for (int x = tid; x < JF(J, win_w); x += nt) {
+                const XTap c = xcoef<RM>(JF(J, win_x) + x, JF(J, scale_x), JF(J, crop_w));
                 xt[x]        = (i32x2){c.sx - G.u_lo, (c.a0 & 0xffff) | (c.a1 << 16)};
             }
         }
-        if (PHOTO && KM != KM_RAW && a.has_hue && build_rec && J.cn == 3 && (J.photo & PHOTO_HUE)) {
+        if (PHOTO && KM != KM_RAW && a.has_hue && build_rec && JF(J, cn) == 3 && (JF(J, photo) & PHOTO_HUE)) {
             // the record's hue table (kHueTabBytes): cvtColor's H of h12, + hue, % 180 as uchar
             const int     tab = L.hsv + kHsvLdsDivBytes;
             const f32x4*  wt  = reinterpret_cast<const f32x4*>(a.hsv_tables + kHsvDivWords);
-            const int     hue = J.hue;
+            const int     hue = JF(J, hue);
             const bool    sp  = fast_photo(f);
             for (int i = tid; i < kHueTabEntries; i += nt) {
                 const int   h12 = i - 30;
@@ -747,47 +804,47 @@ struct Bands {
         }
         const auto yt = lds_ptr<i32x4>(L.yt);
         for (int r = tid; r < f.nrows; r += nt) {
-            const YTap y = ycoef<RM>(J.win_y + f.y0 + r, J.scale_y, J.crop_h);
-            yt[r]        = (i32x4){stage + (y.r0 - G.v_lo) * G.pitch * 4, stage + (y.r1 - G.v_lo) * G.pitch * 4, y.b0, y.b1};
+            const YTap y = ycoef<RM>(JF(J, win_y) + f.y0 + r, JF(J, scale_y), JF(J, crop_h));
+            yt[r]        = (i32x4){stage + (y.r0 - G.v_lo) * G.rp, stage + (y.r1 - G.v_lo) * G.rp, y.b0, y.b1};
         }
     }
 
     // The per-channel tail of the record's chain -- contrast -> lighting -> standardize, each a
     // function of one u8 channel value (image.cpp:336-346, 398-405, etl_image.cpp:316-339) -- as one
     // 3 x 256 f32 table in LDS for the tile's record, so the pixel loop does one lookup per channel.
-    __device__ __forceinline__ bool uses_rtab(cjob& J) const
+    __device__ __forceinline__ bool uses_rtab(const JobRef& J) const
     {
-        return KM == KM_FINAL && PHOTO && a.has_rtab && J.cn == 3 && (J.photo & (PHOTO_CONTRAST | PHOTO_LIGHTING));
+        return KM == KM_FINAL && PHOTO && a.has_rtab && JF(J, cn) == 3 && (JF(J, photo) & (PHOTO_CONTRAST | PHOTO_LIGHTING));
     }
     // lds_shifts: the record's (1-c)*mean per channel in LDS (null: from a.shifts, contrast_reduce's)
     __device__ __forceinline__ void record_table(const Info& f,
                                                  const __attribute__((address_space(3))) double* lds_shifts = nullptr) const
     {
         if (!f.ok) return;
-        cjob& J = job_ref(a, f.job);
+        const JobRef J = jref(f);
         if (!uses_rtab(J)) return;
-        const int photo = J.photo;
+        const int photo = JF(J, photo);
         double    sh[3] = {0, 0, 0};
         if ((photo & PHOTO_CONTRAST) && lds_shifts) {
             sh[0] = lds_shifts[0], sh[1] = lds_shifts[1], sh[2] = lds_shifts[2];
         } else if (photo & PHOTO_CONTRAST) {
-            const double* p = a.shifts + (size_t)J.stats_slot * 4;
+            const double* p = a.shifts + (size_t)JF(J, stats_slot) * 4;
             sh[0] = p[0], sh[1] = p[1], sh[2] = p[2];
         }
-        const float c = J.contrast, la = J.light_a;
+        const float c = JF(J, contrast), la = JF(J, light_a);
         const auto  rt = lds_ptr<float>(L.rtab);
         for (int i = threadIdx.x; i < 3 * 256; i += blockDim.x) {
             const int ch = i >> 8;
             int       y  = i & 255;
             if (photo & PHOTO_CONTRAST) y = u8rnd((float)((double)((float)y * c + 0.f) + sh[ch]));
-            if (photo & PHOTO_LIGHTING) y = sat_u8(u8rnd((float)y * la + 0.f) + J.light_add[ch]);
+            if (photo & PHOTO_LIGHTING) y = sat_u8(u8rnd((float)y * la + 0.f) + JFA(J, light_add, ch));
             rt[i] = lut_at(ch, y << 2);
         }
     }
 
     __device__ __forceinline__ void unpack(const Info& f) const
     {
-        if (f.ok) stage_unpack(job_ref(a, f.job), f.G, L.stage, wave, nw);
+        if (f.ok) stage_unpack(jref(f), f.G, L.stage, wave, nw);
     }
 
     // SPEC_BS_HUE: the tile's record is known (fast_photo) to be 3-channel, 4-pixel-aligned, with
@@ -799,9 +856,9 @@ struct Bands {
     __device__ __forceinline__ bool fast_photo(const Info& f) const
     {
         if (!kHasSpec || !f.ok) return false;
-        cjob& J = job_ref(a, f.job);
-        return J.cn == 3 && (J.photo & (PHOTO_BS | PHOTO_HUE)) == (PHOTO_BS | PHOTO_HUE) && J.bs_kind == BS_FIXPT &&
-               (J.win_w & 3) == 0;
+        const JobRef J = jref(f);
+        return JF(J, cn) == 3 && (JF(J, photo) & (PHOTO_BS | PHOTO_HUE)) == (PHOTO_BS | PHOTO_HUE) && JF(J, bs_kind) == BS_FIXPT &&
+               (JF(J, win_w) & 3) == 0;
     }
     __device__ __forceinline__ int compute_any(const Info& f) const
     {
@@ -818,20 +875,20 @@ struct Bands {
         if (!f.ok) return 0;
         constexpr bool SP = SPEC == SPEC_BS_HUE;
         const int  band = f.band, y0 = f.y0, nrows = f.nrows;
-        cjob&      J     = job_ref(a, f.job);
+        const JobRef J = jref(f);
         const int  tid   = threadIdx.x;
         const int  nt    = blockDim.x;
-        const int  cn    = SP ? 3 : J.cn;
-        const int  win_w = J.win_w;
+        const int  cn    = SP ? 3 : JF(J, cn);
+        const int  win_w = JF(J, win_w);
         const auto xt    = lds_ptr<const i32x2>(L.xt);
         const auto yt    = lds_ptr<const i32x4>(L.yt);
         const auto sdv   = lds_ptr<const i32x2>(L.hsv);
         const auto hdiv  = lds_ptr<const int32_t>(L.hsv + 256 * 8);
         // (a STATS tile's chain ends at the intermediate: only BS and HUE matter to it)
-        const int  photo = SP ? (PHOTO_BS | PHOTO_HUE) : (PHOTO && KM != KM_RAW && cn == 3) ? J.photo : 0;
+        const int  photo = SP ? (PHOTO_BS | PHOTO_HUE) : (PHOTO && KM != KM_RAW && cn == 3) ? JF(J, photo) : 0;
         double     sh0 = 0, sh1 = 0, sh2 = 0;
         if (KM == KM_FINAL && (photo & PHOTO_CONTRAST)) {
-            const double* sh = a.shifts + (size_t)J.stats_slot * 4;
+            const double* sh = a.shifts + (size_t)JF(J, stats_slot) * 4;
             sh0 = sh[0], sh1 = sh[1], sh2 = sh[2];
         }
         uint32_t sum0 = 0, sum1 = 0, sum2 = 0;
@@ -839,20 +896,21 @@ struct Bands {
         const auto htab8 = lds_ptr<const i32x2>(L.hsv + kHsvLdsDivBytes) + 30; // SPEC_BS_HUE form
         BsRegs   bsr{};
         int      bs_kind = 0;
-        if (PHOTO && (photo & PHOTO_BS)) bs_kind = SP ? (int)BS_FIXPT : J.bs_kind, bsr = bs_regs(J);
+        if (PHOTO && (photo & PHOTO_BS)) bs_kind = SP ? (int)BS_FIXPT : JF(J, bs_kind), bsr = bs_regs(J);
 
         const int  elem  = KM != KM_FINAL ? 1 : out_elem_bytes(a.out_dtype);
-        const int  plane = win_w * J.win_h;
-        const int  obytes = (KM == KM_FINAL ? J.out_plane : plane) * cn * elem;
-        const auto orsrc = __builtin_amdgcn_make_buffer_rsrc((void*)J.out_ptr, (short)0, obytes, 0x00020000);
-        const bool tail  = TAIL && RM == RESIZE_LINEAR && J.xv < J.dst_w * cn; // OpenCV scalar row tail
-        const int  wx0   = J.win_x;
-        const int  xv    = J.xv;
-        const int  flip  = J.flip;
+        const int  plane = win_w * JF(J, win_h);
+        const int  obytes = (KM == KM_FINAL ? JF(J, out_plane) : plane) * cn * elem;
+        const auto orsrc = __builtin_amdgcn_make_buffer_rsrc((void*)JF(J, out_ptr), (short)0, obytes, 0x00020000);
+        const bool tail  = TAIL && RM == RESIZE_LINEAR && JF(J, xv) < JF(J, dst_w) * cn; // OpenCV scalar row tail
+        const int  wx0   = JF(J, win_x);
+        const int  xv    = JF(J, xv);
+        const int  flip  = JF(J, flip);
         const int  bgr   = a.bgr_to_rgb && cn == 3;
         // Lane -> (column group, row phase), fixed for the tile
         const int  gpr    = (win_w + 3) >> 2;
         const bool full4  = SP || (win_w & 3) == 0; // every lane's group is 4 pixels of the window
+        constexpr bool kStrided = AEON_HIP_STRIDED && KM == KM_FINAL && OF == OF_F32_CHW_VEC;
         const int  ncg    = min(gpr, nt);
         const int  nph    = nt / ncg;
         const int  lph    = tid / ncg;
@@ -867,8 +925,14 @@ struct Bands {
         // uint8 standardize through the LUT
         auto u8_out = [&](int c, int v) { return a.u8_map ? (int)lut_of(c, v) : u8_of(v); };
 
+        // A lane's four output columns: ox0 + k * cst.  Contiguous (cst 1: one 16-byte store per
+        // channel plane), or, with AEON_HIP_STRIDED on the f32 CHW path, strided by a quarter of the
+        // window (cst = gpr): then the lanes of one LDS read gather consecutive output columns, i.e.
+        // source pixels ~scale words apart (conflict-free banks) instead of ~4 * scale (a 4-way
+        // conflict per read), and each channel plane takes four coalesced 4-byte stores.
+        const int cst = (kStrided && full4) ? gpr : 1;
         for (int cg = active ? lcg : gpr; cg < gpr; cg += ncg) {
-            const int ox0 = cg * 4;
+            const int ox0 = cst == 1 ? cg * 4 : cg;
             const int nk  = SP ? 4 : min(4, win_w - ox0);
             int       col[4];
             uint32_t  wxk[4];
@@ -876,7 +940,7 @@ struct Bands {
 #pragma unroll
             for (int k = 0; k < 4; k++) {
                 // columns past the window edge recompute the last one (never stored)
-                const int  ox  = min(ox0 + k, win_w - 1);
+                const int  ox  = min(ox0 + k * cst, win_w - 1);
                 const int  x   = flip ? win_w - 1 - ox : ox;
                 const i32x2 xtt = xt[x];
                 col[k]         = xtt.x * 4; // byte offset in a staged row
@@ -960,16 +1024,16 @@ struct Bands {
                             continue;
                         }
                         if (photo & PHOTO_CONTRAST) {
-                            const float c = J.contrast;
+                            const float c = JF(J, contrast);
                             bb = u8rnd((float)((double)((float)bb * c + 0.f) + sh0));
                             gg = u8rnd((float)((double)((float)gg * c + 0.f) + sh1));
                             rr = u8rnd((float)((double)((float)rr * c + 0.f) + sh2));
                         }
                         if (photo & PHOTO_LIGHTING) {
-                            const float la = J.light_a;
-                            bb = sat_u8(u8rnd((float)bb * la + 0.f) + J.light_add[0]);
-                            gg = sat_u8(u8rnd((float)gg * la + 0.f) + J.light_add[1]);
-                            rr = sat_u8(u8rnd((float)rr * la + 0.f) + J.light_add[2]);
+                            const float la = JF(J, light_a);
+                            bb = sat_u8(u8rnd((float)bb * la + 0.f) + JFA(J, light_add, 0));
+                            gg = sat_u8(u8rnd((float)gg * la + 0.f) + JFA(J, light_add, 1));
+                            rr = sat_u8(u8rnd((float)rr * la + 0.f) + JFA(J, light_add, 2));
                         }
                         val[k][0] = bb, val[k][1] = gg, val[k][2] = rr;
                         __builtin_amdgcn_sched_barrier(0); // one pixel's chain live at a time
@@ -1002,6 +1066,19 @@ struct Bands {
                 }
                 // image::loader::load: source channel c goes to output channel oc (mixChannels
                 // from_to {0,2,1,1,2,0} when bgr_to_rgb); the LUT is indexed by source channel
+                if (OF == OF_F32_CHW_VEC && cst != 1) {
+                    const int idx = y * win_w + ox0;
+#pragma unroll
+                    for (int c = 0; c < 3; c++) {
+                        const int oc = bgr ? 2 - c : c;
+#pragma unroll
+                        for (int k = 0; k < 4; k++)
+                            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(lut_of(c, val[k][c])), orsrc,
+                                                                  (oc * plane + idx + k * cst) * 4, 0, kStoreAux);
+                        __builtin_amdgcn_sched_barrier(0);
+                    }
+                    continue;
+                }
                 if (OF == OF_F32_CHW_VEC) {
                     const int idx = y * win_w + ox0;
 #pragma unroll
@@ -1025,7 +1102,7 @@ struct Bands {
                     for (int c = 0; c < 3; c++) {
                         if (c >= cn) break;
                         const int oc = bgr ? 2 - c : c;
-                        const int i0 = (cn == 1 ? 0 : oc * J.out_plane) + y * J.out_pitch + ox0;
+                        const int i0 = (cn == 1 ? 0 : oc * JF(J, out_plane)) + y * JF(J, out_pitch) + ox0;
                         const uint32_t w = ((uint32_t)u8_out(c, val[0][c]) & 0xff) | (((uint32_t)u8_out(c, val[1][c]) & 0xff) << 8) |
                                            (((uint32_t)u8_out(c, val[2][c]) & 0xff) << 16) | ((uint32_t)u8_out(c, val[3][c]) << 24);
                         if ((i0 & 3) == 0) {
@@ -1045,8 +1122,8 @@ struct Bands {
 #pragma unroll
                     for (int k = 0; k < 4; k++) {
                         if (k >= nk) break;
-                        const int i = a.channel_major ? oc * J.out_plane + y * J.out_pitch + ox0 + k
-                                                      : (y * J.out_pitch + ox0 + k) * cn + oc;
+                        const int i = a.channel_major ? oc * JF(J, out_plane) + y * JF(J, out_pitch) + ox0 + k
+                                                      : (y * JF(J, out_pitch) + ox0 + k) * cn + oc;
                         // image::loader (convert_mix_channels: Mat::convertTo of the uint8 record,
                         // saturating; standardize for float / double)
                         const int v = u8_of(val[k][c]);
@@ -1087,7 +1164,7 @@ struct Bands {
         if (KM == KM_STATS) { // exact per-(tile, wave) sums; unused wave slots are zeroed
             sum0 = wave_sum(sum0), sum1 = wave_sum(sum1), sum2 = wave_sum(sum2);
             const int lane = tid & 63;
-            uint32_t* p    = a.partials + ((size_t)J.stats_slot * a.partial_stride + (size_t)band * 8) * 4;
+            uint32_t* p    = a.partials + ((size_t)JF(J, stats_slot) * a.partial_stride + (size_t)band * 8) * 4;
             auto put = [&](uint32_t* q, uint32_t v) { *q = v; };
             if (lane == 0) put(p + wave * 4 + 0, sum0), put(p + wave * 4 + 1, sum1), put(p + wave * 4 + 2, sum2);
             if (wave == 0 && lane >= nw && lane < 8) put(p + lane * 4 + 0, 0), put(p + lane * 4 + 1, 0), put(p + lane * 4 + 2, 0);
@@ -1175,16 +1252,23 @@ void augment_tiles(LaunchArgs a)
         t    = draw();
         live = t >= 0;
     }
-    Info f = W.info(live ? t : 0);
+    int js = 0; // LDS job slot of the current tile
+    if (wave == 0) fetch_job(a, live ? t : -1, L.job);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    Info f{};
+    if (live) f = W.info(t, L.job);
     for (int it = 0; live; it++) {
-        // the staging phases (job loads, LDS-DMA issue, tap tables, unpack) at a raised wave
-        // priority: they are this workgroup's critical path while the CU's other workgroups
-        // stream stores (measured 38.8 -> 37.7 us on C2); the VALU-bound contrast pass 1 prefers
-        // the reverse (293 -> 283 us on C3)
+        // the staging phases (LDS-DMA issue, tap tables, unpack) at a raised wave priority: they
+        // are this workgroup's critical path while the CU's other workgroups stream stores
+        // (measured 38.8 -> 37.7 us on C2); the VALU-bound contrast pass 1 prefers the reverse
+        // (293 -> 283 us on C3)
         __builtin_amdgcn_s_setprio(KM == KM_STATS ? kComputePrio : kStagePrio);
         stamp(it, 0);
         const bool more = t + G < t_dyn; // a static next tile
-        if (wave == 0) prefetch_job(a, more ? t + G : -1, L.pf);
+        const int  jn   = L.job + (js ^ 1) * (int)sizeof(AugJob); // the next tile's job slot
+        if (wave == 0) fetch_job(a, more ? t + G : -1, jn);
+        stamp(it, 1);
         W.issue(f);
         stamp(it, 2);
         const bool same = f.ok && f.job == prev_job; // the LDS tables still hold this record's
@@ -1201,18 +1285,25 @@ void augment_tiles(LaunchArgs a)
         __builtin_amdgcn_s_setprio(KM == KM_STATS ? kStagePrio : kComputePrio);
         // the next static tile's geometry: derived by one wave (its f64 tap bounds are uniform work
         // every wave would otherwise repeat) during the compute, handed over through LDS
-        if (more && wave == nw - 1) W.put_info(W.info(t + G));
+        if (more && wave == nw - 1) W.put_info(W.info(t + G, jn));
         W.compute_any(f);
         stamp(it, 7);
         lds_barrier(); // everyone is done reading the buffer before it is refilled
         stamp(it, 8);
+        js ^= 1;
         if (more) {
             f = W.get_info();
             t += G;
         } else if (t_tail) {
             t    = draw();
             live = t >= 0;
-            if (live) f = W.info(t);
+            if (live) {
+                const int jl = L.job + js * (int)sizeof(AugJob);
+                if (wave == 0) fetch_job(a, t, jl);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __syncthreads();
+                f = W.info(t, jl);
+            }
         } else {
             break;
         }

@@ -225,13 +225,9 @@ struct LaunchPlan {
         has_hue = hue, has_contrast = contrast;
         for (int pass = 0; pass < 2; pass++) {
             for (int t = tr_cap; t >= 1; t--) {
-                // staged rows x whole 4-pixel groups, in whole DMA instructions (64 groups = 1 KiB
-                // for BGR, 64 gray pixels = 256 B)
+                // staged rows, each in whole DMA instructions (stage_bytes_for)
                 long by = 0;
-                for (const J_& J : jobs) {
-                    const long groups = (long)stage_rows_for(J, t) * ((stage_cols(J) + 3) / 4);
-                    by = std::max(by, J.cn == 3 ? (groups + 63) / 64 * 1024 : (groups * 4 + 63) / 64 * 256);
-                }
+                for (const J_& J : jobs) by = std::max(by, stage_bytes_for(J.cn, stage_rows_for(J, t), stage_cols(J)));
                 by = (by + 1023) / 1024 * 1024;
                 if (by <= budget || (t == 1 && pass == 1)) {
                     tr = t, stage_bytes = (int)by;
