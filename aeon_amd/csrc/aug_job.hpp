@@ -92,7 +92,8 @@ struct alignas(16) ExpandJob {
 
 // Per-launch uniform arguments.
 struct LaunchArgs {
-    const AugJob*  jobs;
+    const AugJob*  jobs;       // the launch's jobs: device memory, or the device view of a pinned host slot
+    int32_t        jobs_host;  // jobs is pinned host memory (read through to the host)
     const float*   lut;        // [3][256] per SOURCE channel: standardized value of output
                                // channel (bgr_to_rgb ? 2-c : c), or (float)x without mean
     const int32_t* hsv_tables; // sdiv[256], hdiv180[256], then per uchar H the HSV2RGB weights (B, G, R, 0) as float bits
@@ -148,14 +149,13 @@ constexpr int kHueTabBytes   = 184 * 16;
 #define AEON_HD
 #endif
 
-// LDS bytes of a staged source of `rows` rows x `cols` columns (augment_kernels.hip stage_layout):
-// every row in whole 64-unit DMA instructions -- BGR groups of 4 pixels as 16-byte slots (1 KiB per
-// instruction), or gray pixels as words (256 B per instruction).
+// LDS bytes of a staged source of `rows` rows x `cols` columns (augment_kernels.hip stage_need): the
+// rows' units back to back in whole 64-unit DMA instructions -- BGR groups of 4 pixels as 16-byte
+// slots (1 KiB per instruction), or gray pixels as words (256 B per instruction).
 AEON_HD inline long stage_bytes_for(int cn, int rows, int cols)
 {
-    const long groups = (cols + 3) / 4;
-    const long upr    = cn == 3 ? groups : 4 * groups;
-    return (long)rows * ((upr + 63) / 64) * (cn == 3 ? 1024 : 256);
+    const long groups = (long)rows * ((cols + 3) / 4);
+    return cn == 3 ? (groups + 63) / 64 * 1024 : (groups * 4 + 63) / 64 * 256;
 }
 
 // LDS carve of one workgroup (bytes; every region 16-byte aligned, see the CDNA guide G17).
@@ -173,7 +173,7 @@ AEON_HD inline LdsLayout lds_layout(int max_win_w, int rows_per_tile, int stage_
     L.rtab = o; o += rtab ? 3 * 256 * 4 : 0;                 // the tile's record table (f32, source channel order)
     L.xt  = o; o += ((max_win_w * 8 + 15) / 16) * 16; // per-column taps + weights
     L.yt  = o; o += rows_per_tile * 16;               // per-row taps + weights
-    L.job = o; o += 2 * (int)sizeof(AugJob);                 // the current and next tiles' jobs (LDS-DMA copies)
+    L.job = o; o += 3 * (int)sizeof(AugJob);                 // a ring of three tiles' jobs (LDS-DMA copies)
     L.info = o; o += 64;                                     // the next tile's geometry (one wave computes it)
     L.stage_bytes = stage_bytes;                             // source pixels, 4 B each (B,G,R,x)
     L.stage = o; o += stage_bytes;

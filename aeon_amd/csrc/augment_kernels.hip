@@ -68,37 +68,29 @@ __device__ __forceinline__ __attribute__((address_space(3))) T* lds_ptr(int byte
 }
 __device__ __forceinline__ float    lds_ldf(int byte_addr) { return *(const lds_f32*)(size_t)(uint32_t)byte_addr; }
 
-// The job of a tile.  AEON_HIP_LDSJOB (default): a copy of the AugJob in one of the workgroup's two
-// LDS job slots, brought in by one LDS-DMA a tile ahead, its fields read as uniform values
-// (ds_read + readfirstlane: no scalar-cache round trip at the head of a tile); otherwise the
-// launch's job table through constant-address scalar loads.
-#ifndef AEON_HIP_LDSJOB
-#define AEON_HIP_LDSJOB 1
-#endif
+// The job of a tile: a copy of its AugJob in one of the workgroup's two LDS job slots, brought in
+// by one LDS-DMA a tile ahead (from the device job table, or straight from the caller's pinned
+// slot over PCIe for single-pass calls: no planner or upload launch), its fields read as uniform
+// values (ds_read + readfirstlane).  Measured equal to constant-address scalar loads of a device
+// table (C2 39.9-40.6 vs 40.1-40.4 us), and it is what lets the job table live in host memory.
 struct JobRef {
-    cjob* c;   // the job in the launch's table
-    int   lds; // byte address of its LDS copy (AEON_HIP_LDSJOB)
+    int lds; // byte address of the LDS copy
 };
 template <typename T>
 __device__ __forceinline__ T job_get(const JobRef& J, int off)
 {
     if constexpr (sizeof(T) == 8) {
-        const uint64_t lo = __builtin_amdgcn_readfirstlane(lds_ld(J.lds + off));
-        const uint64_t hi = __builtin_amdgcn_readfirstlane(lds_ld(J.lds + off + 4));
+        const uint64_t lo = (uint32_t)__builtin_amdgcn_readfirstlane(lds_ld(J.lds + off));
+        const uint64_t hi = (uint32_t)__builtin_amdgcn_readfirstlane(lds_ld(J.lds + off + 4));
         return __builtin_bit_cast(T, lo | (hi << 32));
     } else {
         return __builtin_bit_cast(T, (uint32_t)__builtin_amdgcn_readfirstlane(lds_ld(J.lds + off)));
     }
 }
-#if AEON_HIP_LDSJOB
 #define JF(J, field) job_get<decltype(AugJob::field)>(J, (int)__builtin_offsetof(AugJob, field))
 #define JFA(J, field, i)                                                                                     \
     job_get<__remove_extent(decltype(AugJob::field))>(J, (int)__builtin_offsetof(AugJob, field) +           \
                                                              (int)sizeof(AugJob::field[0]) * (i))
-#else
-#define JF(J, field) ((J).c->field)
-#define JFA(J, field, i) ((J).c->field[i])
-#endif
 
 // ---- resize coefficients (OpenCV 2.4 resizeGeneric_ / resizeNN) -----------------------------
 // Taps are (sx, sx+1) and (r0, r1); a weight of 0 marks a single-tap column / row.
@@ -415,20 +407,20 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* p, in
 
 struct StageGeom { // uniform: the staged source of one tile
     int v_lo, nr, u_lo, nc, ng, pitch; // rows [v_lo, v_lo + nr), columns [u_lo, u_lo + nc), pitch = 4 * ng
-    int rp, ipr;                       // LDS bytes per staged row, DMA instructions per staged row
+    int rp;                            // LDS bytes per staged row
 };
 
-// The LDS image of a tile's staged rows (stage_bytes_for, aug_job.hpp): row j at j * rp, each
-// row's units (BGR groups of 4 pixels as 16-byte slots, or gray pixels as words) in ipr whole
-// DMA instructions of 64 units, so a DMA instruction never straddles two source rows and its
-// lanes' source offsets are one row base + lane * unit bytes.
-__device__ __forceinline__ void stage_layout(int cn, StageGeom& G)
+// The LDS image of a tile's staged rows (stage_bytes_for, aug_job.hpp): the rows' units (BGR groups
+// of 4 pixels as 16-byte slots, or gray pixels as words) back to back, rp = 16 * ng bytes per row,
+// loaded by whole 64-unit DMA instructions.  (Row-aligned instructions -- every row in its own whole
+// instructions, so a lane's source offset is a row base + lane * unit bytes -- measured slower: a
+// 256-wide crop needs 65 groups per row, i.e. two instructions, and the doubled LDS cuts C2's
+// rows per tile from 32 to 19: 46.3 vs 40.1 us.)
+__device__ __forceinline__ void stage_layout(int cn, StageGeom& G) { G.rp = G.pitch * 4; }
+__device__ __forceinline__ int stage_need(const StageGeom& G, int cn)
 {
-    const int upr = cn == 3 ? G.ng : G.pitch;
-    G.ipr         = (upr + 63) >> 6;
-    G.rp          = G.ipr * (cn == 3 ? 1024 : 256);
+    return cn == 3 ? (G.nr * G.ng + 63) / 64 * 1024 : (G.nr * G.pitch + 63) / 64 * 256;
 }
-__device__ __forceinline__ int stage_need(const StageGeom& G) { return G.nr * G.rp; }
 
 // byte offset in the source buffer of staged pixel (row j, column u); negative above/left of a
 // padded crop
@@ -440,27 +432,29 @@ __device__ __forceinline__ int src_off(const JobRef& J, const StageGeom& G, int 
 // Units (BGR groups or gray pixels) per staged row.
 __device__ __forceinline__ int stage_units_per_row(const JobRef& J, const StageGeom& G) { return JF(J, cn) == 3 ? G.ng : G.pitch; }
 
-// (1) This wave's share of the tile's LDS-DMA loads: instructions wave, wave + nw, ... of the
-// nr * ipr; instruction i = part s of row j (i = j * ipr + s) loads units s * 64 + lane.
+// (1) This wave's share of the tile's LDS-DMA loads: instructions wave, wave + nw, ...; unit q of
+// the tile (row q / upr) lands in slot q.
 __device__ __forceinline__ void stage_issue(const JobRef& J, const StageGeom& G, int buf, int wave, int nw)
 {
-    const int  lane = threadIdx.x & 63;
-    const int  cn   = JF(J, cn);
-    const auto rsrc = uniform_rsrc((const void*)JF(J, src_ptr), (int)JF(J, src_bytes));
-    const int  upr  = stage_units_per_row(J, G);
-    const int  ub   = cn == 3 ? 12 : 1;          // source bytes per unit
-    const int  row0 = src_off(J, G, 0, 0);        // (padded jobs: fixed in stage_unpack)
-    const int  rs   = JF(J, src_stride);
-    int        j = 0, sp = wave;                   // instruction wave = (row j, part sp)
-    while (sp >= G.ipr) sp -= G.ipr, j++;
-    for (int i = wave; i < G.nr * G.ipr; i += nw) {
-        const int u    = sp * 64 + lane;
-        const int b    = row0 + j * rs + u * ub;
-        const uint32_t voff = (u < upr && b >= 0) ? (uint32_t)b : kOutOfRange;
+    const int   lane = threadIdx.x & 63;
+    const int   cn   = JF(J, cn);
+    const auto  rsrc = uniform_rsrc((const void*)JF(J, src_ptr), (int)JF(J, src_bytes));
+    const int   upr  = stage_units_per_row(J, G);
+    const int   Q    = G.nr * upr;
+    const int   ub   = cn == 3 ? 12 : 1; // source bytes per unit
+    const int   row0 = src_off(J, G, 0, 0);
+    const int   rs   = JF(J, src_stride);
+    const float inv  = 1.f / (float)upr;
+    for (int i = wave; i * 64 < Q; i += nw) {
+        const int q    = i * 64 + lane;
+        uint32_t  voff = kOutOfRange;
+        if (q < Q) {
+            const int j = (int)(((float)q + 0.5f) * inv); // exact in f32 for q < 2^20
+            const int b = row0 + j * rs + (q - j * upr) * ub;
+            voff        = b >= 0 ? (uint32_t)b : kOutOfRange; // (padded jobs: fixed in stage_unpack)
+        }
         if (cn == 3) lds_dma<12>(rsrc, buf + i * 1024, voff);
         else lds_dma<4>(rsrc, buf + i * 256, voff);
-        sp += nw;
-        while (sp >= G.ipr) sp -= G.ipr, j++;
     }
 }
 
@@ -479,37 +473,38 @@ __device__ __forceinline__ void stage_unpack(const JobRef& J, const StageGeom& G
     const bool padded    = JF(J, padded) != 0;
     const bool at_end    = src_off(J, G, G.nr - 1, G.pitch) + 12 > src_bytes;
     if (cn != 3 && !padded && !at_end) return;
-    const int NI = G.nr * G.ipr; // DMA instructions of the tile
+    const int   upr = stage_units_per_row(J, G);
+    const int   Q   = G.nr * upr;
     if (cn == 3 && !padded && !at_end) {
-        // common case: in-place unpack of every slot of this wave's instructions (slots past a
-        // row's units are never read), reads of several instructions in flight before their writes
+        // common case: in-place unpack of this wave's slots, reads of several instructions in
+        // flight before their writes
         int i = wave;
-        for (; i + 2 * nw < NI; i += 3 * nw) {
+        for (; (i + 2 * nw) * 64 < Q; i += 3 * nw) {
             u32x4 w[3];
 #pragma unroll
             for (int k = 0; k < 3; k++) w[k] = *lds_ptr<const u32x4>(buf + ((i + k * nw) * 64 + lane) * 16);
 #pragma unroll
-            for (int k = 0; k < 3; k++) *lds_ptr<u32x4>(buf + ((i + k * nw) * 64 + lane) * 16) = unpack_bgr(w[k]);
+            for (int k = 0; k < 3; k++) {
+                const int q = (i + k * nw) * 64 + lane;
+                if (q < Q) *lds_ptr<u32x4>(buf + q * 16) = unpack_bgr(w[k]);
+            }
         }
-        for (; i < NI; i += nw) {
-            const auto slot = lds_ptr<u32x4>(buf + (i * 64 + lane) * 16);
+        for (; i * 64 < Q; i += nw) {
+            const int q = i * 64 + lane;
+            if (q >= Q) continue;
+            const auto slot = lds_ptr<u32x4>(buf + q * 16);
             *slot           = unpack_bgr(*slot);
         }
         return;
     }
-    const int upr = stage_units_per_row(J, G);
-    int       j = 0, sp = wave;
-    while (sp >= G.ipr) sp -= G.ipr, j++;
-    for (int i = wave; i < NI; i += nw) {
-        const int u  = sp * 64 + lane; // unit of this lane's slot
-        const int q  = i * 64 + lane;  // the slot
-        sp += nw;
-        const int jj = j;
-        while (sp >= G.ipr) sp -= G.ipr, j++;
-        if (u >= upr) continue;
-        const int u0 = u * (cn == 3 ? 4 : 1); // first staged column of this unit
-        const int np = cn == 3 ? 4 : 1;       // pixels of this unit
-        const int b  = src_off(J, G, jj, u0);
+    const float inv = 1.f / (float)upr;
+    for (int i = wave; i * 64 < Q; i += nw) {
+        const int q = i * 64 + lane;
+        if (q >= Q) continue;
+        const int j  = (int)(((float)q + 0.5f) * inv);
+        const int u0 = (q - j * upr) * (cn == 3 ? 4 : 1); // first staged column of this unit
+        const int np = cn == 3 ? 4 : 1;                   // pixels of this unit
+        const int b  = src_off(J, G, j, u0);
         const bool slow = padded || b < 0 || (at_end && b + (cn == 3 ? 12 : 4) > src_bytes);
         if (cn == 3 && !slow) {
             const auto slot = lds_ptr<u32x4>(buf + q * 16);
@@ -517,7 +512,7 @@ __device__ __forceinline__ void stage_unpack(const JobRef& J, const StageGeom& G
         } else if (slow) {
             const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)JF(J, src_ptr), (short)0, src_bytes, 0x00020000);
             for (int k = 0; k < np; k++) {
-                const int cy = G.v_lo + jj + JF(J, shift_y), cx = G.u_lo + u0 + k + JF(J, shift_x);
+                const int cy = G.v_lo + j + JF(J, shift_y), cx = G.u_lo + u0 + k + JF(J, shift_x);
                 uint32_t  p  = 0;
                 if (!padded || (cy >= 0 && cy < JF(J, crop_h) && cx >= 0 && cx < JF(J, crop_w))) {
                     const int bb = b + k * cn;
@@ -531,15 +526,22 @@ __device__ __forceinline__ void stage_unpack(const JobRef& J, const StageGeom& G
     }
 }
 
-// The job descriptor of tile t into an LDS job slot (one 64-lane LDS-DMA of its 256 bytes): the
-// tile's copy with AEON_HIP_LDSJOB, otherwise an L2 warm-up for its scalar loads.
-__device__ __forceinline__ void fetch_job(const LaunchArgs& a, int t, int lds_sink)
+// The job descriptor of tile t into an LDS job slot: one 64-lane LDS-DMA of its 256 bytes.  A job
+// table in pinned host memory (a.jobs_host) is read through to the host (sc0 sc1: the host wrote
+// the slot since the GPU last read it).
+__device__ __forceinline__ void fetch_job(const LaunchArgs& a, int t, int lds_slot)
 {
     if (t < 0 || t >= a.total_tiles) return;
     const int      job  = t / a.max_tiles;
     const auto     rs   = uniform_rsrc((const void*)(a.jobs + job), (int)sizeof(AugJob));
     const uint32_t lane = threadIdx.x & 63;
-    lds_dma<4>(rs, lds_sink, lane * 4 < sizeof(AugJob) ? lane * 4 : kOutOfRange);
+    const uint32_t voff = lane * 4 < sizeof(AugJob) ? lane * 4 : kOutOfRange;
+    const int      base = __builtin_amdgcn_readfirstlane(lds_slot);
+    if (a.jobs_host)
+        asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dword %1, %2, 0 offen sc0 sc1 lds" : : "s"(base), "v"(voff), "s"(rs)
+                     : "memory");
+    else
+        lds_dma<4>(rs, lds_slot, voff);
 }
 
 // Wait until at most n vector-memory instructions of this wave are outstanding (the immediate
@@ -564,10 +566,6 @@ __device__ __forceinline__ void lds_barrier()
     asm volatile("" ::: "memory");
 }
 
-// Lane -> output column mapping of the f32 CHW store path (Bands::compute): 1 = strided columns.
-#ifndef AEON_HIP_STRIDED
-#define AEON_HIP_STRIDED 0
-#endif
 // Output cache policy: streaming stores (written once, read by the consumer of the batch).
 #ifndef AEON_HIP_STORE_AUX
 #define AEON_HIP_STORE_AUX 2 // nt
@@ -691,18 +689,17 @@ struct Bands {
     struct Info {
         bool      ok;
         int       job, band, y0, nrows;
-        int       jl; // LDS byte address of the job's copy (AEON_HIP_LDSJOB)
+        int       jl;   // LDS byte address of the job's copy
+        int       t;    // the launch tile (-1: no more tiles for this workgroup)
         StageGeom G;
     };
-    __device__ __forceinline__ JobRef jref(const Info& f) const
-    {
-        return JobRef{&job_ref(a, f.job), f.jl};
-    }
-    // tile t -> Info; jl: the LDS slot holding the tile's job (AEON_HIP_LDSJOB)
+    __device__ __forceinline__ JobRef jref(const Info& f) const { return JobRef{f.jl}; }
+    // tile t -> Info; jl: the LDS slot holding the tile's job
     __device__ __forceinline__ Info info(int t, int jl) const
     {
         Info f;
         f.ok   = false;
+        f.t    = t;
         f.job  = t / a.max_tiles;
         f.band = t - f.job * a.max_tiles;
         f.jl   = jl;
@@ -725,7 +722,7 @@ struct Bands {
         G.v_lo  = ycoef<RM>(JF(J, win_y) + f.y0, JF(J, scale_y), JF(J, crop_h)).r0;
         G.nr    = ycoef<RM>(JF(J, win_y) + f.y0 + f.nrows - 1, JF(J, scale_y), JF(J, crop_h)).r1 - G.v_lo + 1;
         stage_layout(JF(J, cn), G);
-        const int need = stage_need(G);
+        const int need = stage_need(G, JF(J, cn));
         if (need > L.stage_bytes || JF(J, win_w) > a.max_win_w || f.nrows <= 0) {
             if ((threadIdx.x & 63) == 0) atomicOr(a.error, 2); // (lane 0 of whichever wave derives it)
             return f;
@@ -742,7 +739,7 @@ struct Bands {
         const auto p = lds_ptr<int32_t>(L.info);
         p[0] = f.ok, p[1] = f.job, p[2] = f.band, p[3] = f.y0, p[4] = f.nrows;
         p[5] = f.G.v_lo, p[6] = f.G.nr, p[7] = f.G.u_lo, p[8] = f.G.nc, p[9] = f.G.ng, p[10] = f.G.pitch;
-        p[11] = f.G.rp, p[12] = f.G.ipr, p[13] = f.jl;
+        p[11] = f.G.rp, p[12] = f.t, p[13] = f.jl;
     }
     __device__ __forceinline__ Info get_info() const
     {
@@ -751,7 +748,7 @@ struct Bands {
         Info       f;
         f.ok = rf(0) != 0, f.job = rf(1), f.band = rf(2), f.y0 = rf(3), f.nrows = rf(4);
         f.G.v_lo = rf(5), f.G.nr = rf(6), f.G.u_lo = rf(7), f.G.nc = rf(8), f.G.ng = rf(9), f.G.pitch = rf(10);
-        f.G.rp = rf(11), f.G.ipr = rf(12), f.jl = rf(13);
+        f.G.rp = rf(11), f.t = rf(12), f.jl = rf(13);
         return f;
     }
 
@@ -773,7 +770,7 @@ struct Bands {
             const auto xt = lds_ptr<i32x2>(L.xt);
             for (int x = tid; x < JF(J, win_w); x += nt) {
                 const XTap c = xcoef<RM>(JF(J, win_x) + x, JF(J, scale_x), JF(J, crop_w));
-                xt[x]        = (i32x2){c.sx - G.u_lo, (c.a0 & 0xffff) | (c.a1 << 16)};
+                xt[x]        = (i32x2){4 * (c.sx - G.u_lo), (c.a0 & 0xffff) | (c.a1 << 16)};
             }
         }
         if (PHOTO && KM != KM_RAW && a.has_hue && build_rec && JF(J, cn) == 3 && (JF(J, photo) & PHOTO_HUE)) {
@@ -910,7 +907,6 @@ struct Bands {
         // Lane -> (column group, row phase), fixed for the tile
         const int  gpr    = (win_w + 3) >> 2;
         const bool full4  = SP || (win_w & 3) == 0; // every lane's group is 4 pixels of the window
-        constexpr bool kStrided = AEON_HIP_STRIDED && KM == KM_FINAL && OF == OF_F32_CHW_VEC;
         const int  ncg    = min(gpr, nt);
         const int  nph    = nt / ncg;
         const int  lph    = tid / ncg;
@@ -925,14 +921,8 @@ struct Bands {
         // uint8 standardize through the LUT
         auto u8_out = [&](int c, int v) { return a.u8_map ? (int)lut_of(c, v) : u8_of(v); };
 
-        // A lane's four output columns: ox0 + k * cst.  Contiguous (cst 1: one 16-byte store per
-        // channel plane), or, with AEON_HIP_STRIDED on the f32 CHW path, strided by a quarter of the
-        // window (cst = gpr): then the lanes of one LDS read gather consecutive output columns, i.e.
-        // source pixels ~scale words apart (conflict-free banks) instead of ~4 * scale (a 4-way
-        // conflict per read), and each channel plane takes four coalesced 4-byte stores.
-        const int cst = (kStrided && full4) ? gpr : 1;
         for (int cg = active ? lcg : gpr; cg < gpr; cg += ncg) {
-            const int ox0 = cst == 1 ? cg * 4 : cg;
+            const int ox0 = cg * 4;
             const int nk  = SP ? 4 : min(4, win_w - ox0);
             int       col[4];
             uint32_t  wxk[4];
@@ -940,10 +930,10 @@ struct Bands {
 #pragma unroll
             for (int k = 0; k < 4; k++) {
                 // columns past the window edge recompute the last one (never stored)
-                const int  ox  = min(ox0 + k * cst, win_w - 1);
+                const int  ox  = min(ox0 + k, win_w - 1);
                 const int  x   = flip ? win_w - 1 - ox : ox;
                 const i32x2 xtt = xt[x];
-                col[k]         = xtt.x * 4; // byte offset in a staged row
+                col[k]         = xtt.x; // byte offset in a staged row
                 wxk[k]         = (uint32_t)xtt.y;
                 if (TAIL && RM == RESIZE_LINEAR && tail && (wx0 + x) * cn + 2 >= xv) tmask |= 1 << k;
             }
@@ -1066,19 +1056,6 @@ struct Bands {
                 }
                 // image::loader::load: source channel c goes to output channel oc (mixChannels
                 // from_to {0,2,1,1,2,0} when bgr_to_rgb); the LUT is indexed by source channel
-                if (OF == OF_F32_CHW_VEC && cst != 1) {
-                    const int idx = y * win_w + ox0;
-#pragma unroll
-                    for (int c = 0; c < 3; c++) {
-                        const int oc = bgr ? 2 - c : c;
-#pragma unroll
-                        for (int k = 0; k < 4; k++)
-                            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(lut_of(c, val[k][c])), orsrc,
-                                                                  (oc * plane + idx + k * cst) * 4, 0, kStoreAux);
-                        __builtin_amdgcn_sched_barrier(0);
-                    }
-                    continue;
-                }
                 if (OF == OF_F32_CHW_VEC) {
                     const int idx = y * win_w + ox0;
 #pragma unroll
@@ -1245,6 +1222,15 @@ void augment_tiles(LaunchArgs a)
         const int k = (int)__builtin_amdgcn_readfirstlane(*slot);
         return k < t_tail ? t_dyn + k : -1;
     };
+    // Job slots: three, a ring.  A static tile's job is fetched two tiles ahead by wave 0, after its
+    // share of the staging loads, so that the wave's staging wait (vmcnt(1)) leaves the fetch in
+    // flight (loads and stores retire in order on the vector-memory counter): a job read over PCIe
+    // from a pinned host table is not waited for on the critical path.  The next static tile's
+    // geometry is derived from its (landed) job by one wave during the compute.  A dynamic-tail tile
+    // is drawn when the workgroup gets to it and its job fetched then: drawing a tile ahead (so the
+    // fetch could land during the compute) hands out the last tiles a tile's time earlier and
+    // lengthened the tail more than the hidden fetch saved (C2 44.8 vs 42.7 us).
+    const auto slot_of = [&](int i) { return L.job + (i % 3) * (int)sizeof(AugJob); };
     int  t        = blockIdx.x;
     int  prev_job = -1;
     bool live     = t < t_dyn;
@@ -1252,12 +1238,15 @@ void augment_tiles(LaunchArgs a)
         t    = draw();
         live = t >= 0;
     }
-    int js = 0; // LDS job slot of the current tile
-    if (wave == 0) fetch_job(a, live ? t : -1, L.job);
+    int js = 0; // ring index of the current tile's job slot
+    if (wave == 0) {
+        fetch_job(a, live ? t : -1, slot_of(0));
+        fetch_job(a, live && t + G < t_dyn ? t + G : -1, slot_of(1));
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     Info f{};
-    if (live) f = W.info(t, L.job);
+    if (live) f = W.info(t, slot_of(0));
     for (int it = 0; live; it++) {
         // the staging phases (LDS-DMA issue, tap tables, unpack) at a raised wave priority: they
         // are this workgroup's critical path while the CU's other workgroups stream stores
@@ -1265,44 +1254,43 @@ void augment_tiles(LaunchArgs a)
         // (293 -> 283 us on C3)
         __builtin_amdgcn_s_setprio(KM == KM_STATS ? kComputePrio : kStagePrio);
         stamp(it, 0);
-        const bool more = t + G < t_dyn; // a static next tile
-        const int  jn   = L.job + (js ^ 1) * (int)sizeof(AugJob); // the next tile's job slot
-        if (wave == 0) fetch_job(a, more ? t + G : -1, jn);
+        const bool more  = t + G < t_dyn;     // a static next tile (its job is in slot js + 1)
+        const bool more2 = t + 2 * G < t_dyn; // ... and a static one after it
         stamp(it, 1);
         W.issue(f);
+        if (wave == 0 && more2) fetch_job(a, t + 2 * G, slot_of(js + 2));
         stamp(it, 2);
         const bool same = f.ok && f.job == prev_job; // the LDS tables still hold this record's
         prev_job        = f.ok ? f.job : -1;
         W.tables(f, !same, !same);
         W.record_table(f);
         stamp(it, 3);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (wave == 0 && more2) asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); // the staging loads
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         stamp(it, 4);
         W.unpack(f);
         stamp(it, 5);
-        __syncthreads();
+        lds_barrier(); // (not __syncthreads: a fence there would wait for wave 0's job fetch)
         stamp(it, 6);
         __builtin_amdgcn_s_setprio(KM == KM_STATS ? kStagePrio : kComputePrio);
-        // the next static tile's geometry: derived by one wave (its f64 tap bounds are uniform work
-        // every wave would otherwise repeat) during the compute, handed over through LDS
-        if (more && wave == nw - 1) W.put_info(W.info(t + G, jn));
+        if (more && wave == nw - 1) W.put_info(W.info(t + G, slot_of(js + 1)));
         W.compute_any(f);
         stamp(it, 7);
         lds_barrier(); // everyone is done reading the buffer before it is refilled
         stamp(it, 8);
-        js ^= 1;
         if (more) {
             f = W.get_info();
             t += G;
+            js = (js + 1) % 3;
         } else if (t_tail) {
             t    = draw();
             live = t >= 0;
             if (live) {
-                const int jl = L.job + js * (int)sizeof(AugJob);
-                if (wave == 0) fetch_job(a, t, jl);
+                js = (js + 1) % 3;
+                if (wave == 0) fetch_job(a, t, slot_of(js));
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 __syncthreads();
-                f = W.info(t, jl);
+                f = W.info(t, slot_of(js));
             }
         } else {
             break;

@@ -1,8 +1,7 @@
 // plan_record.hpp -- the per-record arithmetic aeon does on the host before touching pixels
-// (cv::resize dispatch, cropbox window, cv::transform matrix, lighting pixel), shared by the host
-// planner (stage.cpp) and the device planner (plan_kernels.hip): one source, compiled as host C++
-// and as HIP device code, with -ffp-contract=off on both sides so every float/double expression
-// rounds the same way.
+// (cv::resize dispatch, cropbox window, cv::transform matrix, lighting pixel): the host planner's
+// (stage.cpp) job of one record, built with -ffp-contract=off so every float/double expression
+// rounds as aeon's x86 build does.
 #pragma once
 #include <stdint.h>
 
@@ -143,25 +142,5 @@ AEON_HD inline void plan_direct(const aeon_img_desc& d, uint64_t src_base, const
         J.photo = photo;
     }
 }
-
-// Compact per-record input of the device planner: what the caller handed over for the record.
-struct alignas(16) PlanRecord {
-    aeon_img_desc   desc;   // 32 B
-    aeon_aug_params params; // 108 B (-> 144 with the alignment)
-};
-constexpr int kPlanRecordPieces = (int)sizeof(PlanRecord) / 16;
-static_assert(sizeof(PlanRecord) == 144, "PlanRecord is 144 bytes (9 x 16-byte loads)");
-
-// Per-call uniform arguments of the device planner.
-struct PlanArgs {
-    uint64_t src_base;    // device address the descriptors' offsets are relative to
-    uint64_t out_base;    // output item 0
-    uint64_t item_stride; // bytes between output items
-    OutGeom  out;
-    int32_t  n;           // records
-    int32_t  is_mask;
-    int32_t  rows_per_tile; // the launch's TR: AugJob::tiles = ceil(win_h / TR)
-    int32_t  pad_;
-};
 
 } // namespace aeon_hip

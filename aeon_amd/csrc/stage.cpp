@@ -38,7 +38,6 @@ hipError_t launch_expand(const ExpandJob* jobs, int n_jobs, int max_pixels, hipS
 hipError_t launch_nearest(const Mask16Job* jobs, int n_jobs, int max_h, int max_w, int max_seg_bytes, int max_slots, hipStream_t stream,
                           hipEvent_t start, hipEvent_t stop);
 hipError_t launch_upload_table(const void* host_dev, void* dst, size_t bytes, hipStream_t stream);
-hipError_t launch_plan_records(const void* host_records, void* jobs, const PlanArgs& a, hipStream_t stream);
 void       jpeg_decode_batch(JpegState* S, int n, const void* const* data, const size_t* sizes,
                              const aeon_img_desc* descs, void* dst_base, hipStream_t stream);
 void       jpeg_info(const void* data, size_t size, int* w, int* h, int* ncomp);
@@ -84,7 +83,14 @@ std::string device_error_text(int err)
     } while (0)
 
 constexpr int kMaxLds        = 160 * 1024;
-constexpr int kStageBudget   = 48 * 1024;   // preferred LDS bytes of the staging buffer
+// launch-shape constants (compile-time overrides only for tuning builds, tools/build_variants.sh)
+#ifndef AEON_HIP_STAGE_BUDGET_KB
+#define AEON_HIP_STAGE_BUDGET_KB 48
+#endif
+#ifndef AEON_HIP_FIXED_THREADS
+#define AEON_HIP_FIXED_THREADS 0
+#endif
+constexpr int kStageBudget   = AEON_HIP_STAGE_BUDGET_KB * 1024; // preferred LDS bytes of the staging buffer
 constexpr int kStageBudgetHi = 140 * 1024;  // fallback for very wide crops
 constexpr size_t kUploadKernelMax = 128 * 1024; // job tables above this go up by SDMA (run_batch)
 
@@ -209,6 +215,7 @@ struct LaunchPlan {
         // contrast pass 2 (photometric over the u8 intermediate, no resize): full workgroups
         // beat the fewest-idle-lanes choice (C3: 140 vs 158 us at 512 vs 448 lanes)
         if (rm == RESIZE_COPY && photo) threads = kBlockMax;
+        if (AEON_HIP_FIXED_THREADS) threads = AEON_HIP_FIXED_THREADS;
         const int nph = threads / ncg;
         // one staging buffer and four rows per lane (a multiple of the row phases): the CU's other
         // workgroups cover a tile's staging latency.  Measured on C2/C3 against two buffers
@@ -529,9 +536,9 @@ struct aeon_hip_ctx {
     int        next = 0;
     int        done_every = 8;
     size_t     table_cap = 0, partials_cap = 0, shifts_cap = 0; // per-slot capacities (ensure_ring)
-    // device planning (run_direct): calls whose records are one job each of one launch group
-    // upload the caller's descriptors + params and let plan_records build the jobs on the GPU
-    bool                 device_plan = true; // AEON_HIP_DEVICE_PLAN=0: always plan on the host
+    // direct calls (run_direct): records of one job each, one launch group: the tile kernel reads
+    // the jobs from the pinned slot itself
+    bool                 direct = true; // AEON_HIP_DIRECT=0: the multi-pass path (device job table) for every call
     std::vector<JobGeom> geoms;              // reused per call
     JpegState*           jpeg = nullptr;     // JPEG decode stage (pool, staging ring), on first use
     std::vector<int> open_slots; // used since the last completion event, on open_stream
@@ -769,7 +776,10 @@ LaunchArgs launch_args(aeon_hip_ctx* ctx, const Slot& s, const uint8_t* table, c
     // or four full rounds measured within noise or slower), the slot's own counter so
     // launches of calls in flight never share one
     a.tail_ctr    = ctx->d_tail + (&s - ctx->slots);
-    a.tail_rounds = 2;
+#ifndef AEON_HIP_TAIL_ROUNDS
+#define AEON_HIP_TAIL_ROUNDS 2
+#endif
+    a.tail_rounds = AEON_HIP_TAIL_ROUNDS;
     a.jobs           = (const AugJob*)(table + L.blob_off);
     a.lut            = d_lut; // [3][256]: standardized, or (float)x without mean
     a.hsv_tables     = ctx->d_hsv;
@@ -801,13 +811,13 @@ LaunchArgs launch_args(aeon_hip_ctx* ctx, const Slot& s, const uint8_t* table, c
     return a;
 }
 
-// Device-planned call (the common case: C2, C5's image, every record transformed straight from
-// its source in one launch group).  The host checks the records and sizes the launch from their
-// geometry; the caller's descriptors + params (128 B per record) go to the slot's pinned table and
-// plan_records -- on the launch stream, ahead of the tile kernel -- reads them over PCIe and
-// writes each record's AugJob with the same plan_direct the host planner uses.  Returns false
-// (nothing done) when some record needs the host planner: rotation, resize_short, contrast's two
-// passes, 2x-area + photometric, the mask gather pass, or records of several launch groups.
+// Direct call (the common case: C2, C5's image, every record transformed straight from its source in
+// one launch group): one launch and nothing else on the stream.  The host checks the records, sizes
+// the launch from their geometry and writes each record's AugJob (plan_direct) into the slot's
+// pinned table; the tile kernel reads the jobs from there itself (an LDS-DMA of one job per tile,
+// a tile ahead, over PCIe) -- no planner or upload launch ahead of it.  Returns false (nothing done)
+// when some record needs the multi-pass planner: rotation, resize_short, contrast's two passes,
+// 2x-area + photometric, the mask gather pass, or records of several launch groups.
 template <typename Phase>
 bool run_direct(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* src_base,
                 const aeon_aug_params* params, const aeon_out_desc& od, void* out_dev, hipStream_t stream,
@@ -856,21 +866,22 @@ bool run_direct(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void
     phase(3);
     const float* d_lut = resident_lut(ctx, od, ov.u8_map);
     ensure_ring(ctx, (size_t)n * sizeof(AugJob), 16, 32);
-    PlanRecord* R = (PlanRecord*)s.host;
+    AugJob*       jt = (AugJob*)s.host;
+    const OutGeom og = out_geom(o);
     for (int i = 0; i < n; i++) {
-        std::memcpy(&R[i].desc, &descs[i], sizeof(aeon_img_desc));
-        std::memcpy(&R[i].params, &params[i], sizeof(aeon_aug_params));
+        plan_direct(descs[i], (uint64_t)src_base, params[i], og, (uint64_t)out_dev + (uint64_t)i * o.item_stride,
+                    is_mask, jt[i]);
+        jt[i].tiles = (jt[i].win_h + P.tr - 1) / P.tr;
     }
     phase(4);
-    const PlanArgs pa{(uint64_t)src_base, (uint64_t)out_dev, o.item_stride, out_geom(o), n, is_mask ? 1 : 0, P.tr, 0};
-    HIP_OK(launch_plan_records(s.host_dev, s.dev, pa, stream));
     phase(5);
     const bool timed = ctx->timing && (ctx->timing_calls++ % ctx->timing_every) == ctx->timing_every - 1;
     if (o.fixed_aspect_ratio) // std::fill_n of each item's canvas, its whole byte size (etl_image.cpp:263)
         HIP_OK(hipMemset2DAsync(out_dev, o.item_stride, 0,
                                 (size_t)o.canvas_w * o.canvas_h * o.channels * out_elem_bytes(od.dtype), n, stream));
-    timed_launch(ctx, KM_FINAL, P, launch_args(ctx, s, s.dev, P, n, o, d_lut, 1, ov.u8_map), stream,
-                 launch_bytes(geo, KM_FINAL, out_elem_bytes(o.dtype)), timed);
+    LaunchArgs a = launch_args(ctx, s, s.host_dev, P, n, o, d_lut, 1, ov.u8_map);
+    a.jobs_host  = 1;
+    timed_launch(ctx, KM_FINAL, P, a, stream, launch_bytes(geo, KM_FINAL, out_elem_bytes(o.dtype)), timed);
     phase(6);
     release_slot(ctx, slot, stream);
     phase(7);
@@ -918,7 +929,7 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
     };
     HIP_OK(hipSetDevice(ctx->device));
     phase(0);
-    if (ctx->device_plan &&
+    if (ctx->direct &&
         run_direct(ctx, n, descs, src_base, params, od, out_dev, stream, is_mask, phase))
         return 0;
 
@@ -1172,9 +1183,9 @@ int aeon_hip_ctx_create(int device, aeon_hip_ctx** out)
             // the ring at the size a 512-record call needs (job tables of 128 KB), so steady-state
             // calls of that size never allocate
             ensure_ring(c, 128 * 1024, 64 * 1024, 8 * 1024);
-            // diagnostics: host time per phase (printed at destroy); the host planner for every call
+            // diagnostics: host time per phase (printed at destroy); the multi-pass path for every call
             if (const char* e = std::getenv("AEON_HIP_HOST_PROFILE")) c->host_profile = std::atoi(e) != 0;
-            if (const char* e = std::getenv("AEON_HIP_DEVICE_PLAN")) c->device_plan = std::atoi(e) != 0;
+            if (const char* e = std::getenv("AEON_HIP_DIRECT")) c->direct = std::atoi(e) != 0;
             HIP_OK(hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, device));
         } catch (...) {
             delete c;

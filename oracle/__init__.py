@@ -118,6 +118,10 @@ def lib():
         for fn in (L.orc_resize_linear, L.orc_resize_nearest):
             fn.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                            ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+        L.orc_resize_cv.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                    ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+        L.orc_lanczos4_coeffs.argtypes = [ctypes.c_float, P(ctypes.c_float)]
+        L.orc_lanczos4_coeffs.restype = None
         L.orc_cbsjitter.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_float,
                                     ctypes.c_float, ctypes.c_float, ctypes.c_int]
         L.orc_lighting.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, P(ctypes.c_float),
@@ -318,6 +322,26 @@ def resize_linear(src, dw, dh):
     out = np.zeros((dh, dw, cn), np.uint8)
     _check(lib().orc_resize_linear(src.ctypes.data, w, h, w * cn, cn, out.ctypes.data, dw, dh))
     return out
+
+
+INTERP = {"LINEAR": 0, "NEAREST": 1, "CUBIC": 2, "AREA": 3, "LANCZOS4": 4}
+
+
+def resize(src, dw, dh, interp):
+    """cv::resize (OpenCV 2.4.9) of HWC uint8 with interpolation code or name (INTERP)."""
+    code = INTERP[interp.upper()] if isinstance(interp, str) else int(interp)
+    src = np.ascontiguousarray(src, dtype=np.uint8)
+    h, w = src.shape[:2]
+    cn = 1 if src.ndim == 2 else src.shape[2]
+    out = np.zeros((dh, dw) + (() if src.ndim == 2 else (cn,)), np.uint8)
+    _check(lib().orc_resize_cv(src.ctypes.data, w, h, w * cn, cn, out.ctypes.data, dw, dh, code))
+    return out
+
+
+def lanczos4_coeffs(x):
+    out = (ctypes.c_float * 8)()
+    lib().orc_lanczos4_coeffs(x, out)
+    return np.array(out[:], np.float32)
 
 
 def resize_nearest(src, dw, dh):

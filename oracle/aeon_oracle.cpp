@@ -394,6 +394,246 @@ void resize_nearest(const Img& s, Img& d)
     }
 }
 
+
+// ---- cv::resize INTER_CUBIC / INTER_LANCZOS4 / INTER_AREA, 8U --------------------------------
+// PARITY UNPINNED: aeon's tests hold no output of these methods (its interpolation_method map,
+// src/image.cpp:30-36, reaches them from the "interpolation_method" config, used by image::resize
+// :93-106 and image::resize_short :118-127).  Restated from OpenCV 2.4.9 imgwarp.cpp: cv::resize's
+// coefficient set-up (x: sx/fx with the xmin/xmax clamps, y: unclamped sy, rows clipped),
+// interpolateCubic (A = -0.75) / interpolateLanczos4, 11-bit fixed-point coefficients
+// (saturate_cast<short>(c * 2048)), resizeGeneric_ with HResizeCubic / HResizeLanczos4 (exact int,
+// edge taps clamped) and VResizeCubic (VResizeCubicVec_32s8u, SSE2: float sums, 8 elements at a time
+// while x <= W - 8, cvtps round-half-even, packs/packus saturation; the scalar tail
+// FixedPtCast<int, uchar, 22>) / VResizeLanczos4 (all scalar FixedPtCast, int32 sums wrapping as on
+// x86); INTER_AREA: downscale in both axes -> resizeAreaFast_ for integer factors (2x2: the
+// (a+b+c+d+2)>>2 fast mode; otherwise saturate_cast<uchar>(sum * (1.f/area))) or resizeArea_ with
+// computeResizeAreaTab (float sums in table order); otherwise bilinear with area-mode coefficients.
+enum { ORC_LINEAR = 0, ORC_NEAREST = 1, ORC_CUBIC = 2, ORC_AREA = 3, ORC_LANCZOS4 = 4 };
+
+static void interpolate_cubic(float x, float* c)
+{
+    const float A = -0.75f;
+    c[0] = ((A * (x + 1) - 5 * A) * (x + 1) + 8 * A) * (x + 1) - 4 * A;
+    c[1] = ((A + 2) * x - (A + 3)) * x * x + 1;
+    c[2] = ((A + 2) * (1 - x) - (A + 3)) * (1 - x) * (1 - x) + 1;
+    c[3] = 1.f - c[0] - c[1] - c[2];
+}
+
+void interpolate_lanczos4(float x, float* c)
+{
+    static const double s45   = 0.70710678118654752440084436210485;
+    static const double cs[][2] = {{1, 0}, {-s45, -s45}, {0, 1}, {s45, -s45}, {-1, 0}, {s45, s45}, {0, -1}, {-s45, s45}};
+    const double        kPi   = 3.1415926535897932384626433832795;
+    if (x < FLT_EPSILON) {
+        for (int i = 0; i < 8; i++) c[i] = 0;
+        c[3] = 1;
+        return;
+    }
+    float  sum = 0;
+    double y0 = -(x + 3) * kPi * 0.25, s0 = std::sin(y0), c0 = std::cos(y0);
+    for (int i = 0; i < 8; i++) {
+        double y = -(x + 3 - i) * kPi * 0.25;
+        c[i]     = (float)((cs[i][0] * s0 + cs[i][1] * c0) / (y * y));
+        sum += c[i];
+    }
+    sum = 1.f / sum;
+    for (int i = 0; i < 8; i++) c[i] *= sum;
+}
+
+// cv::resize's coefficient set-up for the ksize-tap filters (ksize 2 with area_mode: INTER_AREA's
+// bilinear emulation): per destination column its (clamped) sx and fixed-point taps, per row sy.
+struct GenTaps {
+    std::vector<int> sx, sy;       // first-tap anchors (x after the clamps; y raw)
+    std::vector<short> ax, by;     // ksize coefficients per column / row
+};
+static void coeffs_for(int interp, float f, float* c)
+{
+    if (interp == ORC_CUBIC) interpolate_cubic(f, c);
+    else if (interp == ORC_LANCZOS4) interpolate_lanczos4(f, c);
+    else c[0] = 1.f - f, c[1] = f;
+}
+static GenTaps gen_taps(int interp, int ksize, bool area_mode, int sw, int sh, int dw, int dh)
+{
+    GenTaps T;
+    const double inv_sx = (double)dw / sw, inv_sy = (double)dh / sh;
+    const double scale_x = 1. / inv_sx, scale_y = 1. / inv_sy;
+    const int    k2 = ksize / 2;
+    T.sx.resize(dw), T.sy.resize(dh), T.ax.resize((size_t)dw * ksize), T.by.resize((size_t)dh * ksize);
+    float cbuf[8];
+    for (int dx = 0; dx < dw; dx++) {
+        float fx;
+        int   sx;
+        if (!area_mode) {
+            fx = (float)((dx + 0.5) * scale_x - 0.5);
+            sx = cv_floor(fx);
+            fx -= sx;
+        } else {
+            sx = cv_floor(dx * scale_x);
+            fx = (float)((dx + 1) - (sx + 1) * inv_sx);
+            fx = fx <= 0 ? 0.f : fx - cv_floor(fx);
+        }
+        if (sx < k2 - 1 && sx < 0) fx = 0, sx = 0;
+        if (sx + k2 >= sw && sx >= sw - 1) fx = 0, sx = sw - 1;
+        T.sx[dx] = sx;
+        coeffs_for(interp, fx, cbuf);
+        for (int k = 0; k < ksize; k++) T.ax[(size_t)dx * ksize + k] = (short)sat_s16(cv_roundf(cbuf[k] * 2048));
+    }
+    for (int dy = 0; dy < dh; dy++) {
+        float fy;
+        int   sy;
+        if (!area_mode) {
+            fy = (float)((dy + 0.5) * scale_y - 0.5);
+            sy = cv_floor(fy);
+            fy -= sy;
+        } else {
+            sy = cv_floor(dy * scale_y);
+            fy = (float)((dy + 1) - (sy + 1) * inv_sy);
+            fy = fy <= 0 ? 0.f : fy - cv_floor(fy);
+        }
+        T.sy[dy] = sy;
+        coeffs_for(interp, fy, cbuf);
+        for (int k = 0; k < ksize; k++) T.by[(size_t)dy * ksize + k] = (short)sat_s16(cv_roundf(cbuf[k] * 2048));
+    }
+    return T;
+}
+
+// First element of a W-element row on the scalar tail of the ksize-tap vertical pass (SSE2 build):
+// linear VResizeLinearVec_32s8u (16 then 4 at a time), cubic VResizeCubicVec_32s8u (8 at a time),
+// Lanczos4 none.
+int vresize_simd_end(int ksize, int W)
+{
+    int x = 0;
+    if (ksize == 2) {
+        x = W >= 16 ? (W / 16) * 16 : 0;
+        while (x < W - 4) x += 4;
+    } else if (ksize == 4) {
+        while (x <= W - 8) x += 8;
+    }
+    return x;
+}
+
+// resizeGeneric_ for ksize 2 (area-mode bilinear), 4 (cubic) and 8 (Lanczos4), 8U.
+void resize_generic(const Img& s, Img& d, int interp, bool area_mode)
+{
+    const int ksize = interp == ORC_CUBIC ? 4 : (interp == ORC_LANCZOS4 ? 8 : 2), k2 = ksize / 2;
+    const int sw = s.w, sh = s.h, cn = s.cn, dw = d.w, dh = d.h, W = dw * cn;
+    const GenTaps T = gen_taps(interp, ksize, area_mode, sw, sh, dw, dh);
+    const int xv = vresize_simd_end(ksize, W);
+    std::vector<int> H((size_t)ksize * W);
+    for (int dy = 0; dy < dh; dy++) {
+        // horizontal pass of the ksize source rows (clip(sy - k2 + 1 + k, 0, sh))
+        for (int k = 0; k < ksize; k++) {
+            const int      r = std::min(std::max(T.sy[dy] - k2 + 1 + k, 0), sh - 1);
+            const uint8_t* S = s.row(r);
+            for (int dx = 0; dx < dw; dx++)
+                for (int c = 0; c < cn; c++) {
+                    int v = 0;
+                    for (int j = 0; j < ksize; j++) {
+                        const int x = std::min(std::max(T.sx[dx] - k2 + 1 + j, 0), sw - 1);
+                        v += S[x * cn + c] * T.ax[(size_t)dx * ksize + j];
+                    }
+                    H[(size_t)k * W + dx * cn + c] = v;
+                }
+        }
+        const short* b = &T.by[(size_t)dy * ksize];
+        uint8_t*     D = d.row(dy);
+        for (int x = 0; x < W; x++) {
+            if (x < xv && ksize == 2) { // VResizeLinearVec_32s8u
+                int h0 = sat_s16(H[x] >> 4), h1 = sat_s16(H[W + x] >> 4);
+                int m  = sat_s16(((h0 * (int)b[0]) >> 16) + ((h1 * (int)b[1]) >> 16));
+                D[x]   = sat_u8(sat_s16(m + 2) >> 2);
+            } else if (x < xv && ksize == 4) { // VResizeCubicVec_32s8u: float, in SSE's order
+                const float sc = 1.f / (2048 * 2048);
+                float       v  = (float)H[x] * ((float)b[0] * sc) + (float)H[W + x] * ((float)b[1] * sc);
+                v              = v + (float)H[2 * W + x] * ((float)b[2] * sc);
+                v              = v + (float)H[3 * W + x] * ((float)b[3] * sc);
+                D[x]           = sat_u8(sat_s16(cv_roundf(v)));
+            } else { // FixedPtCast<int, uchar, 22> over int sums (wrapping as x86 int arithmetic)
+                uint32_t acc = 0;
+                for (int k = 0; k < ksize; k++) acc += (uint32_t)H[(size_t)k * W + x] * (uint32_t)(int)b[k];
+                D[x] = sat_u8((int32_t)(acc + (1u << 21)) >> 22);
+            }
+        }
+    }
+}
+
+// resizeAreaFast_ (integer factors iscale_x x iscale_y, both >= 1), 8U.
+void resize_area_fast(const Img& s, Img& d, int isx, int isy)
+{
+    const int cn = s.cn;
+    const bool fast2 = isx == 2 && isy == 2 && (cn == 1 || cn == 3 || cn == 4);
+    const float scale = 1.f / (isx * isy);
+    for (int dy = 0; dy < d.h; dy++) {
+        uint8_t* D = d.row(dy);
+        for (int dx = 0; dx < d.w; dx++)
+            for (int c = 0; c < cn; c++) {
+                int sum = 0;
+                for (int y = 0; y < isy; y++)
+                    for (int x = 0; x < isx; x++) sum += s.row(dy * isy + y)[(dx * isx + x) * cn + c];
+                D[dx * cn + c] = fast2 ? (uint8_t)((sum + 2) >> 2) : sat_u8(cv_roundf((float)sum * scale));
+            }
+    }
+}
+
+// computeResizeAreaTab + resizeArea_ (non-integer downscale in both axes), 8U.
+struct AreaTab {
+    int   di, si;
+    float alpha;
+};
+std::vector<AreaTab> area_tab(int ssize, int dsize, double scale)
+{
+    std::vector<AreaTab> tab;
+    for (int dx = 0; dx < dsize; dx++) {
+        const double fsx1 = dx * scale, fsx2 = fsx1 + scale;
+        const double cell = std::min(scale, ssize - fsx1);
+        int          sx1 = (int)std::ceil(fsx1), sx2 = cv_floor(fsx2);
+        sx2 = std::min(sx2, ssize - 1);
+        sx1 = std::min(sx1, sx2);
+        if (sx1 - fsx1 > 1e-3) tab.push_back({dx, sx1 - 1, (float)((sx1 - fsx1) / cell)});
+        for (int sx = sx1; sx < sx2; sx++) tab.push_back({dx, sx, (float)(1.0 / cell)});
+        if (fsx2 - sx2 > 1e-3) tab.push_back({dx, sx2, (float)(std::min(std::min(fsx2 - sx2, 1.), cell) / cell)});
+    }
+    return tab;
+}
+void resize_area_generic(const Img& s, Img& d, double scale_x, double scale_y)
+{
+    const int cn = s.cn;
+    const std::vector<AreaTab> xt = area_tab(s.w, d.w, scale_x), yt = area_tab(s.h, d.h, scale_y);
+    std::vector<float> buf((size_t)d.w * cn), sum((size_t)d.w * cn, 0.f);
+    int prev = yt.empty() ? 0 : yt[0].di;
+    for (const AreaTab& y : yt) {
+        std::fill(buf.begin(), buf.end(), 0.f);
+        const uint8_t* S = s.row(y.si);
+        for (const AreaTab& x : xt)
+            for (int c = 0; c < cn; c++) buf[(size_t)x.di * cn + c] = buf[(size_t)x.di * cn + c] + S[x.si * cn + c] * x.alpha;
+        if (y.di != prev) {
+            uint8_t* D = d.row(prev);
+            for (size_t i = 0; i < buf.size(); i++) D[i] = sat_u8f(sum[i]), sum[i] = y.alpha * buf[i];
+            prev = y.di;
+        } else {
+            for (size_t i = 0; i < buf.size(); i++) sum[i] = sum[i] + y.alpha * buf[i];
+        }
+    }
+    uint8_t* D = d.row(prev);
+    for (size_t i = 0; i < sum.size(); i++) D[i] = sat_u8f(sum[i]);
+}
+
+// cv::resize (OpenCV 2.4.9) for every interpolation aeon's config names, 8U.
+void resize_cv(const Img& s, Img& d, int interp)
+{
+    if (interp == ORC_NEAREST) return resize_nearest(s, d);
+    if (interp == ORC_LINEAR) return resize_linear(s, d);
+    const double inv_sx = (double)d.w / s.w, inv_sy = (double)d.h / s.h;
+    const double scale_x = 1. / inv_sx, scale_y = 1. / inv_sy;
+    if (interp == ORC_AREA && scale_x >= 1 && scale_y >= 1) {
+        const int isx = cv_round(scale_x), isy = cv_round(scale_y);
+        if (std::abs(scale_x - isx) < DBL_EPSILON && std::abs(scale_y - isy) < DBL_EPSILON)
+            return resize_area_fast(s, d, isx, isy);
+        return resize_area_generic(s, d, scale_x, scale_y);
+    }
+    resize_generic(s, d, interp == ORC_AREA ? ORC_LINEAR : interp, interp == ORC_AREA);
+}
+
 // image::resize (image.cpp:93-106): identity when the size already matches.
 void resize_any(const Img& s, Img& d, int interp)
 {
@@ -401,8 +641,7 @@ void resize_any(const Img& s, Img& d, int interp)
         for (int y = 0; y < s.h; y++) std::memcpy(d.row(y), s.row(y), (size_t)s.w * s.cn);
         return;
     }
-    if (interp == 1) resize_nearest(s, d);
-    else resize_linear(s, d);
+    resize_cv(s, d, interp);
 }
 
 // ---- photometric::cbsjitter (src/image.cpp:358-406) -----------------------------------------
@@ -709,8 +948,7 @@ Img transform_single_image(const Img& src, const orc_params& p)
         int rw, rh;
         resized_short_size(base.w, base.h, p.resize_short_size, &rw, &rh);
         rs = Img::alloc(rw, rh, src.cn);
-        if (p.interp == 1) resize_nearest(base, rs);
-        else resize_linear(base, rs);
+        resize_cv(base, rs, p.interp); // image::resize_short: cv::resize, no same-size shortcut
         base = Img::view(rs.data, rs.w, rs.h, rs.cn, rs.stride);
     }
     if (p.crop_x < 0 || p.crop_y < 0 || p.crop_w <= 0 || p.crop_h <= 0 ||
@@ -999,6 +1237,20 @@ int orc_resize_nearest(const uint8_t* src, int sw, int sh, int sstride, int cn, 
         resize_nearest(s, d);
     });
 }
+
+// cv::resize with any of aeon's interpolation methods (0 LINEAR, 1 NEAREST, 2 CUBIC, 3 AREA, 4 LANCZOS4)
+int orc_resize_cv(const uint8_t* src, int sw, int sh, int sstride, int cn, uint8_t* dst, int dw, int dh, int interp)
+{
+    return guarded([&] {
+        if (interp < 0 || interp > 4) throw std::invalid_argument("unknown interpolation");
+        Img s = Img::view(src, sw, sh, cn, sstride);
+        Img d = Img::view(dst, dw, dh, cn, dw * cn);
+        resize_cv(s, d, interp);
+    });
+}
+
+// interpolateLanczos4's coefficients of fraction x (the product builds them on the host too)
+void orc_lanczos4_coeffs(float x, float* out) { interpolate_lanczos4(x, out); }
 
 void orc_cbsjitter(uint8_t* img, int w, int h, float contrast, float brightness, float saturation,
                    int hue)

@@ -108,6 +108,9 @@ int  orc_resize_linear(const uint8_t* src, int sw, int sh, int sstride, int cn, 
                        int dw, int dh);
 int  orc_resize_nearest(const uint8_t* src, int sw, int sh, int sstride, int cn, uint8_t* dst,
                         int dw, int dh);
+int  orc_resize_cv(const uint8_t* src, int sw, int sh, int sstride, int cn, uint8_t* dst, int dw, int dh,
+                   int interp);
+void orc_lanczos4_coeffs(float x, float* out);
 void orc_cbsjitter(uint8_t* img, int w, int h, float contrast, float brightness,
                    float saturation, int hue);
 void orc_lighting(uint8_t* img, int w, int h, const float* lighting, int n, float color_noise_std);

