@@ -30,6 +30,9 @@ DTYPES = {"uint8": (0, np.uint8), "float32": (1, np.float32), "int8": (2, np.int
 NP_DTYPE = {code: t for code, t in DTYPES.values()}
 INTERP_LINEAR = 0
 INTERP_NEAREST = 1
+INTERP_CUBIC = 2
+INTERP_AREA = 3
+INTERP_LANCZOS4 = 4
 
 
 class ImgDesc(ctypes.Structure):

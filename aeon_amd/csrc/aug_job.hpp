@@ -90,6 +90,35 @@ struct alignas(16) ExpandJob {
     int32_t  pad_[3];
 };
 
+// cv::resize with INTER_CUBIC / INTER_LANCZOS4 / INTER_AREA (aeon's interpolation_method, image.cpp:30-36)
+// of one record: a pre-pass (resize_kernels.hip) writing the resized window as HWC uint8 into the slot
+// scratch; the record's tile job then copies it (RESIZE_COPY) through the photometric stages and the
+// loader.  GR_LINEAR_AREA is INTER_AREA's bilinear emulation when an axis is upscaled.
+enum GrMethod : int32_t { GR_LINEAR_AREA = 0, GR_CUBIC = 1, GR_LANCZOS4 = 2, GR_AREA_FAST = 3, GR_AREA = 4 };
+struct alignas(16) ResizeJob {
+    double   scale_x, scale_y;  // OpenCV's 1 / inv_scale
+    double   inv_x, inv_y;      // inv_scale = dst / src (area-mode coefficients)
+    uint64_t src_ptr;           // HWC uint8: the record, or its rotated / expanded / resize_short copy
+    uint64_t out_ptr;           // HWC uint8 window, win_w * cn bytes per row (slot scratch)
+    int32_t  src_stride, cn;
+    int32_t  crop_x, crop_y, crop_w, crop_h; // the region resized (cv::resize's source)
+    int32_t  shift_x, shift_y, padded;       // add_padding as a virtual zero border (as AugJob)
+    int32_t  dst_w, dst_h;                   // the full resize target
+    int32_t  win_x, win_y, win_w, win_h;     // its window produced here
+    int32_t  method;                         // GrMethod
+    int32_t  isx, isy;                       // GR_AREA_FAST integer factors
+    int32_t  coef_x, coef_y;                 // GR_LANCZOS4: host-built taps, byte offsets in the call's table
+    int32_t  tiles_x, tiles;                 // column bands of the window, tiles in all
+    int32_t  src_scratch, out_scratch;       // host bookkeeping: offsets into the slot scratch until relocated
+    int32_t  pad_[2];
+};
+// GR_LANCZOS4 taps per destination column / row as the host builds them (interpolateLanczos4 with
+// the C library's sin / cos, as OpenCV): first source index, then 8 fixed-point coefficients.
+struct GrTap {
+    int32_t s;
+    int16_t c[8];
+};
+
 // Per-launch uniform arguments.
 struct LaunchArgs {
     const AugJob*  jobs;       // the launch's jobs: device memory, or the device view of a pinned host slot

@@ -230,7 +230,9 @@ int param_factory::interp_code() const
     std::transform(m.begin(), m.end(), m.begin(), ::toupper);
     if (m == "LINEAR") return AEON_INTERP_LINEAR;
     if (m == "NEAREST") return AEON_INTERP_NEAREST;
-    if (m == "CUBIC" || m == "AREA" || m == "LANCZOS4") return -1;
+    if (m == "CUBIC") return AEON_INTERP_CUBIC;
+    if (m == "AREA") return AEON_INTERP_AREA;
+    if (m == "LANCZOS4") return AEON_INTERP_LANCZOS4;
     throw std::invalid_argument("Provided interpolation method (" + interpolation_method +
                                 " is unrecognized.");
 }

@@ -85,7 +85,7 @@ public:
     mutable std::bernoulli_distribution           flip_distribution{0};
     mutable std::uniform_int_distribution<int>    padding_crop_offset_distribution{0, 0};
 
-    int interp_code() const; // AEON_INTERP_* (or -1 for CUBIC/AREA/LANCZOS4)
+    int interp_code() const; // AEON_INTERP_*
 
     // src/augment_image.cpp:232-301 (boxes: n x (xmin, ymin, xmax, ymax) boundingbox::box)
     template <typename URNG>

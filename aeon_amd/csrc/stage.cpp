@@ -38,6 +38,8 @@ hipError_t launch_expand(const ExpandJob* jobs, int n_jobs, int max_pixels, hipS
 hipError_t launch_nearest(const Mask16Job* jobs, int n_jobs, int max_h, int max_w, int max_seg_bytes, int max_slots, hipStream_t stream,
                           hipEvent_t start, hipEvent_t stop);
 hipError_t launch_upload_table(const void* host_dev, void* dst, size_t bytes, hipStream_t stream);
+hipError_t launch_resize_generic(const ResizeJob* jobs, const uint8_t* table, int n_jobs, int max_tiles, int TR, int CW,
+                                 int NR, int xs, int amax, int cn_max, int32_t* error, hipStream_t stream);
 void       jpeg_decode_batch(JpegState* S, int n, const void* const* data, const size_t* sizes,
                              const aeon_img_desc* descs, void* dst_base, hipStream_t stream);
 void       jpeg_info(const void* data, size_t size, int* w, int* h, int* ncomp);
@@ -69,7 +71,8 @@ std::string device_error_text(int err)
                 {4, "dynamic LDS not at address 0"},
                 {16, "hue table without a t1 channel"},
                 {32, "dynamic-tail counter left over by an earlier launch"},
-                {64, "rotation source box exceeds the launch's LDS"}};
+                {64, "rotation source box exceeds the launch's LDS"},
+                {128, "generic resize footprint exceeds the launch's LDS"}};
     std::string s;
     for (const auto& b : bits)
         if (err & b.bit) s += (s.empty() ? "" : "; ") + std::string(b.what);
@@ -341,8 +344,7 @@ void validate_record(const aeon_img_desc& d, const aeon_aug_params& p, const aeo
     if (d.width <= 0 || d.height <= 0 || d.stride < d.width * cn)
         fail(AEON_HIP_EINVAL, "invalid source image descriptor");
     const int interp = is_mask ? AEON_INTERP_NEAREST : p.interp;
-    if (interp != AEON_INTERP_LINEAR && interp != AEON_INTERP_NEAREST)
-        fail(AEON_HIP_EUNSUPPORTED, "only LINEAR and NEAREST interpolation are implemented");
+    if (interp < AEON_INTERP_LINEAR || interp > AEON_INTERP_LANCZOS4) fail(AEON_HIP_EINVAL, "unknown interpolation");
     if (p.out_w <= 0 || p.out_h <= 0) fail(AEON_HIP_EINVAL, "invalid output size");
     const size_t elem = out_elem_bytes(o.dtype);
     if ((size_t)p.out_w * p.out_h * cn * elem > o.item_stride)
@@ -367,12 +369,154 @@ void validate_record(const aeon_img_desc& d, const aeon_aug_params& p, const aeo
 
 OutGeom out_geom(const aeon_out_desc& o) { return OutGeom{o.fixed_aspect_ratio, o.canvas_w, o.canvas_h}; }
 
-// Launch order: rot (image::rotate) -> pre (resize_short) -> pre2 (2x-area resize ahead of photometric stages) ->
-// pass1 (contrast statistics) -> main; each reads only what an earlier group wrote.
+// The cv::resize of a (sw x sh -> dw x dh) resize with interpolation `interp` when the tile kernel
+// has no mode for it: a resize_generic method (CUBIC, LANCZOS4, INTER_AREA but its exact 2x box), or
+// -1 -- LINEAR / NEAREST, any identity (every method reproduces the source at scale 1) and INTER_AREA's
+// 2x fast path (RESIZE_AREA2X, the same (a+b+c+d+2)>>2).  OpenCV 2.4.9 cv::resize's dispatch.
+int generic_method(int sw, int sh, int dw, int dh, int interp, int cn, int* isx, int* isy)
+{
+    if (interp != AEON_INTERP_CUBIC && interp != AEON_INTERP_AREA && interp != AEON_INTERP_LANCZOS4) return -1;
+    if (sw == dw && sh == dh) return -1;
+    if (interp == AEON_INTERP_CUBIC) return GR_CUBIC;
+    if (interp == AEON_INTERP_LANCZOS4) return GR_LANCZOS4;
+    const double sx = 1. / ((double)dw / sw), sy = 1. / ((double)dh / sh);
+    if (sx < 1 || sy < 1) return GR_LINEAR_AREA; // an upscaled axis: bilinear over area-mode coefficients
+    const int ix = cv_round(sx), iy = cv_round(sy);
+    if (std::fabs(sx - ix) < DBL_EPSILON && std::fabs(sy - iy) < DBL_EPSILON) {
+        if (ix == 2 && iy == 2 && (cn == 1 || cn == 3)) return -1;
+        *isx = ix, *isy = iy;
+        return GR_AREA_FAST;
+    }
+    return GR_AREA;
+}
+
+// interpolateLanczos4 (OpenCV 2.4.9 imgwarp.cpp), double sin / cos of the C library as OpenCV's.
+void lanczos4_coeffs(float x, float* c)
+{
+    static const double s45 = 0.70710678118654752440084436210485;
+    static const double cs[][2] = {{1, 0}, {-s45, -s45}, {0, 1}, {s45, -s45}, {-1, 0}, {s45, s45}, {0, -1}, {-s45, s45}};
+    const double kPi = 3.1415926535897932384626433832795;
+    if (x < FLT_EPSILON) {
+        for (int i = 0; i < 8; i++) c[i] = 0;
+        c[3] = 1;
+        return;
+    }
+    float        sum = 0;
+    const double y0 = -(x + 3) * kPi * 0.25, s0 = std::sin(y0), c0 = std::cos(y0);
+    for (int i = 0; i < 8; i++) {
+        const double y = -(x + 3 - i) * kPi * 0.25;
+        c[i]           = (float)((cs[i][0] * s0 + cs[i][1] * c0) / (y * y));
+        sum += c[i];
+    }
+    sum = 1.f / sum;
+    for (int i = 0; i < 8; i++) c[i] *= sum;
+}
+
+// Lanczos4 taps of destinations [d0, d0 + n) of an ssize -> dsize axis (x: the anchor clamped as
+// cv::resize does for columns; y: raw, the rows clipped per tap on use).
+void lanczos4_taps(int ssize, double scale, int d0, int n, bool clamp, std::vector<GrTap>& out)
+{
+    for (int d = d0; d < d0 + n; d++) {
+        float f = (float)((d + 0.5) * scale - 0.5);
+        int   s = (int)std::floor(f);
+        f -= (float)s;
+        if (clamp && s < 0) f = 0, s = 0;
+        if (clamp && s >= ssize - 1) f = 0, s = ssize - 1;
+        float c[8];
+        lanczos4_coeffs(f, c);
+        GrTap t{};
+        t.s = s;
+        for (int k = 0; k < 8; k++) t.c[k] = (int16_t)std::min(std::max((int)std::rint(c[k] * 2048.f), -32768), 32767);
+        out.push_back(t);
+    }
+}
+
+// One resize_generic launch: its jobs, the Lanczos tap tables, and the tile shape every job of it
+// shares (rows x columns of a tile sized so the taps and the horizontal sums fit 64 KiB of LDS).
+struct GrPlan {
+    std::vector<ResizeJob> jobs;
+    std::vector<GrTap>     taps;
+    size_t                 off = 0, taps_off = 0; // byte offsets in the call's table
+    int TR = 16, CW = 128, NR = 1, xs = 3, amax = 1, cn_max = 1, max_tiles = 0;
+    double bytes = 0; // algorithmic: the source region read once + the window written
+
+    void add(ResizeJob R)
+    {
+        if (R.method == GR_LANCZOS4) {
+            R.coef_x = (int32_t)(taps.size() * sizeof(GrTap)); // relative until the table is laid out
+            lanczos4_taps(R.crop_w, R.scale_x, R.win_x, R.win_w, true, taps);
+            R.coef_y = (int32_t)(taps.size() * sizeof(GrTap));
+            lanczos4_taps(R.crop_h, R.scale_y, R.win_y, R.win_h, false, taps);
+        }
+        jobs.push_back(R);
+    }
+    // rows of H a tile of `tr` output rows needs at most
+    int rows_for(int tr) const
+    {
+        int nr = 1;
+        for (const ResizeJob& R : jobs) {
+            const int K = R.method == GR_CUBIC ? 4 : (R.method == GR_LANCZOS4 ? 8 : 2);
+            if (R.method == GR_AREA) nr = std::max(nr, (int)std::ceil(tr * R.scale_y) + 3);
+            else if (R.method != GR_AREA_FAST) nr = std::max(nr, (int)std::ceil((tr - 1) * R.scale_y) + K + 2);
+        }
+        return nr;
+    }
+    void finalize()
+    {
+        if (jobs.empty()) return;
+        int K = 2, ww = 1;
+        for (const ResizeJob& R : jobs) {
+            K = std::max(K, R.method == GR_CUBIC ? 4 : (R.method == GR_LANCZOS4 ? 8 : 2));
+            if (R.method == GR_AREA)
+                amax = std::max(amax, (int)std::ceil(std::max(R.scale_x, R.scale_y)) + 3);
+            cn_max = std::max(cn_max, R.cn);
+            ww     = std::max(ww, R.win_w);
+        }
+        xs = std::max(1 + K, 2 + amax);
+        CW = std::min(128, ww);
+        TR = 16;
+        auto lds = [&] { return ((size_t)CW * xs + (size_t)TR * xs + (size_t)rows_for(TR) * CW * cn_max) * 4; };
+        while (lds() > kGenericLds && TR > 1) TR--;
+        while (lds() > kGenericLds && CW > 8) CW /= 2;
+        if (lds() > kGenericLds) fail(AEON_HIP_EUNSUPPORTED, "resize scale too large for the generic resize's LDS tiles");
+        NR        = rows_for(TR);
+        max_tiles = 0;
+        bytes     = 0;
+        for (ResizeJob& R : jobs) {
+            R.tiles_x = (R.win_w + CW - 1) / CW;
+            R.tiles   = R.tiles_x * ((R.win_h + TR - 1) / TR);
+            max_tiles = std::max(max_tiles, R.tiles);
+            bytes += (double)R.crop_w * R.crop_h * R.cn * ((double)R.win_w / R.dst_w) * ((double)R.win_h / R.dst_h) +
+                     (double)R.win_w * R.win_h * R.cn;
+        }
+    }
+    static constexpr size_t kGenericLds = 64 * 1024;
+};
+
+// A resize of the (cropped, padded) region of J's source to its window, into scratch at `off`.
+ResizeJob resize_job(const AugJob& J, int method, int isx, int isy)
+{
+    ResizeJob R{};
+    R.scale_x = J.scale_x, R.scale_y = J.scale_y;
+    R.inv_x = (double)J.dst_w / J.crop_w, R.inv_y = (double)J.dst_h / J.crop_h;
+    R.src_ptr = J.src_ptr, R.src_scratch = J.src_scratch;
+    R.src_stride = J.src_stride, R.cn = J.cn;
+    R.crop_x = J.crop_x, R.crop_y = J.crop_y, R.crop_w = J.crop_w, R.crop_h = J.crop_h;
+    R.shift_x = J.shift_x, R.shift_y = J.shift_y, R.padded = J.padded;
+    R.dst_w = J.dst_w, R.dst_h = J.dst_h;
+    R.win_x = J.win_x, R.win_y = J.win_y, R.win_w = J.win_w, R.win_h = J.win_h;
+    R.method = method, R.isx = isx, R.isy = isy;
+    return R;
+}
+
+// Launch order: rot (image::rotate) -> exp (image::expand) -> gr_short / pre (resize_short, generic
+// or tile) -> gr_main (CUBIC / LANCZOS4 / AREA resize of the crop) -> pre2 (2x-area resize ahead of
+// photometric stages) -> pass1 (contrast statistics) -> main; each reads only what an earlier group
+// wrote.
 void plan_image(const aeon_img_desc& d, const void* src_base, const aeon_aug_params& p,
                 const aeon_out_desc& o, uint8_t* out_item, bool is_mask, std::vector<RotJob>& rot,
-                std::vector<ExpandJob>& exp, LaunchPlan& pre, LaunchPlan& pre2, LaunchPlan& pass1, LaunchPlan& main,
-                size_t& scratch_bytes)
+                std::vector<ExpandJob>& exp, GrPlan& gr_short, LaunchPlan& pre, GrPlan& gr_main, LaunchPlan& pre2,
+                LaunchPlan& pass1, LaunchPlan& main, size_t& scratch_bytes)
 {
     validate_record(d, p, o, is_mask);
     const int cn = d.channels;
@@ -439,12 +583,42 @@ void plan_image(const aeon_img_desc& d, const void* src_base, const aeon_aug_par
         size_t off = (scratch_bytes + 15) & ~(size_t)15;
         scratch_bytes = off + (size_t)p.crop_w * p.crop_h * cn + 16;
         P.out_ptr = off; // relocated to the slot's scratch by the caller
-        pre.jobs.push_back(P);
+        int       isx = 0, isy = 0;
+        const int gm  = generic_method(bw, bh, rw, rh, p.interp, cn, &isx, &isy);
+        if (gm >= 0) {
+            ResizeJob R   = resize_job(P, gm, isx, isy);
+            R.out_ptr     = off;
+            R.out_scratch = 1;
+            gr_short.add(R);
+        } else {
+            pre.jobs.push_back(P);
+        }
         J.src_ptr = off; // likewise
         J.src_bytes  = (uint64_t)p.crop_w * p.crop_h * cn;
         J.src_w = p.crop_w, J.src_h = p.crop_h, J.src_stride = p.crop_w * cn;
         J.crop_x = 0, J.crop_y = 0;
         J.src_scratch = 1; // relocated to the slot's scratch by the caller
+    }
+    int isx = 0, isy = 0;
+    const int gm = is_mask ? -1 : generic_method(J.crop_w, J.crop_h, J.dst_w, J.dst_h, p.interp, cn, &isx, &isy);
+    if (gm >= 0) {
+        // CUBIC / LANCZOS4 / INTER_AREA resize of the (padded) crop into scratch (resize_kernels.hip),
+        // then the photometric stages, flip and the loader as a copy pass over it
+        ResizeJob R   = resize_job(J, gm, isx, isy);
+        size_t    off = (scratch_bytes + 15) & ~(size_t)15;
+        scratch_bytes = off + (size_t)J.win_w * J.win_h * cn + 16;
+        R.out_ptr     = off; // relocated to the slot's scratch by the caller
+        R.out_scratch = 1;
+        gr_main.add(R);
+        J.src_ptr     = off;
+        J.src_scratch = 1;
+        J.src_bytes   = (uint64_t)J.win_w * J.win_h * cn;
+        J.src_w = J.win_w, J.src_h = J.win_h, J.src_stride = J.win_w * cn;
+        J.crop_x = J.crop_y = 0, J.crop_w = J.win_w, J.crop_h = J.win_h;
+        J.shift_x = J.shift_y = J.padded = 0;
+        J.mode    = RESIZE_COPY;
+        J.scale_x = J.scale_y = 1.0;
+        J.xv      = simd_boundary(J.win_w * cn);
     }
     const int photo = J.photo;
     if (photo && J.mode == RESIZE_AREA2X) {
@@ -835,6 +1009,7 @@ bool run_direct(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void
         if (d.elem_bytes != 0 && d.elem_bytes != 1) return false;
         if (is_mask && d.channels == 1 && o.channels == 1 && p.angle == 0) return false; // mask gather pass
         if (p.angle != 0 || (!is_mask && (p.resize_short_size > 0 || expands(p)))) return false;
+        if (!is_mask && p.interp > AEON_INTERP_NEAREST) return false; // CUBIC / AREA / LANCZOS4 (plan_image)
         validate_record(d, p, o, is_mask);
         const int photo = is_mask ? 0 : photo_flags(p);
         const int mode  = choose_mode(p.crop_w, p.crop_h, p.out_w, p.out_h, is_mask ? AEON_INTERP_NEAREST : p.interp,
@@ -934,6 +1109,7 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
         return 0;
 
     LaunchPlan             pre_all, pre2_all, pass1_all, main_all;
+    GrPlan                 gr_short, gr_main;
     std::vector<RotJob>    rot;
     std::vector<ExpandJob> exp;
     std::vector<Mask16Job> m16;
@@ -946,8 +1122,8 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
                              (descs[i].elem_bytes == 0 || descs[i].elem_bytes == 1));
         if (gather) plan_mask16(descs[i], src_base, params[i], o, item, is_mask, m16, rot, scratch_bytes);
         else if (descs[i].elem_bytes == 0 || descs[i].elem_bytes == 1)
-            plan_image(descs[i], src_base, params[i], o, item, is_mask, rot, exp, pre_all, pre2_all, pass1_all,
-                       main_all, scratch_bytes);
+            plan_image(descs[i], src_base, params[i], o, item, is_mask, rot, exp, gr_short, pre_all, gr_main, pre2_all,
+                       pass1_all, main_all, scratch_bytes);
         else fail(AEON_HIP_EINVAL, "elem_bytes must be 1 (CV_8U) or 2 (CV_16U)");
     }
 
@@ -971,6 +1147,18 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
     const size_t     m16_off   = rot_off + rot.size() * sizeof(RotJob);
     const size_t     exp_off   = m16_off + m16.size() * sizeof(Mask16Job);
     size_t           blob      = exp_off + exp.size() * sizeof(ExpandJob);
+    for (GrPlan* g : {&gr_short, &gr_main}) { // jobs, then their Lanczos taps (offsets made absolute)
+        if (g->jobs.empty()) continue;
+        g->finalize();
+        blob        = (blob + 15) & ~(size_t)15;
+        g->off      = blob;
+        blob += g->jobs.size() * sizeof(ResizeJob);
+        g->taps_off = blob;
+        blob += g->taps.size() * sizeof(GrTap);
+        for (ResizeJob& R : g->jobs)
+            if (R.method == GR_LANCZOS4) R.coef_x += (int32_t)g->taps_off, R.coef_y += (int32_t)g->taps_off;
+    }
+    blob = (blob + 15) & ~(size_t)15;
     int              exp_max_px = 0;
     for (const ExpandJob& E : exp) exp_max_px = std::max(exp_max_px, E.ew * E.eh);
     int              m16_max_h = 0, m16_max_w = 0, m16_max_seg = 0;
@@ -1037,6 +1225,15 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
         if (E.src_scratch) E.src_ptr += (uint64_t)s.scratch;
     }
     if (!exp.empty()) std::memcpy(s.host + exp_off, exp.data(), exp.size() * sizeof(ExpandJob));
+    for (GrPlan* g : {&gr_short, &gr_main}) {
+        if (g->jobs.empty()) continue;
+        for (ResizeJob& R : g->jobs) {
+            if (R.src_scratch) R.src_ptr += (uint64_t)s.scratch;
+            if (R.out_scratch) R.out_ptr += (uint64_t)s.scratch;
+        }
+        std::memcpy(s.host + g->off, g->jobs.data(), g->jobs.size() * sizeof(ResizeJob));
+        if (!g->taps.empty()) std::memcpy(s.host + g->taps_off, g->taps.data(), g->taps.size() * sizeof(GrTap));
+    }
     if (!rot.empty()) std::memcpy(s.host + rot_off, rot.data(), rot.size() * sizeof(RotJob));
     if (!m16.empty()) std::memcpy(s.host + m16_off, m16.data(), m16.size() * sizeof(Mask16Job));
     for (auto* v : {&pre, &pre2, &pass1, &main})
@@ -1085,9 +1282,24 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
                               timed ? t.start : nullptr, timed ? t.stop : nullptr));
         if (timed) ctx->timers.push_back(t);
     }
-    for (auto* v : {&pre, &pre2})
-        for (LaunchPlan& P : *v)
-            if (!P.jobs.empty()) timed_launch(ctx, KM_RAW, P, args(P), stream, launch_bytes(P.jobs, KM_RAW, 1), timed);
+    auto generic = [&](const GrPlan& g) {
+        if (g.jobs.empty()) return;
+        KernelTimer t{};
+        if (timed) t = take_timer(ctx, KM_RAW, g.bytes);
+        if (timed) HIP_OK(hipEventRecord(t.start, stream));
+        HIP_OK(launch_resize_generic((const ResizeJob*)(table + g.off), table, (int)g.jobs.size(), g.max_tiles, g.TR, g.CW,
+                                     g.NR, g.xs, g.amax, g.cn_max, ctx->d_error, stream));
+        if (timed) {
+            HIP_OK(hipEventRecord(t.stop, stream));
+            ctx->timers.push_back(t);
+        }
+    };
+    generic(gr_short);
+    for (LaunchPlan& P : pre)
+        if (!P.jobs.empty()) timed_launch(ctx, KM_RAW, P, args(P), stream, launch_bytes(P.jobs, KM_RAW, 1), timed);
+    generic(gr_main);
+    for (LaunchPlan& P : pre2)
+        if (!P.jobs.empty()) timed_launch(ctx, KM_RAW, P, args(P), stream, launch_bytes(P.jobs, KM_RAW, 1), timed);
     for (LaunchPlan& P : pass1)
         if (!P.jobs.empty())
             timed_launch(ctx, KM_STATS, P, args(P), stream, launch_bytes(P.jobs, KM_STATS, oelem), timed);

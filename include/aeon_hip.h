@@ -44,6 +44,9 @@ extern "C" {
 /* resize interpolation (image::config "interpolation_method") */
 #define AEON_INTERP_LINEAR 0
 #define AEON_INTERP_NEAREST 1
+#define AEON_INTERP_CUBIC 2    /* cv::INTER_CUBIC (a resize pre-pass, resize_kernels.hip) */
+#define AEON_INTERP_AREA 3     /* cv::INTER_AREA (2x box in the tile kernel, else a pre-pass) */
+#define AEON_INTERP_LANCZOS4 4 /* cv::INTER_LANCZOS4 (a resize pre-pass) */
 
 typedef struct aeon_hip_ctx aeon_hip_ctx;
 typedef struct aeon_param_factory aeon_param_factory;

@@ -29,8 +29,7 @@ def oracle_aug_config(aug):
             kw[key] = aug[key]
     if "fixed_scaling_factor" in aug:
         kw["fixed_scaling_factor"] = aug["fixed_scaling_factor"]
-    if aug.get("interpolation_method", "LINEAR").upper() == "NEAREST":
-        kw["interp"] = 1
+    kw["interp"] = O.INTERP[aug.get("interpolation_method", "LINEAR").upper()]
     if "expand_ratio" in aug:
         kw["expand_ratio_min"], kw["expand_ratio_max"] = aug["expand_ratio"]
     if "expand_probability" in aug:
