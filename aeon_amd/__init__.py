@@ -374,10 +374,10 @@ class Context:
         _check(lib().aeon_hip_set_timing(self._h, int(every)))
 
     def kernel_times(self):
-        """{'augment'|'stats'|'resize_short': (total_ms, total_algorithmic_bytes, launches)}"""
-        ms, by, ct = (ctypes.c_double * 3)(), (ctypes.c_double * 3)(), (ctypes.c_long * 3)()
+        """{'augment'|'stats'|'pre'|'jpeg': (total_ms, total_algorithmic_bytes, launches)}"""
+        ms, by, ct = (ctypes.c_double * 4)(), (ctypes.c_double * 4)(), (ctypes.c_long * 4)()
         _check(lib().aeon_hip_kernel_times(self._h, ms, by, ct))
-        return {k: (ms[i], by[i], ct[i]) for i, k in enumerate(("augment", "stats", "resize_short"))}
+        return {k: (ms[i], by[i], ct[i]) for i, k in enumerate(("augment", "stats", "pre", "jpeg"))}
 
     def synchronize(self, stream=0):
         _check(lib().aeon_hip_synchronize(self._h, ctypes.c_void_p(stream or 0)))

@@ -2,6 +2,7 @@
 #include "host.hpp"
 
 #include <hip/hip_runtime.h>
+#include <rocprofiler-sdk-roctx/roctx.h>
 #include <sched.h>
 
 #include <algorithm>
@@ -537,6 +538,15 @@ void* zero_copy_view(void* p)
     return (uint8_t*)a.devicePointer + ((uint8_t*)p - (uint8_t*)a.hostPointer);
 }
 
+// A roctx range over one host phase of a decode window (rocprofv3 --marker-trace shows them
+// next to the kernels: draw, stage, jpeg, augment, transpose, d2h).
+struct phase_range {
+    explicit phase_range(const char* name) { roctxRangePush(name); }
+    ~phase_range() { roctxRangePop(); }
+    phase_range(const phase_range&) = delete;
+    phase_range& operator=(const phase_range&) = delete;
+};
+
 void grow_dev(uint8_t*& p, size_t& cap, size_t bytes)
 {
     if (bytes <= cap) return;
@@ -622,13 +632,21 @@ void batch_decoder::enqueue(window_slot& ws, int n, const decoded_element* in, v
     // order on this thread -- aeon's single-threaded order, the only reproducible one, since
     // the lighting normal_distribution caches a value inside the shared factory -- and the
     // pool threads stage the pixels into the pinned arena.
-    for (int i = 0; i < n; i++)
-        m_provider->draw(i, records.data() + (size_t)i * ne, w, m_deterministic ? m_random[i] : m_local_random);
+    {
+        phase_range r("aeon.draw");
+        for (int i = 0; i < n; i++)
+            m_provider->draw(i, records.data() + (size_t)i * ne, w, m_deterministic ? m_random[i] : m_local_random);
+    }
     if (staged) {
-        m_pool->run(n, [&](int i) { m_provider->stage(i, records.data() + (size_t)i * ne, w); });
+        {
+            phase_range r("aeon.stage");
+            m_pool->run(n, [&](int i) { m_provider->stage(i, records.data() + (size_t)i * ne, w); });
+        }
+        phase_range r("aeon.h2d_enqueue");
         hip_check(hipMemcpyAsync(ws.dev_src, ws.pinned, staged, hipMemcpyHostToDevice, stream), "hipMemcpyAsync");
     }
     for (int k = 0; k < ne; k++) {
+        phase_range r("aeon.jpeg");
         std::vector<const void*> files;
         std::vector<size_t>      sizes;
         std::vector<aeon_img_desc> descs;
@@ -655,6 +673,7 @@ void batch_decoder::enqueue(window_slot& ws, int n, const decoded_element* in, v
             copy_out[k] = true;
         }
     }
+    phase_range launch("aeon.launch");
     if (m_batch_major) {
         m_provider->post_process(m_ctx, w, ws.dev_src, outs.data(), stream);
     } else {
@@ -676,10 +695,12 @@ void batch_decoder::enqueue(window_slot& ws, int n, const decoded_element* in, v
         }
     }
     for (int k = 0; k < ne; k++)
-        if (copy_out[k])
+        if (copy_out[k]) {
+            phase_range d2h("aeon.d2h_enqueue");
             hip_check(hipMemcpyAsync(outputs[k], outs[k], (size_t)n * m_provider->providers()[k]->shape().byte_size(),
                                      hipMemcpyDeviceToHost, stream),
                       "hipMemcpyAsync");
+        }
     if (!ws.done) hip_check(hipEventCreateWithFlags(&ws.done, hipEventDisableTiming), "hipEventCreate");
     hip_check(hipEventRecord(ws.done, stream), "hipEventRecord");
     ws.pending = true;

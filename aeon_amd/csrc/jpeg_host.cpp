@@ -22,7 +22,7 @@
 
 namespace aeon_hip {
 hipError_t launch_jpeg(const JpegImage* imgs, const JpegChunk* chunks, int n_chunks, const JpegRows* rows, int n_rows,
-                       hipStream_t stream);
+                       int color_lds, hipStream_t stream);
 
 namespace {
 
@@ -708,8 +708,9 @@ void jpeg_state_destroy(JpegState* s)
 
 // The decode call (aeon_hip_decode_jpeg_batch): entropy-decode every file on the pool, stage the
 // coefficient streams + tables in one pinned buffer, one H2D, IDCT and colour kernels on `stream`.
+// start / stop (may be null): events recorded around the IDCT + colour launches (kernel timing)
 void jpeg_decode_batch(JpegState* S, int n, const void* const* data, const size_t* sizes, const aeon_img_desc* descs,
-                       void* dst_base, hipStream_t stream)
+                       void* dst_base, hipStream_t stream, hipEvent_t start, hipEvent_t stop)
 {
     std::lock_guard<std::mutex> lock(S->mu);
     for (auto& a : S->arenas) a.used = 0;
@@ -737,6 +738,7 @@ void jpeg_decode_batch(JpegState* S, int n, const void* const* data, const size_
     std::vector<JpegRows>  rows;
     size_t                 plane_bytes = 0;
     std::vector<size_t>    plane_off(3 * (size_t)n, 0);
+    int                    color_lds = 0;
     for (int i = 0; i < n; i++) {
         const Frame& f  = frames[i];
         const int    nc = descs[i].channels == 1 ? 1 : f.ncomp; // grayscale output needs Y only
@@ -744,9 +746,21 @@ void jpeg_decode_batch(JpegState* S, int n, const void* const* data, const size_
             plane_off[3 * (size_t)i + k] = plane_bytes;
             plane_bytes += ((size_t)f.c[k].bw * 8 * f.c[k].bh * 8 + 255) & ~(size_t)255;
             const int nb = f.c[k].bw * f.c[k].bh;
-            for (int b = 0; b < nb; b += kJpegIdctLanes) chunks.push_back({i, k, b, std::min(kJpegIdctLanes, nb - b)});
+            for (int b = 0; b < nb; b += kJpegIdctBlocks) chunks.push_back({i, k, b, std::min(kJpegIdctBlocks, nb - b)});
         }
-        for (int y = 0; y < f.H; y += kJpegRowsPerWg) rows.push_back({i, y, std::min(kJpegRowsPerWg, f.H - y), 0});
+        // colour bands: as many rows as the staged plane rows of the band fit the LDS
+        int band = kJpegRowsPerWg, lds = 0;
+        for (;; band /= 2) {
+            lds = 0;
+            for (int k = 0; k < nc; k++) {
+                const int hf = f.hmax / f.c[k].h, vf = f.vmax / f.c[k].v;
+                lds += jpeg_stage_rows(jpeg_upsample_mode(hf, vf, f.c[k].dw), vf, band) * f.c[k].bw * 8;
+            }
+            if (lds <= kJpegColorLds || band == 1) break;
+        }
+        if (lds > kJpegColorLds) unsupported("image too wide for the colour pass's LDS rows");
+        color_lds = std::max(color_lds, lds);
+        for (int y = 0; y < f.H; y += band) rows.push_back({i, y, std::min(band, f.H - y), 0});
     }
     const size_t img_bytes = (size_t)n * sizeof(JpegImage);
     const size_t chk_off   = img_bytes;
@@ -777,6 +791,8 @@ void jpeg_decode_batch(JpegState* S, int n, const void* const* data, const size_
             J.planes[k] = (uint64_t)st.planes + plane_off[3 * (size_t)i + k];
             J.bw[k] = f.c[k].bw, J.bh[k] = f.c[k].bh, J.dw[k] = f.c[k].dw, J.dh[k] = f.c[k].dh;
             J.hs[k] = f.c[k].h, J.vs[k] = f.c[k].v;
+            J.hf[k] = f.hmax / f.c[k].h, J.vf[k] = f.vmax / f.c[k].v;
+            J.up[k] = jpeg_upsample_mode(J.hf[k], J.vf[k], f.c[k].dw);
             std::memcpy(J.q[k], f.q[f.c[k].tq], sizeof(J.q[k]));
         }
         J.values     = base + val[i];
@@ -790,9 +806,11 @@ void jpeg_decode_batch(JpegState* S, int n, const void* const* data, const size_
         if (S->arenas[w].used) std::memcpy(st.pinned + arena_off[w], S->arenas[w].host.data(), S->arenas[w].used);
     });
     hip_ok(hipMemcpyAsync(st.dev, st.pinned, total, hipMemcpyHostToDevice, stream), "hipMemcpyAsync");
+    if (start) hip_ok(hipEventRecord(start, stream), "hipEventRecord");
     hip_ok(launch_jpeg((const JpegImage*)st.dev, (const JpegChunk*)(st.dev + chk_off), (int)chunks.size(),
-                       (const JpegRows*)(st.dev + row_off), (int)rows.size(), stream),
+                       (const JpegRows*)(st.dev + row_off), (int)rows.size(), color_lds, stream),
            "JPEG kernels");
+    if (stop) hip_ok(hipEventRecord(stop, stream), "hipEventRecord");
     hip_ok(hipEventRecord(st.done, stream), "hipEventRecord");
     st.pending = true;
 }

@@ -41,7 +41,8 @@ hipError_t launch_upload_table(const void* host_dev, void* dst, size_t bytes, hi
 hipError_t launch_resize_generic(const ResizeJob* jobs, const uint8_t* table, int n_jobs, int max_tiles, int TR, int CW,
                                  int NR, int xs, int amax, int cn_max, int32_t* error, hipStream_t stream);
 void       jpeg_decode_batch(JpegState* S, int n, const void* const* data, const size_t* sizes,
-                             const aeon_img_desc* descs, void* dst_base, hipStream_t stream);
+                             const aeon_img_desc* descs, void* dst_base, hipStream_t stream, hipEvent_t start,
+                             hipEvent_t stop);
 void       jpeg_info(const void* data, size_t size, int* w, int* h, int* ncomp);
 void       jpeg_entropy_only(const void* data, size_t size, int* w, int* h, int* ncomp, int64_t* n_blocks,
                              int64_t* n_values, uint64_t* hash);
@@ -96,6 +97,7 @@ constexpr int kMaxLds        = 160 * 1024;
 constexpr int kStageBudget   = AEON_HIP_STAGE_BUDGET_KB * 1024; // preferred LDS bytes of the staging buffer
 constexpr int kStageBudgetHi = 140 * 1024;  // fallback for very wide crops
 constexpr size_t kUploadKernelMax = 128 * 1024; // job tables above this go up by SDMA (run_batch)
+constexpr size_t kDirectFetchMax  = 512 * 1024; // run_direct: most job bytes a launch's tiles read over PCIe
 
 // ---------------------------------------------------------------------------------------------
 // Per-image constants (aeon computes these on the host per record, too)
@@ -691,9 +693,10 @@ struct Slot {
 
 } // namespace
 
+constexpr int kTimerJpeg = 3; // KernelTimer kind of the JPEG kernels (after the KernelMode kinds)
 struct KernelTimer {
     hipEvent_t start, stop;
-    int        kind;   // KernelMode
+    int        kind;   // KernelMode, or kTimerJpeg
     double     bytes;  // algorithmic bytes of the launch
 };
 
@@ -735,13 +738,13 @@ struct aeon_hip_ctx {
     // optional per-launch timing (aeon_hip_set_timing): events recorded on the launch stream
     bool                     timing = false;
     std::vector<KernelTimer> timers, free_timers;
-    double                   ms[3]    = {0, 0, 0};
+    double                   ms[4]    = {0, 0, 0, 0};
     // AEON_HIP_HOST_PROFILE=1: host time per run_batch phase, printed when the context is destroyed
     bool                     host_profile = false;
     std::vector<double>      host_ns[8];  // per call, per phase
     long                     host_calls   = 0;
-    double                   bytes[3] = {0, 0, 0};
-    long                     count[3] = {0, 0, 0};
+    double                   bytes[4] = {0, 0, 0, 0};
+    long                     count[4] = {0, 0, 0, 0};
 };
 
 struct aeon_param_factory {
@@ -1035,6 +1038,10 @@ bool run_direct(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void
     P.rtab   = P.photo && o.dtype == AEON_DTYPE_F32;
     P.shape(geo);
     P.max_tiles = (max_h + P.tr - 1) / P.tr;
+    // every tile reads its job over PCIe: past ~512 KB of such reads per launch the multi-pass path's
+    // device table wins (C5's image launch, 4,096 tiles of 256 B: 98 vs 90 us of kernels per step;
+    // C2, 1,792 tiles: direct 3 us faster)
+    if ((size_t)P.max_tiles * n * sizeof(AugJob) > kDirectFetchMax) return false;
     phase(2);
     int         slot;
     Slot&       s     = take_slot(ctx, stream, slot);
@@ -1544,7 +1551,7 @@ int aeon_hip_kernel_times(aeon_hip_ctx* ctx, double* ms, double* bytes, long* co
             ctx->free_timers.push_back(t);
         }
         ctx->timers.clear();
-        for (int k = 0; k < 3; k++) {
+        for (int k = 0; k < 4; k++) {
             ms[k] = ctx->ms[k], bytes[k] = ctx->bytes[k], count[k] = ctx->count[k];
             ctx->ms[k] = ctx->bytes[k] = 0, ctx->count[k] = 0;
         }
@@ -1681,7 +1688,23 @@ int aeon_hip_decode_jpeg_batch(aeon_hip_ctx* ctx, int n, const void* const* data
         if (n == 0) return 0;
         HIP_OK(hipSetDevice(ctx->device));
         if (!ctx->jpeg) ctx->jpeg = jpeg_state_create();
-        jpeg_decode_batch(ctx->jpeg, n, data, sizes, descs, dst_base, (hipStream_t)stream);
+        KernelTimer t{};
+        bool        timed = false;
+        if (ctx->timing) {
+            std::lock_guard<std::mutex> lock(ctx->mu);
+            timed = (ctx->timing_calls++ % ctx->timing_every) == ctx->timing_every - 1;
+            if (timed) {
+                double px = 0;
+                for (int i = 0; i < n; i++) px += (double)descs[i].width * descs[i].height * descs[i].channels;
+                t = take_timer(ctx, kTimerJpeg, px);
+            }
+        }
+        jpeg_decode_batch(ctx->jpeg, n, data, sizes, descs, dst_base, (hipStream_t)stream, timed ? t.start : nullptr,
+                          timed ? t.stop : nullptr);
+        if (timed) {
+            std::lock_guard<std::mutex> lock(ctx->mu);
+            ctx->timers.push_back(t);
+        }
         return 0;
     });
 }

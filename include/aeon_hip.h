@@ -180,7 +180,9 @@ int aeon_hip_synchronize(aeon_hip_ctx* ctx, void* stream);
  * sample); 0 disables timing. */
 int aeon_hip_set_timing(aeon_hip_ctx* ctx, int every);
 /* Drain the timers: per kernel kind [0]=augment (final), [1]=contrast statistics,
- * [2]=resize_short pre-pass: total ms, total algorithmic bytes, launches. Resets the totals. */
+ * [2]=pre-passes (resize_short, CUBIC / AREA / LANCZOS4 resize, 2x-area ahead of photometric),
+ * [3]=JPEG IDCT + colour kernels of aeon_hip_decode_jpeg_batch (bytes: decoded pixels): total ms,
+ * total algorithmic bytes, launches -- arrays of 4.  Resets the totals. */
 int aeon_hip_kernel_times(aeon_hip_ctx* ctx, double* ms, double* bytes, long* count);
 
 /* ---- augmentation parameters (host) ------------------------------------------------------- */
