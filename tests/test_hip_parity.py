@@ -360,8 +360,13 @@ def test_empty_batch(ctx):
 def test_errors(ctx):
     img = A.synthetic_image(0, 64, 64)
     out = A.out_desc(**MEAN_OUT)
+    with pytest.raises(A.AeonHipError) as e:  # no cv::INTER_* value 9
+        H.hip_records(ctx, [img], [A.aug_params(crop_w=64, crop_h=64, out_w=224, out_h=224, interp=9)], out)
+    assert e.value.code == A.AEON_HIP_EINVAL
+    bad = A.out_desc(**MEAN_OUT)
+    bad.dtype = 99
     with pytest.raises(A.AeonHipError) as e:
-        H.hip_records(ctx, [img], [A.aug_params(crop_w=64, crop_h=64, out_w=224, out_h=224, interp=2)], out)
+        H.hip_records(ctx, [img], [A.aug_params(crop_w=64, crop_h=64, out_w=224, out_h=224)], bad)
     assert e.value.code == A.AEON_HIP_EUNSUPPORTED
     with pytest.raises(A.AeonHipError) as e:
         H.hip_records(ctx, [img], [A.aug_params(crop_x=10, crop_w=64, crop_h=64, out_w=224, out_h=224)], out)
