@@ -150,6 +150,7 @@ def lib():
                                                P(ctypes.c_int)]
         L.aeon_decoder_decode.argtypes = [vp, ctypes.c_int, P(RecordElem), P(vp), ctypes.c_int, vp]
         L.aeon_decoder_decode_encoded.argtypes = [vp, ctypes.c_int, P(EncodedElem), P(vp), ctypes.c_int, vp]
+        L.aeon_decoder_draw_params.argtypes = [vp, ctypes.c_int, P(RecordElem), P(AugParams), ctypes.c_int]
         L.aeon_decoder_submit.argtypes = [vp, ctypes.c_int, P(EncodedElem), P(vp), ctypes.c_int]
         L.aeon_decoder_wait.argtypes = [vp]
         L.aeon_decoder_last_error.restype = ctypes.c_char_p
@@ -500,6 +501,20 @@ class Decoder:
                 elems[i * ne + k] = RecordElem(a.ctypes.data, w, h, cn, w * cn)
         _check_host(lib().aeon_decoder_decode(self._h, n, elems, ptrs, 0, ctypes.c_void_p(stream or 0)))
         return outs
+
+    def draw_params(self, sizes, serial=False):
+        """The draw phase of one window alone (aeon_decoder_draw_params, host only): sizes = one
+        (width, height) per record (of its first element; the others get the same size); returns
+        the records' AugParams.  The slot engines advance as in a real window."""
+        n, ne = len(sizes), len(self.outputs)
+        elems = (RecordElem * (n * ne))()
+        dummy = ctypes.c_uint8(0)
+        for i, (w, h) in enumerate(sizes):
+            for k in range(ne):
+                elems[i * ne + k] = RecordElem(ctypes.addressof(dummy), w, h, 3, w * 3)
+        out = (AugParams * max(n, 1))()
+        _check_host(lib().aeon_decoder_draw_params(self._h, n, elems, out, int(serial)))
+        return list(out[:n])
 
     def submit(self, records, output_ptrs, on_device=False):
         """Double-buffered window (aeon_decoder_submit): output_ptrs[k] = address of n items of

@@ -190,14 +190,19 @@ public:
         }
     }
     void provide(int, const decoded_element& in, augmentation& aug, std::minstd_rand0& random,
-                 aeon_aug_params& params) const override
+                 aeon_aug_params& params, light_split* ls) const override
     {
         if (!aug.has) {
-            m_factory.make_params(random, in.width, in.height, (int)m_cfg.width, (int)m_cfg.height, &aug.image);
+            if (ls)
+                m_factory.make_params_split(random, in.width, in.height, (int)m_cfg.width, (int)m_cfg.height,
+                                            ls->entry_avail, &aug.image, &ls->exit_saved);
+            else
+                m_factory.make_params(random, in.width, in.height, (int)m_cfg.width, (int)m_cfg.height, &aug.image);
             aug.has = true;
         }
         params = aug.image;
     }
+    const param_factory& factory() const override { return m_factory; }
     bool               is_mask() const override { return false; }
     const shape_type&  shape() const override { return m_cfg.shape; }
     const std::string& buffer_name() const override { return m_name; }
@@ -231,14 +236,19 @@ public:
     {
     }
     void provide(int, const decoded_element& in, augmentation& aug, std::minstd_rand0& random,
-                 aeon_aug_params& params) const override
+                 aeon_aug_params& params, light_split* ls) const override
     {
         if (!aug.has) {
-            m_factory.make_params(random, in.width, in.height, (int)m_cfg.width, (int)m_cfg.height, &aug.image);
+            if (ls)
+                m_factory.make_params_split(random, in.width, in.height, (int)m_cfg.width, (int)m_cfg.height,
+                                            ls->entry_avail, &aug.image, &ls->exit_saved);
+            else
+                m_factory.make_params(random, in.width, in.height, (int)m_cfg.width, (int)m_cfg.height, &aug.image);
             aug.has = true;
         }
         params = aug.image;
     }
+    const param_factory& factory() const override { return m_factory; }
     bool               is_mask() const override { return true; }
     const shape_type&  shape() const override { return m_cfg.shape; }
     const std::string& buffer_name() const override { return m_name; }
@@ -289,7 +299,8 @@ void provider_base::provide(int idx, const decoded_element* elems, decode_window
     stage(idx, elems, w);
 }
 
-void provider_base::draw(int idx, const decoded_element* elems, decode_window& w, std::minstd_rand0& random) const
+void provider_base::draw(int idx, const decoded_element* elems, decode_window& w, std::minstd_rand0& random,
+                         light_split* ls) const
 {
     augmentation aug;
     for (size_t k = 0; k < m_providers.size(); k++) {
@@ -300,8 +311,46 @@ void provider_base::draw(int idx, const decoded_element* elems, decode_window& w
                << " with size 0, at idx " << idx;
             throw std::runtime_error(ss.str());
         }
-        m_providers[k]->provide(idx, e, aug, random, w.params[k][idx]);
+        m_providers[k]->provide(idx, e, aug, random, w.params[k][idx], ls);
     }
+}
+
+// aeon runs provide() -- make_params included -- on its pool threads (batch_decoder.cpp:62-71); with
+// one engine per record the draws are independent but for the lighting normal_distribution's cache
+// inside the shared factory (augment_image.hpp:153-185), which passes one value from a record to the
+// next.  Record i makes exactly three normal draws, each toggling the cache, so whether it starts
+// with a cached value is known before any record is drawn: every record draws on the pool with that
+// entry state (make_params_split), and one in-order pass hands each cached value to the next record.
+// The params equal the in-order loop's bit for bit (tests/test_host.py draw-window tests).
+void provider_base::draw_window(int n, const decoded_element* records, decode_window& w,
+                                std::vector<std::minstd_rand0>& engines, thread_pool& pool) const
+{
+    const size_t ne = m_providers.size();
+    const param_factory& F = m_providers[0]->factory(); // the first element draws (aug.has after it)
+    const bool               lit = F.lighting_on();
+    std::vector<light_split> ls(lit ? n : 0);
+    const bool               a0 = F.light_avail();
+    for (int i = 0; i < (int)ls.size(); i++) ls[i].entry_avail = a0 != ((i & 1) != 0);
+    // tasks of 32 consecutive records, each engine drawn from a local copy: eight engines share a
+    // cache line, and threads drawing neighbouring records through them made the pool slower than
+    // one thread (C3 window of 1024: 399 vs 374 us)
+    constexpr int kChunk = 32;
+    pool.run((n + kChunk - 1) / kChunk, [&](int t) {
+        for (int i = t * kChunk; i < std::min(n, (t + 1) * kChunk); i++) {
+            std::minstd_rand0 e = engines[i];
+            draw(i, records + (size_t)i * ne, w, e, lit ? &ls[i] : nullptr);
+            engines[i] = e;
+        }
+    });
+    if (!lit) return;
+    float cached = F.light_saved();
+    for (int i = 0; i < n; i++) {
+        if (ls[i].entry_avail)
+            for (size_t k = 0; k < ne; k++) w.params[k][i].lighting[0] = cached;
+        else
+            cached = ls[i].exit_saved;
+    }
+    F.set_light_state(!ls[n - 1].entry_avail, cached);
 }
 
 void provider_base::stage(int idx, const decoded_element* elems, decode_window& w) const
@@ -628,14 +677,16 @@ void batch_decoder::enqueue(window_slot& ws, int n, const decoded_element* in, v
     grow_dev(ws.dev_src, ws.dev_src_cap, total);
     w.arena = ws.pinned;
     // batch_decoder::process: the slot engine of record i draws its params (deterministic mode
-    // swaps the slot engine in and out, batch_decoder.cpp:62-71).  The draws run in record
-    // order on this thread -- aeon's single-threaded order, the only reproducible one, since
-    // the lighting normal_distribution caches a value inside the shared factory -- and the
-    // pool threads stage the pixels into the pinned arena.
+    // swaps the slot engine in and out, batch_decoder.cpp:62-71).  With slot engines the draws run
+    // on the pool (draw_window: aeon's in-order params exactly); then the pool threads stage the
+    // pixels into the pinned arena.
     {
         phase_range r("aeon.draw");
-        for (int i = 0; i < n; i++)
-            m_provider->draw(i, records.data() + (size_t)i * ne, w, m_deterministic ? m_random[i] : m_local_random);
+        if (m_deterministic) {
+            m_provider->draw_window(n, records.data(), w, m_random, *m_pool);
+        } else { // one engine for the window: in record order
+            for (int i = 0; i < n; i++) m_provider->draw(i, records.data() + (size_t)i * ne, w, m_local_random);
+        }
     }
     if (staged) {
         {
@@ -704,6 +755,23 @@ void batch_decoder::enqueue(window_slot& ws, int n, const decoded_element* in, v
     if (!ws.done) hip_check(hipEventCreateWithFlags(&ws.done, hipEventDisableTiming), "hipEventCreate");
     hip_check(hipEventRecord(ws.done, stream), "hipEventRecord");
     ws.pending = true;
+}
+
+void batch_decoder::draw_params(int n, const decoded_element* records, aeon_aug_params* params, bool serial)
+{
+    if (n <= 0) return;
+    const int ne = (int)m_provider->get_input_count();
+    if (m_deterministic) grow_slot_engines(n);
+    decode_window w;
+    w.n = n;
+    w.params.assign(ne, std::vector<aeon_aug_params>(n));
+    if (m_deterministic && !serial) {
+        m_provider->draw_window(n, records, w, m_random, *m_pool);
+    } else {
+        for (int i = 0; i < n; i++)
+            m_provider->draw(i, records + (size_t)i * ne, w, m_deterministic ? m_random[i] : m_local_random);
+    }
+    std::copy(w.params[0].begin(), w.params[0].end(), params);
 }
 
 void batch_decoder::decode(int n, const decoded_element* records, void* const* outputs, bool on_device, void* stream_)
@@ -891,6 +959,20 @@ int aeon_decoder_decode(aeon_decoder* d, int n, const aeon_record_elem* elems, v
     });
 }
 
+int aeon_decoder_draw_params(aeon_decoder* d, int n, const aeon_record_elem* elems, aeon_aug_params* params,
+                             int serial)
+{
+    return host_guarded([&] {
+        if (!d || (n > 0 && (!elems || !params))) throw std::invalid_argument("null argument");
+        const int ne = (int)d->d->provider().get_input_count();
+        std::vector<aeon_hip::decoded_element> recs((size_t)n * ne);
+        for (size_t i = 0; i < recs.size(); i++)
+            recs[i] = aeon_hip::decoded_element{(const uint8_t*)elems[i].data, elems[i].width, elems[i].height,
+                                                elems[i].channels,
+                                                elems[i].stride ? elems[i].stride : elems[i].width * elems[i].channels};
+        d->d->draw_params(n, recs.data(), params, serial != 0);
+    });
+}
 
 int aeon_decoder_decode_encoded(aeon_decoder* d, int n, const aeon_encoded_elem* elems, void* const* outputs,
                                 int outputs_on_device, void* stream)

@@ -105,13 +105,24 @@ protected:
     size_t                                          m_input_count = 0;
 };
 
+class thread_pool;
+
+// One record's share of a parallel window draw (param_factory::make_params_split): the lighting
+// cache state it starts from, and the value it leaves cached.
+struct light_split {
+    bool  entry_avail = false;
+    float exit_saved  = 0.f;
+};
+
 // One ETL element provider of the HIP stage (provider::image / provider::pixelmask).
 class etl_provider {
 public:
     virtual ~etl_provider() = default;
-    // host half of provide(): params for record idx (shared through aug) + its descriptor
+    // host half of provide(): params for record idx (shared through aug) + its descriptor; with ls,
+    // the record is drawn out of order (provider_base::draw_window)
     virtual void provide(int idx, const decoded_element& in, augmentation& aug, std::minstd_rand0& random,
-                         aeon_aug_params& params) const = 0;
+                         aeon_aug_params& params, light_split* ls = nullptr) const = 0;
+    virtual const param_factory& factory() const = 0;
     virtual bool               is_mask() const = 0;
     virtual const shape_type&  shape() const = 0;
     virtual const std::string& buffer_name() const = 0;
@@ -124,7 +135,12 @@ public:
     // record idx of the window: params for every ETL element from one shared augmentation
     // (provider_base::provide, provider.cpp:109-119), then its pixels into the pinned arena
     void provide(int idx, const decoded_element* elems, decode_window& w, std::minstd_rand0& random) const;
-    void draw(int idx, const decoded_element* elems, decode_window& w, std::minstd_rand0& random) const;
+    void draw(int idx, const decoded_element* elems, decode_window& w, std::minstd_rand0& random,
+              light_split* ls = nullptr) const;
+    // draw() for every record of a window with its own engine (deterministic mode), on the pool:
+    // the same params as the in-order loop (the lighting cache hand-off is fixed up afterwards)
+    void draw_window(int n, const decoded_element* records, decode_window& w, std::vector<std::minstd_rand0>& engines,
+                     thread_pool& pool) const;
     void stage(int idx, const decoded_element* elems, decode_window& w) const;
     // aeon's vestigial post_process hook, used as the per-window GPU flush: outputs[k] receives
     // n items of provider k (device pointers if on_device, else host memory)
@@ -180,6 +196,9 @@ public:
     // consumed (drawn, staged, entropy-decoded); outputs are complete after the matching wait().
     void submit(int n, const decoded_element* records, void* const* outputs, bool outputs_on_device);
     void wait(); // oldest submitted window
+    // the draw phase of one window alone (host only): params[i] = record i's (first element's)
+    // params; serial = the in-order loop instead of draw_window
+    void draw_params(int n, const decoded_element* records, aeon_aug_params* params, bool serial);
     int  outstanding() const { return (int)m_queue.size(); }
     provider_base& provider() { return *m_provider; }
     int            batch_size() const { return m_batch_size; }

@@ -58,6 +58,20 @@ public:
     template <typename URNG>
     void make_params(URNG& random, int in_w, int in_h, int out_w, int out_h, aeon_aug_params* p) const;
 
+    // make_params of one record of a decode window drawn out of order (the decoder's parallel draw):
+    // `lighting`'s cache (below) is the only state one record's draw hands to the next, and its
+    // availability at record i's entry is known up front (every record makes exactly three normal
+    // draws, each toggling it), so record i draws with its own engine as if the cache held
+    // `entry_avail`; a cached first value is left as NaN for the window's in-order fix-up
+    // (light_fixup), and a value the record leaves cached is returned in *exit_saved.
+    template <typename URNG>
+    void make_params_split(URNG& random, int in_w, int in_h, int out_w, int out_h, bool entry_avail,
+                           aeon_aug_params* p, float* exit_saved) const;
+    bool  lighting_on() const { return lighting.stddev() != 0; }
+    bool  light_avail() const { return m_light_avail; }
+    float light_saved() const { return m_light_saved; }
+    void  set_light_state(bool avail, float saved) const { m_light_avail = avail, m_light_saved = saved; }
+
     bool                do_area_scale        = false;
     bool                crop_enable          = true;
     bool                fixed_aspect_ratio   = false;
@@ -87,6 +101,32 @@ public:
 
     int interp_code() const; // AEON_INTERP_*
 
+private:
+    // std::normal_distribution<float>'s cache, restated (libstdc++ bits/random.tcc: the polar
+    // method makes a pair, returns one value and keeps the other for the next call): lighting
+    // draws go through light_draw, which makes each pair with a fresh distribution of the same
+    // param -- the pair depends only on the engine -- so the cache can be read, set and handed
+    // across records (make_params_split).
+    mutable bool  m_light_avail = false;
+    mutable float m_light_saved = 0.f;
+    template <typename URNG>
+    float light_draw(URNG& random) const
+    {
+        if (m_light_avail) {
+            m_light_avail = false;
+            return m_light_saved;
+        }
+        std::normal_distribution<float> d(lighting.param());
+        const float y = d(random);
+        m_light_saved = d(random); // the pair's cached second value: no engine draw
+        m_light_avail = true;
+        return y;
+    }
+    template <typename URNG>
+    void make_geometry(URNG& random, int in_w, int in_h, int out_w, int out_h, aeon_aug_params* p) const;
+
+public:
+
     // src/augment_image.cpp:232-301 (boxes: n x (xmin, ymin, xmax, ymax) boundingbox::box)
     template <typename URNG>
     void make_ssd_params(URNG& random, int in_w, int in_h, int out_w, int out_h, const float* boxes, int n_boxes,
@@ -109,6 +149,40 @@ inline int cv_roundf(float v) { return (int)std::nearbyintf(v); }
 template <typename URNG>
 void param_factory::make_params(URNG& random, int in_w, int in_h, int out_w, int out_h,
                                 aeon_aug_params* p) const
+{
+    make_geometry(random, in_w, in_h, out_w, out_h, p);
+    if (lighting.stddev() != 0) { // the last draws of make_params (augment_image.cpp:218-225)
+        for (int i = 0; i < 3; i++) p->lighting[i] = light_draw(random);
+        p->n_lighting      = 3;
+        p->color_noise_std = lighting.stddev();
+    }
+}
+
+template <typename URNG>
+void param_factory::make_params_split(URNG& random, int in_w, int in_h, int out_w, int out_h, bool entry_avail,
+                                      aeon_aug_params* p, float* exit_saved) const
+{
+    make_geometry(random, in_w, in_h, out_w, out_h, p);
+    if (lighting.stddev() == 0) return;
+    std::normal_distribution<float> d(lighting.param());
+    if (entry_avail) { // cached value first (light_fixup), then one pair from this engine: cache empty
+        p->lighting[0] = NAN;
+        p->lighting[1] = d(random);
+        p->lighting[2] = d(random);
+    } else { // two pairs from this engine; the second pair's other value stays cached
+        p->lighting[0] = d(random);
+        p->lighting[1] = d(random);
+        p->lighting[2] = d(random);
+        *exit_saved    = d(random);
+    }
+    p->n_lighting      = 3;
+    p->color_noise_std = lighting.stddev();
+}
+
+// make_params up to (not including) the lighting draws
+template <typename URNG>
+void param_factory::make_geometry(URNG& random, int in_w, int in_h, int out_w, int out_h,
+                                  aeon_aug_params* p) const
 {
     *p            = aeon_aug_params{};
     p->expand_ratio = 1.0f; // augment::image::params default (augment_image.hpp:99): make_params leaves it
@@ -177,11 +251,6 @@ void param_factory::make_params(URNG& random, int in_w, int in_h, int out_w, int
         p->crop_y = (int)((ish - ch) * oy);
         p->crop_w = cv_roundf(cw);          // cv::Rect(Point2i, Size2f) -> saturate_cast
         p->crop_h = cv_roundf(ch);
-    }
-    if (lighting.stddev() != 0) {
-        for (int i = 0; i < 3; i++) p->lighting[i] = lighting(random);
-        p->n_lighting      = 3;
-        p->color_noise_std = lighting.stddev();
     }
 }
 

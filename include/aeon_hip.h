@@ -266,6 +266,12 @@ int aeon_decoder_output_info(aeon_decoder* d, int index, char* name, size_t name
  * the window is complete (batch_decoder::filler, src/batch_decoder.cpp:73-99). */
 int aeon_decoder_decode(aeon_decoder* d, int n, const aeon_record_elem* elems, void* const* outputs,
                         int outputs_on_device, void* stream);
+/* The host half of a window alone (no GPU): batch_decoder::process's make_params for n records
+ * (src/batch_decoder.cpp:62-71, augment_image.cpp:107-230) with the decoder's slot engines, which
+ * advance as in a real window; params[i] = record i's params.  serial = 1 draws in record order on
+ * the calling thread, 0 on the decoder's pool (identical params).  Only elems' sizes are read. */
+int aeon_decoder_draw_params(aeon_decoder* d, int n, const aeon_record_elem* elems, aeon_aug_params* params,
+                             int serial);
 /* A record element as aeon's encoded_record holds it (src/buffer_batch.hpp:45-152): an encoded
  * JPEG file (width == 0: data/size, decoded by the JPEG stage with the provider's channel count),
  * or -- width > 0 -- decoded HWC uint8 pixels as in aeon_record_elem (pixel masks must be). */

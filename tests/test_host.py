@@ -157,3 +157,44 @@ def test_bench_synthetic_pool_matches_synthetic_image():
     L = 19 * 11 * 3
     for k, g in enumerate(recs):
         assert np.array_equal(pool[k * L:(k + 1) * L], A.synthetic_image(g, 19, 11, 3).reshape(-1))
+
+
+def _param_tuple(p):
+    return (p.crop_x, p.crop_y, p.crop_w, p.crop_h, p.flip, p.angle, p.hue, p.contrast, p.brightness,
+            p.saturation, tuple(p.lighting[:3]), p.n_lighting)
+
+
+@pytest.mark.parametrize("aug_name", ["C2", "C3"])
+def test_decoder_draw_window_matches_in_order_draws(aug_name):
+    """batch_decoder's parallel window draw (draw_window: every record on the pool with its slot
+    engine, the lighting normal_distribution's cached value handed on in one in-order pass) gives
+    the params of aeon's in-order draws: the decoder's own serial loop, and the oracle's factory
+    whose libstdc++ normal_distribution keeps the cache itself.  Windows of odd and even sizes so
+    the cache is both empty and full at window starts (batch_decoder.cpp:62-71)."""
+    from tests import helpers as H
+    import oracle as O
+    aug = {"C2": C.C2_AUG, "C3": C.C3_AUG}[aug_name]
+    cfg = dict(batch_size=1, random_seed=7, etl=[C.IMAGE_224], augmentation=[aug])
+    par, ser = A.Decoder(cfg), A.Decoder(cfg)
+    fac = O.Factory(H.oracle_aug_config(aug))
+    windows = [5, 130, 33, 64, 1]
+    states = O.seed_slots(7, max(windows))
+    rng = np.random.default_rng(3)
+    for n in windows:
+        sizes = [(int(rng.integers(200, 600)), int(rng.integers(200, 600))) for _ in range(n)]
+        a = par.draw_params(sizes, serial=False)
+        b = ser.draw_params(sizes, serial=True)
+        ref = []
+        for i, (w, h) in enumerate(sizes):
+            st = states[i:i + 1]
+            ref.append(fac.make_params(st, w, h, 224, 224))
+            states[i] = st[0]
+        for i in range(n):
+            assert _param_tuple(a[i]) == _param_tuple(b[i]), (n, i)
+            r = ref[i]
+            assert (a[i].crop_x, a[i].crop_y, a[i].crop_w, a[i].crop_h, a[i].flip, a[i].hue) == \
+                (r.crop_x, r.crop_y, r.crop_w, r.crop_h, r.flip, r.hue), (n, i)
+            assert (a[i].contrast, a[i].brightness, a[i].saturation) == (r.contrast, r.brightness, r.saturation)
+            assert tuple(a[i].lighting[:3]) == tuple(r.lighting[:3]), (n, i)
+    if aug_name == "C3":
+        assert any(p.lighting[0] != 0 for p in a)

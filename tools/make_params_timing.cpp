@@ -7,6 +7,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
+#include <string>
 #include <vector>
 
 int main()
@@ -37,6 +38,28 @@ int main()
         std::printf("%s: make_params x %d records: median %.1f us per window (%.3f us per record)\n", c[0], n, us[10],
                     us[10] / n);
         aeon_param_factory_destroy(f);
+        // the decoder's draw phase of a 1024-record window: in record order vs on its pool
+        const std::string dcfg = std::string(R"({"batch_size":32,"random_seed":1,"etl":[{"type":"image","height":224,)"
+                                             R"("width":224,"channels":3}],"augmentation":[)") + c[1] + "]}";
+        aeon_decoder* d = nullptr;
+        if (aeon_decoder_create(dcfg.c_str(), 0, &d) != 0) {
+            std::printf("%s: decoder create failed: %s\n", c[0], aeon_decoder_last_error());
+            return 1;
+        }
+        static uint8_t                px = 0;
+        std::vector<aeon_record_elem> el(n, aeon_record_elem{&px, 256, 256, 3, 768});
+        for (int serial = 1; serial >= 0; serial--) {
+            std::vector<double> ds;
+            for (int w = 0; w < 21; w++) {
+                auto t0 = std::chrono::steady_clock::now();
+                aeon_decoder_draw_params(d, n, el.data(), out.data(), serial);
+                ds.push_back(std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
+            }
+            std::sort(ds.begin(), ds.end());
+            std::printf("%s: decoder window draw x %d records, %s: median %.1f us\n", c[0], n,
+                        serial ? "in record order" : "on the pool", ds[10]);
+        }
+        aeon_decoder_destroy(d);
     }
     return 0;
 }
