@@ -37,7 +37,6 @@ int        rot_box_words(int angle);
 hipError_t launch_expand(const ExpandJob* jobs, int n_jobs, int max_pixels, hipStream_t stream);
 hipError_t launch_nearest(const Mask16Job* jobs, int n_jobs, int max_h, int max_w, int max_seg_bytes, int max_slots, hipStream_t stream,
                           hipEvent_t start, hipEvent_t stop);
-hipError_t launch_rows(const LaunchArgs& a, int grid, hipStream_t stream, hipEvent_t start, hipEvent_t stop);
 hipError_t launch_upload_table(const void* host_dev, void* dst, size_t bytes, hipStream_t stream);
 hipError_t launch_resize_generic(const ResizeJob* jobs, const uint8_t* table, int n_jobs, int max_tiles, int TR, int CW,
                                  int NR, int xs, int amax, int cn_max, int32_t* error, hipStream_t stream);
@@ -717,7 +716,6 @@ struct aeon_hip_ctx {
     // direct calls (run_direct): records of one job each, one launch group: the tile kernel reads
     // the jobs from the pinned slot itself
     bool                 direct = true; // AEON_HIP_DIRECT=0: the multi-pass path (device job table) for every call
-    int                  rows_tr = 28;  // augment_rows: output rows per workgroup (AEON_HIP_ROWS_TR; 0 = tile kernel)
     std::vector<JobGeom> geoms;              // reused per call
     JpegState*           jpeg = nullptr;     // JPEG decode stage (pool, staging ring), on first use
     std::vector<int> open_slots; // used since the last completion event, on open_stream
@@ -885,8 +883,10 @@ KernelTimer take_timer(aeon_hip_ctx* ctx, int kind, double bytes)
         t = ctx->free_timers.back();
         ctx->free_timers.pop_back();
     } else {
-        HIP_OK(hipEventCreate(&t.start));
-        HIP_OK(hipEventCreate(&t.stop));
+        // timing only: no system-scope fence (cache writeback + invalidate) when they complete,
+        // which cost the stream ~11 us of idle GPU per timed launch
+        HIP_OK(hipEventCreateWithFlags(&t.start, hipEventDisableSystemFence));
+        HIP_OK(hipEventCreateWithFlags(&t.stop, hipEventDisableSystemFence));
     }
     t.kind  = kind;
     t.bytes = bytes;
@@ -1008,13 +1008,10 @@ bool run_direct(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void
     geo.resize(n);
     int  key = -1, max_h = 0;
     bool vec_ok = !o.fixed_aspect_ratio;
-    bool rows_ok = !is_mask; // augment_rows: 3-channel, unpadded records
     for (int i = 0; i < n; i++) {
         const aeon_img_desc&   d = descs[i];
         const aeon_aug_params& p = params[i];
         if (d.elem_bytes != 0 && d.elem_bytes != 1) return false;
-        if (d.channels != 3 || !(p.padding == 0 || (p.pad_off_x == p.padding && p.pad_off_y == p.padding)))
-            rows_ok = false;
         if (is_mask && d.channels == 1 && o.channels == 1 && p.angle == 0) return false; // mask gather pass
         if (p.angle != 0 || (!is_mask && (p.resize_short_size > 0 || expands(p)))) return false;
         if (!is_mask && p.interp > AEON_INTERP_NEAREST) return false; // CUBIC / AREA / LANCZOS4 (plan_image)
@@ -1068,26 +1065,7 @@ bool run_direct(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void
                                 (size_t)o.canvas_w * o.canvas_h * o.channels * out_elem_bytes(od.dtype), n, stream));
     LaunchArgs a = launch_args(ctx, s, s.host_dev, P, n, o, d_lut, 1, ov.u8_map);
     a.jobs_host  = 1;
-    // the plain bilinear float32-CHW shape (C2, C5's images): the streaming kernel (rows_kernels.hip)
-    rows_ok = rows_ok && ctx->rows_tr > 0 && P.rm == RESIZE_LINEAR && !P.tail && !P.photo && vec_ok &&
-              o.dtype == AEON_DTYPE_F32 && o.channel_major && !ov.u8_map;
-    if (rows_ok) {
-        a.rows_per_tile = ctx->rows_tr;
-        a.max_tiles     = (max_h + ctx->rows_tr - 1) / ctx->rows_tr;
-        a.total_tiles   = a.max_tiles * n;
-        static const bool dev_jobs = [] { const char* e = std::getenv("AEON_HIP_ROWS_DEVJOBS"); return e && std::atoi(e); }();
-        if (dev_jobs) { // development A/B: the job table copied to device memory first
-            HIP_OK(hipMemcpyAsync(s.dev, s.host, (size_t)n * sizeof(AugJob), hipMemcpyHostToDevice, stream));
-            a.jobs      = (const AugJob*)s.dev;
-            a.jobs_host = 0;
-        }
-        KernelTimer t{};
-        if (timed) t = take_timer(ctx, KM_FINAL, launch_bytes(geo, KM_FINAL, 4));
-        HIP_OK(launch_rows(a, a.total_tiles, stream, timed ? t.start : nullptr, timed ? t.stop : nullptr));
-        if (timed) ctx->timers.push_back(t);
-    } else {
-        timed_launch(ctx, KM_FINAL, P, a, stream, launch_bytes(geo, KM_FINAL, out_elem_bytes(o.dtype)), timed);
-    }
+    timed_launch(ctx, KM_FINAL, P, a, stream, launch_bytes(geo, KM_FINAL, out_elem_bytes(o.dtype)), timed);
     phase(6);
     release_slot(ctx, slot, stream);
     phase(7);
@@ -1419,7 +1397,13 @@ int aeon_hip_ctx_create(int device, aeon_hip_ctx** out)
             HIP_OK(hipMalloc((void**)&c->d_hsv, sizeof(tab)));
             HIP_OK(hipMemcpy(c->d_hsv, tab, sizeof(tab), hipMemcpyHostToDevice));
             for (Slot& s : c->slots) {
-                HIP_OK(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
+                // the ring's completion events only tell the host that the GPU is done reading a
+                // slot: no system-scope fence needed (each one idled the GPU ~6 us between launches)
+#ifndef AEON_HIP_DONE_FENCE
+#define AEON_HIP_DONE_FENCE 0
+#endif
+                HIP_OK(hipEventCreateWithFlags(&s.done, hipEventDisableTiming |
+                                                            (AEON_HIP_DONE_FENCE ? 0 : hipEventDisableSystemFence)));
                 HIP_OK(hipEventCreateWithFlags(&s.copied, hipEventDisableTiming));
             }
             HIP_OK(hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
@@ -1429,7 +1413,6 @@ int aeon_hip_ctx_create(int device, aeon_hip_ctx** out)
             // diagnostics: host time per phase (printed at destroy); the multi-pass path for every call
             if (const char* e = std::getenv("AEON_HIP_HOST_PROFILE")) c->host_profile = std::atoi(e) != 0;
             if (const char* e = std::getenv("AEON_HIP_DIRECT")) c->direct = std::atoi(e) != 0;
-            if (const char* e = std::getenv("AEON_HIP_ROWS_TR")) c->rows_tr = std::max(0, std::atoi(e));
             HIP_OK(hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, device));
         } catch (...) {
             delete c;

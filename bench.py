@@ -45,8 +45,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the C3 and end-to-end side runs")
     ap.add_argument("--streams", type=int, default=1, help="development: alternate batches over N streams")
-    ap.add_argument("--timing-every", type=int, default=5,
-                    help="bracket the kernels of one step in N (the N-th, 2N-th, ...: not the first call after the idle barrier) with HIP events (0 = none)")
+    ap.add_argument("--timing-every", type=int, default=10,
+                    help="bracket the kernels of one step in N (the N-th, 2N-th, ...: not the first call after the idle barrier) "
+                         "with HIP events (0 = none); each timed launch idles the queue ~9 us around it")
     ap.add_argument("--cpu-extra-seconds", type=float, default=3.0,
                     help="CPU-baseline sample budget of each of C1/C3/C5")
     ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic_r02.json"))
