@@ -35,23 +35,31 @@ inline int out_elem_bytes(int dt)
     return dt == OUT_U8 || dt == OUT_S8 ? 1 : (dt == OUT_S16 || dt == OUT_U16 ? 2 : (dt == OUT_F64 ? 8 : 4));
 }
 
-// 16-byte aligned, plain data (copied H2D as an array).
+// 16-byte aligned, plain data (copied H2D as an array).  Every field a tile of a launch without
+// photometric stages reads lies in the first kJobHotBytes: such launches fetch only that half of
+// each job (a single-pass call's tiles read their jobs over PCIe from the caller's pinned slot).
 struct alignas(16) AugJob {
     double   scale_x, scale_y;  // OpenCV's 1/inv_scale (bilinear/nearest coefficient maths)
     uint64_t src_ptr;           // device address of the source image (HWC uint8)
     uint64_t src_bytes;         // bytes readable from src_ptr (buffer-descriptor range)
     uint64_t out_ptr;           // device address of the output item
-    int32_t  src_w, src_h, src_stride, cn;
+    int32_t  src_stride, cn;
     int32_t  crop_x, crop_y, crop_w, crop_h; // region fed to the resize
     int32_t  shift_x, shift_y, padded;       // add_padding (image.cpp:77-91) as a virtual zero
                                              // border: resize-source (u,v) reads crop
                                              // (u+shift_x, v+shift_y), zero outside the crop
-    int32_t  mode;                           // ResizeMode
-    int32_t  dst_w, dst_h;                   // full resize target
+    int32_t  dst_w;                          // full resize target width
     int32_t  win_x, win_y, win_w, win_h;     // window of the target produced by this job
     int32_t  xv;                             // first element (x*cn+c) on OpenCV's scalar row tail
     int32_t  flip;
     int32_t  photo;                          // PhotoFlags
+    int32_t  tiles;                          // row chunks (workgroups) of this job
+    int32_t  stats_slot;                     // contrast partial-sum slot (-1 if none)
+    int32_t  out_pitch, out_plane;           // loader output row pitch / plane stride (elements):
+                                             // win_w / win_w*win_h, or the fixed_aspect_ratio canvas
+    // -- photometric constants and host bookkeeping
+    int32_t  mode;                           // ResizeMode
+    int32_t  src_w, src_h, dst_h;
     int32_t  bs_kind;                        // BsKind
     int32_t  bsq[9];                         // 10-bit fixed-point transform coefficients
     float    bsm[9];                         // float transform matrix (diag / float paths)
@@ -59,13 +67,12 @@ struct alignas(16) AugJob {
     int32_t  hue;
     float    light_a;                        // (float)(1/(1+sigma))
     int32_t  light_add[3];                   // cvRound(pixel_c / (1+sigma))
-    int32_t  tiles;                          // row chunks (workgroups) of this job
-    int32_t  stats_slot;                     // contrast partial-sum slot (-1 if none)
     int32_t  src_scratch;                    // host bookkeeping: source lives in the slot scratch
     int32_t  stats_tiles;                    // chunks of the pass-1 job that wrote this slot's sums
-    int32_t  out_pitch, out_plane;           // loader output row pitch / plane stride (elements):
-                                             // win_w / win_w*win_h, or the fixed_aspect_ratio canvas
 };
+constexpr int kJobHotBytes = 128;
+static_assert(__builtin_offsetof(AugJob, mode) <= kJobHotBytes, "AugJob hot fields");
+static_assert(sizeof(AugJob) == 256, "AugJob size");
 
 // image::rotate pre-pass of one record (rotate_kernels.hip): source -> same-size scratch image.
 struct alignas(16) RotJob {
@@ -123,6 +130,7 @@ struct GrTap {
 struct LaunchArgs {
     const AugJob*  jobs;       // the launch's jobs: device memory, or the device view of a pinned host slot
     int32_t        jobs_host;  // jobs is pinned host memory (read through to the host)
+    int32_t        job_bytes;  // bytes of each job the tiles fetch: kJobHotBytes without photometric jobs
     const float*   lut;        // [3][256] per SOURCE channel: standardized value of output
                                // channel (bgr_to_rgb ? 2-c : c), or (float)x without mean
     const int32_t* hsv_tables; // sdiv[256], hdiv180[256], then per uchar H the HSV2RGB weights (B, G, R, 0) as float bits

@@ -526,16 +526,17 @@ __device__ __forceinline__ void stage_unpack(const JobRef& J, const StageGeom& G
     }
 }
 
-// The job descriptor of tile t into an LDS job slot: one 64-lane LDS-DMA of its 256 bytes.  A job
-// table in pinned host memory (a.jobs_host) is read through to the host (sc0 sc1: the host wrote
-// the slot since the GPU last read it).
+// The job descriptor of tile t into an LDS job slot: one 64-lane LDS-DMA of its a.job_bytes (256, or
+// the 128 hot bytes when no job of the launch has photometric stages).  A job table in pinned host
+// memory (a.jobs_host) is read through to the host (sc0 sc1: the host wrote the slot since the GPU
+// last read it).
 __device__ __forceinline__ void fetch_job(const LaunchArgs& a, int t, int lds_slot)
 {
     if (t < 0 || t >= a.total_tiles) return;
     const int      job  = t / a.max_tiles;
-    const auto     rs   = uniform_rsrc((const void*)(a.jobs + job), (int)sizeof(AugJob));
+    const auto     rs   = uniform_rsrc((const void*)(a.jobs + job), a.job_bytes);
     const uint32_t lane = threadIdx.x & 63;
-    const uint32_t voff = lane * 4 < sizeof(AugJob) ? lane * 4 : kOutOfRange;
+    const uint32_t voff = lane * 4 < (uint32_t)a.job_bytes ? lane * 4 : kOutOfRange; // (the rest of the slot: 0)
     const int      base = __builtin_amdgcn_readfirstlane(lds_slot);
     if (a.jobs_host)
         asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dword %1, %2, 0 offen sc0 sc1 lds" : : "s"(base), "v"(voff), "s"(rs)

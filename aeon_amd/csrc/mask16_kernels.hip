@@ -278,7 +278,7 @@ __global__ __launch_bounds__(256) void nearest_staged(const Mask16Job* __restric
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds_rows[];
     __shared__ RowMap M;
-    const Mask16Job& J  = jobs[blockIdx.y];
+    const Mask16Job J = jobs[blockIdx.y]; // loaded once: the table may be the caller's pinned slot (over PCIe)
     const int        y0 = blockIdx.x * rows_per_block;
     if (y0 >= J.out_h) return;
     if (threadIdx.x < 64) map_rows(J, blockIdx.y, y0, min(rows_per_block, J.out_h - y0), max_slots, M);
@@ -290,7 +290,7 @@ __global__ __launch_bounds__(256) void nearest_staged(const Mask16Job* __restric
 
 __global__ __launch_bounds__(256) void nearest_records(const Mask16Job* __restrict__ jobs, int rows_per_block)
 {
-    const Mask16Job& J  = jobs[blockIdx.y];
+    const Mask16Job J = jobs[blockIdx.y];
     const int        y0 = blockIdx.x * rows_per_block;
     if (y0 >= J.out_h) return;
     const int y1 = min(y0 + rows_per_block, J.out_h);

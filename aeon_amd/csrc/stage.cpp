@@ -960,6 +960,7 @@ LaunchArgs launch_args(aeon_hip_ctx* ctx, const Slot& s, const uint8_t* table, c
 #endif
     a.tail_rounds = AEON_HIP_TAIL_ROUNDS;
     a.jobs           = (const AugJob*)(table + L.blob_off);
+    a.job_bytes      = L.photo ? (int)sizeof(AugJob) : kJobHotBytes;
     a.lut            = d_lut; // [3][256]: standardized, or (float)x without mean
     a.hsv_tables     = ctx->d_hsv;
     a.partials       = s.partials;
@@ -1043,6 +1044,10 @@ bool run_direct(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void
     // every tile reads its job over PCIe: past ~512 KB of such reads per launch the multi-pass path's
     // device table wins (C5's image launch, 4,096 tiles of 256 B: 98 vs 90 us of kernels per step;
     // C2, 1,792 tiles: direct 3 us faster)
+    // every tile reads its job over PCIe: past ~512 KB of such reads per launch the multi-pass path's
+    // device table wins (C5's image launch, 4,096 tiles: 98 vs 90 us of kernels per step; C2, 1,792
+    // tiles: direct 3 us faster; a job table the kernel imports itself -- one PCIe read per job
+    // into device memory, flags, tiles fetching through L2 -- measured no faster, profiles/r03)
     if ((size_t)P.max_tiles * n * sizeof(AugJob) > kDirectFetchMax) return false;
     phase(2);
     int         slot;
@@ -1259,8 +1264,14 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
     // 43.5 vs 44.2 us per C2 step against an SDMA copy + event, which costs a ~6.6 us dispatch gap);
     // larger ones by SDMA on copy_stream, which overlaps the previous call's kernels while the
     // upload kernel would read PCIe at ~34 GB/s (C3, 512 KB: 347 vs 357 us per step).
-    const uint8_t* table = s.dev;
-    if (blob > kUploadKernelMax) {
+    // A call of pixel-mask gather jobs only (C5's masks): the gather reads its few jobs (one per
+    // workgroup) from the pinned slot itself, no upload launch ahead of it.
+    bool mask_only = !m16.empty() && rot.empty() && exp.empty() && gr_short.jobs.empty() && gr_main.jobs.empty();
+    for (auto* v : {&pre, &pre2, &pass1, &main})
+        for (LaunchPlan& P : *v) mask_only = mask_only && P.jobs.empty();
+    const uint8_t* table = mask_only ? s.host_dev : s.dev;
+    if (mask_only) {
+    } else if (blob > kUploadKernelMax) {
         HIP_OK(hipMemcpyAsync(s.dev, s.host, blob, hipMemcpyHostToDevice, ctx->copy_stream));
         HIP_OK(hipEventRecord(s.copied, ctx->copy_stream));
         HIP_OK(hipStreamWaitEvent(stream, s.copied, 0));
@@ -1404,7 +1415,7 @@ int aeon_hip_ctx_create(int device, aeon_hip_ctx** out)
 #endif
                 HIP_OK(hipEventCreateWithFlags(&s.done, hipEventDisableTiming |
                                                             (AEON_HIP_DONE_FENCE ? 0 : hipEventDisableSystemFence)));
-                HIP_OK(hipEventCreateWithFlags(&s.copied, hipEventDisableTiming));
+                HIP_OK(hipEventCreateWithFlags(&s.copied, hipEventDisableTiming | hipEventDisableSystemFence));
             }
             HIP_OK(hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
             // the ring at the size a 512-record call needs (job tables of 128 KB), so steady-state
