@@ -50,7 +50,7 @@ def parse():
                          "with HIP events (0 = none); each timed launch idles the queue ~9 us around it")
     ap.add_argument("--cpu-extra-seconds", type=float, default=3.0,
                     help="CPU-baseline sample budget of each of C1/C3/C5")
-    ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic_r02.json"))
+    ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic_r03.json"))
     ap.add_argument("--share-device", action="store_true",
                     help="development: ranks share the visible GPUs round-robin (gloo barrier), to run "
                          "the N-rank path on a 1-GPU box")
