@@ -24,7 +24,7 @@ def measure(cfg, batch, steps=20, warmup=3):
 
 
 if __name__ == "__main__":
-    variants = [dict()] + [dict(AEON_HIP_TR=str(t), AEON_HIP_BANDS=str(b)) for t in (8, 9) for b in (1, 2, 4, 7)]
+    variants = [dict()]
     cfgs = (("C2", 256), ("C3", 1024))
     argv = sys.argv[1:]
     if argv and argv[0] in ("C2", "C3"):
@@ -36,8 +36,6 @@ if __name__ == "__main__":
         variants = [dict(kv.split("=", 1) for kv in argv)]
     for cfg, batch in cfgs:
         for v in variants:
-            for k in ("AEON_HIP_TR", "AEON_HIP_STAGE_KB", "AEON_HIP_BANDS"):
-                os.environ.pop(k, None)
             os.environ.update(v)
             r = measure(cfg, batch)
             print(cfg, v, {k: f"{ms*1e3:.1f}us {gbs:.0f}GB/s" for k, (ms, gbs) in r.items()}, flush=True)
