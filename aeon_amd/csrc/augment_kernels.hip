@@ -971,15 +971,20 @@ struct Bands {
                     hue_pack_n<2, 0>(sdv, hdiv, htab8, val, pk);
                     hue_pack_n<2, 2>(sdv, hdiv, htab8, val, pk);
 #endif
-#pragma unroll
-                    for (int k = 0; k < 4; k++) {
-                        sum0 = __builtin_amdgcn_udot4(pk[k], 0x1u, sum0, false);
-                        sum1 = __builtin_amdgcn_udot4(pk[k], 0x100u, sum1, false);
-                        sum2 = __builtin_amdgcn_udot4(pk[k], 0x10000u, sum2, false);
-                    }
+                    // the 12-byte HWC group B0 G0 R0 B1 | G1 R1 B2 G2 | R2 B3 G3 R3, and the exact channel
+                    // sums as byte picks of those three words (9 v_dot4 instead of 12 on the pixels)
                     const u32x3 q = {__builtin_amdgcn_perm(pk[1], pk[0], 0x04020100u),
                                      __builtin_amdgcn_perm(pk[2], pk[1], 0x05040201u),
                                      __builtin_amdgcn_perm(pk[3], pk[2], 0x06050402u)};
+                    sum0 = __builtin_amdgcn_udot4(q.x, 0x01000001u, sum0, false);
+                    sum0 = __builtin_amdgcn_udot4(q.y, 0x00010000u, sum0, false);
+                    sum0 = __builtin_amdgcn_udot4(q.z, 0x00000100u, sum0, false);
+                    sum1 = __builtin_amdgcn_udot4(q.x, 0x00000100u, sum1, false);
+                    sum1 = __builtin_amdgcn_udot4(q.y, 0x01000001u, sum1, false);
+                    sum1 = __builtin_amdgcn_udot4(q.z, 0x00010000u, sum1, false);
+                    sum2 = __builtin_amdgcn_udot4(q.x, 0x00010000u, sum2, false);
+                    sum2 = __builtin_amdgcn_udot4(q.y, 0x00000100u, sum2, false);
+                    sum2 = __builtin_amdgcn_udot4(q.z, 0x01000001u, sum2, false);
                     __builtin_amdgcn_raw_buffer_store_b96(q, orsrc, (y * win_w + ox0) * 3, 0, 0);
                     continue;
                 }
