@@ -45,9 +45,10 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the C3 and end-to-end side runs")
     ap.add_argument("--streams", type=int, default=1, help="development: alternate batches over N streams")
-    ap.add_argument("--timing-every", type=int, default=10,
-                    help="bracket the kernels of one step in N (the N-th, 2N-th, ...: not the first call after the idle barrier) "
-                         "with HIP events (0 = none); each timed launch idles the queue ~9 us around it")
+    ap.add_argument("--timing-every", type=int, default=0,
+                    help="development: also bracket the kernels of one step in N with HIP events (0 = none; the "
+                         "roofline's duration comes from one event pair around the timed region's launches, "
+                         "run_device(region=True)); each timed launch idles the queue ~9 us around it")
     ap.add_argument("--cpu-extra-seconds", type=float, default=3.0,
                     help="CPU-baseline sample budget of each of C1/C3/C5")
     ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic_r03.json"))
@@ -149,7 +150,21 @@ class Workload:
                           self.dst[s & 1].data_ptr(), stream)
 
 
-def run_device(A, C, torch, cfg, batch, steps, warmup, rank, world, pool_mib, dist, timing=8, streams=1):
+def step_bytes(params):
+    """Algorithmic bytes of one single-pass step (stage.cpp launch_bytes): each record's
+    crop read once (u8 HWC) + its float32 CHW output written once."""
+    return float(sum(p.crop_w * p.crop_h * 3 + p.out_w * p.out_h * 3 * 4 for p in params))
+
+
+def run_device(A, C, torch, cfg, batch, steps, warmup, rank, world, pool_mib, dist, timing=8, streams=1,
+               region=False):
+    """region: time the kernels as the timed region runs them, back to back -- one HIP event pair on
+    the launch stream around steps 2..K (the first step only fills the queue), kt['augment'] = (that
+    span, the steps' algorithmic bytes, K - 1).  A step of this workload is one tile-kernel launch
+    (single-pass calls: no planner, upload or copy ahead of it), so the span / (K - 1) is the average
+    launch duration with each launch following the previous one, as rocprofv3 sees them; per-launch
+    event pairs (timing) idle the queue around the launch they bracket and time it on a GPU that
+    has drained the previous launch's stores (~8 % shorter)."""
     ctx = A.Context(torch.cuda.current_device())
     wl = Workload(A, C, torch, cfg, batch, steps + warmup, rank, pool_mib, world=world)
     # streams > 1 (development): consecutive batches alternate between caller streams, as a
@@ -164,9 +179,14 @@ def run_device(A, C, torch, cfg, batch, steps, warmup, rank, world, pool_mib, di
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)] if region else None
     t0 = time.perf_counter()
     for s in range(warmup, warmup + steps):
         wl.step(ctx, s, strs[s % streams])
+        if region and s == warmup:
+            ev[0].record(torch.cuda.current_stream())  # (strs[0] is the current stream)
+    if region:
+        ev[1].record(torch.cuda.current_stream())
     wl.submit_s = time.perf_counter() - t0  # host time to plan + enqueue all steps
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
@@ -176,6 +196,9 @@ def run_device(A, C, torch, cfg, batch, steps, warmup, rank, world, pool_mib, di
         ctx.synchronize(st)
     kt = ctx.kernel_times()
     ctx.set_timing(False)
+    if region and steps > 1 and streams == 1:
+        kt["augment"] = (ev[0].elapsed_time(ev[1]),
+                         sum(step_bytes(wl.params[s]) for s in range(warmup + 1, warmup + steps)), steps - 1)
     if dist:
         dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -573,13 +596,13 @@ def main():
 
     elapsed, kt, param_us, submit_s = run_device(A, C, torch, args.config, batch, args.steps, args.warmup,
                                                  rank, world, args.pool_mib, dist, args.timing_every,
-                                                 args.streams)
+                                                 args.streams, region=args.config == "C2")
     total = batch * args.steps * world
     value = total / elapsed
     k_ms, k_bytes, k_n = kt["augment"]
     # dominant kernel = augment_tiles<KM_FINAL,...>: algorithmic bytes per launch / its average
-    # launch duration (HIP events on the launch stream, on every --timing-every-th step of the
-    # timed region; one launch per step unless a batch mixes resize modes)
+    # launch duration (one HIP event pair on the launch stream around the timed region's launches
+    # 2..K, back to back: run_device(region=True); one launch per C2 step)
     achieved = k_bytes / (k_ms * 1e-3) / 1e9 if k_ms else 0.0
     bytes_per_launch = k_bytes / max(k_n, 1)
 
@@ -662,6 +685,8 @@ def main():
                      "traffic": load_traffic(args.traffic_file, args.config),
                      "kernel": "augment_tiles<KM_FINAL,...>", "kernel_avg_launch_ms": k_ms / max(k_n, 1),
                      "algorithmic_bytes_per_launch": bytes_per_launch, "timed_launches": k_n,
+                     "timing": "one HIP event pair on the launch stream around launches 2..K of the timed region "
+                               "(back to back, as rocprofv3 sees them)",
                      # the same algorithmic bytes over the whole step (upload + kernel + host)
                      "step_gbs": bytes_per_launch / (elapsed / args.steps) / 1e9 if k_n else None},
         "host_make_params_us_per_record": param_us,

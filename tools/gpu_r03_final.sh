@@ -17,7 +17,7 @@ prof() { # name, program...
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/prof_$n" -o run --output-format csv -- "$@" > "$O/prof_$n.log" 2>&1 || { tail -5 "$O/prof_$n.log"; return 1; }
   cp "$O/prof_$n/run_kernel_stats.csv" "$O/${n}_kernel_stats.csv"
 }
-prof c2 python3 "$R/bench.py" --steps 100 --warmup 5 --no-cpu-baseline --no-extra || exit 1
+prof c2 python3 "$R/bench.py" --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --no-extra || exit 1
 prof c3 python3 "$R/tools/kbench.py" C3 default || exit 1
 prof c5 python3 "$R/tools/c5_run.py" 30 || exit 1
 prof jpeg python3 "$R/tools/jpeg_ab.py" || exit 1
