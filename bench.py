@@ -594,9 +594,13 @@ def main():
         torch.cuda.set_device(0)
     batch = args.batch or C.CONFIGS[args.config]["batch_size"]
 
+    # C2 (one launch per step): the region event pair; C3 (two passes and a reduce per step): sampled
+    # per-launch events, one step in ten unless --timing-every says otherwise
+    region = args.config == "C2" and args.streams == 1
+    timing = args.timing_every or (0 if region else 10)
     elapsed, kt, param_us, submit_s = run_device(A, C, torch, args.config, batch, args.steps, args.warmup,
-                                                 rank, world, args.pool_mib, dist, args.timing_every,
-                                                 args.streams, region=args.config == "C2")
+                                                 rank, world, args.pool_mib, dist, timing, args.streams,
+                                                 region=region)
     total = batch * args.steps * world
     value = total / elapsed
     k_ms, k_bytes, k_n = kt["augment"]
