@@ -96,7 +96,10 @@ constexpr int kMaxLds        = 160 * 1024;
 #endif
 constexpr int kStageBudget   = AEON_HIP_STAGE_BUDGET_KB * 1024; // preferred LDS bytes of the staging buffer
 constexpr int kStageBudgetHi = 140 * 1024;  // fallback for very wide crops
-constexpr size_t kUploadKernelMax = 128 * 1024; // job tables above this go up by SDMA (run_batch)
+#ifndef AEON_HIP_UPLOAD_KERNEL_MAX_KB
+#define AEON_HIP_UPLOAD_KERNEL_MAX_KB 128
+#endif
+constexpr size_t kUploadKernelMax = AEON_HIP_UPLOAD_KERNEL_MAX_KB * 1024; // job tables above this go up by SDMA (run_batch)
 constexpr size_t kDirectFetchMax  = 512 * 1024; // run_direct: most job bytes a launch's tiles read over PCIe
 
 // ---------------------------------------------------------------------------------------------
