@@ -304,6 +304,10 @@ EDGE_CASES = [
      dict(item_stride=3 * 512 * 384 * 4)),
     ("big_source_c3", (4096, 3072), dict(crop_x=0, crop_y=0, crop_w=4096, crop_h=3072, out_w=224, out_h=224,
                                          brightness=0.7, saturation=1.6, contrast=0.6, hue=9), {}),
+    # a contrast record of more than 2^32 / 255 pixels: its channel sums need 64 bits (contrast_reduce)
+    ("contrast_u64_sums", (1030, 16400), dict(crop_x=0, crop_y=0, crop_w=1030, crop_h=16400, out_w=1030,
+                                              out_h=16400, contrast=0.6, brightness=1.2),
+     dict(item_stride=3 * 1030 * 16400 * 4)),
     # uint8 planes: 4-byte groups stored as dwords when aligned, bytewise when the plane's rows are not
     ("u8_chw_odd_width", (256, 256), dict(crop_x=5, crop_y=9, crop_w=200, crop_h=180, out_w=221, out_h=37, flip=1),
      dict(dtype="uint8", mean=None, stddev=None, item_stride=221 * 37 * 3)),
