@@ -1046,11 +1046,9 @@ bool run_direct(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void
     P.max_tiles = (max_h + P.tr - 1) / P.tr;
     // every tile reads its job over PCIe: past ~512 KB of such reads per launch the multi-pass path's
     // device table wins (C5's image launch, 4,096 tiles of 256 B: 98 vs 90 us of kernels per step;
-    // C2, 1,792 tiles: direct 3 us faster)
-    // every tile reads its job over PCIe: past ~512 KB of such reads per launch the multi-pass path's
-    // device table wins (C5's image launch, 4,096 tiles: 98 vs 90 us of kernels per step; C2, 1,792
-    // tiles: direct 3 us faster; a job table the kernel imports itself -- one PCIe read per job
-    // into device memory, flags, tiles fetching through L2 -- measured no faster, profiles/r03)
+    // C2, 1,792 tiles: direct 3 us faster; a job table the kernel imports itself -- one PCIe read per
+    // job into device memory, flags, tiles fetching through L2 -- measured no faster, profiles/r03)
+    // (C5's image launch with 128-B hot-half fetches, 512 KB: 112.5 vs 95.5 us per step)
     if ((size_t)P.max_tiles * n * sizeof(AugJob) > kDirectFetchMax) return false;
     phase(2);
     int         slot;
