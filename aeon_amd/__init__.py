@@ -120,7 +120,7 @@ def lib():
         if hasattr(L, "aeon_hip_transpose_batch"):  # absent only in older tuning-variant builds
             L.aeon_hip_transpose_batch.argtypes = [vp, vp, vp, ctypes.c_int64, ctypes.c_int64, ctypes.c_int, vp]
         L.aeon_hip_set_timing.argtypes = [vp, ctypes.c_int]
-        L.aeon_hip_kernel_times.argtypes = [vp, P(ctypes.c_double), P(ctypes.c_double), P(ctypes.c_long)]
+        L.aeon_hip_kernel_times.argtypes = [vp, ctypes.c_int, P(ctypes.c_double), P(ctypes.c_double), P(ctypes.c_long)]
         L.aeon_param_factory_create.argtypes = [ctypes.c_char_p, P(vp)]
         L.aeon_param_factory_destroy.argtypes = [vp]
         L.aeon_make_params.argtypes = [vp, P(ctypes.c_uint32), ctypes.c_int, ctypes.c_int,
@@ -154,6 +154,10 @@ def lib():
         L.aeon_decoder_submit.argtypes = [vp, ctypes.c_int, P(EncodedElem), P(vp), ctypes.c_int]
         L.aeon_decoder_wait.argtypes = [vp]
         L.aeon_decoder_last_error.restype = ctypes.c_char_p
+        L.aeon_thread_affinity_map.argtypes = [ctypes.c_char_p, P(ctypes.c_int), ctypes.c_int, P(ctypes.c_int)]
+        L.aeon_decoder_pool_size.argtypes = [vp, P(ctypes.c_int)]
+        L.aeon_decoder_pool_cpus.argtypes = [vp, ctypes.c_int, P(ctypes.c_int), P(ctypes.c_int), ctypes.c_int,
+                                             P(ctypes.c_int)]
         L.aeon_manifest_node_slice.argtypes = [ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                                P(ctypes.c_int64), P(ctypes.c_int64)]
         L.aeon_hip_last_error.restype = ctypes.c_char_p
@@ -377,7 +381,7 @@ class Context:
     def kernel_times(self):
         """{'augment'|'stats'|'pre'|'jpeg': (total_ms, total_algorithmic_bytes, launches)}"""
         ms, by, ct = (ctypes.c_double * 4)(), (ctypes.c_double * 4)(), (ctypes.c_long * 4)()
-        _check(lib().aeon_hip_kernel_times(self._h, ms, by, ct))
+        _check(lib().aeon_hip_kernel_times(self._h, 4, ms, by, ct))
         return {k: (ms[i], by[i], ct[i]) for i, k in enumerate(("augment", "stats", "pre", "jpeg"))}
 
     def synchronize(self, stream=0):
@@ -526,6 +530,28 @@ class Decoder:
 
     def wait(self):
         _check_host(lib().aeon_decoder_wait(self._h))
+
+    def pool_cpus(self):
+        """Per decode-pool worker: (CPU of the affinity map it was pinned to or -1, the CPUs its own
+        sched_getaffinity reported after pinning)."""
+        n = ctypes.c_int()
+        _check_host(lib().aeon_decoder_pool_size(self._h, ctypes.byref(n)))
+        res = []
+        for w in range(n.value):
+            mc, cnt = ctypes.c_int(), ctypes.c_int()
+            buf = (ctypes.c_int * 4096)()
+            _check_host(lib().aeon_decoder_pool_cpus(self._h, w, ctypes.byref(mc), buf, 4096, ctypes.byref(cnt)))
+            res.append((mc.value, list(buf[:min(cnt.value, 4096)])))
+        return res
+
+
+def thread_affinity_map(cpu_list=""):
+    """nervana::get_thread_affinity_map (aeon src/util.cpp:337-373): the CPUs the decode pool's
+    workers are pinned to (AEON_CPU_LIST, else cpu_list, else the default policy)."""
+    cnt = ctypes.c_int()
+    buf = (ctypes.c_int * 4096)()
+    _check_host(lib().aeon_thread_affinity_map(cpu_list.encode(), buf, 4096, ctypes.byref(cnt)))
+    return list(buf[:min(cnt.value, 4096)])
 
 
 def manifest_node_slice(record_count, batch_size, node_id, node_count):

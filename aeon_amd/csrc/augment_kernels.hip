@@ -1199,13 +1199,18 @@ void augment_tiles(LaunchArgs a)
         hsv_div_tables(L, a.hsv_tables);
     }
     if (KM == KM_FINAL && PHOTO && a.has_rtab) __syncthreads(); // record tables read the LUT
-    // development: s_memtime stamps per (workgroup, iteration, phase) when a.trace is set;
-    // s_memrealtime (chip-wide 100 MHz) at entry and exit
+    // development builds (-DAEON_HIP_TRACE, tools/trace_kernel.py): s_memtime stamps per (workgroup,
+    // iteration, phase) when a.trace is set; s_memrealtime (chip-wide 100 MHz) at entry and exit.
+    // The product library compiles them out.
+#ifdef AEON_HIP_TRACE
     auto stamp = [&](int it, int ph) {
         if (a.trace && tid == 0 && it < 16)
             a.trace[(blockIdx.x * 16 + it) * 16 + ph] = (uint32_t)__builtin_amdgcn_s_memtime();
     };
     if (a.trace && tid == 0) a.trace[(blockIdx.x * 16) * 16 + 15] = (uint32_t)__builtin_amdgcn_s_memrealtime();
+#else
+    auto stamp = [](int, int) {};
+#endif
     using Info = typename Bands<KM, RM, PHOTO, OF, TAIL>::Info;
     // Schedule: static rounds, tiles blockIdx.x, +G, +2G, ... (the tiles in flight at any moment are
     // consecutive bands of a few records: measured faster than contiguous ranges per workgroup and
@@ -1302,7 +1307,9 @@ void augment_tiles(LaunchArgs a)
             break;
         }
     }
+#ifdef AEON_HIP_TRACE
     if (a.trace && tid == 0) a.trace[(blockIdx.x * 16 + 1) * 16 + 15] = (uint32_t)__builtin_amdgcn_s_memrealtime();
+#endif
 }
 
 

@@ -3,6 +3,7 @@
 
 #include <hip/hip_runtime.h>
 #include <rocprofiler-sdk-roctx/roctx.h>
+#include <pthread.h>
 #include <sched.h>
 
 #include <algorithm>
@@ -334,14 +335,15 @@ void provider_base::draw_window(int n, const decoded_element* records, decode_wi
     // tasks of 32 consecutive records, each engine drawn from a local copy: eight engines share a
     // cache line, and threads drawing neighbouring records through them made the pool slower than
     // one thread (C3 window of 1024: 399 vs 374 us)
+    // The engines advance in a scratch copy committed (with the lighting state) only once every
+    // record drew: a record that throws (an element of size 0) leaves the decoder as it was.
     constexpr int kChunk = 32;
+    std::vector<std::minstd_rand0> next(engines.begin(), engines.begin() + n);
     pool.run((n + kChunk - 1) / kChunk, [&](int t) {
-        for (int i = t * kChunk; i < std::min(n, (t + 1) * kChunk); i++) {
-            std::minstd_rand0 e = engines[i];
-            draw(i, records + (size_t)i * ne, w, e, lit ? &ls[i] : nullptr);
-            engines[i] = e;
-        }
+        for (int i = t * kChunk; i < std::min(n, (t + 1) * kChunk); i++)
+            draw(i, records + (size_t)i * ne, w, next[i], lit ? &ls[i] : nullptr);
     });
+    std::copy(next.begin(), next.end(), engines.begin());
     if (!lit) return;
     float cached = F.light_saved();
     for (int i = 0; i < n; i++) {
@@ -400,9 +402,11 @@ std::shared_ptr<provider_base> provider_factory::create(const Json& config)
 }
 
 // ---- thread_pool ----------------------------------------------------------------------------------
-thread_pool::thread_pool(int nthreads)
+thread_pool::thread_pool(std::vector<int> affinity_map) : m_map(std::move(affinity_map))
 {
-    for (int i = 0; i < std::max(1, nthreads); i++) m_threads.emplace_back([this, i] { worker(i); });
+    const int n = std::max<int>(1, (int)m_map.size());
+    m_worker_cpus.resize(n);
+    for (int i = 0; i < n; i++) m_threads.emplace_back([this, i] { worker(i); });
 }
 
 thread_pool::~thread_pool()
@@ -415,8 +419,33 @@ thread_pool::~thread_pool()
     for (auto& t : m_threads) t.join();
 }
 
+std::vector<std::vector<int>> thread_pool::worker_cpus()
+{
+    std::unique_lock<std::mutex> l(m_mu);
+    m_done_cv.wait(l, [&] { return m_started == (int)m_threads.size(); });
+    return m_worker_cpus;
+}
+
 void thread_pool::worker(int index)
 {
+    // thread_pool.hpp:133-138: pin to thread_affinity_map[index] (the result is not checked there
+    // either: a CPU outside the cpuset leaves the thread on the process mask)
+    if (index < (int)m_map.size()) {
+        cpu_set_t set;
+        CPU_ZERO(&set);
+        CPU_SET(m_map[index], &set);
+        (void)pthread_setaffinity_np(pthread_self(), sizeof(set), &set);
+    }
+    {
+        std::vector<int> cpus;
+        cpu_set_t        got;
+        if (sched_getaffinity(0, sizeof(got), &got) == 0)
+            for (int c = 0; c < CPU_SETSIZE; c++)
+                if (CPU_ISSET(c, &got)) cpus.push_back(c);
+        std::lock_guard<std::mutex> l(m_mu);
+        m_worker_cpus[index] = std::move(cpus);
+        if (++m_started == (int)m_threads.size()) m_done_cv.notify_all();
+    }
     long seen = 0;
     for (;;) {
         const std::function<void(int, int)>* fn;
@@ -469,34 +498,69 @@ void thread_pool::run_indexed(int n, const std::function<void(int, int)>& fn)
 }
 
 // ---- batch_decoder -------------------------------------------------------------------------------
-int aeon_thread_count(const std::string& cpu_list)
+std::vector<int> parse_cpu_list(const std::string& cpu_list)
 {
-    // util.cpp:337-373: AEON_CPU_LIST / cpu_list, else hardware_concurrency - min(2, hc/8)
+    std::vector<int>  cpus;
+    std::stringstream ss(cpu_list);
+    std::string       tok;
+    try {
+        while (std::getline(ss, tok, ',')) {
+            if (tok.empty()) continue;
+            const auto dash = tok.find('-');
+            if (dash == std::string::npos) {
+                cpus.push_back(std::stoi(tok));
+            } else {
+                const int from = std::stoi(tok.substr(0, dash)), to = std::stoi(tok.substr(dash + 1));
+                for (int i = from; i <= to; i++) cpus.push_back(i);
+            }
+        }
+    } catch (const std::exception&) {
+        invalid("Failed to parse cpu list '" + cpu_list + "'");
+    }
+    std::sort(cpus.begin(), cpus.end());
+    cpus.erase(std::unique(cpus.begin(), cpus.end()), cpus.end());
+    const int hc = (int)std::thread::hardware_concurrency();
+    if (!cpus.empty() && (cpus.front() < 0 || cpus.back() >= hc))
+        invalid("One or more indexes computed from cpu list '" + cpu_list +
+                "' exceed number of logical cores. Use values in range [0, " + std::to_string(hc - 1) + "].");
+    return cpus;
+}
+
+std::vector<int> thread_affinity_map(const std::string& cpu_list)
+{
+    // util.cpp:337-373: the environment has precedence over the config
     std::string list = cpu_list;
     if (const char* e = std::getenv("AEON_CPU_LIST"))
         if (*e) list = e;
-    if (!list.empty()) {
-        std::set<int>     cpus;
-        std::stringstream ss(list);
-        std::string       tok;
-        while (std::getline(ss, tok, ',')) {
-            auto dash = tok.find('-');
-            if (dash == std::string::npos) cpus.insert(std::stoi(tok));
-            else
-                for (int i = std::stoi(tok.substr(0, dash)); i <= std::stoi(tok.substr(dash + 1)); i++)
-                    cpus.insert(i);
-        }
-        return std::max<int>(1, (int)cpus.size());
+    std::vector<int> map = list.empty() ? std::vector<int>() : parse_cpu_list(list);
+    if (!map.empty()) return map;
+    // hc - min(2, hc/8) over the CPUs this process may run on (its affinity mask: the GPU box gives
+    // each job 16 of its 256 CPUs, and workers pinned outside it would stay unpinned), further
+    // capped by OMP_NUM_THREADS when the launcher sets it
+    std::vector<int> allowed;
+    cpu_set_t        set;
+    if (sched_getaffinity(0, sizeof(set), &set) == 0)
+        for (int c = 0; c < CPU_SETSIZE; c++)
+            if (CPU_ISSET(c, &set)) allowed.push_back(c);
+    if (allowed.empty()) {
+        allowed.resize(std::max(1u, std::thread::hardware_concurrency()));
+        std::iota(allowed.begin(), allowed.end(), 0);
     }
-    // hardware_concurrency, capped by the CPUs this process may run on (affinity mask) and by
-    // OMP_NUM_THREADS when the launcher sets it (a container's CPU share: the GPU box gives each
-    // job 16 of its 256 CPUs, and 254 pool threads would only contend for them)
-    int hc = (int)std::thread::hardware_concurrency();
-    cpu_set_t set;
-    if (sched_getaffinity(0, sizeof(set), &set) == 0) hc = std::min(hc, std::max(1, CPU_COUNT(&set)));
+    int hc = (int)allowed.size();
     if (const char* e = std::getenv("OMP_NUM_THREADS"))
         if (std::atoi(e) > 0) hc = std::min(hc, std::atoi(e));
-    return std::max(1, hc - std::min(2, hc / 8));
+    allowed.resize(std::max(1, hc - std::min(2, hc / 8)));
+    return allowed;
+}
+
+int aeon_thread_count(const std::string& cpu_list) { return (int)thread_affinity_map(cpu_list).size(); }
+
+std::vector<int> affinity_for(const std::vector<int>& map, int n)
+{
+    std::vector<int> out(std::max(1, n));
+    for (size_t i = 0; i < out.size(); i++) out[i] = map.empty() ? -1 : map[i % map.size()];
+    if (map.empty()) out.clear();
+    return out;
 }
 
 batch_decoder::batch_decoder(const Json& config, int device) : m_device(device)
@@ -521,10 +585,15 @@ batch_decoder::batch_decoder(const Json& config, int device) : m_device(device)
     get_bool(config, "batch_major", m_batch_major);
     std::string cpu_list;
     get_str(config, "cpu_list", cpu_list);
-    int threads = aeon_thread_count(cpu_list);
-    get_num(config, "decode_thread_count", threads);
+    std::vector<int> map = thread_affinity_map(cpu_list); // loader.cpp:159-171
+    if (config.has("decode_thread_count")) { // (this stage's own knob: the map cycled or cut to it)
+        int threads = 0;
+        get_num(config, "decode_thread_count", threads);
+        if (threads <= 0) invalid("decode_thread_count must be > 0");
+        map = affinity_for(map, threads);
+    }
     m_provider = provider_factory::create(config);
-    m_pool.reset(new thread_pool(threads));
+    m_pool.reset(new thread_pool(map));
     m_local_random.seed(std::random_device{}());
     // decoder seed = random_seed + node_id (loader.cpp:174); deterministic when non-zero
     const uint32_t dseed = seed ? seed + node_id : 0;
@@ -780,7 +849,7 @@ void batch_decoder::decode(int n, const decoded_element* records, void* const* o
     if (!m_batch_major && n % m_batch_size != 0) invalid("batch_major=false needs whole batches per decode window");
     while (!m_queue.empty()) wait(); // windows are completed in submission order
     if (m_deterministic) grow_slot_engines(n);
-    if (!m_ctx) check(aeon_hip_ctx_create(m_device, &m_ctx));
+    if (!m_ctx) check(aeon_hip_ctx_create(m_device, &m_ctx)), ctx_share_pool(m_ctx, m_pool.get());
     hip_check(hipSetDevice(m_device), "hipSetDevice");
     window_slot& ws = m_slots[m_next];
     m_next ^= 1;
@@ -798,7 +867,7 @@ void batch_decoder::submit(int n, const decoded_element* records, void* const* o
     if (!m_batch_major && n % m_batch_size != 0) invalid("batch_major=false needs whole batches per decode window");
     if (m_queue.size() >= 2) invalid("two windows are in flight: wait() for the oldest before submitting another");
     if (m_deterministic) grow_slot_engines(n);
-    if (!m_ctx) check(aeon_hip_ctx_create(m_device, &m_ctx));
+    if (!m_ctx) check(aeon_hip_ctx_create(m_device, &m_ctx)), ctx_share_pool(m_ctx, m_pool.get());
     hip_check(hipSetDevice(m_device), "hipSetDevice");
     const int    slot = m_next;
     window_slot& ws   = m_slots[slot];
@@ -1010,6 +1079,38 @@ int aeon_manifest_node_slice(int64_t record_count, int batch_size, int node_id, 
         auto v = aeon_hip::manifest_node_slice(record_count, batch_size, node_id, node_count);
         if (indices) std::copy(v.begin(), v.end(), indices);
         *count = (int64_t)v.size();
+    });
+}
+
+int aeon_thread_affinity_map(const char* cpu_list, int* cpus, int cap, int* count)
+{
+    return host_guarded([&] {
+        if (!count || (cap > 0 && !cpus)) throw std::invalid_argument("null argument");
+        const auto map = aeon_hip::thread_affinity_map(cpu_list ? cpu_list : "");
+        for (int i = 0; i < std::min(cap, (int)map.size()); i++) cpus[i] = map[i];
+        *count = (int)map.size();
+    });
+}
+
+int aeon_decoder_pool_cpus(aeon_decoder* d, int worker, int* map_cpu, int* cpus, int cap, int* count)
+{
+    return host_guarded([&] {
+        if (!d || !count || (cap > 0 && !cpus)) throw std::invalid_argument("null argument");
+        aeon_hip::thread_pool& p = d->d->pool();
+        if (worker < 0 || worker >= p.size()) throw std::invalid_argument("worker out of range");
+        const auto all = p.worker_cpus();
+        const auto& w  = all[worker];
+        if (map_cpu) *map_cpu = worker < (int)p.affinity_map().size() ? p.affinity_map()[worker] : -1;
+        for (int i = 0; i < std::min(cap, (int)w.size()); i++) cpus[i] = w[i];
+        *count = (int)w.size();
+    });
+}
+
+int aeon_decoder_pool_size(aeon_decoder* d, int* workers)
+{
+    return host_guarded([&] {
+        if (!d || !workers) throw std::invalid_argument("null argument");
+        *workers = d->d->pool().size();
     });
 }
 

@@ -156,19 +156,29 @@ struct provider_factory {
     static std::shared_ptr<provider_base> create(const Json& config);
 };
 
-// thread_pool (src/thread_pool.hpp): persistent workers, run(n, fn) hands out task ids from
-// one atomic counter; the first exception is kept and rethrown after the barrier.
+// thread_pool (src/thread_pool.hpp:82-175): persistent workers, worker i pinned to CPU
+// affinity_map[i] (pthread_setaffinity_np, thread_pool.hpp:133-138); run(n, fn) hands out task ids
+// from one atomic counter; the first exception is kept and rethrown after the barrier.
 class thread_pool {
 public:
-    explicit thread_pool(int nthreads);
+    // one worker per entry of affinity_map (at least one; an empty map = one unpinned worker)
+    explicit thread_pool(std::vector<int> affinity_map);
     ~thread_pool();
     void run(int n, const std::function<void(int)>& fn);
     // fn(task, worker): worker in [0, size()) identifies the calling pool thread
     void run_indexed(int n, const std::function<void(int, int)>& fn);
     int  size() const { return (int)m_threads.size(); }
+    const std::vector<int>& affinity_map() const { return m_map; }
+    // what worker i's own sched_getaffinity returned after it pinned itself (blocks until every
+    // worker has started); a CPU outside the process's cpuset cannot be pinned to, and that worker
+    // keeps the process mask -- aeon ignores pthread_setaffinity_np's result the same way
+    std::vector<std::vector<int>> worker_cpus();
 
 private:
     void                                 worker(int index);
+    std::vector<int>                     m_map;
+    std::vector<std::vector<int>>        m_worker_cpus;
+    int                                  m_started = 0;
     std::vector<std::thread>             m_threads;
     std::mutex                           m_mu;
     std::condition_variable              m_cv, m_done_cv;
@@ -201,6 +211,7 @@ public:
     void draw_params(int n, const decoded_element* records, aeon_aug_params* params, bool serial);
     int  outstanding() const { return (int)m_queue.size(); }
     provider_base& provider() { return *m_provider; }
+    thread_pool&   pool() { return *m_pool; }
     int            batch_size() const { return m_batch_size; }
 
 private:
@@ -238,6 +249,18 @@ private:
 // manifest_file node slicing (generate_blocks, src/manifest_file.cpp:278-295)
 std::vector<int64_t> manifest_node_slice(int64_t record_count, int batch_size, int node_id, int node_count);
 
-int aeon_thread_count(const std::string& cpu_list); // get_thread_affinity_map policy
+// nervana::parse_cpu_list (src/util.cpp:283-330): "0-4,30,10" -> sorted, de-duplicated CPU ids;
+// std::invalid_argument for an id >= hardware_concurrency
+std::vector<int> parse_cpu_list(const std::string& cpu_list);
+// nervana::get_thread_affinity_map (src/util.cpp:337-373): AEON_CPU_LIST over the config's cpu_list;
+// else hc - min(2, hc/8) CPUs.  aeon's default is iota(0, ...); here it is the first CPUs of the
+// process's own affinity mask (the same list on an unrestricted host; inside a container given 16
+// of 256 CPUs, CPUs the workers can actually be pinned to), capped by OMP_NUM_THREADS.
+std::vector<int> thread_affinity_map(const std::string& cpu_list);
+int aeon_thread_count(const std::string& cpu_list); // thread_affinity_map(cpu_list).size()
+// the decoder's pool runs its context's JPEG entropy decoding too (stage.cpp)
+void ctx_share_pool(aeon_hip_ctx* ctx, thread_pool* pool);
+// a map stretched or cut to n workers (decode_thread_count / AEON_HIP_JPEG_THREADS): worker i on map[i % size]
+std::vector<int> affinity_for(const std::vector<int>& map, int n);
 
 } // namespace aeon_hip

@@ -23,7 +23,10 @@ struct jpeg_error : std::runtime_error {
 };
 
 struct JpegState;
-JpegState* jpeg_state_create();
+class thread_pool;
+// shared: entropy-decode on that pool (the decoder's own, pinned to its cpu_list -- aeon's extract
+// runs inside provide() on the decode pool); null: a pool of the stage's own (thread_affinity_map)
+JpegState* jpeg_state_create(thread_pool* shared = nullptr);
 void       jpeg_state_destroy(JpegState* s);
 
 // One 8x8 block: bit z of `mask` = zigzag coefficient z is non-zero; its values follow in zigzag

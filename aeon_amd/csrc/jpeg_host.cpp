@@ -647,7 +647,8 @@ void decode_file(const uint8_t* d, size_t size, Frame& f, Arena& a, size_t blk_o
 // Per-context JPEG state: the decode pool, worker arenas, a two-deep ring of pinned staging +
 // device buffers (a call reuses a set once the copies and kernels of the call before last are done).
 struct JpegState {
-    std::unique_ptr<thread_pool> pool;
+    std::unique_ptr<thread_pool> own;
+    thread_pool*                 pool = nullptr;
     std::vector<Arena>           arenas;
     struct Set {
         hipEvent_t done    = nullptr;
@@ -683,12 +684,17 @@ void hip_ok(hipError_t e, const char* what)
 
 } // namespace
 
-JpegState* jpeg_state_create()
+JpegState* jpeg_state_create(thread_pool* shared)
 {
     auto* s = new JpegState();
-    int   threads = aeon_thread_count("");
-    if (const char* e = std::getenv("AEON_HIP_JPEG_THREADS")) threads = std::max(1, std::atoi(e));
-    s->pool.reset(new thread_pool(threads));
+    if (shared) {
+        s->pool = shared;
+    } else {
+        std::vector<int> map = thread_affinity_map(""); // pinned like aeon's decode pool (AEON_CPU_LIST)
+        if (const char* e = std::getenv("AEON_HIP_JPEG_THREADS")) map = affinity_for(map, std::max(1, std::atoi(e)));
+        s->own.reset(new thread_pool(map));
+        s->pool = s->own.get();
+    }
     s->arenas.resize(s->pool->size());
     return s;
 }

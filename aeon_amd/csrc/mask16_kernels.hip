@@ -272,13 +272,28 @@ __device__ __forceinline__ void gather_any(const Mask16Job& J, const RowMap& M, 
     else gather_rows<uint8_t>(J, M, pitch, lds, perm_ok);
 }
 
+// The workgroup's job, loaded once.  The table may be the caller's pinned ring slot, which the host
+// rewrote since the GPU last read that memory: the first lanes read it dword by dword at system scope
+// (sc0 sc1, through to the host, like the tile kernel's fetch_job) into LDS, and every lane copies it.
+__device__ __forceinline__ Mask16Job load_job(const Mask16Job* src, Mask16Job& lds)
+{
+    constexpr int kWords = (int)(sizeof(Mask16Job) / 4);
+    static_assert(sizeof(Mask16Job) % 4 == 0 && kWords <= 64, "Mask16Job: whole dwords, one wave");
+    if (threadIdx.x < kWords)
+        reinterpret_cast<uint32_t*>(&lds)[threadIdx.x] = __hip_atomic_load(
+            reinterpret_cast<const uint32_t*>(src) + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __syncthreads();
+    return lds;
+}
+
 // one block of rows per workgroup: grid (row blocks, records)
 __global__ __launch_bounds__(256) void nearest_staged(const Mask16Job* __restrict__ jobs, int rows_per_block, int pitch,
                                                       int perm_ok, int max_slots)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds_rows[];
     __shared__ RowMap M;
-    const Mask16Job J = jobs[blockIdx.y]; // loaded once: the table may be the caller's pinned slot (over PCIe)
+    __shared__ Mask16Job Js;
+    const Mask16Job J = load_job(jobs + blockIdx.y, Js);
     const int        y0 = blockIdx.x * rows_per_block;
     if (y0 >= J.out_h) return;
     if (threadIdx.x < 64) map_rows(J, blockIdx.y, y0, min(rows_per_block, J.out_h - y0), max_slots, M);
@@ -290,7 +305,8 @@ __global__ __launch_bounds__(256) void nearest_staged(const Mask16Job* __restric
 
 __global__ __launch_bounds__(256) void nearest_records(const Mask16Job* __restrict__ jobs, int rows_per_block)
 {
-    const Mask16Job J = jobs[blockIdx.y];
+    __shared__ Mask16Job Js;
+    const Mask16Job J = load_job(jobs + blockIdx.y, Js);
     const int        y0 = blockIdx.x * rows_per_block;
     if (y0 >= J.out_h) return;
     const int y1 = min(y0 + rows_per_block, J.out_h);

@@ -124,7 +124,7 @@ __device__ __forceinline__ void area_taps(int ssize, double scale, int d, int* t
     if (s1 - fs1 > 1e-3) t[0] = s1 - 1, t[2 + n++] = __float_as_int((float)((s1 - fs1) / cell));
     for (int s = s1; s < s2 && n < amax; s++) t[2 + n++] = __float_as_int((float)(1.0 / cell));
     if (fs2 - s2 > 1e-3 && n < amax) t[2 + n++] = __float_as_int((float)(min(min(fs2 - s2, 1.), cell) / cell));
-    if (s2 - s1 + 2 > amax && threadIdx.x == 0) atomicOr(error, 128); // (the host sizes amax: never)
+    if (s2 - s1 + 2 > amax) atomicOr(error, 128); // any lane whose taps were cut (the host sizes amax: never)
     t[1] = n;
 }
 

@@ -721,6 +721,7 @@ struct aeon_hip_ctx {
     bool                 direct = true; // AEON_HIP_DIRECT=0: the multi-pass path (device job table) for every call
     std::vector<JobGeom> geoms;              // reused per call
     JpegState*           jpeg = nullptr;     // JPEG decode stage (pool, staging ring), on first use
+    thread_pool*         host_pool = nullptr; // the owning decoder's pool (ctx_share_pool), for the JPEG stage
     std::vector<int> open_slots; // used since the last completion event, on open_stream
     hipStream_t      open_stream = nullptr;
     // job tables go up on their own stream, so a call's H2D overlaps the previous call's kernels
@@ -748,6 +749,9 @@ struct aeon_hip_ctx {
     long                     host_calls   = 0;
     double                   bytes[4] = {0, 0, 0, 0};
     long                     count[4] = {0, 0, 0, 0};
+#ifdef AEON_HIP_TRACE
+    uint32_t*                trace = nullptr; // AEON_HIP_TRACE_PTR, read once at ctx_create
+#endif
 };
 
 struct aeon_param_factory {
@@ -970,7 +974,9 @@ LaunchArgs launch_args(aeon_hip_ctx* ctx, const Slot& s, const uint8_t* table, c
     a.shifts         = s.shifts;
     a.partial_stride = partial_stride;
     a.error          = ctx->d_error;
-    if (const char* e = std::getenv("AEON_HIP_TRACE_PTR")) a.trace = (uint32_t*)std::strtoull(e, nullptr, 0);
+#ifdef AEON_HIP_TRACE
+    a.trace = ctx->trace; // development builds only (tools/build_variants.sh trace)
+#endif
     a.rows_per_tile = L.tr;
     a.max_tiles     = L.max_tiles;
     a.total_tiles   = L.max_tiles * n_jobs;
@@ -1368,6 +1374,14 @@ int guarded(F&& f)
 
 } // namespace
 
+namespace aeon_hip {
+// The owning decoder's pool runs the context's JPEG entropy decoding (set before the first JPEG call).
+void ctx_share_pool(aeon_hip_ctx* ctx, thread_pool* pool)
+{
+    if (ctx && !ctx->jpeg) ctx->host_pool = pool;
+}
+} // namespace aeon_hip
+
 extern "C" {
 
 int aeon_hip_ctx_create(int device, aeon_hip_ctx** out)
@@ -1416,7 +1430,9 @@ int aeon_hip_ctx_create(int device, aeon_hip_ctx** out)
 #endif
                 HIP_OK(hipEventCreateWithFlags(&s.done, hipEventDisableTiming |
                                                             (AEON_HIP_DONE_FENCE ? 0 : hipEventDisableSystemFence)));
-                HIP_OK(hipEventCreateWithFlags(&s.copied, hipEventDisableTiming | hipEventDisableSystemFence));
+                // s.copied orders the SDMA job-table upload (copy_stream) before the kernels that read
+                // it on the launch stream: it keeps the system-scope release
+                HIP_OK(hipEventCreateWithFlags(&s.copied, hipEventDisableTiming));
             }
             HIP_OK(hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
             // the ring at the size a 512-record call needs (job tables of 128 KB), so steady-state
@@ -1425,6 +1441,10 @@ int aeon_hip_ctx_create(int device, aeon_hip_ctx** out)
             // diagnostics: host time per phase (printed at destroy); the multi-pass path for every call
             if (const char* e = std::getenv("AEON_HIP_HOST_PROFILE")) c->host_profile = std::atoi(e) != 0;
             if (const char* e = std::getenv("AEON_HIP_DIRECT")) c->direct = std::atoi(e) != 0;
+#ifdef AEON_HIP_TRACE
+            // development builds only: s_memtime phase stamps of the tile kernel into this device buffer
+            if (const char* e = std::getenv("AEON_HIP_TRACE_PTR")) c->trace = (uint32_t*)std::strtoull(e, nullptr, 0);
+#endif
             HIP_OK(hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, device));
         } catch (...) {
             delete c;
@@ -1555,10 +1575,11 @@ int aeon_hip_set_timing(aeon_hip_ctx* ctx, int enable)
     });
 }
 
-int aeon_hip_kernel_times(aeon_hip_ctx* ctx, double* ms, double* bytes, long* count)
+int aeon_hip_kernel_times(aeon_hip_ctx* ctx, int kinds, double* ms, double* bytes, long* count)
 {
     return guarded([&] {
         if (!ctx || !ms || !bytes || !count) fail(AEON_HIP_EINVAL, "null argument");
+        if (kinds < 0) fail(AEON_HIP_EINVAL, "negative kinds");
         std::lock_guard<std::mutex> lock(ctx->mu);
         HIP_OK(hipSetDevice(ctx->device));
         for (KernelTimer& t : ctx->timers) {
@@ -1572,7 +1593,7 @@ int aeon_hip_kernel_times(aeon_hip_ctx* ctx, double* ms, double* bytes, long* co
         }
         ctx->timers.clear();
         for (int k = 0; k < 4; k++) {
-            ms[k] = ctx->ms[k], bytes[k] = ctx->bytes[k], count[k] = ctx->count[k];
+            if (k < kinds) ms[k] = ctx->ms[k], bytes[k] = ctx->bytes[k], count[k] = ctx->count[k];
             ctx->ms[k] = ctx->bytes[k] = 0, ctx->count[k] = 0;
         }
         return 0;
@@ -1707,7 +1728,7 @@ int aeon_hip_decode_jpeg_batch(aeon_hip_ctx* ctx, int n, const void* const* data
         if (!ctx || n < 0 || (n > 0 && (!data || !sizes || !descs || !dst_base))) fail(AEON_HIP_EINVAL, "null argument");
         if (n == 0) return 0;
         HIP_OK(hipSetDevice(ctx->device));
-        if (!ctx->jpeg) ctx->jpeg = jpeg_state_create();
+        if (!ctx->jpeg) ctx->jpeg = jpeg_state_create(ctx->host_pool);
         KernelTimer t{};
         bool        timed = false;
         if (ctx->timing) {

@@ -84,6 +84,76 @@ def rank_slice(n_records, batch, rank, world):
     return A.manifest_node_slice(n_records, batch, rank, world), 1 + rank
 
 
+def cpu_list_str(cpus):
+    """[0, 1, 2, 5] -> "0-2,5" (aeon's cpu_list syntax, src/util.cpp:283-330)."""
+    out, cpus = [], sorted(set(cpus))
+    i = 0
+    while i < len(cpus):
+        j = i
+        while j + 1 < len(cpus) and cpus[j + 1] == cpus[j] + 1:
+            j += 1
+        out.append(str(cpus[i]) if i == j else f"{cpus[i]}-{cpus[j]}")
+        i = j + 1
+    return ",".join(out)
+
+
+def parse_cpulist(text):
+    cpus = set()
+    for tok in text.strip().split(","):
+        if not tok:
+            continue
+        a, _, b = tok.partition("-")
+        cpus.update(range(int(a), int(b or a) + 1))
+    return cpus
+
+
+def gpu_local_cpus(torch, device):
+    """The CPUs of GPU `device`'s NUMA node (sysfs local_cpulist of its PCI function), or None."""
+    try:
+        p = torch.cuda.get_device_properties(device)
+        addr = f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}.0"
+        with open(f"/sys/bus/pci/devices/{addr}/local_cpulist") as f:
+            cpus = parse_cpulist(f.read())
+        return cpus or None
+    except (OSError, ValueError, AttributeError, RuntimeError):
+        return None
+
+
+def rank_cpu_lists(local, allowed, world):
+    """Disjoint per-rank decode-pool cpu lists for one process per GPU (aeon pins each pool worker to
+    one CPU of its cpu_list, src/thread_pool.hpp:133-138): rank r prefers the CPUs of its GPU's NUMA
+    node that this process may use (local[r]; None = unknown -> any allowed CPU).  The allowed CPUs are
+    shared out as evenly as the preferences permit (one CPU per rank in turn), then each rank takes its
+    count of the lowest free CPUs of its preference, so ranks of one node get contiguous blocks.  With
+    more ranks than CPUs a rank without one shares a CPU of its preference."""
+    allowed = sorted(allowed)
+    pref = []
+    for r in range(world):
+        loc = local[r] if r < len(local) else None
+        p = sorted(set(loc) & set(allowed)) if loc else []
+        pref.append(p or allowed)
+    free, counts = set(allowed), [0] * world
+    progress = True
+    while free and progress:
+        progress = False
+        for r in range(world):
+            c = next((x for x in pref[r] if x in free), None)
+            if c is None:
+                c = min(free) if free else None
+            if c is not None:
+                free.discard(c)
+                counts[r] += 1
+                progress = True
+    free, out = set(allowed), []
+    for r in range(world):
+        mine = [x for x in pref[r] if x in free][:counts[r]]
+        if len(mine) < counts[r]:
+            mine += sorted(free - set(mine))[:counts[r] - len(mine)]
+        free -= set(mine)
+        out.append(sorted(mine) or [pref[r][r % len(pref[r])]])
+    return out
+
+
 def synthetic_pool(torch, records, w, h, cn=3, seed=0x5EED, chunk=64, device="cuda"):
     """A.synthetic_image(g, w, h, cn) for every global record index g, computed on the device:
     splitmix64 in int64 arithmetic (wrapping add/mul; logical shifts by masking)."""
@@ -331,6 +401,16 @@ def pool_threads():
     return max(1, hc - min(2, hc // 8)), hc, visible
 
 
+def pin_baseline(A):
+    """The CPU baseline's pool pinned like aeon's decode pool: worker t on CPU t of the product's
+    thread_affinity_map (AEON_CPU_LIST, else aeon's hc - min(2, hc/8) policy over this process's CPUs)."""
+    import oracle as O
+    _, hc, visible = pool_threads()
+    cpus = A.thread_affinity_map()
+    O.set_affinity(cpus)
+    return len(cpus), hc, visible, cpus
+
+
 def cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
@@ -349,7 +429,7 @@ def cpu_baseline(A, C, budget_s, cfg="C2"):
     import numpy as np
     import oracle as O
     from tests import helpers as H
-    threads, hc, visible = pool_threads()
+    threads, hc, visible, cpus = pin_baseline(A)
     if cfg == "C5":
         n, w, h = 128, 640, 480
         imgs = [A.synthetic_image(i, w, h, 3) for i in range(n)]
@@ -381,7 +461,8 @@ def cpu_baseline(A, C, budget_s, cfg="C2"):
     return {"value": done / secs, "unit": "images/s" if cfg != "C5" else "image+mask pairs/s", "cores": threads,
             "kind": "port",
             "sample": f"{what}: {done} records in windows of {n} ({secs:.1f} s CPU wall); oracle/ C++ restatement "
-                      f"of aeon's transform+load on {threads} pool threads (aeon's policy over {hc} usable CPUs; "
+                      f"of aeon's transform+load on {threads} pool threads pinned one per CPU to "
+                      f"[{cpu_list_str(cpus)}] (aeon's thread_affinity_map over {hc} usable CPUs; "
                       f"{visible} in the affinity mask, {os.cpu_count()} on the machine; CPU: {cpu_model()}); "
                       "scalar C++, a lower bound on aeon's OpenCV-SIMD path"}
 
@@ -473,7 +554,7 @@ def cpu_baseline_jpeg(A, C, budget_s):
     same encoded files and C2 params, aeon's pool policy: a lower bound (scalar decode, no SIMD)."""
     import oracle as O
     from tests import helpers as H
-    threads, hc, visible = pool_threads()
+    threads, hc, visible, cpus = pin_baseline(A)
     files = jpeg_files(256)
     sizes = [O.jpeg_info(f)[:2] for f in files]
     params = [H.to_oracle_params(p) for p in H.draw_params(C.C2_AUG, sizes, 224, 224, seed=1)]
@@ -484,7 +565,8 @@ def cpu_baseline_jpeg(A, C, budget_s):
         done += len(files)
     return {"value": done / secs, "unit": "images/s", "cores": threads, "kind": "port",
             "sample": f"{done} JPEG records (img_2112_70.jpg / flowers.jpg) decoded + C2-augmented by the oracle "
-                      f"on {threads} pool threads ({secs:.1f} s); scalar C++, a lower bound on aeon's "
+                      f"on {threads} pool threads pinned to [{cpu_list_str(cpus)}] ({secs:.1f} s); scalar C++, "
+                      "a lower bound on aeon's "
                       "libjpeg-turbo + OpenCV-SIMD path"}
 
 
@@ -497,7 +579,7 @@ def run_c1_decoder(A, C, torch, budget_s=2.0):
     cfg = dict(C.CONFIGS["C1"], random_seed=1)
     d = A.Decoder(cfg)
     batch = cfg["batch_size"]
-    threads = pool_threads()[0]
+    threads = len(A.thread_affinity_map())
     n = batch * ((threads * 8 - 1) // batch + 1)
     recs = [(A.synthetic_image(i, 480, 360, 3),) for i in range(n)]
     bufs = [torch.empty(n * 3 * 224 * 224 * 4, dtype=torch.uint8).pin_memory() for _ in range(2)]
@@ -550,8 +632,10 @@ def dry_run(args, world, rank):
     for _ in range(args.steps):
         time.sleep(0.0005)
     elapsed = time.perf_counter() - t0
+    cpus = rank_cpu_lists([None] * world, set(os.sched_getaffinity(0)), world)[rank]
     mine = {"rank": rank, "node_id": rank, "seed": seed, "slice_len": len(records),
-            "slice_head": [int(x) for x in records[:2 * batch]], "slot_states": [int(x) for x in states]}
+            "slice_head": [int(x) for x in records[:2 * batch]], "slot_states": [int(x) for x in states],
+            "cpu_list": cpu_list_str(cpus)}
     allv = [None] * world
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64)
@@ -593,6 +677,14 @@ def main():
     else:
         torch.cuda.set_device(0)
     batch = args.batch or C.CONFIGS[args.config]["batch_size"]
+    cpu_lists = None
+    if world > 1:
+        # one process per GPU: every rank's decode pools (aeon_decoder, the JPEG stage) pinned to its own
+        # block of its GPU's NUMA-local CPUs (AEON_CPU_LIST, util.cpp:344-357), no two ranks sharing one
+        ngpu = torch.cuda.device_count()
+        local_sets = [gpu_local_cpus(torch, (r % ngpu) if args.share_device else r) for r in range(world)]
+        cpu_lists = rank_cpu_lists(local_sets, set(os.sched_getaffinity(0)), world)
+        os.environ["AEON_CPU_LIST"] = cpu_list_str(cpu_lists[rank])
 
     # C2 (one launch per step): the region event pair; C3 (two passes and a reduce per step): sampled
     # per-launch events, one step in ten unless --timing-every says otherwise
@@ -694,6 +786,8 @@ def main():
                      # the same algorithmic bytes over the whole step (upload + kernel + host)
                      "step_gbs": bytes_per_launch / (elapsed / args.steps) / 1e9 if k_n else None},
         "host_make_params_us_per_record": param_us,
+        "decode_pool_cpus": ({str(r): cpu_list_str(l) for r, l in enumerate(cpu_lists)} if cpu_lists else
+                             cpu_list_str(A.thread_affinity_map())),
         "host_submit_ms_per_step": submit_s / args.steps * 1e3,
     }
     if extra:

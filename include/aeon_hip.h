@@ -182,8 +182,10 @@ int aeon_hip_set_timing(aeon_hip_ctx* ctx, int every);
 /* Drain the timers: per kernel kind [0]=augment (final), [1]=contrast statistics,
  * [2]=pre-passes (resize_short, CUBIC / AREA / LANCZOS4 resize, 2x-area ahead of photometric),
  * [3]=JPEG IDCT + colour kernels of aeon_hip_decode_jpeg_batch (bytes: decoded pixels): total ms,
- * total algorithmic bytes, launches -- arrays of 4.  Resets the totals. */
-int aeon_hip_kernel_times(aeon_hip_ctx* ctx, double* ms, double* bytes, long* count);
+ * total algorithmic bytes, launches.  The arrays hold `kinds` entries (AEON_HIP_TIMER_KINDS = all;
+ * fewer are filled, more are left alone).  Resets the totals of every kind. */
+#define AEON_HIP_TIMER_KINDS 4
+int aeon_hip_kernel_times(aeon_hip_ctx* ctx, int kinds, double* ms, double* bytes, long* count);
 
 /* ---- augmentation parameters (host) ------------------------------------------------------- */
 /* augment::image::param_factory(json) (src/augment_image.cpp:28-89) from the JSON text of the
@@ -294,6 +296,16 @@ int aeon_decoder_decode_encoded(aeon_decoder* d, int n, const aeon_encoded_elem*
 int aeon_decoder_submit(aeon_decoder* d, int n, const aeon_encoded_elem* elems, void* const* outputs,
                         int outputs_on_device);
 int aeon_decoder_wait(aeon_decoder* d);
+/* The decode pool's CPU pinning (thread_pool.hpp:133-138 + util.cpp:337-373).
+ * aeon_thread_affinity_map: nervana::get_thread_affinity_map -- AEON_CPU_LIST, else cpu_list ("0-3,8"),
+ * else hc - min(2, hc/8) CPUs: the first ones of the process's affinity mask (aeon: iota from 0, which is
+ * the same list on an unrestricted host).  Writes up to cap ids, the map's length to *count.
+ * aeon_decoder_pool_size / aeon_decoder_pool_cpus: the decoder's workers; for worker i, the CPU of the map
+ * it was pinned to (*map_cpu, -1 = none) and the CPUs its own sched_getaffinity reported after pinning
+ * (a CPU outside the process's cpuset cannot be pinned to: that worker reports the process mask). */
+int aeon_thread_affinity_map(const char* cpu_list, int* cpus, int cap, int* count);
+int aeon_decoder_pool_size(aeon_decoder* d, int* workers);
+int aeon_decoder_pool_cpus(aeon_decoder* d, int worker, int* map_cpu, int* cpus, int cap, int* count);
 const char* aeon_decoder_last_error(void);
 
 /* manifest_file node slicing (src/manifest_file.cpp:278-295): the record indices of node

@@ -138,6 +138,10 @@ def lib():
                                            P(ctypes.c_int), P(Params), P(LoadConfig), ctypes.c_void_p,
                                            ctypes.c_size_t, P(LoadConfig), ctypes.c_void_p, ctypes.c_size_t,
                                            ctypes.c_int]
+        L.orc_set_affinity.argtypes = [P(ctypes.c_int), ctypes.c_int]
+        L.orc_set_affinity.restype = None
+        L.orc_pool_cpus.argtypes = [ctypes.c_int, P(ctypes.c_int)]
+        L.orc_pool_cpus.restype = None
         L.orc_rotate.argtypes = [ctypes.c_void_p] + [ctypes.c_int] * 6 + [ctypes.c_void_p]
         L.orc_transpose.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int]
         L.orc_unbiased_round.argtypes = [ctypes.c_float]
@@ -376,6 +380,19 @@ def augment_record(src, p, lc):
 def u8_standardize(x, mean, stddev):
     """uint8 result of standardizing a CV_8U canvas value x (fixed_aspect_ratio loader)."""
     return lib().orc_u8_standardize_value(int(x), mean, stddev)
+
+
+def set_affinity(cpus):
+    """Pin the baseline pool like aeon's thread_pool: worker t on cpus[t % len(cpus)]; [] = unpinned."""
+    arr = (ctypes.c_int * max(1, len(cpus)))(*cpus)
+    lib().orc_set_affinity(arr, len(cpus))
+
+
+def pool_cpus(threads):
+    """The single CPU each of `threads` baseline-pool workers is pinned to (-1: not pinned to one)."""
+    out = (ctypes.c_int * max(1, threads))()
+    lib().orc_pool_cpus(threads, out)
+    return list(out[:threads])
 
 
 def batch_augment(srcs, params_list, lc, item_shape, threads):

@@ -16,6 +16,9 @@
 #include <stdexcept>
 #include <string>
 #include <thread>
+
+#include <pthread.h>
+#include <sched.h>
 #include <vector>
 
 namespace {
@@ -1293,6 +1296,50 @@ int orc_rotate(const uint8_t* src, int w, int h, int cn, int stride, int angle, 
     });
 }
 
+} // extern "C"
+
+namespace {
+// The CPU baseline's pool: aeon's thread_pool (src/thread_pool.hpp:133-138) pins worker t to
+// thread_affinity_map[t]; orc_set_affinity installs that map (worker t -> cpus[t % n]), none = unpinned.
+std::vector<int> g_affinity;
+
+template <typename W>
+void run_pool(int threads, W&& work)
+{
+    std::vector<std::thread> pool;
+    for (int t = 0; t < std::max(1, threads); t++)
+        pool.emplace_back([&, t] {
+            if (!g_affinity.empty()) {
+                cpu_set_t set;
+                CPU_ZERO(&set);
+                CPU_SET(g_affinity[t % g_affinity.size()], &set);
+                (void)pthread_setaffinity_np(pthread_self(), sizeof(set), &set);
+            }
+            work(t);
+        });
+    for (auto& t : pool) t.join();
+}
+} // namespace
+
+extern "C" {
+
+void orc_set_affinity(const int* cpus, int n)
+{
+    g_affinity.assign(cpus, cpus + std::max(0, n));
+}
+
+// worker t of a `threads` pool: the CPU its sched_getaffinity holds when that is exactly one, else -1
+void orc_pool_cpus(int threads, int* out)
+{
+    run_pool(threads, [&](int t) {
+        cpu_set_t set;
+        out[t] = -1;
+        if (sched_getaffinity(0, sizeof(set), &set) == 0 && CPU_COUNT(&set) == 1)
+            for (int c = 0; c < CPU_SETSIZE; c++)
+                if (CPU_ISSET(c, &set)) out[t] = c;
+    });
+}
+
 double orc_batch_augment(int n, const uint8_t* const* srcs, const int* widths, const int* heights,
                          const orc_params* params, const orc_load_config* lc, void* out,
                          size_t item_bytes, int threads)
@@ -1315,9 +1362,7 @@ double orc_batch_augment(int n, const uint8_t* const* srcs, const int* widths, c
         }
     };
     auto t0 = std::chrono::steady_clock::now();
-    std::vector<std::thread> pool;
-    for (int t = 0; t < std::max(1, threads); t++) pool.emplace_back(work);
-    for (auto& t : pool) t.join();
+    run_pool(threads, [&](int) { work(); });
     auto t1 = std::chrono::steady_clock::now();
     if (failed) return -1.0;
     return std::chrono::duration<double>(t1 - t0).count();
@@ -1346,9 +1391,7 @@ double orc_batch_image_mask(int n, const uint8_t* const* srcs, const uint8_t* co
         }
     };
     auto t0 = std::chrono::steady_clock::now();
-    std::vector<std::thread> pool;
-    for (int t = 0; t < std::max(1, threads); t++) pool.emplace_back(work);
-    for (auto& t : pool) t.join();
+    run_pool(threads, [&](int) { work(); });
     auto t1 = std::chrono::steady_clock::now();
     if (failed) return -1.0;
     return std::chrono::duration<double>(t1 - t0).count();
@@ -1389,9 +1432,7 @@ double orc_batch_decode_augment(int n, const uint8_t* const* files, const size_t
         }
     };
     auto t0 = std::chrono::steady_clock::now();
-    std::vector<std::thread> pool;
-    for (int t = 0; t < std::max(1, threads); t++) pool.emplace_back(work);
-    for (auto& t : pool) t.join();
+    run_pool(threads, [&](int) { work(); });
     auto t1 = std::chrono::steady_clock::now();
     if (failed) return -1.0;
     return std::chrono::duration<double>(t1 - t0).count();

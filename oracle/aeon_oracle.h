@@ -129,6 +129,9 @@ int orc_rotate(const uint8_t* src, int w, int h, int cn, int stride, int angle, 
  * dest[c * rows + r] = src[r * cols + c], element_size 1, 2, 4 or 8.  Returns -1 otherwise. */
 int orc_transpose(void* dest, const void* src, int64_t rows, int64_t cols, int element_size);
 
+/* the CPU baseline pool's pinning (aeon's thread_affinity_map): worker t on cpus[t % n]; n = 0 unpinned */
+void orc_set_affinity(const int* cpus, int n);
+void orc_pool_cpus(int threads, int* out);
 double orc_batch_augment(int n, const uint8_t* const* srcs, const int* widths, const int* heights,
                          const orc_params* params, const orc_load_config* lc, void* out,
                          size_t item_bytes, int threads);

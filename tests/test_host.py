@@ -142,6 +142,11 @@ def test_bench_launcher_dry_run_two_ranks():
         assert info["slice_len"] == len(ref) and info["slice_head"] == ref[:2 * b]
         assert info["slot_states"] == list(A.seed_slots(1 + rk, 4))
     assert line["ranks"][0]["slot_states"] != line["ranks"][1]["slot_states"]
+    # each rank's decode-pool cpu_list (AEON_CPU_LIST): non-empty, allowed, disjoint across ranks
+    lists = [set(A.thread_affinity_map(info["cpu_list"])) for info in line["ranks"]]
+    assert all(lists) and all(l <= set(os.sched_getaffinity(0)) for l in lists)
+    if len(os.sched_getaffinity(0)) >= 2:
+        assert not lists[0] & lists[1]
 
 
 def test_bench_synthetic_pool_matches_synthetic_image():

@@ -1,4 +1,7 @@
 """Development: per-phase s_memtime stamps of the band kernel (C2), via AEON_HIP_TRACE_PTR.
+Needs a trace build (the product library compiles the stamps out):
+  tools/build_variants.sh trace=-DAEON_HIP_TRACE
+  AEON_HIP_LIB=aeon_amd/variants/trace.so python tools/trace_kernel.py C2
 Layout [workgroup][iteration 0..15][slot 0..15]; slot 15 of iteration 0 / 1 = s_memrealtime
 (chip-wide 100 MHz) at kernel entry / exit.  Single-buffered phases: 0 start, 1 info, 2 DMA
 issued, 3 tap tables, 4 loads landed, 5 unpacked, 6 barrier, 7 computed, 8 end barrier.
