@@ -140,6 +140,12 @@ def lib():
         L.aeon_decode_png.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int, vp, ctypes.c_size_t,
                                       P(ctypes.c_int)]
         L.aeon_hip_decode_jpeg_batch.argtypes = [vp, ctypes.c_int, P(vp), P(ctypes.c_size_t), P(ImgDesc), vp, vp]
+        L.aeon_hip_stager_create.argtypes = [vp, ctypes.c_int, P(OutDesc), ctypes.c_int, P(vp)]
+        L.aeon_hip_stager_destroy.argtypes = [vp]
+        L.aeon_hip_stager_stage.argtypes = [vp, vp, ctypes.c_int, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                            ctypes.c_int, ctypes.c_int, P(AugParams)]
+        L.aeon_hip_stager_flush.argtypes = [vp, vp]
+        L.aeon_hip_stager_last_error.restype = ctypes.c_char_p
         L.aeon_hip_host_alloc.argtypes = [ctypes.c_size_t, P(vp)]
         L.aeon_hip_host_free.argtypes = [vp]
         L.aeon_decoder_create.argtypes = [ctypes.c_char_p, ctypes.c_int, P(vp)]
@@ -391,6 +397,49 @@ class Context:
         """batch_major=false layout: dst[c*rows + r] = src[r*cols + c] (async on stream)."""
         _check(lib().aeon_hip_transpose_batch(self._h, ctypes.c_void_p(src_ptr), ctypes.c_void_p(dst_ptr),
                                               rows, cols, element_size, ctypes.c_void_p(stream or 0)))
+
+
+STAGER_IMAGE, STAGER_MASK, STAGER_DEVICE_OUT = 0, 1, 0x100
+
+
+def _check_stager(rc):
+    if rc != 0:
+        raise AeonHipError(rc, lib().aeon_hip_stager_last_error().decode())
+    return rc
+
+
+class Stager:
+    """aeon_hip_stager: what the aeon-side provider::image / ::pixelmask hold (INTEGRATION.md).
+    stage() from provide() on any pool thread (the ctypes call releases the GIL), flush() from
+    post_process() once per batch: the first flush of a window launches the whole window."""
+
+    def __init__(self, ctx, out, batch_size, kind=STAGER_IMAGE):
+        h = ctypes.c_void_p()
+        self._out = out
+        _check_stager(lib().aeon_hip_stager_create(ctx._h, kind, ctypes.byref(out), batch_size, ctypes.byref(h)))
+        self._h = h
+
+    def stage(self, batch_out, idx, pixels, params):
+        """pixels: HxWxC or HxW uint8 / uint16 array (host)."""
+        a = np.ascontiguousarray(pixels)
+        h, w = a.shape[:2]
+        cn = 1 if a.ndim == 2 else a.shape[2]
+        _check_stager(lib().aeon_hip_stager_stage(self._h, ctypes.c_void_p(batch_out), idx, a.ctypes.data, w, h,
+                                                   a.strides[0], cn, a.itemsize, ctypes.byref(params)))
+
+    def flush(self, batch_out):
+        _check_stager(lib().aeon_hip_stager_flush(self._h, ctypes.c_void_p(batch_out)))
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().aeon_hip_stager_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def pack_images(images, align=16):

@@ -313,6 +313,34 @@ const char* aeon_decoder_last_error(void);
 int aeon_manifest_node_slice(int64_t record_count, int batch_size, int node_id, int node_count,
                              int64_t* indices, int64_t* count);
 
+/* ---- the aeon-side drop-in: provide() stages, post_process() flushes ---------------------------
+ * What provider::image / provider::pixelmask hold.  aeon's batch_decoder::filler runs
+ * provide(idx, record, out_buf) for a decode window on its pool (src/batch_decoder.cpp:62-99) and, with
+ * the one-line change, post_process(out_buf) once per batch of the window; provider_base forwards
+ * post_process to each ETL provider (src/provider.hpp:64-76 gains the override).
+ *   aeon_hip_stager_stage (from provide(), any pool thread, concurrently): record idx of the batch whose
+ *     buffer is batch_out (out_buf[name]->get_item(0): the staging key) -- its decoded pixels (HWC,
+ *     copied into pinned memory before the call returns) and its augment::image::params.
+ *   aeon_hip_stager_flush (from post_process(), the filler thread): the first flush after a window's
+ *     stages launches the WHOLE window -- one H2D per pinned staging chunk, one augment (or pixel-mask)
+ *     launch over every staged record of every batch, a D2H into each batch buffer (pinned,
+ *     device-mapped batch buffers are stored into directly; AEON_STAGER_DEVICE_OUT: batch_out is device
+ *     memory) -- and each flush returns once ITS batch buffer is complete.  A batch must hold idx 0..n-1.
+ * Images: aeon_hip_augment_batch semantics; masks (AEON_STAGER_MASK): aeon_hip_mask_batch, staged with
+ * the record's image params (provider.cpp:378-391).  Errors: AEON_HIP_E* codes,
+ * aeon_hip_stager_last_error(); a window whose launch fails is dropped whole. */
+typedef struct aeon_hip_stager aeon_hip_stager;
+#define AEON_STAGER_IMAGE      0
+#define AEON_STAGER_MASK       1
+#define AEON_STAGER_DEVICE_OUT 0x100 /* or-ed into kind: batch buffers are device memory */
+int aeon_hip_stager_create(aeon_hip_ctx* ctx, int kind, const aeon_out_desc* out, int batch_size,
+                           aeon_hip_stager** stager);
+int aeon_hip_stager_destroy(aeon_hip_stager* stager);
+int aeon_hip_stager_stage(aeon_hip_stager* stager, void* batch_out, int idx, const void* pixels, int width,
+                          int height, int stride, int channels, int elem_bytes, const aeon_aug_params* params);
+int aeon_hip_stager_flush(aeon_hip_stager* stager, void* batch_out);
+const char* aeon_hip_stager_last_error(void);
+
 /* ---- host staging (replaces the dead cuMemAllocHost branch, src/buffer_batch.cpp:150-186) -- */
 int aeon_hip_host_alloc(size_t bytes, void** out);
 int aeon_hip_host_free(void* p);
