@@ -218,4 +218,39 @@ AEON_HD inline LdsLayout lds_layout(int max_win_w, int rows_per_tile, int stage_
     return L;
 }
 
+// ---- record_kernels.hip: contrast records in one launch (the post-hue record in registers) ------
+constexpr int kRecPhases = 16;                     // row phases (lanes per column group)
+constexpr int kRecRows   = 14;                     // rows per lane held in registers (win_h <= 224)
+constexpr int kRecTileRows = 2;                    // rows per lane per tile
+constexpr int kRecTR     = kRecPhases * kRecTileRows; // output rows per tile
+constexpr int kRecTiles  = kRecRows / kRecTileRows;   // register tiles (the rotation period)
+constexpr int kRecWords  = 3 * kRecRows;           // 12 bytes (4 BGR pixels) per row
+
+// LDS carve of the record kernel (bytes, 16-aligned regions)
+struct RecLds {
+    int rtab, hsv, htab, xt, yt, job, sums, stage, stage_bytes, total;
+};
+AEON_HD inline RecLds rec_lds_layout(int win_w, int stage_bytes)
+{
+    RecLds L;
+    int    o = 0;
+    L.rtab = o; o += 3 * 256 * 4;           // record table of the B record (f32, source channel order)
+    L.hsv  = o; o += kHsvLdsDivBytes;       // sdiv + v/255, hdiv180
+    L.htab = o; o += kHueTabBytes;          // hue table of the A record
+    L.xt   = o; o += ((win_w * 8 + 15) / 16) * 16; // column taps of the A record
+    L.yt   = o; o += 2 * kRecTR * 16;       // row taps, one table per staging buffer
+    L.job  = o; o += 3 * (int)sizeof(AugJob); // a ring of three records' jobs
+    L.sums = o; o += 16 * 16;               // per-wave channel sums
+    L.stage_bytes = stage_bytes;
+    L.stage = o; o += 2 * stage_bytes;      // two staging buffers
+    L.total = o;
+    return L;
+}
+
+struct RecArgs {
+    int n_jobs;    // records of the launch
+    int win_w, win_h; // output size of every record (win_w % 4 == 0, win_w <= 256, win_h <= 224)
+    int tiles;     // tiles per record = ceil(rows per lane / 2)
+};
+
 } // namespace aeon_hip

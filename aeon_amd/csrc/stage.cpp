@@ -38,6 +38,9 @@ hipError_t launch_expand(const ExpandJob* jobs, int n_jobs, int max_pixels, hipS
 hipError_t launch_nearest(const Mask16Job* jobs, int n_jobs, int max_h, int max_w, int max_seg_bytes, int max_slots, hipStream_t stream,
                           hipEvent_t start, hipEvent_t stop);
 hipError_t launch_upload_table(const void* host_dev, void* dst, size_t bytes, hipStream_t stream);
+hipError_t launch_contrast_records(bool fast, const LaunchArgs& a, const RecArgs& r, int grid, hipStream_t stream,
+                                   hipEvent_t start, hipEvent_t stop);
+hipError_t contrast_records_lds_limit(int bytes);
 hipError_t launch_resize_generic(const ResizeJob* jobs, const uint8_t* table, int n_jobs, int max_tiles, int TR, int CW,
                                  int NR, int xs, int amax, int cn_max, int32_t* error, hipStream_t stream);
 void       jpeg_decode_batch(JpegState* S, int n, const void* const* data, const size_t* sizes,
@@ -719,6 +722,7 @@ struct aeon_hip_ctx {
     // direct calls (run_direct): records of one job each, one launch group: the tile kernel reads
     // the jobs from the pinned slot itself
     bool                 direct = true; // AEON_HIP_DIRECT=0: the multi-pass path (device job table) for every call
+    bool                 records = true; // AEON_HIP_RECORDS=0: contrast calls through the two-launch path
     std::vector<JobGeom> geoms;              // reused per call
     JpegState*           jpeg = nullptr;     // JPEG decode stage (pool, staging ring), on first use
     thread_pool*         host_pool = nullptr; // the owning decoder's pool (ctx_share_pool), for the JPEG stage
@@ -1084,6 +1088,92 @@ bool run_direct(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void
     return true;
 }
 
+// Contrast records in ONE launch (record_kernels.hip): every record 3-channel, INTER_LINEAR with no
+// OpenCV scalar-tail columns, no rotation / resize_short / expand, one output size that the lanes'
+// registers hold (win_w <= 256, a multiple of 4; win_h <= 224), float32 CHW out; some record with
+// contrast (else the single-pass direct call is the better one).  The post-hue record stays on chip:
+// no u8 intermediate written and read back, no contrast_reduce launch.  Returns false (nothing done)
+// for any other call.  AEON_HIP_RECORDS=0 sends such calls through the two-launch path.
+template <typename Phase>
+bool run_records(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* src_base,
+                 const aeon_aug_params* params, const aeon_out_desc& od, void* out_dev, hipStream_t stream,
+                 bool is_mask, Phase&& phase)
+{
+    if (is_mask || !ctx->records || n <= 0) return false;
+    const OutView        ov = out_view(od);
+    const aeon_out_desc& o  = ov.ko;
+    if (o.dtype != AEON_DTYPE_F32 || !o.channel_major || o.fixed_aspect_ratio || o.channels != 3) return false;
+    if ((((uint64_t)out_dev) & 15) != 0 || (o.item_stride & 15) != 0) return false;
+    const int W = params[0].out_w, H = params[0].out_h;
+    if (W <= 0 || (W & 3) != 0 || W > 4 * 64 || H <= 0 || (H + kRecPhases - 1) / kRecPhases > kRecRows) return false;
+    if (simd_boundary(W * 3) < W * 3) return false; // OpenCV's scalar row tail
+    bool      contrast = false;
+    long      stage    = 0;
+    JobGeom   g{};
+    for (int i = 0; i < n; i++) {
+        const aeon_img_desc&   d = descs[i];
+        const aeon_aug_params& p = params[i];
+        if (d.channels != 3 || (d.elem_bytes != 0 && d.elem_bytes != 1)) return false;
+        if (p.angle != 0 || p.resize_short_size > 0 || expands(p) || p.interp != AEON_INTERP_LINEAR) return false;
+        if (p.out_w != W || p.out_h != H || p.crop_w <= 0 || p.crop_h <= 0) return false;
+        if (choose_mode(p.crop_w, p.crop_h, W, H, AEON_INTERP_LINEAR, 3) != RESIZE_LINEAR) return false;
+        contrast |= (photo_flags(p) & PHOTO_CONTRAST) != 0;
+        g.mode = RESIZE_LINEAR, g.cn = 3, g.crop_w = p.crop_w, g.crop_h = p.crop_h, g.win_w = W, g.win_h = H;
+        g.scale_x = 1. / ((double)W / p.crop_w);
+        g.scale_y = 1. / ((double)H / p.crop_h);
+        stage     = std::max(stage, stage_bytes_for(3, stage_rows_for(g, kRecTR), stage_cols(g)));
+    }
+    if (!contrast) return false;
+    stage         = (stage + 1023) / 1024 * 1024;
+    const int lds = rec_lds_layout(W, (int)stage).total;
+    if (lds > kMaxLds) return false;
+    for (int i = 0; i < n; i++) validate_record(descs[i], params[i], o, false);
+    phase(2);
+    int   slot;
+    Slot& s = take_slot(ctx, stream, slot);
+    phase(3);
+    const float* d_lut = resident_lut(ctx, od, false);
+    ensure_ring(ctx, (size_t)n * sizeof(AugJob), 16, 32);
+    AugJob*       jt   = (AugJob*)s.host;
+    const OutGeom og   = out_geom(o);
+    bool          fast = true;
+    double        bytes = 0;
+    for (int i = 0; i < n; i++) {
+        plan_direct(descs[i], (uint64_t)src_base, params[i], og, (uint64_t)out_dev + (uint64_t)i * o.item_stride, false,
+                    jt[i]);
+        if ((jt[i].photo & PHOTO_BS) && jt[i].bs_kind != BS_FIXPT) fast = false;
+        // algorithmic bytes: the crop read once + the float32 output written once
+        bytes += (double)params[i].crop_w * params[i].crop_h * 3 + (double)W * H * 3 * 4;
+    }
+    phase(4);
+    phase(5);
+    LaunchArgs a{};
+    a.jobs        = (const AugJob*)s.host_dev;
+    a.jobs_host   = 1;
+    a.job_bytes   = (int)sizeof(AugJob);
+    a.lut         = d_lut;
+    a.hsv_tables  = ctx->d_hsv;
+    a.error       = ctx->d_error;
+    a.stage_bytes = (int)stage;
+    a.max_win_w   = W;
+    a.out_dtype   = AEON_DTYPE_F32;
+    a.channel_major = 1;
+    a.bgr_to_rgb  = o.bgr_to_rgb && o.channels == 3;
+    a.threads     = (kRecPhases * (W / 4) + 63) / 64 * 64;
+    a.lds_bytes   = lds;
+    const RecArgs r{n, W, H, ((H + kRecPhases - 1) / kRecPhases + kRecTileRows - 1) / kRecTileRows};
+    const int     grid  = std::min(n, ctx->n_cu); // one workgroup per CU (LDS, 14-16 waves at <= 128 VGPRs)
+    const bool    timed = ctx->timing && (ctx->timing_calls++ % ctx->timing_every) == ctx->timing_every - 1;
+    KernelTimer   t{};
+    if (timed) t = take_timer(ctx, KM_FINAL, bytes);
+    HIP_OK(launch_contrast_records(fast, a, r, grid, stream, timed ? t.start : nullptr, timed ? t.stop : nullptr));
+    if (timed) ctx->timers.push_back(t);
+    phase(6);
+    release_slot(ctx, slot, stream);
+    phase(7);
+    return true;
+}
+
 int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* src_base,
               const aeon_aug_params* params, const aeon_out_desc* out, void* out_dev, void* stream_,
               bool is_mask)
@@ -1128,6 +1218,7 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
     if (ctx->direct &&
         run_direct(ctx, n, descs, src_base, params, od, out_dev, stream, is_mask, phase))
         return 0;
+    if (run_records(ctx, n, descs, src_base, params, od, out_dev, stream, is_mask, phase)) return 0;
 
     LaunchPlan             pre_all, pre2_all, pass1_all, main_all;
     GrPlan                 gr_short, gr_main;
@@ -1393,6 +1484,7 @@ int aeon_hip_ctx_create(int device, aeon_hip_ctx** out)
         try {
             HIP_OK(hipSetDevice(device));
             HIP_OK(set_kernel_lds_limit(kMaxLds));
+            HIP_OK(contrast_records_lds_limit(kMaxLds));
             HIP_OK(hipMalloc((void**)&c->d_error, sizeof(int32_t)));
             HIP_OK(hipMemset(c->d_error, 0, sizeof(int32_t)));
             HIP_OK(hipMalloc((void**)&c->d_tail, aeon_hip_ctx::kSlots * sizeof(uint32_t)));
@@ -1441,6 +1533,7 @@ int aeon_hip_ctx_create(int device, aeon_hip_ctx** out)
             // diagnostics: host time per phase (printed at destroy); the multi-pass path for every call
             if (const char* e = std::getenv("AEON_HIP_HOST_PROFILE")) c->host_profile = std::atoi(e) != 0;
             if (const char* e = std::getenv("AEON_HIP_DIRECT")) c->direct = std::atoi(e) != 0;
+            if (const char* e = std::getenv("AEON_HIP_RECORDS")) c->records = std::atoi(e) != 0;
 #ifdef AEON_HIP_TRACE
             // development builds only: s_memtime phase stamps of the tile kernel into this device buffer
             if (const char* e = std::getenv("AEON_HIP_TRACE_PTR")) c->trace = (uint32_t*)std::strtoull(e, nullptr, 0);
