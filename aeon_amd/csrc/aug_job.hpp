@@ -219,26 +219,28 @@ AEON_HD inline LdsLayout lds_layout(int max_win_w, int rows_per_tile, int stage_
 }
 
 // ---- record_kernels.hip: contrast records in one launch (the post-hue record in registers) ------
-constexpr int kRecPhases = 16;                     // row phases (lanes per column group)
+constexpr int kRecPhasesMax = 32;                  // row phases (lanes per column group), at most
 constexpr int kRecRows   = 14;                     // rows per lane held in registers (win_h <= 224)
 constexpr int kRecTileRows = 2;                    // rows per lane per tile
-constexpr int kRecTR     = kRecPhases * kRecTileRows; // output rows per tile
+constexpr int kRecTRMax  = kRecPhasesMax * kRecTileRows; // output rows per tile (2 x phases), at most
 constexpr int kRecTiles  = kRecRows / kRecTileRows;   // register tiles (the rotation period)
 constexpr int kRecWords  = 3 * kRecRows;           // 12 bytes (4 BGR pixels) per row
 
 // LDS carve of the record kernel (bytes, 16-aligned regions)
 struct RecLds {
-    int rtab, hsv, htab, xt, yt, job, sums, stage, stage_bytes, total;
+    int rtab, lut, hwt, hsv, htab, xt, yt, job, sums, stage, stage_bytes, total;
 };
 AEON_HD inline RecLds rec_lds_layout(int win_w, int stage_bytes)
 {
     RecLds L;
     int    o = 0;
     L.rtab = o; o += 3 * 256 * 4;           // record table of the B record (f32, source channel order)
+    L.lut  = o; o += 3 * 256 * 4;           // the launch's standardize LUT (record tables read it)
+    L.hwt  = o; o += 256 * 16;              // HSV2RGB weights per uchar H (hue tables read them)
     L.hsv  = o; o += kHsvLdsDivBytes;       // sdiv + v/255, hdiv180
     L.htab = o; o += kHueTabBytes;          // hue table of the A record
     L.xt   = o; o += ((win_w * 8 + 15) / 16) * 16; // column taps of the A record
-    L.yt   = o; o += 2 * kRecTR * 16;       // row taps, one table per staging buffer
+    L.yt   = o; o += 2 * kRecTRMax * 16;    // row taps, one table per staging buffer
     L.job  = o; o += 3 * (int)sizeof(AugJob); // a ring of three records' jobs
     L.sums = o; o += 16 * 16;               // per-wave channel sums
     L.stage_bytes = stage_bytes;
@@ -247,8 +249,20 @@ AEON_HD inline RecLds rec_lds_layout(int win_w, int stage_bytes)
     return L;
 }
 
+// Row phases of a win_w-wide record: as many 4-column lane groups as 1024 lanes hold (at most
+// kRecPhasesMax), so a 224-wide record takes 18 x 56 = 1,008 lanes (16 waves); 0 if the lanes'
+// registers cannot hold win_h rows (more than kRecRows per lane).
+AEON_HD inline int rec_phases(int win_w, int win_h)
+{
+    const int gpr = win_w / 4;
+    if (gpr <= 0) return 0;
+    const int nph = 1024 / gpr < kRecPhasesMax ? 1024 / gpr : kRecPhasesMax;
+    return nph > 0 && (win_h + nph - 1) / nph <= kRecRows ? nph : 0;
+}
+
 struct RecArgs {
     int n_jobs;    // records of the launch
+    int phases;    // row phases (rec_phases)
     int win_w, win_h; // output size of every record (win_w % 4 == 0, win_w <= 256, win_h <= 224)
     int tiles;     // tiles per record = ceil(rows per lane / 2)
 };

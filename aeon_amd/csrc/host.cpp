@@ -404,9 +404,12 @@ std::shared_ptr<provider_base> provider_factory::create(const Json& config)
 // ---- thread_pool ----------------------------------------------------------------------------------
 thread_pool::thread_pool(std::vector<int> affinity_map) : m_map(std::move(affinity_map))
 {
-    const int n = std::max<int>(1, (int)m_map.size());
-    m_worker_cpus.resize(n);
-    for (int i = 0; i < n; i++) m_threads.emplace_back([this, i] { worker(i); });
+    // the worker count is fixed before any worker starts: a worker must not read m_threads while this
+    // constructor is still growing it (ThreadSanitizer, tests/sanitize/host_driver.cpp)
+    m_nthreads = std::max<int>(1, (int)m_map.size());
+    m_worker_cpus.resize(m_nthreads);
+    m_threads.reserve(m_nthreads);
+    for (int i = 0; i < m_nthreads; i++) m_threads.emplace_back([this, i] { worker(i); });
 }
 
 thread_pool::~thread_pool()
@@ -422,7 +425,7 @@ thread_pool::~thread_pool()
 std::vector<std::vector<int>> thread_pool::worker_cpus()
 {
     std::unique_lock<std::mutex> l(m_mu);
-    m_done_cv.wait(l, [&] { return m_started == (int)m_threads.size(); });
+    m_done_cv.wait(l, [&] { return m_started == m_nthreads; });
     return m_worker_cpus;
 }
 
@@ -444,7 +447,7 @@ void thread_pool::worker(int index)
                 if (CPU_ISSET(c, &got)) cpus.push_back(c);
         std::lock_guard<std::mutex> l(m_mu);
         m_worker_cpus[index] = std::move(cpus);
-        if (++m_started == (int)m_threads.size()) m_done_cv.notify_all();
+        if (++m_started == m_nthreads) m_done_cv.notify_all();
     }
     long seen = 0;
     for (;;) {
@@ -486,7 +489,7 @@ void thread_pool::run_indexed(int n, const std::function<void(int, int)>& fn)
         std::lock_guard<std::mutex> l(m_mu);
         m_fn     = &fn;
         m_n      = n;
-        m_active = (int)m_threads.size();
+        m_active = m_nthreads;
         m_error  = nullptr;
         m_next   = 0;
         m_generation++;

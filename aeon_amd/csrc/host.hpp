@@ -167,7 +167,7 @@ public:
     void run(int n, const std::function<void(int)>& fn);
     // fn(task, worker): worker in [0, size()) identifies the calling pool thread
     void run_indexed(int n, const std::function<void(int, int)>& fn);
-    int  size() const { return (int)m_threads.size(); }
+    int  size() const { return m_nthreads; }
     const std::vector<int>& affinity_map() const { return m_map; }
     // what worker i's own sched_getaffinity returned after it pinned itself (blocks until every
     // worker has started); a CPU outside the process's cpuset cannot be pinned to, and that worker
@@ -178,7 +178,7 @@ private:
     void                                 worker(int index);
     std::vector<int>                     m_map;
     std::vector<std::vector<int>>        m_worker_cpus;
-    int                                  m_started = 0;
+    int                                  m_started = 0, m_nthreads = 0;
     std::vector<std::thread>             m_threads;
     std::mutex                           m_mu;
     std::condition_variable              m_cv, m_done_cv;

@@ -20,6 +20,21 @@
 // Every byte equals the two-launch path's (tests: test_full_batch_c3_all_records and the C3 cases).
 #include "augment_device.hpp"
 
+// development ablations / variants (tools/build_variants.sh): HUE4 = four pixels per hue batch;
+// NOB / NOA = no B stores / no A compute (wrong outputs)
+#ifndef AEON_REC_HUE4
+#define AEON_REC_HUE4 0
+#endif
+#ifndef AEON_REC_NOB
+#define AEON_REC_NOB 0
+#endif
+#ifndef AEON_REC_NOA
+#define AEON_REC_NOA 0
+#endif
+#ifndef AEON_REC_FUSED // FAST form: A and B of a row interleaved (rec_row_fast); 0 = B's row, then A's
+#define AEON_REC_FUSED 1
+#endif
+
 namespace aeon_hip {
 
 namespace {
@@ -46,12 +61,12 @@ struct RecTile {
 };
 
 // staged-source geometry of tile `band` (rows band*32 ...) of the record whose job is J
-__device__ __forceinline__ RecTile rec_tile(const JobRef& J, int band, int H, int stage_bytes, int32_t* error)
+__device__ __forceinline__ RecTile rec_tile(const JobRef& J, int band, int TR, int H, int stage_bytes, int32_t* error)
 {
     RecTile f;
     f.ok    = false;
-    f.y0    = band * kRecTR;
-    f.nrows = min(kRecTR, H - f.y0);
+    f.y0    = band * TR;
+    f.nrows = min(TR, H - f.y0);
     if (f.nrows <= 0) return f;
     const XTap xf = xcoef<RESIZE_LINEAR>(JF(J, win_x), JF(J, scale_x), JF(J, crop_w));
     const XTap xl = xcoef<RESIZE_LINEAR>(JF(J, win_x) + JF(J, win_w) - 1, JF(J, scale_x), JF(J, crop_w));
@@ -92,7 +107,7 @@ __device__ __forceinline__ void rec_record_tables(const LaunchArgs& a, const Rec
         xt[x]        = (i32x2){4 * (c.sx - u_lo), (c.a0 & 0xffff) | (c.a1 << 16)};
     }
     if (!(JF(J, photo) & PHOTO_HUE)) return;
-    const f32x4* wt  = reinterpret_cast<const f32x4*>(a.hsv_tables + kHsvDivWords);
+    const auto   wt  = lds_ptr<const f32x4>(L.hwt);
     const int    hue = JF(J, hue);
     const bool   sp  = fast;
     for (int i = tid; i < kHueTabEntries; i += nt) {
@@ -124,7 +139,9 @@ __device__ __forceinline__ void rec_table(const LaunchArgs& a, const RecLds& L, 
     for (int w = 0; w < nw; w++)
         for (int c = 0; c < 3; c++) s[c] += ps[w * 4 + c];
     // contrast_reduce: cv::mean = sum * (1./N) in f64, times (1 - c)
-    const double inv_n = 1. / (double)(W * H);
+    // (N from the job's LDS copy, not the kernel's W*H: a loop-invariant double would be hoisted out of
+    // the record loop and spilled, and its scratch reload waits for every store in flight)
+    const double inv_n = 1. / (double)(JF(J, win_w) * JF(J, win_h));
     const double kc    = 1.0 - (double)JF(J, contrast);
     double       sh[3];
     for (int c = 0; c < 3; c++) sh[c] = kc * ((double)s[c] * inv_n);
@@ -135,7 +152,7 @@ __device__ __forceinline__ void rec_table(const LaunchArgs& a, const RecLds& L, 
         int       y  = i & 255;
         if (photo & PHOTO_CONTRAST) y = u8rnd((float)((double)((float)y * c + 0.f) + sh[ch]));
         if (photo & PHOTO_LIGHTING) y = sat_u8(u8rnd((float)y * la + 0.f) + JFA(J, light_add, ch));
-        rt[i] = a.lut[ch * 256 + y];
+        rt[i] = lds_ldf(L.lut + (ch * 256 + y) * 4);
     }
 }
 
@@ -168,8 +185,12 @@ __device__ __forceinline__ u32x3 rec_pixels(const RecA& R, const RecLds& L, i32x
     if (FAST && (R.photo & PHOTO_HUE)) {
         const auto htab8 = lds_ptr<const i32x2>(L.htab) + 30;
         uint32_t   pk[4];
+#if AEON_REC_HUE4
+        hue_pack_n<4, 0>(sdv, hdiv, htab8, val, pk);
+#else
         hue_pack_n<2, 0>(sdv, hdiv, htab8, val, pk);
         hue_pack_n<2, 2>(sdv, hdiv, htab8, val, pk);
+#endif
         q = (u32x3){__builtin_amdgcn_perm(pk[1], pk[0], 0x04020100u), __builtin_amdgcn_perm(pk[2], pk[1], 0x05040201u),
                     __builtin_amdgcn_perm(pk[3], pk[2], 0x06050402u)};
     } else {
@@ -209,6 +230,68 @@ __device__ __forceinline__ void rec_store(const RecLds& L, __amdgpu_buffer_rsrc_
     store_f32x4(orsrc, ((bgr ? 0 : 2) * plane + idx) * 4, t(2, w0, 2), t(2, w1, 1), t(2, w2, 0), t(2, w2, 3));
 }
 
+
+// FAST form, A and B of one row of the tile interleaved in one instruction stream: B's table lookups
+// of one output plane are issued ahead of a third of A's arithmetic and its float4 store after it,
+// so the lookups' LDS latency is covered by A's VALU work instead of stalling every wave of the
+// workgroup at once (the waves leave each tile barrier together).  B's stores go through `orsrc`
+// with out-of-range offsets (dropped by the buffer bounds check) for lanes without a B row and
+// when the step has no B record (its resource has 0 bytes); A's bytes count only where `va`.
+__device__ __forceinline__ u32x3 rec_row_fast(const RecA& R, const RecLds& L, i32x4 ytr, bool va, uint32_t& s0,
+                                              uint32_t& s1, uint32_t& s2, __amdgpu_buffer_rsrc_t orsrc, int plane,
+                                              int idx_b, bool bgr, uint32_t w0, uint32_t w1, uint32_t w2)
+{
+    const auto T   = [&](int c, uint32_t w, int b) { return lds_ldf(L.rtab + c * 1024 + (int)((w >> (8 * b)) & 0xff) * 4); };
+    const auto off = [&](int oc) { return idx_b < 0 ? (int)kOutOfRange : (oc * plane + idx_b) * 4; };
+    const auto sdv  = lds_ptr<const i32x2>(L.hsv);
+    const auto hdiv = lds_ptr<const int32_t>(L.hsv + 256 * 8);
+    const auto htab8 = lds_ptr<const i32x2>(L.htab) + 30;
+    // B plane of source channel 0: lookups
+    float b[4] = {T(0, w0, 0), T(0, w0, 3), T(0, w1, 2), T(0, w2, 1)};
+    __builtin_amdgcn_sched_barrier(0);
+    int val[4][3];
+#pragma unroll
+    for (int k = 0; k < 4; k++) resize_px<RESIZE_LINEAR, false>(ytr, R.col[k], R.wx[k], val[k]);
+    __builtin_amdgcn_sched_barrier(0);
+    store_f32x4(orsrc, off(bgr ? 2 : 0), b[0], b[1], b[2], b[3]);
+    float g[4] = {T(1, w0, 1), T(1, w1, 0), T(1, w1, 3), T(1, w2, 2)};
+    __builtin_amdgcn_sched_barrier(0);
+    if (R.photo & PHOTO_BS) {
+#pragma unroll
+        for (int k = 0; k < 4; k++) bs_apply(BS_FIXPT, R.bs, val[k][0], val[k][1], val[k][2]);
+    }
+    uint32_t pk[4];
+    const bool hue = (R.photo & PHOTO_HUE) != 0;
+    if (hue) hue_pack_n<2, 0>(sdv, hdiv, htab8, val, pk);
+    __builtin_amdgcn_sched_barrier(0);
+    store_f32x4(orsrc, off(1), g[0], g[1], g[2], g[3]);
+    float r[4] = {T(2, w0, 2), T(2, w1, 1), T(2, w2, 0), T(2, w2, 3)};
+    __builtin_amdgcn_sched_barrier(0);
+    u32x3 q;
+    if (hue) {
+        hue_pack_n<2, 2>(sdv, hdiv, htab8, val, pk);
+        q = (u32x3){__builtin_amdgcn_perm(pk[1], pk[0], 0x04020100u), __builtin_amdgcn_perm(pk[2], pk[1], 0x05040201u),
+                    __builtin_amdgcn_perm(pk[3], pk[2], 0x06050402u)};
+    } else {
+        q = (u32x3){(uint32_t)val[0][0] | ((uint32_t)val[0][1] << 8) | ((uint32_t)val[0][2] << 16) | ((uint32_t)val[1][0] << 24),
+                    (uint32_t)val[1][1] | ((uint32_t)val[1][2] << 8) | ((uint32_t)val[2][0] << 16) | ((uint32_t)val[2][1] << 24),
+                    (uint32_t)val[2][2] | ((uint32_t)val[3][0] << 8) | ((uint32_t)val[3][1] << 16) | ((uint32_t)val[3][2] << 24)};
+    }
+    if (!va) q = (u32x3){0u, 0u, 0u};
+    s0 = __builtin_amdgcn_udot4(q.x, 0x01000001u, s0, false);
+    s0 = __builtin_amdgcn_udot4(q.y, 0x00010000u, s0, false);
+    s0 = __builtin_amdgcn_udot4(q.z, 0x00000100u, s0, false);
+    s1 = __builtin_amdgcn_udot4(q.x, 0x00000100u, s1, false);
+    s1 = __builtin_amdgcn_udot4(q.y, 0x01000001u, s1, false);
+    s1 = __builtin_amdgcn_udot4(q.z, 0x00010000u, s1, false);
+    s2 = __builtin_amdgcn_udot4(q.x, 0x00010000u, s2, false);
+    s2 = __builtin_amdgcn_udot4(q.y, 0x00000100u, s2, false);
+    s2 = __builtin_amdgcn_udot4(q.z, 0x01000001u, s2, false);
+    __builtin_amdgcn_sched_barrier(0);
+    store_f32x4(orsrc, off(bgr ? 0 : 2), r[0], r[1], r[2], r[3]);
+    return q;
+}
+
 } // namespace
 
 // One persistent workgroup per CU; records blockIdx.x, +G, ...  Lane (lph, lcg): column group lcg
@@ -228,7 +311,8 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) void 
     const RecLds L = rec_lds_layout(W, a.stage_bytes);
     const int    gpr = W >> 2;
     const int    lph = tid / gpr, lcg = tid - lph * gpr;
-    const bool   active = lph < kRecPhases;
+    const int    nph = r.phases, TR = nph * kRecTileRows;
+    const bool   active = lph < nph;
     const int    ox0 = lcg * 4;
     const int    plane = W * H;
     const bool   bgr = a.bgr_to_rgb != 0;
@@ -239,6 +323,10 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) void 
     const auto rec_of = [&](int k) { return (int)blockIdx.x + k * G; };
 
     hsv_div_tables(LdsLayout{0, L.hsv, 0, 0, 0, 0, 0, 0, 0, 0}, a.hsv_tables);
+    // the launch's constant tables in LDS: the per-record tables are then built without global loads,
+    // whose vmcnt waits would drain the B stores in flight at every record boundary
+    for (int i = tid; i < 3 * 256; i += nt) lds_ptr<float>(L.lut)[i] = a.lut[i];
+    for (int i = tid; i < 256 * 4; i += nt) lds_ptr<int32_t>(L.hwt)[i] = a.hsv_tables[kHsvDivWords + i];
     if (wave == 0) {
         rec_fetch_job(a, rec_of(0), slot(0));
         if (K > 1) rec_fetch_job(a, rec_of(1), slot(1));
@@ -247,7 +335,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) void 
     __syncthreads();
     rec_record_tables(a, L, JobRef{slot(0)}, W, FAST);
     // the first tile's staging and row taps
-    RecTile f = rec_tile(JobRef{slot(0)}, 0, H, L.stage_bytes, a.error);
+    RecTile f = rec_tile(JobRef{slot(0)}, 0, TR, H, L.stage_bytes, a.error);
     if (f.ok) {
         stage_issue(JobRef{slot(0)}, f.G, L.stage, wave, nw);
         rec_row_taps(JobRef{slot(0)}, f, L.yt, L.stage);
@@ -299,12 +387,12 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) void 
             if (next_same || next_rec) {
                 const JobRef JN{slot(next_same ? k : k + 1)};
                 if (next_rec && wave == 0 && k + 2 < K) rec_fetch_job(a, rec_of(k + 2), slot(k + 2));
-                fn = rec_tile(JN, next_same ? t + 1 : 0, H, L.stage_bytes, a.error);
+                fn = rec_tile(JN, next_same ? t + 1 : 0, TR, H, L.stage_bytes, a.error);
                 if (fn.ok) {
                     const int sb = L.stage + (par ^ 1) * L.stage_bytes;
                     stage_issue(JN, fn.G, sb, wave, nw);
                     pending = 0; // (the counted wait of that tile: the stores issued after these loads)
-                    rec_row_taps(JN, fn, L.yt + (par ^ 1) * kRecTR * 16, sb);
+                    rec_row_taps(JN, fn, L.yt + (par ^ 1) * kRecTRMax * 16, sb);
                 }
             }
             // the tile's two rows per lane: B's from the oldest held tile, A's into the newest
@@ -312,19 +400,35 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) void 
 #pragma unroll
             for (int u = 0; u < kRecTileRows; u++) {
                 const int j = t * kRecTileRows + u;
-                const int y = lph + kRecPhases * j;
-                if (hasB && __builtin_amdgcn_ballot_w64(active && y < H) != 0) {
+                const int y = lph + nph * j;
+                nwv[3 * u] = nwv[3 * u + 1] = nwv[3 * u + 2] = 0;
+                if (FAST && AEON_REC_FUSED && tile_a && f.ok) { // (uniform) A and B interleaved
+                    const bool  va  = active && y < H;
+                    const i32x4 ytr = lds_ptr<const i32x4>(L.yt + par * kRecTRMax * 16)[min(y - t * TR, TR - 1)];
+                    const u32x3 q   = rec_row_fast(R, L, ytr, va, s0, s1, s2, orsrc, plane, hasB && va ? y * W + ox0 : -1,
+                                                   bgr, rec[3 * u], rec[3 * u + 1], rec[3 * u + 2]);
+                    pending += 3;
+                    rec[3 * u] = q.x, rec[3 * u + 1] = q.y, rec[3 * u + 2] = q.z; // (B has read them)
+                    continue;
+                }
+                if (!AEON_REC_NOB && hasB && __builtin_amdgcn_ballot_w64(active && y < H) != 0) {
                     pending += 3;
                     if (active && y < H) rec_store(L, orsrc, plane, y * W + ox0, bgr, rec[3 * u], rec[3 * u + 1], rec[3 * u + 2]);
                 }
-                nwv[3 * u] = nwv[3 * u + 1] = nwv[3 * u + 2] = 0;
-                if (tile_a && f.ok && active && y < H) {
-                    const i32x4 ytr = lds_ptr<const i32x4>(L.yt + par * kRecTR * 16)[y - t * kRecTR];
-                    const u32x3 q   = rec_pixels<FAST>(R, L, ytr, s0, s1, s2);
-                    nwv[3 * u] = q.x, nwv[3 * u + 1] = q.y, nwv[3 * u + 2] = q.z;
+                if constexpr (!(FAST && AEON_REC_FUSED)) {
+                    if (!AEON_REC_NOA && tile_a && f.ok && active && y < H) {
+                        const i32x4 ytr = lds_ptr<const i32x4>(L.yt + par * kRecTRMax * 16)[y - t * TR];
+                        const u32x3 q   = rec_pixels<FAST>(R, L, ytr, s0, s1, s2);
+                        nwv[3 * u] = q.x, nwv[3 * u + 1] = q.y, nwv[3 * u + 2] = q.z;
+                    }
                 }
             }
-            // rotate: drop the tile B consumed, append the tile A produced
+            // rotate: drop the tile B consumed, append the tile A produced (the fused rows wrote A's
+            // words over B's in place: a cyclic rotation)
+            if (FAST && AEON_REC_FUSED && tile_a && f.ok) {
+#pragma unroll
+                for (int i = 0; i < 6; i++) nwv[i] = rec[i];
+            }
 #pragma unroll
             for (int i = 0; i < kRecWords - 6; i++) rec[i] = rec[i + 6];
 #pragma unroll

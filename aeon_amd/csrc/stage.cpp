@@ -1105,7 +1105,8 @@ bool run_records(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const voi
     if (o.dtype != AEON_DTYPE_F32 || !o.channel_major || o.fixed_aspect_ratio || o.channels != 3) return false;
     if ((((uint64_t)out_dev) & 15) != 0 || (o.item_stride & 15) != 0) return false;
     const int W = params[0].out_w, H = params[0].out_h;
-    if (W <= 0 || (W & 3) != 0 || W > 4 * 64 || H <= 0 || (H + kRecPhases - 1) / kRecPhases > kRecRows) return false;
+    const int nph = rec_phases(W, H);
+    if (W <= 0 || (W & 3) != 0 || W > 4 * 256 || H <= 0 || nph <= 0) return false;
     if (simd_boundary(W * 3) < W * 3) return false; // OpenCV's scalar row tail
     bool      contrast = false;
     long      stage    = 0;
@@ -1121,7 +1122,7 @@ bool run_records(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const voi
         g.mode = RESIZE_LINEAR, g.cn = 3, g.crop_w = p.crop_w, g.crop_h = p.crop_h, g.win_w = W, g.win_h = H;
         g.scale_x = 1. / ((double)W / p.crop_w);
         g.scale_y = 1. / ((double)H / p.crop_h);
-        stage     = std::max(stage, stage_bytes_for(3, stage_rows_for(g, kRecTR), stage_cols(g)));
+        stage     = std::max(stage, stage_bytes_for(3, stage_rows_for(g, nph * kRecTileRows), stage_cols(g)));
     }
     if (!contrast) return false;
     stage         = (stage + 1023) / 1024 * 1024;
@@ -1159,9 +1160,9 @@ bool run_records(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const voi
     a.out_dtype   = AEON_DTYPE_F32;
     a.channel_major = 1;
     a.bgr_to_rgb  = o.bgr_to_rgb && o.channels == 3;
-    a.threads     = (kRecPhases * (W / 4) + 63) / 64 * 64;
+    a.threads     = (nph * (W / 4) + 63) / 64 * 64;
     a.lds_bytes   = lds;
-    const RecArgs r{n, W, H, ((H + kRecPhases - 1) / kRecPhases + kRecTileRows - 1) / kRecTileRows};
+    const RecArgs r{n, nph, W, H, ((H + nph - 1) / nph + kRecTileRows - 1) / kRecTileRows};
     const int     grid  = std::min(n, ctx->n_cu); // one workgroup per CU (LDS, 14-16 waves at <= 128 VGPRs)
     const bool    timed = ctx->timing && (ctx->timing_calls++ % ctx->timing_every) == ctx->timing_every - 1;
     KernelTimer   t{};

@@ -179,10 +179,23 @@ def synthetic_pool(torch, records, w, h, cn=3, seed=0x5EED, chunk=64, device="cu
     return out
 
 
+def real_pool(torch, n, w, h):
+    """n HWC u8 w x h sources cut from aeon's decoded img_2112_70.jpg (tests/golden, 480x360 BGR) at
+    offsets that vary per record (natural-image statistics for the hue tables' LDS access pattern)."""
+    img = np.load(os.path.join(ROOT, "tests", "golden", "img_2112_70_bgr.npz"))["bgr"]
+    big = np.tile(img, (2, 2, 1))  # 960 x 720
+    H, W = big.shape[:2]
+    rng = np.random.default_rng(70)
+    wins = [big[y:y + h, x:x + w] for x, y in zip(rng.integers(0, W - w, 64), rng.integers(0, H - h, 64))]
+    base = torch.from_numpy(np.stack(wins).reshape(-1).copy()).to("cuda")
+    reps = (n + 63) // 64
+    return base.repeat(reps)[:n * w * h * 3].contiguous()
+
+
 class Workload:
     """Synthetic already-decoded sources in HBM + pre-drawn params for every step."""
 
-    def __init__(self, A, C, torch, cfg, batch, steps, rank, pool_mib, src_wh=(256, 256), world=1):
+    def __init__(self, A, C, torch, cfg, batch, steps, rank, pool_mib, src_wh=(256, 256), world=1, real=False):
         self.batch = batch
         self.aug = {"C2": C.C2_AUG, "C3": C.C3_AUG}[cfg]
         w, h = src_wh
@@ -193,6 +206,8 @@ class Workload:
         # pixels = A.synthetic_image(global record index) generated on the device
         records, seed = rank_slice(self.n_pool * batch * world, batch, rank, world)
         self.src = synthetic_pool(torch, records[:self.n_pool * batch], w, h)
+        if real:  # natural-image pixels instead: windows of aeon's img_2112_70.jpg record, tiled
+            self.src = real_pool(torch, self.n_pool * batch, w, h)
         self.descs = [(A.ImgDesc * batch)(*[A.ImgDesc(offset=(b * batch + i) * img_bytes, width=w, height=h,
                                                       stride=w * 3, channels=3) for i in range(batch)])
                       for b in range(self.n_pool)]
@@ -227,7 +242,7 @@ def step_bytes(params):
 
 
 def run_device(A, C, torch, cfg, batch, steps, warmup, rank, world, pool_mib, dist, timing=8, streams=1,
-               region=False):
+               region=False, real=False):
     """region: time the kernels as the timed region runs them, back to back -- one HIP event pair on
     the launch stream around steps 2..K (the first step only fills the queue), kt['augment'] = (that
     span, the steps' algorithmic bytes, K - 1).  A step of this workload is one tile-kernel launch
@@ -236,7 +251,7 @@ def run_device(A, C, torch, cfg, batch, steps, warmup, rank, world, pool_mib, di
     event pairs (timing) idle the queue around the launch they bracket and time it on a GPU that
     has drained the previous launch's stores (~8 % shorter)."""
     ctx = A.Context(torch.cuda.current_device())
-    wl = Workload(A, C, torch, cfg, batch, steps + warmup, rank, pool_mib, world=world)
+    wl = Workload(A, C, torch, cfg, batch, steps + warmup, rank, pool_mib, world=world, real=real)
     # streams > 1 (development): consecutive batches alternate between caller streams, as a
     # loader double-buffering its output batches would
     strs = [torch.cuda.current_stream().cuda_stream] + [torch.cuda.Stream().cuda_stream for _ in range(streams - 1)]

@@ -56,7 +56,8 @@ def test_records_c3_batch_sizes(ctxs, n):
     _check(ctxs, imgs, params, 224, 224, f"C3 n={n}")
 
 
-@pytest.mark.parametrize("out_w,out_h", [(224, 200), (128, 96), (64, 32), (4, 17), (256, 224), (96, 224)])
+@pytest.mark.parametrize("out_w,out_h", [(224, 200), (128, 96), (64, 32), (4, 17), (256, 224), (96, 224),
+                                         (320, 96), (512, 48), (1024, 24)])
 def test_records_output_sizes(ctxs, out_w, out_h):
     """Heights below 224 (fewer tiles than the register rotation), widths 4 .. 256."""
     rng = np.random.default_rng(out_w * 1000 + out_h)

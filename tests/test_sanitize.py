@@ -93,3 +93,38 @@ def test_product_library_agrees_with_sanitized_driver(corpus_run):
             assert want.startswith(got), (k, got, want)
             checked += 1
     assert checked > 1000
+
+
+HOST_ASAN = os.path.join(ROOT, "aeon_amd", "csrc", "build_sanitize", "host_driver_asan")
+HOST_TSAN = os.path.join(ROOT, "aeon_amd", "csrc", "build_sanitize", "host_driver_tsan")
+
+
+def _host_driver(target, exe, env_extra):
+    """tests/sanitize/host_driver.cpp over host.cpp + stager.cpp with the HIP runtime stubbed
+    (tests/sanitize/hip_stubs.cpp): loader configs, the pinned thread_pool, window draws on the pool
+    against serial draws over odd and even windows, a failing window, concurrent stager stages."""
+    if not os.path.exists("/opt/rocm/llvm/bin/clang++"):
+        pytest.skip("no clang with sanitizer runtimes")
+    subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "aeon_amd", "csrc"), target])
+    env = dict(os.environ, **env_extra)
+    env.pop("LD_PRELOAD", None)
+    r = subprocess.run([exe, "2"], capture_output=True, text=True, env=env, timeout=900)
+    lines = [l for l in r.stdout.splitlines() if "\t" in l]
+    return r, lines
+
+
+def test_host_layer_under_asan_ubsan():
+    r, lines = _host_driver("sanitize", HOST_ASAN, {"ASAN_OPTIONS": "detect_leaks=1:exitcode=86",
+                                                    "UBSAN_OPTIONS": "print_stacktrace=1:halt_on_error=1:exitcode=87"})
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
+    assert "Sanitizer" not in r.stderr and "runtime error" not in r.stderr, r.stderr[-3000:]
+    assert len(lines) >= 20 and all("\tok" in l for l in lines), r.stdout
+
+
+def test_host_layer_under_tsan():
+    """aeon's SANITIZER_TYPE=Thread build (/root/reference/CMakeLists.txt:80-101) of the pool code:
+    the draws of a window on the pool, pools started and stopped back to back, concurrent stages."""
+    r, lines = _host_driver("tsan", HOST_TSAN, {"TSAN_OPTIONS": "halt_on_error=1:exitcode=66"})
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
+    assert "ThreadSanitizer" not in r.stderr, r.stderr[-3000:]
+    assert len(lines) >= 20 and all("\tok" in l for l in lines), r.stdout
