@@ -228,7 +228,7 @@ constexpr int kRecWords  = 3 * kRecRows;           // 12 bytes (4 BGR pixels) pe
 
 // LDS carve of the record kernel (bytes, 16-aligned regions)
 struct RecLds {
-    int rtab, lut, hwt, hsv, htab, xt, yt, job, sums, stage, stage_bytes, total;
+    int rtab, lut, hwt, hsv, htab, xt, xt2, yt, job, sums, stage, stage_bytes, total;
 };
 AEON_HD inline RecLds rec_lds_layout(int win_w, int stage_bytes)
 {
@@ -240,6 +240,7 @@ AEON_HD inline RecLds rec_lds_layout(int win_w, int stage_bytes)
     L.hsv  = o; o += kHsvLdsDivBytes;       // sdiv + v/255, hdiv180
     L.htab = o; o += kHueTabBytes;          // hue table of the A record
     L.xt   = o; o += ((win_w * 8 + 15) / 16) * 16; // column taps of the A record
+    L.xt2  = o; o += ((win_w * 8 + 15) / 16) * 16; // (plain_records: the next record's)
     L.yt   = o; o += 2 * kRecTRMax * 16;    // row taps, one table per staging buffer
     L.job  = o; o += 3 * (int)sizeof(AugJob); // a ring of three records' jobs
     L.sums = o; o += 16 * 16;               // per-wave channel sums
@@ -249,14 +250,16 @@ AEON_HD inline RecLds rec_lds_layout(int win_w, int stage_bytes)
     return L;
 }
 
-// Row phases of a win_w-wide record: as many 4-column lane groups as 1024 lanes hold (at most
-// kRecPhasesMax), so a 224-wide record takes 18 x 56 = 1,008 lanes (16 waves); 0 if the lanes'
-// registers cannot hold win_h rows (more than kRecRows per lane).
+// Row phases of a win_w-wide record: 16 (a 224-wide record on 16 x 56 = 896 lanes, 14 waves: measured
+// 262 us per C3 batch against 271-275 us with 18 phases, 1,008 lanes) when the lanes' registers then
+// hold win_h rows (kRecRows per lane), else as many as 1024 lanes allow (at most kRecPhasesMax); 0 if
+// no lane count holds the record.
 AEON_HD inline int rec_phases(int win_w, int win_h)
 {
     const int gpr = win_w / 4;
     if (gpr <= 0) return 0;
-    const int nph = 1024 / gpr < kRecPhasesMax ? 1024 / gpr : kRecPhasesMax;
+    const int most = 1024 / gpr < kRecPhasesMax ? 1024 / gpr : kRecPhasesMax;
+    const int nph  = most >= 16 && (win_h + 15) / 16 <= kRecRows ? 16 : most;
     return nph > 0 && (win_h + nph - 1) / nph <= kRecRows ? nph : 0;
 }
 

@@ -79,7 +79,7 @@ __device__ __forceinline__ RecTile rec_tile(const JobRef& J, int band, int TR, i
     G.nr    = ycoef<RESIZE_LINEAR>(JF(J, win_y) + f.y0 + f.nrows - 1, JF(J, scale_y), JF(J, crop_h)).r1 - G.v_lo + 1;
     stage_layout(3, G);
     if (stage_need(G, 3) > stage_bytes) {
-        if ((threadIdx.x & 63) == 0) atomicOr(error, 2);
+        if (error && (threadIdx.x & 63) == 0) atomicOr(error, 2);
         return f;
     }
     f.ok = true;

@@ -1099,7 +1099,7 @@ bool run_records(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const voi
                  const aeon_aug_params* params, const aeon_out_desc& od, void* out_dev, hipStream_t stream,
                  bool is_mask, Phase&& phase)
 {
-    if (is_mask || !ctx->records || n <= 0) return false;
+    if (is_mask || n <= 0 || !ctx->records) return false;
     const OutView        ov = out_view(od);
     const aeon_out_desc& o  = ov.ko;
     if (o.dtype != AEON_DTYPE_F32 || !o.channel_major || o.fixed_aspect_ratio || o.channels != 3) return false;

@@ -111,3 +111,4 @@ def test_records_real_image_and_rerun(ctxs, golden):
     assert all(np.array_equal(a, b) for a, b in zip(r1, r2))
     ref = H.oracle_records(imgs[:40], params[:40], out)
     assert all(np.array_equal(a, b) for a, b in zip(r1[:40], ref))
+
