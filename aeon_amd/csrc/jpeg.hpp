@@ -2,12 +2,17 @@
 // descriptors shared by the host entropy decoder (jpeg_host.cpp) and the GPU kernels
 // (jpeg_kernels.hip).
 //
-// Split: Huffman decoding is a serial bit-stream walk per file, so it runs on the host pool (one
-// file per task); everything per pixel -- dequantisation, the ISLOW IDCT, fancy upsampling and the
-// YCbCr -> BGR conversion -- runs on the GPU, which writes the decoded HWC records straight into the
-// device source arena the augmentation kernels read.  What crosses PCIe is the sparse coefficient
-// stream: per 8x8 block a 64-bit zigzag mask of its non-zero coefficients plus those values (int16),
-// typically a fraction of the decoded pixels' bytes.
+// Split: the host pool parses each file's markers and tables.  A sequential file whose one scan
+// carries every component (baseline / extended, interleaved, or a grayscale scan) then goes to the GPU
+// whole: the host only unstuffs its entropy-coded bytes (splitting them at RSTn markers) into the
+// staging buffer, and jpeg_huff (jpeg_huff.hip) Huffman-decodes them -- subsequences of
+// kHuffSubBits bits decoded in parallel, self-synchronising from guessed starts, then a prefix sum
+// of block counts and DC differences and a final decode that writes every block's coefficients.
+// Progressive and multi-scan files are entropy-decoded on the host pool into the sparse stream (per
+// 8x8 block a 64-bit zigzag mask of its non-zero coefficients plus those values, int16).  Everything
+// per pixel -- dequantisation, the ISLOW IDCT, fancy upsampling and the YCbCr -> BGR conversion --
+// runs on the GPU, which writes the decoded HWC records straight into the device source arena the
+// augmentation kernels read.
 #pragma once
 #include <stdint.h>
 
@@ -25,8 +30,9 @@ struct jpeg_error : std::runtime_error {
 struct JpegState;
 class thread_pool;
 // shared: entropy-decode on that pool (the decoder's own, pinned to its cpu_list -- aeon's extract
-// runs inside provide() on the decode pool); null: a pool of the stage's own (thread_affinity_map)
-JpegState* jpeg_state_create(thread_pool* shared = nullptr);
+// runs inside provide() on the decode pool); null: a pool of the stage's own (thread_affinity_map).
+// gpu_huff false: every file through the host entropy decoder (AEON_HIP_JPEG_HUFF=host, A/B runs)
+JpegState* jpeg_state_create(thread_pool* shared = nullptr, bool gpu_huff = true);
 void       jpeg_state_destroy(JpegState* s);
 
 // One 8x8 block: bit z of `mask` = zigzag coefficient z is non-zero; its values follow in zigzag
@@ -40,7 +46,8 @@ struct alignas(16) JpegBlock {
 // One file of a decode call, as the kernels see it (device addresses).
 struct alignas(16) JpegImage {
     uint64_t blocks[3]; // JpegBlock[bh][bw] per component
-    uint64_t values;    // int16 coefficient values
+    uint64_t values;    // int16 coefficient values (sparse stream: host-decoded files)
+    uint64_t dvals[3];  // GPU-decoded files: 64 int16 per block (zigzag order, the mask's bits valid), else 0
     uint64_t planes[3]; // IDCT output per component: (bw*8) x (bh*8) uint8, row pitch bw*8
     uint64_t out;       // decoded record: HWC uint8 (BGR or gray), out_stride bytes per row
     int32_t  W, H, ncomp, out_cn, out_stride, hmax, vmax, pad_;
@@ -69,6 +76,53 @@ struct JpegChunk {
 struct JpegRows {
     int32_t img, y0, rows, pad_;
 };
+
+// ---- GPU entropy decoding (jpeg_huff.hip) ----
+
+constexpr int kHuffSubBits  = 1024; // subsequence: the bits one lane decodes per pass
+constexpr int kHuffLanes    = 256;  // jpeg_huff workgroup (one per file)
+constexpr int kHuffMaxBpm   = 16;   // blocks per MCU the GPU path takes (libjpeg allows 10)
+constexpr int kHuffFastBits = 10;   // lookahead of the LDS decode tables
+
+// One DHT table as the file defines it (code lengths 1..16, then the symbols), validated on the host.
+struct JpegHuffTab {
+    uint8_t counts[16];
+    uint8_t symbols[256];
+};
+
+// A restart interval of a scan (the whole scan without DRI): its unstuffed bytes, as bit offsets into
+// the file's data; its subsequences are [first_sub, first_sub + nsub) of the file.
+struct JpegHuffSeg {
+    uint32_t start_bit, end_bit;
+    int32_t  first_sub, nsub;
+};
+
+// Per-subsequence device scratch: start / end decoder state (bit position | block-in-MCU << 32 |
+// zigzag index << 40), blocks started and DC differences per component, their exclusive sums.
+struct alignas(16) JpegHuffSub {
+    uint64_t st, en;
+    int32_t  cnt[4]; // blocks started, DC difference sums of components 0..2
+    int32_t  ex[4];  // exclusive prefix of cnt over the file's subsequences
+};
+
+// One GPU-decoded file (device addresses).
+struct alignas(16) JpegHuffFile {
+    uint64_t data;      // unstuffed entropy-coded bytes, 4-byte aligned, segments back to back
+    uint64_t segs;      // JpegHuffSeg[nseg]
+    uint64_t sub_seg;   // int32 per subsequence: its segment
+    uint64_t tabs;      // JpegHuffTab[6]: DC of frame component k at k, AC at 3 + k
+    uint64_t subs;      // JpegHuffSub[nsub] (device scratch)
+    uint64_t blocks[3]; // JpegBlock[bh][bw] per frame component (zeroed before the launch)
+    uint64_t dvals[3];  // 64 int16 per block per frame component
+    uint64_t blk_tab[2]; // byte c (c < kHuffMaxBpm) = MCU block c: frame component | x << 2 | y << 4
+    int32_t  nseg, nsub, restart, n_mcu; // restart: MCUs per segment (n_mcu without DRI)
+    int32_t  bpm, mcux, ncomp;           // a non-interleaved (grayscale) scan: bpm 1, mcux = blocks per row
+    int32_t  truncated; // first segment whose data ends with the file, not a marker (reading past it is an error); -1: none
+    int32_t  bw[3], hs[3], vs[3], pad_;
+};
+
+// Device error word bit of a GPU-decoded file whose entropy-coded data is corrupt or truncated.
+constexpr int kJpegCorruptBit = 256;
 
 constexpr int kJpegIdctLanes  = 256;                             // IDCT workgroup: 8 lanes per block
 constexpr int kJpegIdctUnroll = 4;                               // blocks per lane group

@@ -19,10 +19,12 @@
 #include "../../include/aeon_hip.h"
 #include "host.hpp"
 #include "jpeg.hpp"
+#include "jpeg_huff.hpp"
 
 namespace aeon_hip {
 hipError_t launch_jpeg(const JpegImage* imgs, const JpegChunk* chunks, int n_chunks, const JpegRows* rows, int n_rows,
                        int color_lds, hipStream_t stream);
+hipError_t launch_jpeg_huff(const JpegHuffFile* files, int n_files, int32_t* error, hipStream_t stream);
 
 namespace {
 
@@ -36,11 +38,13 @@ const uint8_t kZigzagToNatural[80] = {
 
 inline int extend(int v, int s) { return v < (1 << (s - 1)) ? v - (1 << s) + 1 : v; }
 
-// AC fast table (10-bit lookahead): a code of L bits whose symbol (run r, size z) and value bits fit
-// in the 10 (L + z <= 10) decodes in one lookup.  Entry: bits 0-4 bits consumed, 5-8 run, 9-10 kind
-// (kAcValue: value in bits 16-31; kAcEob; kAcZrl), 0 = take the general path.
-constexpr int      kAcFastBits = 10;
-constexpr uint32_t kAcValue = 1u << 9, kAcEob = 2u << 9, kAcZrl = 3u << 9;
+// AC fast table (kAcFastBits lookahead): a code of L <= kAcFastBits bits decodes in one lookup -- with its
+// value when the value bits fit too (L + z <= kAcFastBits: kAcValue, value in bits 16-31), else its
+// symbol (kAcSym: run in bits 5-8, size z in bits 16-19; the value bits follow with one get()).
+// Entry: bits 0-4 bits consumed, 5-8 run, 9-11 kind (kAcValue, kAcEob, kAcZrl, kAcSym); 0 = a code
+// longer than the lookahead (the general path).
+constexpr int      kAcFastBits = 12;
+constexpr uint32_t kAcValue = 1u << 9, kAcEob = 2u << 9, kAcZrl = 3u << 9, kAcSym = 4u << 9, kAcKind = 7u << 9;
 
 // Canonical Huffman table with a 9-bit lookahead (libjpeg's jdhuff.c scheme).
 struct Huffman {
@@ -90,6 +94,8 @@ struct Huffman {
                         const int bits = (f >> (kAcFastBits - l - z)) & ((1 << z) - 1);
                         e = kAcValue | (uint32_t)(l + z) | ((uint32_t)r << 5) |
                             ((uint32_t)(uint16_t)(int16_t)extend(bits, z) << 16);
+                    } else if (z) {
+                        e = kAcSym | (uint32_t)l | ((uint32_t)r << 5) | ((uint32_t)z << 16);
                     }
                     fast[(code << (kAcFastBits - l)) | f] = e;
                 }
@@ -173,12 +179,14 @@ struct Bits {
         n -= e >> 8;
         return e & 0xff;
     }
-    // RSTn: drop buffered bits, skip to just past the marker
+    // RSTn: drop buffered bits, skip to just past the marker; none left: zeros follow (libjpeg's
+    // resync warns and decodes the missing intervals from no data)
     [[gnu::always_inline]] void restart()
     {
         buf = 0, n = 0, marker = false;
         while (p + 1 < end && !(p[0] == 0xFF && p[1] >= 0xD0 && p[1] <= 0xD7)) p++;
         if (p + 1 < end) p += 2;
+        else marker = true;
     }
 };
 
@@ -201,6 +209,7 @@ struct Arena {
     std::vector<uint8_t> host; // pageable staging, copied into the set's pinned buffer
     size_t               used = 0;
     std::vector<int16_t> coef; // progressive files: every block's 64 coefficients (zigzag order)
+    std::vector<uint32_t> seg; // GPU-decoded files: segment starts while unstuffing
     uint8_t*             reserve(size_t bytes)
     {
         used = (used + 15) & ~(size_t)15;
@@ -285,7 +294,7 @@ void parse_frame(const uint8_t* d, size_t size, Frame& f, const uint8_t** after)
     for (int k = 1; k < 64;) {
         b.fill();
         const uint32_t e    = act.fast[b.buf >> (64 - kAcFastBits)];
-        const uint32_t kind = e & (3u << 9);
+        const uint32_t kind = e & kAcKind;
         int            v;
         if (kind == kAcValue) { // code + value bits in one lookup
             const int used = e & 31;
@@ -293,6 +302,12 @@ void parse_frame(const uint8_t* d, size_t size, Frame& f, const uint8_t** after)
             b.n -= used;
             k += (e >> 5) & 15;
             v = (int16_t)(e >> 16);
+        } else if (kind == kAcSym) { // the code's symbol; its value bits next (filled: <= 16 + 16 bits)
+            const int used = e & 31, sz = (int)(e >> 16);
+            b.buf <<= used;
+            b.n -= used;
+            k += (e >> 5) & 15;
+            v = extend((int)b.get(sz), sz);
         } else if (e) { // EOB / ZRL
             b.buf <<= (e & 31);
             b.n -= (e & 31);
@@ -518,7 +533,10 @@ void decode_file(const uint8_t* d, size_t size, Frame& f, Arena& a, size_t blk_o
             break; // missing EOI: tolerated, as libjpeg does
         }
         const int m = *p++;
-        if (m == 0xD9) break;
+        if (m == 0xD9) {
+            if (!any_scan) bad("no scan data"); // (an image without a scan: libjpeg refuses it too)
+            break;
+        }
         if (m == 0xD8 || (m >= 0xD0 && m <= 0xD7) || m == 0x01) continue;
         if (p + 2 > end) bad("truncated marker segment");
         const int len = be16(p);
@@ -642,6 +660,237 @@ void decode_file(const uint8_t* d, size_t size, Frame& f, Arena& a, size_t blk_o
     a.used = *val_off + (size_t)nvals * sizeof(int16_t);
 }
 
+// A file whose entropy decoding runs on the GPU (jpeg_huff.hip): where its pieces sit in the worker's
+// arena and the scan's shape.
+struct GpuScan {
+    size_t   tabs = 0, segs = 0, sub_seg = 0, data = 0; // arena offsets
+    int      nseg = 0, nsub = 0, restart = 0, n_mcu = 0, bpm = 0, mcux = 0, truncated = -1;
+    bool     interleaved = false;
+    uint64_t blk_tab[2] = {0, 0};
+};
+
+// jdhuff.c jpeg_make_d_derived_tbl's code-space check (as Huffman::build).
+void check_code_space(const uint8_t* counts)
+{
+    int64_t code = 0;
+    for (int l = 1; l <= 16; l++) {
+        code += counts[l - 1];
+        if (code >= ((int64_t)1 << l)) bad("bad Huffman table");
+        code <<= 1;
+    }
+}
+
+// The markers, tables and scan header of a file for the GPU entropy decoder, and its entropy-coded
+// bytes unstuffed into the arena (segments split at RSTn when DRI is set; the data ends at the first
+// other marker -- jdhuff.c's fill_bit_buffer: zeros follow a marker -- or with the file).  Returns false
+// for the files the host decodes instead (decode_file): progressive (SOF2), a scan without every
+// component (non-interleaved multi-scan), a second scan, more than kHuffMaxBpm blocks per MCU, data
+// past 2^28 bytes.  Header errors throw as decode_file's do.
+bool prepare_gpu(const uint8_t* d, size_t size, Frame& f, Arena& a, GpuScan& g)
+{
+    const uint8_t* p = nullptr;
+    parse_frame(d, size, f, &p);
+    if (f.progressive) return false;
+    const uint8_t* end   = d + size;
+    const size_t   used0 = a.used;
+    JpegHuffTab    dct[4], act[4];
+    bool           dset[4] = {false, false, false, false}, aset[4] = {false, false, false, false};
+    int            restart = 0;
+    bool           adobe_rgb = false;
+    auto segment = [&](int m, const uint8_t* s, int len) {
+        const uint8_t* e = s + len - 2;
+        if (m == 0xC4) {
+            while (s < e) {
+                const int tc = s[0] >> 4, th = s[0] & 15;
+                if (tc > 1 || th > 3 || s + 17 > e) bad("bad Huffman table segment");
+                int tot = 0;
+                for (int i = 0; i < 16; i++) tot += s[1 + i];
+                if (tot > 256 || s + 17 + tot > e) bad("bad Huffman table segment");
+                check_code_space(s + 1);
+                JpegHuffTab& t = tc ? act[th] : dct[th];
+                std::memcpy(t.counts, s + 1, 16);
+                std::memset(t.symbols, 0, sizeof(t.symbols));
+                std::memcpy(t.symbols, s + 17, tot);
+                (tc ? aset : dset)[th] = true;
+                s += 17 + tot;
+            }
+        } else if (m == 0xDB) {
+            while (s < e) {
+                const int pq = s[0] >> 4, tq = s[0] & 15;
+                if (tq > 3 || pq > 1 || s + 1 + 64 * (pq + 1) > e) bad("bad quantisation table segment");
+                for (int i = 0; i < 64; i++) f.q[tq][kZigzagToNatural[i]] = pq ? be16(s + 1 + 2 * i) : s[1 + i];
+                f.qset[tq] = true;
+                s += 1 + 64 * (pq + 1);
+            }
+        } else if (m == 0xDD) {
+            if (len < 4) bad("bad restart interval segment");
+            restart = be16(s);
+        } else if (m == 0xEE) {
+            if (len >= 14 && std::memcmp(s, "Adobe", 5) == 0 && s[11] == 0) adobe_rgb = true;
+        }
+    };
+    { // tables before SOF
+        const uint8_t* q = d + 2;
+        while (q < p) {
+            while (q < p && *q != 0xFF) q++;
+            while (q < p && *q == 0xFF) q++;
+            if (q >= p) break;
+            const int m = *q++;
+            if (m == 0xD8 || (m >= 0xD0 && m <= 0xD7) || m == 0x01) continue;
+            const int len = be16(q);
+            if (m == 0xC0 || m == 0xC1 || m == 0xC2) break;
+            segment(m, q + 2, len);
+            q += len;
+        }
+    }
+    // markers up to the scan
+    int sc[3] = {0, 0, 0}, ns = 0;
+    for (;;) {
+        while (p < end && *p != 0xFF) p++;
+        while (p < end && *p == 0xFF) p++;
+        if (p >= end) bad("no scan data");
+        const int m = *p++;
+        if (m == 0xD9) bad("no scan data");
+        if (m == 0xD8 || (m >= 0xD0 && m <= 0xD7) || m == 0x01) continue;
+        if (p + 2 > end) bad("truncated marker segment");
+        const int len = be16(p);
+        if (len < 2 || p + len > end) bad("truncated marker segment");
+        if (m != 0xDA) {
+            if ((m >= 0xC0 && m <= 0xCF && m != 0xC4 && m != 0xC8 && m != 0xCC)) bad("second frame header");
+            segment(m, p + 2, len);
+            p += len;
+            continue;
+        }
+        if (len < 6) bad("bad scan header");
+        const uint8_t* s = p + 2;
+        ns               = s[0];
+        if (ns < 1 || ns > f.ncomp || len != 6 + 2 * ns) bad("bad scan header");
+        for (int i = 0; i < ns; i++) {
+            const int cid = s[1 + 2 * i], t = s[2 + 2 * i];
+            int       k   = 0;
+            while (k < f.ncomp && f.c[k].id != cid) k++;
+            if (k == f.ncomp) bad("scan names an unknown component");
+            f.c[k].td = t >> 4, f.c[k].ta = t & 15;
+            if (f.c[k].td > 3 || f.c[k].ta > 3) bad("bad Huffman table selector");
+            if (!f.qset[f.c[k].tq]) bad("component uses an undefined quantisation table");
+            sc[i] = k;
+        }
+        if (ns != f.ncomp) return false; // components in separate scans: the host decoder
+        for (int i = 0; i < ns; i++)
+            if (!dset[f.c[sc[i]].td] || !aset[f.c[sc[i]].ta]) bad("scan uses an undefined Huffman table");
+        if (s[1 + 2 * ns] != 0 || s[2 + 2 * ns] != 63 || s[3 + 2 * ns] != 0)
+            unsupported("progressive scan parameters in a sequential file");
+        p += len;
+        break;
+    }
+    // the scan's shape
+    const bool inter = ns > 1;
+    g.interleaved    = inter;
+    g.bpm = 0, g.blk_tab[0] = g.blk_tab[1] = 0;
+    if (inter) {
+        for (int i = 0; i < ns; i++) {
+            const Comp& c = f.c[sc[i]];
+            for (int y = 0; y < c.v; y++)
+                for (int x = 0; x < c.h; x++) {
+                    if (g.bpm == kHuffMaxBpm) return false;
+                    g.blk_tab[g.bpm >> 3] |= (uint64_t)(sc[i] | x << 2 | y << 4) << (8 * (g.bpm & 7));
+                    g.bpm++;
+                }
+        }
+        g.mcux = f.mcux, g.n_mcu = f.mcux * f.mcuy;
+    } else {
+        g.bpm = 1, g.blk_tab[0] = (uint64_t)sc[0];
+        g.mcux = (f.c[sc[0]].dw + 7) / 8, g.n_mcu = g.mcux * ((f.c[sc[0]].dh + 7) / 8);
+    }
+    g.restart = restart ? restart : g.n_mcu;
+    const int nseg_need = (g.n_mcu + g.restart - 1) / g.restart;
+    // unstuff the entropy-coded bytes into the arena (upper bound: what is left of the file)
+    const size_t left = (size_t)(end - p);
+    if (left >= ((size_t)1 << 28)) return false;
+    g.data       = (size_t)(a.reserve(left + 16) - a.host.data());
+    uint8_t* out = a.host.data() + g.data;
+    size_t   o   = 0;
+    auto&    seg = a.seg;
+    seg.assign(1, 0);
+    g.truncated = -1;
+    for (;;) {
+        const uint8_t* ff   = (const uint8_t*)std::memchr(p, 0xFF, (size_t)(end - p));
+        const uint8_t* stop = ff ? ff : end;
+        std::memcpy(out + o, p, (size_t)(stop - p));
+        o += (size_t)(stop - p);
+        if (!ff) { // the data runs into the end of the file
+            g.truncated = (int)seg.size() - 1;
+            p           = end;
+            break;
+        }
+        const int nx = ff + 1 < end ? ff[1] : 0xD9;
+        if (nx == 0) {
+            out[o++] = 0xFF, p = ff + 2;
+        } else if (restart && nx >= 0xD0 && nx <= 0xD7) {
+            seg.push_back((uint32_t)o), p = ff + 2;
+        } else if (restart && (int)seg.size() < nseg_need) {
+            // another marker inside a restart interval: its data ends (zeros follow), and the next
+            // interval starts after the next RSTn, wherever it is (decode_file's Bits::restart)
+            const uint8_t* r = ff;
+            while (r + 1 < end && !(r[0] == 0xFF && r[1] >= 0xD0 && r[1] <= 0xD7)) r++;
+            if (r + 1 >= end) {
+                p = ff;
+                break;
+            }
+            seg.push_back((uint32_t)o), p = r + 2;
+        } else {
+            p = ff; // a marker ends the scan's data
+            break;
+        }
+    }
+    std::memset(out + o, 0, 16);
+    a.used = g.data + ((o + 16 + 3) & ~(size_t)3);
+    // the markers after the scan: a second scan goes to the host decoder; Adobe APP14 as decode_file
+    for (;;) {
+        while (p < end && *p != 0xFF) p++;
+        while (p < end && *p == 0xFF) p++;
+        if (p >= end) break;
+        const int m = *p++;
+        if (m == 0xD9) break;
+        if (m == 0xD8 || (m >= 0xD0 && m <= 0xD7) || m == 0x01) continue;
+        if (p + 2 > end) bad("truncated marker segment");
+        const int len = be16(p);
+        if (len < 2 || p + len > end) bad("truncated marker segment");
+        if (m == 0xDA) {
+            a.used = used0;
+            return false;
+        }
+        if ((m >= 0xC0 && m <= 0xCF && m != 0xC4 && m != 0xC8 && m != 0xCC)) bad("second frame header");
+        if (m == 0xEE) segment(m, p + 2, len);
+        p += len;
+    }
+    if (adobe_rgb && f.ncomp == 3) unsupported("RGB (Adobe transform 0) JPEGs");
+    // segments: the ones past the scan's restart intervals are ignored, missing ones are empty
+    std::vector<JpegHuffSeg> segs(nseg_need);
+    int                      nsub = 0;
+    for (int s = 0; s < nseg_need; s++) {
+        const uint32_t b0 = s < (int)seg.size() ? seg[s] : (uint32_t)o;
+        const uint32_t b1 = s + 1 < (int)seg.size() ? seg[s + 1] : (uint32_t)o;
+        const uint32_t bits = 8 * (b1 - b0);
+        segs[s] = {8 * b0, 8 * b1, nsub, std::max(1, (int)((bits + kHuffSubBits - 1) / kHuffSubBits))};
+        nsub += segs[s].nsub;
+    }
+    if (g.truncated >= nseg_need) g.truncated = -1; // (data of an ignored interval)
+    g.nseg = nseg_need, g.nsub = nsub;
+    // tables of the frame's components (DC at k, AC at 3 + k), segments, subsequence -> segment
+    g.tabs           = (size_t)(a.reserve(6 * sizeof(JpegHuffTab)) - a.host.data());
+    JpegHuffTab* tab = (JpegHuffTab*)(a.host.data() + g.tabs);
+    std::memset(tab, 0, 6 * sizeof(JpegHuffTab));
+    for (int k = 0; k < f.ncomp; k++) tab[k] = dct[f.c[k].td], tab[3 + k] = act[f.c[k].ta];
+    g.segs = (size_t)(a.reserve(segs.size() * sizeof(JpegHuffSeg)) - a.host.data());
+    std::memcpy(a.host.data() + g.segs, segs.data(), segs.size() * sizeof(JpegHuffSeg));
+    g.sub_seg   = (size_t)(a.reserve((size_t)nsub * sizeof(int32_t)) - a.host.data());
+    int32_t* ss = (int32_t*)(a.host.data() + g.sub_seg);
+    for (int s = 0; s < nseg_need; s++)
+        for (int j = 0; j < segs[s].nsub; j++) *ss++ = s;
+    return true;
+}
+
 } // namespace
 
 // Per-context JPEG state: the decode pool, worker arenas, a two-deep ring of pinned staging +
@@ -659,8 +908,11 @@ struct JpegState {
         size_t     dev_cap = 0;
         uint8_t*   planes  = nullptr;
         size_t     planes_cap = 0;
+        uint8_t*   work    = nullptr; // GPU-decoded files: block records, dense coefficients, subsequence scratch
+        size_t     work_cap = 0;
     } sets[2];
     int        next = 0;
+    bool       gpu_huff = true; // false: every file through the host entropy decoder
     std::mutex mu;
 };
 
@@ -684,9 +936,10 @@ void hip_ok(hipError_t e, const char* what)
 
 } // namespace
 
-JpegState* jpeg_state_create(thread_pool* shared)
+JpegState* jpeg_state_create(thread_pool* shared, bool gpu_huff)
 {
     auto* s = new JpegState();
+    s->gpu_huff = gpu_huff;
     if (shared) {
         s->pool = shared;
     } else {
@@ -708,28 +961,39 @@ void jpeg_state_destroy(JpegState* s)
         if (st.pinned) (void)hipHostFree(st.pinned);
         if (st.dev) (void)hipFree(st.dev);
         if (st.planes) (void)hipFree(st.planes);
+        if (st.work) (void)hipFree(st.work);
     }
     delete s;
 }
 
-// The decode call (aeon_hip_decode_jpeg_batch): entropy-decode every file on the pool, stage the
-// coefficient streams + tables in one pinned buffer, one H2D, IDCT and colour kernels on `stream`.
-// start / stop (may be null): events recorded around the IDCT + colour launches (kernel timing)
+// The decode call (aeon_hip_decode_jpeg_batch): on the pool, each file's headers, then either its
+// entropy-coded bytes unstuffed for the GPU decoder (prepare_gpu) or the host entropy decoder's sparse
+// stream (decode_file); all of it staged in one pinned buffer, one H2D, then jpeg_huff, the IDCT and
+// the colour kernels on `stream`.  error: the context's device error word (corrupt entropy-coded data of
+// a GPU-decoded file sets kJpegCorruptBit; aeon_hip_synchronize reports it).
+// start / stop (may be null): events recorded around the GPU launches (kernel timing)
 void jpeg_decode_batch(JpegState* S, int n, const void* const* data, const size_t* sizes, const aeon_img_desc* descs,
-                       void* dst_base, hipStream_t stream, hipEvent_t start, hipEvent_t stop)
+                       void* dst_base, int32_t* error, hipStream_t stream, hipEvent_t start, hipEvent_t stop)
 {
     std::lock_guard<std::mutex> lock(S->mu);
     for (auto& a : S->arenas) a.used = 0;
-    std::vector<Frame>  frames(n);
-    std::vector<int>    owner(n);
-    std::vector<size_t> blk(3 * (size_t)n), val(n);
+    std::vector<Frame>   frames(n);
+    std::vector<int>     owner(n);
+    std::vector<size_t>  blk(3 * (size_t)n), val(n);
+    std::vector<GpuScan> gs(n);
+    std::vector<char>    on_gpu(n, 0);
     S->pool->run_indexed(n, [&](int i, int w) {
         try {
             if (!data[i] || !sizes[i]) bad("empty file");
             const aeon_img_desc& d = descs[i];
             if (d.channels != 1 && d.channels != 3) bad("decoded channels must be 1 or 3");
-            decode_file((const uint8_t*)data[i], sizes[i], frames[i], S->arenas[w], &blk[3 * (size_t)i], &val[i],
-                        d.channels == 1);
+            const uint8_t* b = (const uint8_t*)data[i];
+            if (S->gpu_huff && prepare_gpu(b, sizes[i], frames[i], S->arenas[w], gs[i])) {
+                on_gpu[i] = 1;
+            } else {
+                frames[i] = Frame();
+                decode_file(b, sizes[i], frames[i], S->arenas[w], &blk[3 * (size_t)i], &val[i], d.channels == 1);
+            }
             owner[i] = w;
             if (frames[i].W != d.width || frames[i].H != d.height)
                 bad("decoded size " + std::to_string(frames[i].W) + "x" + std::to_string(frames[i].H) +
@@ -739,15 +1003,28 @@ void jpeg_decode_batch(JpegState* S, int n, const void* const* data, const size_
             throw jpeg_error(e.code, std::string(e.what()) + " (record " + std::to_string(i) + ")");
         }
     });
-    // device layout of the call: [images][chunks][rows][arena 0][arena 1]...
+    // device layout of the call: [images][GPU-decoded files][chunks][rows][arena 0][arena 1]...; the
+    // work buffer (device only): [block records of the GPU-decoded files][their dense coefficients]
+    // [their subsequence scratch]
     std::vector<JpegChunk> chunks;
     std::vector<JpegRows>  rows;
     size_t                 plane_bytes = 0;
     std::vector<size_t>    plane_off(3 * (size_t)n, 0);
-    int                    color_lds = 0;
+    int                    color_lds = 0, n_gpu = 0;
+    size_t                 rec_bytes = 0, coef_bytes = 0, sub_bytes = 0;
+    std::vector<size_t>    wrec(3 * (size_t)n, 0), wcoef(3 * (size_t)n, 0), wsub(n, 0);
     for (int i = 0; i < n; i++) {
         const Frame& f  = frames[i];
         const int    nc = descs[i].channels == 1 ? 1 : f.ncomp; // grayscale output needs Y only
+        if (on_gpu[i]) {
+            n_gpu++;
+            for (int k = 0; k < f.ncomp; k++) {
+                const size_t nb = (size_t)f.c[k].bw * f.c[k].bh;
+                wrec[3 * (size_t)i + k] = rec_bytes, rec_bytes += (nb * sizeof(JpegBlock) + 255) & ~(size_t)255;
+                wcoef[3 * (size_t)i + k] = coef_bytes, coef_bytes += (nb * 64 * sizeof(int16_t) + 255) & ~(size_t)255;
+            }
+            wsub[i] = sub_bytes, sub_bytes += (size_t)gs[i].nsub * sizeof(JpegHuffSub);
+        }
         for (int k = 0; k < nc; k++) {
             plane_off[3 * (size_t)i + k] = plane_bytes;
             plane_bytes += ((size_t)f.c[k].bw * 8 * f.c[k].bh * 8 + 255) & ~(size_t)255;
@@ -769,7 +1046,8 @@ void jpeg_decode_batch(JpegState* S, int n, const void* const* data, const size_
         for (int y = 0; y < f.H; y += band) rows.push_back({i, y, std::min(band, f.H - y), 0});
     }
     const size_t img_bytes = (size_t)n * sizeof(JpegImage);
-    const size_t chk_off   = img_bytes;
+    const size_t huf_off   = (img_bytes + 255) & ~(size_t)255;
+    const size_t chk_off   = huf_off + (((size_t)n_gpu * sizeof(JpegHuffFile) + 255) & ~(size_t)255);
     const size_t row_off   = chk_off + ((chunks.size() * sizeof(JpegChunk) + 255) & ~(size_t)255);
     size_t       total     = row_off + ((rows.size() * sizeof(JpegRows) + 255) & ~(size_t)255);
     std::vector<size_t> arena_off(S->arenas.size());
@@ -785,15 +1063,23 @@ void jpeg_decode_batch(JpegState* S, int n, const void* const* data, const size_
     grow_buf(st.pinned, st.pinned_cap, total, true);
     grow_buf(st.dev, st.dev_cap, total, false);
     grow_buf(st.planes, st.planes_cap, std::max<size_t>(plane_bytes, 256), false);
-    const uint64_t dev = (uint64_t)st.dev;
+    const size_t coef_off = rec_bytes, sub_off = rec_bytes + coef_bytes;
+    if (n_gpu) grow_buf(st.work, st.work_cap, sub_off + sub_bytes, false);
+    const uint64_t dev  = (uint64_t)st.dev, work = (uint64_t)st.work;
     JpegImage*     imgs = (JpegImage*)st.pinned;
+    JpegHuffFile*  hf   = (JpegHuffFile*)(st.pinned + huf_off);
     for (int i = 0; i < n; i++) {
         const Frame& f = frames[i];
         JpegImage&   J = imgs[i];
         std::memset(&J, 0, sizeof(J));
         const uint64_t base = dev + arena_off[owner[i]];
         for (int k = 0; k < f.ncomp; k++) {
-            J.blocks[k] = base + blk[3 * (size_t)i + k];
+            if (on_gpu[i]) {
+                J.blocks[k] = work + wrec[3 * (size_t)i + k];
+                J.dvals[k]  = work + coef_off + wcoef[3 * (size_t)i + k];
+            } else {
+                J.blocks[k] = base + blk[3 * (size_t)i + k];
+            }
             J.planes[k] = (uint64_t)st.planes + plane_off[3 * (size_t)i + k];
             J.bw[k] = f.c[k].bw, J.bh[k] = f.c[k].bh, J.dw[k] = f.c[k].dw, J.dh[k] = f.c[k].dh;
             J.hs[k] = f.c[k].h, J.vs[k] = f.c[k].v;
@@ -801,10 +1087,27 @@ void jpeg_decode_batch(JpegState* S, int n, const void* const* data, const size_
             J.up[k] = jpeg_upsample_mode(J.hf[k], J.vf[k], f.c[k].dw);
             std::memcpy(J.q[k], f.q[f.c[k].tq], sizeof(J.q[k]));
         }
-        J.values     = base + val[i];
+        J.values     = on_gpu[i] ? 0 : base + val[i];
         J.out        = (uint64_t)dst_base + descs[i].offset;
         J.W          = f.W, J.H = f.H, J.ncomp = f.ncomp, J.out_cn = descs[i].channels, J.out_stride = descs[i].stride;
         J.hmax       = f.hmax, J.vmax = f.vmax;
+        if (!on_gpu[i]) continue;
+        const GpuScan& g = gs[i];
+        JpegHuffFile&  H = *hf++;
+        std::memset(&H, 0, sizeof(H));
+        H.data    = base + g.data;
+        H.segs    = base + g.segs;
+        H.sub_seg = base + g.sub_seg;
+        H.tabs    = base + g.tabs;
+        H.subs    = work + sub_off + wsub[i];
+        for (int k = 0; k < f.ncomp; k++) {
+            H.blocks[k] = J.blocks[k], H.dvals[k] = J.dvals[k];
+            H.bw[k] = f.c[k].bw;
+            H.hs[k] = g.interleaved ? f.c[k].h : 1, H.vs[k] = g.interleaved ? f.c[k].v : 1;
+        }
+        H.blk_tab[0] = g.blk_tab[0], H.blk_tab[1] = g.blk_tab[1];
+        H.nseg = g.nseg, H.nsub = g.nsub, H.restart = g.restart, H.n_mcu = g.n_mcu;
+        H.bpm = g.bpm, H.mcux = g.mcux, H.ncomp = f.ncomp, H.truncated = g.truncated;
     }
     if (!chunks.empty()) std::memcpy(st.pinned + chk_off, chunks.data(), chunks.size() * sizeof(JpegChunk));
     if (!rows.empty()) std::memcpy(st.pinned + row_off, rows.data(), rows.size() * sizeof(JpegRows));
@@ -812,7 +1115,9 @@ void jpeg_decode_batch(JpegState* S, int n, const void* const* data, const size_
         if (S->arenas[w].used) std::memcpy(st.pinned + arena_off[w], S->arenas[w].host.data(), S->arenas[w].used);
     });
     hip_ok(hipMemcpyAsync(st.dev, st.pinned, total, hipMemcpyHostToDevice, stream), "hipMemcpyAsync");
+    if (n_gpu) hip_ok(hipMemsetAsync(st.work, 0, rec_bytes, stream), "hipMemsetAsync");
     if (start) hip_ok(hipEventRecord(start, stream), "hipEventRecord");
+    if (n_gpu) hip_ok(launch_jpeg_huff((const JpegHuffFile*)(st.dev + huf_off), n_gpu, error, stream), "JPEG Huffman kernel");
     hip_ok(launch_jpeg((const JpegImage*)st.dev, (const JpegChunk*)(st.dev + chk_off), (int)chunks.size(),
                        (const JpegRows*)(st.dev + row_off), (int)rows.size(), color_lds, stream),
            "JPEG kernels");
@@ -857,6 +1162,63 @@ void jpeg_entropy_only(const void* data, size_t size, int* w, int* h, int* ncomp
         }
     }
     *w = f.W, *h = f.H, *ncomp = f.ncomp, *n_blocks = nb, *n_values = nv, *hash = hv;
+}
+
+// The GPU entropy decoder's algorithm on this thread (host-only, for tests): prepare_gpu, then
+// jpeg_huff's phases (jpeg_huff.hpp) one subsequence after another, the exclusive prefix serially --
+// summarised as jpeg_entropy_only summarises the host decoder, so the two can be compared.  Returns 0
+// when the file goes to the host decoder instead, 1 when decoded, -1 on corrupt entropy-coded data;
+// *rounds: the Jacobi rounds until every start settled.
+int jpeg_gpu_entropy_emulate(const void* data, size_t size, int* w, int* h, int* ncomp, int64_t* n_blocks,
+                             int64_t* n_values, uint64_t* hash, int* rounds)
+{
+    Frame   f;
+    Arena   a;
+    GpuScan g;
+    if (!prepare_gpu((const uint8_t*)data, size, f, a, g)) return 0;
+    std::vector<JpegBlock>   recs[3];
+    std::vector<int16_t>     coef[3];
+    std::vector<JpegHuffSub> subs(g.nsub);
+    JpegHuffFile             F;
+    std::memset(&F, 0, sizeof(F));
+    uint8_t* base = a.host.data();
+    F.data = (uint64_t)(base + g.data), F.segs = (uint64_t)(base + g.segs);
+    F.sub_seg = (uint64_t)(base + g.sub_seg), F.tabs = (uint64_t)(base + g.tabs), F.subs = (uint64_t)subs.data();
+    for (int k = 0; k < f.ncomp; k++) {
+        const size_t nb = (size_t)f.c[k].bw * f.c[k].bh;
+        recs[k].assign(nb, JpegBlock{0, 0, 0});
+        coef[k].assign(nb * 64, 0);
+        F.blocks[k] = (uint64_t)recs[k].data(), F.dvals[k] = (uint64_t)coef[k].data();
+        F.bw[k] = f.c[k].bw, F.hs[k] = g.interleaved ? f.c[k].h : 1, F.vs[k] = g.interleaved ? f.c[k].v : 1;
+    }
+    F.blk_tab[0] = g.blk_tab[0], F.blk_tab[1] = g.blk_tab[1];
+    F.nseg = g.nseg, F.nsub = g.nsub, F.restart = g.restart, F.n_mcu = g.n_mcu;
+    F.bpm = g.bpm, F.mcux = g.mcux, F.ncomp = f.ncomp, F.truncated = g.truncated;
+    std::unique_ptr<huff::Tables> T(new huff::Tables());
+    huff::tables_codes(*T, F, 0, 1);
+    huff::tables_fast(*T, F, 0, 1);
+    huff::pass_guess(*T, F, 0, 1);
+    int r = 0;
+    while (huff::pass_compare(F, 0, 1)) huff::pass_rewalk(*T, F, 0, 1), r++;
+    int32_t acc[4] = {0, 0, 0, 0};
+    for (auto& s : subs)
+        for (int i = 0; i < 4; i++) s.ex[i] = acc[i], acc[i] += s.cnt[i];
+    if (!huff::pass_write(*T, F, 0, 1)) return -1;
+    uint64_t hv  = 1469598103934665603ull;
+    auto     mix = [&](uint64_t x) {
+        for (int b = 0; b < 8; b++) hv = (hv ^ ((x >> (8 * b)) & 0xff)) * 1099511628211ull;
+    };
+    int64_t nb = 0, nv = 0;
+    for (int k = 0; k < f.ncomp; k++)
+        for (size_t b = 0; b < recs[k].size(); b++) {
+            const uint64_t m = recs[k][b].mask;
+            mix(m);
+            for (int z = 0; z < 64; z++)
+                if (m >> z & 1) mix((uint64_t)(uint16_t)coef[k][b * 64 + z]), nv++;
+            nb++;
+        }
+    *w = f.W, *h = f.H, *ncomp = f.ncomp, *n_blocks = nb, *n_values = nv, *hash = hv, *rounds = r;
+    return 1;
 }
 
 } // namespace aeon_hip

@@ -1,0 +1,96 @@
+// jpeg_huff.hip -- GPU Huffman decoding of sequential JPEG scans (ITU T.81 F.2.2; libjpeg's jdhuff.c
+// decode_mcu as cv::imdecode runs it under aeon's image::extractor::extract, src/etl_image.cpp:83-99),
+// for the files jpeg_host.cpp hands over whole: one scan carrying every component, its entropy-coded
+// bytes unstuffed and split at RSTn markers into segments (restart intervals) by the host.
+//
+// One workgroup per file.  A segment's bits are cut into subsequences of kHuffSubBits; the decoder
+// state at a codeword boundary is (bit position, block within the MCU c, zigzag index k), and the
+// state at a subsequence's end is a function of the state at its start.  So:
+//   1. every subsequence is decoded from a guessed start (its first bit, c = 0, k = 0; the segment's
+//      first subsequence starts exactly) up to the first codeword boundary at or past its end;
+//   2. Jacobi rounds: a subsequence whose start differs from its predecessor's end takes that end as
+//      its start and is decoded again -- until no start changes.  The segment's first start is exact,
+//      so after round r the first r + 1 starts are; Huffman codes (and JPEG's block structure)
+//      re-synchronise within a few codewords, so two or three rounds settle a file in practice;
+//   3. with exact starts, an exclusive prefix sum over the subsequences gives each one its first
+//      block and its DC predictors (blocks started, DC differences per component);
+//   4. a final decode of each subsequence writes its coefficients into the dense block slots (64 int16
+//      per block, zigzag order) and the blocks' non-zero masks, which jpeg_idct reads.
+// Decoding tables live in LDS: a kHuffFastBits lookahead per table whose entries carry the code
+// length, the AC run and, when the value bits fit the lookahead too, the decoded value; longer codes
+// take the canonical maxcode walk.  The bit reader holds 64 bits and one word loaded ahead, so the
+// next refill's global load is in flight while the current bits decode.  The per-lane logic is in
+// jpeg_huff.hpp (shared with the host emulation the CPU tests run).
+#include <hip/hip_runtime.h>
+
+#include "jpeg_huff.hpp"
+
+namespace aeon_hip {
+namespace {
+
+struct Scan {
+    int4 wsum[kHuffLanes / 64];
+    int4 carry;
+};
+
+// Inclusive scan of v over the workgroup's lanes, plus the running carry of earlier chunks.
+__device__ int4 wg_scan(Scan& X, int4 v)
+{
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int x = __shfl_up(v.x, o), y = __shfl_up(v.y, o), z = __shfl_up(v.z, o), w = __shfl_up(v.w, o);
+        if (lane >= o) v.x += x, v.y += y, v.z += z, v.w += w;
+    }
+    if (lane == 63) X.wsum[wave] = v;
+    __syncthreads();
+    int4 off = X.carry;
+    for (int i = 0; i < wave; i++) off.x += X.wsum[i].x, off.y += X.wsum[i].y, off.z += X.wsum[i].z, off.w += X.wsum[i].w;
+    v.x += off.x, v.y += off.y, v.z += off.z, v.w += off.w;
+    __syncthreads();
+    if (threadIdx.x == kHuffLanes - 1) X.carry = v;
+    return v;
+}
+
+} // namespace
+
+__global__ __launch_bounds__(kHuffLanes) void jpeg_huff(const JpegHuffFile* __restrict__ files, int32_t* __restrict__ error)
+{
+    __shared__ huff::Tables T;
+    __shared__ Scan         X;
+    const JpegHuffFile&     F    = files[blockIdx.x];
+    JpegHuffSub*            subs = (JpegHuffSub*)F.subs;
+    const int               tid = threadIdx.x, nsub = F.nsub;
+
+    huff::tables_codes(T, F, tid, kHuffLanes);
+    if (tid == 0) X.carry = make_int4(0, 0, 0, 0);
+    __syncthreads();
+    huff::tables_fast(T, F, tid, kHuffLanes);
+    __syncthreads();
+    // 1. guessed starts; 2. Jacobi rounds until every start is its predecessor's end
+    huff::pass_guess(T, F, tid, kHuffLanes);
+    for (;;) {
+        __syncthreads();
+        const int any = huff::pass_compare(F, tid, kHuffLanes);
+        if (!__syncthreads_or(any)) break;
+        huff::pass_rewalk(T, F, tid, kHuffLanes);
+    }
+    // 3. exclusive prefix of (blocks, DC differences) over the file's subsequences
+    for (int base = 0; base < nsub; base += kHuffLanes) {
+        const int  j = base + tid;
+        const int4 v = j < nsub ? *(const int4*)subs[j].cnt : make_int4(0, 0, 0, 0);
+        const int4 s = wg_scan(X, v);
+        if (j < nsub) *(int4*)subs[j].ex = make_int4(s.x - v.x, s.y - v.y, s.z - v.z, s.w - v.w);
+        __syncthreads();
+    }
+    // 4. the final decode: coefficients and masks
+    if (!huff::pass_write(T, F, tid, kHuffLanes)) atomicOr(error, kJpegCorruptBit);
+}
+
+hipError_t launch_jpeg_huff(const JpegHuffFile* files, int n_files, int32_t* error, hipStream_t stream)
+{
+    if (n_files > 0) hipLaunchKernelGGL(jpeg_huff, dim3(n_files), dim3(kHuffLanes), 0, stream, files, error);
+    return hipGetLastError();
+}
+
+} // namespace aeon_hip

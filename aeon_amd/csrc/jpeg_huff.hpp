@@ -1,0 +1,377 @@
+// jpeg_huff.hpp -- the GPU Huffman decoder's per-lane logic (jpeg_huff.hip), written once for the
+// device and for the host: jpeg_huff runs its phases on a workgroup's lanes with barriers between
+// them; tests/sanitize/huff_emu.cpp runs the same phases one subsequence after another to check them
+// against the host entropy decoder on CPU.  See jpeg_huff.hip for the algorithm.
+#pragma once
+#include "jpeg.hpp"
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define HUFF_FN __host__ __device__ __forceinline__
+#else
+#define HUFF_FN inline
+#endif
+
+namespace aeon_hip {
+namespace huff {
+
+// Fast-table entry: bits 0-4 bits consumed, 5-8 AC run, 9-11 kind, 16-31 value (kValue) or value
+// size (kSym).  0: no code of <= kHuffFastBits bits is a prefix (the long-code walk).
+constexpr uint32_t kValue = 1u << 9, kEob = 2u << 9, kZrl = 3u << 9, kSym = 4u << 9, kKind = 7u << 9;
+constexpr int      kTabs = 6; // DC of frame components 0..2, then AC of 0..2
+constexpr int      kFast = 1 << kHuffFastBits;
+
+struct Tables {
+    uint32_t fast[kTabs][kFast];
+    int32_t  maxcode[kTabs][17]; // largest code of each length (-1: none)
+    int32_t  delta[kTabs][17];   // index of its first symbol - its first code
+    uint8_t  vals[kTabs][256];
+};
+
+HUFF_FN int imin(int a, int b) { return a < b ? a : b; }
+HUFF_FN int extend(int v, int s) { return v < (1 << (s - 1)) ? v - (1 << s) + 1 : v; }
+
+HUFF_FN void or_mask(uint64_t* m, uint64_t v)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    atomicOr((unsigned long long*)m, (unsigned long long)v);
+#else
+    *m |= v;
+#endif
+}
+
+// Tables, part 1 (tables t0, t0 + dt, ...; symbols i0, i0 + di, ...): symbols, maxcode, delta.
+HUFF_FN void tables_codes(Tables& T, const JpegHuffFile& F, int i0, int di)
+{
+    const JpegHuffTab* tabs = (const JpegHuffTab*)F.tabs;
+    for (int i = i0; i < kTabs * 256; i += di)
+        if ((i >> 8) % 3 < F.ncomp) T.vals[i >> 8][i & 255] = tabs[i >> 8].symbols[i & 255];
+    for (int t = i0; t < kTabs; t += di) {
+        if (t % 3 >= F.ncomp) continue;
+        int code = 0, s = 0;
+        for (int l = 1; l <= 16; l++) {
+            const int n = tabs[t].counts[l - 1];
+            T.delta[t][l]   = s - code;
+            T.maxcode[t][l] = n ? code + n - 1 : -1;
+            code = (code + n) << 1;
+            s += n;
+        }
+    }
+}
+
+// The entry of lookahead x (kHuffFastBits bits) of table t.
+HUFF_FN uint32_t fast_entry(const Tables& T, int t, int x)
+{
+    for (int l = 1; l <= kHuffFastBits; l++) {
+        const int code = x >> (kHuffFastBits - l);
+        if (code > T.maxcode[t][l]) continue;
+        const int sym = T.vals[t][T.delta[t][l] + code];
+        if (t < 3) { // DC: the symbol is the difference's size
+            if (sym <= 15 && l + sym <= kHuffFastBits) {
+                const int bits = sym ? (x >> (kHuffFastBits - l - sym)) & ((1 << sym) - 1) : 0;
+                const int v    = sym ? extend(bits, sym) : 0;
+                return kValue | (uint32_t)(l + sym) | ((uint32_t)(uint16_t)(int16_t)v << 16);
+            }
+            return kSym | (uint32_t)l | ((uint32_t)sym << 16);
+        }
+        const int r = sym >> 4, z = sym & 15;
+        if (!z) return (r == 15 ? kZrl : kEob) | (uint32_t)l; // (jdhuff.c: size 0, run < 15 ends the block)
+        if (l + z <= kHuffFastBits) {
+            const int bits = (x >> (kHuffFastBits - l - z)) & ((1 << z) - 1);
+            return kValue | (uint32_t)(l + z) | ((uint32_t)r << 5) | ((uint32_t)(uint16_t)(int16_t)extend(bits, z) << 16);
+        }
+        return kSym | (uint32_t)l | ((uint32_t)r << 5) | ((uint32_t)z << 16);
+    }
+    return 0;
+}
+
+// Tables, part 2: the fast entries.
+HUFF_FN void tables_fast(Tables& T, const JpegHuffFile& F, int i0, int di)
+{
+    for (int i = i0; i < kTabs * kFast; i += di)
+        if ((i / kFast) % 3 < F.ncomp) T.fast[i / kFast][i % kFast] = fast_entry(T, i / kFast, i % kFast);
+}
+
+// Bits of a segment: words at or past `end` read as zeros (libjpeg's fill after a marker).  64 bits
+// in hand and the next word loaded ahead.
+struct Bits {
+    const uint32_t* w;
+    int             end;
+    uint64_t        buf; // next bits, first in bit 63
+    int             n;   // valid bits in buf
+    int             p;   // bit position of buf's bit 63
+    uint32_t        nxt; // word nw, loaded ahead
+    int             nw;
+
+    HUFF_FN uint32_t word(int i) const
+    {
+        const int      last = end > 0 ? (end - 1) >> 5 : 0;
+        const uint32_t v    = __builtin_bswap32(w[imin(i, last)]);
+        const int      rem  = end - i * 32;
+        return rem >= 32 ? v : (rem <= 0 ? 0u : v & (0xffffffffu << (32 - rem)));
+    }
+    HUFF_FN void start(int pos)
+    {
+        const int i = pos >> 5, s = pos & 31;
+        buf = (((uint64_t)word(i) << 32) | word(i + 1)) << s;
+        n   = 64 - s;
+        p   = pos;
+        nw  = i + 2;
+        nxt = word(nw);
+    }
+    // >= 32 valid bits: a code (<= 16) and its value bits (<= 15) without another check
+    HUFF_FN void fill()
+    {
+        if (n < 32) {
+            buf |= (uint64_t)nxt << (32 - n);
+            n += 32;
+            nxt = word(++nw);
+        }
+    }
+    HUFF_FN void skip(int l)
+    {
+        buf <<= l;
+        n -= l;
+        p += l;
+    }
+    HUFF_FN int get(int z) // 1..15 bits
+    {
+        const int v = (int)(buf >> (64 - z));
+        skip(z);
+        return v;
+    }
+};
+
+HUFF_FN Bits bits_at(const JpegHuffFile& F, const JpegHuffSeg& S, int pos)
+{
+    Bits b;
+    b.w   = (const uint32_t*)F.data;
+    b.end = (int)S.end_bit;
+    b.start(pos);
+    return b;
+}
+
+HUFF_FN uint64_t pack_state(int p, int c, int k) { return (uint32_t)p | ((uint64_t)c << 32) | ((uint64_t)k << 40); }
+
+// Where the blocks of a walk go (the final pass).
+struct Out {
+    int blk, blk_end; // current block (scan order), the segment's end
+    int mx, my;       // MCU of the current block
+    int pred0, pred1, pred2;
+    int trunc; // reading past the segment's data is an error
+};
+
+// Decode from state (b.p, c, k).  SYNC (!WRITE): up to the first codeword boundary at or past `stop`,
+// counting blocks started and DC differences per component in cnt.  WRITE: the same walk (the last
+// subsequence of a segment: until the segment's blocks are done) storing coefficients and masks.
+// Returns false on corrupt data (WRITE only).
+template <bool WRITE>
+HUFF_FN bool walk(const Tables& T, const JpegHuffFile& F, Bits& b, int& c, int& k, int stop, bool last, int4& cnt,
+                  Out& o)
+{
+    const uint64_t tab_lo = F.blk_tab[0], tab_hi = F.blk_tab[1];
+    auto blk_byte = [&](int cc) { return (int)(((cc < 8 ? tab_lo : tab_hi) >> (8 * (cc & 7))) & 0xff); };
+    int       comp = blk_byte(c) & 3;
+    uint64_t  mask = 0;
+    int16_t*  coef = nullptr;
+    uint64_t* mrec = nullptr;
+    bool      own  = k == 0; // the current block started in this walk
+    auto open = [&]() {     // WRITE: locate the current block in its component plane
+        const int    bt = blk_byte(c), x = (bt >> 2) & 3, y = (bt >> 4) & 3;
+        const int    bw = comp == 0 ? F.bw[0] : (comp == 1 ? F.bw[1] : F.bw[2]);
+        const int    hs = comp == 0 ? F.hs[0] : (comp == 1 ? F.hs[1] : F.hs[2]);
+        const int    vs = comp == 0 ? F.vs[0] : (comp == 1 ? F.vs[1] : F.vs[2]);
+        const size_t idx = (size_t)(o.my * vs + y) * bw + o.mx * hs + x;
+        coef = (int16_t*)(comp == 0 ? F.dvals[0] : (comp == 1 ? F.dvals[1] : F.dvals[2])) + idx * 64;
+        mrec = (uint64_t*)(comp == 0 ? F.blocks[0] : (comp == 1 ? F.blocks[1] : F.blocks[2])) + idx * 2;
+    };
+    if (WRITE && o.blk < o.blk_end) open();
+    for (;;) {
+        if (WRITE) {
+            if (o.blk >= o.blk_end || (!last && b.p >= stop)) break;
+        } else if (b.p >= stop) {
+            break;
+        }
+        b.fill();
+        const int t = k == 0 ? comp : 3 + comp;
+        uint32_t  e = T.fast[t][(int)(b.buf >> (64 - kHuffFastBits))];
+        if (!(e & kKind)) { // a code longer than the lookahead
+            int l = kHuffFastBits + 1, sym = -1;
+            for (; l <= 16; l++) {
+                const int code = (int)(b.buf >> (64 - l));
+                if (code <= T.maxcode[t][l]) {
+                    sym = T.vals[t][T.delta[t][l] + code];
+                    break;
+                }
+            }
+            if (sym < 0) {
+                if (WRITE) return false;
+                sym = 0, l = 1; // a guessed start off the code boundaries: any fixed continuation
+            }
+            if (k == 0) e = kSym | (uint32_t)l | ((uint32_t)sym << 16);
+            else if (!(sym & 15)) e = ((sym >> 4) == 15 ? kZrl : kEob) | (uint32_t)l;
+            else e = kSym | (uint32_t)l | ((uint32_t)(sym >> 4) << 5) | ((uint32_t)(sym & 15) << 16);
+        }
+        const uint32_t kind = e & kKind;
+        b.skip(e & 31);
+        int v = 0;
+        if (kind == kValue) {
+            v = (int)(int16_t)(e >> 16);
+        } else if (kind == kSym) {
+            int z = (int)(e >> 16);
+            if (z > 15) { // a DC size above 15 (the host decoder refuses it too)
+                if (WRITE) return false;
+                z = 15;
+            }
+            if (z) v = extend(b.get(z), z);
+        }
+        if (WRITE && o.trunc && b.p > b.end) return false; // past the end of the file's data
+        if (k == 0) { // DC difference
+            if (WRITE) {
+                const int pr = (comp == 0 ? o.pred0 : (comp == 1 ? o.pred1 : o.pred2)) + v;
+                if (comp == 0) o.pred0 = pr;
+                else if (comp == 1) o.pred1 = pr;
+                else o.pred2 = pr;
+                const int16_t dc = (int16_t)pr;
+                if (dc) {
+                    mask    = 1;
+                    coef[0] = dc;
+                }
+            } else {
+                cnt.x++;
+                if (comp == 0) cnt.y += v;
+                else if (comp == 1) cnt.z += v;
+                else cnt.w += v;
+            }
+            k = 1;
+        } else if (kind == kEob) {
+            k = 64;
+        } else if (kind == kZrl) {
+            k += 16;
+        } else {
+            k += (e >> 5) & 15;
+            if (WRITE) { // jpeg_natural_order's extra entries clamp a run past 63 to 63
+                const int z = imin(k, 63);
+                mask |= 1ull << z;
+                coef[z] = (int16_t)v;
+            }
+            k++;
+        }
+        if (k >= 64) { // block done
+            if (WRITE) {
+                if (own) mrec[0] = mask;
+                else if (mask) or_mask(mrec, mask);
+                mask = 0, own = true;
+                o.blk++;
+            }
+            k = 0;
+            if (++c == F.bpm) {
+                c = 0;
+                if (WRITE && ++o.mx == F.mcux) o.mx = 0, o.my++;
+            }
+            comp = blk_byte(c) & 3;
+            if (WRITE && o.blk < o.blk_end) open();
+        }
+    }
+    if (WRITE && k > 0 && mask) or_mask(mrec, mask); // a block split with the next subsequence
+    return true;
+}
+
+// Phase 1: subsequences j0, j0 + dj, ... from their guessed starts.
+HUFF_FN void pass_guess(const Tables& T, const JpegHuffFile& F, int j0, int dj)
+{
+    const JpegHuffSeg* segs = (const JpegHuffSeg*)F.segs;
+    const int32_t*     sseg = (const int32_t*)F.sub_seg;
+    JpegHuffSub*       subs = (JpegHuffSub*)F.subs;
+    Out                none{};
+    for (int j = j0; j < F.nsub; j += dj) {
+        const JpegHuffSeg S   = segs[sseg[j]];
+        const int         i   = j - S.first_sub, p = (int)S.start_bit + i * kHuffSubBits;
+        int4              cnt = make_int4(0, 0, 0, 0);
+        uint64_t          en  = 0;
+        if (i + 1 < S.nsub) { // (the segment's last subsequence ends nobody's start)
+            Bits b = bits_at(F, S, p);
+            int  c = 0, k = 0;
+            walk<false>(T, F, b, c, k, p + kHuffSubBits, false, cnt, none);
+            en = pack_state(b.p, c, k);
+        }
+        subs[j].st          = pack_state(p, 0, 0);
+        subs[j].en          = en;
+        *(int4*)subs[j].cnt = cnt;
+    }
+}
+
+// Phase 2a: a start that differs from its predecessor's end takes it (ex[0]: walk again).  Returns
+// whether any start changed.
+HUFF_FN int pass_compare(const JpegHuffFile& F, int j0, int dj)
+{
+    const JpegHuffSeg* segs = (const JpegHuffSeg*)F.segs;
+    const int32_t*     sseg = (const int32_t*)F.sub_seg;
+    JpegHuffSub*       subs = (JpegHuffSub*)F.subs;
+    int                any  = 0;
+    for (int j = j0; j < F.nsub; j += dj) {
+        const JpegHuffSeg S = segs[sseg[j]];
+        int               dirty = 0;
+        if (j > S.first_sub) {
+            const uint64_t e = subs[j - 1].en;
+            if (e != subs[j].st) subs[j].st = e, dirty = j + 1 < S.first_sub + S.nsub, any = 1;
+        }
+        subs[j].ex[0] = dirty;
+    }
+    return any;
+}
+
+// Phase 2b: walk the changed subsequences again from their new starts.
+HUFF_FN void pass_rewalk(const Tables& T, const JpegHuffFile& F, int j0, int dj)
+{
+    const JpegHuffSeg* segs = (const JpegHuffSeg*)F.segs;
+    const int32_t*     sseg = (const int32_t*)F.sub_seg;
+    JpegHuffSub*       subs = (JpegHuffSub*)F.subs;
+    Out                none{};
+    for (int j = j0; j < F.nsub; j += dj) {
+        if (!subs[j].ex[0]) continue;
+        const JpegHuffSeg S  = segs[sseg[j]];
+        const uint64_t    st = subs[j].st;
+        const int         p = (int)(uint32_t)st, stop = (int)S.start_bit + (j - S.first_sub + 1) * kHuffSubBits;
+        int               c = (int)(st >> 32) & 0xff, k = (int)(st >> 40) & 0xff;
+        int4              cnt = make_int4(0, 0, 0, 0);
+        Bits              b   = bits_at(F, S, p);
+        walk<false>(T, F, b, c, k, stop, false, cnt, none);
+        subs[j].en          = pack_state(b.p, c, k);
+        *(int4*)subs[j].cnt = cnt;
+    }
+}
+
+// Phase 4 (after the exclusive prefix of cnt into ex): the final decode.  Returns false if any of
+// the walks met corrupt data.
+HUFF_FN bool pass_write(const Tables& T, const JpegHuffFile& F, int j0, int dj)
+{
+    const JpegHuffSeg* segs = (const JpegHuffSeg*)F.segs;
+    const int32_t*     sseg = (const int32_t*)F.sub_seg;
+    JpegHuffSub*       subs = (JpegHuffSub*)F.subs;
+    const int          per_seg = F.restart * F.bpm, total = F.n_mcu * F.bpm;
+    bool               ok = true;
+    for (int j = j0; j < F.nsub; j += dj) {
+        const int         sg = sseg[j];
+        const JpegHuffSeg S  = segs[sg];
+        const int         i  = j - S.first_sub;
+        const int4        e0 = *(const int4*)subs[S.first_sub].ex, e1 = *(const int4*)subs[j].ex;
+        const uint64_t    st = subs[j].st;
+        int               c = (int)(st >> 32) & 0xff, k = (int)(st >> 40) & 0xff;
+        Out               o;
+        o.blk     = sg * per_seg + (e1.x - e0.x) - (k > 0);
+        o.blk_end = imin(sg * per_seg + per_seg, total);
+        o.pred0 = e1.y - e0.y, o.pred1 = e1.z - e0.z, o.pred2 = e1.w - e0.w;
+        o.trunc = F.truncated >= 0 && sg >= F.truncated;
+        if (o.blk < sg * per_seg) continue; // (a continuation with no block before it cannot be exact)
+        const int mcu = o.blk / F.bpm;
+        o.mx = mcu % F.mcux, o.my = mcu / F.mcux;
+        int4 cnt;
+        Bits b = bits_at(F, S, (int)(uint32_t)st);
+        if (!walk<true>(T, F, b, c, k, (int)S.start_bit + (i + 1) * kHuffSubBits, i + 1 == S.nsub, cnt, o)) ok = false;
+    }
+    return ok;
+}
+
+} // namespace huff
+} // namespace aeon_hip

@@ -80,23 +80,37 @@ __global__ __launch_bounds__(kJpegIdctLanes) void jpeg_idct(const JpegImage* __r
     const int        g = threadIdx.x >> 3, j = threadIdx.x & 7;
     const JpegBlock* blocks = (const JpegBlock*)I.blocks[k] + C.first;
     const int16_t*   vals   = (const int16_t*)I.values;
+    const int16_t*   dense  = (const int16_t*)I.dvals[k];
     JpegBlock        B[kJpegIdctUnroll];
 #pragma unroll
     for (int u = 0; u < kJpegIdctUnroll; u++) B[u] = blocks[min(g + u * G, C.count - 1)];
     int qv[8];
 #pragma unroll
     for (int r = 0; r < 8; r++) qv[r] = I.q[k][r * 8 + j];
-    // pass 1 inputs: column j of every block, dequantised (jidctint.c DEQUANTIZE = coef * quantval)
+    // pass 1 inputs: column j of every block, dequantised (jidctint.c DEQUANTIZE = coef * quantval);
+    // a GPU-decoded file's coefficients sit at their zigzag slot of the block's 64
     int col[kJpegIdctUnroll][8];
+    if (dense) {
 #pragma unroll
-    for (int u = 0; u < kJpegIdctUnroll; u++)
+        for (int u = 0; u < kJpegIdctUnroll; u++) {
+            const int16_t* bv = dense + (size_t)(C.first + min(g + u * G, C.count - 1)) * 64;
 #pragma unroll
-        for (int r = 0; r < 8; r++) {
-            const int z = kZzInv[r * 8 + j];
-            col[u][r]   = 0;
-            if ((B[u].mask >> z) & 1)
-                col[u][r] = (int)vals[B[u].val_off + __builtin_popcountll(B[u].mask & ((1ull << z) - 1))] * qv[r];
+            for (int r = 0; r < 8; r++) {
+                const int z = kZzInv[r * 8 + j];
+                col[u][r]   = (B[u].mask >> z) & 1 ? (int)bv[z] * qv[r] : 0;
+            }
         }
+    } else {
+#pragma unroll
+        for (int u = 0; u < kJpegIdctUnroll; u++)
+#pragma unroll
+            for (int r = 0; r < 8; r++) {
+                const int z = kZzInv[r * 8 + j];
+                col[u][r]   = 0;
+                if ((B[u].mask >> z) & 1)
+                    col[u][r] = (int)vals[B[u].val_off + __builtin_popcountll(B[u].mask & ((1ull << z) - 1))] * qv[r];
+            }
+    }
     int* s = slot + g * kSlot;
     const int bw = I.bw[k];
 #pragma unroll

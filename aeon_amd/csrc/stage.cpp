@@ -44,8 +44,8 @@ hipError_t contrast_records_lds_limit(int bytes);
 hipError_t launch_resize_generic(const ResizeJob* jobs, const uint8_t* table, int n_jobs, int max_tiles, int TR, int CW,
                                  int NR, int xs, int amax, int cn_max, int32_t* error, hipStream_t stream);
 void       jpeg_decode_batch(JpegState* S, int n, const void* const* data, const size_t* sizes,
-                             const aeon_img_desc* descs, void* dst_base, hipStream_t stream, hipEvent_t start,
-                             hipEvent_t stop);
+                             const aeon_img_desc* descs, void* dst_base, int32_t* error, hipStream_t stream,
+                             hipEvent_t start, hipEvent_t stop);
 void       jpeg_info(const void* data, size_t size, int* w, int* h, int* ncomp);
 void       jpeg_entropy_only(const void* data, size_t size, int* w, int* h, int* ncomp, int64_t* n_blocks,
                              int64_t* n_values, uint64_t* hash);
@@ -76,7 +76,8 @@ std::string device_error_text(int err)
                 {16, "hue table without a t1 channel"},
                 {32, "dynamic-tail counter left over by an earlier launch"},
                 {64, "rotation source box exceeds the launch's LDS"},
-                {128, "generic resize footprint exceeds the launch's LDS"}};
+                {128, "generic resize footprint exceeds the launch's LDS"},
+                {256, "JPEG entropy-coded data corrupt or truncated (GPU Huffman decoder)"}};
     std::string s;
     for (const auto& b : bits)
         if (err & b.bit) s += (s.empty() ? "" : "; ") + std::string(b.what);
@@ -723,6 +724,7 @@ struct aeon_hip_ctx {
     // the jobs from the pinned slot itself
     bool                 direct = true; // AEON_HIP_DIRECT=0: the multi-pass path (device job table) for every call
     bool                 records = true; // AEON_HIP_RECORDS=0: contrast calls through the two-launch path
+    bool                 jpeg_gpu_huff = true; // AEON_HIP_JPEG_HUFF=host: every JPEG through the host entropy decoder
     std::vector<JobGeom> geoms;              // reused per call
     JpegState*           jpeg = nullptr;     // JPEG decode stage (pool, staging ring), on first use
     thread_pool*         host_pool = nullptr; // the owning decoder's pool (ctx_share_pool), for the JPEG stage
@@ -1535,6 +1537,7 @@ int aeon_hip_ctx_create(int device, aeon_hip_ctx** out)
             if (const char* e = std::getenv("AEON_HIP_HOST_PROFILE")) c->host_profile = std::atoi(e) != 0;
             if (const char* e = std::getenv("AEON_HIP_DIRECT")) c->direct = std::atoi(e) != 0;
             if (const char* e = std::getenv("AEON_HIP_RECORDS")) c->records = std::atoi(e) != 0;
+            if (const char* e = std::getenv("AEON_HIP_JPEG_HUFF")) c->jpeg_gpu_huff = std::strcmp(e, "host") != 0;
 #ifdef AEON_HIP_TRACE
             // development builds only: s_memtime phase stamps of the tile kernel into this device buffer
             if (const char* e = std::getenv("AEON_HIP_TRACE_PTR")) c->trace = (uint32_t*)std::strtoull(e, nullptr, 0);
@@ -1822,7 +1825,7 @@ int aeon_hip_decode_jpeg_batch(aeon_hip_ctx* ctx, int n, const void* const* data
         if (!ctx || n < 0 || (n > 0 && (!data || !sizes || !descs || !dst_base))) fail(AEON_HIP_EINVAL, "null argument");
         if (n == 0) return 0;
         HIP_OK(hipSetDevice(ctx->device));
-        if (!ctx->jpeg) ctx->jpeg = jpeg_state_create(ctx->host_pool);
+        if (!ctx->jpeg) ctx->jpeg = jpeg_state_create(ctx->host_pool, ctx->jpeg_gpu_huff);
         KernelTimer t{};
         bool        timed = false;
         if (ctx->timing) {
@@ -1834,7 +1837,8 @@ int aeon_hip_decode_jpeg_batch(aeon_hip_ctx* ctx, int n, const void* const* data
                 t = take_timer(ctx, kTimerJpeg, px);
             }
         }
-        jpeg_decode_batch(ctx->jpeg, n, data, sizes, descs, dst_base, (hipStream_t)stream, timed ? t.start : nullptr,
+        jpeg_decode_batch(ctx->jpeg, n, data, sizes, descs, dst_base, ctx->d_error, (hipStream_t)stream,
+                          timed ? t.start : nullptr,
                           timed ? t.stop : nullptr);
         if (timed) {
             std::lock_guard<std::mutex> lock(ctx->mu);

@@ -197,7 +197,12 @@ class Workload:
 
     def __init__(self, A, C, torch, cfg, batch, steps, rank, pool_mib, src_wh=(256, 256), world=1, real=False):
         self.batch = batch
-        self.aug = {"C2": C.C2_AUG, "C3": C.C3_AUG}[cfg]
+        # "C2:CUBIC" etc.: the C2 workload with image::config's interpolation_method (the generic
+        # resize pre-pass, resize_kernels.hip)
+        base, _, interp = cfg.partition(":")
+        self.aug = dict({"C2": C.C2_AUG, "C3": C.C3_AUG}[base])
+        if interp:
+            self.aug["interpolation_method"] = interp
         w, h = src_wh
         img_bytes = w * h * 3
         per_batch = batch * img_bytes
@@ -750,6 +755,15 @@ def main():
                                     "ms_per_step": e2 / args.steps * 1e3,
                                     "what": "same workload, consecutive batches on two streams"}
         extra["C5"] = run_c5(A, C, torch, max(20, args.steps), 3, args.pool_mib)
+        # aeon's other interpolation methods on the C2 workload: a generic resize pre-pass
+        # (OpenCV 2.4's resizeGeneric_ / resizeArea_) into scratch, then the tile kernel's copy pass
+        extra["interpolation"] = {}
+        for m in ("CUBIC", "AREA", "LANCZOS4"):
+            em, ktm, _, _ = run_device(A, C, torch, "C2:" + m, batch, 20, 3, 0, 1, args.pool_mib, None, 1)
+            extra["interpolation"][m] = {"value": batch * 20 / em, "unit": "images/s", "ms_per_step": em / 20 * 1e3,
+                                         "kernels_us_per_step": {k: v[0] / 20 * 1e3 for k, v in ktm.items() if v[2]}}
+        extra["interpolation"]["what"] = ("C2 workload (batch 256) with interpolation_method set; every launch timed "
+                                          "(events idle the queue between launches: rates are lower bounds)")
         extra["e2e_host_to_host"] = {"value": run_e2e(A, C, torch, 256, 20), "unit": "images/s",
                                      "what": "pinned H2D of decoded 256x256 u8 + kernel + D2H of fp32 CHW"}
         extra["e2e_zero_copy"] = {"value": run_e2e(A, C, torch, 256, 20, zero_copy=True), "unit": "images/s",

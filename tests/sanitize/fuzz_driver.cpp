@@ -5,7 +5,9 @@
 // param_factory (json.hpp, param_factory.cpp) are called directly.
 //
 // Usage: fuzz_driver FILE...   (*.jpg, *.png, *.json).  One line per file: the outcome, "ok ..." or
-// "error <code> <message>"; a sanitizer finding aborts the run with a non-zero exit status.
+// "error <code> <message>"; for a JPEG a second line "gpu<TAB>FILE<TAB>..." with the outcome of the GPU
+// entropy decoder's algorithm (jpeg_huff, emulated on the host) on the same bytes.  A sanitizer finding
+// aborts the run with a non-zero exit status.
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
@@ -24,6 +26,8 @@ namespace aeon_hip {
 void jpeg_info(const void* data, size_t size, int* w, int* h, int* ncomp);
 void jpeg_entropy_only(const void* data, size_t size, int* w, int* h, int* ncomp, int64_t* n_blocks,
                        int64_t* n_values, uint64_t* hash);
+int  jpeg_gpu_entropy_emulate(const void* data, size_t size, int* w, int* h, int* ncomp, int64_t* n_blocks,
+                              int64_t* n_values, uint64_t* hash, int* rounds);
 void png_header(const void* data, size_t size, int* w, int* h, int* depth, int* ctype);
 void png_decode(const void* data, size_t size, int mode, void* dst, size_t stride, int* out_elem_bytes);
 } // namespace aeon_hip
@@ -38,6 +42,25 @@ bool ends_with(const std::string& s, const char* suf)
     return s.size() >= n && s.compare(s.size() - n, n, suf) == 0;
 }
 
+// The GPU entropy decoder's algorithm (host emulation of jpeg_huff) on the same bytes: "gpu host"
+// (the file goes to the host decoder), "gpu ok <hash> rounds <r>", "gpu corrupt" or "gpu error <code>".
+std::string run_jpeg_gpu(const std::vector<uint8_t>& d)
+{
+    try {
+        int      w, h, n, rounds = 0;
+        int64_t  nb, nv;
+        uint64_t hv;
+        const int r = jpeg_gpu_entropy_emulate(d.data(), d.size(), &w, &h, &n, &nb, &nv, &hv, &rounds);
+        if (r == 0) return "gpu host";
+        if (r < 0) return "gpu corrupt";
+        char buf[96];
+        std::snprintf(buf, sizeof(buf), "gpu ok %016llx rounds %d", (unsigned long long)hv, rounds);
+        return buf;
+    } catch (const jpeg_error& e) {
+        return "gpu error " + std::to_string(e.code) + " " + e.what();
+    }
+}
+
 std::string run_jpeg(const std::vector<uint8_t>& d)
 {
     int w, h, n;
@@ -45,8 +68,9 @@ std::string run_jpeg(const std::vector<uint8_t>& d)
     int64_t  nb, nv;
     uint64_t hv;
     jpeg_entropy_only(d.data(), d.size(), &w, &h, &n, &nb, &nv, &hv);
-    char buf[128];
-    std::snprintf(buf, sizeof(buf), "ok %dx%dx%d blocks %lld values %lld", w, h, n, (long long)nb, (long long)nv);
+    char buf[160];
+    std::snprintf(buf, sizeof(buf), "ok %dx%dx%d blocks %lld values %lld hash %016llx", w, h, n, (long long)nb,
+                  (long long)nv, (unsigned long long)hv);
     return buf;
 }
 
@@ -87,9 +111,12 @@ int main(int argc, char** argv)
         const std::string    name = argv[i];
         std::ifstream        in(name, std::ios::binary);
         std::vector<uint8_t> d((std::istreambuf_iterator<char>(in)), std::istreambuf_iterator<char>());
-        std::string          r;
+        std::string          r, gpu;
         try {
-            if (ends_with(name, ".jpg")) r = run_jpeg(d);
+            if (ends_with(name, ".jpg")) {
+                gpu = run_jpeg_gpu(d);
+                r   = run_jpeg(d);
+            }
             else if (ends_with(name, ".png")) r = run_png(d);
             else if (ends_with(name, ".json")) r = run_json(d);
             else r = "skipped";
@@ -103,6 +130,7 @@ int main(int argc, char** argv)
             r = std::string("error -2 ") + e.what();
         }
         std::printf("%s\t%s\n", name.c_str(), r.c_str());
+        if (!gpu.empty()) std::printf("gpu\t%s\t%s\n", name.c_str(), gpu.c_str());
     }
     return 0;
 }

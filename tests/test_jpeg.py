@@ -4,8 +4,10 @@ ISLOW + fancy upsampling, BGR / grayscale output).
 CPU: the oracle restatement (oracle/jpeg_oracle.cpp) against the committed goldens
 (tests/golden/make_jpeg_fixtures.py: Pillow/libjpeg-turbo decodes of aeon's own
 test/test_data/img_2112_70.jpg and flowers.jpg plus Pillow-encoded files), and the product's header
-parser (aeon_jpeg_info).  GPU: the product's decode (host entropy decode -> aeon_hip_decode_jpeg_batch
-IDCT / upsampling / colour kernels) bit-exact against the same goldens and the oracle.
+parser (aeon_jpeg_info).  GPU: the product's decode (aeon_hip_decode_jpeg_batch: sequential files
+entropy-decoded on the GPU by jpeg_huff, progressive ones on the host pool, then the IDCT / upsampling /
+colour kernels) bit-exact against the same goldens and the oracle, and the GPU entropy decoder against
+the host one (AEON_HIP_JPEG_HUFF=host) file for file.
 """
 import hashlib
 import os
@@ -129,3 +131,63 @@ def test_gpu_jpeg_errors(ctx):
     with pytest.raises(A.AeonHipError):
         ctx.decode_jpeg_batch([b[:40]], [A.ImgDesc(offset=0, width=3, height=2, stride=9, channels=3)],
                               dst.data_ptr())
+
+
+@pytest.fixture(scope="module")
+def host_ctx():
+    """A context whose JPEG stage entropy-decodes every file on the host (the flag is read when the
+    context is created)."""
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need a GPU"
+    os.environ["AEON_HIP_JPEG_HUFF"] = "host"
+    try:
+        c = A.Context(0)
+    finally:
+        del os.environ["AEON_HIP_JPEG_HUFF"]
+    yield c
+    c.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("channels", [3, 1])
+def test_gpu_huffman_matches_host_huffman(ctx, host_ctx, channels):
+    """Every fixture through the GPU entropy decoder (jpeg_huff) and through the host one: the same
+    decoded records, in one mixed call (sequential, restart-interval and progressive files together)."""
+    files = [_jpg(n) for n in NAMES] * 3
+    a = _decode_gpu(ctx, files, channels)
+    b = _decode_gpu(host_ctx, files, channels)
+    for i, (x, y) in enumerate(zip(a, b)):
+        assert np.array_equal(x, y), NAMES[i % len(NAMES)]
+
+
+@pytest.mark.gpu
+def test_gpu_huffman_window_of_aeon_files(ctx, oracle):
+    """A bench-sized window (256 records: aeon's img_2112_70.jpg and flowers.jpg alternating) through
+    the GPU entropy decoder: bit-exact against the oracle's decode of each file."""
+    files = [_jpg("img_2112_70"), _jpg("flowers")] * 128
+    res = _decode_gpu(ctx, files, 3)
+    want = [oracle.jpeg_decode(files[0], 3), oracle.jpeg_decode(files[1], 3)]
+    for i, r in enumerate(res):
+        assert np.array_equal(r, want[i % 2]), i
+
+
+@pytest.mark.gpu
+def test_gpu_huffman_corrupt_data_reported(ctx):
+    """Corrupt entropy-coded data of a GPU-decoded file (a flipped scan byte: an invalid Huffman code,
+    and a scan cut off with the file) comes back from aeon_hip_synchronize as a device error, and the
+    context decodes the next good window normally."""
+    import torch
+    # two inputs of tests/sanitize/corpus.npz (make_corpus.py), kept in tests/golden for the GPU box
+    corpus = np.load(os.path.join(HERE, "golden", "jpeg_corrupt.npz"))
+    for bad in ("s411_q85__flip10.jpg", "gray_rst__trunc_scan0.jpg"):
+        b = corpus[bad].tobytes()
+        w, h, n = A.jpeg_info(b)
+        dst = torch.zeros(w * h * 3 + 16, dtype=torch.uint8, device="cuda")
+        stream = torch.cuda.current_stream().cuda_stream
+        ctx.decode_jpeg_batch([b], [A.ImgDesc(offset=0, width=w, height=h, stride=w * 3, channels=3)],
+                              dst.data_ptr(), stream)
+        with pytest.raises(A.AeonHipError, match="JPEG entropy-coded data corrupt"):
+            ctx.synchronize(stream)
+    good = [_jpg("s420_q50")]
+    r = _decode_gpu(ctx, good, 3)
+    assert np.array_equal(_sha(r[0]), FX["s420_q50.bgr"])

@@ -5,7 +5,9 @@ the PNG decoder and the JSON reader + param_factory (aeon's SANITIZER_TYPE build
 /root/reference/CMakeLists.txt:80-101); it runs over tests/sanitize/corpus.npz (1,749 truncated,
 bit-flipped, over-full-table, oversized and deeply nested inputs, tests/sanitize/make_corpus.py).
 Every input must end in a clean result or a refused-input error, with no sanitizer report; the
-product library (non-sanitized, through the C ABI) must give the same outcome per input.
+product library (non-sanitized, through the C ABI) must give the same outcome per input.  The driver
+also runs the GPU entropy decoder's algorithm (jpeg_huff.hpp's phases, emulated on the host) on every
+JPEG: it must produce the host decoder's coefficients bit for bit, or refuse what the host refuses.
 """
 import os
 import subprocess
@@ -35,15 +37,34 @@ def corpus_run(tmp_path_factory):
     env.pop("LD_PRELOAD", None) if "asan" in env.get("LD_PRELOAD", "") else None
     r = subprocess.run([DRIVER] + [str(d / k) for k in names], capture_output=True, text=True, env=env,
                        timeout=600)
-    results = {}
-    for line in r.stdout.splitlines():
-        path, res = line.split("\t", 1)
-        results[os.path.basename(path)] = res
-    return r, results, corpus
+    return r, *_parse(r.stdout), corpus
+
+
+def _parse(stdout):
+    results, gpu = {}, {}
+    for line in stdout.splitlines():
+        if line.startswith("gpu\t"):
+            _, path, res = line.split("\t")
+            gpu[os.path.basename(path)] = res
+        else:
+            path, res = line.split("\t", 1)
+            results[os.path.basename(path)] = res
+    return results, gpu
+
+
+def _gpu_agrees(host, gpu):
+    """The emulated GPU decoder's outcome against the host decoder's on the same bytes."""
+    if gpu == "gpu host":  # progressive / multi-scan: the host decodes it
+        return True
+    if gpu.startswith("gpu ok"):
+        return host.startswith("ok") and host.split("hash ")[1] == gpu.split()[2]
+    if gpu == "gpu corrupt":  # corrupt or truncated entropy-coded data
+        return host.startswith("error -1 JPEG: corrupt") or host.startswith("error -1 JPEG: truncated scan data")
+    return host.startswith("error " + gpu[len("gpu error "):])  # the same header error
 
 
 def test_corpus_runs_clean_under_asan_ubsan(corpus_run):
-    r, results, corpus = corpus_run
+    r, results, _, corpus = corpus_run
     assert r.returncode == 0, r.stderr[-3000:]
     assert "Sanitizer" not in r.stderr and "runtime error" not in r.stderr, r.stderr[-3000:]
     assert set(results) == set(corpus.keys())
@@ -52,7 +73,7 @@ def test_corpus_runs_clean_under_asan_ubsan(corpus_run):
 
 
 def test_corpus_expected_outcomes(corpus_run):
-    _, results, _ = corpus_run
+    _, results, _, _ = corpus_run
     for k, res in results.items():
         if k.startswith("seed__"):
             assert res.startswith("ok"), (k, res)
@@ -68,15 +89,15 @@ def test_corpus_expected_outcomes(corpus_run):
 def test_product_library_agrees_with_sanitized_driver(corpus_run):
     """The shipped library (aeon_jpeg_entropy_decode / aeon_png_info + aeon_decode_png through the C
     ABI) on the same JPEG / PNG inputs: same accept / refuse decision and error code."""
-    _, results, corpus = corpus_run
+    _, results, _, corpus = corpus_run
     checked = 0
     for k in sorted(corpus.keys()):
         data = corpus[k].tobytes()
         want = results[k]
         if k.endswith(".jpg"):
             try:
-                w, h, n, nb, nv, _ = A.jpeg_entropy_decode(data)
-                got = f"ok {w}x{h}x{n} blocks {nb} values {nv}"
+                w, h, n, nb, nv, hv = A.jpeg_entropy_decode(data)
+                got = f"ok {w}x{h}x{n} blocks {nb} values {nv} hash {hv:016x}"
             except A.AeonHipError as e:
                 got = f"error {e.code}"
             assert got == want if got.startswith("ok") else want.startswith(got + " "), (k, got, want)
@@ -93,6 +114,42 @@ def test_product_library_agrees_with_sanitized_driver(corpus_run):
             assert want.startswith(got), (k, got, want)
             checked += 1
     assert checked > 1000
+
+
+def test_corpus_gpu_entropy_decoder_agrees(corpus_run):
+    """jpeg_huff's algorithm (guessed starts, Jacobi rounds, prefix sums, final decode) on every corpus
+    JPEG: the host decoder's coefficients bit for bit, or the same refusal."""
+    _, results, gpu, corpus = corpus_run
+    jpgs = [k for k in corpus.keys() if k.endswith(".jpg")]
+    assert set(gpu) == set(jpgs)
+    bad = [(k, results[k], gpu[k]) for k in jpgs if not _gpu_agrees(results[k], gpu[k])]
+    assert not bad, bad[:5]
+    assert sum(g.startswith("gpu ok") for g in gpu.values()) > 100  # decoded on the GPU path
+    assert sum(g == "gpu corrupt" for g in gpu.values()) > 10  # corrupt scan data caught
+
+
+def test_fixtures_gpu_entropy_decoder_bit_exact(tmp_path):
+    """aeon's two JPEGs and the synthetic fixtures (4:4:4 / 4:2:2 / 4:2:0 / 4:1:1, restart intervals,
+    grayscale, 1x1 .. 600x800, q10 .. q100): every sequential file decodes on the GPU path with the host
+    decoder's coefficients; the progressive ones stay on the host."""
+    if not os.path.exists("/opt/rocm/llvm/bin/clang++"):
+        pytest.skip("no clang with sanitizer runtimes")
+    subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "aeon_amd", "csrc"), "sanitize"])
+    fx = np.load(os.path.join(ROOT, "tests", "golden", "jpeg_fixtures.npz"))
+    names = [k for k in fx.files if k.endswith(".jpg")]
+    for k in names:
+        (tmp_path / k).write_bytes(fx[k].tobytes())
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:exitcode=86")
+    env.pop("LD_PRELOAD", None)
+    r = subprocess.run([DRIVER] + [str(tmp_path / k) for k in names], capture_output=True, text=True, env=env,
+                       timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    results, gpu = _parse(r.stdout)
+    for k in names:
+        if k.startswith("prog_"):
+            assert gpu[k] == "gpu host", (k, gpu[k])
+        else:
+            assert gpu[k].startswith("gpu ok") and _gpu_agrees(results[k], gpu[k]), (k, results[k], gpu[k])
 
 
 HOST_ASAN = os.path.join(ROOT, "aeon_amd", "csrc", "build_sanitize", "host_driver_asan")

@@ -28,8 +28,8 @@ if __name__ == "__main__":
     variants = [dict()]
     cfgs = (("C2", 256), ("C3", 1024))
     argv = sys.argv[1:]
-    if argv and argv[0] in ("C2", "C3"):
-        cfgs = tuple(c for c in cfgs if c[0] == argv[0])
+    if argv and argv[0].split(":")[0] in ("C2", "C3"):
+        cfgs = ((argv[0], 1024 if argv[0].startswith("C3") else 256),)
         argv = argv[1:]
     if argv == ["default"]:
         variants = [dict()]

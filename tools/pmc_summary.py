@@ -31,7 +31,7 @@ if __name__ == "__main__":
             print(f"    {c:28s} {v:16.1f}")
     if len(sys.argv) > 3:
         cfg, out = sys.argv[2], sys.argv[3]
-        main = [k for k in s if "augment_tiles<0," in k or "augment_tilesILi0E" in k]  # KM_FINAL
+        main = [k for k in s if "augment_tiles<0," in k or "augment_tilesILi0E" in k or "contrast_records" in k]
         tot = {}
         for k in main:
             cs = s[k]
