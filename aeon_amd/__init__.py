@@ -136,6 +136,7 @@ def lib():
         L.aeon_jpeg_info.argtypes = [ctypes.c_char_p, ctypes.c_size_t] + [P(ctypes.c_int)] * 3
         L.aeon_jpeg_entropy_decode.argtypes = ([ctypes.c_char_p, ctypes.c_size_t] + [P(ctypes.c_int)] * 3 +
                                                [P(ctypes.c_int64)] * 2 + [P(ctypes.c_uint64)])
+        L.aeon_jpeg_host_stage.argtypes = [ctypes.c_char_p, ctypes.c_size_t, P(ctypes.c_int), P(ctypes.c_int64)]
         L.aeon_png_info.argtypes = [ctypes.c_char_p, ctypes.c_size_t] + [P(ctypes.c_int)] * 4
         L.aeon_decode_png.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int, vp, ctypes.c_size_t,
                                       P(ctypes.c_int)]
@@ -254,6 +255,14 @@ def jpeg_entropy_decode(data):
     _check(lib().aeon_jpeg_entropy_decode(bytes(data), len(data), ctypes.byref(w), ctypes.byref(h), ctypes.byref(n),
                                           ctypes.byref(nb), ctypes.byref(nv), ctypes.byref(hv)))
     return w.value, h.value, n.value, nb.value, nv.value, hv.value
+
+
+def jpeg_host_stage(data):
+    """The JPEG batch decode's host work for one file (aeon_jpeg_host_stage): (GPU entropy decoding?,
+    bytes staged for the H2D)."""
+    g, nb = ctypes.c_int(), ctypes.c_int64()
+    _check(lib().aeon_jpeg_host_stage(bytes(data), len(data), ctypes.byref(g), ctypes.byref(nb)))
+    return bool(g.value), nb.value
 
 
 PNG_BGR8, PNG_GRAY8, PNG_ANYDEPTH = 0, 1, 2

@@ -6,7 +6,7 @@
 // carries every component (baseline / extended, interleaved, or a grayscale scan) then goes to the GPU
 // whole: the host only unstuffs its entropy-coded bytes (splitting them at RSTn markers) into the
 // staging buffer, and jpeg_huff (jpeg_huff.hip) Huffman-decodes them -- subsequences of
-// kHuffSubBits bits decoded in parallel, self-synchronising from guessed starts, then a prefix sum
+// a few hundred bits decoded in parallel, self-synchronising from guessed starts, then a prefix sum
 // of block counts and DC differences and a final decode that writes every block's coefficients.
 // Progressive and multi-scan files are entropy-decoded on the host pool into the sparse stream (per
 // 8x8 block a 64-bit zigzag mask of its non-zero coefficients plus those values, int16).  Everything
@@ -79,8 +79,9 @@ struct JpegRows {
 
 // ---- GPU entropy decoding (jpeg_huff.hip) ----
 
-constexpr int kHuffSubBits  = 1024; // subsequence: the bits one lane decodes per pass
-constexpr int kHuffLanes    = 256;  // jpeg_huff workgroup (one per file)
+constexpr int kHuffSubMin   = 256;  // subsequence (the bits one lane decodes per pass): per file, the
+constexpr int kHuffSubMax   = 1024; // multiple of 32 in [min, max] nearest to spreading it over the lanes
+constexpr int kHuffLanes    = 1024; // jpeg_huff workgroup (one per file)
 constexpr int kHuffMaxBpm   = 16;   // blocks per MCU the GPU path takes (libjpeg allows 10)
 constexpr int kHuffFastBits = 10;   // lookahead of the LDS decode tables
 
@@ -118,7 +119,7 @@ struct alignas(16) JpegHuffFile {
     int32_t  nseg, nsub, restart, n_mcu; // restart: MCUs per segment (n_mcu without DRI)
     int32_t  bpm, mcux, ncomp;           // a non-interleaved (grayscale) scan: bpm 1, mcux = blocks per row
     int32_t  truncated; // first segment whose data ends with the file, not a marker (reading past it is an error); -1: none
-    int32_t  bw[3], hs[3], vs[3], pad_;
+    int32_t  bw[3], hs[3], vs[3], sub_bits; // sub_bits: the file's subsequence length
 };
 
 // Device error word bit of a GPU-decoded file whose entropy-coded data is corrupt or truncated.

@@ -24,7 +24,7 @@
 namespace aeon_hip {
 hipError_t launch_jpeg(const JpegImage* imgs, const JpegChunk* chunks, int n_chunks, const JpegRows* rows, int n_rows,
                        int color_lds, hipStream_t stream);
-hipError_t launch_jpeg_huff(const JpegHuffFile* files, int n_files, int32_t* error, hipStream_t stream);
+hipError_t launch_jpeg_huff(const JpegHuffFile* files, int n_files, int lanes, int32_t* error, hipStream_t stream);
 
 namespace {
 
@@ -664,7 +664,7 @@ void decode_file(const uint8_t* d, size_t size, Frame& f, Arena& a, size_t blk_o
 // arena and the scan's shape.
 struct GpuScan {
     size_t   tabs = 0, segs = 0, sub_seg = 0, data = 0; // arena offsets
-    int      nseg = 0, nsub = 0, restart = 0, n_mcu = 0, bpm = 0, mcux = 0, truncated = -1;
+    int      nseg = 0, nsub = 0, restart = 0, n_mcu = 0, bpm = 0, mcux = 0, truncated = -1, sub_bits = 0;
     bool     interleaved = false;
     uint64_t blk_tab[2] = {0, 0};
 };
@@ -686,7 +686,7 @@ void check_code_space(const uint8_t* counts)
 // for the files the host decodes instead (decode_file): progressive (SOF2), a scan without every
 // component (non-interleaved multi-scan), a second scan, more than kHuffMaxBpm blocks per MCU, data
 // past 2^28 bytes.  Header errors throw as decode_file's do.
-bool prepare_gpu(const uint8_t* d, size_t size, Frame& f, Arena& a, GpuScan& g)
+bool prepare_gpu(const uint8_t* d, size_t size, Frame& f, Arena& a, GpuScan& g, int lanes)
 {
     const uint8_t* p = nullptr;
     parse_frame(d, size, f, &p);
@@ -865,14 +865,17 @@ bool prepare_gpu(const uint8_t* d, size_t size, Frame& f, Arena& a, GpuScan& g)
         p += len;
     }
     if (adobe_rgb && f.ncomp == 3) unsupported("RGB (Adobe transform 0) JPEGs");
-    // segments: the ones past the scan's restart intervals are ignored, missing ones are empty
+    // segments: the ones past the scan's restart intervals are ignored, missing ones are empty;
+    // subsequences: the data spread over the workgroup's lanes, within [kHuffSubMin, kHuffSubMax] bits
+    const int64_t spread = ((int64_t)8 * o / std::max(lanes, 1) + 31) & ~(int64_t)31;
+    g.sub_bits = (int)std::min<int64_t>(kHuffSubMax, std::max<int64_t>(kHuffSubMin, spread));
     std::vector<JpegHuffSeg> segs(nseg_need);
     int                      nsub = 0;
     for (int s = 0; s < nseg_need; s++) {
         const uint32_t b0 = s < (int)seg.size() ? seg[s] : (uint32_t)o;
         const uint32_t b1 = s + 1 < (int)seg.size() ? seg[s + 1] : (uint32_t)o;
         const uint32_t bits = 8 * (b1 - b0);
-        segs[s] = {8 * b0, 8 * b1, nsub, std::max(1, (int)((bits + kHuffSubBits - 1) / kHuffSubBits))};
+        segs[s] = {8 * b0, 8 * b1, nsub, std::max(1, (int)((bits + g.sub_bits - 1) / g.sub_bits))};
         nsub += segs[s].nsub;
     }
     if (g.truncated >= nseg_need) g.truncated = -1; // (data of an ignored interval)
@@ -913,6 +916,7 @@ struct JpegState {
     } sets[2];
     int        next = 0;
     bool       gpu_huff = true; // false: every file through the host entropy decoder
+    int        huff_lanes = kHuffLanes; // jpeg_huff workgroup size (AEON_HIP_JPEG_HUFF_LANES=256: A/B)
     std::mutex mu;
 };
 
@@ -940,6 +944,7 @@ JpegState* jpeg_state_create(thread_pool* shared, bool gpu_huff)
 {
     auto* s = new JpegState();
     s->gpu_huff = gpu_huff;
+    if (const char* e = std::getenv("AEON_HIP_JPEG_HUFF_LANES")) s->huff_lanes = std::atoi(e) == 256 ? 256 : kHuffLanes;
     if (shared) {
         s->pool = shared;
     } else {
@@ -988,7 +993,7 @@ void jpeg_decode_batch(JpegState* S, int n, const void* const* data, const size_
             const aeon_img_desc& d = descs[i];
             if (d.channels != 1 && d.channels != 3) bad("decoded channels must be 1 or 3");
             const uint8_t* b = (const uint8_t*)data[i];
-            if (S->gpu_huff && prepare_gpu(b, sizes[i], frames[i], S->arenas[w], gs[i])) {
+            if (S->gpu_huff && prepare_gpu(b, sizes[i], frames[i], S->arenas[w], gs[i], S->huff_lanes)) {
                 on_gpu[i] = 1;
             } else {
                 frames[i] = Frame();
@@ -1107,7 +1112,7 @@ void jpeg_decode_batch(JpegState* S, int n, const void* const* data, const size_
         }
         H.blk_tab[0] = g.blk_tab[0], H.blk_tab[1] = g.blk_tab[1];
         H.nseg = g.nseg, H.nsub = g.nsub, H.restart = g.restart, H.n_mcu = g.n_mcu;
-        H.bpm = g.bpm, H.mcux = g.mcux, H.ncomp = f.ncomp, H.truncated = g.truncated;
+        H.bpm = g.bpm, H.mcux = g.mcux, H.ncomp = f.ncomp, H.truncated = g.truncated, H.sub_bits = g.sub_bits;
     }
     if (!chunks.empty()) std::memcpy(st.pinned + chk_off, chunks.data(), chunks.size() * sizeof(JpegChunk));
     if (!rows.empty()) std::memcpy(st.pinned + row_off, rows.data(), rows.size() * sizeof(JpegRows));
@@ -1117,7 +1122,9 @@ void jpeg_decode_batch(JpegState* S, int n, const void* const* data, const size_
     hip_ok(hipMemcpyAsync(st.dev, st.pinned, total, hipMemcpyHostToDevice, stream), "hipMemcpyAsync");
     if (n_gpu) hip_ok(hipMemsetAsync(st.work, 0, rec_bytes, stream), "hipMemsetAsync");
     if (start) hip_ok(hipEventRecord(start, stream), "hipEventRecord");
-    if (n_gpu) hip_ok(launch_jpeg_huff((const JpegHuffFile*)(st.dev + huf_off), n_gpu, error, stream), "JPEG Huffman kernel");
+    if (n_gpu)
+        hip_ok(launch_jpeg_huff((const JpegHuffFile*)(st.dev + huf_off), n_gpu, S->huff_lanes, error, stream),
+               "JPEG Huffman kernel");
     hip_ok(launch_jpeg((const JpegImage*)st.dev, (const JpegChunk*)(st.dev + chk_off), (int)chunks.size(),
                        (const JpegRows*)(st.dev + row_off), (int)rows.size(), color_lds, stream),
            "JPEG kernels");
@@ -1164,18 +1171,35 @@ void jpeg_entropy_only(const void* data, size_t size, int* w, int* h, int* ncomp
     *w = f.W, *h = f.H, *ncomp = f.ncomp, *n_blocks = nb, *n_values = nv, *hash = hv;
 }
 
+// aeon_jpeg_host_stage's body: the batch decode's host work for one file on this thread -- headers
+// and the unstuffed entropy-coded bytes for the GPU decoder, or the host entropy decoder's sparse
+// stream -- and the bytes it stages for the H2D.
+void jpeg_host_stage(const void* data, size_t size, int* gpu_entropy, int64_t* staged_bytes)
+{
+    Frame   f;
+    Arena   a;
+    GpuScan g;
+    *gpu_entropy = prepare_gpu((const uint8_t*)data, size, f, a, g, kHuffLanes) ? 1 : 0;
+    if (!*gpu_entropy) {
+        size_t blk_off[3] = {0, 0, 0}, val_off = 0;
+        f = Frame(), a.used = 0;
+        decode_file((const uint8_t*)data, size, f, a, blk_off, &val_off, false);
+    }
+    *staged_bytes = (int64_t)a.used;
+}
+
 // The GPU entropy decoder's algorithm on this thread (host-only, for tests): prepare_gpu, then
 // jpeg_huff's phases (jpeg_huff.hpp) one subsequence after another, the exclusive prefix serially --
 // summarised as jpeg_entropy_only summarises the host decoder, so the two can be compared.  Returns 0
 // when the file goes to the host decoder instead, 1 when decoded, -1 on corrupt entropy-coded data;
 // *rounds: the Jacobi rounds until every start settled.
-int jpeg_gpu_entropy_emulate(const void* data, size_t size, int* w, int* h, int* ncomp, int64_t* n_blocks,
+int jpeg_gpu_entropy_emulate(const void* data, size_t size, int lanes, int* w, int* h, int* ncomp, int64_t* n_blocks,
                              int64_t* n_values, uint64_t* hash, int* rounds)
 {
     Frame   f;
     Arena   a;
     GpuScan g;
-    if (!prepare_gpu((const uint8_t*)data, size, f, a, g)) return 0;
+    if (!prepare_gpu((const uint8_t*)data, size, f, a, g, lanes)) return 0;
     std::vector<JpegBlock>   recs[3];
     std::vector<int16_t>     coef[3];
     std::vector<JpegHuffSub> subs(g.nsub);
@@ -1193,7 +1217,7 @@ int jpeg_gpu_entropy_emulate(const void* data, size_t size, int* w, int* h, int*
     }
     F.blk_tab[0] = g.blk_tab[0], F.blk_tab[1] = g.blk_tab[1];
     F.nseg = g.nseg, F.nsub = g.nsub, F.restart = g.restart, F.n_mcu = g.n_mcu;
-    F.bpm = g.bpm, F.mcux = g.mcux, F.ncomp = f.ncomp, F.truncated = g.truncated;
+    F.bpm = g.bpm, F.mcux = g.mcux, F.ncomp = f.ncomp, F.truncated = g.truncated, F.sub_bits = g.sub_bits;
     std::unique_ptr<huff::Tables> T(new huff::Tables());
     huff::tables_codes(*T, F, 0, 1);
     huff::tables_fast(*T, F, 0, 1);

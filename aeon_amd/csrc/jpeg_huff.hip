@@ -3,7 +3,7 @@
 // for the files jpeg_host.cpp hands over whole: one scan carrying every component, its entropy-coded
 // bytes unstuffed and split at RSTn markers into segments (restart intervals) by the host.
 //
-// One workgroup per file.  A segment's bits are cut into subsequences of kHuffSubBits; the decoder
+// One workgroup per file.  A segment's bits are cut into subsequences of F.sub_bits; the decoder
 // state at a codeword boundary is (bit position, block within the MCU c, zigzag index k), and the
 // state at a subsequence's end is a function of the state at its start.  So:
 //   1. every subsequence is decoded from a guessed start (its first bit, c = 0, k = 0; the segment's
@@ -29,11 +29,12 @@ namespace aeon_hip {
 namespace {
 
 struct Scan {
-    int4 wsum[kHuffLanes / 64];
+    int4 wsum[1024 / 64];
     int4 carry;
 };
 
-// Inclusive scan of v over the workgroup's lanes, plus the running carry of earlier chunks.
+// Inclusive scan of v over the workgroup's LANES lanes, plus the running carry of earlier chunks.
+template <int LANES>
 __device__ int4 wg_scan(Scan& X, int4 v)
 {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -48,13 +49,14 @@ __device__ int4 wg_scan(Scan& X, int4 v)
     for (int i = 0; i < wave; i++) off.x += X.wsum[i].x, off.y += X.wsum[i].y, off.z += X.wsum[i].z, off.w += X.wsum[i].w;
     v.x += off.x, v.y += off.y, v.z += off.z, v.w += off.w;
     __syncthreads();
-    if (threadIdx.x == kHuffLanes - 1) X.carry = v;
+    if (threadIdx.x == LANES - 1) X.carry = v;
     return v;
 }
 
 } // namespace
 
-__global__ __launch_bounds__(kHuffLanes) void jpeg_huff(const JpegHuffFile* __restrict__ files, int32_t* __restrict__ error)
+template <int LANES>
+__global__ __launch_bounds__(LANES) void jpeg_huff(const JpegHuffFile* __restrict__ files, int32_t* __restrict__ error)
 {
     __shared__ huff::Tables T;
     __shared__ Scan         X;
@@ -62,34 +64,36 @@ __global__ __launch_bounds__(kHuffLanes) void jpeg_huff(const JpegHuffFile* __re
     JpegHuffSub*            subs = (JpegHuffSub*)F.subs;
     const int               tid = threadIdx.x, nsub = F.nsub;
 
-    huff::tables_codes(T, F, tid, kHuffLanes);
+    huff::tables_codes(T, F, tid, LANES);
     if (tid == 0) X.carry = make_int4(0, 0, 0, 0);
     __syncthreads();
-    huff::tables_fast(T, F, tid, kHuffLanes);
+    huff::tables_fast(T, F, tid, LANES);
     __syncthreads();
     // 1. guessed starts; 2. Jacobi rounds until every start is its predecessor's end
-    huff::pass_guess(T, F, tid, kHuffLanes);
+    huff::pass_guess(T, F, tid, LANES);
     for (;;) {
         __syncthreads();
-        const int any = huff::pass_compare(F, tid, kHuffLanes);
+        const int any = huff::pass_compare(F, tid, LANES);
         if (!__syncthreads_or(any)) break;
-        huff::pass_rewalk(T, F, tid, kHuffLanes);
+        huff::pass_rewalk(T, F, tid, LANES);
     }
     // 3. exclusive prefix of (blocks, DC differences) over the file's subsequences
-    for (int base = 0; base < nsub; base += kHuffLanes) {
+    for (int base = 0; base < nsub; base += LANES) {
         const int  j = base + tid;
         const int4 v = j < nsub ? *(const int4*)subs[j].cnt : make_int4(0, 0, 0, 0);
-        const int4 s = wg_scan(X, v);
+        const int4 s = wg_scan<LANES>(X, v);
         if (j < nsub) *(int4*)subs[j].ex = make_int4(s.x - v.x, s.y - v.y, s.z - v.z, s.w - v.w);
         __syncthreads();
     }
     // 4. the final decode: coefficients and masks
-    if (!huff::pass_write(T, F, tid, kHuffLanes)) atomicOr(error, kJpegCorruptBit);
+    if (!huff::pass_write(T, F, tid, LANES)) atomicOr(error, kJpegCorruptBit);
 }
 
-hipError_t launch_jpeg_huff(const JpegHuffFile* files, int n_files, int32_t* error, hipStream_t stream)
+hipError_t launch_jpeg_huff(const JpegHuffFile* files, int n_files, int lanes, int32_t* error, hipStream_t stream)
 {
-    if (n_files > 0) hipLaunchKernelGGL(jpeg_huff, dim3(n_files), dim3(kHuffLanes), 0, stream, files, error);
+    if (n_files <= 0) return hipSuccess;
+    if (lanes == 256) hipLaunchKernelGGL(jpeg_huff<256>, dim3(n_files), dim3(256), 0, stream, files, error);
+    else hipLaunchKernelGGL(jpeg_huff<1024>, dim3(n_files), dim3(1024), 0, stream, files, error);
     return hipGetLastError();
 }
 

@@ -286,13 +286,13 @@ HUFF_FN void pass_guess(const Tables& T, const JpegHuffFile& F, int j0, int dj)
     Out                none{};
     for (int j = j0; j < F.nsub; j += dj) {
         const JpegHuffSeg S   = segs[sseg[j]];
-        const int         i   = j - S.first_sub, p = (int)S.start_bit + i * kHuffSubBits;
+        const int         i   = j - S.first_sub, p = (int)S.start_bit + i * F.sub_bits;
         int4              cnt = make_int4(0, 0, 0, 0);
         uint64_t          en  = 0;
         if (i + 1 < S.nsub) { // (the segment's last subsequence ends nobody's start)
             Bits b = bits_at(F, S, p);
             int  c = 0, k = 0;
-            walk<false>(T, F, b, c, k, p + kHuffSubBits, false, cnt, none);
+            walk<false>(T, F, b, c, k, p + F.sub_bits, false, cnt, none);
             en = pack_state(b.p, c, k);
         }
         subs[j].st          = pack_state(p, 0, 0);
@@ -332,7 +332,7 @@ HUFF_FN void pass_rewalk(const Tables& T, const JpegHuffFile& F, int j0, int dj)
         if (!subs[j].ex[0]) continue;
         const JpegHuffSeg S  = segs[sseg[j]];
         const uint64_t    st = subs[j].st;
-        const int         p = (int)(uint32_t)st, stop = (int)S.start_bit + (j - S.first_sub + 1) * kHuffSubBits;
+        const int         p = (int)(uint32_t)st, stop = (int)S.start_bit + (j - S.first_sub + 1) * F.sub_bits;
         int               c = (int)(st >> 32) & 0xff, k = (int)(st >> 40) & 0xff;
         int4              cnt = make_int4(0, 0, 0, 0);
         Bits              b   = bits_at(F, S, p);
@@ -368,7 +368,7 @@ HUFF_FN bool pass_write(const Tables& T, const JpegHuffFile& F, int j0, int dj)
         o.mx = mcu % F.mcux, o.my = mcu / F.mcux;
         int4 cnt;
         Bits b = bits_at(F, S, (int)(uint32_t)st);
-        if (!walk<true>(T, F, b, c, k, (int)S.start_bit + (i + 1) * kHuffSubBits, i + 1 == S.nsub, cnt, o)) ok = false;
+        if (!walk<true>(T, F, b, c, k, (int)S.start_bit + (i + 1) * F.sub_bits, i + 1 == S.nsub, cnt, o)) ok = false;
     }
     return ok;
 }

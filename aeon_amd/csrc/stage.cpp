@@ -49,6 +49,7 @@ void       jpeg_decode_batch(JpegState* S, int n, const void* const* data, const
 void       jpeg_info(const void* data, size_t size, int* w, int* h, int* ncomp);
 void       jpeg_entropy_only(const void* data, size_t size, int* w, int* h, int* ncomp, int64_t* n_blocks,
                              int64_t* n_values, uint64_t* hash);
+void       jpeg_host_stage(const void* data, size_t size, int* gpu_entropy, int64_t* staged_bytes);
 void       png_header(const void* data, size_t size, int* w, int* h, int* depth, int* ctype);
 void       png_decode(const void* data, size_t size, int mode, void* dst, size_t stride, int* out_elem_bytes);
 } // namespace aeon_hip
@@ -1814,6 +1815,15 @@ int aeon_jpeg_entropy_decode(const void* data, size_t size, int* width, int* hei
         if (!data || !width || !height || !components || !n_blocks || !n_values || !hash)
             fail(AEON_HIP_EINVAL, "null argument");
         jpeg_entropy_only(data, size, width, height, components, n_blocks, n_values, hash);
+        return 0;
+    });
+}
+
+int aeon_jpeg_host_stage(const void* data, size_t size, int* gpu_entropy, int64_t* staged_bytes)
+{
+    return guarded([&] {
+        if (!data || !gpu_entropy || !staged_bytes) fail(AEON_HIP_EINVAL, "null argument");
+        jpeg_host_stage(data, size, gpu_entropy, staged_bytes);
         return 0;
     });
 }

@@ -157,13 +157,21 @@ int aeon_jpeg_info(const void* data, size_t size, int* width, int* height, int* 
  * decode. */
 int aeon_jpeg_entropy_decode(const void* data, size_t size, int* width, int* height, int* components,
                              int64_t* n_blocks, int64_t* n_values, uint64_t* hash);
+/* The host work aeon_hip_decode_jpeg_batch does for one file, on the calling thread, no device: a
+ * sequential file with one scan of every component gets its headers parsed and its entropy-coded
+ * bytes unstuffed for the GPU Huffman decoder (*gpu_entropy = 1); any other (progressive,
+ * multi-scan) is entropy-decoded into the sparse stream (*gpu_entropy = 0).  *staged_bytes: what it
+ * stages for the H2D.  For timing the host side of the stage per file. */
+int aeon_jpeg_host_stage(const void* data, size_t size, int* gpu_entropy, int64_t* staged_bytes);
 /* cv::imdecode(CV_LOAD_IMAGE_COLOR / GRAYSCALE) of n JPEG files (baseline / extended sequential /
  * progressive Huffman, 8-bit, 1 or 3 components) as libjpeg decodes them (ISLOW IDCT, fancy upsampling),
  * into device memory: record i as HWC uint8 (BGR if descs[i].channels == 3, the Y component if 1)
  * at dst_base + descs[i].offset with descs[i].stride bytes per row; descs[i].width/height must be
- * the file's (aeon_jpeg_info).  Huffman decoding runs on the context's host pool; the sparse
- * coefficients go up in one H2D and the IDCT / upsampling / colour conversion run as kernels on
- * `stream`.  The files may be released when the call returns; dst must stay valid until the stream
+ * the file's (aeon_jpeg_info).  Headers are parsed on the context's host pool; sequential files with
+ * one scan of every component are Huffman-decoded on the GPU (their unstuffed entropy-coded bytes go
+ * up), the others on the pool (their sparse coefficients go up), all in one H2D; the Huffman, IDCT /
+ * upsampling / colour conversion kernels run on `stream`.  Corrupt entropy-coded data of a
+ * GPU-decoded file is reported by aeon_hip_synchronize (AEON_HIP_EDEVICE).  The files may be released when the call returns; dst must stay valid until the stream
  * reaches the work.  Arithmetic-coded / lossless / 12-bit / CMYK files: AEON_HIP_EUNSUPPORTED. */
 int aeon_hip_decode_jpeg_batch(aeon_hip_ctx* ctx, int n, const void* const* data, const size_t* sizes,
                                const aeon_img_desc* descs, void* dst_base, void* stream);
