@@ -1221,13 +1221,13 @@ int jpeg_gpu_entropy_emulate(const void* data, size_t size, int lanes, int* w, i
     std::unique_ptr<huff::Tables> T(new huff::Tables());
     huff::tables_codes(*T, F, 0, 1);
     huff::tables_fast(*T, F, 0, 1);
-    huff::pass_guess(*T, F, 0, 1);
+    huff::pass_guess(*T, F, subs.data(), 0, 1);
     int r = 0;
-    while (huff::pass_compare(F, 0, 1)) huff::pass_rewalk(*T, F, 0, 1), r++;
+    while (huff::pass_compare(F, subs.data(), 0, 1)) huff::pass_rewalk(*T, F, subs.data(), 0, 1), r++;
     int32_t acc[4] = {0, 0, 0, 0};
     for (auto& s : subs)
         for (int i = 0; i < 4; i++) s.ex[i] = acc[i], acc[i] += s.cnt[i];
-    if (!huff::pass_write(*T, F, 0, 1)) return -1;
+    if (!huff::pass_write(*T, F, subs.data(), 0, 1)) return -1;
     uint64_t hv  = 1469598103934665603ull;
     auto     mix = [&](uint64_t x) {
         for (int b = 0; b < 8; b++) hv = (hv ^ ((x >> (8 * b)) & 0xff)) * 1099511628211ull;

@@ -19,7 +19,8 @@
 // Decoding tables live in LDS: a kHuffFastBits lookahead per table whose entries carry the code
 // length, the AC run and, when the value bits fit the lookahead too, the decoded value; longer codes
 // take the canonical maxcode walk.  The bit reader holds 64 bits and one word loaded ahead, so the
-// next refill's global load is in flight while the current bits decode.  The per-lane logic is in
+// next refill's global load is in flight while the current bits decode.  A file with at most one
+// subsequence per lane keeps the subsequence states in LDS.  The per-lane logic is in
 // jpeg_huff.hpp (shared with the host emulation the CPU tests run).
 #include <hip/hip_runtime.h>
 
@@ -55,14 +56,17 @@ __device__ int4 wg_scan(Scan& X, int4 v)
 
 } // namespace
 
+// Dynamic LDS: the subsequence states of a file with at most LANES of them (one per lane), so the
+// Jacobi rounds and the prefix read and write LDS; larger files keep them in F.subs.
 template <int LANES>
 __global__ __launch_bounds__(LANES) void jpeg_huff(const JpegHuffFile* __restrict__ files, int32_t* __restrict__ error)
 {
     __shared__ huff::Tables T;
     __shared__ Scan         X;
+    extern __shared__ JpegHuffSub lsubs[];
     const JpegHuffFile&     F    = files[blockIdx.x];
-    JpegHuffSub*            subs = (JpegHuffSub*)F.subs;
     const int               tid = threadIdx.x, nsub = F.nsub;
+    JpegHuffSub*            subs = nsub <= LANES ? lsubs : (JpegHuffSub*)F.subs;
 
     huff::tables_codes(T, F, tid, LANES);
     if (tid == 0) X.carry = make_int4(0, 0, 0, 0);
@@ -70,12 +74,12 @@ __global__ __launch_bounds__(LANES) void jpeg_huff(const JpegHuffFile* __restric
     huff::tables_fast(T, F, tid, LANES);
     __syncthreads();
     // 1. guessed starts; 2. Jacobi rounds until every start is its predecessor's end
-    huff::pass_guess(T, F, tid, LANES);
+    huff::pass_guess(T, F, subs, tid, LANES);
     for (;;) {
         __syncthreads();
-        const int any = huff::pass_compare(F, tid, LANES);
+        const int any = huff::pass_compare(F, subs, tid, LANES);
         if (!__syncthreads_or(any)) break;
-        huff::pass_rewalk(T, F, tid, LANES);
+        huff::pass_rewalk(T, F, subs, tid, LANES);
     }
     // 3. exclusive prefix of (blocks, DC differences) over the file's subsequences
     for (int base = 0; base < nsub; base += LANES) {
@@ -86,14 +90,21 @@ __global__ __launch_bounds__(LANES) void jpeg_huff(const JpegHuffFile* __restric
         __syncthreads();
     }
     // 4. the final decode: coefficients and masks
-    if (!huff::pass_write(T, F, tid, LANES)) atomicOr(error, kJpegCorruptBit);
+    if (!huff::pass_write(T, F, subs, tid, LANES)) atomicOr(error, kJpegCorruptBit);
 }
 
 hipError_t launch_jpeg_huff(const JpegHuffFile* files, int n_files, int lanes, int32_t* error, hipStream_t stream)
 {
     if (n_files <= 0) return hipSuccess;
-    if (lanes == 256) hipLaunchKernelGGL(jpeg_huff<256>, dim3(n_files), dim3(256), 0, stream, files, error);
-    else hipLaunchKernelGGL(jpeg_huff<1024>, dim3(n_files), dim3(1024), 0, stream, files, error);
+    const size_t lds = (size_t)lanes * sizeof(JpegHuffSub);
+    if (lanes == 256) {
+        hipLaunchKernelGGL(jpeg_huff<256>, dim3(n_files), dim3(256), lds, stream, files, error);
+    } else {
+        static const hipError_t attr = hipFuncSetAttribute((const void*)jpeg_huff<1024>,
+                                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (attr != hipSuccess) return attr;
+        hipLaunchKernelGGL(jpeg_huff<1024>, dim3(n_files), dim3(1024), lds, stream, files, error);
+    }
     return hipGetLastError();
 }
 

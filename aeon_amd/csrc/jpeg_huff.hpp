@@ -1,7 +1,7 @@
 // jpeg_huff.hpp -- the GPU Huffman decoder's per-lane logic (jpeg_huff.hip), written once for the
 // device and for the host: jpeg_huff runs its phases on a workgroup's lanes with barriers between
-// them; tests/sanitize/huff_emu.cpp runs the same phases one subsequence after another to check them
-// against the host entropy decoder on CPU.  See jpeg_huff.hip for the algorithm.
+// them; jpeg_host.cpp's jpeg_gpu_entropy_emulate runs the same phases one subsequence after another
+// (tests/sanitize/fuzz_driver.cpp compares it with the host entropy decoder on CPU).  See jpeg_huff.hip for the algorithm.
 #pragma once
 #include "jpeg.hpp"
 
@@ -277,12 +277,13 @@ HUFF_FN bool walk(const Tables& T, const JpegHuffFile& F, Bits& b, int& c, int& 
     return true;
 }
 
+// The phases below take the file's subsequence states `subs` (F.subs in device memory, or an LDS
+// copy when the file's subsequences fit the workgroup).
 // Phase 1: subsequences j0, j0 + dj, ... from their guessed starts.
-HUFF_FN void pass_guess(const Tables& T, const JpegHuffFile& F, int j0, int dj)
+HUFF_FN void pass_guess(const Tables& T, const JpegHuffFile& F, JpegHuffSub* subs, int j0, int dj)
 {
     const JpegHuffSeg* segs = (const JpegHuffSeg*)F.segs;
     const int32_t*     sseg = (const int32_t*)F.sub_seg;
-    JpegHuffSub*       subs = (JpegHuffSub*)F.subs;
     Out                none{};
     for (int j = j0; j < F.nsub; j += dj) {
         const JpegHuffSeg S   = segs[sseg[j]];
@@ -303,11 +304,10 @@ HUFF_FN void pass_guess(const Tables& T, const JpegHuffFile& F, int j0, int dj)
 
 // Phase 2a: a start that differs from its predecessor's end takes it (ex[0]: walk again).  Returns
 // whether any start changed.
-HUFF_FN int pass_compare(const JpegHuffFile& F, int j0, int dj)
+HUFF_FN int pass_compare(const JpegHuffFile& F, JpegHuffSub* subs, int j0, int dj)
 {
     const JpegHuffSeg* segs = (const JpegHuffSeg*)F.segs;
     const int32_t*     sseg = (const int32_t*)F.sub_seg;
-    JpegHuffSub*       subs = (JpegHuffSub*)F.subs;
     int                any  = 0;
     for (int j = j0; j < F.nsub; j += dj) {
         const JpegHuffSeg S = segs[sseg[j]];
@@ -322,11 +322,10 @@ HUFF_FN int pass_compare(const JpegHuffFile& F, int j0, int dj)
 }
 
 // Phase 2b: walk the changed subsequences again from their new starts.
-HUFF_FN void pass_rewalk(const Tables& T, const JpegHuffFile& F, int j0, int dj)
+HUFF_FN void pass_rewalk(const Tables& T, const JpegHuffFile& F, JpegHuffSub* subs, int j0, int dj)
 {
     const JpegHuffSeg* segs = (const JpegHuffSeg*)F.segs;
     const int32_t*     sseg = (const int32_t*)F.sub_seg;
-    JpegHuffSub*       subs = (JpegHuffSub*)F.subs;
     Out                none{};
     for (int j = j0; j < F.nsub; j += dj) {
         if (!subs[j].ex[0]) continue;
@@ -344,11 +343,10 @@ HUFF_FN void pass_rewalk(const Tables& T, const JpegHuffFile& F, int j0, int dj)
 
 // Phase 4 (after the exclusive prefix of cnt into ex): the final decode.  Returns false if any of
 // the walks met corrupt data.
-HUFF_FN bool pass_write(const Tables& T, const JpegHuffFile& F, int j0, int dj)
+HUFF_FN bool pass_write(const Tables& T, const JpegHuffFile& F, const JpegHuffSub* subs, int j0, int dj)
 {
     const JpegHuffSeg* segs = (const JpegHuffSeg*)F.segs;
     const int32_t*     sseg = (const int32_t*)F.sub_seg;
-    JpegHuffSub*       subs = (JpegHuffSub*)F.subs;
     const int          per_seg = F.restart * F.bpm, total = F.n_mcu * F.bpm;
     bool               ok = true;
     for (int j = j0; j < F.nsub; j += dj) {
