@@ -487,6 +487,15 @@ def cpu_baseline(A, C, budget_s, cfg="C2"):
                       "scalar C++, a lower bound on aeon's OpenCV-SIMD path"}
 
 
+def side(extra, key, fn):
+    """One side run of the bench line (rank 0's extras): a failure is recorded in the line under its
+    key instead of losing the line."""
+    try:
+        extra[key] = fn()
+    except Exception as e:  # noqa: BLE001 -- any failure of a side run
+        extra[key] = {"error": f"{type(e).__name__}: {e}"}
+
+
 def jpeg_files(batch):
     """Encoded records of a decode window: aeon's own JPEG fixtures (test/test_data/img_2112_70.jpg
     480x360 and flowers.jpg 600x800, 4:2:0 baseline; committed in tests/golden), cycled."""
@@ -740,53 +749,63 @@ def main():
         if args.config == "C2":
             # rate untimed (an event pair between a step's launches costs ~10 us of GPU time there),
             # the kernel durations from a second run timing every launch
-            st3 = max(30, args.steps)
-            e3, _, _, _ = run_device(A, C, torch, "C3", 1024, st3, 3, 0, 1, args.pool_mib, None, 0)
-            _, kt3, _, _ = run_device(A, C, torch, "C3", 1024, 6, 2, 0, 1, args.pool_mib, None, 1)
-            m3, b3, n3 = kt3["augment"]
-            s3 = kt3["stats"]
-            extra["C3"] = {"value": 1024 * st3 / e3, "unit": "images/s", "batch": 1024,
-                           "ms_per_step": e3 / st3 * 1e3,
-                           "augment_kernel_avg_launch_ms": m3 / max(n3, 1),
-                           "stats_kernel_avg_launch_ms": s3[0] / max(s3[2], 1),
-                           "augment_kernel_gbs": b3 / (m3 * 1e-3) / 1e9 if m3 else 0}
+            def c3():
+                st3 = max(30, args.steps)
+                e3, _, _, _ = run_device(A, C, torch, "C3", 1024, st3, 3, 0, 1, args.pool_mib, None, 0)
+                _, kt3, _, _ = run_device(A, C, torch, "C3", 1024, 6, 2, 0, 1, args.pool_mib, None, 1)
+                m3, b3, n3 = kt3["augment"]
+                s3 = kt3["stats"]
+                return {"value": 1024 * st3 / e3, "unit": "images/s", "batch": 1024,
+                        "ms_per_step": e3 / st3 * 1e3,
+                        "augment_kernel_avg_launch_ms": m3 / max(n3, 1),
+                        "stats_kernel_avg_launch_ms": s3[0] / max(s3[2], 1),
+                        "augment_kernel_gbs": b3 / (m3 * 1e-3) / 1e9 if m3 else 0}
+            side(extra, "C3", c3)
         if args.streams == 1:
             # the same C2 steps alternating over two caller streams (one per output container,
             # as aeon's double-buffered async_manager holds two batches): the next batch's launch
             # is dispatched while the current one drains, hiding the ~6 us dispatch gap
-            e2, _, _, _ = run_device(A, C, torch, args.config, batch, args.steps, args.warmup, 0, 1,
-                                     args.pool_mib, None, 0, 2)
-            extra["two_streams"] = {"value": batch * args.steps / e2, "unit": "images/s",
-                                    "ms_per_step": e2 / args.steps * 1e3,
-                                    "what": "same workload, consecutive batches on two streams"}
-        extra["C5"] = run_c5(A, C, torch, max(20, args.steps), 3, args.pool_mib)
+            def two_streams():
+                e2, _, _, _ = run_device(A, C, torch, args.config, batch, args.steps, args.warmup, 0, 1,
+                                         args.pool_mib, None, 0, 2)
+                return {"value": batch * args.steps / e2, "unit": "images/s", "ms_per_step": e2 / args.steps * 1e3,
+                        "what": "same workload, consecutive batches on two streams"}
+            side(extra, "two_streams", two_streams)
+        side(extra, "C5", lambda: run_c5(A, C, torch, max(20, args.steps), 3, args.pool_mib))
+
         # aeon's other interpolation methods on the C2 workload: a generic resize pre-pass
         # (OpenCV 2.4's resizeGeneric_ / resizeArea_) into scratch, then the tile kernel's copy pass
-        extra["interpolation"] = {}
-        for m in ("CUBIC", "AREA", "LANCZOS4"):
-            em, ktm, _, _ = run_device(A, C, torch, "C2:" + m, batch, 20, 3, 0, 1, args.pool_mib, None, 1)
-            extra["interpolation"][m] = {"value": batch * 20 / em, "unit": "images/s", "ms_per_step": em / 20 * 1e3,
-                                         "kernels_us_per_step": {k: v[0] / 20 * 1e3 for k, v in ktm.items() if v[2]}}
-        extra["interpolation"]["what"] = ("C2 workload (batch 256) with interpolation_method set; every launch timed "
-                                          "(events idle the queue between launches: rates are lower bounds)")
-        extra["e2e_host_to_host"] = {"value": run_e2e(A, C, torch, 256, 20), "unit": "images/s",
-                                     "what": "pinned H2D of decoded 256x256 u8 + kernel + D2H of fp32 CHW"}
-        extra["e2e_zero_copy"] = {"value": run_e2e(A, C, torch, 256, 20, zero_copy=True), "unit": "images/s",
-                                  "what": "pinned H2D of decoded 256x256 u8 + kernel storing fp32 CHW straight "
-                                          "into the pinned host batch (zero-copy over PCIe, no D2H)"}
-        extra["C1"] = {"decoder": run_c1_decoder(A, C, torch)}
-        extra["e2e_jpeg_decoder"] = {
+        def interpolation():
+            out = {}
+            for m in ("CUBIC", "AREA", "LANCZOS4"):
+                em, ktm, _, _ = run_device(A, C, torch, "C2:" + m, batch, 20, 3, 0, 1, args.pool_mib, None, 1)
+                out[m] = {"value": batch * 20 / em, "unit": "images/s", "ms_per_step": em / 20 * 1e3,
+                          "kernels_us_per_step": {k: v[0] / 20 * 1e3 for k, v in ktm.items() if v[2]}}
+            out["what"] = ("C2 workload (batch 256) with interpolation_method set; every launch timed "
+                           "(events idle the queue between launches: rates are lower bounds)")
+            return out
+        side(extra, "interpolation", interpolation)
+        side(extra, "e2e_host_to_host", lambda: {
+            "value": run_e2e(A, C, torch, 256, 20), "unit": "images/s",
+            "what": "pinned H2D of decoded 256x256 u8 + kernel + D2H of fp32 CHW"})
+        side(extra, "e2e_zero_copy", lambda: {
+            "value": run_e2e(A, C, torch, 256, 20, zero_copy=True), "unit": "images/s",
+            "what": "pinned H2D of decoded 256x256 u8 + kernel storing fp32 CHW straight into the pinned host "
+                    "batch (zero-copy over PCIe, no D2H)"})
+        side(extra, "C1", lambda: {"decoder": run_c1_decoder(A, C, torch)})
+        side(extra, "e2e_jpeg_decoder", lambda: {
             "host_outputs": {"value": run_e2e_jpeg(A, C, torch, on_device=False), "unit": "images/s"},
             "device_outputs": {"value": run_e2e_jpeg(A, C, torch, on_device=True), "unit": "images/s"},
             "jpeg_stage": run_jpeg_stage(A, torch),
             "what": "encoded JPEG records (aeon's img_2112_70.jpg / flowers.jpg) -> aeon_decoder submit/wait "
-                    "(two windows in flight): extract on the JPEG stage + C2 augmentation, 256-record windows"}
+                    "(two windows in flight): extract on the JPEG stage + C2 augmentation, 256-record windows"})
         if not args.no_cpu_baseline:
-            extra["e2e_jpeg_decoder"]["cpu_baseline"] = cpu_baseline_jpeg(A, C, args.cpu_extra_seconds)
-        if not args.no_cpu_baseline:
-            extra["C1"]["cpu_baseline"] = cpu_baseline(A, C, args.cpu_extra_seconds, "C1")
-            extra["C3"]["cpu_baseline"] = cpu_baseline(A, C, args.cpu_extra_seconds, "C3") if "C3" in extra else None
-            extra["C5"]["cpu_baseline"] = cpu_baseline(A, C, args.cpu_extra_seconds, "C5")
+            for key, fn in (("e2e_jpeg_decoder", lambda: cpu_baseline_jpeg(A, C, args.cpu_extra_seconds)),
+                            ("C1", lambda: cpu_baseline(A, C, args.cpu_extra_seconds, "C1")),
+                            ("C3", lambda: cpu_baseline(A, C, args.cpu_extra_seconds, "C3")),
+                            ("C5", lambda: cpu_baseline(A, C, args.cpu_extra_seconds, "C5"))):
+                if isinstance(extra.get(key), dict) and "error" not in extra[key]:
+                    side(extra[key], "cpu_baseline", fn)
 
     line = {
         "metric": METRIC,
