@@ -6,6 +6,8 @@
 // jpeg_idct_islow (LL&M, CONST_BITS 13, PASS1_BITS 2; the post-IDCT range limit of jdmaster.c,
 // x & 1023 wrap) -- integer multiply-adds only -- a column each, then a row each, and each lane
 // writes its output row of the block into the component plane (one 8-byte store).
+// jpeg_bands (round 4) runs both in one workgroup per band of MCU rows, the planes in LDS; jpeg_idct +
+// jpeg_color remain for images whose bands outgrow the LDS.
 // jpeg_color: one lane per 4 output pixels of each of kJpegRowsPerWg rows: each component sampled
 // through jdsample.c's upsampler (h2v1 / h1v2 / h2v2 fancy triangle filters, context rows
 // replicated at the edges as jdmainct.c does; box replication for the other ratios and for
@@ -151,6 +153,16 @@ struct CompView {
     int            lo, pw, dw, dh, up, hf, vf;
 };
 
+// The plane rows [lo, hi] of component k that output rows [y0, y1]'s upsampling reads (jdsample.c's
+// context rows for the triangle filters, clamped at the image edges).
+__device__ __forceinline__ void comp_rows(const JpegImage& I, int k, int y0, int y1, CompView& c, int& hi)
+{
+    c.pw = I.bw[k] * 8, c.dw = I.dw[k], c.dh = I.dh[k], c.up = I.up[k], c.hf = I.hf[k], c.vf = I.vf[k];
+    if (c.up == UP_H1V2 || c.up == UP_H2V2) c.lo = max((y0 >> 1) - 1, 0), hi = min((y1 >> 1) + 1, c.dh - 1);
+    else if (c.up == UP_BOX) c.lo = y0 / c.vf, hi = y1 / c.vf;
+    else c.lo = y0, hi = y1;
+}
+
 // Sample (x, y) of the image from a component's plane through libjpeg's upsampler.
 __device__ __forceinline__ int upsampled(const CompView& c, int x, int y)
 {
@@ -180,42 +192,17 @@ __device__ __forceinline__ int upsampled(const CompView& c, int x, int y)
     }
 }
 
-// A workgroup per band of output rows: the plane rows the band's upsampling reads are copied into
-// LDS with coalesced 8-byte loads (jpeg_stage_rows bounds them), then one lane per 4 consecutive
-// pixels of the band: one dword (gray) or three dwords (BGR) when the group is whole and 4-byte
-// aligned, bytewise otherwise.
-__global__ __launch_bounds__(256) void jpeg_color(const JpegImage* __restrict__ imgs, const JpegRows* __restrict__ rows)
+// Output rows [y0, y0 + rows) of image I from its staged component rows cv: one lane per 4 consecutive
+// pixels -- one dword (gray) or three dwords (BGR) when the group is whole and 4-byte aligned,
+// bytewise otherwise.
+__device__ __forceinline__ void color_rows(const JpegImage& I, const CompView* cv, int y0, int nrows)
 {
-    extern __shared__ uint8_t lds_b[];
-    const JpegRows   R  = rows[blockIdx.x];
-    const JpegImage& I  = imgs[R.img];
-    const int        W = I.W, cn = I.out_cn, nc = cn == 1 ? 1 : I.ncomp;
-    const int        y1 = R.y0 + R.rows - 1;
-    CompView         cv[3];
-    int              off = 0;
-#pragma unroll
-    for (int k = 0; k < 3; k++) {
-        if (k >= nc) break;
-        CompView& c = cv[k];
-        c.pw = I.bw[k] * 8, c.dw = I.dw[k], c.dh = I.dh[k], c.up = I.up[k], c.hf = I.hf[k], c.vf = I.vf[k];
-        int hi;
-        if (c.up == UP_H1V2 || c.up == UP_H2V2) c.lo = max((R.y0 >> 1) - 1, 0), hi = min((y1 >> 1) + 1, c.dh - 1);
-        else if (c.up == UP_BOX) c.lo = R.y0 / c.vf, hi = y1 / c.vf;
-        else c.lo = R.y0, hi = y1;
-        c.P = lds_b + off;
-        // stage plane rows [lo, hi]: whole rows of pw bytes (a multiple of 8) are contiguous
-        const uint2* src = (const uint2*)((const uint8_t*)I.planes[k] + (size_t)c.lo * c.pw);
-        uint2*       dst = (uint2*)(lds_b + off);
-        const int    n8  = (hi - c.lo + 1) * c.pw / 8;
-        for (int e = threadIdx.x; e < n8; e += blockDim.x) dst[e] = src[e];
-        off += (hi - c.lo + 1) * c.pw;
-    }
-    __syncthreads();
+    const int W = I.W, cn = I.out_cn, nc = cn == 1 ? 1 : I.ncomp;
     uint8_t*  out    = (uint8_t*)I.out;
     const int stride = I.out_stride;
     const int groups = (W + 3) >> 2;
-    for (int q = threadIdx.x; q < groups * R.rows; q += blockDim.x) {
-        const int y = R.y0 + q / groups, x0 = (q % groups) * 4;
+    for (int q = threadIdx.x; q < groups * nrows; q += blockDim.x) {
+        const int y = y0 + q / groups, x0 = (q % groups) * 4;
         uint32_t  p[4];
 #pragma unroll
         for (int e = 0; e < 4; e++) {
@@ -249,9 +236,131 @@ __global__ __launch_bounds__(256) void jpeg_color(const JpegImage* __restrict__ 
     }
 }
 
-hipError_t launch_jpeg(const JpegImage* imgs, const JpegChunk* chunks, int n_chunks, const JpegRows* rows, int n_rows,
-                       int color_lds, hipStream_t stream)
+// A workgroup per band of output rows: the plane rows the band's upsampling reads are copied into
+// LDS with coalesced 8-byte loads (jpeg_stage_rows bounds them), then color_rows.  (Images too wide
+// for jpeg_bands' LDS.)
+__global__ __launch_bounds__(256) void jpeg_color(const JpegImage* __restrict__ imgs, const JpegRows* __restrict__ rows)
 {
+    extern __shared__ uint8_t lds_b[];
+    const JpegRows   R  = rows[blockIdx.x];
+    const JpegImage& I  = imgs[R.img];
+    const int        nc = I.out_cn == 1 ? 1 : I.ncomp;
+    const int        y1 = R.y0 + R.rows - 1;
+    CompView         cv[3];
+    int              off = 0;
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        if (k >= nc) break;
+        CompView& c = cv[k];
+        int       hi;
+        comp_rows(I, k, R.y0, y1, c, hi);
+        c.P = lds_b + off;
+        // stage plane rows [lo, hi]: whole rows of pw bytes (a multiple of 8) are contiguous
+        const uint2* src = (const uint2*)((const uint8_t*)I.planes[k] + (size_t)c.lo * c.pw);
+        uint2*       dst = (uint2*)(lds_b + off);
+        const int    n8  = (hi - c.lo + 1) * c.pw / 8;
+        for (int e = threadIdx.x; e < n8; e += blockDim.x) dst[e] = src[e];
+        off += (hi - c.lo + 1) * c.pw;
+    }
+    __syncthreads();
+    color_rows(I, cv, R.y0, R.rows);
+}
+
+// The IDCT and the colour pass in one workgroup per band of whole MCU rows: every block of the block
+// rows that hold the band's component rows [lo, hi] (context rows included) goes through
+// jpeg_idct's arithmetic -- eight lanes per block, column pass, transpose through the group's LDS
+// slot, row pass -- and its rows inside [lo, hi] land in the component's LDS plane; then color_rows.
+// The planes never leave the chip (jpeg_idct + jpeg_color write them to HBM and read them back), and
+// the call is one launch.  A context block row above / below the band is transformed whole for the
+// one row the triangle filters read from it.
+__global__ __launch_bounds__(256) void jpeg_bands(const JpegImage* __restrict__ imgs, const JpegRows* __restrict__ rows)
+{
+    extern __shared__ uint8_t lds_b[];
+    __shared__ int   slot[32 * kSlot];
+    const JpegRows   R  = rows[blockIdx.x];
+    const JpegImage& I  = imgs[R.img];
+    const int        nc = I.out_cn == 1 ? 1 : I.ncomp;
+    const int        y1 = R.y0 + R.rows - 1;
+    const int        g = threadIdx.x >> 3, j = threadIdx.x & 7;
+    int*             s = slot + g * kSlot;
+    CompView         cv[3];
+    int              off = 0;
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        if (k >= nc) break;
+        CompView& c = cv[k];
+        int       hi;
+        comp_rows(I, k, R.y0, y1, c, hi);
+        c.P                     = lds_b + off;
+        uint8_t*         plane  = lds_b + off;
+        const int        bw     = I.bw[k], br0 = c.lo >> 3, nblk = ((hi >> 3) - br0 + 1) * bw;
+        const JpegBlock* blocks = (const JpegBlock*)I.blocks[k];
+        const int16_t*   dense  = (const int16_t*)I.dvals[k];
+        const int16_t*   vals   = (const int16_t*)I.values;
+        int              qv[8];
+#pragma unroll
+        for (int r = 0; r < 8; r++) qv[r] = I.q[k][r * 8 + j];
+        for (int b = g; b < nblk; b += 32) {
+            const int       by = br0 + b / bw, bx = b % bw;
+            const size_t    idx = (size_t)by * bw + bx;
+            const JpegBlock B   = blocks[idx];
+            int             col[8], out[8], in[8];
+            if (dense) { // the 8 loads do not wait for the mask
+                const int16_t* bv = dense + idx * 64;
+#pragma unroll
+                for (int r = 0; r < 8; r++) {
+                    const int z = kZzInv[r * 8 + j], v = bv[z];
+                    col[r]      = (B.mask >> z) & 1 ? v * qv[r] : 0;
+                }
+            } else {
+#pragma unroll
+                for (int r = 0; r < 8; r++) {
+                    const int z = kZzInv[r * 8 + j];
+                    col[r]      = (B.mask >> z) & 1
+                                      ? (int)vals[B.val_off + __builtin_popcountll(B.mask & ((1ull << z) - 1))] * qv[r]
+                                      : 0;
+                }
+            }
+            llm8<11, false>(col, out);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier(); // the previous block's pass-2 reads are done
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+            for (int r = 0; r < 8; r++) s[r * 8 + j] = out[r];
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+            for (int cc = 0; cc < 8; cc++) in[cc] = s[j * 8 + cc];
+            llm8<18, true>(in, out);
+            const int y = by * 8 + j; // this lane's output row of the block
+            if (y >= c.lo && y <= hi) {
+                const uint32_t lo32 = idct_limit(out[0]) | idct_limit(out[1]) << 8 | idct_limit(out[2]) << 16 |
+                                      idct_limit(out[3]) << 24;
+                const uint32_t hi32 = idct_limit(out[4]) | idct_limit(out[5]) << 8 | idct_limit(out[6]) << 16 |
+                                      idct_limit(out[7]) << 24;
+                *(uint2*)(plane + (y - c.lo) * c.pw + bx * 8) = make_uint2(lo32, hi32);
+            }
+        }
+        off += (hi - c.lo + 1) * c.pw;
+    }
+    __syncthreads();
+    color_rows(I, cv, R.y0, R.rows);
+}
+
+// bands: jpeg_bands work items (LDS band_lds); chunks + rows: the IDCT / colour items of images too
+// wide for it (LDS color_lds).
+hipError_t launch_jpeg(const JpegImage* imgs, const JpegRows* bands, int n_bands, int band_lds, const JpegChunk* chunks,
+                       int n_chunks, const JpegRows* rows, int n_rows, int color_lds, hipStream_t stream)
+{
+    if (n_bands > 0) {
+        if (band_lds > 64 * 1024 - 32 * kSlot * 4) {
+            const hipError_t e = hipFuncSetAttribute((const void*)jpeg_bands, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                     band_lds);
+            if (e != hipSuccess) return e;
+        }
+        hipLaunchKernelGGL(jpeg_bands, dim3(n_bands), dim3(256), (size_t)band_lds, stream, imgs, bands);
+    }
     if (n_chunks > 0) hipLaunchKernelGGL(jpeg_idct, dim3(n_chunks), dim3(kJpegIdctLanes), 0, stream, imgs, chunks);
     if (n_rows > 0) {
         if (color_lds > 64 * 1024) {
