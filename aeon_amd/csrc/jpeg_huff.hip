@@ -56,23 +56,15 @@ __device__ int4 wg_scan(Scan& X, int4 v)
 
 } // namespace
 
-// Dynamic LDS: the subsequence states of a file with at most LANES of them (one per lane), so the
-// Jacobi rounds and the prefix read and write LDS; larger files keep them in F.subs.
-template <int LANES>
-__global__ __launch_bounds__(LANES) void jpeg_huff(const JpegHuffFile* __restrict__ files, int32_t* __restrict__ error)
-{
-    __shared__ huff::Tables T;
-    __shared__ Scan         X;
-    extern __shared__ JpegHuffSub lsubs[];
-    const JpegHuffFile&     F    = files[blockIdx.x];
-    const int               tid = threadIdx.x, nsub = F.nsub;
-    JpegHuffSub*            subs = nsub <= LANES ? lsubs : (JpegHuffSub*)F.subs;
+typedef __attribute__((address_space(3))) JpegHuffSub lds_sub;
+typedef __attribute__((address_space(1))) JpegHuffSub glb_sub;
 
-    huff::tables_codes(T, F, tid, LANES);
-    if (tid == 0) X.carry = make_int4(0, 0, 0, 0);
-    __syncthreads();
-    huff::tables_fast(T, F, tid, LANES);
-    __syncthreads();
+// The file's phases with its subsequence states behind SP (LDS or device memory).
+template <int LANES, typename SP>
+__device__ __forceinline__ void decode_file(const huff::Tables& T, Scan& X, const JpegHuffFile& F, SP subs,
+                                            int32_t* error)
+{
+    const int tid = threadIdx.x, nsub = F.nsub;
     // 1. guessed starts; 2. Jacobi rounds until every start is its predecessor's end
     huff::pass_guess(T, F, subs, tid, LANES);
     for (;;) {
@@ -84,13 +76,34 @@ __global__ __launch_bounds__(LANES) void jpeg_huff(const JpegHuffFile* __restric
     // 3. exclusive prefix of (blocks, DC differences) over the file's subsequences
     for (int base = 0; base < nsub; base += LANES) {
         const int  j = base + tid;
-        const int4 v = j < nsub ? *(const int4*)subs[j].cnt : make_int4(0, 0, 0, 0);
+        const int4 v = j < nsub ? make_int4(subs[j].cnt[0], subs[j].cnt[1], subs[j].cnt[2], subs[j].cnt[3])
+                                : make_int4(0, 0, 0, 0);
         const int4 s = wg_scan<LANES>(X, v);
-        if (j < nsub) *(int4*)subs[j].ex = make_int4(s.x - v.x, s.y - v.y, s.z - v.z, s.w - v.w);
+        if (j < nsub) subs[j].ex[0] = s.x - v.x, subs[j].ex[1] = s.y - v.y, subs[j].ex[2] = s.z - v.z, subs[j].ex[3] = s.w - v.w;
         __syncthreads();
     }
     // 4. the final decode: coefficients and masks
     if (!huff::pass_write(T, F, subs, tid, LANES)) atomicOr(error, kJpegCorruptBit);
+}
+
+// Dynamic LDS: the subsequence states of a file with at most LANES of them (one per lane), so the
+// Jacobi rounds and the prefix read and write LDS; larger files keep them in F.subs.
+template <int LANES>
+__global__ __launch_bounds__(LANES) void jpeg_huff(const JpegHuffFile* __restrict__ files, int32_t* __restrict__ error)
+{
+    __shared__ huff::Tables T;
+    __shared__ Scan         X;
+    extern __shared__ JpegHuffSub lsubs[];
+    const JpegHuffFile&     F   = files[blockIdx.x];
+    const int               tid = threadIdx.x;
+
+    huff::tables_codes(T, F, tid, LANES);
+    if (tid == 0) X.carry = make_int4(0, 0, 0, 0);
+    __syncthreads();
+    huff::tables_fast(T, F, tid, LANES);
+    __syncthreads();
+    if (F.nsub <= LANES) decode_file<LANES>(T, X, F, (lds_sub*)lsubs, error);
+    else decode_file<LANES>(T, X, F, (glb_sub*)F.subs, error);
 }
 
 hipError_t launch_jpeg_huff(const JpegHuffFile* files, int n_files, int lanes, int32_t* error, hipStream_t stream)

@@ -12,8 +12,23 @@
 #define HUFF_FN inline
 #endif
 
+// Device-memory pointers the walks read and write are address-space-1 (global) pointers on the device:
+// generic (flat) accesses count on the LDS counter too, so every table lookup would wait for the bit
+// reader's loads and the coefficient stores in flight.
+#if defined(__HIP_DEVICE_COMPILE__)
+#define HUFF_GLOBAL __attribute__((address_space(1)))
+#else
+#define HUFF_GLOBAL
+#endif
+
 namespace aeon_hip {
 namespace huff {
+
+template <typename T>
+HUFF_FN HUFF_GLOBAL T* gmem(uint64_t a)
+{
+    return (HUFF_GLOBAL T*)a;
+}
 
 // Fast-table entry: bits 0-4 bits consumed, 5-8 AC run, 9-11 kind, 16-31 value (kValue) or value
 // size (kSym).  0: no code of <= kHuffFastBits bits is a prefix (the long-code walk).
@@ -31,10 +46,10 @@ struct Tables {
 HUFF_FN int imin(int a, int b) { return a < b ? a : b; }
 HUFF_FN int extend(int v, int s) { return v < (1 << (s - 1)) ? v - (1 << s) + 1 : v; }
 
-HUFF_FN void or_mask(uint64_t* m, uint64_t v)
+HUFF_FN void or_mask(HUFF_GLOBAL uint64_t* m, uint64_t v)
 {
 #if defined(__HIP_DEVICE_COMPILE__)
-    atomicOr((unsigned long long*)m, (unsigned long long)v);
+    __hip_atomic_fetch_or(m, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #else
     *m |= v;
 #endif
@@ -43,7 +58,7 @@ HUFF_FN void or_mask(uint64_t* m, uint64_t v)
 // Tables, part 1 (tables t0, t0 + dt, ...; symbols i0, i0 + di, ...): symbols, maxcode, delta.
 HUFF_FN void tables_codes(Tables& T, const JpegHuffFile& F, int i0, int di)
 {
-    const JpegHuffTab* tabs = (const JpegHuffTab*)F.tabs;
+    const HUFF_GLOBAL JpegHuffTab* tabs = gmem<const JpegHuffTab>(F.tabs);
     for (int i = i0; i < kTabs * 256; i += di)
         if ((i >> 8) % 3 < F.ncomp) T.vals[i >> 8][i & 255] = tabs[i >> 8].symbols[i & 255];
     for (int t = i0; t < kTabs; t += di) {
@@ -95,7 +110,7 @@ HUFF_FN void tables_fast(Tables& T, const JpegHuffFile& F, int i0, int di)
 // Bits of a segment: words at or past `end` read as zeros (libjpeg's fill after a marker).  64 bits
 // in hand and the next word loaded ahead.
 struct Bits {
-    const uint32_t* w;
+    const HUFF_GLOBAL uint32_t* w;
     int             end;
     uint64_t        buf; // next bits, first in bit 63
     int             n;   // valid bits in buf
@@ -145,7 +160,7 @@ struct Bits {
 HUFF_FN Bits bits_at(const JpegHuffFile& F, const JpegHuffSeg& S, int pos)
 {
     Bits b;
-    b.w   = (const uint32_t*)F.data;
+    b.w   = gmem<const uint32_t>(F.data);
     b.end = (int)S.end_bit;
     b.start(pos);
     return b;
@@ -173,8 +188,8 @@ HUFF_FN bool walk(const Tables& T, const JpegHuffFile& F, Bits& b, int& c, int& 
     auto blk_byte = [&](int cc) { return (int)(((cc < 8 ? tab_lo : tab_hi) >> (8 * (cc & 7))) & 0xff); };
     int       comp = blk_byte(c) & 3;
     uint64_t  mask = 0;
-    int16_t*  coef = nullptr;
-    uint64_t* mrec = nullptr;
+    HUFF_GLOBAL int16_t*  coef = nullptr;
+    HUFF_GLOBAL uint64_t* mrec = nullptr;
     bool      own  = k == 0; // the current block started in this walk
     auto open = [&]() {     // WRITE: locate the current block in its component plane
         const int    bt = blk_byte(c), x = (bt >> 2) & 3, y = (bt >> 4) & 3;
@@ -182,8 +197,8 @@ HUFF_FN bool walk(const Tables& T, const JpegHuffFile& F, Bits& b, int& c, int& 
         const int    hs = comp == 0 ? F.hs[0] : (comp == 1 ? F.hs[1] : F.hs[2]);
         const int    vs = comp == 0 ? F.vs[0] : (comp == 1 ? F.vs[1] : F.vs[2]);
         const size_t idx = (size_t)(o.my * vs + y) * bw + o.mx * hs + x;
-        coef = (int16_t*)(comp == 0 ? F.dvals[0] : (comp == 1 ? F.dvals[1] : F.dvals[2])) + idx * 64;
-        mrec = (uint64_t*)(comp == 0 ? F.blocks[0] : (comp == 1 ? F.blocks[1] : F.blocks[2])) + idx * 2;
+        coef = gmem<int16_t>(comp == 0 ? F.dvals[0] : (comp == 1 ? F.dvals[1] : F.dvals[2])) + idx * 64;
+        mrec = gmem<uint64_t>(comp == 0 ? F.blocks[0] : (comp == 1 ? F.blocks[1] : F.blocks[2])) + idx * 2;
     };
     if (WRITE && o.blk < o.blk_end) open();
     for (;;) {
@@ -277,13 +292,26 @@ HUFF_FN bool walk(const Tables& T, const JpegHuffFile& F, Bits& b, int& c, int& 
     return true;
 }
 
-// The phases below take the file's subsequence states `subs` (F.subs in device memory, or an LDS
-// copy when the file's subsequences fit the workgroup).
-// Phase 1: subsequences j0, j0 + dj, ... from their guessed starts.
-HUFF_FN void pass_guess(const Tables& T, const JpegHuffFile& F, JpegHuffSub* subs, int j0, int dj)
+template <typename S>
+HUFF_FN void set_cnt(S& s, int4 v)
 {
-    const JpegHuffSeg* segs = (const JpegHuffSeg*)F.segs;
-    const int32_t*     sseg = (const int32_t*)F.sub_seg;
+    s.cnt[0] = v.x, s.cnt[1] = v.y, s.cnt[2] = v.z, s.cnt[3] = v.w;
+}
+template <typename S>
+HUFF_FN int4 get_ex(const S& s)
+{
+    return make_int4(s.ex[0], s.ex[1], s.ex[2], s.ex[3]);
+}
+
+// The phases below take the file's subsequence states `subs` (F.subs in device memory, or an LDS
+// array when the file's subsequences fit the workgroup: on the device a pointer type of either
+// address space).
+// Phase 1: subsequences j0, j0 + dj, ... from their guessed starts.
+template <typename SP>
+HUFF_FN void pass_guess(const Tables& T, const JpegHuffFile& F, SP subs, int j0, int dj)
+{
+    const HUFF_GLOBAL JpegHuffSeg* segs = gmem<const JpegHuffSeg>(F.segs);
+    const HUFF_GLOBAL int32_t*     sseg = gmem<const int32_t>(F.sub_seg);
     Out                none{};
     for (int j = j0; j < F.nsub; j += dj) {
         const JpegHuffSeg S   = segs[sseg[j]];
@@ -296,18 +324,19 @@ HUFF_FN void pass_guess(const Tables& T, const JpegHuffFile& F, JpegHuffSub* sub
             walk<false>(T, F, b, c, k, p + F.sub_bits, false, cnt, none);
             en = pack_state(b.p, c, k);
         }
-        subs[j].st          = pack_state(p, 0, 0);
-        subs[j].en          = en;
-        *(int4*)subs[j].cnt = cnt;
+        subs[j].st = pack_state(p, 0, 0);
+        subs[j].en = en;
+        set_cnt(subs[j], cnt);
     }
 }
 
 // Phase 2a: a start that differs from its predecessor's end takes it (ex[0]: walk again).  Returns
 // whether any start changed.
-HUFF_FN int pass_compare(const JpegHuffFile& F, JpegHuffSub* subs, int j0, int dj)
+template <typename SP>
+HUFF_FN int pass_compare(const JpegHuffFile& F, SP subs, int j0, int dj)
 {
-    const JpegHuffSeg* segs = (const JpegHuffSeg*)F.segs;
-    const int32_t*     sseg = (const int32_t*)F.sub_seg;
+    const HUFF_GLOBAL JpegHuffSeg* segs = gmem<const JpegHuffSeg>(F.segs);
+    const HUFF_GLOBAL int32_t*     sseg = gmem<const int32_t>(F.sub_seg);
     int                any  = 0;
     for (int j = j0; j < F.nsub; j += dj) {
         const JpegHuffSeg S = segs[sseg[j]];
@@ -322,10 +351,11 @@ HUFF_FN int pass_compare(const JpegHuffFile& F, JpegHuffSub* subs, int j0, int d
 }
 
 // Phase 2b: walk the changed subsequences again from their new starts.
-HUFF_FN void pass_rewalk(const Tables& T, const JpegHuffFile& F, JpegHuffSub* subs, int j0, int dj)
+template <typename SP>
+HUFF_FN void pass_rewalk(const Tables& T, const JpegHuffFile& F, SP subs, int j0, int dj)
 {
-    const JpegHuffSeg* segs = (const JpegHuffSeg*)F.segs;
-    const int32_t*     sseg = (const int32_t*)F.sub_seg;
+    const HUFF_GLOBAL JpegHuffSeg* segs = gmem<const JpegHuffSeg>(F.segs);
+    const HUFF_GLOBAL int32_t*     sseg = gmem<const int32_t>(F.sub_seg);
     Out                none{};
     for (int j = j0; j < F.nsub; j += dj) {
         if (!subs[j].ex[0]) continue;
@@ -336,24 +366,25 @@ HUFF_FN void pass_rewalk(const Tables& T, const JpegHuffFile& F, JpegHuffSub* su
         int4              cnt = make_int4(0, 0, 0, 0);
         Bits              b   = bits_at(F, S, p);
         walk<false>(T, F, b, c, k, stop, false, cnt, none);
-        subs[j].en          = pack_state(b.p, c, k);
-        *(int4*)subs[j].cnt = cnt;
+        subs[j].en = pack_state(b.p, c, k);
+        set_cnt(subs[j], cnt);
     }
 }
 
 // Phase 4 (after the exclusive prefix of cnt into ex): the final decode.  Returns false if any of
 // the walks met corrupt data.
-HUFF_FN bool pass_write(const Tables& T, const JpegHuffFile& F, const JpegHuffSub* subs, int j0, int dj)
+template <typename SP>
+HUFF_FN bool pass_write(const Tables& T, const JpegHuffFile& F, SP subs, int j0, int dj)
 {
-    const JpegHuffSeg* segs = (const JpegHuffSeg*)F.segs;
-    const int32_t*     sseg = (const int32_t*)F.sub_seg;
+    const HUFF_GLOBAL JpegHuffSeg* segs = gmem<const JpegHuffSeg>(F.segs);
+    const HUFF_GLOBAL int32_t*     sseg = gmem<const int32_t>(F.sub_seg);
     const int          per_seg = F.restart * F.bpm, total = F.n_mcu * F.bpm;
     bool               ok = true;
     for (int j = j0; j < F.nsub; j += dj) {
         const int         sg = sseg[j];
         const JpegHuffSeg S  = segs[sg];
         const int         i  = j - S.first_sub;
-        const int4        e0 = *(const int4*)subs[S.first_sub].ex, e1 = *(const int4*)subs[j].ex;
+        const int4        e0 = get_ex(subs[S.first_sub]), e1 = get_ex(subs[j]);
         const uint64_t    st = subs[j].st;
         int               c = (int)(st >> 32) & 0xff, k = (int)(st >> 40) & 0xff;
         Out               o;

@@ -19,6 +19,21 @@
 
 namespace aeon_hip {
 
+// Device memory through address-space-1 pointers: generic (flat) loads and stores count on the LDS
+// counter too, so the LDS transposes and upsampling reads would wait for them.
+#if defined(__HIP_DEVICE_COMPILE__)
+template <typename T>
+using gp = __attribute__((address_space(1))) T*;
+#else
+template <typename T>
+using gp = T*; // (the host pass only parses the kernels)
+#endif
+template <typename T>
+__device__ __forceinline__ gp<T> gaddr(uint64_t a)
+{
+    return (gp<T>)a;
+}
+
 __constant__ uint8_t kZz[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,
                                 12, 19, 26, 33, 40, 48, 41, 34, 27, 20, 13, 6,  7,  14, 21, 28,
                                 35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51,
@@ -80,9 +95,9 @@ __global__ __launch_bounds__(kJpegIdctLanes) void jpeg_idct(const JpegImage* __r
     const JpegImage& I  = imgs[C.img];
     const int        k  = C.comp;
     const int        g = threadIdx.x >> 3, j = threadIdx.x & 7;
-    const JpegBlock* blocks = (const JpegBlock*)I.blocks[k] + C.first;
-    const int16_t*   vals   = (const int16_t*)I.values;
-    const int16_t*   dense  = (const int16_t*)I.dvals[k];
+    const gp<const JpegBlock> blocks = gaddr<const JpegBlock>(I.blocks[k]) + C.first;
+    const gp<const int16_t>   vals   = gaddr<const int16_t>(I.values);
+    const gp<const int16_t>   dense  = gaddr<const int16_t>(I.dvals[k]);
     JpegBlock        B[kJpegIdctUnroll];
 #pragma unroll
     for (int u = 0; u < kJpegIdctUnroll; u++) B[u] = blocks[min(g + u * G, C.count - 1)];
@@ -95,7 +110,7 @@ __global__ __launch_bounds__(kJpegIdctLanes) void jpeg_idct(const JpegImage* __r
     if (dense) {
 #pragma unroll
         for (int u = 0; u < kJpegIdctUnroll; u++) {
-            const int16_t* bv = dense + (size_t)(C.first + min(g + u * G, C.count - 1)) * 64;
+            const gp<const int16_t> bv = dense + (size_t)(C.first + min(g + u * G, C.count - 1)) * 64;
 #pragma unroll
             for (int r = 0; r < 8; r++) {
                 const int z = kZzInv[r * 8 + j];
@@ -136,12 +151,12 @@ __global__ __launch_bounds__(kJpegIdctLanes) void jpeg_idct(const JpegImage* __r
         if (bi < C.count) {
             const int b  = C.first + bi;
             const int bx = b % bw, by = b / bw;
-            uint8_t*  o  = (uint8_t*)I.planes[k] + (size_t)(by * 8 + j) * (bw * 8) + bx * 8;
+            const gp<uint8_t> o = gaddr<uint8_t>(I.planes[k]) + (size_t)(by * 8 + j) * (bw * 8) + bx * 8;
             const uint32_t lo = idct_limit(out[0]) | idct_limit(out[1]) << 8 | idct_limit(out[2]) << 16 |
                                 idct_limit(out[3]) << 24;
             const uint32_t hi = idct_limit(out[4]) | idct_limit(out[5]) << 8 | idct_limit(out[6]) << 16 |
                                 idct_limit(out[7]) << 24;
-            *(uint2*)o = make_uint2(lo, hi);
+            *(gp<uint2>)o = make_uint2(lo, hi);
         }
     }
 }
@@ -198,8 +213,8 @@ __device__ __forceinline__ int upsampled(const CompView& c, int x, int y)
 __device__ __forceinline__ void color_rows(const JpegImage& I, const CompView* cv, int y0, int nrows)
 {
     const int W = I.W, cn = I.out_cn, nc = cn == 1 ? 1 : I.ncomp;
-    uint8_t*  out    = (uint8_t*)I.out;
-    const int stride = I.out_stride;
+    const gp<uint8_t> out = gaddr<uint8_t>(I.out);
+    const int         stride = I.out_stride;
     const int groups = (W + 3) >> 2;
     for (int q = threadIdx.x; q < groups * nrows; q += blockDim.x) {
         const int y = y0 + q / groups, x0 = (q % groups) * 4;
@@ -219,12 +234,12 @@ __device__ __forceinline__ void color_rows(const JpegImage& I, const CompView* c
                        (uint32_t)min(max(r, 0), 255) << 16;
             }
         }
-        uint8_t* o = out + (size_t)y * stride + (size_t)x0 * cn;
+        const gp<uint8_t> o = out + (size_t)y * stride + (size_t)x0 * cn;
         if (x0 + 3 < W && ((uintptr_t)o & 3) == 0) {
             if (cn == 1) {
-                *(uint32_t*)o = p[0] | p[1] << 8 | p[2] << 16 | p[3] << 24;
+                *(gp<uint32_t>)o = p[0] | p[1] << 8 | p[2] << 16 | p[3] << 24;
             } else {
-                uint32_t* d = (uint32_t*)o;
+                const gp<uint32_t> d = (gp<uint32_t>)o;
                 d[0] = p[0] | p[1] << 24;
                 d[1] = p[1] >> 8 | p[2] << 16;
                 d[2] = p[2] >> 16 | p[3] << 8;
@@ -256,7 +271,7 @@ __global__ __launch_bounds__(256) void jpeg_color(const JpegImage* __restrict__ 
         comp_rows(I, k, R.y0, y1, c, hi);
         c.P = lds_b + off;
         // stage plane rows [lo, hi]: whole rows of pw bytes (a multiple of 8) are contiguous
-        const uint2* src = (const uint2*)((const uint8_t*)I.planes[k] + (size_t)c.lo * c.pw);
+        const gp<const uint2> src = (gp<const uint2>)(gaddr<const uint8_t>(I.planes[k]) + (size_t)c.lo * c.pw);
         uint2*       dst = (uint2*)(lds_b + off);
         const int    n8  = (hi - c.lo + 1) * c.pw / 8;
         for (int e = threadIdx.x; e < n8; e += blockDim.x) dst[e] = src[e];
@@ -294,9 +309,9 @@ __global__ __launch_bounds__(256) void jpeg_bands(const JpegImage* __restrict__ 
         c.P                     = lds_b + off;
         uint8_t*         plane  = lds_b + off;
         const int        bw     = I.bw[k], br0 = c.lo >> 3, nblk = ((hi >> 3) - br0 + 1) * bw;
-        const JpegBlock* blocks = (const JpegBlock*)I.blocks[k];
-        const int16_t*   dense  = (const int16_t*)I.dvals[k];
-        const int16_t*   vals   = (const int16_t*)I.values;
+        const gp<const JpegBlock> blocks = gaddr<const JpegBlock>(I.blocks[k]);
+        const gp<const int16_t>   dense  = gaddr<const int16_t>(I.dvals[k]);
+        const gp<const int16_t>   vals   = gaddr<const int16_t>(I.values);
         int              qv[8];
 #pragma unroll
         for (int r = 0; r < 8; r++) qv[r] = I.q[k][r * 8 + j];
@@ -306,7 +321,7 @@ __global__ __launch_bounds__(256) void jpeg_bands(const JpegImage* __restrict__ 
             const JpegBlock B   = blocks[idx];
             int             col[8], out[8], in[8];
             if (dense) { // the 8 loads do not wait for the mask
-                const int16_t* bv = dense + idx * 64;
+                const gp<const int16_t> bv = dense + idx * 64;
 #pragma unroll
                 for (int r = 0; r < 8; r++) {
                     const int z = kZzInv[r * 8 + j], v = bv[z];

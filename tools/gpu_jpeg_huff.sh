@@ -17,5 +17,5 @@ for l in open("gpurun_out/jpeg_stage.json"):
           "host us/file", {k: round(v, 1) for k, v in s["host_stage_us_per_file"].items()}, "e2e", round(d["e2e_device_outputs"]))
 PY
 rm -rf gpurun_out/jpeg_prof
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/jpeg_prof -o run -- python tools/jpeg_stage.py gpu > gpurun_out/jpeg_prof.log 2>&1 || { tail -5 gpurun_out/jpeg_prof.log; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/jpeg_prof -o run -- python tools/jpeg_stage.py gpu > gpurun_out/jpeg_prof.log 2>&1 || { tail -5 gpurun_out/jpeg_prof.log; exit 1; }
 f=$(find gpurun_out/jpeg_prof -name '*kernel_stats.csv' | head -1); [ -n "$f" ] && cut -d, -f1-8 "$f" | head -12
