@@ -20,7 +20,7 @@
 // length, the AC run and, when the value bits fit the lookahead too, the decoded value; longer codes
 // take the canonical maxcode walk.  The bit reader holds 64 bits and one word loaded ahead, so the
 // next refill's global load is in flight while the current bits decode.  A file with at most one
-// subsequence per lane keeps the subsequence states in LDS.  The per-lane logic is in
+// subsequence per lane keeps each lane's subsequence state in registers (decode_lanes).  The per-lane logic is in
 // jpeg_huff.hpp (shared with the host emulation the CPU tests run).
 #include <hip/hip_runtime.h>
 
@@ -56,15 +56,14 @@ __device__ int4 wg_scan(Scan& X, int4 v)
 
 } // namespace
 
-typedef __attribute__((address_space(3))) JpegHuffSub lds_sub;
 typedef __attribute__((address_space(1))) JpegHuffSub glb_sub;
 
-// The file's phases with its subsequence states behind SP (LDS or device memory).
-template <int LANES, typename SP>
-__device__ __forceinline__ void decode_file(const huff::Tables& T, Scan& X, const JpegHuffFile& F, SP subs,
-                                            int32_t* error)
+// A file with more subsequences than lanes: the phases over the subsequence states in F.subs.
+template <int LANES>
+__device__ __forceinline__ void decode_strided(const huff::Tables& T, Scan& X, const JpegHuffFile& F, int32_t* error)
 {
     const int tid = threadIdx.x, nsub = F.nsub;
+    glb_sub*  subs = (glb_sub*)F.subs;
     // 1. guessed starts; 2. Jacobi rounds until every start is its predecessor's end
     huff::pass_guess(T, F, subs, tid, LANES);
     for (;;) {
@@ -86,38 +85,99 @@ __device__ __forceinline__ void decode_file(const huff::Tables& T, Scan& X, cons
     if (!huff::pass_write(T, F, subs, tid, LANES)) atomicOr(error, kJpegCorruptBit);
 }
 
-// Dynamic LDS: the subsequence states of a file with at most LANES of them (one per lane), so the
-// Jacobi rounds and the prefix read and write LDS; larger files keep them in F.subs.
+// LDS of a file with at most LANES subsequences: each lane's end state and exclusive sums.
+template <int LANES>
+struct LaneStates {
+    uint64_t en[LANES];
+    int4     ex[LANES];
+};
+
+// A file with at most one subsequence per lane (the common case): lane j owns subsequence j and keeps
+// its segment, start state and counts in registers across the phases; the end states (which the next
+// lane reads) and the exclusive sums (which the segment's lanes read) go through LDS.  The same
+// phases as jpeg_huff.hpp's pass_* functions, which the host emulation checks.
+template <int LANES>
+__device__ __forceinline__ void decode_lanes(const huff::Tables& T, Scan& X, LaneStates<LANES>& L,
+                                             const JpegHuffFile& F, int32_t* error)
+{
+    const int  tid = threadIdx.x, nsub = F.nsub;
+    const bool have = tid < nsub;
+    int        sg = 0, i = 0;
+    JpegHuffSeg S{0, 0, 0, 1};
+    if (have) {
+        sg = huff::gmem<const int32_t>(F.sub_seg)[tid];
+        S  = huff::gmem<const JpegHuffSeg>(F.segs)[sg];
+        i  = tid - S.first_sub;
+    }
+    const bool     first = i == 0, last = i + 1 == S.nsub;
+    const int      p0    = (int)S.start_bit + i * F.sub_bits, stop = p0 + F.sub_bits;
+    uint64_t       st    = huff::pack_state(p0, 0, 0);
+    int4           cnt   = make_int4(0, 0, 0, 0);
+    huff::Out      none{};
+    auto walk_sync = [&]() {
+        int        c = (int)(st >> 32) & 0xff, k = (int)(st >> 40) & 0xff;
+        huff::Bits b = huff::bits_at(F, S, (int)(uint32_t)st);
+        cnt          = make_int4(0, 0, 0, 0);
+        huff::walk<false>(T, F, b, c, k, stop, false, cnt, none);
+        L.en[tid] = huff::pack_state(b.p, c, k);
+    };
+    // 1. the guessed start (the segment's last subsequence ends nobody's start)
+    if (have && !last) walk_sync();
+    // 2. Jacobi rounds
+    for (;;) {
+        __syncthreads();
+        bool dirty = false;
+        if (have && !first) {
+            const uint64_t e = L.en[tid - 1];
+            if (e != st) st = e, dirty = true;
+        }
+        if (!__syncthreads_or(dirty)) break;
+        if (dirty && !last) walk_sync();
+    }
+    // 3. exclusive prefix (one chunk: nsub <= LANES)
+    const int4 s = wg_scan<LANES>(X, cnt);
+    L.ex[tid]    = make_int4(s.x - cnt.x, s.y - cnt.y, s.z - cnt.z, s.w - cnt.w);
+    __syncthreads();
+    if (!have) return;
+    // 4. the final decode
+    const int4 e0 = L.ex[S.first_sub], e1 = L.ex[tid];
+    const int  per_seg = F.restart * F.bpm, total = F.n_mcu * F.bpm;
+    int        c = (int)(st >> 32) & 0xff, k = (int)(st >> 40) & 0xff;
+    huff::Out  o;
+    o.blk     = sg * per_seg + (e1.x - e0.x) - (k > 0);
+    o.blk_end = min(sg * per_seg + per_seg, total);
+    o.pred0 = e1.y - e0.y, o.pred1 = e1.z - e0.z, o.pred2 = e1.w - e0.w;
+    o.trunc = F.truncated >= 0 && sg >= F.truncated;
+    if (o.blk < sg * per_seg) return;
+    const int mcu = o.blk / F.bpm;
+    o.mx = mcu % F.mcux, o.my = mcu / F.mcux;
+    huff::Bits b = huff::bits_at(F, S, (int)(uint32_t)st);
+    if (!huff::walk<true>(T, F, b, c, k, stop, last, cnt, o)) atomicOr(error, kJpegCorruptBit);
+}
+
 template <int LANES>
 __global__ __launch_bounds__(LANES) void jpeg_huff(const JpegHuffFile* __restrict__ files, int32_t* __restrict__ error)
 {
-    __shared__ huff::Tables T;
-    __shared__ Scan         X;
-    extern __shared__ JpegHuffSub lsubs[];
-    const JpegHuffFile&     F   = files[blockIdx.x];
-    const int               tid = threadIdx.x;
+    __shared__ huff::Tables      T;
+    __shared__ Scan              X;
+    __shared__ LaneStates<LANES> L;
+    const JpegHuffFile&          F   = files[blockIdx.x];
+    const int                    tid = threadIdx.x;
 
     huff::tables_codes(T, F, tid, LANES);
     if (tid == 0) X.carry = make_int4(0, 0, 0, 0);
     __syncthreads();
     huff::tables_fast(T, F, tid, LANES);
     __syncthreads();
-    if (F.nsub <= LANES) decode_file<LANES>(T, X, F, (lds_sub*)lsubs, error);
-    else decode_file<LANES>(T, X, F, (glb_sub*)F.subs, error);
+    if (F.nsub <= LANES) decode_lanes<LANES>(T, X, L, F, error);
+    else decode_strided<LANES>(T, X, F, error);
 }
 
 hipError_t launch_jpeg_huff(const JpegHuffFile* files, int n_files, int lanes, int32_t* error, hipStream_t stream)
 {
     if (n_files <= 0) return hipSuccess;
-    const size_t lds = (size_t)lanes * sizeof(JpegHuffSub);
-    if (lanes == 256) {
-        hipLaunchKernelGGL(jpeg_huff<256>, dim3(n_files), dim3(256), lds, stream, files, error);
-    } else {
-        static const hipError_t attr = hipFuncSetAttribute((const void*)jpeg_huff<1024>,
-                                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        if (attr != hipSuccess) return attr;
-        hipLaunchKernelGGL(jpeg_huff<1024>, dim3(n_files), dim3(1024), lds, stream, files, error);
-    }
+    if (lanes == 256) hipLaunchKernelGGL(jpeg_huff<256>, dim3(n_files), dim3(256), 0, stream, files, error);
+    else hipLaunchKernelGGL(jpeg_huff<1024>, dim3(n_files), dim3(1024), 0, stream, files, error);
     return hipGetLastError();
 }
 
