@@ -108,39 +108,42 @@ HUFF_FN void tables_fast(Tables& T, const JpegHuffFile& F, int i0, int di)
 }
 
 // Bits of a segment: words at or past `end` read as zeros (libjpeg's fill after a marker).  64 bits
-// in hand and the next word loaded ahead.
+// in hand and the next word's load in flight: it is byte-swapped and masked only when a refill takes
+// it, so its latency overlaps the codewords decoded meanwhile.
 struct Bits {
     const HUFF_GLOBAL uint32_t* w;
-    int             end;
-    uint64_t        buf; // next bits, first in bit 63
-    int             n;   // valid bits in buf
-    int             p;   // bit position of buf's bit 63
-    uint32_t        nxt; // word nw, loaded ahead
-    int             nw;
+    int                         end;
+    int                         last; // last word index holding segment bits (clamps the loads)
+    uint64_t                    buf;  // next bits, first in bit 63
+    int                         n;    // valid bits in buf
+    int                         p;    // bit position of buf's bit 63
+    uint32_t                    raw;  // word nw as loaded
+    int                         nw;
 
-    HUFF_FN uint32_t word(int i) const
+    HUFF_FN uint32_t load(int i) const { return w[imin(i, last)]; }
+    HUFF_FN uint32_t fix(uint32_t v, int i) const // big-endian, bits at or past `end` zeroed
     {
-        const int      last = end > 0 ? (end - 1) >> 5 : 0;
-        const uint32_t v    = __builtin_bswap32(w[imin(i, last)]);
-        const int      rem  = end - i * 32;
+        v             = __builtin_bswap32(v);
+        const int rem = end - i * 32;
         return rem >= 32 ? v : (rem <= 0 ? 0u : v & (0xffffffffu << (32 - rem)));
     }
     HUFF_FN void start(int pos)
     {
         const int i = pos >> 5, s = pos & 31;
-        buf = (((uint64_t)word(i) << 32) | word(i + 1)) << s;
-        n   = 64 - s;
-        p   = pos;
-        nw  = i + 2;
-        nxt = word(nw);
+        last = end > 0 ? (end - 1) >> 5 : 0;
+        buf  = (((uint64_t)fix(load(i), i) << 32) | fix(load(i + 1), i + 1)) << s;
+        n    = 64 - s;
+        p    = pos;
+        nw   = i + 2;
+        raw  = load(nw);
     }
     // >= 32 valid bits: a code (<= 16) and its value bits (<= 15) without another check
     HUFF_FN void fill()
     {
         if (n < 32) {
-            buf |= (uint64_t)nxt << (32 - n);
+            buf |= (uint64_t)fix(raw, nw) << (32 - n);
             n += 32;
-            nxt = word(++nw);
+            raw = load(++nw);
         }
     }
     HUFF_FN void skip(int l)

@@ -112,9 +112,9 @@ __global__ __launch_bounds__(kJpegIdctLanes) void jpeg_idct(const JpegImage* __r
         for (int u = 0; u < kJpegIdctUnroll; u++) {
             const gp<const int16_t> bv = dense + (size_t)(C.first + min(g + u * G, C.count - 1)) * 64;
 #pragma unroll
-            for (int r = 0; r < 8; r++) {
+            for (int r = 0; r < 8; r++) { // unconditional loads, the mask zeroes the stale slots
                 const int z = kZzInv[r * 8 + j];
-                col[u][r]   = (B[u].mask >> z) & 1 ? (int)bv[z] * qv[r] : 0;
+                col[u][r]   = ((int)bv[z] * qv[r]) & -(int)((B[u].mask >> z) & 1);
             }
         }
     } else {
@@ -298,6 +298,9 @@ __global__ __launch_bounds__(256) void jpeg_bands(const JpegImage* __restrict__ 
     const int        y1 = R.y0 + R.rows - 1;
     const int        g = threadIdx.x >> 3, j = threadIdx.x & 7;
     int*             s = slot + g * kSlot;
+    int              zz[8]; // zigzag index of (row r, column j), in registers: the wave fences below
+#pragma unroll              // would make the compiler reload the table for every block
+    for (int r = 0; r < 8; r++) zz[r] = kZzInv[r * 8 + j];
     CompView         cv[3];
     int              off = 0;
 #pragma unroll
@@ -315,22 +318,34 @@ __global__ __launch_bounds__(256) void jpeg_bands(const JpegImage* __restrict__ 
         int              qv[8];
 #pragma unroll
         for (int r = 0; r < 8; r++) qv[r] = I.q[k][r * 8 + j];
+        // a GPU-decoded file's block b: its mask and column j's 8 slots, loaded unconditionally (the
+        // unmasked slots hold stale values, zeroed by the mask) one block ahead of the transform
+        auto fetch = [&](int b, uint64_t& m, int (&v)[8]) {
+            const size_t            idx = (size_t)(br0 + b / bw) * bw + b % bw;
+            const gp<const int16_t> bv  = dense + idx * 64;
+            m                           = blocks[idx].mask;
+#pragma unroll
+            for (int r = 0; r < 8; r++) v[r] = bv[zz[r]];
+        };
+        uint64_t nmask = 0;
+        int      nv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (dense && g < nblk) fetch(g, nmask, nv);
         for (int b = g; b < nblk; b += 32) {
-            const int       by = br0 + b / bw, bx = b % bw;
-            const size_t    idx = (size_t)by * bw + bx;
-            const JpegBlock B   = blocks[idx];
-            int             col[8], out[8], in[8];
-            if (dense) { // the 8 loads do not wait for the mask
-                const gp<const int16_t> bv = dense + idx * 64;
+            const int by = br0 + b / bw, bx = b % bw;
+            int       col[8], out[8], in[8];
+            if (dense) {
+                const uint64_t m = nmask;
+                int            v[8];
 #pragma unroll
-                for (int r = 0; r < 8; r++) {
-                    const int z = kZzInv[r * 8 + j], v = bv[z];
-                    col[r]      = (B.mask >> z) & 1 ? v * qv[r] : 0;
-                }
+                for (int r = 0; r < 8; r++) v[r] = nv[r];
+                if (b + 32 < nblk) fetch(b + 32, nmask, nv);
+#pragma unroll
+                for (int r = 0; r < 8; r++) col[r] = (v[r] * qv[r]) & -(int)((m >> zz[r]) & 1);
             } else {
+                const JpegBlock B = blocks[(size_t)by * bw + bx];
 #pragma unroll
                 for (int r = 0; r < 8; r++) {
-                    const int z = kZzInv[r * 8 + j];
+                    const int z = zz[r];
                     col[r]      = (B.mask >> z) & 1
                                       ? (int)vals[B.val_off + __builtin_popcountll(B.mask & ((1ull << z) - 1))] * qv[r]
                                       : 0;
