@@ -867,16 +867,26 @@ bool prepare_gpu(const uint8_t* d, size_t size, Frame& f, Arena& a, GpuScan& g, 
     if (adobe_rgb && f.ncomp == 3) unsupported("RGB (Adobe transform 0) JPEGs");
     // segments: the ones past the scan's restart intervals are ignored, missing ones are empty;
     // subsequences: the data spread over the workgroup's lanes, within [kHuffSubMin, kHuffSubMax] bits
-    const int64_t spread = ((int64_t)8 * o / std::max(lanes, 1) + 31) & ~(int64_t)31;
-    g.sub_bits = (int)std::min<int64_t>(kHuffSubMax, std::max<int64_t>(kHuffSubMin, spread));
+    // (longer when the segments' rounding up would give a lane more than one)
     std::vector<JpegHuffSeg> segs(nseg_need);
-    int                      nsub = 0;
     for (int s = 0; s < nseg_need; s++) {
         const uint32_t b0 = s < (int)seg.size() ? seg[s] : (uint32_t)o;
         const uint32_t b1 = s + 1 < (int)seg.size() ? seg[s + 1] : (uint32_t)o;
-        const uint32_t bits = 8 * (b1 - b0);
-        segs[s] = {8 * b0, 8 * b1, nsub, std::max(1, (int)((bits + g.sub_bits - 1) / g.sub_bits))};
-        nsub += segs[s].nsub;
+        segs[s]           = {8 * b0, 8 * b1, 0, 0};
+    }
+    auto count = [&](int sub_bits) {
+        int64_t c = 0;
+        for (const JpegHuffSeg& S : segs) c += std::max<int64_t>(1, (S.end_bit - S.start_bit + sub_bits - 1) / sub_bits);
+        return c;
+    };
+    const int64_t spread = ((int64_t)8 * o / std::max(lanes, 1) + 31) & ~(int64_t)31;
+    g.sub_bits = (int)std::min<int64_t>(kHuffSubMax, std::max<int64_t>(kHuffSubMin, spread));
+    while (g.sub_bits < kHuffSubMax && count(g.sub_bits) > lanes) g.sub_bits = std::min(kHuffSubMax, g.sub_bits + 32);
+    int nsub = 0;
+    for (JpegHuffSeg& S : segs) {
+        S.first_sub = nsub;
+        S.nsub      = std::max(1, (int)((S.end_bit - S.start_bit + g.sub_bits - 1) / g.sub_bits));
+        nsub += S.nsub;
     }
     if (g.truncated >= nseg_need) g.truncated = -1; // (data of an ignored interval)
     g.nseg = nseg_need, g.nsub = nsub;
