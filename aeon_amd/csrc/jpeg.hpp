@@ -84,6 +84,7 @@ constexpr int kHuffSubMax   = 1024; // multiple of 32 in [min, max] nearest to s
 constexpr int kHuffLanes    = 1024; // jpeg_huff workgroup (one per file)
 constexpr int kHuffMaxBpm   = 16;   // blocks per MCU the GPU path takes (libjpeg allows 10)
 constexpr int kHuffFastBits = 10;   // lookahead of the LDS decode tables
+constexpr int kHuffStageMax = 96 * 1024; // a file's data up to this is copied into LDS for its walks
 
 // One DHT table as the file defines it (code lengths 1..16, then the symbols), validated on the host.
 struct JpegHuffTab {
@@ -120,6 +121,7 @@ struct alignas(16) JpegHuffFile {
     int32_t  bpm, mcux, ncomp;           // a non-interleaved (grayscale) scan: bpm 1, mcux = blocks per row
     int32_t  truncated; // first segment whose data ends with the file, not a marker (reading past it is an error); -1: none
     int32_t  bw[3], hs[3], vs[3], sub_bits; // sub_bits: the file's subsequence length
+    int32_t  data_words, pad_[3];           // the data's 32-bit words (padding included)
 };
 
 // Device error word bit of a GPU-decoded file whose entropy-coded data is corrupt or truncated.

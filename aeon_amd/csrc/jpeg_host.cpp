@@ -24,7 +24,8 @@
 namespace aeon_hip {
 hipError_t launch_jpeg(const JpegImage* imgs, const JpegRows* bands, int n_bands, int band_lds, const JpegChunk* chunks,
                        int n_chunks, const JpegRows* rows, int n_rows, int color_lds, hipStream_t stream);
-hipError_t launch_jpeg_huff(const JpegHuffFile* files, int n_files, int lanes, int32_t* error, hipStream_t stream);
+hipError_t launch_jpeg_huff(const JpegHuffFile* files, int n_files, int lanes, int stage_bytes, int32_t* error,
+                            hipStream_t stream);
 
 namespace {
 
@@ -664,7 +665,7 @@ void decode_file(const uint8_t* d, size_t size, Frame& f, Arena& a, size_t blk_o
 // arena and the scan's shape.
 struct GpuScan {
     size_t   tabs = 0, segs = 0, sub_seg = 0, data = 0; // arena offsets
-    int      nseg = 0, nsub = 0, restart = 0, n_mcu = 0, bpm = 0, mcux = 0, truncated = -1, sub_bits = 0;
+    int      nseg = 0, nsub = 0, restart = 0, n_mcu = 0, bpm = 0, mcux = 0, truncated = -1, sub_bits = 0, data_words = 0;
     bool     interleaved = false;
     uint64_t blk_tab[2] = {0, 0};
 };
@@ -844,7 +845,8 @@ bool prepare_gpu(const uint8_t* d, size_t size, Frame& f, Arena& a, GpuScan& g, 
         }
     }
     std::memset(out + o, 0, 16);
-    a.used = g.data + ((o + 16 + 3) & ~(size_t)3);
+    a.used       = g.data + ((o + 16 + 3) & ~(size_t)3);
+    g.data_words = (int)(((o + 16 + 3) & ~(size_t)3) / 4);
     // the markers after the scan: a second scan goes to the host decoder; Adobe APP14 as decode_file
     for (;;) {
         while (p < end && *p != 0xFF) p++;
@@ -1111,6 +1113,7 @@ void jpeg_decode_batch(JpegState* S, int n, const void* const* data, const size_
     const uint64_t dev  = (uint64_t)st.dev, work = (uint64_t)st.work;
     JpegImage*     imgs = (JpegImage*)st.pinned;
     JpegHuffFile*  hf   = (JpegHuffFile*)(st.pinned + huf_off);
+    int            huff_stage = 0; // LDS for the largest GPU-decoded file's data that fits kHuffStageMax
     for (int i = 0; i < n; i++) {
         const Frame& f = frames[i];
         JpegImage&   J = imgs[i];
@@ -1151,6 +1154,8 @@ void jpeg_decode_batch(JpegState* S, int n, const void* const* data, const size_
         H.blk_tab[0] = g.blk_tab[0], H.blk_tab[1] = g.blk_tab[1];
         H.nseg = g.nseg, H.nsub = g.nsub, H.restart = g.restart, H.n_mcu = g.n_mcu;
         H.bpm = g.bpm, H.mcux = g.mcux, H.ncomp = f.ncomp, H.truncated = g.truncated, H.sub_bits = g.sub_bits;
+        H.data_words = g.data_words;
+        if (g.data_words * 4 <= kHuffStageMax) huff_stage = std::max(huff_stage, g.data_words * 4);
     }
     if (!bands.empty()) std::memcpy(st.pinned + band_off, bands.data(), bands.size() * sizeof(JpegRows));
     if (!chunks.empty()) std::memcpy(st.pinned + chk_off, chunks.data(), chunks.size() * sizeof(JpegChunk));
@@ -1162,7 +1167,7 @@ void jpeg_decode_batch(JpegState* S, int n, const void* const* data, const size_
     if (n_gpu) hip_ok(hipMemsetAsync(st.work, 0, rec_bytes, stream), "hipMemsetAsync");
     if (start) hip_ok(hipEventRecord(start, stream), "hipEventRecord");
     if (n_gpu)
-        hip_ok(launch_jpeg_huff((const JpegHuffFile*)(st.dev + huf_off), n_gpu, S->huff_lanes, error, stream),
+        hip_ok(launch_jpeg_huff((const JpegHuffFile*)(st.dev + huf_off), n_gpu, S->huff_lanes, huff_stage, error, stream),
                "JPEG Huffman kernel");
     hip_ok(launch_jpeg((const JpegImage*)st.dev, (const JpegRows*)(st.dev + band_off), (int)bands.size(), band_lds,
                        (const JpegChunk*)(st.dev + chk_off), (int)chunks.size(), (const JpegRows*)(st.dev + row_off),
@@ -1258,6 +1263,7 @@ int jpeg_gpu_entropy_emulate(const void* data, size_t size, int lanes, int* w, i
     F.blk_tab[0] = g.blk_tab[0], F.blk_tab[1] = g.blk_tab[1];
     F.nseg = g.nseg, F.nsub = g.nsub, F.restart = g.restart, F.n_mcu = g.n_mcu;
     F.bpm = g.bpm, F.mcux = g.mcux, F.ncomp = f.ncomp, F.truncated = g.truncated, F.sub_bits = g.sub_bits;
+    F.data_words = g.data_words;
     std::unique_ptr<huff::Tables> T(new huff::Tables());
     huff::tables_codes(*T, F, 0, 1);
     huff::tables_fast(*T, F, 0, 1);

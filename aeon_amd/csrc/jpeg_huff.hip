@@ -96,9 +96,9 @@ struct LaneStates {
 // its segment, start state and counts in registers across the phases; the end states (which the next
 // lane reads) and the exclusive sums (which the segment's lanes read) go through LDS.  The same
 // phases as jpeg_huff.hpp's pass_* functions, which the host emulation checks.
-template <int LANES>
+template <int LANES, typename WP>
 __device__ __forceinline__ void decode_lanes(const huff::Tables& T, Scan& X, LaneStates<LANES>& L,
-                                             const JpegHuffFile& F, int32_t* error)
+                                             const JpegHuffFile& F, WP words, int32_t* error)
 {
     const int  tid = threadIdx.x, nsub = F.nsub;
     const bool have = tid < nsub;
@@ -116,8 +116,8 @@ __device__ __forceinline__ void decode_lanes(const huff::Tables& T, Scan& X, Lan
     huff::Out      none{};
     auto walk_sync = [&]() {
         int        c = (int)(st >> 32) & 0xff, k = (int)(st >> 40) & 0xff;
-        huff::Bits b = huff::bits_at(F, S, (int)(uint32_t)st);
-        cnt          = make_int4(0, 0, 0, 0);
+        auto b = huff::bits_from(words, S, (int)(uint32_t)st);
+        cnt    = make_int4(0, 0, 0, 0);
         huff::walk<false>(T, F, b, c, k, stop, false, cnt, none);
         L.en[tid] = huff::pack_state(b.p, c, k);
     };
@@ -151,33 +151,56 @@ __device__ __forceinline__ void decode_lanes(const huff::Tables& T, Scan& X, Lan
     if (o.blk < sg * per_seg) return;
     const int mcu = o.blk / F.bpm;
     o.mx = mcu % F.mcux, o.my = mcu / F.mcux;
-    huff::Bits b = huff::bits_at(F, S, (int)(uint32_t)st);
+    auto b = huff::bits_from(words, S, (int)(uint32_t)st);
     if (!huff::walk<true>(T, F, b, c, k, stop, last, cnt, o)) atomicOr(error, kJpegCorruptBit);
 }
 
+typedef __attribute__((address_space(3))) const uint32_t* lds_words;
+
+// Dynamic LDS (stage_bytes): a copy of the file's data when it fits, so every walk's start and
+// refills read LDS instead of device memory.
 template <int LANES>
-__global__ __launch_bounds__(LANES) void jpeg_huff(const JpegHuffFile* __restrict__ files, int32_t* __restrict__ error)
+__global__ __launch_bounds__(LANES) void jpeg_huff(const JpegHuffFile* __restrict__ files, int stage_bytes,
+                                                   int32_t* __restrict__ error)
 {
     __shared__ huff::Tables      T;
     __shared__ Scan              X;
     __shared__ LaneStates<LANES> L;
+    extern __shared__ uint32_t   stage[];
     const JpegHuffFile&          F   = files[blockIdx.x];
     const int                    tid = threadIdx.x;
+    const bool                   staged = F.nsub <= LANES && F.data_words * 4 <= stage_bytes;
 
+    if (staged) { // 16-byte copies, all in flight before the tables are built
+        const auto src = huff::gmem<const uint4>(F.data);
+        for (int i = tid; i < (F.data_words + 3) / 4; i += LANES) ((uint4*)stage)[i] = src[i];
+    }
     huff::tables_codes(T, F, tid, LANES);
     if (tid == 0) X.carry = make_int4(0, 0, 0, 0);
     __syncthreads();
     huff::tables_fast(T, F, tid, LANES);
     __syncthreads();
-    if (F.nsub <= LANES) decode_lanes<LANES>(T, X, L, F, error);
+    if (staged) decode_lanes<LANES>(T, X, L, F, (lds_words)stage, error);
+    else if (F.nsub <= LANES) decode_lanes<LANES>(T, X, L, F, huff::gmem<const uint32_t>(F.data), error);
     else decode_strided<LANES>(T, X, F, error);
 }
 
-hipError_t launch_jpeg_huff(const JpegHuffFile* files, int n_files, int lanes, int32_t* error, hipStream_t stream)
+hipError_t launch_jpeg_huff(const JpegHuffFile* files, int n_files, int lanes, int stage_bytes, int32_t* error,
+                            hipStream_t stream)
 {
     if (n_files <= 0) return hipSuccess;
-    if (lanes == 256) hipLaunchKernelGGL(jpeg_huff<256>, dim3(n_files), dim3(256), 0, stream, files, error);
-    else hipLaunchKernelGGL(jpeg_huff<1024>, dim3(n_files), dim3(1024), 0, stream, files, error);
+    stage_bytes = (stage_bytes + 15) & ~15;
+    if (lanes == 256) {
+        static const hipError_t a = hipFuncSetAttribute((const void*)jpeg_huff<256>,
+                                                        hipFuncAttributeMaxDynamicSharedMemorySize, kHuffStageMax);
+        if (a != hipSuccess) return a;
+        hipLaunchKernelGGL(jpeg_huff<256>, dim3(n_files), dim3(256), stage_bytes, stream, files, stage_bytes, error);
+    } else {
+        static const hipError_t a = hipFuncSetAttribute((const void*)jpeg_huff<1024>,
+                                                        hipFuncAttributeMaxDynamicSharedMemorySize, kHuffStageMax);
+        if (a != hipSuccess) return a;
+        hipLaunchKernelGGL(jpeg_huff<1024>, dim3(n_files), dim3(1024), stage_bytes, stream, files, stage_bytes, error);
+    }
     return hipGetLastError();
 }
 

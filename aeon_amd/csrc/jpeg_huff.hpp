@@ -110,8 +110,9 @@ HUFF_FN void tables_fast(Tables& T, const JpegHuffFile& F, int i0, int di)
 // Bits of a segment: words at or past `end` read as zeros (libjpeg's fill after a marker).  64 bits
 // in hand and the next word's load in flight: it is byte-swapped and masked only when a refill takes
 // it, so its latency overlaps the codewords decoded meanwhile.
-struct Bits {
-    const HUFF_GLOBAL uint32_t* w;
+template <typename WP>
+struct BitsT {
+    WP                          w;    // the file's data as 32-bit words (device memory, or its LDS copy)
     int                         end;
     int                         last; // last word index holding segment bits (clamps the loads)
     uint64_t                    buf;  // next bits, first in bit 63
@@ -160,13 +161,21 @@ struct Bits {
     }
 };
 
-HUFF_FN Bits bits_at(const JpegHuffFile& F, const JpegHuffSeg& S, int pos)
+using Bits = BitsT<const HUFF_GLOBAL uint32_t*>;
+
+template <typename WP>
+HUFF_FN BitsT<WP> bits_from(WP w, const JpegHuffSeg& S, int pos)
 {
-    Bits b;
-    b.w   = gmem<const uint32_t>(F.data);
+    BitsT<WP> b;
+    b.w   = w;
     b.end = (int)S.end_bit;
     b.start(pos);
     return b;
+}
+
+HUFF_FN Bits bits_at(const JpegHuffFile& F, const JpegHuffSeg& S, int pos)
+{
+    return bits_from(gmem<const uint32_t>(F.data), S, pos);
 }
 
 HUFF_FN uint64_t pack_state(int p, int c, int k) { return (uint32_t)p | ((uint64_t)c << 32) | ((uint64_t)k << 40); }
@@ -183,8 +192,8 @@ struct Out {
 // counting blocks started and DC differences per component in cnt.  WRITE: the same walk (the last
 // subsequence of a segment: until the segment's blocks are done) storing coefficients and masks.
 // Returns false on corrupt data (WRITE only).
-template <bool WRITE>
-HUFF_FN bool walk(const Tables& T, const JpegHuffFile& F, Bits& b, int& c, int& k, int stop, bool last, int4& cnt,
+template <bool WRITE, typename B>
+HUFF_FN bool walk(const Tables& T, const JpegHuffFile& F, B& b, int& c, int& k, int stop, bool last, int4& cnt,
                   Out& o)
 {
     const uint64_t tab_lo = F.blk_tab[0], tab_hi = F.blk_tab[1];
