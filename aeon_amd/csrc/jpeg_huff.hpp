@@ -250,7 +250,11 @@ HUFF_FN bool walk(const Tables& T, const JpegHuffFile& F, B& b, int& c, int& k, 
                 if (WRITE) return false;
                 z = 15;
             }
-            if (z) v = extend(b.get(z), z);
+            if (WRITE || k == 0) { // (a sync walk only skips AC value bits)
+                if (z) v = extend(b.get(z), z);
+            } else {
+                b.skip(z);
+            }
         }
         if (WRITE && o.trunc && b.p > b.end) return false; // past the end of the file's data
         if (k == 0) { // DC difference
