@@ -1267,6 +1267,7 @@ int jpeg_gpu_entropy_emulate(const void* data, size_t size, int lanes, int* w, i
     std::unique_ptr<huff::Tables> T(new huff::Tables());
     huff::tables_codes(*T, F, 0, 1);
     huff::tables_fast(*T, F, 0, 1);
+    huff::tables_long(*T, F, 0, 1);
     huff::pass_guess(*T, F, subs.data(), 0, 1);
     int r = 0;
     while (huff::pass_compare(F, subs.data(), 0, 1)) huff::pass_rewalk(*T, F, subs.data(), 0, 1), r++;

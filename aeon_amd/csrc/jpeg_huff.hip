@@ -29,6 +29,24 @@
 namespace aeon_hip {
 namespace {
 
+// AEON_HUFF_PROBE builds (tools/build_variants.sh, development only): lane 0 of workgroup 0 stamps
+// the wall clock (100 MHz) at the phase boundaries of its file and prints them at the end.
+#ifdef AEON_HUFF_PROBE
+__shared__ unsigned long long probe_t[256];
+__shared__ int                probe_n[256];
+__shared__ int                probe_k;
+#define HUFF_STAMP(what, n)                                                                                   \
+    do {                                                                                                      \
+        if (blockIdx.x == 0 && threadIdx.x == 0 && probe_k < 256)                                             \
+            probe_t[probe_k] = wall_clock64(), probe_n[probe_k++] = (int)(n);                                 \
+    } while (0)
+#else
+#define HUFF_STAMP(what, n) \
+    do {                    \
+        (void)(n);          \
+    } while (0)
+#endif
+
 struct Scan {
     int4 wsum[1024 / 64];
     int4 carry;
@@ -113,19 +131,20 @@ __device__ __forceinline__ void decode_lanes(const huff::Tables& T, Scan& X, Lan
     const int      p0    = (int)S.start_bit + i * F.sub_bits, stop = p0 + F.sub_bits;
     uint64_t       st    = huff::pack_state(p0, 0, 0);
     int4           cnt   = make_int4(0, 0, 0, 0);
-    huff::Out      none{};
     auto walk_sync = [&]() {
         int        c = (int)(st >> 32) & 0xff, k = (int)(st >> 40) & 0xff;
         auto b = huff::bits_from(words, S, (int)(uint32_t)st);
         cnt    = make_int4(0, 0, 0, 0);
-        huff::walk<false>(T, F, b, c, k, stop, false, cnt, none);
+        huff::walk_sync(T, F, b, c, k, stop, cnt);
         L.en[tid] = huff::pack_state(b.p, c, k);
     };
+    HUFF_STAMP("start", nsub);
     // 1. the guessed start (the segment's last subsequence ends nobody's start)
     if (have && !last) walk_sync();
     // 2. Jacobi rounds
-    for (;;) {
+    for (int round = 0;; round++) {
         __syncthreads();
+        HUFF_STAMP("round", round);
         bool dirty = false;
         if (have && !first) {
             const uint64_t e = L.en[tid - 1];
@@ -138,6 +157,7 @@ __device__ __forceinline__ void decode_lanes(const huff::Tables& T, Scan& X, Lan
     const int4 s = wg_scan<LANES>(X, cnt);
     L.ex[tid]    = make_int4(s.x - cnt.x, s.y - cnt.y, s.z - cnt.z, s.w - cnt.w);
     __syncthreads();
+    HUFF_STAMP("scanned", 0);
     if (!have) return;
     // 4. the final decode
     const int4 e0 = L.ex[S.first_sub], e1 = L.ex[tid];
@@ -152,7 +172,8 @@ __device__ __forceinline__ void decode_lanes(const huff::Tables& T, Scan& X, Lan
     const int mcu = o.blk / F.bpm;
     o.mx = mcu % F.mcux, o.my = mcu / F.mcux;
     auto b = huff::bits_from(words, S, (int)(uint32_t)st);
-    if (!huff::walk<true>(T, F, b, c, k, stop, last, cnt, o)) atomicOr(error, kJpegCorruptBit);
+    if (!huff::walk_write(T, F, b, c, k, stop, last, o)) atomicOr(error, kJpegCorruptBit);
+    HUFF_STAMP("written", b.p - p0);
 }
 
 typedef __attribute__((address_space(3))) const uint32_t* lds_words;
@@ -175,14 +196,26 @@ __global__ __launch_bounds__(LANES) void jpeg_huff(const JpegHuffFile* __restric
         const auto src = huff::gmem<const uint4>(F.data);
         for (int i = tid; i < (F.data_words + 3) / 4; i += LANES) ((uint4*)stage)[i] = src[i];
     }
+#ifdef AEON_HUFF_PROBE
+    if (tid == 0) probe_k = 0;
+#endif
+    HUFF_STAMP("enter", F.data_words);
     huff::tables_codes(T, F, tid, LANES);
     if (tid == 0) X.carry = make_int4(0, 0, 0, 0);
     __syncthreads();
+    HUFF_STAMP("codes", 0);
     huff::tables_fast(T, F, tid, LANES);
+    huff::tables_long(T, F, tid, LANES);
     __syncthreads();
+    HUFF_STAMP("tables", staged);
     if (staged) decode_lanes<LANES>(T, X, L, F, (lds_words)stage, error);
     else if (F.nsub <= LANES) decode_lanes<LANES>(T, X, L, F, huff::gmem<const uint32_t>(F.data), error);
     else decode_strided<LANES>(T, X, F, error);
+#ifdef AEON_HUFF_PROBE
+    if (blockIdx.x == 0 && tid == 0)
+        for (int i = 1; i < probe_k; i++)
+            printf("huff %d %d %d\n", i, probe_n[i], (int)(probe_t[i] - probe_t[i - 1]));
+#endif
 }
 
 hipError_t launch_jpeg_huff(const JpegHuffFile* files, int n_files, int lanes, int stage_bytes, int32_t* error,

@@ -36,10 +36,15 @@ constexpr uint32_t kValue = 1u << 9, kEob = 2u << 9, kZrl = 3u << 9, kSym = 4u <
 constexpr int      kTabs = 6; // DC of frame components 0..2, then AC of 0..2
 constexpr int      kFast = 1 << kHuffFastBits;
 
+constexpr int kLongSub = 16; // second-level tables per DHT table: codes of 11..16 bits by the 6 bits after
+                             // their 10-bit prefix (canonical long codes share a few prefixes at the top)
+
 struct Tables {
     uint32_t fast[kTabs][kFast];
-    int32_t  maxcode[kTabs][17]; // largest code of each length (-1: none)
-    int32_t  delta[kTabs][17];   // index of its first symbol - its first code
+    uint16_t longt[kTabs][kLongSub * 64]; // (length << 8) | symbol; 0: no code
+    int32_t  long_first[kTabs];           // the first 10-bit prefix of a long code
+    int32_t  maxcode[kTabs][17];          // largest code of each length (-1: none)
+    int32_t  delta[kTabs][17];            // index of its first symbol - its first code
     uint8_t  vals[kTabs][256];
 };
 
@@ -70,7 +75,28 @@ HUFF_FN void tables_codes(Tables& T, const JpegHuffFile& F, int i0, int di)
             T.maxcode[t][l] = n ? code + n - 1 : -1;
             code = (code + n) << 1;
             s += n;
+            if (l == kHuffFastBits) T.long_first[t] = code >> 1; // the 10-bit prefixes short codes leave
         }
+    }
+}
+
+// Tables, part 3 (after part 1): the long-code subtables.
+HUFF_FN void tables_long(Tables& T, const JpegHuffFile& F, int i0, int di)
+{
+    for (int i = i0; i < kTabs * kLongSub * 64; i += di) {
+        const int t = i / (kLongSub * 64), r = i % (kLongSub * 64);
+        if (t % 3 >= F.ncomp) continue;
+        const int prefix = T.long_first[t] + r / 64;
+        uint16_t  e      = 0;
+        if (prefix < kFast)
+            for (int l = kHuffFastBits + 1; l <= 16; l++) {
+                const int code = ((prefix << 6) | (r % 64)) >> (16 - l);
+                if (code <= T.maxcode[t][l]) {
+                    e = (uint16_t)((l << 8) | T.vals[t][T.delta[t][l] + code]);
+                    break;
+                }
+            }
+        T.longt[t][r] = e;
     }
 }
 
@@ -188,23 +214,93 @@ struct Out {
     int trunc; // reading past the segment's data is an error
 };
 
-// Decode from state (b.p, c, k).  SYNC (!WRITE): up to the first codeword boundary at or past `stop`,
-// counting blocks started and DC differences per component in cnt.  WRITE: the same walk (the last
-// subsequence of a segment: until the segment's blocks are done) storing coefficients and masks.
-// Returns false on corrupt data (WRITE only).
-template <bool WRITE, typename B>
-HUFF_FN bool walk(const Tables& T, const JpegHuffFile& F, B& b, int& c, int& k, int stop, bool last, int4& cnt,
-                  Out& o)
+// A code longer than the lookahead (fast entry 0) as a fast-table entry: the second-level table, or
+// for prefixes beyond it the canonical maxcode walk.  *ok = false: no code of <= 16 bits (the entry
+// then stands for a 1-bit code of symbol 0, a fixed continuation for a guessed start).
+HUFF_FN uint32_t long_entry(const Tables& T, int t, uint64_t buf, bool& ok)
 {
-    const uint64_t tab_lo = F.blk_tab[0], tab_hi = F.blk_tab[1];
-    auto blk_byte = [&](int cc) { return (int)(((cc < 8 ? tab_lo : tab_hi) >> (8 * (cc & 7))) & 0xff); };
-    int       comp = blk_byte(c) & 3;
-    uint64_t  mask = 0;
+    const int sub = (int)(buf >> (64 - kHuffFastBits)) - T.long_first[t];
+    int       l = 0, sym = 0;
+    if (sub >= 0 && sub < kLongSub) {
+        const int e = T.longt[t][sub * 64 + (int)((buf >> (64 - kHuffFastBits - 6)) & 63)];
+        l = e >> 8, sym = e & 255;
+    } else {
+        for (int ll = kHuffFastBits + 1; ll <= 16; ll++) {
+            const int code = (int)(buf >> (64 - ll));
+            if (code <= T.maxcode[t][ll]) {
+                l = ll, sym = T.vals[t][T.delta[t][ll] + code];
+                break;
+            }
+        }
+    }
+    ok = l != 0;
+    if (!ok) l = 1, sym = 0;
+    if (t < 3) return kSym | (uint32_t)l | ((uint32_t)sym << 16);
+    if (!(sym & 15)) return ((sym >> 4) == 15 ? kZrl : kEob) | (uint32_t)l; // (jdhuff.c: size 0, run < 15 ends the block)
+    return kSym | (uint32_t)l | ((uint32_t)(sym >> 4) << 5) | ((uint32_t)(sym & 15) << 16);
+}
+
+HUFF_FN int blk_comp(const JpegHuffFile& F, int c)
+{
+    return (int)(((c < 8 ? F.blk_tab[0] : F.blk_tab[1]) >> (8 * (c & 7))) & 3);
+}
+
+// A sync walk from state (b.p, c, k) to the first codeword boundary at or past `stop`: blocks started
+// and DC differences per component into cnt.  Written for a wave's lanes to stay together: a codeword
+// is one fast-table lookup and a handful of selects; the only branches are the refill, a code longer
+// than the lookahead and a DC difference whose bits exceed it.  AC value bits are skipped, not
+// decoded.  (A guessed start can meet no-code bit patterns and DC sizes above 15: fixed continuations.)
+template <typename B>
+HUFF_FN void walk_sync(const Tables& T, const JpegHuffFile& F, B& b, int& c, int& k, int stop, int4& cnt)
+{
+    int comp = blk_comp(F, c);
+    while (b.p < stop) {
+        b.fill();
+        const int t = k == 0 ? comp : 3 + comp;
+        uint32_t  e = T.fast[t][(int)(b.buf >> (64 - kHuffFastBits))];
+        if (!(e & kKind)) {
+            bool ok;
+            e = long_entry(T, t, b.buf, ok);
+        }
+        const uint32_t kind = e & kKind;
+        const int      used = (int)(e & 31);
+        const int      z    = kind == kSym ? imin((int)((e >> 16) & 0xff), 15) : 0;
+        int            v    = kind == kValue ? (int)(int16_t)(e >> 16) : 0;
+        if (k == 0 && z) v = extend((int)((b.buf << used) >> (64 - z)), z);
+        b.skip(used + z);
+        if (k == 0) {
+            cnt.x++;
+            cnt.y += comp == 0 ? v : 0;
+            cnt.z += comp == 1 ? v : 0;
+            cnt.w += comp == 2 ? v : 0;
+            k = 1;
+        } else {
+            k += kind == kEob ? 64 : (kind == kZrl ? 16 : (int)((e >> 5) & 15) + 1);
+        }
+        if (k >= 64) {
+            k    = 0;
+            c    = c + 1 == F.bpm ? 0 : c + 1;
+            comp = blk_comp(F, c);
+        }
+    }
+}
+
+// The final walk from an exact state: every block's coefficients into its dense slots and its mask
+// (plain store for a block this walk starts and ends, OR-ed where another walk holds part of it);
+// up to the first codeword boundary at or past `stop`, or -- the segment's last subsequence -- until the
+// segment's blocks are done.  Returns false on corrupt data: no code of <= 16 bits, a DC size above
+// 15, bits past the end of a file whose data ends without a marker.
+template <typename B>
+HUFF_FN bool walk_write(const Tables& T, const JpegHuffFile& F, B& b, int& c, int& k, int stop, bool last, Out& o)
+{
+    int                   comp = blk_comp(F, c);
+    uint64_t              mask = 0;
     HUFF_GLOBAL int16_t*  coef = nullptr;
     HUFF_GLOBAL uint64_t* mrec = nullptr;
-    bool      own  = k == 0; // the current block started in this walk
-    auto open = [&]() {     // WRITE: locate the current block in its component plane
-        const int    bt = blk_byte(c), x = (bt >> 2) & 3, y = (bt >> 4) & 3;
+    bool                  own  = k == 0; // the current block started in this walk
+    auto open = [&]() {                  // locate the current block in its component plane
+        const int    bt = (int)(((c < 8 ? F.blk_tab[0] : F.blk_tab[1]) >> (8 * (c & 7))) & 0xff);
+        const int    x = (bt >> 2) & 3, y = (bt >> 4) & 3;
         const int    bw = comp == 0 ? F.bw[0] : (comp == 1 ? F.bw[1] : F.bw[2]);
         const int    hs = comp == 0 ? F.hs[0] : (comp == 1 ? F.hs[1] : F.hs[2]);
         const int    vs = comp == 0 ? F.vs[0] : (comp == 1 ? F.vs[1] : F.vs[2]);
@@ -212,101 +308,60 @@ HUFF_FN bool walk(const Tables& T, const JpegHuffFile& F, B& b, int& c, int& k, 
         coef = gmem<int16_t>(comp == 0 ? F.dvals[0] : (comp == 1 ? F.dvals[1] : F.dvals[2])) + idx * 64;
         mrec = gmem<uint64_t>(comp == 0 ? F.blocks[0] : (comp == 1 ? F.blocks[1] : F.blocks[2])) + idx * 2;
     };
-    if (WRITE && o.blk < o.blk_end) open();
-    for (;;) {
-        if (WRITE) {
-            if (o.blk >= o.blk_end || (!last && b.p >= stop)) break;
-        } else if (b.p >= stop) {
-            break;
-        }
+    if (o.blk < o.blk_end) open();
+    while (o.blk < o.blk_end && (last || b.p < stop)) {
         b.fill();
         const int t = k == 0 ? comp : 3 + comp;
         uint32_t  e = T.fast[t][(int)(b.buf >> (64 - kHuffFastBits))];
-        if (!(e & kKind)) { // a code longer than the lookahead
-            int l = kHuffFastBits + 1, sym = -1;
-            for (; l <= 16; l++) {
-                const int code = (int)(b.buf >> (64 - l));
-                if (code <= T.maxcode[t][l]) {
-                    sym = T.vals[t][T.delta[t][l] + code];
-                    break;
-                }
-            }
-            if (sym < 0) {
-                if (WRITE) return false;
-                sym = 0, l = 1; // a guessed start off the code boundaries: any fixed continuation
-            }
-            if (k == 0) e = kSym | (uint32_t)l | ((uint32_t)sym << 16);
-            else if (!(sym & 15)) e = ((sym >> 4) == 15 ? kZrl : kEob) | (uint32_t)l;
-            else e = kSym | (uint32_t)l | ((uint32_t)(sym >> 4) << 5) | ((uint32_t)(sym & 15) << 16);
+        if (!(e & kKind)) {
+            bool ok;
+            e = long_entry(T, t, b.buf, ok);
+            if (!ok) return false;
         }
         const uint32_t kind = e & kKind;
-        b.skip(e & 31);
-        int v = 0;
-        if (kind == kValue) {
-            v = (int)(int16_t)(e >> 16);
-        } else if (kind == kSym) {
-            int z = (int)(e >> 16);
-            if (z > 15) { // a DC size above 15 (the host decoder refuses it too)
-                if (WRITE) return false;
-                z = 15;
-            }
-            if (WRITE || k == 0) { // (a sync walk only skips AC value bits)
-                if (z) v = extend(b.get(z), z);
-            } else {
-                b.skip(z);
-            }
-        }
-        if (WRITE && o.trunc && b.p > b.end) return false; // past the end of the file's data
+        const int      used = (int)(e & 31);
+        const int      z    = kind == kSym ? (int)((e >> 16) & 0xff) : 0;
+        if (z > 15) return false; // (a DC size: the host decoder refuses it too)
+        int v = kind == kValue ? (int)(int16_t)(e >> 16) : 0;
+        if (z) v = extend((int)((b.buf << used) >> (64 - z)), z);
+        b.skip(used + z);
+        if (o.trunc && b.p > b.end) return false; // past the end of the file's data
         if (k == 0) { // DC difference
-            if (WRITE) {
-                const int pr = (comp == 0 ? o.pred0 : (comp == 1 ? o.pred1 : o.pred2)) + v;
-                if (comp == 0) o.pred0 = pr;
-                else if (comp == 1) o.pred1 = pr;
-                else o.pred2 = pr;
-                const int16_t dc = (int16_t)pr;
-                if (dc) {
-                    mask    = 1;
-                    coef[0] = dc;
-                }
-            } else {
-                cnt.x++;
-                if (comp == 0) cnt.y += v;
-                else if (comp == 1) cnt.z += v;
-                else cnt.w += v;
-            }
-            k = 1;
-        } else if (kind == kEob) {
-            k = 64;
-        } else if (kind == kZrl) {
-            k += 16;
+            const int pr = (comp == 0 ? o.pred0 : (comp == 1 ? o.pred1 : o.pred2)) + v;
+            o.pred0 = comp == 0 ? pr : o.pred0;
+            o.pred1 = comp == 1 ? pr : o.pred1;
+            o.pred2 = comp == 2 ? pr : o.pred2;
+            const int16_t dc = (int16_t)pr;
+            if (dc) coef[0] = dc;
+            mask = dc ? 1 : 0;
+            k    = 1;
+        } else if (kind == kEob || kind == kZrl) {
+            k += kind == kEob ? 64 : 16;
         } else {
-            k += (e >> 5) & 15;
-            if (WRITE) { // jpeg_natural_order's extra entries clamp a run past 63 to 63
-                const int z = imin(k, 63);
-                mask |= 1ull << z;
-                coef[z] = (int16_t)v;
-            }
+            k += (int)((e >> 5) & 15);
+            const int zz = imin(k, 63); // jpeg_natural_order's extra entries clamp a run past 63 to 63
+            mask |= 1ull << zz;
+            coef[zz] = (int16_t)v;
             k++;
         }
         if (k >= 64) { // block done
-            if (WRITE) {
-                if (own) mrec[0] = mask;
-                else if (mask) or_mask(mrec, mask);
-                mask = 0, own = true;
-                o.blk++;
-            }
+            if (own) mrec[0] = mask;
+            else if (mask) or_mask(mrec, mask);
+            mask = 0, own = true;
+            o.blk++;
             k = 0;
             if (++c == F.bpm) {
                 c = 0;
-                if (WRITE && ++o.mx == F.mcux) o.mx = 0, o.my++;
+                if (++o.mx == F.mcux) o.mx = 0, o.my++;
             }
-            comp = blk_byte(c) & 3;
-            if (WRITE && o.blk < o.blk_end) open();
+            comp = blk_comp(F, c);
+            if (o.blk < o.blk_end) open();
         }
     }
-    if (WRITE && k > 0 && mask) or_mask(mrec, mask); // a block split with the next subsequence
+    if (k > 0 && mask) or_mask(mrec, mask); // a block split with the next subsequence
     return true;
 }
+
 
 template <typename S>
 HUFF_FN void set_cnt(S& s, int4 v)
@@ -328,7 +383,6 @@ HUFF_FN void pass_guess(const Tables& T, const JpegHuffFile& F, SP subs, int j0,
 {
     const HUFF_GLOBAL JpegHuffSeg* segs = gmem<const JpegHuffSeg>(F.segs);
     const HUFF_GLOBAL int32_t*     sseg = gmem<const int32_t>(F.sub_seg);
-    Out                none{};
     for (int j = j0; j < F.nsub; j += dj) {
         const JpegHuffSeg S   = segs[sseg[j]];
         const int         i   = j - S.first_sub, p = (int)S.start_bit + i * F.sub_bits;
@@ -337,7 +391,7 @@ HUFF_FN void pass_guess(const Tables& T, const JpegHuffFile& F, SP subs, int j0,
         if (i + 1 < S.nsub) { // (the segment's last subsequence ends nobody's start)
             Bits b = bits_at(F, S, p);
             int  c = 0, k = 0;
-            walk<false>(T, F, b, c, k, p + F.sub_bits, false, cnt, none);
+            walk_sync(T, F, b, c, k, p + F.sub_bits, cnt);
             en = pack_state(b.p, c, k);
         }
         subs[j].st = pack_state(p, 0, 0);
@@ -372,7 +426,6 @@ HUFF_FN void pass_rewalk(const Tables& T, const JpegHuffFile& F, SP subs, int j0
 {
     const HUFF_GLOBAL JpegHuffSeg* segs = gmem<const JpegHuffSeg>(F.segs);
     const HUFF_GLOBAL int32_t*     sseg = gmem<const int32_t>(F.sub_seg);
-    Out                none{};
     for (int j = j0; j < F.nsub; j += dj) {
         if (!subs[j].ex[0]) continue;
         const JpegHuffSeg S  = segs[sseg[j]];
@@ -381,7 +434,7 @@ HUFF_FN void pass_rewalk(const Tables& T, const JpegHuffFile& F, SP subs, int j0
         int               c = (int)(st >> 32) & 0xff, k = (int)(st >> 40) & 0xff;
         int4              cnt = make_int4(0, 0, 0, 0);
         Bits              b   = bits_at(F, S, p);
-        walk<false>(T, F, b, c, k, stop, false, cnt, none);
+        walk_sync(T, F, b, c, k, stop, cnt);
         subs[j].en = pack_state(b.p, c, k);
         set_cnt(subs[j], cnt);
     }
@@ -411,9 +464,8 @@ HUFF_FN bool pass_write(const Tables& T, const JpegHuffFile& F, SP subs, int j0,
         if (o.blk < sg * per_seg) continue; // (a continuation with no block before it cannot be exact)
         const int mcu = o.blk / F.bpm;
         o.mx = mcu % F.mcux, o.my = mcu / F.mcux;
-        int4 cnt;
         Bits b = bits_at(F, S, (int)(uint32_t)st);
-        if (!walk<true>(T, F, b, c, k, (int)S.start_bit + (i + 1) * F.sub_bits, i + 1 == S.nsub, cnt, o)) ok = false;
+        if (!walk_write(T, F, b, c, k, (int)S.start_bit + (i + 1) * F.sub_bits, i + 1 == S.nsub, o)) ok = false;
     }
     return ok;
 }
