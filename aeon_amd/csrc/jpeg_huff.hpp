@@ -240,10 +240,13 @@ HUFF_FN uint32_t long_entry(const Tables& T, int t, uint64_t buf, bool& ok)
     return kSym | (uint32_t)l | ((uint32_t)(sym >> 4) << 5) | ((uint32_t)(sym & 15) << 16);
 }
 
-HUFF_FN int blk_comp(const JpegHuffFile& F, int c)
-{
-    return (int)(((c < 8 ? F.blk_tab[0] : F.blk_tab[1]) >> (8 * (c & 7))) & 3);
-}
+// The MCU's block table in registers (F lives in device memory: a lane-dependent index into it would
+// be a memory round trip at every block end).
+struct BlkTab {
+    uint64_t lo, hi;
+    HUFF_FN int byte(int c) const { return (int)(((c < 8 ? lo : hi) >> (8 * (c & 7))) & 0xff); }
+    HUFF_FN int comp(int c) const { return byte(c) & 3; }
+};
 
 // A sync walk from state (b.p, c, k) to the first codeword boundary at or past `stop`: blocks started
 // and DC differences per component into cnt.  Written for a wave's lanes to stay together: a codeword
@@ -253,7 +256,9 @@ HUFF_FN int blk_comp(const JpegHuffFile& F, int c)
 template <typename B>
 HUFF_FN void walk_sync(const Tables& T, const JpegHuffFile& F, B& b, int& c, int& k, int stop, int4& cnt)
 {
-    int comp = blk_comp(F, c);
+    const BlkTab bt{F.blk_tab[0], F.blk_tab[1]};
+    const int    bpm  = F.bpm;
+    int          comp = bt.comp(c);
     while (b.p < stop) {
         b.fill();
         const int t = k == 0 ? comp : 3 + comp;
@@ -279,8 +284,8 @@ HUFF_FN void walk_sync(const Tables& T, const JpegHuffFile& F, B& b, int& c, int
         }
         if (k >= 64) {
             k    = 0;
-            c    = c + 1 == F.bpm ? 0 : c + 1;
-            comp = blk_comp(F, c);
+            c    = c + 1 == bpm ? 0 : c + 1;
+            comp = bt.comp(c);
         }
     }
 }
@@ -293,17 +298,19 @@ HUFF_FN void walk_sync(const Tables& T, const JpegHuffFile& F, B& b, int& c, int
 template <typename B>
 HUFF_FN bool walk_write(const Tables& T, const JpegHuffFile& F, B& b, int& c, int& k, int stop, bool last, Out& o)
 {
-    int                   comp = blk_comp(F, c);
+    const BlkTab          bt{F.blk_tab[0], F.blk_tab[1]};
+    const int             bw0 = F.bw[0], bw1 = F.bw[1], bw2 = F.bw[2], hs0 = F.hs[0], hs1 = F.hs[1], hs2 = F.hs[2];
+    const int             vs0 = F.vs[0], vs1 = F.vs[1], vs2 = F.vs[2], bpm = F.bpm, mcux = F.mcux;
+    int                   comp = bt.comp(c);
     uint64_t              mask = 0;
     HUFF_GLOBAL int16_t*  coef = nullptr;
     HUFF_GLOBAL uint64_t* mrec = nullptr;
     bool                  own  = k == 0; // the current block started in this walk
     auto open = [&]() {                  // locate the current block in its component plane
-        const int    bt = (int)(((c < 8 ? F.blk_tab[0] : F.blk_tab[1]) >> (8 * (c & 7))) & 0xff);
-        const int    x = (bt >> 2) & 3, y = (bt >> 4) & 3;
-        const int    bw = comp == 0 ? F.bw[0] : (comp == 1 ? F.bw[1] : F.bw[2]);
-        const int    hs = comp == 0 ? F.hs[0] : (comp == 1 ? F.hs[1] : F.hs[2]);
-        const int    vs = comp == 0 ? F.vs[0] : (comp == 1 ? F.vs[1] : F.vs[2]);
+        const int    by = bt.byte(c), x = (by >> 2) & 3, y = (by >> 4) & 3;
+        const int    bw = comp == 0 ? bw0 : (comp == 1 ? bw1 : bw2);
+        const int    hs = comp == 0 ? hs0 : (comp == 1 ? hs1 : hs2);
+        const int    vs = comp == 0 ? vs0 : (comp == 1 ? vs1 : vs2);
         const size_t idx = (size_t)(o.my * vs + y) * bw + o.mx * hs + x;
         coef = gmem<int16_t>(comp == 0 ? F.dvals[0] : (comp == 1 ? F.dvals[1] : F.dvals[2])) + idx * 64;
         mrec = gmem<uint64_t>(comp == 0 ? F.blocks[0] : (comp == 1 ? F.blocks[1] : F.blocks[2])) + idx * 2;
@@ -350,11 +357,11 @@ HUFF_FN bool walk_write(const Tables& T, const JpegHuffFile& F, B& b, int& c, in
             mask = 0, own = true;
             o.blk++;
             k = 0;
-            if (++c == F.bpm) {
+            if (++c == bpm) {
                 c = 0;
-                if (++o.mx == F.mcux) o.mx = 0, o.my++;
+                if (++o.mx == mcux) o.mx = 0, o.my++;
             }
-            comp = blk_comp(F, c);
+            comp = bt.comp(c);
             if (o.blk < o.blk_end) open();
         }
     }
