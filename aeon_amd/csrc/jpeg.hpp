@@ -84,7 +84,11 @@ constexpr int kHuffSubMax   = 1024; // multiple of 32 in [min, max] nearest to s
 constexpr int kHuffLanes    = 1024; // jpeg_huff workgroup (one per file)
 constexpr int kHuffMaxBpm   = 16;   // blocks per MCU the GPU path takes (libjpeg allows 10)
 constexpr int kHuffFastBits = 10;   // lookahead of the LDS decode tables
-constexpr int kHuffStageMax = 92 * 1024; // a file's data up to this is copied into LDS for its walks
+#ifndef AEON_HUFF_PROBE
+constexpr int kHuffStageMax = 84 * 1024; // a file's data up to this is copied into LDS for its walks
+#else
+constexpr int kHuffStageMax = 80 * 1024; // (probe builds hold their stamps in LDS too)
+#endif
 
 // One DHT table as the file defines it (code lengths 1..16, then the symbols), validated on the host.
 struct JpegHuffTab {

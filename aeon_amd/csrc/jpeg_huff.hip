@@ -103,22 +103,27 @@ __device__ __forceinline__ void decode_strided(const huff::Tables& T, Scan& X, c
     if (!huff::pass_write(T, F, subs, tid, LANES)) atomicOr(error, kJpegCorruptBit);
 }
 
-// LDS of a file with at most LANES subsequences: each lane's end state and exclusive sums.
+// LDS of a file with at most LANES subsequences: each one's end state, walk bounds (stop, segment end)
+// and counts (exclusive sums after the prefix), and a round's list of subsequences to walk again.
 template <int LANES>
 struct LaneStates {
     uint64_t en[LANES];
+    uint2    se[LANES];
     int4     ex[LANES];
+    int      todo[LANES];
+    int      wave_n[LANES / 64];
 };
 
-// A file with at most one subsequence per lane (the common case): lane j owns subsequence j and keeps
-// its segment, start state and counts in registers across the phases; the end states (which the next
-// lane reads) and the exclusive sums (which the segment's lanes read) go through LDS.  The same
-// phases as jpeg_huff.hpp's pass_* functions, which the host emulation checks.
+// A file with at most one subsequence per lane (the common case): lane j owns subsequence j (its
+// segment and start state in registers) for the guessed start and the final decode.  A Jacobi round
+// compacts the subsequences whose start changed into the first lanes (wave ballots), so the walks of
+// a round occupy ceil(changed / 64) waves instead of every wave holding one.  The same phases as
+// jpeg_huff.hpp's pass_* functions, which the host emulation checks.
 template <int LANES, typename WP>
 __device__ __forceinline__ void decode_lanes(const huff::Tables& T, Scan& X, LaneStates<LANES>& L,
                                              const JpegHuffFile& F, WP words, int32_t* error)
 {
-    const int  tid = threadIdx.x, nsub = F.nsub;
+    const int  tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nsub = F.nsub;
     const bool have = tid < nsub;
     int        sg = 0, i = 0;
     JpegHuffSeg S{0, 0, 0, 1};
@@ -127,35 +132,57 @@ __device__ __forceinline__ void decode_lanes(const huff::Tables& T, Scan& X, Lan
         S  = huff::gmem<const JpegHuffSeg>(F.segs)[sg];
         i  = tid - S.first_sub;
     }
-    const bool     first = i == 0, last = i + 1 == S.nsub;
-    const int      p0    = (int)S.start_bit + i * F.sub_bits, stop = p0 + F.sub_bits;
-    uint64_t       st    = huff::pack_state(p0, 0, 0);
-    int4           cnt   = make_int4(0, 0, 0, 0);
-    auto walk_sync = [&]() {
-        int        c = (int)(st >> 32) & 0xff, k = (int)(st >> 40) & 0xff;
-        auto b = huff::bits_from(words, S, (int)(uint32_t)st);
-        cnt    = make_int4(0, 0, 0, 0);
-        huff::walk_sync(T, F, b, c, k, stop, cnt);
-        L.en[tid] = huff::pack_state(b.p, c, k);
-    };
+    const bool first = i == 0, last = i + 1 == S.nsub;
+    const int  p0    = (int)S.start_bit + i * F.sub_bits, stop = p0 + F.sub_bits;
+    uint64_t   st    = huff::pack_state(p0, 0, 0);
+    L.se[tid]        = make_uint2((uint32_t)stop, S.end_bit);
+    L.ex[tid]        = make_int4(0, 0, 0, 0);
     HUFF_STAMP("start", nsub);
+    // a walk of subsequence j from state s (bounds from L.se): its end state and counts into L
+    auto walk_sync = [&](int j, uint64_t s0) __attribute__((always_inline)) {
+        int              c = (int)(s0 >> 32) & 0xff, k = (int)(s0 >> 40) & 0xff;
+        const uint2      se = L.se[j];
+        const JpegHuffSeg Sj{0, se.y, 0, 0};
+        auto             b   = huff::bits_from(words, Sj, (int)(uint32_t)s0);
+        int4             cnt = make_int4(0, 0, 0, 0);
+        huff::walk_sync(T, F, b, c, k, (int)se.x, cnt);
+        L.en[j] = huff::pack_state(b.p, c, k);
+        L.ex[j] = cnt;
+    };
     // 1. the guessed start (the segment's last subsequence ends nobody's start)
-    if (have && !last) walk_sync();
+    if (have && !last) walk_sync(tid, st);
     // 2. Jacobi rounds
     for (int round = 0;; round++) {
         __syncthreads();
         HUFF_STAMP("round", round);
-        bool dirty = false;
+        bool changed = false;
         if (have && !first) {
             const uint64_t e = L.en[tid - 1];
-            if (e != st) st = e, dirty = true;
+            if (e != st) st = e, changed = true;
         }
-        if (!__syncthreads_or(dirty)) break;
-        if (dirty && !last) walk_sync();
+        const bool     dirty = changed && !last;
+        const uint64_t bal   = __ballot(dirty);
+        if (lane == 0) L.wave_n[wave] = __popcll(bal);
+        if (!__syncthreads_or(changed)) break;
+        int rank = __popcll(bal & ((1ull << lane) - 1)), total = 0;
+        for (int w = 0; w < LANES / 64; w++) {
+            const int n = L.wave_n[w];
+            rank += w < wave ? n : 0;
+            total += n;
+        }
+        if (dirty) L.todo[rank] = tid;
+        __syncthreads();
+        int      j  = 0;
+        uint64_t s0 = 0;
+        if (tid < total) j = L.todo[tid], s0 = L.en[j - 1]; // (every start read before any walk writes)
+        __syncthreads();
+        if (tid < total) walk_sync(j, s0);
     }
     // 3. exclusive prefix (one chunk: nsub <= LANES)
-    const int4 s = wg_scan<LANES>(X, cnt);
-    L.ex[tid]    = make_int4(s.x - cnt.x, s.y - cnt.y, s.z - cnt.z, s.w - cnt.w);
+    const int4 cnt = L.ex[tid];
+    const int4 s   = wg_scan<LANES>(X, cnt);
+    __syncthreads();
+    L.ex[tid] = make_int4(s.x - cnt.x, s.y - cnt.y, s.z - cnt.z, s.w - cnt.w);
     __syncthreads();
     HUFF_STAMP("scanned", 0);
     if (!have) return;

@@ -49,6 +49,13 @@ struct Tables {
 };
 
 HUFF_FN int imin(int a, int b) { return a < b ? a : b; }
+// v[comp] of three per-component values as arithmetic: a select chain over locals can become a
+// stack lookup table (scratch memory) on the device
+HUFF_FN int pick3(int comp, int a, int b, int c) { return a + (comp >= 1) * (b - a) + (comp >= 2) * (c - b); }
+HUFF_FN uint64_t pick3(int comp, uint64_t a, uint64_t b, uint64_t c)
+{
+    return a + (uint64_t)(comp >= 1) * (b - a) + (uint64_t)(comp >= 2) * (c - b);
+}
 HUFF_FN int extend(int v, int s) { return v < (1 << (s - 1)) ? v - (1 << s) + 1 : v; }
 
 HUFF_FN void or_mask(HUFF_GLOBAL uint64_t* m, uint64_t v)
@@ -301,6 +308,8 @@ HUFF_FN bool walk_write(const Tables& T, const JpegHuffFile& F, B& b, int& c, in
     const BlkTab          bt{F.blk_tab[0], F.blk_tab[1]};
     const int             bw0 = F.bw[0], bw1 = F.bw[1], bw2 = F.bw[2], hs0 = F.hs[0], hs1 = F.hs[1], hs2 = F.hs[2];
     const int             vs0 = F.vs[0], vs1 = F.vs[1], vs2 = F.vs[2], bpm = F.bpm, mcux = F.mcux;
+    const uint64_t        dv0 = F.dvals[0], dv1 = F.dvals[1], dv2 = F.dvals[2];
+    const uint64_t        bk0 = F.blocks[0], bk1 = F.blocks[1], bk2 = F.blocks[2];
     int                   comp = bt.comp(c);
     uint64_t              mask = 0;
     HUFF_GLOBAL int16_t*  coef = nullptr;
@@ -308,12 +317,10 @@ HUFF_FN bool walk_write(const Tables& T, const JpegHuffFile& F, B& b, int& c, in
     bool                  own  = k == 0; // the current block started in this walk
     auto open = [&]() {                  // locate the current block in its component plane
         const int    by = bt.byte(c), x = (by >> 2) & 3, y = (by >> 4) & 3;
-        const int    bw = comp == 0 ? bw0 : (comp == 1 ? bw1 : bw2);
-        const int    hs = comp == 0 ? hs0 : (comp == 1 ? hs1 : hs2);
-        const int    vs = comp == 0 ? vs0 : (comp == 1 ? vs1 : vs2);
+        const int    bw = pick3(comp, bw0, bw1, bw2), hs = pick3(comp, hs0, hs1, hs2), vs = pick3(comp, vs0, vs1, vs2);
         const size_t idx = (size_t)(o.my * vs + y) * bw + o.mx * hs + x;
-        coef = gmem<int16_t>(comp == 0 ? F.dvals[0] : (comp == 1 ? F.dvals[1] : F.dvals[2])) + idx * 64;
-        mrec = gmem<uint64_t>(comp == 0 ? F.blocks[0] : (comp == 1 ? F.blocks[1] : F.blocks[2])) + idx * 2;
+        coef = gmem<int16_t>(pick3(comp, dv0, dv1, dv2)) + idx * 64;
+        mrec = gmem<uint64_t>(pick3(comp, bk0, bk1, bk2)) + idx * 2;
     };
     if (o.blk < o.blk_end) open();
     while (o.blk < o.blk_end && (last || b.p < stop)) {
@@ -334,7 +341,7 @@ HUFF_FN bool walk_write(const Tables& T, const JpegHuffFile& F, B& b, int& c, in
         b.skip(used + z);
         if (o.trunc && b.p > b.end) return false; // past the end of the file's data
         if (k == 0) { // DC difference
-            const int pr = (comp == 0 ? o.pred0 : (comp == 1 ? o.pred1 : o.pred2)) + v;
+            const int pr = pick3(comp, o.pred0, o.pred1, o.pred2) + v;
             o.pred0 = comp == 0 ? pr : o.pred0;
             o.pred1 = comp == 1 ? pr : o.pred1;
             o.pred2 = comp == 2 ? pr : o.pred2;
