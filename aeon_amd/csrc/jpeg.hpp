@@ -84,6 +84,7 @@ constexpr int kHuffSubMax   = 1024; // multiple of 32 in [min, max] nearest to s
 constexpr int kHuffLanes    = 1024; // jpeg_huff workgroup (one per file)
 constexpr int kHuffMaxBpm   = 16;   // blocks per MCU the GPU path takes (libjpeg allows 10)
 constexpr int kHuffFastBits = 10;   // lookahead of the LDS decode tables
+constexpr int kHuffLeadBits = 512;  // a guessed walk starts this far before its subsequence (re-synchronising)
 #ifndef AEON_HUFF_PROBE
 constexpr int kHuffStageMax = 84 * 1024; // a file's data up to this is copied into LDS for its walks
 #else

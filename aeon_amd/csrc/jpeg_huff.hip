@@ -149,8 +149,13 @@ __device__ __forceinline__ void decode_lanes(const huff::Tables& T, Scan& X, Lan
         L.en[j] = huff::pack_state(b.p, c, k);
         L.ex[j] = cnt;
     };
-    // 1. the guessed start (the segment's last subsequence ends nobody's start)
-    if (have && !last) walk_sync(tid, st);
+    // 1. the guessed start, kHuffLeadBits ahead (the segment's last subsequence ends nobody's start)
+    if (have) {
+        int4     cnt;
+        uint64_t en;
+        huff::guess_walk(T, F, S, huff::bits_from(words, S, huff::guess_from(S, p0)), p0, !last, st, en, cnt);
+        if (!last) L.en[tid] = en, L.ex[tid] = cnt;
+    }
     // 2. Jacobi rounds
     for (int round = 0;; round++) {
         __syncthreads();

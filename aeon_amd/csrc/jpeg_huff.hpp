@@ -391,6 +391,30 @@ HUFF_FN int4 get_ex(const S& s)
 // The phases below take the file's subsequence states `subs` (F.subs in device memory, or an LDS
 // array when the file's subsequences fit the workgroup: on the device a pointer type of either
 // address space).
+// Where the guessed walk of the subsequence starting at bit p of segment S begins: kHuffLeadBits
+// earlier (its guess at a block start re-synchronises over the lead-in), the segment's start (exact)
+// when that is nearer.
+HUFF_FN int guess_from(const JpegHuffSeg& S, int p) { return p - kHuffLeadBits <= (int)S.start_bit ? (int)S.start_bit : p - kHuffLeadBits; }
+
+// The guessed walk: from guess_from (state block start), the state at the first codeword boundary at
+// or past p is the subsequence's start st; when `ends` (not the segment's last subsequence), on to its
+// end: en and the counts of its own bits.
+template <typename B>
+HUFF_FN void guess_walk(const Tables& T, const JpegHuffFile& F, const JpegHuffSeg& S, B b, int p, bool ends,
+                        uint64_t& st, uint64_t& en, int4& cnt)
+{
+    int  c = 0, k = 0;
+    int4 lead = make_int4(0, 0, 0, 0);
+    walk_sync(T, F, b, c, k, p, lead);
+    st  = pack_state(b.p, c, k);
+    cnt = make_int4(0, 0, 0, 0);
+    en  = 0;
+    if (ends) {
+        walk_sync(T, F, b, c, k, p + F.sub_bits, cnt);
+        en = pack_state(b.p, c, k);
+    }
+}
+
 // Phase 1: subsequences j0, j0 + dj, ... from their guessed starts.
 template <typename SP>
 HUFF_FN void pass_guess(const Tables& T, const JpegHuffFile& F, SP subs, int j0, int dj)
@@ -398,17 +422,12 @@ HUFF_FN void pass_guess(const Tables& T, const JpegHuffFile& F, SP subs, int j0,
     const HUFF_GLOBAL JpegHuffSeg* segs = gmem<const JpegHuffSeg>(F.segs);
     const HUFF_GLOBAL int32_t*     sseg = gmem<const int32_t>(F.sub_seg);
     for (int j = j0; j < F.nsub; j += dj) {
-        const JpegHuffSeg S   = segs[sseg[j]];
-        const int         i   = j - S.first_sub, p = (int)S.start_bit + i * F.sub_bits;
+        const JpegHuffSeg S = segs[sseg[j]];
+        const int         i = j - S.first_sub, p = (int)S.start_bit + i * F.sub_bits;
         int4              cnt = make_int4(0, 0, 0, 0);
-        uint64_t          en  = 0;
-        if (i + 1 < S.nsub) { // (the segment's last subsequence ends nobody's start)
-            Bits b = bits_at(F, S, p);
-            int  c = 0, k = 0;
-            walk_sync(T, F, b, c, k, p + F.sub_bits, cnt);
-            en = pack_state(b.p, c, k);
-        }
-        subs[j].st = pack_state(p, 0, 0);
+        uint64_t          st, en = 0;
+        guess_walk(T, F, S, bits_at(F, S, guess_from(S, p)), p, i + 1 < S.nsub, st, en, cnt);
+        subs[j].st = st;
         subs[j].en = en;
         set_cnt(subs[j], cnt);
     }
