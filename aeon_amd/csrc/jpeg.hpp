@@ -137,8 +137,6 @@ constexpr int kJpegIdctUnroll = 4;                               // blocks per l
 constexpr int kJpegIdctBlocks = kJpegIdctLanes / 8 * kJpegIdctUnroll; // blocks per IDCT workgroup (chunk)
 constexpr int kJpegRowsPerWg = 8;   // output rows per colour workgroup (fewer when the staged rows outgrow LDS)
 constexpr int kJpegColorLds  = 160 * 1024; // most LDS a colour workgroup stages
-constexpr int kJpegBandLds   = 32 * 1024;  // jpeg_bands: MCU rows per band (4, 2, 1) while the planes fit this,
-constexpr int kJpegBandMax   = 150 * 1024; // else one MCU row up to this; wider images: jpeg_idct + jpeg_color
 
 // jdsample.c's choice for a component (h / v expansion factors, dw samples per row): fancy
 // upsampling needs 3+ samples per row.

@@ -22,8 +22,8 @@
 #include "jpeg_huff.hpp"
 
 namespace aeon_hip {
-hipError_t launch_jpeg(const JpegImage* imgs, const JpegRows* bands, int n_bands, int band_lds, const JpegChunk* chunks,
-                       int n_chunks, const JpegRows* rows, int n_rows, int color_lds, hipStream_t stream);
+hipError_t launch_jpeg(const JpegImage* imgs, const JpegChunk* chunks, int n_chunks, const JpegRows* rows, int n_rows,
+                       int color_lds, hipStream_t stream);
 hipError_t launch_jpeg_huff(const JpegHuffFile* files, int n_files, int lanes, int stage_bytes, int32_t* error,
                             hipStream_t stream);
 
@@ -929,7 +929,6 @@ struct JpegState {
     int        next = 0;
     bool       gpu_huff = true; // false: every file through the host entropy decoder
     int        huff_lanes = kHuffLanes; // jpeg_huff workgroup size (AEON_HIP_JPEG_HUFF_LANES=256: A/B)
-    bool       bands = true; // AEON_HIP_JPEG_BANDS=0: every image through jpeg_idct + jpeg_color (A/B, tests)
     std::mutex mu;
 };
 
@@ -958,7 +957,6 @@ JpegState* jpeg_state_create(thread_pool* shared, bool gpu_huff)
     auto* s = new JpegState();
     s->gpu_huff = gpu_huff;
     if (const char* e = std::getenv("AEON_HIP_JPEG_HUFF_LANES")) s->huff_lanes = std::atoi(e) == 256 ? 256 : kHuffLanes;
-    if (const char* e = std::getenv("AEON_HIP_JPEG_BANDS")) s->bands = std::atoi(e) != 0;
     if (shared) {
         s->pool = shared;
     } else {
@@ -1026,10 +1024,10 @@ void jpeg_decode_batch(JpegState* S, int n, const void* const* data, const size_
     // work buffer (device only): [block records of the GPU-decoded files][their dense coefficients]
     // [their subsequence scratch]
     std::vector<JpegChunk> chunks;
-    std::vector<JpegRows>  rows, bands;
+    std::vector<JpegRows>  rows;
     size_t                 plane_bytes = 0;
     std::vector<size_t>    plane_off(3 * (size_t)n, 0);
-    int                    color_lds = 0, band_lds = 0, n_gpu = 0;
+    int                    color_lds = 0, n_gpu = 0;
     size_t                 rec_bytes = 0, coef_bytes = 0, sub_bytes = 0;
     std::vector<size_t>    wrec(3 * (size_t)n, 0), wcoef(3 * (size_t)n, 0), wsub(n, 0);
     for (int i = 0; i < n; i++) {
@@ -1044,31 +1042,6 @@ void jpeg_decode_batch(JpegState* S, int n, const void* const* data, const size_
             }
             wsub[i] = sub_bytes, sub_bytes += (size_t)gs[i].nsub * sizeof(JpegHuffSub);
         }
-        // the staged plane rows of a band of `rows` output rows (a bound: jpeg_stage_rows)
-        auto stage_lds = [&](int band_rows) {
-            int lds = 0;
-            for (int k = 0; k < nc; k++) {
-                const int hf = f.hmax / f.c[k].h, vf = f.vmax / f.c[k].v;
-                lds += jpeg_stage_rows(jpeg_upsample_mode(hf, vf, f.c[k].dw), vf, band_rows) * f.c[k].bw * 8;
-            }
-            return lds;
-        };
-        // jpeg_bands: whole MCU rows per band, as many as keep the planes within kJpegBandLds
-        const int mcu_rows = 8 * f.vmax;
-        int       per      = 0;
-        for (int r : {4, 2, 1})
-            if (stage_lds(r * mcu_rows) <= kJpegBandLds) {
-                per = r;
-                break;
-            }
-        if (!per && stage_lds(mcu_rows) <= kJpegBandMax) per = 1;
-        if (!S->bands) per = 0;
-        if (per) {
-            band_lds = std::max(band_lds, stage_lds(per * mcu_rows));
-            for (int y = 0; y < f.H; y += per * mcu_rows) bands.push_back({i, y, std::min(per * mcu_rows, f.H - y), 0});
-            continue;
-        }
-        // wider images: jpeg_idct into planes, then jpeg_color's bands
         for (int k = 0; k < nc; k++) {
             plane_off[3 * (size_t)i + k] = plane_bytes;
             plane_bytes += ((size_t)f.c[k].bw * 8 * f.c[k].bh * 8 + 255) & ~(size_t)255;
@@ -1091,8 +1064,7 @@ void jpeg_decode_batch(JpegState* S, int n, const void* const* data, const size_
     }
     const size_t img_bytes = (size_t)n * sizeof(JpegImage);
     const size_t huf_off   = (img_bytes + 255) & ~(size_t)255;
-    const size_t band_off  = huf_off + (((size_t)n_gpu * sizeof(JpegHuffFile) + 255) & ~(size_t)255);
-    const size_t chk_off   = band_off + ((bands.size() * sizeof(JpegRows) + 255) & ~(size_t)255);
+    const size_t chk_off   = huf_off + (((size_t)n_gpu * sizeof(JpegHuffFile) + 255) & ~(size_t)255);
     const size_t row_off   = chk_off + ((chunks.size() * sizeof(JpegChunk) + 255) & ~(size_t)255);
     size_t       total     = row_off + ((rows.size() * sizeof(JpegRows) + 255) & ~(size_t)255);
     std::vector<size_t> arena_off(S->arenas.size());
@@ -1157,7 +1129,6 @@ void jpeg_decode_batch(JpegState* S, int n, const void* const* data, const size_
         H.data_words = g.data_words;
         if (g.data_words * 4 <= kHuffStageMax) huff_stage = std::max(huff_stage, g.data_words * 4);
     }
-    if (!bands.empty()) std::memcpy(st.pinned + band_off, bands.data(), bands.size() * sizeof(JpegRows));
     if (!chunks.empty()) std::memcpy(st.pinned + chk_off, chunks.data(), chunks.size() * sizeof(JpegChunk));
     if (!rows.empty()) std::memcpy(st.pinned + row_off, rows.data(), rows.size() * sizeof(JpegRows));
     S->pool->run((int)S->arenas.size(), [&](int w) {
@@ -1169,9 +1140,8 @@ void jpeg_decode_batch(JpegState* S, int n, const void* const* data, const size_
     if (n_gpu)
         hip_ok(launch_jpeg_huff((const JpegHuffFile*)(st.dev + huf_off), n_gpu, S->huff_lanes, huff_stage, error, stream),
                "JPEG Huffman kernel");
-    hip_ok(launch_jpeg((const JpegImage*)st.dev, (const JpegRows*)(st.dev + band_off), (int)bands.size(), band_lds,
-                       (const JpegChunk*)(st.dev + chk_off), (int)chunks.size(), (const JpegRows*)(st.dev + row_off),
-                       (int)rows.size(), color_lds, stream),
+    hip_ok(launch_jpeg((const JpegImage*)st.dev, (const JpegChunk*)(st.dev + chk_off), (int)chunks.size(),
+                       (const JpegRows*)(st.dev + row_off), (int)rows.size(), color_lds, stream),
            "JPEG kernels");
     if (stop) hip_ok(hipEventRecord(stop, stream), "hipEventRecord");
     hip_ok(hipEventRecord(st.done, stream), "hipEventRecord");

@@ -6,8 +6,6 @@
 // jpeg_idct_islow (LL&M, CONST_BITS 13, PASS1_BITS 2; the post-IDCT range limit of jdmaster.c,
 // x & 1023 wrap) -- integer multiply-adds only -- a column each, then a row each, and each lane
 // writes its output row of the block into the component plane (one 8-byte store).
-// jpeg_bands (round 4) runs both in one workgroup per band of MCU rows, the planes in LDS; jpeg_idct +
-// jpeg_color remain for images whose bands outgrow the LDS.
 // jpeg_color: one lane per 4 output pixels of each of kJpegRowsPerWg rows: each component sampled
 // through jdsample.c's upsampler (h2v1 / h1v2 / h2v2 fancy triangle filters, context rows
 // replicated at the edges as jdmainct.c does; box replication for the other ratios and for
@@ -252,8 +250,7 @@ __device__ __forceinline__ void color_rows(const JpegImage& I, const CompView* c
 }
 
 // A workgroup per band of output rows: the plane rows the band's upsampling reads are copied into
-// LDS with coalesced 8-byte loads (jpeg_stage_rows bounds them), then color_rows.  (Images too wide
-// for jpeg_bands' LDS.)
+// LDS with coalesced 8-byte loads (jpeg_stage_rows bounds them), then color_rows.
 __global__ __launch_bounds__(256) void jpeg_color(const JpegImage* __restrict__ imgs, const JpegRows* __restrict__ rows)
 {
     extern __shared__ uint8_t lds_b[];
@@ -281,116 +278,9 @@ __global__ __launch_bounds__(256) void jpeg_color(const JpegImage* __restrict__ 
     color_rows(I, cv, R.y0, R.rows);
 }
 
-// The IDCT and the colour pass in one workgroup per band of whole MCU rows: every block of the block
-// rows that hold the band's component rows [lo, hi] (context rows included) goes through
-// jpeg_idct's arithmetic -- eight lanes per block, column pass, transpose through the group's LDS
-// slot, row pass -- and its rows inside [lo, hi] land in the component's LDS plane; then color_rows.
-// The planes never leave the chip (jpeg_idct + jpeg_color write them to HBM and read them back), and
-// the call is one launch.  A context block row above / below the band is transformed whole for the
-// one row the triangle filters read from it.
-__global__ __launch_bounds__(256) void jpeg_bands(const JpegImage* __restrict__ imgs, const JpegRows* __restrict__ rows)
+hipError_t launch_jpeg(const JpegImage* imgs, const JpegChunk* chunks, int n_chunks, const JpegRows* rows, int n_rows,
+                       int color_lds, hipStream_t stream)
 {
-    extern __shared__ uint8_t lds_b[];
-    __shared__ int   slot[32 * kSlot];
-    const JpegRows   R  = rows[blockIdx.x];
-    const JpegImage& I  = imgs[R.img];
-    const int        nc = I.out_cn == 1 ? 1 : I.ncomp;
-    const int        y1 = R.y0 + R.rows - 1;
-    const int        g = threadIdx.x >> 3, j = threadIdx.x & 7;
-    int*             s = slot + g * kSlot;
-    int              zz[8]; // zigzag index of (row r, column j), in registers: the wave fences below
-#pragma unroll              // would make the compiler reload the table for every block
-    for (int r = 0; r < 8; r++) zz[r] = kZzInv[r * 8 + j];
-    CompView         cv[3];
-    int              off = 0;
-#pragma unroll
-    for (int k = 0; k < 3; k++) {
-        if (k >= nc) break;
-        CompView& c = cv[k];
-        int       hi;
-        comp_rows(I, k, R.y0, y1, c, hi);
-        c.P                     = lds_b + off;
-        uint8_t*         plane  = lds_b + off;
-        const int        bw     = I.bw[k], br0 = c.lo >> 3, nblk = ((hi >> 3) - br0 + 1) * bw;
-        const gp<const JpegBlock> blocks = gaddr<const JpegBlock>(I.blocks[k]);
-        const gp<const int16_t>   dense  = gaddr<const int16_t>(I.dvals[k]);
-        const gp<const int16_t>   vals   = gaddr<const int16_t>(I.values);
-        int              qv[8];
-#pragma unroll
-        for (int r = 0; r < 8; r++) qv[r] = I.q[k][r * 8 + j];
-        // a GPU-decoded file's block b: its mask and column j's 8 slots, loaded unconditionally (the
-        // unmasked slots hold stale values, zeroed by the mask) one block ahead of the transform
-        auto fetch = [&](int b, uint64_t& m, int (&v)[8]) {
-            const size_t            idx = (size_t)(br0 + b / bw) * bw + b % bw;
-            const gp<const int16_t> bv  = dense + idx * 64;
-            m                           = blocks[idx].mask;
-#pragma unroll
-            for (int r = 0; r < 8; r++) v[r] = bv[zz[r]];
-        };
-        uint64_t nmask = 0;
-        int      nv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        if (dense && g < nblk) fetch(g, nmask, nv);
-        for (int b = g; b < nblk; b += 32) {
-            const int by = br0 + b / bw, bx = b % bw;
-            int       col[8], out[8], in[8];
-            if (dense) {
-                const uint64_t m = nmask;
-                int            v[8];
-#pragma unroll
-                for (int r = 0; r < 8; r++) v[r] = nv[r];
-                if (b + 32 < nblk) fetch(b + 32, nmask, nv);
-#pragma unroll
-                for (int r = 0; r < 8; r++) col[r] = (v[r] * qv[r]) & -(int)((m >> zz[r]) & 1);
-            } else {
-                const JpegBlock B = blocks[(size_t)by * bw + bx];
-#pragma unroll
-                for (int r = 0; r < 8; r++) {
-                    const int z = zz[r];
-                    col[r]      = (B.mask >> z) & 1
-                                      ? (int)vals[B.val_off + __builtin_popcountll(B.mask & ((1ull << z) - 1))] * qv[r]
-                                      : 0;
-                }
-            }
-            llm8<11, false>(col, out);
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier(); // the previous block's pass-2 reads are done
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-            for (int r = 0; r < 8; r++) s[r * 8 + j] = out[r];
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-            for (int cc = 0; cc < 8; cc++) in[cc] = s[j * 8 + cc];
-            llm8<18, true>(in, out);
-            const int y = by * 8 + j; // this lane's output row of the block
-            if (y >= c.lo && y <= hi) {
-                const uint32_t lo32 = idct_limit(out[0]) | idct_limit(out[1]) << 8 | idct_limit(out[2]) << 16 |
-                                      idct_limit(out[3]) << 24;
-                const uint32_t hi32 = idct_limit(out[4]) | idct_limit(out[5]) << 8 | idct_limit(out[6]) << 16 |
-                                      idct_limit(out[7]) << 24;
-                *(uint2*)(plane + (y - c.lo) * c.pw + bx * 8) = make_uint2(lo32, hi32);
-            }
-        }
-        off += (hi - c.lo + 1) * c.pw;
-    }
-    __syncthreads();
-    color_rows(I, cv, R.y0, R.rows);
-}
-
-// bands: jpeg_bands work items (LDS band_lds); chunks + rows: the IDCT / colour items of images too
-// wide for it (LDS color_lds).
-hipError_t launch_jpeg(const JpegImage* imgs, const JpegRows* bands, int n_bands, int band_lds, const JpegChunk* chunks,
-                       int n_chunks, const JpegRows* rows, int n_rows, int color_lds, hipStream_t stream)
-{
-    if (n_bands > 0) {
-        if (band_lds > 64 * 1024 - 32 * kSlot * 4) {
-            const hipError_t e = hipFuncSetAttribute((const void*)jpeg_bands, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                     band_lds);
-            if (e != hipSuccess) return e;
-        }
-        hipLaunchKernelGGL(jpeg_bands, dim3(n_bands), dim3(256), (size_t)band_lds, stream, imgs, bands);
-    }
     if (n_chunks > 0) hipLaunchKernelGGL(jpeg_idct, dim3(n_chunks), dim3(kJpegIdctLanes), 0, stream, imgs, chunks);
     if (n_rows > 0) {
         if (color_lds > 64 * 1024) {

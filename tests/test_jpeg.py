@@ -191,24 +191,3 @@ def test_gpu_huffman_corrupt_data_reported(ctx):
     good = [_jpg("s420_q50")]
     r = _decode_gpu(ctx, good, 3)
     assert np.array_equal(_sha(r[0]), FX["s420_q50.bgr"])
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("channels", [3, 1])
-def test_gpu_jpeg_bands_match_two_kernel_path(ctx, channels):
-    """jpeg_bands (IDCT and colour in one workgroup per band of MCU rows, planes in LDS) against
-    jpeg_idct + jpeg_color (AEON_HIP_JPEG_BANDS=0, the path of images too wide for the bands): every
-    fixture, both entropy paths, bit-identical records."""
-    import torch
-    assert torch.cuda.is_available()
-    os.environ["AEON_HIP_JPEG_BANDS"] = "0"
-    try:
-        two = A.Context(0)
-        files = [_jpg(n) for n in NAMES] * 2
-        b = _decode_gpu(two, files, channels)  # the JPEG state (and the flag) is made on the first call
-    finally:
-        del os.environ["AEON_HIP_JPEG_BANDS"]
-    two.close()
-    a = _decode_gpu(ctx, files, channels)
-    for i, (x, y) in enumerate(zip(a, b)):
-        assert np.array_equal(x, y), NAMES[i % len(NAMES)]

@@ -1,13 +1,11 @@
 #!/bin/bash
-# JPEG stage on the GPU box: the JPEG tests (GPU entropy decoder vs host, jpeg_bands vs the two-kernel
-# path, goldens, oracle), then tools/jpeg_stage.py A/B runs -> gpurun_out/jpeg_stage.json, and a
+# JPEG stage on the GPU box: the JPEG tests (GPU entropy decoder vs host, goldens, oracle), then tools/jpeg_stage.py A/B runs -> gpurun_out/jpeg_stage.json, and a
 # rocprofv3 kernel summary of the default stage -> gpurun_out/jpeg_prof.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"; mkdir -p gpurun_out; export TMPDIR=/tmp
 timeout -k 10 400 python -u -m pytest tests/test_jpeg.py -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/jpeg_tests.log 2>&1
 rc=$?; tail -24 gpurun_out/jpeg_tests.log; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 300 python tools/jpeg_stage.py gpu host > gpurun_out/jpeg_stage.json 2> gpurun_out/jpeg_stage.err || { tail -5 gpurun_out/jpeg_stage.err; exit 1; }
-AEON_HIP_JPEG_BANDS=0 timeout -k 10 200 python tools/jpeg_stage.py gpu >> gpurun_out/jpeg_stage.json 2>> gpurun_out/jpeg_stage.err || { tail -5 gpurun_out/jpeg_stage.err; exit 1; }
 AEON_HIP_JPEG_HUFF_LANES=256 timeout -k 10 200 python tools/jpeg_stage.py gpu >> gpurun_out/jpeg_stage.json 2>> gpurun_out/jpeg_stage.err || { tail -5 gpurun_out/jpeg_stage.err; exit 1; }
 python - <<'PY'
 import json
