@@ -22,7 +22,7 @@ prof() { # name, program...
 prof c2 python3 "$R/bench.py" --steps 100 --warmup 5 --no-cpu-baseline --no-extra || exit 1
 prof c3 python3 "$R/tools/kbench.py" C3 default || exit 1
 prof c5 python3 "$R/tools/c5_run.py" 30 || exit 1
-prof jpeg python3 "$R/tools/jpeg_ab.py" || exit 1
+prof jpeg python3 "$R/tools/jpeg_stage.py" gpu || exit 1
 for m in CUBIC AREA LANCZOS4; do prof c2_$m python3 "$R/tools/kbench.py" C2:$m default || exit 1; done
 echo "rocprof ok"
 cd "$R"
