@@ -17,6 +17,7 @@
 
 #include "../../include/aeon_hip.h"
 #include "aug_job.hpp"
+#include "host.hpp"
 #include "jpeg.hpp"
 #include "mask16.hpp"
 #include "json.hpp"
@@ -423,8 +424,8 @@ void lanczos4_coeffs(float x, float* c)
 }
 
 // Lanczos4 taps of destinations [d0, d0 + n) of an ssize -> dsize axis (x: the anchor clamped as
-// cv::resize does for columns; y: raw, the rows clipped per tap on use).
-void lanczos4_taps(int ssize, double scale, int d0, int n, bool clamp, std::vector<GrTap>& out)
+// cv::resize does for columns; y: raw, the rows clipped per tap on use), into out[0 .. n).
+void lanczos4_taps(int ssize, double scale, int d0, int n, bool clamp, GrTap* out)
 {
     for (int d = d0; d < d0 + n; d++) {
         float f = (float)((d + 0.5) * scale - 0.5);
@@ -437,7 +438,7 @@ void lanczos4_taps(int ssize, double scale, int d0, int n, bool clamp, std::vect
         GrTap t{};
         t.s = s;
         for (int k = 0; k < 8; k++) t.c[k] = (int16_t)std::min(std::max((int)std::rint(c[k] * 2048.f), -32768), 32767);
-        out.push_back(t);
+        out[d - d0] = t;
     }
 }
 
@@ -450,15 +451,29 @@ struct GrPlan {
     int TR = 16, CW = 128, NR = 1, xs = 3, amax = 1, cn_max = 1, max_tiles = 0;
     double bytes = 0; // algorithmic: the source region read once + the window written
 
+    size_t n_taps = 0; // Lanczos4 taps reserved by add(), computed by fill_taps()
+
     void add(ResizeJob R)
     {
-        if (R.method == GR_LANCZOS4) {
-            R.coef_x = (int32_t)(taps.size() * sizeof(GrTap)); // relative until the table is laid out
-            lanczos4_taps(R.crop_w, R.scale_x, R.win_x, R.win_w, true, taps);
-            R.coef_y = (int32_t)(taps.size() * sizeof(GrTap));
-            lanczos4_taps(R.crop_h, R.scale_y, R.win_y, R.win_h, false, taps);
+        if (R.method == GR_LANCZOS4) { // byte offsets, relative until the table is laid out
+            R.coef_x = (int32_t)(n_taps * sizeof(GrTap)), n_taps += R.win_w;
+            R.coef_y = (int32_t)(n_taps * sizeof(GrTap)), n_taps += R.win_h;
         }
         jobs.push_back(R);
+    }
+    // The Lanczos4 tap tables (a sin and a cos per destination column and row: ~18 us of libm per
+    // 224x224 record), on `pool` when there are enough jobs to pay for it.
+    void fill_taps(thread_pool* pool)
+    {
+        taps.resize(n_taps);
+        auto one = [&](int i) {
+            const ResizeJob& R = jobs[i];
+            if (R.method != GR_LANCZOS4) return;
+            lanczos4_taps(R.crop_w, R.scale_x, R.win_x, R.win_w, true, taps.data() + R.coef_x / sizeof(GrTap));
+            lanczos4_taps(R.crop_h, R.scale_y, R.win_y, R.win_h, false, taps.data() + R.coef_y / sizeof(GrTap));
+        };
+        if (pool && n_taps > 4096) pool->run((int)jobs.size(), one);
+        else for (int i = 0; i < (int)jobs.size(); i++) one(i);
     }
     // rows of H a tile of `tr` output rows needs at most
     int rows_for(int tr) const
@@ -729,6 +744,7 @@ struct aeon_hip_ctx {
     std::vector<JobGeom> geoms;              // reused per call
     JpegState*           jpeg = nullptr;     // JPEG decode stage (pool, staging ring), on first use
     thread_pool*         host_pool = nullptr; // the owning decoder's pool (ctx_share_pool), for the JPEG stage
+    std::unique_ptr<thread_pool> plan_pool;        // the context's own, made for the first call with many Lanczos4 taps
     std::vector<int> open_slots; // used since the last completion event, on open_stream
     hipStream_t      open_stream = nullptr;
     // job tables go up on their own stream, so a call's H2D overlaps the previous call's kernels
@@ -1265,6 +1281,8 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
     size_t           blob      = exp_off + exp.size() * sizeof(ExpandJob);
     for (GrPlan* g : {&gr_short, &gr_main}) { // jobs, then their Lanczos taps (offsets made absolute)
         if (g->jobs.empty()) continue;
+        if (g->n_taps > 4096 && !ctx->plan_pool) ctx->plan_pool.reset(new thread_pool(thread_affinity_map("")));
+        g->fill_taps(ctx->plan_pool.get());
         g->finalize();
         blob        = (blob + 15) & ~(size_t)15;
         g->off      = blob;
