@@ -180,6 +180,16 @@ struct BitsT {
             raw = load(++nw);
         }
     }
+    // the same without a branch, for words in LDS: a word is read at every codeword (the same one
+    // again when no refill was due)
+    HUFF_FN void fill_always()
+    {
+        const bool need = n < 32;
+        buf |= need ? (uint64_t)fix(raw, nw) << ((32 - n) & 63) : 0;
+        n += need ? 32 : 0;
+        nw += need ? 1 : 0;
+        raw = load(nw);
+    }
     HUFF_FN void skip(int l)
     {
         buf <<= l;
@@ -195,6 +205,17 @@ struct BitsT {
 };
 
 using Bits = BitsT<const HUFF_GLOBAL uint32_t*>;
+
+// Whether a walk's words are in device memory (a refill's load is kept a branch and loaded ahead)
+// or in LDS (fill_always).
+template <typename WP>
+struct WordsInMemory {
+    static constexpr bool value = false;
+};
+template <>
+struct WordsInMemory<const HUFF_GLOBAL uint32_t*> {
+    static constexpr bool value = true;
+};
 
 template <typename WP>
 HUFF_FN BitsT<WP> bits_from(WP w, const JpegHuffSeg& S, int pos)
@@ -267,33 +288,35 @@ HUFF_FN void walk_sync(const Tables& T, const JpegHuffFile& F, B& b, int& c, int
     const int    bpm  = F.bpm;
     int          comp = bt.comp(c);
     while (b.p < stop) {
-        b.fill();
+        if constexpr (WordsInMemory<decltype(b.w)>::value) b.fill();
+        else b.fill_always();
         const int t = k == 0 ? comp : 3 + comp;
         uint32_t  e = T.fast[t][(int)(b.buf >> (64 - kHuffFastBits))];
         if (!(e & kKind)) {
             bool ok;
             e = long_entry(T, t, b.buf, ok);
         }
+        // the rest as selects: a wave's lanes take different kinds of codeword every time
         const uint32_t kind = e & kKind;
         const int      used = (int)(e & 31);
         const int      z    = kind == kSym ? imin((int)((e >> 16) & 0xff), 15) : 0;
-        int            v    = kind == kValue ? (int)(int16_t)(e >> 16) : 0;
-        if (k == 0 && z) v = extend((int)((b.buf << used) >> (64 - z)), z);
+        const int      zz   = z > 0 ? z : 1;
+        const int      bits = (int)((b.buf << used) >> (64 - zz));
+        const int      ext  = bits < (1 << (zz - 1)) ? bits - (1 << zz) + 1 : bits;
+        const int      v    = kind == kValue ? (int)(int16_t)(e >> 16) : (z ? ext : 0); // (a DC difference)
         b.skip(used + z);
-        if (k == 0) {
-            cnt.x++;
-            cnt.y += comp == 0 ? v : 0;
-            cnt.z += comp == 1 ? v : 0;
-            cnt.w += comp == 2 ? v : 0;
-            k = 1;
-        } else {
-            k += kind == kEob ? 64 : (kind == kZrl ? 16 : (int)((e >> 5) & 15) + 1);
-        }
-        if (k >= 64) {
-            k    = 0;
-            c    = c + 1 == bpm ? 0 : c + 1;
-            comp = bt.comp(c);
-        }
+        const bool dc = k == 0;
+        const int  vd = dc ? v : 0;
+        cnt.x += dc ? 1 : 0;
+        cnt.y += comp == 0 ? vd : 0;
+        cnt.z += comp == 1 ? vd : 0;
+        cnt.w += comp == 2 ? vd : 0;
+        const int dk = kind == kEob ? 64 : (kind == kZrl ? 16 : (int)((e >> 5) & 15) + 1);
+        k            = dc ? 1 : k + dk;
+        const bool end = k >= 64;
+        k              = end ? 0 : k;
+        c              = end ? (c + 1 == bpm ? 0 : c + 1) : c;
+        comp           = bt.comp(c);
     }
 }
 
