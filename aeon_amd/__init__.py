@@ -116,6 +116,9 @@ def lib():
         L.aeon_hip_ctx_destroy.argtypes = [vp]
         for fn in (L.aeon_hip_augment_batch, L.aeon_hip_mask_batch, L.aeon_hip_depthmap_batch):
             fn.argtypes = [vp, ctypes.c_int, P(ImgDesc), vp, P(AugParams), P(OutDesc), vp, vp]
+        if hasattr(L, "aeon_hip_augment_pair_batch"):  # absent only in older tuning-variant builds
+            L.aeon_hip_augment_pair_batch.argtypes = [vp, ctypes.c_int, P(ImgDesc), vp, P(ImgDesc), vp, P(AugParams),
+                                                      P(OutDesc), vp, P(OutDesc), vp, vp]
         L.aeon_hip_synchronize.argtypes = [vp, vp]
         if hasattr(L, "aeon_hip_transpose_batch"):  # absent only in older tuning-variant builds
             L.aeon_hip_transpose_batch.argtypes = [vp, vp, vp, ctypes.c_int64, ctypes.c_int64, ctypes.c_int, vp]
@@ -373,6 +376,20 @@ class Context:
     def mask_batch(self, descs, src_ptr, params, out, out_ptr, stream=0):
         """pixel_mask transform + load for len(descs) records (async on stream)."""
         self._batch(lib().aeon_hip_mask_batch, descs, src_ptr, params, out, out_ptr, stream)
+
+    def pair_batch(self, descs, src_ptr, mask_descs, mask_src_ptr, params, out, out_ptr, mask_out, mask_out_ptr,
+                   stream=0):
+        """provider::image + provider::pixelmask of the same records, one params set per record
+        (aeon_hip_augment_pair_batch: one launch for 8-bit unrotated masks into uint8 items)."""
+        n = len(descs)
+        d = descs if isinstance(descs, ctypes.Array) else (ImgDesc * n)(*descs)
+        md = mask_descs if isinstance(mask_descs, ctypes.Array) else (ImgDesc * n)(*mask_descs)
+        p = params if isinstance(params, ctypes.Array) else (AugParams * n)(*params)
+        if len(md) < n or len(p) < n:
+            raise ValueError(f"{len(md)} masks / {len(p)} params for {n} records")
+        _check(lib().aeon_hip_augment_pair_batch(self._h, n, d, ctypes.c_void_p(src_ptr), md, ctypes.c_void_p(mask_src_ptr),
+                                                 p, ctypes.byref(out), ctypes.c_void_p(out_ptr), ctypes.byref(mask_out),
+                                                 ctypes.c_void_p(mask_out_ptr), ctypes.c_void_p(stream or 0)))
 
     def depthmap_batch(self, descs, src_ptr, params, out, out_ptr, stream=0):
         """depthmap transform + load (aeon src/etl_depthmap.cpp) for len(descs) records."""

@@ -157,6 +157,14 @@ struct LaunchArgs {
     uint32_t*      tail_ctr;   // non-null: the partial last round of tiles is handed out by this counter
                                // (zero on entry; the launch's last draw resets it)
     int32_t        tail_rounds; // ... and this many full rounds before it
+    // image + mask calls (aeon_hip_augment_pair_batch): the masks' NEAREST row blocks, which the
+    // launch's workgroups draw from m_ctr after their tiles (mask16_device.hpp; 0 blocks: none)
+    const struct Mask16Job* mjobs;
+    uint32_t*      m_ctr;      // zero on entry; the launch's last draw resets it
+    int32_t        m_blocks;   // m_jobs x m_bpj row blocks
+    int32_t        m_bpj;      // row blocks per mask (m_rows output rows each)
+    int32_t        m_rows, m_pitch, m_perm, m_slots; // nearest_staged's geometry (launch_nearest)
+    int32_t        m_lds;      // LDS byte offset of the blocks' row map, job and staged rows
     double         smean[3], sinv[3]; // sinv = 1/stddev, or 0 for stddev 0 (no division)
 };
 

@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 
 #include "augment_device.hpp"
+#include "mask16_device.hpp"
 
 namespace aeon_hip {
 
@@ -539,8 +540,143 @@ constexpr int kMinWaves = (KM == KM_STATS && PHOTO && !TAIL) ? AEON_HIP_STATS_MI
                           : (KM == KM_FINAL && RM == RESIZE_COPY && PHOTO) ? AEON_HIP_PASS2_MIN_WAVES
                                                                           : AEON_HIP_MIN_WAVES;
 
-template <int KM, int RM, bool PHOTO, int OF, bool TAIL>
-__global__ __launch_bounds__(kBlockMax) __attribute__((amdgpu_waves_per_eu(kMinWaves<KM, RM, PHOTO, OF, TAIL>)))
+// An image + mask call in one launch: after its last tile, every workgroup draws the masks' NEAREST
+// row blocks (nearest_staged's work: row map, source-row copy, gather; mask16_device.hpp) from a
+// counter until it runs dry -- exactly m_blocks + G draws, the last of which resets the counter -- so
+// the masks fill the image tiles' ragged end instead of a launch of their own.  8-bit masks to uint8
+// outputs (the host's condition).  Written lean (job fields uniform, 16 output columns per lane as 8
+// VGPRs of perm selectors or packed columns) so that the form keeps the tile kernel's occupancy.  LDS
+// from a.m_lds: the row map, the block's job, the draw word, then the staged rows (m_slots x m_pitch
+// bytes); the tiles' staging buffer is free by then.
+__device__ __forceinline__ uint32_t lds_word_u(const char* p) { return __builtin_amdgcn_readfirstlane(*(const uint32_t*)p); }
+
+__device__ __forceinline__ void mask_gather_u8(const Mask16Job& J, const RowMap& M, int pitch, const uint8_t* lds, bool perm_ok)
+{
+    constexpr int C   = 16; // output columns per lane
+    const int     tid = threadIdx.x;
+    const int     ng  = (J.out_w + C - 1) / C;
+    const int     per = min(ng, (int)blockDim.x), rstep = blockDim.x / per, r0 = tid / per;
+    if (r0 >= rstep) return;
+    const uint32_t* lds32 = (const uint32_t*)lds;
+    auto col = [&](int x) { // source column of output column x (cv::flip after the resize)
+        const int dx = J.flip ? J.out_w - 1 - x : x;
+        return min((int)floor(dx * J.scale_x), J.crop_w - 1);
+    };
+    for (int g = tid % per; g < ng; g += per) {
+        const int x0 = g * C;
+        const int nk = min(C, J.out_w - x0);
+        int       lo[4];
+        uint32_t  rel[4];
+        bool      ok = perm_ok && nk == C && ((J.out_ptr + (size_t)M.y0 * J.out_pitch + x0) & 15) == 0 && (J.out_pitch & 15) == 0;
+#pragma unroll
+        for (int w = 0; w < 4; w++) {
+            int c[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) c[k] = col(min(x0 + 4 * w + k, J.out_w - 1));
+            lo[w]  = min(c[0], c[3]); // ascending, or descending when flipped
+            ok     = ok && max(c[0], c[3]) - lo[w] <= 4;
+            rel[w] = 0;
+#pragma unroll
+            for (int k = 0; k < 4; k++) rel[w] |= (uint32_t)(c[k] - lo[w]) << (8 * k); // (fallback: <= 255 apart)
+        }
+        if (ok) { // every 4 outputs from 5 consecutive staged bytes: one read pair + one v_perm_b32
+            for (int r = r0; r < M.nrows; r += rstep) {
+                const int s    = M.slot[r];
+                const int rowb = s * pitch + (int)(seg_start(J, M, s) & 15);
+                u32x4     q;
+#pragma unroll
+                for (int w = 0; w < 4; w++) {
+                    const int      at  = rowb + lo[w];
+                    const uint32_t sel = rel[w] + (uint32_t)(at & 3) * 0x01010101u;
+                    q[w]               = __builtin_amdgcn_perm(lds32[(at >> 2) + 1], lds32[at >> 2], sel);
+                }
+                __builtin_nontemporal_store(q, gptr<u32x4>(J.out_ptr + (size_t)(M.y0 + r) * J.out_pitch + x0));
+            }
+            continue;
+        }
+        // otherwise element by element (downscales beyond 4/3 across, unaligned rows, the last group)
+        for (int r = r0; r < M.nrows; r += rstep) {
+            const int      s    = M.slot[r];
+            const uint8_t* base = lds + s * pitch + (int)(seg_start(J, M, s) & 15);
+            const uint64_t dst  = J.out_ptr + (size_t)(M.y0 + r) * J.out_pitch + x0;
+            for (int k = 0; k < nk; k++) gptr<uint8_t>(dst)[k] = base[col(x0 + k)];
+        }
+    }
+}
+
+// Schedule: workgroup b's first block is block b (its job words loaded at kernel entry, `jw`), the
+// rest are drawn from the counter (blocks G + c); the next block's draw and job load are issued before
+// this block's gather, so neither latency is on the block chain.  A launch with more blocks than
+// workgroups draws exactly (blocks - G) + G times (every workgroup ends on one failing draw; the last
+// draw resets the counter); with fewer, none.
+#ifndef AEON_HIP_MASK_LOADS // 16-byte row loads in flight per lane (the tile kernel's VGPR budget)
+#define AEON_HIP_MASK_LOADS 4
+#endif
+__device__ __forceinline__ uint32_t mask_job_word(const LaunchArgs& a, int k)
+{
+    const int tid = threadIdx.x;
+    if (k < 0 || tid >= (int)(sizeof(Mask16Job) / 4)) return 0;
+    return gptr<const uint32_t>((uint64_t)(a.mjobs + k / a.m_bpj))[tid];
+}
+
+__device__ __forceinline__ void mask_blocks(const LaunchArgs& a, char* smem, uint32_t jw)
+{
+    constexpr int kMapBytes = (int)((sizeof(RowMap) + 15) & ~(size_t)15);
+    constexpr int kJobBytes = (int)sizeof(Mask16Job);
+    static_assert(kJobBytes % 16 == 0 && kJobBytes / 4 <= 64, "Mask16Job: whole 16-byte units, one wave");
+    static_assert(kMapBytes + kJobBytes + 16 == kMaskBlockHdrBytes, "mask16.hpp's LDS header size");
+    RowMap&        M    = *reinterpret_cast<RowMap*>(smem + a.m_lds);
+    char*          jl   = smem + a.m_lds + kMapBytes;
+    uint32_t&      draw = *reinterpret_cast<uint32_t*>(smem + a.m_lds + kMapBytes + kJobBytes);
+    uint8_t*       rows = reinterpret_cast<uint8_t*>(smem + a.m_lds + kMapBytes + kJobBytes + 16);
+    const int      tid  = threadIdx.x;
+    const int      G    = gridDim.x;
+    const uint32_t D    = a.m_blocks > G ? (uint32_t)(a.m_blocks - G) : 0u; // drawn blocks
+    int            k    = (int)blockIdx.x < a.m_blocks ? (int)blockIdx.x : -1;
+    uint32_t       nraw = 0;
+    if (D && tid == 0) nraw = atomicAdd(a.m_ctr, 1u);
+    while (k >= 0) {
+        lds_barrier(); // (the tiles' staging buffer / the previous block's rows are free)
+        if (tid < kJobBytes / 4) reinterpret_cast<uint32_t*>(jl)[tid] = jw;
+        lds_barrier();
+        Mask16Job J; // uniform: scalar registers
+        {
+            uint32_t* w = reinterpret_cast<uint32_t*>(&J);
+#pragma unroll
+            for (int i = 0; i < kJobBytes / 4; i++) w[i] = lds_word_u(jl + 4 * i);
+        }
+        const int rec = k / a.m_bpj;
+        const int y0  = (k - rec * a.m_bpj) * a.m_rows;
+        const bool has = y0 < J.out_h; // (uniform: a mask shorter than the call's tallest has no block here)
+        if (has && tid < 64) map_rows(J, rec, y0, min(a.m_rows, J.out_h - y0), a.m_slots, M);
+        if (tid == 0) {
+            uint32_t c = ~0u;
+            if (D) {
+                c = nraw;
+                if (c == D + G - 1) atomicExch(a.m_ctr, 0u); // the launch's last draw
+                if (c > D + G - 1) atomicOr(a.error, 32);    // a counter left over by a launch
+            }
+            draw = c;
+        }
+        lds_barrier();
+        if (has) copy_rows<AEON_HIP_MASK_LOADS>(J, M, seg_blocks(J), a.m_pitch, rows);
+        lds_barrier();
+        // the next block: its draw and job load in flight during this block's gather
+        const uint32_t c  = __builtin_amdgcn_readfirstlane(draw);
+        const int      kn = c < D ? G + (int)c : -1;
+        if (kn >= 0) {
+            jw = mask_job_word(a, kn);
+            if (tid == 0) nraw = atomicAdd(a.m_ctr, 1u);
+        }
+        if (has) mask_gather_u8(J, M, a.m_pitch, rows, a.m_perm != 0);
+        k = kn;
+    }
+}
+
+// MASKS: the image + mask form (KM_FINAL only): the launch's masks' row blocks after the tiles
+template <int KM, int RM, bool PHOTO, int OF, bool TAIL, bool MASKS = false>
+__global__ __launch_bounds__(kBlockMax)
+__attribute__((amdgpu_waves_per_eu(kMinWaves<KM, RM, PHOTO, OF, TAIL>)))
 void augment_tiles(LaunchArgs a)
 {
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -562,6 +698,12 @@ void augment_tiles(LaunchArgs a)
         hsv_div_tables(L, a.hsv_tables);
     }
     if (KM == KM_FINAL && PHOTO && a.has_rtab) __syncthreads(); // record tables read the LUT
+#ifndef AEON_HIP_MASKS_FIRST
+#define AEON_HIP_MASKS_FIRST 0
+#endif
+    // an image + mask launch: the job of this workgroup's first mask block, loaded now
+    const uint32_t mjw = MASKS ? mask_job_word(a, (int)blockIdx.x < a.m_blocks ? (int)blockIdx.x : -1) : 0u;
+    if constexpr (MASKS && AEON_HIP_MASKS_FIRST) mask_blocks(a, smem, mjw);
     // development builds (-DAEON_HIP_TRACE, tools/trace_kernel.py): s_memtime stamps per (workgroup,
     // iteration, phase) when a.trace is set; s_memrealtime (chip-wide 100 MHz) at entry and exit.
     // The product library compiles them out.
@@ -670,6 +812,7 @@ void augment_tiles(LaunchArgs a)
             break;
         }
     }
+    if constexpr (MASKS && !AEON_HIP_MASKS_FIRST) mask_blocks(a, smem, mjw);
 #ifdef AEON_HIP_TRACE
     if (a.trace && tid == 0) a.trace[(blockIdx.x * 16 + 1) * 16 + 15] = (uint32_t)__builtin_amdgcn_s_memrealtime();
 #endif
@@ -710,8 +853,18 @@ __global__ __launch_bounds__(64) void contrast_reduce(LaunchArgs a, int n_jobs)
 typedef void (*KernelFn)(LaunchArgs);
 
 template <int KM, int RM, bool TAIL>
-KernelFn pick_form(bool photo, int of)
+KernelFn pick_form(bool photo, int of, bool masks)
 {
+    if (masks) { // image + mask launches: KM_FINAL
+        if constexpr (KM != KM_FINAL || RM == RESIZE_AREA2X) {
+            return nullptr;
+        } else {
+            if (of == OF_F32_CHW_VEC)
+                return photo ? augment_tiles<KM, RM, true, OF_F32_CHW_VEC, TAIL, true>
+                             : augment_tiles<KM, RM, false, OF_F32_CHW_VEC, TAIL, true>;
+            return photo ? augment_tiles<KM, RM, true, OF_GENERIC, TAIL, true> : augment_tiles<KM, RM, false, OF_GENERIC, TAIL, true>;
+        }
+    }
     if constexpr (RM == RESIZE_AREA2X) {
         // the planner splits 2x-area records with photometric stages into a resize-only pre-pass
         // and a copy pass, so these forms are never instantiated
@@ -727,22 +880,23 @@ KernelFn pick_form(bool photo, int of)
 }
 
 template <int KM>
-KernelFn pick_rm(int rm, bool tail, bool photo, int of)
+KernelFn pick_rm(int rm, bool tail, bool photo, int of, bool masks)
 {
     switch (rm) {
     case RESIZE_LINEAR:
-        return tail ? pick_form<KM, RESIZE_LINEAR, true>(photo, of) : pick_form<KM, RESIZE_LINEAR, false>(photo, of);
-    case RESIZE_AREA2X: return pick_form<KM, RESIZE_AREA2X, false>(photo, of);
-    case RESIZE_NEAREST: return pick_form<KM, RESIZE_NEAREST, false>(photo, of);
-    default: return pick_form<KM, RESIZE_COPY, false>(photo, of);
+        return tail ? pick_form<KM, RESIZE_LINEAR, true>(photo, of, masks) : pick_form<KM, RESIZE_LINEAR, false>(photo, of, masks);
+    case RESIZE_AREA2X: return pick_form<KM, RESIZE_AREA2X, false>(photo, of, masks);
+    case RESIZE_NEAREST: return pick_form<KM, RESIZE_NEAREST, false>(photo, of, masks);
+    default: return pick_form<KM, RESIZE_COPY, false>(photo, of, masks);
     }
 }
 
-KernelFn pick_kernel(int km, int rm, bool tail, bool photo, int of)
+KernelFn pick_kernel(int km, int rm, bool tail, bool photo, int of, bool masks = false)
 {
-    if (km == KM_FINAL) return pick_rm<KM_FINAL>(rm, tail, photo, of);
-    if (km == KM_STATS) return pick_rm<KM_STATS>(rm, tail, true, OF_GENERIC);
-    return pick_rm<KM_RAW>(rm, tail, false, OF_GENERIC);
+    if (km == KM_FINAL) return pick_rm<KM_FINAL>(rm, tail, photo, of, masks);
+    if (masks) return nullptr;
+    if (km == KM_STATS) return pick_rm<KM_STATS>(rm, tail, true, OF_GENERIC, false);
+    return pick_rm<KM_RAW>(rm, tail, false, OF_GENERIC, false);
 }
 
 int out_form(const LaunchArgs& a) { return (a.out_dtype == OUT_F32 && a.channel_major && a.vec_ok) ? OF_F32_CHW_VEC : OF_GENERIC; }
@@ -753,7 +907,7 @@ int out_form(const LaunchArgs& a) { return (a.out_dtype == OUT_F32 && a.channel_
 hipError_t launch_tiles(int km, int rm, bool tail, bool photo, const LaunchArgs& a, int grid, hipStream_t stream,
                         hipEvent_t start, hipEvent_t stop)
 {
-    const KernelFn fn = pick_kernel(km, rm, tail, photo, out_form(a));
+    const KernelFn fn = pick_kernel(km, rm, tail, photo, out_form(a), a.m_blocks > 0);
     if (!fn) return hipErrorInvalidDeviceFunction;
     if (start || stop) {
         void* args[1] = {(void*)&a};
@@ -772,7 +926,7 @@ hipError_t launch_contrast_reduce(const LaunchArgs& a, int n_jobs, hipStream_t s
 // Workgroups of this kernel form one CU holds at once (persistent grid sizing).
 hipError_t kernel_occupancy(int km, int rm, bool tail, bool photo, const LaunchArgs& a, int* blocks)
 {
-    const KernelFn fn = pick_kernel(km, rm, tail, photo, out_form(a));
+    const KernelFn fn = pick_kernel(km, rm, tail, photo, out_form(a), a.m_blocks > 0);
     if (!fn) return hipErrorInvalidDeviceFunction;
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, (const void*)fn, a.threads, a.lds_bytes);
 }
@@ -782,8 +936,8 @@ hipError_t set_kernel_lds_limit(int bytes)
     for (int km = 0; km < 3; km++)
         for (int rm = 0; rm < 4; rm++)
             for (int ph = 0; ph < 4; ph++)
-                for (int of = 0; of < 2; of++) {
-                    const KernelFn fn = pick_kernel(km, rm, (ph & 2) != 0, (ph & 1) != 0, of);
+                for (int of = 0; of < 4; of++) {
+                    const KernelFn fn = pick_kernel(km, rm, (ph & 2) != 0, (ph & 1) != 0, of & 1, of >= 2);
                     if (!fn) continue;
                     hipError_t e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
                     if (e != hipSuccess) return e;

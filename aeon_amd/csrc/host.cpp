@@ -375,6 +375,15 @@ void provider_base::stage(int idx, const decoded_element* elems, decode_window& 
 void provider_base::post_process(aeon_hip_ctx* ctx, decode_window& w, const uint8_t* dev_arena,
                                  void* const* outputs, void* stream) const
 {
+    // image + pixelmask with the same params per record (provider.cpp:365-393): one pair call, whose
+    // masks run inside the image launch
+    if (m_providers.size() == 2 && !m_providers[0]->is_mask() && m_providers[1]->is_mask() && w.n > 0 &&
+        std::memcmp(w.params[0].data(), w.params[1].data(), (size_t)w.n * sizeof(aeon_aug_params)) == 0) {
+        aeon_out_desc io = m_providers[0]->out_desc(), mo = m_providers[1]->out_desc();
+        check(aeon_hip_augment_pair_batch(ctx, w.n, w.descs[0].data(), dev_arena, w.descs[1].data(), dev_arena,
+                                          w.params[0].data(), &io, outputs[0], &mo, outputs[1], stream));
+        return;
+    }
     for (size_t k = 0; k < m_providers.size(); k++) {
         const etl_provider& p = *m_providers[k];
         aeon_out_desc       o = p.out_desc();

@@ -21,6 +21,10 @@ struct alignas(16) Mask16Job {
                                       // (the record's image::rotate pre-pass output)
 };
 
+// An image + mask launch (augment_kernels.hip mask_blocks): LDS bytes ahead of a row block's staged
+// rows -- the row map (336 B, 16-aligned), the block's job (80 B) and the draw word (16 B).
+constexpr int kMaskBlockHdrBytes = 336 + 80 + 16;
+
 // LDS-staged gather (nearest_staged) geometry, shared by the host and the launch: bytes per
 // staged source row (a 16-byte-aligned window around the crop segment) and output rows per
 // workgroup (up to 64 rows / ~32K output elements per workgroup, LDS <= 64 KB).

@@ -740,6 +740,7 @@ struct aeon_hip_ctx {
     // the jobs from the pinned slot itself
     bool                 direct = true; // AEON_HIP_DIRECT=0: the multi-pass path (device job table) for every call
     bool                 records = true; // AEON_HIP_RECORDS=0: contrast calls through the two-launch path
+    bool                 fuse_masks = false; // AEON_HIP_FUSE_MASKS=1: a pair call's masks inside the image launch
     bool                 jpeg_gpu_huff = true; // AEON_HIP_JPEG_HUFF=host: every JPEG through the host entropy decoder
     std::vector<JobGeom> geoms;              // reused per call
     JpegState*           jpeg = nullptr;     // JPEG decode stage (pool, staging ring), on first use
@@ -879,7 +880,7 @@ int grid_for(aeon_hip_ctx* ctx, int mode, const LaunchPlan& P, const LaunchArgs&
     int per_cu = 0;
     {
         const std::vector<int> key = {mode, P.rm, (int)P.tail, (int)P.photo, a.threads, a.lds_bytes, a.vec_ok, a.has_rtab,
-                                      a.out_dtype, a.channel_major};
+                                      a.out_dtype, a.channel_major, a.m_blocks > 0};
         for (auto& e : ctx->occ)
             if (e.first == key) per_cu = e.second;
         if (per_cu <= 0) {
@@ -1194,9 +1195,18 @@ bool run_records(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const voi
     return true;
 }
 
+// The masks of an image + mask call (aeon_hip_augment_pair_batch): 8-bit single-channel records
+// without rotation into uint8 items, sharing the images' params.
+struct MaskSet {
+    const aeon_img_desc* descs;
+    const void*          src_base;
+    aeon_out_desc        out;
+    void*                out_dev;
+};
+
 int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* src_base,
               const aeon_aug_params* params, const aeon_out_desc* out, void* out_dev, void* stream_,
-              bool is_mask)
+              bool is_mask, const MaskSet* ms = nullptr)
 {
     if (!ctx || n < 0 || (n > 0 && (!descs || !params || !out || !out_dev || !src_base)))
         fail(AEON_HIP_EINVAL, "null argument");
@@ -1235,10 +1245,10 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
     };
     HIP_OK(hipSetDevice(ctx->device));
     phase(0);
-    if (ctx->direct &&
-        run_direct(ctx, n, descs, src_base, params, od, out_dev, stream, is_mask, phase))
+    // (a pair call goes through the planner: its masks join the images' launch)
+    if (!ms && ctx->direct && run_direct(ctx, n, descs, src_base, params, od, out_dev, stream, is_mask, phase))
         return 0;
-    if (run_records(ctx, n, descs, src_base, params, od, out_dev, stream, is_mask, phase)) return 0;
+    if (!ms && run_records(ctx, n, descs, src_base, params, od, out_dev, stream, is_mask, phase)) return 0;
 
     LaunchPlan             pre_all, pre2_all, pass1_all, main_all;
     GrPlan                 gr_short, gr_main;
@@ -1258,6 +1268,9 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
                        pass1_all, main_all, scratch_bytes);
         else fail(AEON_HIP_EINVAL, "elem_bytes must be 1 (CV_8U) or 2 (CV_16U)");
     }
+    for (int i = 0; ms && i < n; i++) // the pair call's masks: the gather pass's jobs
+        plan_mask16(ms->descs[i], ms->src_base, params[i], ms->out, (uint8_t*)ms->out_dev + (size_t)i * ms->out.item_stride,
+                    true, m16, rot, scratch_bytes);
 
     phase(1);
     // one launch per (resize mode, photometric) group: the kernels are specialised on both
@@ -1390,6 +1403,19 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
     for (auto* v : {&pre, &pre2, &pass1, &main})
         for (LaunchPlan& P : *v) mask_only = mask_only && P.jobs.empty();
     const uint8_t* table = mask_only ? s.host_dev : s.dev;
+    // timing events on one call in timing_every (each event pair costs GPU time between launches)
+    const bool timed = ctx->timing && (ctx->timing_calls++ % ctx->timing_every) == ctx->timing_every - 1;
+    auto launch_masks = [&](const uint8_t* tbl) { // the gather pass, its jobs at tbl + m16_off
+        KernelTimer t{};
+        if (timed) t = take_timer(ctx, KM_FINAL, m16_bytes);
+        HIP_OK(launch_nearest((const Mask16Job*)(tbl + m16_off), (int)m16.size(), m16_max_h, m16_max_w, m16_max_seg,
+                              m16_max_slots, stream, timed ? t.start : nullptr, timed ? t.stop : nullptr));
+        if (timed) ctx->timers.push_back(t);
+    };
+    // (A pair call's tables go up together by the upload kernel, and its gather launch reads the device
+    // copy: C5 93-94 us per step against 96-98 for the image and mask calls, whose gather reads the
+    // pinned slot -- 4.5 us more kernel time -- and 97-98 for the masks first on the pinned slot while
+    // SDMA uploads the images' table; tools/c5_ab.sh)
     if (mask_only) {
     } else if (blob > kUploadKernelMax) {
         HIP_OK(hipMemcpyAsync(s.dev, s.host, blob, hipMemcpyHostToDevice, ctx->copy_stream));
@@ -1404,8 +1430,6 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
         return launch_args(ctx, s, table, L, (int)L.jobs.size(), o, d_lut, partial_stride, ov.u8_map);
     };
     const size_t oelem = out_elem_bytes(o.dtype);
-    // timing events on one call in timing_every (each event pair costs GPU time between launches)
-    const bool timed = ctx->timing && (ctx->timing_calls++ % ctx->timing_every) == ctx->timing_every - 1;
     if (o.fixed_aspect_ratio) // std::fill_n of each item's canvas, its whole byte size (etl_image.cpp:263)
         HIP_OK(hipMemset2DAsync(out_dev, o.item_stride, 0,
                                 (size_t)o.canvas_w * o.canvas_h * o.channels * out_elem_bytes(od.dtype), n, stream));
@@ -1414,14 +1438,40 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
                              stream));
     if (!exp.empty()) // then image::expand (etl_image.cpp:155-159)
         HIP_OK(launch_expand((const ExpandJob*)(table + exp_off), (int)exp.size(), exp_max_px, stream));
-    if (!m16.empty()) {
-        KernelTimer t{};
-        if (timed) t = take_timer(ctx, KM_FINAL, m16_bytes);
-        HIP_OK(launch_nearest((const Mask16Job*)(table + m16_off), (int)m16.size(), m16_max_h, m16_max_w, m16_max_seg,
-                              m16_max_slots, stream,
-                              timed ? t.start : nullptr, timed ? t.stop : nullptr));
-        if (timed) ctx->timers.push_back(t);
+    // A pair call whose images are one tile launch: the masks' row blocks go into that launch (its
+    // workgroups take them after their tiles, augment_kernels.hip mask_blocks) -- no gather launch.
+    LaunchPlan* fused = nullptr;
+    LaunchArgs  fused_masks{};
+    if (ms && ctx->fuse_masks && !m16.empty() && rot.empty() && exp.empty() && gr_short.jobs.empty() && gr_main.jobs.empty()) {
+        int groups = 0;
+        for (auto* v : {&pre, &pre2, &pass1, &main})
+            for (LaunchPlan& P : *v)
+                if (!P.jobs.empty()) groups++, fused = &P;
+#ifndef AEON_HIP_FUSED_MASK_ROWS
+#define AEON_HIP_FUSED_MASK_ROWS 64
+#endif
+        const int srows = std::min(mask16_rows(m16_max_w, m16_max_seg), AEON_HIP_FUSED_MASK_ROWS);
+        bool in_main = false;
+        for (LaunchPlan& P : main) in_main |= fused == &P;
+        if (groups == 1 && in_main && srows >= 1 && !fused->has_contrast) {
+            const int pitch = mask16_pitch(m16_max_seg);
+            const int slots = std::max(1, std::min(m16_max_slots, srows));
+            const int base  = lds_layout(fused->max_win_w, fused->tr, fused->stage_bytes, fused->photo && fused->has_hue,
+                                         fused->rtab).stage;
+            const int need  = base + kMaskBlockHdrBytes + slots * pitch;
+            fused_masks.mjobs    = (const Mask16Job*)(table + m16_off);
+            fused_masks.m_ctr    = ctx->d_tail + aeon_hip_ctx::kSlots + slot;
+            fused_masks.m_bpj    = (m16_max_h + srows - 1) / srows;
+            fused_masks.m_blocks = (int)m16.size() * fused_masks.m_bpj;
+            fused_masks.m_rows = srows, fused_masks.m_pitch = pitch, fused_masks.m_perm = 1, fused_masks.m_slots = slots;
+            fused_masks.m_lds    = base;
+            fused_masks.lds_bytes = std::max(fused->lds, need);
+            if (fused_masks.lds_bytes > kMaxLds) fused = nullptr;
+        } else {
+            fused = nullptr;
+        }
     }
+    if (!m16.empty() && !fused) launch_masks(table);
     auto generic = [&](const GrPlan& g) {
         if (g.jobs.empty()) return;
         KernelTimer t{};
@@ -1446,7 +1496,16 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
     for (LaunchPlan& P : main) {
         if (P.jobs.empty()) continue;
         if (P.has_contrast) HIP_OK(launch_contrast_reduce(args(P), (int)P.jobs.size(), stream));
-        timed_launch(ctx, KM_FINAL, P, args(P), stream, launch_bytes(P.jobs, KM_FINAL, oelem), timed);
+        LaunchArgs a     = args(P);
+        double     bytes = launch_bytes(P.jobs, KM_FINAL, oelem);
+        if (&P == fused) {
+            a.mjobs = fused_masks.mjobs, a.m_ctr = fused_masks.m_ctr, a.m_blocks = fused_masks.m_blocks;
+            a.m_bpj = fused_masks.m_bpj, a.m_rows = fused_masks.m_rows, a.m_pitch = fused_masks.m_pitch;
+            a.m_perm = fused_masks.m_perm, a.m_slots = fused_masks.m_slots, a.m_lds = fused_masks.m_lds;
+            a.lds_bytes = fused_masks.lds_bytes;
+            bytes += m16_bytes;
+        }
+        timed_launch(ctx, KM_FINAL, P, a, stream, bytes, timed);
     }
     phase(6);
     release_slot(ctx, slot, stream);
@@ -1509,8 +1568,9 @@ int aeon_hip_ctx_create(int device, aeon_hip_ctx** out)
             HIP_OK(contrast_records_lds_limit(kMaxLds));
             HIP_OK(hipMalloc((void**)&c->d_error, sizeof(int32_t)));
             HIP_OK(hipMemset(c->d_error, 0, sizeof(int32_t)));
-            HIP_OK(hipMalloc((void**)&c->d_tail, aeon_hip_ctx::kSlots * sizeof(uint32_t)));
-            HIP_OK(hipMemset(c->d_tail, 0, aeon_hip_ctx::kSlots * sizeof(uint32_t)));
+            // per slot: the dynamic-tail counter, then (kSlots on) the mask-block counter of pair calls
+            HIP_OK(hipMalloc((void**)&c->d_tail, 2 * aeon_hip_ctx::kSlots * sizeof(uint32_t)));
+            HIP_OK(hipMemset(c->d_tail, 0, 2 * aeon_hip_ctx::kSlots * sizeof(uint32_t)));
             HIP_OK(hipDeviceSynchronize());
             // RGB2HSV_b division tables (hsv_shift = 12), as OpenCV builds them, then per uchar H
             // HSV2RGB_f's sector fraction f (its own float operations) turned into the weight w of
@@ -1557,6 +1617,7 @@ int aeon_hip_ctx_create(int device, aeon_hip_ctx** out)
             if (const char* e = std::getenv("AEON_HIP_DIRECT")) c->direct = std::atoi(e) != 0;
             if (const char* e = std::getenv("AEON_HIP_RECORDS")) c->records = std::atoi(e) != 0;
             if (const char* e = std::getenv("AEON_HIP_JPEG_HUFF")) c->jpeg_gpu_huff = std::strcmp(e, "host") != 0;
+            if (const char* e = std::getenv("AEON_HIP_FUSE_MASKS")) c->fuse_masks = std::atoi(e) != 0;
 #ifdef AEON_HIP_TRACE
             // development builds only: s_memtime phase stamps of the tile kernel into this device buffer
             if (const char* e = std::getenv("AEON_HIP_TRACE_PTR")) c->trace = (uint32_t*)std::strtoull(e, nullptr, 0);
@@ -1651,6 +1712,32 @@ int aeon_hip_mask_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, co
                         void* stream)
 {
     return guarded([&] { return run_batch(ctx, n, descs, src_base, params, out, out_dev, stream, true); });
+}
+
+int aeon_hip_augment_pair_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* src_base,
+                                const aeon_img_desc* mask_descs, const void* mask_src_base,
+                                const aeon_aug_params* params, const aeon_out_desc* out, void* out_dev,
+                                const aeon_out_desc* mask_out, void* mask_out_dev, void* stream)
+{
+    return guarded([&] {
+        if (!ctx || n < 0 || (n > 0 && (!mask_descs || !mask_src_base || !mask_out || !mask_out_dev)))
+            fail(AEON_HIP_EINVAL, "null argument");
+        if (n == 0) return 0;
+        // one launch when every mask is an 8-bit single-channel record without rotation into plain
+        // uint8 items (the gather pass the launch's workgroups take after the image tiles); otherwise
+        // exactly aeon_hip_augment_batch then aeon_hip_mask_batch
+        bool fuse = mask_out->dtype == AEON_DTYPE_U8 && mask_out->channels == 1 && !mask_out->fixed_aspect_ratio &&
+                    !mask_out->has_mean && !mask_out->bgr_to_rgb && params;
+        for (int i = 0; fuse && i < n; i++)
+            fuse = (mask_descs[i].elem_bytes == 0 || mask_descs[i].elem_bytes == 1) && mask_descs[i].channels == 1 &&
+                   params[i].angle == 0;
+        if (!fuse) {
+            run_batch(ctx, n, descs, src_base, params, out, out_dev, stream, false);
+            return run_batch(ctx, n, mask_descs, mask_src_base, params, mask_out, mask_out_dev, stream, true);
+        }
+        const MaskSet ms{mask_descs, mask_src_base, *mask_out, mask_out_dev};
+        return run_batch(ctx, n, descs, src_base, params, out, out_dev, stream, false, &ms);
+    });
 }
 
 int aeon_hip_depthmap_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* src_base,

@@ -384,10 +384,16 @@ def run_c5(A, C, torch, steps, warmup, pool_mib, src_wh=(640, 480)):
         params.append((A.AugParams * batch)(*ps))
     stream = torch.cuda.current_stream().cuda_stream
 
-    def step(s):
+    separate = os.environ.get("AEON_BENCH_C5_SEPARATE") == "1"  # (A/B: the two calls of round 4)
+
+    def step(s):  # provider::image + provider::pixelmask of the batch: one pair call
         b = s % n_pool
-        ctx.augment_batch(idescs[b], img.data_ptr(), params[s], iout, idst[s & 1].data_ptr(), stream)
-        ctx.mask_batch(mdescs[b], msk.data_ptr(), params[s], mout, mdst[s & 1].data_ptr(), stream)
+        if separate:
+            ctx.augment_batch(idescs[b], img.data_ptr(), params[s], iout, idst[s & 1].data_ptr(), stream)
+            ctx.mask_batch(mdescs[b], msk.data_ptr(), params[s], mout, mdst[s & 1].data_ptr(), stream)
+            return
+        ctx.pair_batch(idescs[b], img.data_ptr(), mdescs[b], msk.data_ptr(), params[s], iout, idst[s & 1].data_ptr(),
+                       mout, mdst[s & 1].data_ptr(), stream)
 
     for s in range(warmup):
         step(s)
@@ -410,7 +416,8 @@ def run_c5(A, C, torch, steps, warmup, pool_mib, src_wh=(640, 480)):
     return {"value": batch * steps / dt, "unit": "images/s (image+mask pairs)", "batch": batch,
             "ms_per_step": dt / steps * 1e3, "source": f"{w}x{h} u8 HWC image + {w}x{h} u8 mask",
             "kernels_ms_per_step": k_ms / steps, "kernels_gbs": k_bytes / (k_ms * 1e-3) / 1e9 if k_ms else 0,
-            "what": "image 512x512x3 f32 CHW (bilinear) + mask 512x512 u8 (nearest), shared params"}
+            "what": "image 512x512x3 f32 CHW (bilinear) + mask 512x512 u8 (nearest), shared params, one "
+                    "aeon_hip_augment_pair_batch call per batch"}
 
 
 def pool_threads():

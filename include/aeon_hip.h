@@ -129,6 +129,19 @@ int aeon_hip_mask_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs,
                         const void* src_base, const aeon_aug_params* params,
                         const aeon_out_desc* out, void* out_dev, void* stream);
 
+/* provider::image and provider::pixelmask of the same records in one call (provider_base::provide
+ * runs both with one params set per record, src/provider.cpp:109-119, 365-393): equal to
+ * aeon_hip_augment_batch(descs, src_base, params, out, out_dev) followed by
+ * aeon_hip_mask_batch(mask_descs, mask_src_base, params, mask_out, mask_out_dev) on `stream`.
+ * When every mask is an 8-bit 1-channel record without rotation into plain uint8 items, both go
+ * in one kernel launch (the masks' gather blocks taken by the image launch's workgroups after
+ * their tiles); otherwise as the two calls. */
+int aeon_hip_augment_pair_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs,
+                                const void* src_base, const aeon_img_desc* mask_descs,
+                                const void* mask_src_base, const aeon_aug_params* params,
+                                const aeon_out_desc* out, void* out_dev,
+                                const aeon_out_desc* mask_out, void* mask_out_dev, void* stream);
+
 /* depthmap::extractor -> transformer -> loader (src/etl_depthmap.cpp:30-134) after extract: the
  * pixel-mask transform (rotate nearest -> crop -> NEAREST resize -> flip) and a plain
  * convert_mix_channels load (no fixed_aspect_ratio canvas).  aeon's provider_factory does not

@@ -111,6 +111,11 @@ int aeon_hip_mask_batch(aeon_hip_ctx*, int, const aeon_img_desc*, const void*, c
 {
     return no_device();
 }
+int aeon_hip_augment_pair_batch(aeon_hip_ctx*, int, const aeon_img_desc*, const void*, const aeon_img_desc*, const void*,
+                                const aeon_aug_params*, const aeon_out_desc*, void*, const aeon_out_desc*, void*, void*)
+{
+    return no_device();
+}
 int aeon_hip_transpose_batch(aeon_hip_ctx*, const void*, void*, int64_t, int64_t, int, void*) { return no_device(); }
 int aeon_hip_decode_jpeg_batch(aeon_hip_ctx*, int, const void* const*, const size_t*, const aeon_img_desc*, void*,
                                void*)
