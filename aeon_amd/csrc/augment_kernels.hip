@@ -690,20 +690,26 @@ void augment_tiles(LaunchArgs a)
     const Bands<KM, RM, PHOTO, OF, TAIL> W{a, L, wave, nw};
 
     // per-launch tables
+#ifndef AEON_HIP_LUT_DMA
+#define AEON_HIP_LUT_DMA 1
+#endif
     if (KM == KM_FINAL && (a.out_dtype == OUT_F32 || a.u8_map)) {
-        const auto lut = lds_ptr<float>(L.lut);
-        for (int i = tid; i < 3 * 256; i += nt) lut[i] = a.lut[i];
+        if (AEON_HIP_LUT_DMA) {
+            // by LDS-DMA, 256 bytes per wave instruction: no VGPR round trip and no wait here, so the
+            // loads are in flight together with the first jobs' fetch (one wait for both, below)
+            const auto rs = uniform_rsrc((const void*)a.lut, 3 * 256 * 4);
+            for (int i = wave; i < 12; i += nw) lds_dma<4>(rs, L.lut + i * 256, (uint32_t)((tid & 63) * 4 + i * 256));
+        } else {
+            const auto lut = lds_ptr<float>(L.lut);
+            for (int i = tid; i < 3 * 256; i += nt) lut[i] = a.lut[i];
+        }
     }
     if (PHOTO && KM != KM_RAW && a.has_hue) {
         hsv_div_tables(L, a.hsv_tables);
     }
-    if (KM == KM_FINAL && PHOTO && a.has_rtab) __syncthreads(); // record tables read the LUT
-#ifndef AEON_HIP_MASKS_FIRST
-#define AEON_HIP_MASKS_FIRST 0
-#endif
+    // (the record tables read the LUT: the wait + barrier before the first tile orders them)
     // an image + mask launch: the job of this workgroup's first mask block, loaded now
     const uint32_t mjw = MASKS ? mask_job_word(a, (int)blockIdx.x < a.m_blocks ? (int)blockIdx.x : -1) : 0u;
-    if constexpr (MASKS && AEON_HIP_MASKS_FIRST) mask_blocks(a, smem, mjw);
     // development builds (-DAEON_HIP_TRACE, tools/trace_kernel.py): s_memtime stamps per (workgroup,
     // iteration, phase) when a.trace is set; s_memrealtime (chip-wide 100 MHz) at entry and exit.
     // The product library compiles them out.
@@ -713,6 +719,7 @@ void augment_tiles(LaunchArgs a)
             a.trace[(blockIdx.x * 16 + it) * 16 + ph] = (uint32_t)__builtin_amdgcn_s_memtime();
     };
     if (a.trace && tid == 0) a.trace[(blockIdx.x * 16) * 16 + 15] = (uint32_t)__builtin_amdgcn_s_memrealtime();
+    if (a.trace && tid == 0) a.trace[(blockIdx.x * 16) * 16 + 14] = (uint32_t)__builtin_amdgcn_s_memtime();
 #else
     auto stamp = [](int, int) {};
 #endif
@@ -755,14 +762,24 @@ void augment_tiles(LaunchArgs a)
         live = t >= 0;
     }
     int js = 0; // ring index of the current tile's job slot
+    // The prologue waits for the first tile's job only: every workgroup fetches at once (768 x 128 B
+    // over PCIe for C2), and the second job is not needed before the first tile's compute, so it is
+    // fetched with the first tile's staging loads.
+#ifndef AEON_HIP_FETCH1
+#define AEON_HIP_FETCH1 1
+#endif
     if (wave == 0) {
         fetch_job(a, live ? t : -1, slot_of(0));
-        fetch_job(a, live && t + G < t_dyn ? t + G : -1, slot_of(1));
+        if (!AEON_HIP_FETCH1) fetch_job(a, live && t + G < t_dyn ? t + G : -1, slot_of(1));
     }
+    stamp(0, 10);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    stamp(0, 11);
     __syncthreads();
+    stamp(0, 12);
     Info f{};
     if (live) f = W.info(t, slot_of(0));
+    stamp(0, 13);
     for (int it = 0; live; it++) {
         // the staging phases (LDS-DMA issue, tap tables, unpack) at a raised wave priority: they
         // are this workgroup's critical path while the CU's other workgroups stream stores
@@ -774,6 +791,7 @@ void augment_tiles(LaunchArgs a)
         const bool more2 = t + 2 * G < t_dyn; // ... and a static one after it
         stamp(it, 1);
         W.issue(f);
+        if (AEON_HIP_FETCH1 && it == 0 && wave == 0 && more) fetch_job(a, t + G, slot_of(js + 1));
         if (wave == 0 && more2) fetch_job(a, t + 2 * G, slot_of(js + 2));
         stamp(it, 2);
         const bool same = f.ok && f.job == prev_job; // the LDS tables still hold this record's
@@ -781,7 +799,8 @@ void augment_tiles(LaunchArgs a)
         W.tables(f, !same, !same);
         W.record_table(f);
         stamp(it, 3);
-        if (wave == 0 && more2) asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); // the staging loads
+        // the staging loads (and in the first tile the next tile's job): all but the newest fetch
+        if (wave == 0 && more2) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         stamp(it, 4);
         W.unpack(f);
@@ -812,7 +831,7 @@ void augment_tiles(LaunchArgs a)
             break;
         }
     }
-    if constexpr (MASKS && !AEON_HIP_MASKS_FIRST) mask_blocks(a, smem, mjw);
+    if constexpr (MASKS) mask_blocks(a, smem, mjw);
 #ifdef AEON_HIP_TRACE
     if (a.trace && tid == 0) a.trace[(blockIdx.x * 16 + 1) * 16 + 15] = (uint32_t)__builtin_amdgcn_s_memrealtime();
 #endif

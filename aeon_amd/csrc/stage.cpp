@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cfloat>
@@ -706,6 +707,8 @@ struct Slot {
     uint8_t*   host_dev = nullptr; // device view of `host` (zero-copy job tables)
     uint8_t*   dev      = nullptr;
     size_t     dev_cap  = 0;
+    uint8_t*   vram     = nullptr; // job tables the host writes straight into HBM (uncached, through the BAR)
+    size_t     vram_cap = 0;
     uint8_t*   scratch  = nullptr;
     size_t     scratch_cap = 0;
     uint32_t*  partials = nullptr;
@@ -741,6 +744,8 @@ struct aeon_hip_ctx {
     bool                 direct = true; // AEON_HIP_DIRECT=0: the multi-pass path (device job table) for every call
     bool                 records = true; // AEON_HIP_RECORDS=0: contrast calls through the two-launch path
     bool                 fuse_masks = false; // AEON_HIP_FUSE_MASKS=1: a pair call's masks inside the image launch
+    bool                 vram_jobs = false; // job tables written by the host into device memory (large-BAR GPUs;
+                                            // AEON_HIP_VRAM_JOBS=0: pinned host tables)
     bool                 jpeg_gpu_huff = true; // AEON_HIP_JPEG_HUFF=host: every JPEG through the host entropy decoder
     std::vector<JobGeom> geoms;              // reused per call
     JpegState*           jpeg = nullptr;     // JPEG decode stage (pool, staging ring), on first use
@@ -800,6 +805,34 @@ void grow(uint8_t*& p, size_t& cap, size_t need, bool pinned)
 
 void close_slots(aeon_hip_ctx* ctx);
 
+// Device memory the host writes directly (a large-BAR GPU maps all of it): uncached, so every GPU read
+// of it -- a kernel's job fetch -- goes to HBM and never meets a stale cache line of the slot's
+// previous call.
+void grow_vram(uint8_t*& p, size_t& cap, size_t need)
+{
+    if (need <= cap) return;
+    size_t n = std::max(need, cap * 2);
+    if (p) HIP_OK(hipFree(p));
+    p   = nullptr;
+    cap = 0;
+    HIP_OK(hipExtMallocWithFlags((void**)&p, n, hipDeviceMallocUncached));
+    cap = n;
+}
+
+// A call's job table (written in the slot's pinned `host` buffer) published where its kernels read it
+// with device-memory latency: copied by the host into the slot's HBM table through the PCIe BAR
+// (write-combined: one contiguous copy, then a full fence so the writes reach the device ahead of the
+// launch's doorbell).  Null when the context has no such tables.  (C2: the workgroups' first job
+// fetch waited 3.7 us over PCIe from pinned memory, 0.3 us from HBM; tools/trace_kernel.py.)
+constexpr size_t kVramTableMax = 1 << 20;
+const uint8_t* publish_table(aeon_hip_ctx* ctx, Slot& s, size_t bytes)
+{
+    if (!ctx->vram_jobs || bytes > kVramTableMax || bytes > s.vram_cap) return nullptr;
+    std::memcpy(s.vram, s.host, bytes);
+    std::atomic_thread_fence(std::memory_order_seq_cst);
+    return s.vram;
+}
+
 // Wait until no kernel of any ring slot can still be running.
 void drain_ring(aeon_hip_ctx* ctx)
 {
@@ -826,6 +859,7 @@ void ensure_ring(aeon_hip_ctx* ctx, size_t table, size_t partials, size_t shifts
         grow(q.host, q.host_cap, tc, true);
         HIP_OK(hipHostGetDevicePointer((void**)&q.host_dev, q.host, 0));
         grow(q.dev, q.dev_cap, tc, false);
+        if (ctx->vram_jobs) grow_vram(q.vram, q.vram_cap, std::min(tc, kVramTableMax));
         uint8_t* p = (uint8_t*)q.partials;
         grow(p, q.partials_cap, pc, false);
         q.partials = (uint32_t*)p;
@@ -1099,8 +1133,9 @@ bool run_direct(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void
     if (o.fixed_aspect_ratio) // std::fill_n of each item's canvas, its whole byte size (etl_image.cpp:263)
         HIP_OK(hipMemset2DAsync(out_dev, o.item_stride, 0,
                                 (size_t)o.canvas_w * o.canvas_h * o.channels * out_elem_bytes(od.dtype), n, stream));
-    LaunchArgs a = launch_args(ctx, s, s.host_dev, P, n, o, d_lut, 1, ov.u8_map);
-    a.jobs_host  = 1;
+    const uint8_t* vt = publish_table(ctx, s, (size_t)n * sizeof(AugJob));
+    LaunchArgs     a  = launch_args(ctx, s, vt ? vt : s.host_dev, P, n, o, d_lut, 1, ov.u8_map);
+    a.jobs_host       = 1; // (read-through loads: pinned host memory, or the uncached HBM copy)
     timed_launch(ctx, KM_FINAL, P, a, stream, launch_bytes(geo, KM_FINAL, out_elem_bytes(o.dtype)), timed);
     phase(6);
     release_slot(ctx, slot, stream);
@@ -1167,10 +1202,11 @@ bool run_records(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const voi
         bytes += (double)params[i].crop_w * params[i].crop_h * 3 + (double)W * H * 3 * 4;
     }
     phase(4);
+    const uint8_t* vt = publish_table(ctx, s, (size_t)n * sizeof(AugJob));
     phase(5);
     LaunchArgs a{};
-    a.jobs        = (const AugJob*)s.host_dev;
-    a.jobs_host   = 1;
+    a.jobs        = (const AugJob*)(vt ? vt : s.host_dev);
+    a.jobs_host   = 1; // (read-through loads: pinned host memory, or the uncached HBM copy)
     a.job_bytes   = (int)sizeof(AugJob);
     a.lut         = d_lut;
     a.hsv_tables  = ctx->d_hsv;
@@ -1402,7 +1438,11 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
     bool mask_only = !m16.empty() && rot.empty() && exp.empty() && gr_short.jobs.empty() && gr_main.jobs.empty();
     for (auto* v : {&pre, &pre2, &pass1, &main})
         for (LaunchPlan& P : *v) mask_only = mask_only && P.jobs.empty();
-    const uint8_t* table = mask_only ? s.host_dev : s.dev;
+    // the tables in HBM written by the host (no upload launch) unless a LANCZOS4 tap table is among
+    // them (read per output pixel: the cached device copy)
+    const bool     vram_ok = gr_short.taps.empty() && gr_main.taps.empty();
+    const uint8_t* vt      = vram_ok ? publish_table(ctx, s, blob) : nullptr;
+    const uint8_t* table   = vt ? vt : mask_only ? s.host_dev : s.dev;
     // timing events on one call in timing_every (each event pair costs GPU time between launches)
     const bool timed = ctx->timing && (ctx->timing_calls++ % ctx->timing_every) == ctx->timing_every - 1;
     auto launch_masks = [&](const uint8_t* tbl) { // the gather pass, its jobs at tbl + m16_off
@@ -1416,7 +1456,7 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
     // copy: C5 93-94 us per step against 96-98 for the image and mask calls, whose gather reads the
     // pinned slot -- 4.5 us more kernel time -- and 97-98 for the masks first on the pinned slot while
     // SDMA uploads the images' table; tools/c5_ab.sh)
-    if (mask_only) {
+    if (mask_only || vt) {
     } else if (blob > kUploadKernelMax) {
         HIP_OK(hipMemcpyAsync(s.dev, s.host, blob, hipMemcpyHostToDevice, ctx->copy_stream));
         HIP_OK(hipEventRecord(s.copied, ctx->copy_stream));
@@ -1609,6 +1649,12 @@ int aeon_hip_ctx_create(int device, aeon_hip_ctx** out)
                 HIP_OK(hipEventCreateWithFlags(&s.copied, hipEventDisableTiming));
             }
             HIP_OK(hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
+            // job tables in HBM written by the host when the GPU exposes all of its memory through
+            // the PCIe BAR (else pinned host tables, read over PCIe)
+            int large_bar = 0;
+            if (hipDeviceGetAttribute(&large_bar, hipDeviceAttributeIsLargeBar, device) != hipSuccess) large_bar = 0;
+            c->vram_jobs = large_bar != 0;
+            if (const char* e = std::getenv("AEON_HIP_VRAM_JOBS")) c->vram_jobs = c->vram_jobs && std::atoi(e) != 0;
             // the ring at the size a 512-record call needs (job tables of 128 KB), so steady-state
             // calls of that size never allocate
             ensure_ring(c, 128 * 1024, 64 * 1024, 8 * 1024);
@@ -1663,6 +1709,7 @@ int aeon_hip_ctx_destroy(aeon_hip_ctx* c)
             if (s.copied) (void)hipEventDestroy(s.copied);
             if (s.host) (void)hipHostFree(s.host);
             if (s.dev) (void)hipFree(s.dev);
+            if (s.vram) (void)hipFree(s.vram);
             if (s.scratch) (void)hipFree(s.scratch);
             if (s.partials) (void)hipFree(s.partials);
             if (s.shifts) (void)hipFree(s.shifts);

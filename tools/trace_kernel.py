@@ -3,7 +3,7 @@ Needs a trace build (the product library compiles the stamps out):
   tools/build_variants.sh trace=-DAEON_HIP_TRACE
   AEON_HIP_LIB=aeon_amd/variants/trace.so python tools/trace_kernel.py C2
 Layout [workgroup][iteration 0..15][slot 0..15]; slot 15 of iteration 0 / 1 = s_memrealtime
-(chip-wide 100 MHz) at kernel entry / exit.  Single-buffered phases: 0 start, 1 info, 2 DMA
+(chip-wide 100 MHz) at kernel entry / exit, slot 14 of iteration 0 = s_memtime at entry.  Single-buffered phases: 0 start, 1 info, 2 DMA
 issued, 3 tap tables, 4 loads landed, 5 unpacked, 6 barrier, 7 computed, 8 end barrier.
 Double-buffered: 0 start, 1 next prep issued, 2 computed, 3 counted wait, 4 unpacked, 5 barrier."""
 import os
@@ -60,3 +60,31 @@ for xcd in range(8):
     s = wid % 8 == xcd
     print("realtime xcd %d: exit p10/p50/p90/max %.2f %.2f %.2f %.2f" % (xcd, np.percentile(ext_us[s], 10), np.median(ext_us[s]),
                                                                    np.percentile(ext_us[s], 90), ext_us[s].max()))
+
+# the ramp: entry -> first tile's loop start (prologue: LUT + first jobs) -> first compute (first stores)
+tpu = np.median(life_ticks / np.maximum(life_us, 1e-3))
+pro = (t[ok, 0, 0] - t[ok, 0, 14]) / tpu
+first = (t[ok, 0, 6] - t[ok, 0, 14]) / tpu
+print("prologue us p10/p50/p90 %.2f %.2f %.2f; entry -> first compute us p10/p50/p90 %.2f %.2f %.2f" % (
+    np.percentile(pro, 10), np.median(pro), np.percentile(pro, 90), np.percentile(first, 10), np.median(first),
+    np.percentile(first, 90)))
+fc_rt = ent_us + first
+print("first compute (realtime us from first entry) p10/p50/p90/max %.2f %.2f %.2f %.2f" % (
+    np.percentile(fc_rt, 10), np.median(fc_rt), np.percentile(fc_rt, 90), fc_rt.max()))
+# workgroups computing (phase 6 -> 7) over time, 1 us bins
+spans = []
+for w in np.nonzero(ok)[0]:
+    for i in range(15):
+        if t[w, i, 0] and t[w, i, 7]:
+            spans.append(((t[w, i, 6] - t[w, 0, 14]) / tpu + ent_us[np.searchsorted(np.nonzero(ok)[0], w)],
+                          (t[w, i, 7] - t[w, 0, 14]) / tpu + ent_us[np.searchsorted(np.nonzero(ok)[0], w)]))
+spans = np.array(spans)
+end = int(np.ceil(ext_us.max()))
+busy = [int(((spans[:, 0] < b + 1) & (spans[:, 1] > b)).sum()) for b in range(end)]
+print("workgroups in compute per us:", busy)
+
+# prologue parts (slots 10..13 of iteration 0: jobs issued, vmcnt(0) done, barrier done, info derived)
+parts = {"issue": (14, 10), "wait": (10, 11), "barrier": (11, 12), "info": (12, 13), "to-loop": (13, 0)}
+print("prologue parts us p50/p90: " + "  ".join(
+    f"{k} {np.median((t[ok, 0, b] - t[ok, 0, a]) / tpu):.2f}/{np.percentile((t[ok, 0, b] - t[ok, 0, a]) / tpu, 90):.2f}"
+    for k, (a, b) in parts.items()))
