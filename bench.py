@@ -51,7 +51,7 @@ def parse():
                          "run_device(region=True)); each timed launch idles the queue ~9 us around it")
     ap.add_argument("--cpu-extra-seconds", type=float, default=3.0,
                     help="CPU-baseline sample budget of each of C1/C3/C5")
-    ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic_r04.json"))
+    ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic_r04s2.json"))
     ap.add_argument("--share-device", action="store_true",
                     help="development: ranks share the visible GPUs round-robin (gloo barrier), to run "
                          "the N-rank path on a 1-GPU box")
