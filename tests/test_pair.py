@@ -160,3 +160,44 @@ def test_pair_unfusable_masks_fall_back(ctx):
     assert launches == 2, launches
     _same(hi, H.oracle_records(imgs, params, iout), "fallback image")
     _same(hm, H.oracle_records(masks, params, mout, mask=True), "fallback mask")
+
+
+@pytest.mark.parametrize("vram", [True, False])
+def test_ring_reuse_changing_params(vram):
+    """20 calls in a row on one context (more than its 16 ring slots) with different params each
+    time, C2 direct calls and C5 pair calls interleaved, outputs checked per call: the job tables the
+    host writes into HBM through the BAR (or, AEON_HIP_VRAM_JOBS=0, pinned host tables) are never read
+    stale when a slot comes round again."""
+    import torch
+    old = os.environ.get("AEON_HIP_VRAM_JOBS")
+    os.environ["AEON_HIP_VRAM_JOBS"] = "1" if vram else "0"
+    try:
+        c = A.Context(0)
+    finally:
+        if old is None:
+            del os.environ["AEON_HIP_VRAM_JOBS"]
+        else:
+            os.environ["AEON_HIP_VRAM_JOBS"] = old
+    try:
+        n = 12
+        imgs = [A.synthetic_image(i, 256, 256, 3) for i in range(n)]
+        out224 = C.out_desc_for(C.IMAGE_224, C.C2_AUG)
+        arena, descs = A.pack_images(imgs)
+        src = torch.from_numpy(arena).to("cuda")
+        stream = torch.cuda.current_stream().cuda_stream
+        c5 = _c5(6, 21)
+        pending = []
+        for call in range(20):
+            params = H.draw_params(C.C2_AUG, [(256, 256)] * n, 224, 224, seed=100 + call)
+            dst = torch.empty(n * out224.item_stride, dtype=torch.uint8, device="cuda")
+            c.augment_batch(descs, src.data_ptr(), params, out224, dst.data_ptr(), stream)
+            pending.append((params, dst))
+            if call % 5 == 4:  # a pair call between them (planner path: its table in the next slot)
+                hi, hm, _ = _pair(c, *c5)
+                _same(hm, H.oracle_records(c5[1], c5[2], c5[4], mask=True), f"pair mask at call {call}")
+        c.synchronize(stream)
+        for call, (params, dst) in enumerate(pending):
+            got = _items(dst.cpu().numpy(), params, out224)
+            _same(got, H.oracle_records(imgs, params, out224), f"C2 call {call}")
+    finally:
+        c.close()
