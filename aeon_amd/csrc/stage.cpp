@@ -808,15 +808,20 @@ void close_slots(aeon_hip_ctx* ctx);
 // Device memory the host writes directly (a large-BAR GPU maps all of it): uncached, so every GPU read
 // of it -- a kernel's job fetch -- goes to HBM and never meets a stale cache line of the slot's
 // previous call.
-void grow_vram(uint8_t*& p, size_t& cap, size_t need)
+bool grow_vram(uint8_t*& p, size_t& cap, size_t need) // false: the allocation failed (p freed)
 {
-    if (need <= cap) return;
+    if (need <= cap) return true;
     size_t n = std::max(need, cap * 2);
     if (p) HIP_OK(hipFree(p));
     p   = nullptr;
     cap = 0;
-    HIP_OK(hipExtMallocWithFlags((void**)&p, n, hipDeviceMallocUncached));
+    if (hipExtMallocWithFlags((void**)&p, n, hipDeviceMallocUncached) != hipSuccess) {
+        (void)hipGetLastError();
+        p = nullptr;
+        return false;
+    }
     cap = n;
+    return true;
 }
 
 // A call's job table (written in the slot's pinned `host` buffer) published where its kernels read it
@@ -859,7 +864,14 @@ void ensure_ring(aeon_hip_ctx* ctx, size_t table, size_t partials, size_t shifts
         grow(q.host, q.host_cap, tc, true);
         HIP_OK(hipHostGetDevicePointer((void**)&q.host_dev, q.host, 0));
         grow(q.dev, q.dev_cap, tc, false);
-        if (ctx->vram_jobs) grow_vram(q.vram, q.vram_cap, std::min(tc, kVramTableMax));
+        if (ctx->vram_jobs && !grow_vram(q.vram, q.vram_cap, std::min(tc, kVramTableMax))) {
+            ctx->vram_jobs = false; // (no HBM tables on this device: the pinned paths)
+            for (Slot& v : ctx->slots)
+                if (v.vram) {
+                    HIP_OK(hipFree(v.vram));
+                    v.vram = nullptr, v.vram_cap = 0;
+                }
+        }
         uint8_t* p = (uint8_t*)q.partials;
         grow(p, q.partials_cap, pc, false);
         q.partials = (uint32_t*)p;
