@@ -201,3 +201,25 @@ def test_ring_reuse_changing_params(vram):
             _same(got, H.oracle_records(imgs, params, out224), f"C2 call {call}")
     finally:
         c.close()
+
+
+@pytest.mark.parametrize("n", [3000, 5000])
+def test_large_tables_take_the_other_transports(n):
+    """Calls whose job table is past the direct path's per-tile fetch budget (3,000 records: the
+    planner path with its table in HBM) and past the HBM table size (5,000 records, 1.28 MB: the SDMA
+    upload), tiny records so the oracle stays quick -- every record against it."""
+    import torch
+    c = A.Context(0)
+    try:
+        rng = np.random.default_rng(n)
+        sizes = [(40 + int(rng.integers(0, 9)), 36 + int(rng.integers(0, 9))) for _ in range(n)]
+        imgs = [A.synthetic_image(i, w, h, 3) for i, (w, h) in enumerate(sizes)]
+        aug = {"type": "image", "center": False, "scale": [0.6, 1.0], "flip_enable": True}
+        etl = {"type": "image", "width": 32, "height": 32, "channels": 3, "output_type": "float",
+               "channel_major": True, "bgr_to_rgb": True}
+        out = C.out_desc_for(etl, aug)
+        params = H.draw_params(aug, sizes, 32, 32, seed=n)
+        got = H.hip_records(c, imgs, params, out)
+        _same(got, H.oracle_records(imgs, params, out), f"{n} records")
+    finally:
+        c.close()
