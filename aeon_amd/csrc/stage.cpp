@@ -832,9 +832,12 @@ bool grow_vram(uint8_t*& p, size_t& cap, size_t need) // false: the allocation f
 constexpr size_t kVramTableMax = 1 << 20;
 const uint8_t* publish_table(aeon_hip_ctx* ctx, Slot& s, size_t bytes)
 {
-    if (!ctx->vram_jobs || bytes > kVramTableMax || bytes > s.vram_cap) return nullptr;
+    if (!ctx->vram_jobs || bytes == 0 || bytes > kVramTableMax || bytes > s.vram_cap) return nullptr;
     std::memcpy(s.vram, s.host, bytes);
     std::atomic_thread_fence(std::memory_order_seq_cst);
+    // a read back through the BAR: PCIe does not let a read pass the posted writes ahead of it, so
+    // the table is in HBM when it returns (~1 us of host time; the host runs ahead of the GPU)
+    (void)*(volatile const uint32_t*)(s.vram + ((bytes - 1) & ~(size_t)3));
     return s.vram;
 }
 
