@@ -149,6 +149,8 @@ def lib():
         L.aeon_hip_stager_stage.argtypes = [vp, vp, ctypes.c_int, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                             ctypes.c_int, ctypes.c_int, P(AugParams)]
         L.aeon_hip_stager_flush.argtypes = [vp, vp]
+        L.aeon_hip_stager_launch.argtypes = [vp, vp]
+        L.aeon_hip_stager_wait.argtypes = [vp, vp]
         L.aeon_hip_stager_last_error.restype = ctypes.c_char_p
         L.aeon_hip_host_alloc.argtypes = [ctypes.c_size_t, P(vp)]
         L.aeon_hip_host_free.argtypes = [vp]
@@ -436,8 +438,10 @@ def _check_stager(rc):
 
 class Stager:
     """aeon_hip_stager: what the aeon-side provider::image / ::pixelmask hold (INTEGRATION.md).
-    stage() from provide() on any pool thread (the ctypes call releases the GIL), flush() from
-    post_process() once per batch: the first flush of a window launches the whole window."""
+    stage() from provide() on any pool thread (the ctypes call releases the GIL); launch() from
+    post_process() once per batch (the first launch of a window launches the whole window and
+    returns), wait() from the consumer before it reads a batch (wait_buffer(): by buffer alone, as
+    batch_iterator_fbm::filler calls it); flush() = launch + wait."""
 
     def __init__(self, ctx, out, batch_size, kind=STAGER_IMAGE):
         h = ctypes.c_void_p()
@@ -455,6 +459,17 @@ class Stager:
 
     def flush(self, batch_out):
         _check_stager(lib().aeon_hip_stager_flush(self._h, ctypes.c_void_p(batch_out)))
+
+    def launch(self, batch_out):
+        _check_stager(lib().aeon_hip_stager_launch(self._h, ctypes.c_void_p(batch_out)))
+
+    def wait(self, batch_out):
+        _check_stager(lib().aeon_hip_stager_wait(self._h, ctypes.c_void_p(batch_out)))
+
+    @staticmethod
+    def wait_buffer(batch_out):
+        """aeon_hip_stager_wait(NULL, batch_out): whichever stager launched the buffer, if any."""
+        _check_stager(lib().aeon_hip_stager_wait(None, ctypes.c_void_p(batch_out)))
 
     def close(self):
         if getattr(self, "_h", None):

@@ -236,7 +236,7 @@ constexpr int kRecWords  = 3 * kRecRows;           // 12 bytes (4 BGR pixels) pe
 
 // LDS carve of the record kernel (bytes, 16-aligned regions)
 struct RecLds {
-    int rtab, lut, hwt, hsv, htab, xt, xt2, yt, job, sums, stage, stage_bytes, total;
+    int rtab, lut, hwt, hsv, htab, xt, xt2, yt, job, sums, flags, stage, stage_bytes, total;
 };
 AEON_HD inline RecLds rec_lds_layout(int win_w, int stage_bytes)
 {
@@ -252,6 +252,7 @@ AEON_HD inline RecLds rec_lds_layout(int win_w, int stage_bytes)
     L.yt   = o; o += 2 * kRecTRMax * 16;    // row taps, one table per staging buffer
     L.job  = o; o += 3 * (int)sizeof(AugJob); // a ring of three records' jobs
     L.sums = o; o += 16 * 16;               // per-wave channel sums
+    L.flags = o; o += 16;                   // (split kernel) staging buffer b's tile is valid: word b
     L.stage_bytes = stage_bytes;
     L.stage = o; o += 2 * stage_bytes;      // two staging buffers
     L.total = o;

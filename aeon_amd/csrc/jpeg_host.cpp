@@ -564,6 +564,13 @@ void decode_file(const uint8_t* d, size_t size, Frame& f, Arena& a, size_t blk_o
             if (!f.qset[f.c[k].tq]) bad("component uses an undefined quantisation table");
             sc[i] = k;
         }
+        // jdinput.c per_scan_setup: an interleaved scan's MCU holds at most D_MAX_BLOCKS_IN_MCU (10) blocks
+        // (JERR_BAD_MCU_SIZE) -- cv::imdecode refuses such files, so they are refused here too
+        if (ns > 1) {
+            int mb = 0;
+            for (int i = 0; i < ns; i++) mb += f.c[sc[i]].h * f.c[sc[i]].v;
+            if (mb > 10) bad("sampling factors too large for an interleaved scan");
+        }
         const ProgScan S{s[1 + 2 * ns], s[2 + 2 * ns], s[3 + 2 * ns] >> 4, s[3 + 2 * ns] & 15};
         if (f.progressive) {
             // jdphuff.c start_pass_phuff_decoder's checks
@@ -775,6 +782,13 @@ bool prepare_gpu(const uint8_t* d, size_t size, Frame& f, Arena& a, GpuScan& g, 
             if (f.c[k].td > 3 || f.c[k].ta > 3) bad("bad Huffman table selector");
             if (!f.qset[f.c[k].tq]) bad("component uses an undefined quantisation table");
             sc[i] = k;
+        }
+        // jdinput.c per_scan_setup: an interleaved scan's MCU holds at most D_MAX_BLOCKS_IN_MCU (10) blocks
+        // (JERR_BAD_MCU_SIZE) -- cv::imdecode refuses such files, so they are refused here too
+        if (ns > 1) {
+            int mb = 0;
+            for (int i = 0; i < ns; i++) mb += f.c[sc[i]].h * f.c[sc[i]].v;
+            if (mb > 10) bad("sampling factors too large for an interleaved scan");
         }
         if (ns != f.ncomp) return false; // components in separate scans: the host decoder
         for (int i = 0; i < ns; i++)

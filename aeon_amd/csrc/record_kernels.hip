@@ -31,6 +31,12 @@
 #ifndef AEON_REC_NOA
 #define AEON_REC_NOA 0
 #endif
+#ifndef AEON_REC_HELPER_PRIO // s_setprio of the split kernel's helper waves
+#define AEON_REC_HELPER_PRIO 3
+#endif
+#ifndef AEON_REC_UNROLL // split kernel: the compute waves' tile loop unrolled (no register rotation)
+#define AEON_REC_UNROLL 1
+#endif
 #ifndef AEON_REC_FUSED // FAST form: A and B of a row interleaved (rec_row_fast); 0 = B's row, then A's
 #define AEON_REC_FUSED 1
 #endif
@@ -87,9 +93,9 @@ __device__ __forceinline__ RecTile rec_tile(const JobRef& J, int band, int TR, i
 }
 
 // row taps of tile f into the table at yt (staged rows in the buffer at `stage`)
-__device__ __forceinline__ void rec_row_taps(const JobRef& J, const RecTile& f, int yt, int stage)
+__device__ __forceinline__ void rec_row_taps(const JobRef& J, const RecTile& f, int yt, int stage, int i0, int step)
 {
-    for (int r = threadIdx.x; r < f.nrows; r += blockDim.x) {
+    for (int r = i0; r < f.nrows; r += step) {
         const YTap y = ycoef<RESIZE_LINEAR>(JF(J, win_y) + f.y0 + r, JF(J, scale_y), JF(J, crop_h));
         lds_ptr<i32x4>(yt)[r] = (i32x4){stage + (y.r0 - f.G.v_lo) * f.G.rp, stage + (y.r1 - f.G.v_lo) * f.G.rp, y.b0, y.b1};
     }
@@ -294,6 +300,39 @@ __device__ __forceinline__ u32x3 rec_row_fast(const RecA& R, const RecLds& L, i3
 
 } // namespace
 
+// Development builds (-DAEON_HIP_TRACE, tools/trace_records.py): s_memtime stamps per (workgroup,
+// step*8 + tile, slot) -- slots 0..7 by lane 0 of wave 0 (of the first helper wave in the split
+// kernel), 16 + w by lane 0 of wave w; entry 63 holds s_memrealtime / s_memtime at entry (0, 1) and
+// exit (2, 3).  The product library compiles them out.  (Vector stores: they count on vmcnt, and a
+// counted wait that sees more operations after its loads than it assumed only waits longer.)
+#ifdef AEON_HIP_TRACE
+#define REC_TRACE_SETUP                                                                                      \
+    auto stamp = [&](int idx, int sl) {                                                                      \
+        if (a.trace && (tid & 63) == 0 && wave == kTraceWave && idx < 64)                                    \
+            a.trace[(blockIdx.x * 64 + idx) * 32 + sl] = (uint32_t)__builtin_amdgcn_s_memtime();              \
+    };                                                                                                       \
+    auto wstamp = [&](int idx) {                                                                             \
+        if (a.trace && (tid & 63) == 0 && idx < 64)                                                          \
+            a.trace[(blockIdx.x * 64 + idx) * 32 + 16 + wave] = (uint32_t)__builtin_amdgcn_s_memtime();       \
+    };                                                                                                       \
+    if (a.trace && tid == 0) {                                                                               \
+        a.trace[(blockIdx.x * 64 + 63) * 32 + 0] = (uint32_t)__builtin_amdgcn_s_memrealtime();               \
+        a.trace[(blockIdx.x * 64 + 63) * 32 + 1] = (uint32_t)__builtin_amdgcn_s_memtime();                   \
+    }                                                                                                        \
+    if (a.trace && (tid & 63) == 0) /* HW_ID: SIMD id in bits 5:4 */                                         \
+        a.trace[(blockIdx.x * 64 + 62) * 32 + 16 + wave] = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));
+#define REC_TRACE_EXIT                                                                                       \
+    if (a.trace && tid == 0) {                                                                               \
+        a.trace[(blockIdx.x * 64 + 63) * 32 + 2] = (uint32_t)__builtin_amdgcn_s_memrealtime();               \
+        a.trace[(blockIdx.x * 64 + 63) * 32 + 3] = (uint32_t)__builtin_amdgcn_s_memtime();                   \
+    }
+#else
+#define REC_TRACE_SETUP                                                                                      \
+    auto stamp  = [](int, int) {};                                                                           \
+    auto wstamp = [](int) {};
+#define REC_TRACE_EXIT
+#endif
+
 // One persistent workgroup per CU; records blockIdx.x, +G, ...  Lane (lph, lcg): column group lcg
 // (output columns 4*lcg ..), rows lph + 16 j.  Requires every record 3-channel, INTER_LINEAR without
 // OpenCV's scalar tail, float32 CHW output through the record table, equal win_w x win_h (host).
@@ -313,6 +352,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) void 
     const int    lph = tid / gpr, lcg = tid - lph * gpr;
     const int    nph = r.phases, TR = nph * kRecTileRows;
     const bool   active = lph < nph;
+    [[maybe_unused]] constexpr int kTraceWave = 0;
     const int    ox0 = lcg * 4;
     const int    plane = W * H;
     const bool   bgr = a.bgr_to_rgb != 0;
@@ -321,6 +361,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) void 
     if (K == 0) return;
     const auto slot = [&](int k) { return L.job + (k % 3) * (int)sizeof(AugJob); };
     const auto rec_of = [&](int k) { return (int)blockIdx.x + k * G; };
+    REC_TRACE_SETUP
 
     hsv_div_tables(LdsLayout{0, L.hsv, 0, 0, 0, 0, 0, 0, 0, 0}, a.hsv_tables);
     // the launch's constant tables in LDS: the per-record tables are then built without global loads,
@@ -338,7 +379,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) void 
     RecTile f = rec_tile(JobRef{slot(0)}, 0, TR, H, L.stage_bytes, a.error);
     if (f.ok) {
         stage_issue(JobRef{slot(0)}, f.G, L.stage, wave, nw);
-        rec_row_taps(JobRef{slot(0)}, f, L.yt, L.stage);
+        rec_row_taps(JobRef{slot(0)}, f, L.yt, L.stage, tid, nt);
     }
     int pending = 0; // this wave's vector-memory ops issued after its latest staging loads
 
@@ -363,12 +404,16 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) void 
 #pragma unroll 1
         for (int t = 0; t < kRecTiles; t++) {
             const bool tile_a = hasA && t < TS; // A has staged rows in this tile
+            stamp(k * 8 + t, 0);
             if (tile_a && f.ok) {
                 // this wave's staging loads of the tile, then unpack its slots in place
                 wait_vm_upto(pending);
+                stamp(k * 8 + t, 1);
                 stage_unpack(JA, f.G, L.stage + par * L.stage_bytes, wave, nw);
             }
+            stamp(k * 8 + t, 2);
             lds_barrier();
+            stamp(k * 8 + t, 3);
             if (tile_a && active) { // the lane's column taps (flip folded in) from the record's table
 #pragma unroll
                 for (int q = 0; q < 4; q++) {
@@ -392,9 +437,10 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) void 
                     const int sb = L.stage + (par ^ 1) * L.stage_bytes;
                     stage_issue(JN, fn.G, sb, wave, nw);
                     pending = 0; // (the counted wait of that tile: the stores issued after these loads)
-                    rec_row_taps(JN, fn, L.yt + (par ^ 1) * kRecTRMax * 16, sb);
+                    rec_row_taps(JN, fn, L.yt + (par ^ 1) * kRecTRMax * 16, sb, tid, nt);
                 }
             }
+            stamp(k * 8 + t, 4);
             // the tile's two rows per lane: B's from the oldest held tile, A's into the newest
             uint32_t nwv[6];
 #pragma unroll
@@ -423,6 +469,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) void 
                     }
                 }
             }
+            wstamp(k * 8 + t);
             // rotate: drop the tile B consumed, append the tile A produced (the fused rows wrote A's
             // words over B's in place: a cyclic rotation)
             if (FAST && AEON_REC_FUSED && tile_a && f.ok) {
@@ -439,24 +486,228 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) void 
         if (!hasA) break;
         // record k is complete in registers: its sums -> (1-c)*mean -> its table; the next record's
         // column taps and hue table
+        stamp(k * 8 + 7, 0);
         s0 = wave_sum(s0), s1 = wave_sum(s1), s2 = wave_sum(s2);
         if ((tid & 63) == 0) {
             const auto ps = lds_ptr<uint32_t>(L.sums);
             ps[wave * 4] = s0, ps[wave * 4 + 1] = s1, ps[wave * 4 + 2] = s2;
         }
         lds_barrier(); // also: every lane is done with this step's tiles (B's record table reads)
+        stamp(k * 8 + 7, 1);
         rec_table(a, L, JA, W, H, nw);
+        stamp(k * 8 + 7, 2);
         b_out = JF(JA, out_ptr);
         if (k + 1 < K) rec_record_tables(a, L, JobRef{slot(k + 1)}, W, FAST);
+        stamp(k * 8 + 7, 3);
         // (published by the next step's first barrier)
     }
+    REC_TRACE_EXIT
+}
+
+// The split form (host: AEON_HIP_REC_HELPERS, default): the workgroup's nwc compute waves hold the
+// record and do only rows and record ends; nh = blockDim/64 - nwc helper waves (2 for 224-wide
+// records: 1,024 lanes) do all of the staging -- job fetches, the next tile's LDS-DMA loads and row
+// taps, and, once their loads landed, its in-place unpack -- during the current tile.  The compute
+// waves then never wait on a load or unpack, and the helpers run on the issue slots the 14 compute
+// waves leave free (they sit 4/4/3/3 on the CU's SIMDs).  The two roles are separate loops (the
+// helpers' staging registers are not live across the compute waves' held record) meeting at the same
+// barriers: one per tile (B1) and one per record end (B2).
+template <bool FAST>
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) void contrast_records_split(LaunchArgs a, RecArgs r)
+{
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    if ((uint32_t)(size_t)(__attribute__((address_space(3))) char*)smem != 0u) { // see lds_ld
+        if (threadIdx.x == 0) atomicOr(a.error, 4);
+        return;
+    }
+    const int    tid = threadIdx.x, nt = blockDim.x;
+    const int    wave = __builtin_amdgcn_readfirstlane(tid >> 6), nw = nt >> 6;
+    const int    W = r.win_w, H = r.win_h, TS = r.tiles;
+    const RecLds L = rec_lds_layout(W, a.stage_bytes);
+    const int    gpr = W >> 2;
+    const int    nph = r.phases, TR = nph * kRecTileRows;
+    const int    nwc = (nph * gpr + 63) >> 6; // compute waves
+    const int    nh  = nw - nwc;               // helper waves (>= 1: the host guarantees it)
+    const bool   helper = wave >= nwc;
+    const int    G = gridDim.x;
+    const int    K = r.n_jobs > (int)blockIdx.x ? (r.n_jobs - 1 - (int)blockIdx.x) / G + 1 : 0; // this workgroup's records
+    if (K == 0) return;
+    const auto slot   = [&](int k) { return L.job + (k % 3) * (int)sizeof(AugJob); };
+    const auto rec_of = [&](int k) { return (int)blockIdx.x + k * G; };
+    const auto flags  = lds_ptr<int32_t>(L.flags);
+    [[maybe_unused]] const int kTraceWave = nwc; // (trace builds: the phase stamps come from the first helper)
+    REC_TRACE_SETUP
+
+    hsv_div_tables(LdsLayout{0, L.hsv, 0, 0, 0, 0, 0, 0, 0, 0}, a.hsv_tables);
+    for (int i = tid; i < 3 * 256; i += nt) lds_ptr<float>(L.lut)[i] = a.lut[i];
+    for (int i = tid; i < 256 * 4; i += nt) lds_ptr<int32_t>(L.hwt)[i] = a.hsv_tables[kHsvDivWords + i];
+    if (wave == nwc) {
+        rec_fetch_job(a, rec_of(0), slot(0));
+        if (K > 1) rec_fetch_job(a, rec_of(1), slot(1));
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    rec_record_tables(a, L, JobRef{slot(0)}, W, FAST);
+
+    if (helper) {
+        // ---- helpers: stage tile by tile, one tile ahead of the compute waves ----
+        const int sw = wave - nwc, stid = tid - nwc * 64, snt = nh * 64;
+        // The helpers run at a raised priority: the CU's arbiter otherwise serves the oldest waves first,
+        // and the helpers (the youngest) would get issue slots only when the compute waves on their SIMDs
+        // stall -- their staging then ends after the compute waves' rows.
+        __builtin_amdgcn_s_setprio(AEON_REC_HELPER_PRIO);
+        int cur_idx = 0; // (trace builds: the entry the staging stamps go to)
+        const auto stage_tile = [&](const JobRef& J, int band, int buf) {
+            const RecTile f = rec_tile(J, band, TR, H, L.stage_bytes, a.error);
+            if (f.ok) {
+                const int sb = L.stage + buf * L.stage_bytes;
+                stage_issue(J, f.G, sb, sw, nh);
+                rec_row_taps(J, f, L.yt + buf * kRecTRMax * 16, sb, stid, snt);
+                stamp(cur_idx, 5);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // (helpers store nothing)
+                stamp(cur_idx, 6);
+                stage_unpack(J, f.G, sb, sw, nh);
+                stamp(cur_idx, 7);
+            }
+            if (stid == 0) flags[buf] = f.ok ? 1 : 0;
+        };
+        int par = 0;
+        stage_tile(JobRef{slot(0)}, 0, 0);
+        for (int k = 0; k <= K; k++) {
+            const bool hasA = k < K;
+#pragma unroll 1
+            for (int t = 0; t < kRecTiles; t++) {
+                const bool tile_a = hasA && t < TS;
+                stamp(k * 8 + t, 0);
+                lds_barrier(); // B1: the staged tile is published; the other buffer is free
+                stamp(k * 8 + t, 3);
+                const bool next_same = hasA && t + 1 < TS;
+                const bool next_rec  = hasA && t + 1 == TS && k + 1 < K;
+                cur_idx = k * 8 + t;
+                if (next_same || next_rec) {
+                    if (next_rec && wave == nwc && k + 2 < K) rec_fetch_job(a, rec_of(k + 2), slot(k + 2));
+                    stage_tile(JobRef{slot(next_same ? k : k + 1)}, next_same ? t + 1 : 0, par ^ 1);
+                }
+                stamp(k * 8 + t, 4);
+                wstamp(k * 8 + t);
+                if (tile_a) par ^= 1;
+            }
+            if (!hasA) break;
+            stamp(k * 8 + 7, 0);
+            lds_barrier(); // B2: the compute waves' sums are in
+            stamp(k * 8 + 7, 1);
+            rec_table(a, L, JobRef{slot(k)}, W, H, nwc);
+            stamp(k * 8 + 7, 2);
+            if (k + 1 < K) rec_record_tables(a, L, JobRef{slot(k + 1)}, W, FAST);
+            stamp(k * 8 + 7, 3);
+        }
+        REC_TRACE_EXIT
+        return;
+    }
+
+    // ---- compute waves: rows (A of record k and B of record k - 1), record ends ----
+    // The tile loop is unrolled (AEON_REC_UNROLL): tile t's rows live in rec[6t .. 6t + 5] for every
+    // record -- B of record k - 1 reads them and A of record k writes them back in place -- so every
+    // register index is a compile-time constant without rotating the held record by one tile per tile
+    // (42 moves per tile).
+    const int  gid = tid; // (compute lanes are the first nwc * 64)
+    const int  lph = gid / gpr, lcg = gid - lph * gpr;
+    const bool active = lph < nph;
+    const int  ox0 = lcg * 4;
+    const int  plane = W * H;
+    const bool bgr = a.bgr_to_rgb != 0;
+    uint32_t   rec[kRecWords];
+#pragma unroll
+    for (int i = 0; i < kRecWords; i++) rec[i] = 0;
+    uint64_t b_out = 0;
+    int      par   = 0;
+    for (int k = 0; k <= K; k++) {
+        const bool   hasA = k < K, hasB = k > 0;
+        const JobRef JA{slot(k)};
+        RecA         R{};
+        if (hasA) {
+            R.photo   = JF(JA, photo);
+            R.bs_kind = JF(JA, bs_kind);
+            R.flip    = JF(JA, flip);
+            if (R.photo & PHOTO_BS) R.bs = bs_regs(JA);
+        }
+        const auto orsrc = __builtin_amdgcn_make_buffer_rsrc((void*)b_out, (short)0, hasB ? plane * 12 : 0, 0x00020000);
+        uint32_t   s0 = 0, s1 = 0, s2 = 0;
+        constexpr bool kUnroll = FAST && AEON_REC_UNROLL; // (the generic form's registers would spill)
+#pragma unroll kUnroll ? kRecTiles : 1
+        for (int t = 0; t < kRecTiles; t++) {
+            const int  rb     = kUnroll ? 6 * t : 0; // the tile's words in rec[]
+            const bool tile_a = hasA && t < TS;
+            lds_barrier(); // B1
+            const bool fok = tile_a && __builtin_amdgcn_readfirstlane(flags[par]) != 0;
+            if (tile_a && active) {
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const int   ox  = min(ox0 + q, W - 1);
+                    const int   x   = R.flip ? W - 1 - ox : ox;
+                    const i32x2 xtt = lds_ptr<const i32x2>(L.xt)[x];
+                    R.col[q] = xtt.x, R.wx[q] = (uint32_t)xtt.y;
+                }
+            }
+            uint32_t nwv[6];
+#pragma unroll
+            for (int u = 0; u < kRecTileRows; u++) {
+                const int j = t * kRecTileRows + u;
+                const int y = lph + nph * j;
+                uint32_t* hw = rec + rb + 3 * u;
+                nwv[3 * u] = nwv[3 * u + 1] = nwv[3 * u + 2] = 0;
+                if (FAST && AEON_REC_FUSED && fok) { // (uniform) A and B interleaved
+                    const bool  va  = active && y < H;
+                    const i32x4 ytr = lds_ptr<const i32x4>(L.yt + par * kRecTRMax * 16)[min(y - t * TR, TR - 1)];
+                    const u32x3 q   = rec_row_fast(R, L, ytr, va, s0, s1, s2, orsrc, plane, hasB && va ? y * W + ox0 : -1,
+                                                   bgr, hw[0], hw[1], hw[2]);
+                    hw[0] = q.x, hw[1] = q.y, hw[2] = q.z; // (B has read them)
+                    nwv[3 * u] = q.x, nwv[3 * u + 1] = q.y, nwv[3 * u + 2] = q.z;
+                    continue;
+                }
+                if (hasB && __builtin_amdgcn_ballot_w64(active && y < H) != 0) {
+                    if (active && y < H) rec_store(L, orsrc, plane, y * W + ox0, bgr, hw[0], hw[1], hw[2]);
+                }
+                if constexpr (!(FAST && AEON_REC_FUSED)) {
+                    if (fok && active && y < H) {
+                        const i32x4 ytr = lds_ptr<const i32x4>(L.yt + par * kRecTRMax * 16)[y - t * TR];
+                        const u32x3 q   = rec_pixels<FAST>(R, L, ytr, s0, s1, s2);
+                        nwv[3 * u] = q.x, nwv[3 * u + 1] = q.y, nwv[3 * u + 2] = q.z;
+                    }
+                }
+            }
+            wstamp(k * 8 + t);
+            if (kUnroll) { // the tile's words: A's (zero where A wrote nothing)
+#pragma unroll
+                for (int i = 0; i < 6; i++) rec[rb + i] = nwv[i];
+            } else { // rotate: drop the tile B consumed, append the tile A produced
+#pragma unroll
+                for (int i = 0; i < kRecWords - 6; i++) rec[i] = rec[i + 6];
+#pragma unroll
+                for (int i = 0; i < 6; i++) rec[kRecWords - 6 + i] = nwv[i];
+            }
+            if (tile_a) par ^= 1;
+        }
+        if (!hasA) break;
+        s0 = wave_sum(s0), s1 = wave_sum(s1), s2 = wave_sum(s2);
+        if ((tid & 63) == 0) {
+            const auto ps = lds_ptr<uint32_t>(L.sums);
+            ps[wave * 4] = s0, ps[wave * 4 + 1] = s1, ps[wave * 4 + 2] = s2;
+        }
+        lds_barrier(); // B2
+        rec_table(a, L, JA, W, H, nwc);
+        b_out = JF(JA, out_ptr);
+        if (k + 1 < K) rec_record_tables(a, L, JobRef{slot(k + 1)}, W, FAST);
+    }
+    REC_TRACE_EXIT
 }
 
 // fast: every record's brightness/saturation is the fixed-point cv::transform (or off) -- rec_pixels
-hipError_t launch_contrast_records(bool fast, const LaunchArgs& a, const RecArgs& r, int grid, hipStream_t stream,
+hipError_t launch_contrast_records(bool fast, bool split, const LaunchArgs& a, const RecArgs& r, int grid, hipStream_t stream,
                                    hipEvent_t start, hipEvent_t stop)
 {
-    const void* fn = fast ? (const void*)contrast_records<true> : (const void*)contrast_records<false>;
+    const void* fn = split ? (fast ? (const void*)contrast_records_split<true> : (const void*)contrast_records_split<false>)
+                           : (fast ? (const void*)contrast_records<true> : (const void*)contrast_records<false>);
     void*       args[2] = {(void*)&a, (void*)&r};
     if (start || stop) return hipExtLaunchKernel(fn, dim3(grid), dim3(a.threads), args, a.lds_bytes, stream, start, stop, 0);
     return hipLaunchKernel(fn, dim3(grid), dim3(a.threads), args, a.lds_bytes, stream);
@@ -464,9 +715,12 @@ hipError_t launch_contrast_records(bool fast, const LaunchArgs& a, const RecArgs
 
 hipError_t contrast_records_lds_limit(int bytes)
 {
-    hipError_t e = hipFuncSetAttribute((const void*)contrast_records<true>, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
-    if (e != hipSuccess) return e;
-    return hipFuncSetAttribute((const void*)contrast_records<false>, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    for (const void* fn : {(const void*)contrast_records<true>, (const void*)contrast_records<false>,
+                           (const void*)contrast_records_split<true>, (const void*)contrast_records_split<false>}) {
+        const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 
 int contrast_records_lds(int win_w, int stage_bytes) { return rec_lds_layout(win_w, stage_bytes).total; }

@@ -12,6 +12,9 @@
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <csetjmp>
+#include <csignal>
+#include <signal.h>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -40,7 +43,7 @@ hipError_t launch_expand(const ExpandJob* jobs, int n_jobs, int max_pixels, hipS
 hipError_t launch_nearest(const Mask16Job* jobs, int n_jobs, int max_h, int max_w, int max_seg_bytes, int max_slots, hipStream_t stream,
                           hipEvent_t start, hipEvent_t stop);
 hipError_t launch_upload_table(const void* host_dev, void* dst, size_t bytes, hipStream_t stream);
-hipError_t launch_contrast_records(bool fast, const LaunchArgs& a, const RecArgs& r, int grid, hipStream_t stream,
+hipError_t launch_contrast_records(bool fast, bool split, const LaunchArgs& a, const RecArgs& r, int grid, hipStream_t stream,
                                    hipEvent_t start, hipEvent_t stop);
 hipError_t contrast_records_lds_limit(int bytes);
 hipError_t launch_resize_generic(const ResizeJob* jobs, const uint8_t* table, int n_jobs, int max_tiles, int TR, int CW,
@@ -743,6 +746,8 @@ struct aeon_hip_ctx {
     // the jobs from the pinned slot itself
     bool                 direct = true; // AEON_HIP_DIRECT=0: the multi-pass path (device job table) for every call
     bool                 records = true; // AEON_HIP_RECORDS=0: contrast calls through the two-launch path
+    int                  rec_helpers = 2; // AEON_HIP_REC_HELPERS: staging-only waves of the record kernel
+    int                  rec_phases  = 0; // AEON_HIP_REC_PHASES (development): row phases of the record kernel
     bool                 fuse_masks = false; // AEON_HIP_FUSE_MASKS=1: a pair call's masks inside the image launch
     bool                 vram_jobs = false; // job tables written by the host into device memory (large-BAR GPUs;
                                             // AEON_HIP_VRAM_JOBS=0: pinned host tables)
@@ -808,6 +813,36 @@ void close_slots(aeon_hip_ctx* ctx);
 // Device memory the host writes directly (a large-BAR GPU maps all of it): uncached, so every GPU read
 // of it -- a kernel's job fetch -- goes to HBM and never meets a stale cache line of the slot's
 // previous call.
+// One guarded host write + read-back through p: false when it faults (SIGSEGV / SIGBUS, caught for the
+// duration of the probe only, the previous handlers restored) or reads back something else.
+thread_local sigjmp_buf* t_probe_jmp = nullptr;
+void probe_fault(int sig, siginfo_t*, void*)
+{
+    if (t_probe_jmp) siglongjmp(*t_probe_jmp, 1);
+    std::signal(sig, SIG_DFL); // another thread's fault inside the probe window: the default action
+}
+bool host_can_write(void* p)
+{
+    struct sigaction sa{}, old_segv{}, old_bus{};
+    sa.sa_sigaction = probe_fault;
+    sa.sa_flags     = SA_SIGINFO;
+    sigemptyset(&sa.sa_mask);
+    sigaction(SIGSEGV, &sa, &old_segv);
+    sigaction(SIGBUS, &sa, &old_bus);
+    sigjmp_buf jb;
+    volatile bool ok = false;
+    t_probe_jmp = &jb;
+    if (sigsetjmp(jb, 1) == 0) {
+        volatile uint32_t* q = (volatile uint32_t*)p;
+        q[0]                 = 0xA5C3E1F7u;
+        ok                   = q[0] == 0xA5C3E1F7u;
+    }
+    t_probe_jmp = nullptr;
+    sigaction(SIGSEGV, &old_segv, nullptr);
+    sigaction(SIGBUS, &old_bus, nullptr);
+    return ok;
+}
+
 bool grow_vram(uint8_t*& p, size_t& cap, size_t need) // false: the allocation failed (p freed)
 {
     if (need <= cap) return true;
@@ -817,6 +852,15 @@ bool grow_vram(uint8_t*& p, size_t& cap, size_t need) // false: the allocation f
     cap = 0;
     if (hipExtMallocWithFlags((void**)&p, n, hipDeviceMallocUncached) != hipSuccess) {
         (void)hipGetLastError();
+        p = nullptr;
+        return false;
+    }
+    // the host writes these tables through p itself: only when a guarded probe write + read-back
+    // through p works (a restricted BAR or a virtualised GPU can allocate it without mapping it for the
+    // CPU; the runtime reports no host pointer for device memory either way) -- the pinned paths then
+    if (!host_can_write(p)) {
+        (void)hipGetLastError();
+        (void)hipFree(p);
         p = nullptr;
         return false;
     }
@@ -1175,7 +1219,9 @@ bool run_records(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const voi
     if (o.dtype != AEON_DTYPE_F32 || !o.channel_major || o.fixed_aspect_ratio || o.channels != 3) return false;
     if ((((uint64_t)out_dev) & 15) != 0 || (o.item_stride & 15) != 0) return false;
     const int W = params[0].out_w, H = params[0].out_h;
-    const int nph = rec_phases(W, H);
+    int       nph = rec_phases(W, H);
+    if (ctx->rec_phases > 0 && W / 4 * ctx->rec_phases <= 1024 && (H + ctx->rec_phases - 1) / ctx->rec_phases <= kRecRows)
+        nph = ctx->rec_phases; // (development: AEON_HIP_REC_PHASES)
     if (W <= 0 || (W & 3) != 0 || W > 4 * 256 || H <= 0 || nph <= 0) return false;
     if (simd_boundary(W * 3) < W * 3) return false; // OpenCV's scalar row tail
     bool      contrast = false;
@@ -1232,13 +1278,19 @@ bool run_records(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const voi
     a.channel_major = 1;
     a.bgr_to_rgb  = o.bgr_to_rgb && o.channels == 3;
     a.threads     = (nph * (W / 4) + 63) / 64 * 64;
+    // helper waves (record_kernels.hip: staging only) when the workgroup has room for them
+    const bool split = ctx->rec_helpers > 0 && a.threads + 64 * ctx->rec_helpers <= 1024;
+    if (split) a.threads += 64 * ctx->rec_helpers;
     a.lds_bytes   = lds;
+#ifdef AEON_HIP_TRACE
+    a.trace = ctx->trace; // development builds only (tools/trace_records.py)
+#endif
     const RecArgs r{n, nph, W, H, ((H + nph - 1) / nph + kRecTileRows - 1) / kRecTileRows};
     const int     grid  = std::min(n, ctx->n_cu); // one workgroup per CU (LDS, 14-16 waves at <= 128 VGPRs)
     const bool    timed = ctx->timing && (ctx->timing_calls++ % ctx->timing_every) == ctx->timing_every - 1;
     KernelTimer   t{};
     if (timed) t = take_timer(ctx, KM_FINAL, bytes);
-    HIP_OK(launch_contrast_records(fast, a, r, grid, stream, timed ? t.start : nullptr, timed ? t.stop : nullptr));
+    HIP_OK(launch_contrast_records(fast, split, a, r, grid, stream, timed ? t.start : nullptr, timed ? t.stop : nullptr));
     if (timed) ctx->timers.push_back(t);
     phase(6);
     release_slot(ctx, slot, stream);
@@ -1675,8 +1727,11 @@ int aeon_hip_ctx_create(int device, aeon_hip_ctx** out)
             ensure_ring(c, 128 * 1024, 64 * 1024, 8 * 1024);
             // diagnostics: host time per phase (printed at destroy); the multi-pass path for every call
             if (const char* e = std::getenv("AEON_HIP_HOST_PROFILE")) c->host_profile = std::atoi(e) != 0;
+            if (c->host_profile) std::fprintf(stderr, "[aeon_hip] job tables in HBM (BAR writes): %d\n", (int)c->vram_jobs);
             if (const char* e = std::getenv("AEON_HIP_DIRECT")) c->direct = std::atoi(e) != 0;
             if (const char* e = std::getenv("AEON_HIP_RECORDS")) c->records = std::atoi(e) != 0;
+            if (const char* e = std::getenv("AEON_HIP_REC_HELPERS")) c->rec_helpers = std::max(0, std::min(4, std::atoi(e)));
+            if (const char* e = std::getenv("AEON_HIP_REC_PHASES")) c->rec_phases = std::atoi(e);
             if (const char* e = std::getenv("AEON_HIP_JPEG_HUFF")) c->jpeg_gpu_huff = std::strcmp(e, "host") != 0;
             if (const char* e = std::getenv("AEON_HIP_FUSE_MASKS")) c->fuse_masks = std::atoi(e) != 0;
 #ifdef AEON_HIP_TRACE

@@ -1,17 +1,22 @@
-// stager.cpp -- the aeon-side drop-in's staging + window flush (aeon_hip_stager_*, include/aeon_hip.h).
+// stager.cpp -- the aeon-side drop-in's staging + window launch (aeon_hip_stager_*, include/aeon_hip.h).
 //
 // aeon runs provide(idx, record, out_buf) for every record of a decode window on its pool and then
 // (the one-line change) post_process(out_buf) once per batch of the window
 // (src/batch_decoder.cpp:62-99).  A stager is what provider::image / provider::pixelmask hold to make
-// those two calls the GPU path:
+// those calls the GPU path:
 //   stage(batch_out, idx, pixels, params)  -- provide(): the decoded record's bytes into pinned memory
 //                                            (lock-free bump allocation in pinned chunks; concurrent)
-//   flush(batch_out)                       -- post_process(): the FIRST flush after a window's stages
+//   launch(batch_out)                      -- post_process(): the FIRST call after a window's stages
 //                                            launches the whole window -- one H2D per pinned chunk, ONE
 //                                            augment (or mask) launch over every staged record of every
 //                                            batch, one D2H per batch buffer (or, for pinned batch
-//                                            buffers, the kernels store into them directly) -- and
-//                                            every flush waits only for its own batch's output.
+//                                            buffers, the kernels store into them directly) -- on the
+//                                            window's own stream, and returns
+//   wait(batch_out)                        -- the consumer (batch_iterator_fbm::filler) before it swaps
+//                                            or copies the batch: blocks until that batch is complete
+//   flush(batch_out)                       -- launch + wait (post_process that returns a finished batch)
+// Two windows are kept, as aeon's async_manager keeps two containers (src/async_manager.hpp:162-204):
+// while window k's copies and kernels run, window k+1 stages into the other one.
 // The batch buffer's own address (out_buf[name]->get_item(0)) is the staging key: batches of one
 // window never share it.
 #include <hip/hip_runtime.h>
@@ -24,6 +29,7 @@
 #include <mutex>
 #include <stdexcept>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/aeon_hip.h"
@@ -84,7 +90,27 @@ struct Batch {
     int        first = 0;     // its first record in the window's launch order
     int        n     = 0;     // records staged (idx 0..n-1)
     hipEvent_t done  = nullptr;
-    bool       flushed = false;
+    bool       launched = false; // a flush / launch named this batch buffer
+    bool       waited   = false; // a flush / wait returned (or is returning) its completion
+};
+
+// A decode window: its pinned staging, its batches, its own stream and device buffers, so that window
+// k's copies and kernels run while window k+1 is staged (aeon's async_manager keeps two containers in
+// flight, src/async_manager.hpp:162-204).
+struct Window {
+    enum State { IDLE, STAGING, LAUNCHED };
+    State                               state = IDLE;
+    uint64_t                            gen   = 0; // launch generation (a retire checks it)
+    std::vector<Chunk>                  chunks;
+    int                                 cur = 0; // chunk being filled
+    std::vector<std::unique_ptr<Batch>> batches; // in first-stage order
+    int                                 unwaited = 0;
+    hipStream_t                         stream  = nullptr;
+    hipEvent_t                          done    = nullptr;
+    uint8_t*                            dev_src = nullptr;
+    size_t                              dev_src_cap = 0;
+    uint8_t*                            dev_out = nullptr;
+    size_t                              dev_out_cap = 0;
 };
 
 } // namespace
@@ -95,22 +121,20 @@ struct aeon_hip_stager {
     aeon_out_desc out{};
     int           batch = 0;
     int           device = 0;
-    hipStream_t   stream = nullptr;
     std::mutex    mu;
-    std::vector<Chunk>                  chunks;
-    int                                 cur = 0; // chunk being filled
-    std::vector<std::unique_ptr<Batch>> batches; // this window's, in first-stage order
-    std::vector<hipEvent_t>             spare_events;
-    bool          launched = false;
-    int           unflushed = 0;
-    hipEvent_t    window_done = nullptr;
-    uint8_t*      dev_src = nullptr;
-    size_t        dev_src_cap = 0;
-    uint8_t*      dev_out = nullptr;
-    size_t        dev_out_cap = 0;
+    Window        win[2];
+    int           cur = 0; // the window stages go to
+    uint64_t      gens = 0;
+    std::vector<hipEvent_t> spare_events;
 };
 
 namespace {
+
+// Batch buffers of launched windows -> their stager, for aeon_hip_stager_wait(NULL, buffer) (the
+// consumer, batch_iterator_fbm::filler, knows the buffers but not the providers).  Lock order: a
+// stager's mu may be held when g_reg_mu is taken, never the reverse.
+std::mutex                                   g_reg_mu;
+std::unordered_map<void*, aeon_hip_stager*> g_pending;
 
 template <typename F>
 int stager_guarded(F&& f)
@@ -130,48 +154,71 @@ int stager_guarded(F&& f)
 void grow(uint8_t*& p, size_t& cap, size_t need)
 {
     if (need <= cap) return;
+    const size_t n = std::max(need, cap + cap / 2);
     if (p) hip_ok(hipFree(p), "hipFree");
     p = nullptr, cap = 0;
-    const size_t n = std::max(need, cap + cap / 2);
     hip_ok(hipMalloc((void**)&p, n), "hipMalloc");
     cap = n;
 }
 
-// Forget the completed window: batches gone, chunks empty (their memory is kept).
-void reset_window(aeon_hip_stager* s)
+// Forget a completed (or dropped) window: batches gone, chunks empty (their memory is kept).  Caller
+// holds s->mu.
+void reset_window(aeon_hip_stager* s, Window& w)
 {
-    for (auto& b : s->batches)
+    if (w.state == Window::LAUNCHED) {
+        std::lock_guard<std::mutex> r(g_reg_mu);
+        for (auto& b : w.batches) {
+            auto it = g_pending.find(b->out);
+            if (it != g_pending.end() && it->second == s) g_pending.erase(it);
+        }
+    }
+    for (auto& b : w.batches)
         if (b->done) s->spare_events.push_back(b->done);
-    s->batches.clear();
-    for (Chunk& c : s->chunks) c.used = 0;
-    s->cur       = 0;
-    s->launched  = false;
-    s->unflushed = 0;
+    w.batches.clear();
+    for (Chunk& c : w.chunks) c.used = 0;
+    w.cur      = 0;
+    w.state    = Window::IDLE;
+    w.unwaited = 0;
+}
+
+// The window stages go to, under s->mu: the current one unless it was launched, else the other one --
+// which, if it is still in flight (its consumer never waited for it), is completed and dropped first.
+Window& staging_window(aeon_hip_stager* s)
+{
+    if (s->win[s->cur].state != Window::LAUNCHED) return s->win[s->cur];
+    s->cur    = 1 - s->cur;
+    Window& w = s->win[s->cur];
+    if (w.state == Window::LAUNCHED) {
+        hip_ok(hipSetDevice(s->device), "hipSetDevice");
+        hip_ok(hipEventSynchronize(w.done), "hipEventSynchronize");
+        reset_window(s, w);
+    }
+    return w;
 }
 
 // Reserve `bytes` (16-aligned) of pinned staging: returns (chunk, offset).  Caller holds s->mu.
-std::pair<int, size_t> reserve(aeon_hip_stager* s, size_t bytes)
+std::pair<int, size_t> reserve(Window& w, size_t bytes)
 {
     bytes = (bytes + 15) & ~(size_t)15;
-    for (;; s->cur++) {
-        if (s->cur == (int)s->chunks.size()) {
+    for (;; w.cur++) {
+        if (w.cur == (int)w.chunks.size()) {
             Chunk c;
             c.cap = std::max(kChunkBytes, bytes);
             hip_ok(hipHostMalloc((void**)&c.host, c.cap, hipHostMallocDefault), "hipHostMalloc");
-            s->chunks.push_back(c);
+            w.chunks.push_back(c);
         }
-        Chunk& c = s->chunks[s->cur];
+        Chunk& c = w.chunks[w.cur];
         if (c.used + bytes <= c.cap) {
             const size_t off = c.used;
             c.used += bytes;
-            return {s->cur, off};
+            return {w.cur, off};
         }
     }
 }
 
-Batch& batch_for(aeon_hip_stager* s, void* out)
+Batch& batch_for(aeon_hip_stager* s, Window& w, void* out)
 {
-    for (auto& b : s->batches)
+    for (auto& b : w.batches)
         if (b->out == out) return *b;
     auto b  = std::make_unique<Batch>();
     b->out  = out;
@@ -179,29 +226,30 @@ Batch& batch_for(aeon_hip_stager* s, void* out)
     b->params.resize(s->batch);
     b->have.reset(new std::atomic<uint8_t>[s->batch]);
     for (int i = 0; i < s->batch; i++) b->have[i] = 0;
-    s->batches.push_back(std::move(b));
-    return *s->batches.back();
+    w.batches.push_back(std::move(b));
+    return *w.batches.back();
 }
 
-// The window's launch (the first flush): H2D of the pinned chunks, one kernel launch over every
-// staged record, then per batch buffer its D2H (or zero-copy stores) and completion event.
-void launch_window(aeon_hip_stager* s)
+// The window's launch (the first flush / launch): H2D of the pinned chunks, one kernel launch over every
+// staged record, then per batch buffer its D2H (or zero-copy stores) and completion event, all on the
+// window's stream.  Caller holds s->mu.
+void launch_window(aeon_hip_stager* s, Window& w)
 {
     size_t total = 0;
-    for (Chunk& c : s->chunks) {
+    for (Chunk& c : w.chunks) {
         c.base = total;
         total += c.used;
     }
-    grow(s->dev_src, s->dev_src_cap, std::max<size_t>(total, 16));
-    for (const Chunk& c : s->chunks)
+    grow(w.dev_src, w.dev_src_cap, std::max<size_t>(total, 16));
+    for (const Chunk& c : w.chunks)
         if (c.used)
-            hip_ok(hipMemcpyAsync(s->dev_src + c.base, c.host, c.used, hipMemcpyHostToDevice, s->stream),
+            hip_ok(hipMemcpyAsync(w.dev_src + c.base, c.host, c.used, hipMemcpyHostToDevice, w.stream),
                    "hipMemcpyAsync");
     std::vector<aeon_img_desc>   descs;
     std::vector<aeon_aug_params> params;
     std::vector<void*>           views;
     bool                         all_mapped = true;
-    for (auto& bp : s->batches) {
+    for (auto& bp : w.batches) {
         Batch& b = *bp;
         b.n = 0;
         while (b.n < s->batch && b.have[b.n]) b.n++;
@@ -210,7 +258,7 @@ void launch_window(aeon_hip_stager* s)
         b.first = (int)descs.size();
         for (int i = 0; i < b.n; i++) {
             aeon_img_desc d = b.descs[i];
-            d.offset        = s->chunks[d.offset >> 48].base + (d.offset & ((1ull << 48) - 1));
+            d.offset        = w.chunks[d.offset >> 48].base + (d.offset & ((1ull << 48) - 1));
             descs.push_back(d);
             params.push_back(b.params[i]);
         }
@@ -222,38 +270,112 @@ void launch_window(aeon_hip_stager* s)
     auto run = [&](int first, int n, void* dst) {
         if (n == 0) return;
         if ((s->kind & ~AEON_STAGER_DEVICE_OUT) == AEON_STAGER_MASK)
-            abi_ok(aeon_hip_mask_batch(s->ctx, n, descs.data() + first, s->dev_src, params.data() + first, &s->out,
-                                       dst, s->stream));
+            abi_ok(aeon_hip_mask_batch(s->ctx, n, descs.data() + first, w.dev_src, params.data() + first, &s->out,
+                                       dst, w.stream));
         else
-            abi_ok(aeon_hip_augment_batch(s->ctx, n, descs.data() + first, s->dev_src, params.data() + first, &s->out,
-                                          dst, s->stream));
+            abi_ok(aeon_hip_augment_batch(s->ctx, n, descs.data() + first, w.dev_src, params.data() + first, &s->out,
+                                          dst, w.stream));
     };
     const bool on_device = (s->kind & AEON_STAGER_DEVICE_OUT) != 0;
     if (on_device || all_mapped) {
         // outputs the kernels can store into directly (device batch buffers, or pinned host ones over
         // PCIe): one launch per batch, queued back to back
-        for (size_t k = 0; k < s->batches.size(); k++) {
-            Batch& b = *s->batches[k];
+        for (size_t k = 0; k < w.batches.size(); k++) {
+            Batch& b = *w.batches[k];
             run(b.first, b.n, on_device ? b.out : views[k]);
-            hip_ok(hipEventRecord(b.done, s->stream), "hipEventRecord");
+            hip_ok(hipEventRecord(b.done, w.stream), "hipEventRecord");
         }
     } else {
         // pageable host batches: the whole window in ONE launch into device memory, then a D2H into
         // each batch buffer
-        grow(s->dev_out, s->dev_out_cap, std::max<size_t>(descs.size() * item, 16));
-        run(0, (int)descs.size(), s->dev_out);
-        for (auto& bp : s->batches) {
+        grow(w.dev_out, w.dev_out_cap, std::max<size_t>(descs.size() * item, 16));
+        run(0, (int)descs.size(), w.dev_out);
+        for (auto& bp : w.batches) {
             Batch& b = *bp;
             if (b.n)
-                hip_ok(hipMemcpyAsync(b.out, s->dev_out + (size_t)b.first * item, (size_t)b.n * item,
-                                      hipMemcpyDeviceToHost, s->stream),
+                hip_ok(hipMemcpyAsync(b.out, w.dev_out + (size_t)b.first * item, (size_t)b.n * item,
+                                      hipMemcpyDeviceToHost, w.stream),
                        "hipMemcpyAsync");
-            hip_ok(hipEventRecord(b.done, s->stream), "hipEventRecord");
+            hip_ok(hipEventRecord(b.done, w.stream), "hipEventRecord");
         }
     }
-    hip_ok(hipEventRecord(s->window_done, s->stream), "hipEventRecord");
-    s->launched  = true;
-    s->unflushed = (int)s->batches.size();
+    hip_ok(hipEventRecord(w.done, w.stream), "hipEventRecord");
+    w.state    = Window::LAUNCHED;
+    w.gen      = ++s->gens;
+    w.unwaited = (int)w.batches.size();
+    std::lock_guard<std::mutex> r(g_reg_mu);
+    for (auto& b : w.batches) g_pending[b->out] = s;
+}
+
+// Launch the staging window if batch_out belongs to it (the first post_process of a window); mark
+// batch_out launched.  Caller holds s->mu.
+void launch_for(aeon_hip_stager* s, void* batch_out)
+{
+    hip_ok(hipSetDevice(s->device), "hipSetDevice");
+    Window& sw = s->win[s->cur];
+    if (sw.state == Window::STAGING) {
+        bool mine = false;
+        for (auto& b : sw.batches) mine = mine || b->out == batch_out;
+        if (mine) {
+            try {
+                launch_window(s, sw);
+            } catch (...) { // nothing of this window is delivered: drop it whole
+                (void)hipStreamSynchronize(sw.stream);
+                sw.state = Window::STAGING; // (never registered)
+                reset_window(s, sw);
+                throw;
+            }
+        }
+    }
+    for (Window& w : s->win) {
+        if (w.state != Window::LAUNCHED) continue;
+        for (auto& b : w.batches)
+            if (b->out == batch_out && !b->waited) {
+                if (b->launched) fail(AEON_HIP_EINVAL, "batch buffer flushed twice in one window");
+                b->launched = true;
+                return;
+            }
+    }
+    fail(AEON_HIP_EINVAL, "no records of this window were staged for this batch buffer");
+}
+
+// Wait until batch_out's outputs are complete.  found = false: no launched window holds it (nothing to
+// wait for).  The window's last wait checks the device error word and retires the window -- unless it
+// was dropped and reused meanwhile (its generation changed).
+void wait_batch(aeon_hip_stager* s, void* batch_out, bool& found)
+{
+    hipEvent_t ev = nullptr, wdone = nullptr;
+    hipStream_t wstream = nullptr;
+    Window*     wp  = nullptr;
+    uint64_t    gen = 0;
+    bool        last = false;
+    {
+        std::lock_guard<std::mutex> l(s->mu);
+        for (Window& w : s->win) {
+            if (w.state != Window::LAUNCHED || ev) continue;
+            for (auto& b : w.batches)
+                if (b->out == batch_out && !b->waited) {
+                    b->waited = true;
+                    ev        = b->done;
+                    wp = &w, gen = w.gen, wdone = w.done, wstream = w.stream;
+                    last = --w.unwaited == 0;
+                    break;
+                }
+        }
+    }
+    found = ev != nullptr;
+    if (!found) return;
+    hip_ok(hipSetDevice(s->device), "hipSetDevice");
+    hip_ok(hipEventSynchronize(ev), "hipEventSynchronize");
+    if (!last) return;
+    // the window is complete: surface a device error word, then free it for the window after next
+    hip_ok(hipEventSynchronize(wdone), "hipEventSynchronize");
+    const int rc = aeon_hip_synchronize(s->ctx, wstream);
+    {
+        std::lock_guard<std::mutex> l(s->mu);
+        if (wp->state == Window::LAUNCHED && wp->gen == gen) reset_window(s, *wp);
+    }
+    abi_ok(rc);
 }
 
 } // namespace
@@ -275,8 +397,10 @@ int aeon_hip_stager_create(aeon_hip_ctx* ctx, int kind, const aeon_out_desc* out
         s->out   = *out;
         s->batch = batch_size;
         hip_ok(hipGetDevice(&s->device), "hipGetDevice");
-        hip_ok(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking), "hipStreamCreate");
-        hip_ok(hipEventCreateWithFlags(&s->window_done, hipEventDisableTiming), "hipEventCreate");
+        for (Window& w : s->win) {
+            hip_ok(hipStreamCreateWithFlags(&w.stream, hipStreamNonBlocking), "hipStreamCreate");
+            hip_ok(hipEventCreateWithFlags(&w.done, hipEventDisableTiming), "hipEventCreate");
+        }
         *result = s.release();
     });
 }
@@ -285,14 +409,20 @@ int aeon_hip_stager_destroy(aeon_hip_stager* s)
 {
     if (!s) return 0;
     (void)hipSetDevice(s->device);
-    if (s->launched) (void)hipEventSynchronize(s->window_done);
-    reset_window(s);
-    for (hipEvent_t e : s->spare_events) (void)hipEventDestroy(e);
-    for (Chunk& c : s->chunks) (void)hipHostFree(c.host);
-    if (s->dev_src) (void)hipFree(s->dev_src);
-    if (s->dev_out) (void)hipFree(s->dev_out);
-    if (s->window_done) (void)hipEventDestroy(s->window_done);
-    if (s->stream) (void)hipStreamDestroy(s->stream);
+    {
+        std::lock_guard<std::mutex> l(s->mu);
+        for (Window& w : s->win) {
+            if (w.state == Window::LAUNCHED) (void)hipEventSynchronize(w.done);
+            reset_window(s, w);
+            for (Chunk& c : w.chunks) (void)hipHostFree(c.host);
+            if (w.dev_src) (void)hipFree(w.dev_src);
+            if (w.dev_out) (void)hipFree(w.dev_out);
+            if (w.done) (void)hipEventDestroy(w.done);
+            if (w.stream) (void)hipStreamDestroy(w.stream);
+        }
+        for (hipEvent_t e : s->spare_events) (void)hipEventDestroy(e);
+        s->spare_events.clear();
+    }
     delete s;
     return 0;
 }
@@ -315,12 +445,9 @@ int aeon_hip_stager_stage(aeon_hip_stager* s, void* batch_out, int idx, const vo
         size_t   tag;
         {
             std::lock_guard<std::mutex> l(s->mu);
-            if (s->launched) { // the previous window (some batch never flushed): let it finish, start anew
-                hip_ok(hipSetDevice(s->device), "hipSetDevice");
-                hip_ok(hipEventSynchronize(s->window_done), "hipEventSynchronize");
-                reset_window(s);
-            }
-            b = &batch_for(s, batch_out);
+            Window& w = staging_window(s);
+            w.state   = Window::STAGING;
+            b         = &batch_for(s, w, batch_out);
             if (!b->done) {
                 if (!s->spare_events.empty()) {
                     b->done = s->spare_events.back();
@@ -331,11 +458,12 @@ int aeon_hip_stager_stage(aeon_hip_stager* s, void* batch_out, int idx, const vo
                 }
             }
             if (b->have[idx]) fail(AEON_HIP_EINVAL, "idx " + std::to_string(idx) + " staged twice for one batch");
-            const auto r = reserve(s, row * height);
-            dst          = s->chunks[r.first].host + r.second;
+            const auto r = reserve(w, row * height);
+            dst          = w.chunks[r.first].host + r.second;
             tag          = ((size_t)r.first << 48) | r.second;
         }
-        // the copy itself runs unlocked, on the calling pool thread
+        // the copy itself runs unlocked, on the calling pool thread (the window cannot launch before
+        // this provide() returns: aeon flushes after its pool run)
         if ((size_t)stride == row) std::memcpy(dst, pixels, row * height);
         else
             for (int y = 0; y < height; y++) std::memcpy(dst + y * row, (const uint8_t*)pixels + (size_t)y * stride, row);
@@ -345,44 +473,41 @@ int aeon_hip_stager_stage(aeon_hip_stager* s, void* batch_out, int idx, const vo
     });
 }
 
+int aeon_hip_stager_launch(aeon_hip_stager* s, void* batch_out)
+{
+    return stager_guarded([&] {
+        if (!s || !batch_out) fail(AEON_HIP_EINVAL, "null argument");
+        std::lock_guard<std::mutex> l(s->mu);
+        launch_for(s, batch_out);
+    });
+}
+
+int aeon_hip_stager_wait(aeon_hip_stager* s, void* batch_out)
+{
+    return stager_guarded([&] {
+        if (!batch_out) fail(AEON_HIP_EINVAL, "null argument");
+        if (!s) { // the consumer's form: whichever stager launched this buffer, if any
+            std::lock_guard<std::mutex> r(g_reg_mu);
+            auto it = g_pending.find(batch_out);
+            if (it == g_pending.end()) return;
+            s = it->second;
+        }
+        bool found = false;
+        wait_batch(s, batch_out, found);
+    });
+}
+
 int aeon_hip_stager_flush(aeon_hip_stager* s, void* batch_out)
 {
     return stager_guarded([&] {
         if (!s || !batch_out) fail(AEON_HIP_EINVAL, "null argument");
-        hipEvent_t ev   = nullptr;
-        bool       last = false;
         {
             std::lock_guard<std::mutex> l(s->mu);
-            hip_ok(hipSetDevice(s->device), "hipSetDevice");
-            if (!s->launched) {
-                if (s->batches.empty()) fail(AEON_HIP_EINVAL, "flush without staged records");
-                try {
-                    launch_window(s);
-                } catch (...) { // nothing of this window is delivered: drop it whole
-                    (void)hipStreamSynchronize(s->stream);
-                    reset_window(s);
-                    throw;
-                }
-            }
-            Batch* b = nullptr;
-            for (auto& bp : s->batches)
-                if (bp->out == batch_out) b = bp.get();
-            if (!b) fail(AEON_HIP_EINVAL, "no records of this window were staged for this batch buffer");
-            if (b->flushed) fail(AEON_HIP_EINVAL, "batch buffer flushed twice in one window");
-            b->flushed = true;
-            ev         = b->done;
-            last       = --s->unflushed == 0;
+            launch_for(s, batch_out);
         }
-        hip_ok(hipEventSynchronize(ev), "hipEventSynchronize");
-        if (last) {
-            // the window is complete: surface a device error word, then take the next window's stages
-            const int rc = aeon_hip_synchronize(s->ctx, s->stream);
-            {
-                std::lock_guard<std::mutex> l(s->mu);
-                reset_window(s);
-            }
-            abi_ok(rc);
-        }
+        bool found = false;
+        wait_batch(s, batch_out, found);
+        if (!found) fail(AEON_HIP_EINVAL, "batch buffer completed by another thread's wait");
     });
 }
 

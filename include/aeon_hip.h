@@ -342,11 +342,21 @@ int aeon_manifest_node_slice(int64_t record_count, int batch_size, int node_id, 
  *   aeon_hip_stager_stage (from provide(), any pool thread, concurrently): record idx of the batch whose
  *     buffer is batch_out (out_buf[name]->get_item(0): the staging key) -- its decoded pixels (HWC,
  *     copied into pinned memory before the call returns) and its augment::image::params.
- *   aeon_hip_stager_flush (from post_process(), the filler thread): the first flush after a window's
- *     stages launches the WHOLE window -- one H2D per pinned staging chunk, one augment (or pixel-mask)
- *     launch over every staged record of every batch, a D2H into each batch buffer (pinned,
- *     device-mapped batch buffers are stored into directly; AEON_STAGER_DEVICE_OUT: batch_out is device
- *     memory) -- and each flush returns once ITS batch buffer is complete.  A batch must hold idx 0..n-1.
+ *   aeon_hip_stager_launch (from post_process(), the filler thread): the first launch after a window's
+ *     stages launches the WHOLE window on the window's own stream -- one H2D per pinned staging chunk,
+ *     one augment (or pixel-mask) launch over every staged record of every batch, a D2H into each batch
+ *     buffer (pinned, device-mapped batch buffers are stored into directly; AEON_STAGER_DEVICE_OUT:
+ *     batch_out is device memory) -- and returns without waiting; later launches of the window's other
+ *     batches only mark them.  A batch must hold idx 0..n-1.
+ *   aeon_hip_stager_wait (from the consumer, batch_iterator_fbm::filler, src/batch_iterator.cpp:109-142,
+ *     before it swaps or copies a batch out of the decoded container): returns once batch_out is
+ *     complete.  stager may be NULL: the library finds the stager that launched batch_out (the consumer
+ *     knows the buffers, not the providers); a buffer no stager launched (another ETL's, or one already
+ *     waited for) returns 0 at once.  The window's last wait surfaces the device error word.
+ *   aeon_hip_stager_flush: launch + wait for batch_out (a post_process that returns a finished batch).
+ * Two windows are kept (aeon's async_manager, src/async_manager.hpp:162-204, has two containers): the
+ * stages of window k+1 go to the other one while window k's copies and kernels run; staging a third
+ * window while the first was never waited for completes and drops that first one.
  * Images: aeon_hip_augment_batch semantics; masks (AEON_STAGER_MASK): aeon_hip_mask_batch, staged with
  * the record's image params (provider.cpp:378-391).  Errors: AEON_HIP_E* codes,
  * aeon_hip_stager_last_error(); a window whose launch fails is dropped whole. */
@@ -359,6 +369,8 @@ int aeon_hip_stager_create(aeon_hip_ctx* ctx, int kind, const aeon_out_desc* out
 int aeon_hip_stager_destroy(aeon_hip_stager* stager);
 int aeon_hip_stager_stage(aeon_hip_stager* stager, void* batch_out, int idx, const void* pixels, int width,
                           int height, int stride, int channels, int elem_bytes, const aeon_aug_params* params);
+int aeon_hip_stager_launch(aeon_hip_stager* stager, void* batch_out);
+int aeon_hip_stager_wait(aeon_hip_stager* stager, void* batch_out);
 int aeon_hip_stager_flush(aeon_hip_stager* stager, void* batch_out);
 const char* aeon_hip_stager_last_error(void);
 

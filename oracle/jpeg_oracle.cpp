@@ -355,6 +355,12 @@ struct Decoder {
                     sc.push_back(k);
                 }
                 const int Ss = u8(), Se = u8(), AhAl = u8();
+                // jdinput.c per_scan_setup: JERR_BAD_MCU_SIZE past D_MAX_BLOCKS_IN_MCU (10) blocks per MCU
+                if (ns > 1) {
+                    int mb = 0;
+                    for (int k : sc) mb += comps[k].h * comps[k].v;
+                    if (mb > 10) bad("sampling factors too large for an interleaved scan");
+                }
                 p = seg + len - 2;
                 if (progressive) prog_scan(sc, Ss, Se, AhAl >> 4, AhAl & 15);
                 else scan(sc);

@@ -99,6 +99,8 @@ class DrawOrder:
 class HipImageProvider:
     """provider::image, HIP flavour (INTEGRATION.md)."""
 
+    overlap = False
+
     def __init__(self, ctx, etl, aug, batch, where, factory):
         self.name = "image"
         self.item = C.out_desc_for(etl, aug).item_stride
@@ -115,7 +117,10 @@ class HipImageProvider:
         self.stager.stage(out_buf[self.name].ptr, idx, img, aug.image_params)
 
     def post_process(self, out_buf):
-        self.stager.flush(out_buf[self.name].ptr)
+        if self.overlap:  # launch only: the consumer waits (batch_iterator_fbm::filler edit)
+            self.stager.launch(out_buf[self.name].ptr)
+        else:
+            self.stager.flush(out_buf[self.name].ptr)
 
 
 class HipPixelmaskProvider(HipImageProvider):
@@ -237,10 +242,138 @@ def test_stager_errors():
         for i in range(4):
             st.stage(buf.ctypes.data, i, img, p)
         with pytest.raises(A.AeonHipError):
-            st.flush(other.ctypes.data)  # not staged in this window (the window is launched by it)
+            st.flush(other.ctypes.data)  # not staged in this window
         st.flush(buf.ctypes.data)
         ref = H.oracle_records([img], [p], out)[0]
         assert np.array_equal(buf[:out.item_stride].view(np.float32), ref.reshape(-1))
+    finally:
+        st.close()
+        ctx.close()
+
+
+def _check_window(cfg, aug, etl, provs, records, checker_states, batch, nbatches, read):
+    """Every batch of a window against the oracle; read(b, name) -> the batch buffer's bytes."""
+    chk = A.ParamFactory(aug)
+    params = []
+    for i, r in enumerate(records):
+        st = checker_states[i:i + 1]
+        params.append(chk.make_params(st, r[0].shape[1], r[0].shape[0], etl[0]["width"], etl[0]["height"]))
+        checker_states[i] = st[0]
+    for k, (p, e) in enumerate(zip(provs, etl)):
+        od = C.out_desc_for(e, aug)
+        ref = H.oracle_records([r[k] for r in records], params, od, mask=(k == 1))
+        dt = A.NP_DTYPE[od.dtype]
+        n = p.item // np.dtype(dt).itemsize
+        for b in range(nbatches):
+            got = read(b, p.name).view(dt)
+            for i in range(batch):
+                assert np.array_equal(got[i * n:(i + 1) * n], ref[b * batch + i].reshape(-1)), (cfg, p.name, b, i)
+
+
+@pytest.mark.parametrize("cfg,where", [("C2", "pageable"), ("C5", "pageable"), ("C3", "pinned"), ("C2", "device")])
+def test_overlapped_windows_consumer_waits(cfg, where):
+    """aeon's async_manager with the second aeon-side edit: the decode stage (batch_decoder::filler) runs
+    provide() on its pool and post_process() per batch, which only LAUNCHES the window, and hands the
+    container on; the consumer (batch_iterator_fbm::filler) calls aeon_hip_stager_wait(NULL, buffer) for
+    every buffer of a batch before it copies the batch out.  Two containers alternate
+    (src/async_manager.hpp:162-204), so window k's GPU work overlaps window k+1's provide() calls.  Four
+    windows; every batch bit-exact against the oracle."""
+    import queue
+    aug = {"C2": C.C2_AUG, "C3": C.C3_AUG, "C5": C.C5_AUG}[cfg]
+    etl = [C.IMAGE_512, C.MASK_512] if cfg == "C5" else [C.IMAGE_224]
+    batch, nbatches, seed = (16, 4, 5) if cfg == "C5" else (32, 4, 3)
+    decode_size, nwin = batch * nbatches, 4
+    ctx = A.Context(0)
+    factory = A.ParamFactory(aug)
+    kinds = [HipImageProvider, HipPixelmaskProvider]
+    provs = [kinds[k](ctx, e, aug, batch, where, factory) for k, e in enumerate(etl)]
+    for p in provs:
+        p.overlap = True
+    base = ProviderBase(provs)
+    shapes = [(p.name, p.item) for p in provs]
+    containers = [[FixedBufferMap(shapes, batch, where) for _ in range(nbatches)] for _ in range(2)]
+    engines = A.seed_slots(seed, decode_size)
+    checker_states = engines.copy()
+    free_q, full_q = queue.Queue(), queue.Queue()
+    for c in range(2):
+        free_q.put(c)
+    all_records = [_records(cfg, decode_size, seed=100 + w) for w in range(nwin)]
+    errors = []
+
+    def decode_stage():  # async_manager::run_filler over batch_decoder::filler
+        try:
+            with ThreadPoolExecutor(max_workers=8) as pool:
+                for w in range(nwin):
+                    c = free_q.get()
+                    outputs, records, order = containers[c], all_records[w], DrawOrder()
+
+                    def process(index):
+                        eng = engines[index:index + 1]
+                        base.provide(index % batch, records[index], outputs[index // batch], eng, order, index)
+
+                    list(pool.map(process, range(decode_size)))
+                    for b in range(nbatches):
+                        base.post_process(outputs[b])  # launch only
+                    full_q.put((w, c))
+        except Exception as e:  # pragma: no cover - surfaced below
+            errors.append(e)
+            full_q.put(None)
+
+    th = threading.Thread(target=decode_stage)
+    th.start()
+    try:
+        for _ in range(nwin):  # batch_iterator_fbm::filler, per decoded container
+            item = full_q.get(timeout=120)
+            assert item is not None, errors
+            w, c = item
+            copies = {}
+            for b in range(nbatches):
+                for name, _ in shapes:
+                    buf = containers[c][b][name]
+                    A.Stager.wait_buffer(buf.ptr)  # the second aeon-side edit
+                    copies[(b, name)] = buf.bytes().copy()  # the swap / copy out of the container
+            free_q.put(c)  # the container goes back to the decode stage
+            _check_window(cfg, aug, etl, provs, all_records[w], checker_states, batch, nbatches,
+                          lambda b, name: copies[(b, name)])
+        th.join(timeout=120)
+        assert not errors, errors
+    finally:
+        th.join(timeout=120)
+        for p in provs:
+            p.stager.close()
+        for cont in containers:
+            for o in cont:
+                for bf in o.buf.values():
+                    bf.free()
+        ctx.close()
+
+
+def test_stager_launch_wait_errors():
+    """launch() of a batch staged in no window; a second launch of one batch; wait() of a buffer no stager
+    launched returns at once; a third window staged while the first was never waited for drops the first."""
+    ctx = A.Context(0)
+    out = C.out_desc_for(C.IMAGE_224, C.C2_AUG)
+    st = A.Stager(ctx, out, 2)
+    f = A.ParamFactory(C.C2_AUG)
+    p = f.make_params(A.seed_slots(1, 1), 300, 300, 224, 224)
+    img = A.synthetic_image(3, 300, 300, 3)
+    bufs = [np.zeros(2 * out.item_stride, np.uint8) for _ in range(3)]
+    ref = H.oracle_records([img], [p], out)[0].reshape(-1)
+    try:
+        with pytest.raises(A.AeonHipError):
+            st.launch(bufs[0].ctypes.data)
+        A.Stager.wait_buffer(bufs[0].ctypes.data)  # nothing launched it: returns
+        for w in range(3):  # windows 0, 1, 2 on one buffer each; nobody waits for 0 and 1
+            for i in range(2):
+                st.stage(bufs[w].ctypes.data, i, img, p)
+            st.launch(bufs[w].ctypes.data)
+            with pytest.raises(A.AeonHipError):
+                st.launch(bufs[w].ctypes.data)  # twice in one window
+        st.wait(bufs[2].ctypes.data)
+        for w in range(3):  # window 0 was completed when window 2 staged; 1 and 2 by their waits
+            A.Stager.wait_buffer(bufs[w].ctypes.data)
+            for i in range(2):
+                assert np.array_equal(bufs[w][i * out.item_stride:(i + 1) * out.item_stride].view(np.float32), ref), (w, i)
     finally:
         st.close()
         ctx.close()

@@ -64,6 +64,31 @@ def test_product_jpeg_info_rejects_garbage():
         A.jpeg_info(b[:100])  # truncated before the frame header ends
 
 
+def _mcu_too_large(name="s444_q90"):
+    """The file with every component's sampling factors set to 2x2 in its SOF0: 12 blocks per MCU of
+    its interleaved scan, past libjpeg's D_MAX_BLOCKS_IN_MCU (10)."""
+    b = bytearray(_jpg(name))
+    i = b.index(b"\xff\xc0")
+    ncomp = b[i + 9]
+    assert ncomp == 3
+    for k in range(ncomp):
+        b[i + 11 + 3 * k] = 0x22
+    return bytes(b)
+
+
+def test_interleaved_mcu_over_ten_blocks_refused(oracle):
+    """libjpeg (jdinput.c per_scan_setup) refuses an interleaved scan of more than 10 blocks per MCU with
+    JERR_BAD_MCU_SIZE, so cv::imdecode -- aeon's extract -- fails on such a file: the product's host stage
+    and host entropy decoder and the oracle refuse it too (the header alone still parses)."""
+    b = _mcu_too_large()
+    assert A.jpeg_info(b)[2] == 3
+    for fn in (A.jpeg_entropy_decode, A.jpeg_host_stage):
+        with pytest.raises(A.AeonHipError, match="sampling factors too large"):
+            fn(b)
+    with pytest.raises(Exception, match="sampling factors too large"):
+        oracle.jpeg_decode(b)
+
+
 def _decode_gpu(ctx, files, channels):
     import torch
     infos = [A.jpeg_info(b) for b in files]
