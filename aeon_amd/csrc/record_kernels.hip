@@ -137,10 +137,11 @@ __device__ __forceinline__ void rec_record_tables(const LaunchArgs& a, const Rec
 
 // Record k's table: y -> contrast (with its (1-c)*mean from the exact sums) -> lighting ->
 // standardize (the LUT in global memory), Bands::record_table's arithmetic.
-__device__ __forceinline__ void rec_table(const LaunchArgs& a, const RecLds& L, const JobRef& J, int W, int H, int nw)
+__device__ __forceinline__ void rec_table(const LaunchArgs& a, const RecLds& L, const JobRef& J, int W, int H, int nw,
+                                          int sums_at)
 {
     const int photo = JF(J, photo);
-    const auto ps   = lds_ptr<const uint32_t>(L.sums);
+    const auto ps   = lds_ptr<const uint32_t>(sums_at);
     uint32_t   s[3] = {0, 0, 0};
     for (int w = 0; w < nw; w++)
         for (int c = 0; c < 3; c++) s[c] += ps[w * 4 + c];
@@ -494,7 +495,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) void 
         }
         lds_barrier(); // also: every lane is done with this step's tiles (B's record table reads)
         stamp(k * 8 + 7, 1);
-        rec_table(a, L, JA, W, H, nw);
+        rec_table(a, L, JA, W, H, nw, L.sums);
         stamp(k * 8 + 7, 2);
         b_out = JF(JA, out_ptr);
         if (k + 1 < K) rec_record_tables(a, L, JobRef{slot(k + 1)}, W, FAST);
@@ -538,15 +539,30 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) void 
     [[maybe_unused]] const int kTraceWave = nwc; // (trace builds: the phase stamps come from the first helper)
     REC_TRACE_SETUP
 
-    hsv_div_tables(LdsLayout{0, L.hsv, 0, 0, 0, 0, 0, 0, 0, 0}, a.hsv_tables);
-    for (int i = tid; i < 3 * 256; i += nt) lds_ptr<float>(L.lut)[i] = a.lut[i];
-    for (int i = tid; i < 256 * 4; i += nt) lds_ptr<int32_t>(L.hwt)[i] = a.hsv_tables[kHsvDivWords + i];
-    if (wave == nwc) {
+    // The prologue: each helper fetches the first record's job itself (the same bytes into the same slot)
+    // and issues the first tile's staging at once, while the compute waves copy the launch's tables;
+    // the helpers unpack after the barrier that publishes the job and the tables.
+    if (helper) {
         rec_fetch_job(a, rec_of(0), slot(0));
-        if (K > 1) rec_fetch_job(a, rec_of(1), slot(1));
+        if (wave == nwc && K > 1) rec_fetch_job(a, rec_of(1), slot(1));
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (tid - nwc * 64 < 6) lds_ptr<uint32_t>(L.sums)[(tid - nwc * 64) / 3 * 4 + (tid - nwc * 64) % 3] = 0;
+    } else {
+        hsv_div_tables(LdsLayout{0, L.hsv, 0, 0, 0, 0, 0, 0, 0, 0}, a.hsv_tables);
+        for (int i = tid; i < 3 * 256; i += nwc * 64) lds_ptr<float>(L.lut)[i] = a.lut[i];
+        for (int i = tid; i < 256 * 4; i += nwc * 64) lds_ptr<int32_t>(L.hwt)[i] = a.hsv_tables[kHsvDivWords + i];
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    RecTile f0{};
+    if (helper) {
+        f0 = rec_tile(JobRef{slot(0)}, 0, TR, H, L.stage_bytes, a.error);
+        if (f0.ok) {
+            stage_issue(JobRef{slot(0)}, f0.G, L.stage, wave - nwc, nh);
+            rec_row_taps(JobRef{slot(0)}, f0, L.yt, L.stage, tid - nwc * 64, nh * 64);
+        }
+    } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    lds_barrier();
     rec_record_tables(a, L, JobRef{slot(0)}, W, FAST);
 
     if (helper) {
@@ -572,7 +588,11 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) void 
             if (stid == 0) flags[buf] = f.ok ? 1 : 0;
         };
         int par = 0;
-        stage_tile(JobRef{slot(0)}, 0, 0);
+        if (f0.ok) { // the first tile: its loads were issued in the prologue
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            stage_unpack(JobRef{slot(0)}, f0.G, L.stage, sw, nh);
+        }
+        if (stid == 0) flags[0] = f0.ok ? 1 : 0;
         for (int k = 0; k <= K; k++) {
             const bool hasA = k < K;
 #pragma unroll 1
@@ -581,6 +601,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) void 
                 stamp(k * 8 + t, 0);
                 lds_barrier(); // B1: the staged tile is published; the other buffer is free
                 stamp(k * 8 + t, 3);
+                if (t == 0 && stid < 3) lds_ptr<uint32_t>(L.sums + ((k + 1) & 1) * 16)[stid] = 0; // (see B2)
                 const bool next_same = hasA && t + 1 < TS;
                 const bool next_rec  = hasA && t + 1 == TS && k + 1 < K;
                 cur_idx = k * 8 + t;
@@ -596,7 +617,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) void 
             stamp(k * 8 + 7, 0);
             lds_barrier(); // B2: the compute waves' sums are in
             stamp(k * 8 + 7, 1);
-            rec_table(a, L, JobRef{slot(k)}, W, H, nwc);
+            rec_table(a, L, JobRef{slot(k)}, W, H, 1, L.sums + (k & 1) * 16);
             stamp(k * 8 + 7, 2);
             if (k + 1 < K) rec_record_tables(a, L, JobRef{slot(k + 1)}, W, FAST);
             stamp(k * 8 + 7, 3);
@@ -689,13 +710,16 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) void 
             if (tile_a) par ^= 1;
         }
         if (!hasA) break;
+        // the record's channel sums: one LDS add per wave into this record's set (k & 1; the helpers clear
+        // the other set in the next step, after every thread has read it for record k - 1)
         s0 = wave_sum(s0), s1 = wave_sum(s1), s2 = wave_sum(s2);
         if ((tid & 63) == 0) {
-            const auto ps = lds_ptr<uint32_t>(L.sums);
-            ps[wave * 4] = s0, ps[wave * 4 + 1] = s1, ps[wave * 4 + 2] = s2;
+            const auto ps = lds_ptr<uint32_t>(L.sums + (k & 1) * 16);
+            __atomic_fetch_add(ps, s0, __ATOMIC_RELAXED), __atomic_fetch_add(ps + 1, s1, __ATOMIC_RELAXED),
+                __atomic_fetch_add(ps + 2, s2, __ATOMIC_RELAXED);
         }
         lds_barrier(); // B2
-        rec_table(a, L, JA, W, H, nwc);
+        rec_table(a, L, JA, W, H, 1, L.sums + (k & 1) * 16);
         b_out = JF(JA, out_ptr);
         if (k + 1 < K) rec_record_tables(a, L, JobRef{slot(k + 1)}, W, FAST);
     }
