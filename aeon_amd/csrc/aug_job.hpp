@@ -131,6 +131,8 @@ struct LaunchArgs {
     const AugJob*  jobs;       // the launch's jobs: device memory, or the device view of a pinned host slot
     int32_t        jobs_host;  // jobs is pinned host memory (read through to the host)
     int32_t        job_bytes;  // bytes of each job the tiles fetch: kJobHotBytes without photometric jobs
+    int32_t        job_stride; // bytes between consecutive jobs of the table: sizeof(AugJob), or kJobHotBytes
+                               // for a direct call's compact table of hot halves
     const float*   lut;        // [3][256] per SOURCE channel: standardized value of output
                                // channel (bgr_to_rgb ? 2-c : c), or (float)x without mean
     const int32_t* hsv_tables; // sdiv[256], hdiv180[256], then per uchar H the HSV2RGB weights (B, G, R, 0) as float bits

@@ -523,7 +523,7 @@ __device__ __forceinline__ void fetch_job(const LaunchArgs& a, int t, int lds_sl
 {
     if (t < 0 || t >= a.total_tiles) return;
     const int      job  = t / a.max_tiles;
-    const auto     rs   = uniform_rsrc((const void*)(a.jobs + job), a.job_bytes);
+    const auto     rs   = uniform_rsrc((const void*)((const char*)a.jobs + (size_t)job * a.job_stride), a.job_bytes);
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t voff = lane * 4 < (uint32_t)a.job_bytes ? lane * 4 : kOutOfRange; // (the rest of the slot: 0)
     const int      base = __builtin_amdgcn_readfirstlane(lds_slot);

@@ -753,6 +753,7 @@ struct aeon_hip_ctx {
                                             // AEON_HIP_VRAM_JOBS=0: pinned host tables)
     bool                 jpeg_gpu_huff = true; // AEON_HIP_JPEG_HUFF=host: every JPEG through the host entropy decoder
     std::vector<JobGeom> geoms;              // reused per call
+    std::vector<AugJob>  direct_jobs;        // (run_direct) the call's jobs before they go into the slot
     JpegState*           jpeg = nullptr;     // JPEG decode stage (pool, staging ring), on first use
     thread_pool*         host_pool = nullptr; // the owning decoder's pool (ctx_share_pool), for the JPEG stage
     std::unique_ptr<thread_pool> plan_pool;        // the context's own, made for the first call with many Lanczos4 taps
@@ -769,6 +770,9 @@ struct aeon_hip_ctx {
         float* dev = nullptr;
     };
     std::vector<Lut> luts;
+    aeon_out_desc    lut_memo_od{}; // the last resident_lut call: its config and LUT
+    bool             lut_memo_u8  = false;
+    const float*     lut_memo_dev = nullptr;
     // per-launch timing events on every `timing_every`-th call only (they cost GPU time)
     int         timing_every = 1;
     long        timing_calls = 0;
@@ -932,21 +936,31 @@ void ensure_ring(aeon_hip_ctx* ctx, size_t table, size_t partials, size_t shifts
 // Device copy of the standardize LUT of output config `o` (uploaded the first time it is seen).
 const float* resident_lut(aeon_hip_ctx* ctx, const aeon_out_desc& o, bool u8_map = false)
 {
+    // the last call's output config again (a loader's steady state): its LUT without rebuilding it
+    if (ctx->lut_memo_dev && ctx->lut_memo_u8 == u8_map && std::memcmp(&ctx->lut_memo_od, &o, sizeof(o)) == 0)
+        return ctx->lut_memo_dev;
     float lut[768];
     build_lut(o, lut, u8_map);
+    const float* dev = nullptr;
     for (auto& L : ctx->luts)
-        if (std::memcmp(L.host, lut, sizeof(lut)) == 0) return L.dev;
-    if (ctx->luts.size() >= 16) { // many configs on one context: start over once the device is idle
-        HIP_OK(hipDeviceSynchronize());
-        for (auto& L : ctx->luts) HIP_OK(hipFree(L.dev));
-        ctx->luts.clear();
+        if (std::memcmp(L.host, lut, sizeof(lut)) == 0) dev = L.dev;
+    if (!dev) {
+        if (ctx->luts.size() >= 16) { // many configs on one context: start over once the device is idle
+            HIP_OK(hipDeviceSynchronize());
+            for (auto& L : ctx->luts) HIP_OK(hipFree(L.dev));
+            ctx->luts.clear();
+        }
+        aeon_hip_ctx::Lut L;
+        std::memcpy(L.host, lut, sizeof(lut));
+        HIP_OK(hipMalloc((void**)&L.dev, sizeof(lut)));
+        HIP_OK(hipMemcpy(L.dev, lut, sizeof(lut), hipMemcpyHostToDevice));
+        ctx->luts.push_back(L);
+        dev = L.dev;
     }
-    aeon_hip_ctx::Lut L;
-    std::memcpy(L.host, lut, sizeof(lut));
-    HIP_OK(hipMalloc((void**)&L.dev, sizeof(lut)));
-    HIP_OK(hipMemcpy(L.dev, lut, sizeof(lut), hipMemcpyHostToDevice));
-    ctx->luts.push_back(L);
-    return L.dev;
+    ctx->lut_memo_od  = o;
+    ctx->lut_memo_u8  = u8_map;
+    ctx->lut_memo_dev = dev;
+    return dev;
 }
 
 // Algorithmic bytes of one launch: the resampled u8 source footprint plus
@@ -1085,6 +1099,7 @@ LaunchArgs launch_args(aeon_hip_ctx* ctx, const Slot& s, const uint8_t* table, c
     a.tail_rounds = AEON_HIP_TAIL_ROUNDS;
     a.jobs           = (const AugJob*)(table + L.blob_off);
     a.job_bytes      = L.photo ? (int)sizeof(AugJob) : kJobHotBytes;
+    a.job_stride     = (int)sizeof(AugJob);
     a.lut            = d_lut; // [3][256]: standardized, or (float)x without mean
     a.hsv_tables     = ctx->d_hsv;
     a.partials       = s.partials;
@@ -1133,8 +1148,11 @@ bool run_direct(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void
     const aeon_out_desc& o  = ov.ko; // what the kernels write
     std::vector<JobGeom>& geo = ctx->geoms;
     geo.resize(n);
+    std::vector<AugJob>& jobs = ctx->direct_jobs; // each record planned once, copied into the slot below
+    if (jobs.size() < (size_t)n) jobs.resize(n);
     int  key = -1, max_h = 0;
     bool vec_ok = !o.fixed_aspect_ratio;
+    const OutGeom og = out_geom(o);
     for (int i = 0; i < n; i++) {
         const aeon_img_desc&   d = descs[i];
         const aeon_aug_params& p = params[i];
@@ -1143,11 +1161,11 @@ bool run_direct(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void
         if (p.angle != 0 || (!is_mask && (p.resize_short_size > 0 || expands(p)))) return false;
         if (!is_mask && p.interp > AEON_INTERP_NEAREST) return false; // CUBIC / AREA / LANCZOS4 (plan_image)
         validate_record(d, p, o, is_mask);
-        const int photo = is_mask ? 0 : photo_flags(p);
-        const int mode  = choose_mode(p.crop_w, p.crop_h, p.out_w, p.out_h, is_mask ? AEON_INTERP_NEAREST : p.interp,
-                                      d.channels);
+        AugJob& J = jobs[i];
+        plan_direct(d, (uint64_t)src_base, p, og, (uint64_t)out_dev + (uint64_t)i * o.item_stride, is_mask, J);
+        const int photo = J.photo, mode = J.mode; // (plan_direct: the cv::resize dispatch, photometric flags)
         if ((photo & PHOTO_CONTRAST) || (photo && mode == RESIZE_AREA2X)) return false;
-        const bool tail = mode == RESIZE_LINEAR && simd_boundary(p.out_w * d.channels) < p.out_w * d.channels;
+        const bool tail = mode == RESIZE_LINEAR && J.xv < p.out_w * d.channels;
         const int  k    = mode * 4 + (tail ? 2 : 0) + (photo ? 1 : 0);
         if (key < 0) key = k;
         else if (k != key) return false;
@@ -1155,8 +1173,7 @@ bool run_direct(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void
         JobGeom& g = geo[i];
         g.mode = mode, g.cn = d.channels, g.crop_w = p.crop_w, g.crop_h = p.crop_h;
         g.win_w = g.dst_w = p.out_w, g.win_h = g.dst_h = p.out_h, g.photo = photo, g.stats_slot = -1;
-        g.scale_x = 1. / ((double)p.out_w / p.crop_w);
-        g.scale_y = 1. / ((double)p.out_h / p.crop_h);
+        g.scale_x = J.scale_x, g.scale_y = J.scale_y;
         max_h     = std::max(max_h, p.out_h);
     }
     LaunchPlan P;
@@ -1179,21 +1196,23 @@ bool run_direct(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void
     phase(3);
     const float* d_lut = resident_lut(ctx, od, ov.u8_map);
     ensure_ring(ctx, (size_t)n * sizeof(AugJob), 16, 32);
-    AugJob*       jt = (AugJob*)s.host;
-    const OutGeom og = out_geom(o);
+    // without photometric stages the tiles read only each job's hot half: the table holds just those
+    // (half the bytes the host writes and publishes)
+    const size_t stride = P.photo ? sizeof(AugJob) : (size_t)kJobHotBytes;
     for (int i = 0; i < n; i++) {
-        plan_direct(descs[i], (uint64_t)src_base, params[i], og, (uint64_t)out_dev + (uint64_t)i * o.item_stride,
-                    is_mask, jt[i]);
-        jt[i].tiles = (jt[i].win_h + P.tr - 1) / P.tr;
+        AugJob& J = jobs[i];
+        J.tiles   = (J.win_h + P.tr - 1) / P.tr;
+        std::memcpy(s.host + i * stride, &J, stride);
     }
     phase(4);
-    phase(5);
     const bool timed = ctx->timing && (ctx->timing_calls++ % ctx->timing_every) == ctx->timing_every - 1;
     if (o.fixed_aspect_ratio) // std::fill_n of each item's canvas, its whole byte size (etl_image.cpp:263)
         HIP_OK(hipMemset2DAsync(out_dev, o.item_stride, 0,
                                 (size_t)o.canvas_w * o.canvas_h * o.channels * out_elem_bytes(od.dtype), n, stream));
-    const uint8_t* vt = publish_table(ctx, s, (size_t)n * sizeof(AugJob));
+    const uint8_t* vt = publish_table(ctx, s, (size_t)n * stride);
+    phase(5);
     LaunchArgs     a  = launch_args(ctx, s, vt ? vt : s.host_dev, P, n, o, d_lut, 1, ov.u8_map);
+    a.job_stride      = (int)stride;
     a.jobs_host       = 1; // (read-through loads: pinned host memory, or the uncached HBM copy)
     timed_launch(ctx, KM_FINAL, P, a, stream, launch_bytes(geo, KM_FINAL, out_elem_bytes(o.dtype)), timed);
     phase(6);
@@ -1754,7 +1773,8 @@ int aeon_hip_ctx_destroy(aeon_hip_ctx* c)
         if (!c) return 0;
         if (c->host_profile && c->host_calls) {
             static const char* names[8] = {"set_device", "plan", "group+finalize", "slot_wait",
-                                           "blob_fill", "h2d+wait_event", "launches", "done_event"};
+                                           "blob_fill", "h2d+wait_event (direct: table publish)", "launches",
+                                           "done_event"};
             std::fprintf(stderr, "[aeon_hip host profile] %ld calls, us per call (median/mean/p90):", c->host_calls);
             double total = 0;
             for (int k = 0; k < 8; k++) {

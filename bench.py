@@ -259,6 +259,10 @@ def run_device(A, C, torch, cfg, batch, steps, warmup, rank, world, pool_mib, di
     wl = Workload(A, C, torch, cfg, batch, steps + warmup, rank, pool_mib, world=world, real=real)
     # streams > 1 (development): consecutive batches alternate between caller streams, as a
     # loader double-buffering its output batches would
+    # the launches go to a stream of our own (non-blocking, as a loader's would be): HIP's legacy null
+    # stream synchronises with every blocking stream, which costs each launch host time
+    prev_stream = torch.cuda.current_stream()
+    torch.cuda.set_stream(torch.cuda.Stream())
     strs = [torch.cuda.current_stream().cuda_stream] + [torch.cuda.Stream().cuda_stream for _ in range(streams - 1)]
     stream = strs[0]
     for s in range(warmup):
@@ -271,13 +275,18 @@ def run_device(A, C, torch, cfg, batch, steps, warmup, rank, world, pool_mib, di
     torch.cuda.synchronize()
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)] if region else None
     t0 = time.perf_counter()
+    call_s = []
     for s in range(warmup, warmup + steps):
+        tc = time.perf_counter()
         wl.step(ctx, s, strs[s % streams])
+        call_s.append(time.perf_counter() - tc)
         if region and s == warmup:
             ev[0].record(torch.cuda.current_stream())  # (strs[0] is the current stream)
     if region:
         ev[1].record(torch.cuda.current_stream())
-    wl.submit_s = time.perf_counter() - t0  # host time to plan + enqueue all steps
+    # host time per call: the median call (once the host is a ring of 16 calls ahead of the GPU, a
+    # call also waits for a slot: the mean then follows the GPU, not the host's own cost)
+    wl.submit_s = sorted(call_s)[len(call_s) // 2] * steps
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     if dist:
@@ -295,6 +304,7 @@ def run_device(A, C, torch, cfg, batch, steps, warmup, rank, world, pool_mib, di
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     ctx.close()
+    torch.cuda.set_stream(prev_stream)
     return elapsed, kt, wl.param_us, wl.submit_s
 
 
