@@ -151,6 +151,7 @@ def lib():
         L.aeon_hip_stager_flush.argtypes = [vp, vp]
         L.aeon_hip_stager_launch.argtypes = [vp, vp]
         L.aeon_hip_stager_wait.argtypes = [vp, vp]
+        L.aeon_hip_release_stream.argtypes = [vp, vp]
         L.aeon_hip_stager_last_error.restype = ctypes.c_char_p
         L.aeon_hip_host_alloc.argtypes = [ctypes.c_size_t, P(vp)]
         L.aeon_hip_host_free.argtypes = [vp]
@@ -382,7 +383,8 @@ class Context:
     def pair_batch(self, descs, src_ptr, mask_descs, mask_src_ptr, params, out, out_ptr, mask_out, mask_out_ptr,
                    stream=0):
         """provider::image + provider::pixelmask of the same records, one params set per record
-        (aeon_hip_augment_pair_batch: one launch for 8-bit unrotated masks into uint8 items)."""
+        (aeon_hip_augment_pair_batch: for 8-bit unrotated masks into uint8 items one job table and two
+        launches -- the image tiles, then the masks' gather; AEON_HIP_FUSE_MASKS=1: one launch)."""
         n = len(descs)
         d = descs if isinstance(descs, ctypes.Array) else (ImgDesc * n)(*descs)
         md = mask_descs if isinstance(mask_descs, ctypes.Array) else (ImgDesc * n)(*mask_descs)
@@ -420,6 +422,10 @@ class Context:
 
     def synchronize(self, stream=0):
         _check(lib().aeon_hip_synchronize(self._h, ctypes.c_void_p(stream or 0)))
+
+    def release_stream(self, stream):
+        """The caller is about to destroy `stream` (aeon_hip_release_stream)."""
+        _check(lib().aeon_hip_release_stream(self._h, ctypes.c_void_p(stream or 0)))
 
     def transpose_batch(self, src_ptr, dst_ptr, rows, cols, element_size, stream=0):
         """batch_major=false layout: dst[c*rows + r] = src[r*cols + c] (async on stream)."""

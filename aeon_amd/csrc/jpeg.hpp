@@ -80,9 +80,9 @@ struct JpegRows {
 // ---- GPU entropy decoding (jpeg_huff.hip) ----
 
 constexpr int kHuffSubMin   = 256;  // subsequence (the bits one lane decodes per pass): per file, the
-constexpr int kHuffSubMax   = 1024; // multiple of 32 in [min, max] nearest to spreading it over the lanes
-constexpr int kHuffLanes    = 1024; // jpeg_huff workgroup (one per file)
-constexpr int kHuffMaxBpm   = 16;   // blocks per MCU the GPU path takes (libjpeg allows 10)
+constexpr int kHuffSubMax   = 2048; // multiple of 32 in [min, max] nearest to spreading it over the lanes
+constexpr int kHuffLanes    = 512;  // jpeg_huff workgroup (one per file, two per CU; AEON_HIP_JPEG_HUFF_LANES=1024 / 256)
+constexpr int kHuffMaxBpm   = 10;   // blocks per MCU (libjpeg's D_MAX_BLOCKS_IN_MCU; the parser refuses more)
 constexpr int kHuffFastBits = 10;   // lookahead of the LDS decode tables
 constexpr int kHuffLeadBits = 512;  // a guessed walk starts this far before its subsequence (re-synchronising)
 #ifndef AEON_HUFF_PROBE
@@ -92,6 +92,7 @@ constexpr int kHuffStageMax = 80 * 1024; // (probe builds hold their stamps in L
 #endif
 
 // One DHT table as the file defines it (code lengths 1..16, then the symbols), validated on the host.
+constexpr int kJpegHuffSlots = 4; // Huffman tables a GPU-decoded scan holds: two DC, two AC
 struct JpegHuffTab {
     uint8_t counts[16];
     uint8_t symbols[256];
@@ -117,11 +118,12 @@ struct alignas(16) JpegHuffFile {
     uint64_t data;      // unstuffed entropy-coded bytes, 4-byte aligned, segments back to back
     uint64_t segs;      // JpegHuffSeg[nseg]
     uint64_t sub_seg;   // int32 per subsequence: its segment
-    uint64_t tabs;      // JpegHuffTab[6]: DC of frame component k at k, AC at 3 + k
+    uint64_t tabs;      // JpegHuffTab[kJpegHuffSlots]: the scan's DC tables in slots 0-1, AC in 2-3
     uint64_t subs;      // JpegHuffSub[nsub] (device scratch)
     uint64_t blocks[3]; // JpegBlock[bh][bw] per frame component (zeroed before the launch)
     uint64_t dvals[3];  // 64 int16 per block per frame component
-    uint64_t blk_tab[2]; // byte c (c < kHuffMaxBpm) = MCU block c: frame component | x << 2 | y << 4
+    uint64_t blk_tab[2]; // byte c (c < kHuffMaxBpm) = MCU block c: frame component | x << 2 | y << 4 |
+                         // its DC table slot << 6 | (its AC table slot - 2) << 7
     int32_t  nseg, nsub, restart, n_mcu; // restart: MCUs per segment (n_mcu without DRI)
     int32_t  bpm, mcux, ncomp;           // a non-interleaved (grayscale) scan: bpm 1, mcux = blocks per row
     int32_t  truncated; // first segment whose data ends with the file, not a marker (reading past it is an error); -1: none

@@ -24,6 +24,7 @@
 namespace aeon_hip {
 hipError_t launch_jpeg(const JpegImage* imgs, const JpegChunk* chunks, int n_chunks, const JpegRows* rows, int n_rows,
                        int color_lds, hipStream_t stream);
+int        jpeg_huff_stage_cap(int lanes);
 hipError_t launch_jpeg_huff(const JpegHuffFile* files, int n_files, int lanes, int stage_bytes, int32_t* error,
                             hipStream_t stream);
 
@@ -798,7 +799,18 @@ bool prepare_gpu(const uint8_t* d, size_t size, Frame& f, Arena& a, GpuScan& g, 
         p += len;
         break;
     }
-    // the scan's shape
+    // the decoder's table slots: the scan's distinct DC tables in slots 0-1, its AC tables in 2-3 (a
+    // scan naming more than two of either -- extended-sequential files may -- goes to the host decoder)
+    int dslot[3] = {0, 0, 0}, aslot[3] = {0, 0, 0}, dids[2] = {-1, -1}, aids[2] = {-1, -1};
+    for (int i = 0; i < ns; i++) {
+        const int td = f.c[sc[i]].td, ta = f.c[sc[i]].ta;
+        int       d = 0, q = 0;
+        while (d < 2 && dids[d] >= 0 && dids[d] != td) d++;
+        while (q < 2 && aids[q] >= 0 && aids[q] != ta) q++;
+        if (d == 2 || q == 2) return false;
+        dids[d] = td, aids[q] = ta, dslot[sc[i]] = d, aslot[sc[i]] = q;
+    }
+    // the scan's shape; each MCU block's byte: component | x << 2 | y << 4 | DC slot << 6 | AC slot - 2 << 7
     const bool inter = ns > 1;
     g.interleaved    = inter;
     g.bpm = 0, g.blk_tab[0] = g.blk_tab[1] = 0;
@@ -808,13 +820,14 @@ bool prepare_gpu(const uint8_t* d, size_t size, Frame& f, Arena& a, GpuScan& g, 
             for (int y = 0; y < c.v; y++)
                 for (int x = 0; x < c.h; x++) {
                     if (g.bpm == kHuffMaxBpm) return false;
-                    g.blk_tab[g.bpm >> 3] |= (uint64_t)(sc[i] | x << 2 | y << 4) << (8 * (g.bpm & 7));
+                    g.blk_tab[g.bpm >> 3] |= (uint64_t)(sc[i] | x << 2 | y << 4 | dslot[sc[i]] << 6 | aslot[sc[i]] << 7)
+                                             << (8 * (g.bpm & 7));
                     g.bpm++;
                 }
         }
         g.mcux = f.mcux, g.n_mcu = f.mcux * f.mcuy;
     } else {
-        g.bpm = 1, g.blk_tab[0] = (uint64_t)sc[0];
+        g.bpm = 1, g.blk_tab[0] = (uint64_t)(sc[0] | dslot[sc[0]] << 6 | aslot[sc[0]] << 7);
         g.mcux = (f.c[sc[0]].dw + 7) / 8, g.n_mcu = g.mcux * ((f.c[sc[0]].dh + 7) / 8);
     }
     g.restart = restart ? restart : g.n_mcu;
@@ -906,11 +919,14 @@ bool prepare_gpu(const uint8_t* d, size_t size, Frame& f, Arena& a, GpuScan& g, 
     }
     if (g.truncated >= nseg_need) g.truncated = -1; // (data of an ignored interval)
     g.nseg = nseg_need, g.nsub = nsub;
-    // tables of the frame's components (DC at k, AC at 3 + k), segments, subsequence -> segment
-    g.tabs           = (size_t)(a.reserve(6 * sizeof(JpegHuffTab)) - a.host.data());
+    // the scan's tables by slot (DC 0-1, AC 2-3; an unused slot has no codes), segments, subsequence -> segment
+    g.tabs           = (size_t)(a.reserve(kJpegHuffSlots * sizeof(JpegHuffTab)) - a.host.data());
     JpegHuffTab* tab = (JpegHuffTab*)(a.host.data() + g.tabs);
-    std::memset(tab, 0, 6 * sizeof(JpegHuffTab));
-    for (int k = 0; k < f.ncomp; k++) tab[k] = dct[f.c[k].td], tab[3 + k] = act[f.c[k].ta];
+    std::memset(tab, 0, kJpegHuffSlots * sizeof(JpegHuffTab));
+    for (int d = 0; d < 2; d++)
+        if (dids[d] >= 0) tab[d] = dct[dids[d]];
+    for (int q = 0; q < 2; q++)
+        if (aids[q] >= 0) tab[2 + q] = act[aids[q]];
     g.segs = (size_t)(a.reserve(segs.size() * sizeof(JpegHuffSeg)) - a.host.data());
     std::memcpy(a.host.data() + g.segs, segs.data(), segs.size() * sizeof(JpegHuffSeg));
     g.sub_seg   = (size_t)(a.reserve((size_t)nsub * sizeof(int32_t)) - a.host.data());
@@ -942,7 +958,7 @@ struct JpegState {
     } sets[2];
     int        next = 0;
     bool       gpu_huff = true; // false: every file through the host entropy decoder
-    int        huff_lanes = kHuffLanes; // jpeg_huff workgroup size (AEON_HIP_JPEG_HUFF_LANES=256: A/B)
+    int        huff_lanes = kHuffLanes; // jpeg_huff workgroup size (AEON_HIP_JPEG_HUFF_LANES=256 / 1024: A/B)
     std::mutex mu;
 };
 
@@ -970,7 +986,10 @@ JpegState* jpeg_state_create(thread_pool* shared, bool gpu_huff)
 {
     auto* s = new JpegState();
     s->gpu_huff = gpu_huff;
-    if (const char* e = std::getenv("AEON_HIP_JPEG_HUFF_LANES")) s->huff_lanes = std::atoi(e) == 256 ? 256 : kHuffLanes;
+    if (const char* e = std::getenv("AEON_HIP_JPEG_HUFF_LANES")) {
+        const int l   = std::atoi(e);
+        s->huff_lanes = l == 256 || l == 512 || l == 1024 ? l : kHuffLanes;
+    }
     if (shared) {
         s->pool = shared;
     } else {
@@ -1099,7 +1118,8 @@ void jpeg_decode_batch(JpegState* S, int n, const void* const* data, const size_
     const uint64_t dev  = (uint64_t)st.dev, work = (uint64_t)st.work;
     JpegImage*     imgs = (JpegImage*)st.pinned;
     JpegHuffFile*  hf   = (JpegHuffFile*)(st.pinned + huf_off);
-    int            huff_stage = 0; // LDS for the largest GPU-decoded file's data that fits kHuffStageMax
+    int            huff_stage = 0; // LDS for the largest GPU-decoded file's data that fits the cap
+    const int      stage_cap  = n_gpu ? jpeg_huff_stage_cap(S->huff_lanes) : 0;
     for (int i = 0; i < n; i++) {
         const Frame& f = frames[i];
         JpegImage&   J = imgs[i];
@@ -1141,7 +1161,7 @@ void jpeg_decode_batch(JpegState* S, int n, const void* const* data, const size_
         H.nseg = g.nseg, H.nsub = g.nsub, H.restart = g.restart, H.n_mcu = g.n_mcu;
         H.bpm = g.bpm, H.mcux = g.mcux, H.ncomp = f.ncomp, H.truncated = g.truncated, H.sub_bits = g.sub_bits;
         H.data_words = g.data_words;
-        if (g.data_words * 4 <= kHuffStageMax) huff_stage = std::max(huff_stage, g.data_words * 4);
+        if (g.data_words * 4 <= stage_cap) huff_stage = std::max(huff_stage, g.data_words * 4);
     }
     if (!chunks.empty()) std::memcpy(st.pinned + chk_off, chunks.data(), chunks.size() * sizeof(JpegChunk));
     if (!rows.empty()) std::memcpy(st.pinned + row_off, rows.data(), rows.size() * sizeof(JpegRows));

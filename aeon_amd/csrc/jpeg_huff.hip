@@ -250,23 +250,47 @@ __global__ __launch_bounds__(LANES) void jpeg_huff(const JpegHuffFile* __restric
 #endif
 }
 
+// Workgroups of jpeg_huff<LANES> a CU holds at once by its LDS (160 KB on gfx950): one 1,024-lane file,
+// two 512-lane ones, three 256-lane ones -- the dynamic part (a file's staged data) is capped to fit.
+constexpr int kCuLds = 160 * 1024;
+constexpr int huff_files_per_cu(int lanes) { return lanes >= 1024 ? 1 : (lanes >= 512 ? 2 : 3); }
+
+template <int LANES>
+int huff_static_lds()
+{
+    static const int bytes = [] {
+        hipFuncAttributes at{};
+        return hipFuncGetAttributes(&at, (const void*)jpeg_huff<LANES>) == hipSuccess ? (int)at.sharedSizeBytes : kCuLds;
+    }();
+    return bytes;
+}
+
+// The largest file data (bytes) jpeg_huff<lanes> copies into LDS at its occupancy goal.
+int jpeg_huff_stage_cap(int lanes)
+{
+    const int st = lanes >= 1024 ? huff_static_lds<1024>() : (lanes >= 512 ? huff_static_lds<512>() : huff_static_lds<256>());
+    const int cap = (kCuLds / huff_files_per_cu(lanes) - st - 256) & ~15;
+    return cap < 0 ? 0 : (cap < kHuffStageMax ? cap : kHuffStageMax);
+}
+
+template <int LANES>
+hipError_t launch_huff(const JpegHuffFile* files, int n_files, int stage_bytes, int32_t* error, hipStream_t stream)
+{
+    static const hipError_t a = hipFuncSetAttribute((const void*)jpeg_huff<LANES>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                    kHuffStageMax);
+    if (a != hipSuccess) return a;
+    hipLaunchKernelGGL(jpeg_huff<LANES>, dim3(n_files), dim3(LANES), stage_bytes, stream, files, stage_bytes, error);
+    return hipGetLastError();
+}
+
 hipError_t launch_jpeg_huff(const JpegHuffFile* files, int n_files, int lanes, int stage_bytes, int32_t* error,
                             hipStream_t stream)
 {
     if (n_files <= 0) return hipSuccess;
     stage_bytes = (stage_bytes + 15) & ~15;
-    if (lanes == 256) {
-        static const hipError_t a = hipFuncSetAttribute((const void*)jpeg_huff<256>,
-                                                        hipFuncAttributeMaxDynamicSharedMemorySize, kHuffStageMax);
-        if (a != hipSuccess) return a;
-        hipLaunchKernelGGL(jpeg_huff<256>, dim3(n_files), dim3(256), stage_bytes, stream, files, stage_bytes, error);
-    } else {
-        static const hipError_t a = hipFuncSetAttribute((const void*)jpeg_huff<1024>,
-                                                        hipFuncAttributeMaxDynamicSharedMemorySize, kHuffStageMax);
-        if (a != hipSuccess) return a;
-        hipLaunchKernelGGL(jpeg_huff<1024>, dim3(n_files), dim3(1024), stage_bytes, stream, files, stage_bytes, error);
-    }
-    return hipGetLastError();
+    if (lanes == 256) return launch_huff<256>(files, n_files, stage_bytes, error, stream);
+    if (lanes == 512) return launch_huff<512>(files, n_files, stage_bytes, error, stream);
+    return launch_huff<1024>(files, n_files, stage_bytes, error, stream);
 }
 
 } // namespace aeon_hip

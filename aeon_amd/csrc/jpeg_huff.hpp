@@ -33,7 +33,7 @@ HUFF_FN HUFF_GLOBAL T* gmem(uint64_t a)
 // Fast-table entry: bits 0-4 bits consumed, 5-8 AC run, 9-11 kind, 16-31 value (kValue) or value
 // size (kSym).  0: no code of <= kHuffFastBits bits is a prefix (the long-code walk).
 constexpr uint32_t kValue = 1u << 9, kEob = 2u << 9, kZrl = 3u << 9, kSym = 4u << 9, kKind = 7u << 9;
-constexpr int      kTabs = 6; // DC of frame components 0..2, then AC of 0..2
+constexpr int      kTabs = kJpegHuffSlots; // the scan's DC tables (slots 0, 1), then its AC tables (2, 3)
 constexpr int      kFast = 1 << kHuffFastBits;
 
 constexpr int kLongSub = 16; // second-level tables per DHT table: codes of 11..16 bits by the 6 bits after
@@ -71,10 +71,8 @@ HUFF_FN void or_mask(HUFF_GLOBAL uint64_t* m, uint64_t v)
 HUFF_FN void tables_codes(Tables& T, const JpegHuffFile& F, int i0, int di)
 {
     const HUFF_GLOBAL JpegHuffTab* tabs = gmem<const JpegHuffTab>(F.tabs);
-    for (int i = i0; i < kTabs * 256; i += di)
-        if ((i >> 8) % 3 < F.ncomp) T.vals[i >> 8][i & 255] = tabs[i >> 8].symbols[i & 255];
+    for (int i = i0; i < kTabs * 256; i += di) T.vals[i >> 8][i & 255] = tabs[i >> 8].symbols[i & 255];
     for (int t = i0; t < kTabs; t += di) {
-        if (t % 3 >= F.ncomp) continue;
         int code = 0, s = 0;
         for (int l = 1; l <= 16; l++) {
             const int n = tabs[t].counts[l - 1];
@@ -92,7 +90,6 @@ HUFF_FN void tables_long(Tables& T, const JpegHuffFile& F, int i0, int di)
 {
     for (int i = i0; i < kTabs * kLongSub * 64; i += di) {
         const int t = i / (kLongSub * 64), r = i % (kLongSub * 64);
-        if (t % 3 >= F.ncomp) continue;
         const int prefix = T.long_first[t] + r / 64;
         uint16_t  e      = 0;
         if (prefix < kFast)
@@ -114,7 +111,7 @@ HUFF_FN uint32_t fast_entry(const Tables& T, int t, int x)
         const int code = x >> (kHuffFastBits - l);
         if (code > T.maxcode[t][l]) continue;
         const int sym = T.vals[t][T.delta[t][l] + code];
-        if (t < 3) { // DC: the symbol is the difference's size
+        if (t < 2) { // DC: the symbol is the difference's size
             if (sym <= 15 && l + sym <= kHuffFastBits) {
                 const int bits = sym ? (x >> (kHuffFastBits - l - sym)) & ((1 << sym) - 1) : 0;
                 const int v    = sym ? extend(bits, sym) : 0;
@@ -136,8 +133,7 @@ HUFF_FN uint32_t fast_entry(const Tables& T, int t, int x)
 // Tables, part 2: the fast entries.
 HUFF_FN void tables_fast(Tables& T, const JpegHuffFile& F, int i0, int di)
 {
-    for (int i = i0; i < kTabs * kFast; i += di)
-        if ((i / kFast) % 3 < F.ncomp) T.fast[i / kFast][i % kFast] = fast_entry(T, i / kFast, i % kFast);
+    for (int i = i0; i < kTabs * kFast; i += di) T.fast[i / kFast][i % kFast] = fast_entry(T, i / kFast, i % kFast);
 }
 
 // Bits of a segment: words at or past `end` read as zeros (libjpeg's fill after a marker).  64 bits
@@ -263,7 +259,7 @@ HUFF_FN uint32_t long_entry(const Tables& T, int t, uint64_t buf, bool& ok)
     }
     ok = l != 0;
     if (!ok) l = 1, sym = 0;
-    if (t < 3) return kSym | (uint32_t)l | ((uint32_t)sym << 16);
+    if (t < 2) return kSym | (uint32_t)l | ((uint32_t)sym << 16);
     if (!(sym & 15)) return ((sym >> 4) == 15 ? kZrl : kEob) | (uint32_t)l; // (jdhuff.c: size 0, run < 15 ends the block)
     return kSym | (uint32_t)l | ((uint32_t)(sym >> 4) << 5) | ((uint32_t)(sym & 15) << 16);
 }
@@ -274,6 +270,12 @@ struct BlkTab {
     uint64_t lo, hi;
     HUFF_FN int byte(int c) const { return (int)(((c < 8 ? lo : hi) >> (8 * (c & 7))) & 0xff); }
     HUFF_FN int comp(int c) const { return byte(c) & 3; }
+    // the block's table slot: DC (slot 0 or 1) at k == 0, AC (2 or 3) after
+    HUFF_FN int tab(int c, int k) const
+    {
+        const int by = byte(c);
+        return k == 0 ? (by >> 6) & 1 : 2 + (by >> 7);
+    }
 };
 
 // A sync walk from state (b.p, c, k) to the first codeword boundary at or past `stop`: blocks started
@@ -290,7 +292,7 @@ HUFF_FN void walk_sync(const Tables& T, const JpegHuffFile& F, B& b, int& c, int
     while (b.p < stop) {
         if constexpr (WordsInMemory<decltype(b.w)>::value) b.fill();
         else b.fill_always();
-        const int t = k == 0 ? comp : 3 + comp;
+        const int t = bt.tab(c, k);
         uint32_t  e = T.fast[t][(int)(b.buf >> (64 - kHuffFastBits))];
         if (!(e & kKind)) {
             bool ok;
@@ -348,7 +350,7 @@ HUFF_FN bool walk_write(const Tables& T, const JpegHuffFile& F, B& b, int& c, in
     if (o.blk < o.blk_end) open();
     while (o.blk < o.blk_end && (last || b.p < stop)) {
         b.fill();
-        const int t = k == 0 ? comp : 3 + comp;
+        const int t = bt.tab(c, k);
         uint32_t  e = T.fast[t][(int)(b.buf >> (64 - kHuffFastBits))];
         if (!(e & kKind)) {
             bool ok;

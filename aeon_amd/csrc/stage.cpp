@@ -1887,10 +1887,28 @@ int aeon_hip_depthmap_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs
     });
 }
 
+int aeon_hip_release_stream(aeon_hip_ctx* ctx, void* stream)
+{
+    return guarded([&] {
+        if (!ctx) fail(AEON_HIP_EINVAL, "null ctx");
+        std::lock_guard<std::mutex> lock(ctx->mu);
+        HIP_OK(hipSetDevice(ctx->device));
+        // the ring slots of the calls still open on this stream get their completion event now, while
+        // the stream exists (the next call on another stream would record it there -- on a destroyed
+        // stream by then); the context then holds no reference to the stream
+        if (ctx->open_stream == (hipStream_t)stream) {
+            close_slots(ctx);
+            ctx->open_stream = nullptr;
+        }
+        return 0;
+    });
+}
+
 int aeon_hip_synchronize(aeon_hip_ctx* ctx, void* stream)
 {
     return guarded([&] {
         if (!ctx) fail(AEON_HIP_EINVAL, "null ctx");
+        if (const int rc = aeon_hip_release_stream(ctx, stream)) return rc;
         HIP_OK(hipSetDevice(ctx->device));
         HIP_OK(hipStreamSynchronize((hipStream_t)stream));
         int32_t err = 0;

@@ -413,6 +413,7 @@ int aeon_hip_stager_destroy(aeon_hip_stager* s)
         std::lock_guard<std::mutex> l(s->mu);
         for (Window& w : s->win) {
             if (w.state == Window::LAUNCHED) (void)hipEventSynchronize(w.done);
+            if (w.stream) (void)aeon_hip_release_stream(s->ctx, w.stream); // (before the stream goes)
             reset_window(s, w);
             for (Chunk& c : w.chunks) (void)hipHostFree(c.host);
             if (w.dev_src) (void)hipFree(w.dev_src);

@@ -392,7 +392,7 @@ def run_c5(A, C, torch, steps, warmup, pool_mib, src_wh=(640, 480)):
             ps.append(f.make_params(st, w, h, 512, 512))
             states[i] = st[0]
         params.append((A.AugParams * batch)(*ps))
-    stream = torch.cuda.current_stream().cuda_stream
+    stream = torch.cuda.Stream().cuda_stream  # (a stream of our own: see run_device)
 
     separate = os.environ.get("AEON_BENCH_C5_SEPARATE") == "1"  # (A/B: the two calls of round 4)
 
@@ -504,6 +504,70 @@ def cpu_baseline(A, C, budget_s, cfg="C2"):
                       "scalar C++, a lower bound on aeon's OpenCV-SIMD path"}
 
 
+def run_aeon_path(A, C, torch, cfg="C2", overlap=True, windows=8, warmup=2):
+    """aeon's own decode stage with the HIP stager in place of provide()'s pixel work, emulated call for
+    call (INTEGRATION.md edits 1-4; tests/test_integration.py checks the same sequence bit-exact): a
+    decode thread runs provide() for a window of decoded records on 8 pool threads (make_params +
+    aeon_hip_stager_stage) and post_process() per batch; the consumer (batch_iterator_fbm::filler) takes
+    the batches out of the container -- two containers alternate (async_manager).  overlap=True:
+    post_process is launch-only and the consumer waits per buffer (edits 3 + 4), so window k's GPU work
+    runs while window k+1 is staged; False: post_process flushes (launch + wait).  Pageable host batch
+    buffers (aeon's default: the stager copies each batch back with a D2H).  Records/s over `windows`."""
+    import queue
+    import threading
+    from concurrent.futures import ThreadPoolExecutor
+    import numpy as np
+    aug = {"C1": C.C1_AUG, "C2": C.C2_AUG}[cfg]
+    batch, nb = (32, 4) if cfg == "C1" else (64, 4)
+    src_w, src_h = (480, 360) if cfg == "C1" else (256, 256)
+    n = batch * nb
+    ctx = A.Context(torch.cuda.current_device())
+    out = C.out_desc_for(C.IMAGE_224, aug)
+    st = A.Stager(ctx, out, batch)
+    factory = A.ParamFactory(aug)
+    engines = A.seed_slots(1, n)
+    recs = [A.synthetic_image(i, src_w, src_h, 3) for i in range(n)]
+    conts = [[np.zeros(batch * out.item_stride, np.uint8) for _ in range(nb)] for _ in range(2)]
+    free_q, full_q = queue.Queue(), queue.Queue()
+    for c in range(2):
+        free_q.put(c)
+    total = warmup + windows
+    t_start = [0.0]
+
+    def decode_stage():
+        with ThreadPoolExecutor(max_workers=8) as pool:
+            for w in range(total):
+                c = free_q.get()
+                if w == warmup:
+                    t_start[0] = time.perf_counter()
+
+                def provide(i):
+                    eng = engines[i:i + 1]
+                    p = factory.make_params(eng, src_w, src_h, 224, 224)
+                    st.stage(conts[c][i // batch].ctypes.data, i % batch, recs[i], p)
+
+                list(pool.map(provide, range(n)))
+                for b in range(nb):
+                    (st.launch if overlap else st.flush)(conts[c][b].ctypes.data)
+                full_q.put(c)
+
+    th = threading.Thread(target=decode_stage)
+    th.start()
+    sink = 0
+    for w in range(total):
+        c = full_q.get(timeout=300)
+        for b in range(nb):
+            A.Stager.wait_buffer(conts[c][b].ctypes.data)  # (flush mode: returns at once)
+            sink += int(conts[c][b][0])  # the consumer touches the batch
+        free_q.put(c)
+    dt = time.perf_counter() - t_start[0]
+    th.join()
+    st.close()
+    ctx.close()
+    return {"value": n * windows / dt, "unit": "images/s", "batch": batch, "decode_size": n,
+            "ms_per_window": dt / windows * 1e3}
+
+
 def side(extra, key, fn):
     """One side run of the bench line (rank 0's extras): a failure is recorded in the line under its
     key instead of losing the line."""
@@ -522,7 +586,7 @@ def jpeg_files(batch):
     return [files[i % 2] for i in range(batch)]
 
 
-def run_e2e_jpeg(A, C, torch, batch=256, windows=12, on_device=False):
+def run_e2e_jpeg(A, C, torch, batch=512, windows=12, on_device=False):
     """The product's whole decode stage from encoded records, double-buffered (aeon_decoder_submit /
     wait over two windows): JPEG entropy decode on the host pool, sparse coefficients H2D, GPU IDCT
     + colour into the source arena, C2 augmentation, and (host outputs) D2H into pinned buffers."""
@@ -551,8 +615,10 @@ def run_e2e_jpeg(A, C, torch, batch=256, windows=12, on_device=False):
     return batch * windows / dt
 
 
-def run_jpeg_stage(A, torch, batch=256, reps=10):
-    """aeon_hip_decode_jpeg_batch alone (extract of a window of JPEG files into device memory)."""
+def run_jpeg_stage(A, torch, batch=512, reps=10):
+    """aeon_hip_decode_jpeg_batch alone (extract of a window of JPEG files into device memory): a
+    512-record window (aeon's decode_size = 2 x batch 256), so the GPU Huffman decoder holds two files per
+    CU."""
     files = jpeg_files(batch)
     ctx = A.Context(torch.cuda.current_device())
     infos = [A.jpeg_info(f) for f in files]
@@ -562,7 +628,7 @@ def run_jpeg_stage(A, torch, batch=256, reps=10):
         off += (w * h * 3 + 15) // 16 * 16
     descs = (A.ImgDesc * batch)(*descs)
     dst = torch.empty(off, dtype=torch.uint8, device="cuda")
-    stream = torch.cuda.current_stream().cuda_stream
+    stream = torch.cuda.Stream().cuda_stream  # (a stream of our own: see run_device)
     ctx.decode_jpeg_batch(files, descs, dst.data_ptr(), stream)
     ctx.synchronize(stream)
     t0 = time.perf_counter()
@@ -810,12 +876,26 @@ def main():
             "what": "pinned H2D of decoded 256x256 u8 + kernel storing fp32 CHW straight into the pinned host "
                     "batch (zero-copy over PCIe, no D2H)"})
         side(extra, "C1", lambda: {"decoder": run_c1_decoder(A, C, torch)})
+
+        def aeon_path():
+            r = {}
+            for cfg in ("C1", "C2"):
+                r[cfg] = {"overlap": run_aeon_path(A, C, torch, cfg, True),
+                          "flush": run_aeon_path(A, C, torch, cfg, False)}
+            r["what"] = ("aeon's decode stage emulated call for call through the stager (INTEGRATION.md edits 1-4): "
+                         "provide() on 8 pool threads (make_params + stage of decoded host records), post_process() "
+                         "per batch, a consumer taking batches out of two alternating containers; 'overlap': "
+                         "launch-only post_process + consumer-side wait, 'flush': post_process waits; pageable "
+                         "batch buffers (D2H)")
+            return r
+        side(extra, "aeon_path", aeon_path)
         side(extra, "e2e_jpeg_decoder", lambda: {
             "host_outputs": {"value": run_e2e_jpeg(A, C, torch, on_device=False), "unit": "images/s"},
             "device_outputs": {"value": run_e2e_jpeg(A, C, torch, on_device=True), "unit": "images/s"},
             "jpeg_stage": run_jpeg_stage(A, torch),
             "what": "encoded JPEG records (aeon's img_2112_70.jpg / flowers.jpg) -> aeon_decoder submit/wait "
-                    "(two windows in flight): extract on the JPEG stage + C2 augmentation, 256-record windows"})
+                    "(two windows in flight): extract on the JPEG stage + C2 augmentation, 512-record windows "
+                    "(decode_size = 2 x batch 256)"})
         if not args.no_cpu_baseline:
             for key, fn in (("e2e_jpeg_decoder", lambda: cpu_baseline_jpeg(A, C, args.cpu_extra_seconds)),
                             ("C1", lambda: cpu_baseline(A, C, args.cpu_extra_seconds, "C1")),

@@ -133,9 +133,11 @@ int aeon_hip_mask_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs,
  * runs both with one params set per record, src/provider.cpp:109-119, 365-393): equal to
  * aeon_hip_augment_batch(descs, src_base, params, out, out_dev) followed by
  * aeon_hip_mask_batch(mask_descs, mask_src_base, params, mask_out, mask_out_dev) on `stream`.
- * When every mask is an 8-bit 1-channel record without rotation into plain uint8 items, both go
- * in one kernel launch (the masks' gather blocks taken by the image launch's workgroups after
- * their tiles); otherwise as the two calls. */
+ * When every mask is an 8-bit 1-channel record without rotation into plain uint8 items, both share
+ * ONE job table (one host write, no upload launch) and run as two launches on `stream`: the image
+ * tile kernel, then the masks' nearest gather reading the same table.  (A single-launch form -- the
+ * masks' gather blocks taken by the image launch's workgroups after their tiles -- exists behind
+ * AEON_HIP_FUSE_MASKS=1; it measured slower)  Other masks go as the two calls. */
 int aeon_hip_augment_pair_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs,
                                 const void* src_base, const aeon_img_desc* mask_descs,
                                 const void* mask_src_base, const aeon_aug_params* params,
@@ -193,6 +195,13 @@ int aeon_hip_decode_jpeg_batch(aeon_hip_ctx* ctx, int n, const void* const* data
  * kernel flagged an inconsistency -- an LDS footprint the host sized too small, a dynamic-tail counter
  * not reset by an earlier launch, a rotation source box over its LDS.  None is expected. */
 int aeon_hip_synchronize(aeon_hip_ctx* ctx, void* stream);
+
+/* Streams: the context records one completion event per few calls on the stream of the calls (its ring
+ * slots are reused after it), so a stream the calls ran on must stay valid until aeon_hip_synchronize or
+ * aeon_hip_release_stream has been called on it (or the context is destroyed).  aeon_hip_release_stream:
+ * the caller is about to destroy `stream` -- the pending completion event is recorded on it now and the
+ * context keeps no reference to it.  No wait. */
+int aeon_hip_release_stream(aeon_hip_ctx* ctx, void* stream);
 
 /* ---- measurement ---------------------------------------------------------------------------- */
 /* every > 0: the kernel launches of one augment/mask call in `every` -- the every-th, 2*every-th,

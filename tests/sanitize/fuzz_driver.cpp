@@ -52,7 +52,7 @@ std::string run_jpeg_gpu(const std::vector<uint8_t>& d)
         uint64_t hv;
         // both workgroup sizes (their subsequence lengths differ: other guessed starts, same result)
         std::string res;
-        for (int lanes : {1024, 256}) {
+        for (int lanes : {1024, 512, 256}) {
             const int r = jpeg_gpu_entropy_emulate(d.data(), d.size(), lanes, &w, &h, &n, &nb, &nv, &hv, &rounds);
             char      buf[96];
             if (r == 0) std::snprintf(buf, sizeof(buf), "gpu host");

@@ -123,6 +123,7 @@ int aeon_hip_decode_jpeg_batch(aeon_hip_ctx*, int, const void* const*, const siz
     return no_device();
 }
 int aeon_hip_synchronize(aeon_hip_ctx*, void*) { return no_device(); }
+int aeon_hip_release_stream(aeon_hip_ctx*, void*) { return no_device(); }
 const char* aeon_hip_last_error(void) { return g_err.c_str(); }
 
 // ---- host-only entry points: the real implementations ----

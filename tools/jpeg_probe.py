@@ -38,7 +38,7 @@ def kernel_us(ctx, files, reps=8):
 
 
 counts = [int(a) for a in sys.argv[1:]] or [1, 256]
-for mode in ("gpu", "host"):
+for mode in (("gpu",) if os.environ.get("JPEG_PROBE_GPU_ONLY") else ("gpu", "host")):
     if mode == "host":
         os.environ["AEON_HIP_JPEG_HUFF"] = "host"
     ctx = A.Context(0)
