@@ -847,13 +847,46 @@ bool host_can_write(void* p)
     return ok;
 }
 
-bool grow_vram(uint8_t*& p, size_t& cap, size_t need) // false: the allocation failed (p freed)
+// The uncached HBM tables are never handed back to the driver: a context's tables go into a process-wide
+// pool when it is destroyed (or grows them) and the next context takes them from there.  Measured on the
+// MI355X boxes: once an uncached block had been freed, a later ordinary device allocation that reused its
+// memory lost writes -- 128-byte lines of a kernel's output read back as zeros by the next kernel on the
+// stream (tests/test_decoder.py after the stager and JPEG tests: 1-2.7 KB of one record, in 3 of 3
+// runs; with the pool, 0 of 2; with cached tables, or pinned ones, 0 of 4).
+std::mutex                               g_vram_pool_mu;
+std::vector<std::pair<uint8_t*, size_t>> g_vram_pool;   // released tables, still allocated and mapped
+std::vector<uint8_t*>                    g_vram_unused; // blocks whose probe failed (kept, never used)
+void free_vram(uint8_t*& p, size_t& cap)
+{
+    if (p) {
+        std::lock_guard<std::mutex> lock(g_vram_pool_mu);
+        g_vram_pool.emplace_back(p, cap);
+    }
+    p = nullptr, cap = 0;
+}
+
+bool grow_vram(int device, uint8_t*& p, size_t& cap, size_t need) // false: no table (p released)
 {
     if (need <= cap) return true;
-    size_t n = std::max(need, cap * 2);
-    if (p) HIP_OK(hipFree(p));
-    p   = nullptr;
-    cap = 0;
+    const size_t n = std::max(need, cap * 2);
+    free_vram(p, cap);
+    {
+        std::lock_guard<std::mutex> lock(g_vram_pool_mu); // the smallest pooled block of this device that fits
+        size_t best = g_vram_pool.size();
+        for (size_t i = 0; i < g_vram_pool.size(); i++) {
+            hipPointerAttribute_t at{};
+            if (g_vram_pool[i].second < n || hipPointerGetAttributes(&at, g_vram_pool[i].first) != hipSuccess ||
+                at.device != device)
+                continue;
+            if (best == g_vram_pool.size() || g_vram_pool[i].second < g_vram_pool[best].second) best = i;
+        }
+        (void)hipGetLastError();
+        if (best < g_vram_pool.size()) {
+            p = g_vram_pool[best].first, cap = g_vram_pool[best].second;
+            g_vram_pool.erase(g_vram_pool.begin() + (long)best);
+            return true;
+        }
+    }
     if (hipExtMallocWithFlags((void**)&p, n, hipDeviceMallocUncached) != hipSuccess) {
         (void)hipGetLastError();
         p = nullptr;
@@ -864,7 +897,8 @@ bool grow_vram(uint8_t*& p, size_t& cap, size_t need) // false: the allocation f
     // CPU; the runtime reports no host pointer for device memory either way) -- the pinned paths then
     if (!host_can_write(p)) {
         (void)hipGetLastError();
-        (void)hipFree(p);
+        std::lock_guard<std::mutex> lock(g_vram_pool_mu);
+        g_vram_unused.push_back(p); // (not freed either: see above)
         p = nullptr;
         return false;
     }
@@ -915,13 +949,10 @@ void ensure_ring(aeon_hip_ctx* ctx, size_t table, size_t partials, size_t shifts
         grow(q.host, q.host_cap, tc, true);
         HIP_OK(hipHostGetDevicePointer((void**)&q.host_dev, q.host, 0));
         grow(q.dev, q.dev_cap, tc, false);
-        if (ctx->vram_jobs && !grow_vram(q.vram, q.vram_cap, std::min(tc, kVramTableMax))) {
+        if (ctx->vram_jobs && !grow_vram(ctx->device, q.vram, q.vram_cap, std::min(tc, kVramTableMax))) {
             ctx->vram_jobs = false; // (no HBM tables on this device: the pinned paths)
             for (Slot& v : ctx->slots)
-                if (v.vram) {
-                    HIP_OK(hipFree(v.vram));
-                    v.vram = nullptr, v.vram_cap = 0;
-                }
+                free_vram(v.vram, v.vram_cap);
         }
         uint8_t* p = (uint8_t*)q.partials;
         grow(p, q.partials_cap, pc, false);
@@ -1799,7 +1830,7 @@ int aeon_hip_ctx_destroy(aeon_hip_ctx* c)
             if (s.copied) (void)hipEventDestroy(s.copied);
             if (s.host) (void)hipHostFree(s.host);
             if (s.dev) (void)hipFree(s.dev);
-            if (s.vram) (void)hipFree(s.vram);
+            if (s.vram) free_vram(s.vram, s.vram_cap);
             if (s.scratch) (void)hipFree(s.scratch);
             if (s.partials) (void)hipFree(s.partials);
             if (s.shifts) (void)hipFree(s.shifts);

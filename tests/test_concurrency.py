@@ -68,7 +68,7 @@ def test_three_threads_one_context():
             st.close()
 
     def mask_stager():
-        st = A.Stager(ctx, mask_out, 4)
+        st = A.Stager(ctx, mask_out, 4, A.STAGER_MASK)
         f = A.ParamFactory(C.C5_AUG)
         eng = A.seed_slots(5, 1)
         bufs = []
@@ -105,19 +105,14 @@ def test_three_threads_one_context():
         except Exception as e:  # noqa: BLE001
             errors.append(e)
 
-    ths = [threading.Thread(target=t) for t in (image_stager, mask_stager, direct_calls)]
-    for t in ths:
-        t.start()
-    for t in ths:
-        t.join(timeout=300)
-    try:
-        assert not errors, errors
-        assert len(results) == 6 + 6 + 8
-        for (kind, w), (srcs, ps, got) in results.items():
+    def check():
+        bad = []
+        for (kind, w), (srcs, ps, got) in sorted(results.items()):
             if kind == "direct":
                 ref = H.oracle_records(srcs, ps, img_out)
                 for i, (g, r) in enumerate(zip(got, ref)):
-                    assert np.array_equal(g, r), (kind, w, i)
+                    if not np.array_equal(g, r):
+                        bad.append((kind, w, i, int((g != r).sum()), int(g.size)))
                 continue
             od = img_out if kind == "image" else mask_out
             ref = H.oracle_records(srcs, ps, od, mask=(kind == "mask"))
@@ -126,6 +121,26 @@ def test_three_threads_one_context():
             n = od.item_stride // np.dtype(dt).itemsize
             for i, r in enumerate(ref):
                 item = got[i // per].view(dt)[(i % per) * n:(i % per + 1) * n]
-                assert np.array_equal(item, r.reshape(-1)), (kind, w, i)
+                if not np.array_equal(item, r.reshape(-1)):
+                    bad.append((kind, w, i, int((item != r.reshape(-1)).sum()), int(item.size),
+                                int((item == 0).sum())))
+        return bad
+
+    try:
+        # each worker alone first, then the three at once
+        for t in (image_stager, mask_stager, direct_calls):
+            t()
+        assert not errors, errors
+        bad_serial = check()
+        results.clear()
+        ths = [threading.Thread(target=t) for t in (image_stager, mask_stager, direct_calls)]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join(timeout=300)
+        assert not errors, errors
+        assert len(results) == 6 + 6 + 8
+        bad = check()
+        assert not bad_serial and not bad, (bad_serial[:8], bad[:8], len(bad_serial), len(bad))
     finally:
         ctx.close()

@@ -136,7 +136,8 @@ def test_decoder_encoded_and_decoded_elements_mix():
     cfg = dict(batch_size=len(files), random_seed=3, etl=[C.IMAGE_512, C.MASK_512], augmentation=[C.C5_AUG])
     img_a, msk_a = A.Decoder(cfg).decode([(f, m) for f, m in zip(files, masks)])
     img_b, msk_b = A.Decoder(cfg).decode([(d, m) for d, m in zip(dec, masks)])
-    assert np.array_equal(img_a, img_b) and np.array_equal(msk_a, msk_b)
+    assert np.array_equal(img_a, img_b) and np.array_equal(msk_a, msk_b), (
+        _diff_report(img_a, img_b), int((msk_a != msk_b).sum()))
 
 
 def test_decoder_submit_wait_double_buffered():
@@ -219,6 +220,24 @@ def test_decoder_png_image_and_mask():
         assert np.array_equal(msk[i], want.reshape(msk[i].shape)), i
 
 
+def _diff_report(want, got):
+    """Where two outputs differ (for an assertion message): element offsets, 128-byte lines touched,
+    the first wrong values next to the right ones, and where the wrong values occur in the right output."""
+    dt = {4: np.float32, 2: np.uint16}.get(want.dtype.itemsize, np.uint8)
+    a, b = want.reshape(-1).view(dt), got.reshape(-1).view(dt)
+    ut = {4: np.uint32, 2: np.uint16}.get(want.dtype.itemsize, np.uint8)
+    d = np.nonzero(a.view(ut) != b.view(ut))[0]
+    if not len(d):
+        return "equal"
+    es = a.itemsize
+    lines = np.unique(d * es // 128)
+    where = [np.nonzero(b.view(ut) == a.view(ut)[i])[0][:3].tolist() for i in d[:6]]
+    return (f"{len(d)} elements differ in [{d[0]}, {d[-1]}] ({d[0] * es:#x}..{d[-1] * es + es:#x}), {len(lines)} "
+            f"lines of 128 B ({lines[0]}..{lines[-1]}); first wrong {a[d[:6]].tolist()} right {b[d[:6]].tolist()}; "
+            f"wrong hex {[hex(int(x)) for x in a.view(ut)[d[:6]]]}; the wrong values at these offsets of the right "
+            f"output: {where}")
+
+
 def _decode_pinned(d, recs):
     """One window through submit/wait into pinned host buffers: the kernels store there directly
     (zero-copy host outputs)."""
@@ -249,4 +268,29 @@ def test_decoder_zero_copy_outputs_match_staged(case):
     want = A.Decoder(cfg).decode(recs)
     got = _decode_pinned(A.Decoder(cfg), recs)
     for w, g in zip(want, got):
-        assert w.dtype == g.dtype and np.array_equal(w.view(np.uint8), g.view(np.uint8)), case
+        assert w.dtype == g.dtype, case
+        assert np.array_equal(w.view(np.uint8), g.view(np.uint8)), (case, _diff_report(w, g))
+
+
+def test_decoder_after_contexts_come_and_go():
+    """Contexts created and destroyed before a decode (each with its HBM job tables): the later
+    device allocations still get every kernel write.  Freed uncached table blocks once came back as
+    ordinary device memory that lost 128-byte lines of a contrast record's output (zeros); the tables
+    are pooled for the process since (stage.cpp free_vram)."""
+    od = C.out_desc_for(C.IMAGE_224, C.C3_AUG)
+    f = A.ParamFactory(C.C3_AUG)
+    eng = A.seed_slots(4, 1)
+    for k in range(4):
+        ctx = A.Context(0)
+        imgs = [A.synthetic_image(900 + 8 * k + i, 300, 280, 3) for i in range(8)]
+        ps = [f.make_params(eng, 300, 280, 224, 224) for _ in imgs]
+        got = H.hip_records(ctx, imgs, ps, od)
+        ctx.close()
+        for g, r in zip(got, H.oracle_records(imgs, ps, od)):
+            assert np.array_equal(g, r), k
+    cfg = dict(batch_size=4, random_seed=9, batch_major=False, etl=[C.IMAGE_224], augmentation=[C.C3_AUG])
+    recs = _records(8, seed=4)
+    for _ in range(2):
+        (out,) = A.Decoder(cfg).decode(recs)
+        (pin,) = _decode_pinned(A.Decoder(cfg), recs)
+        assert np.array_equal(out.view(np.uint8), pin.view(np.uint8)), _diff_report(out, pin)
