@@ -51,7 +51,7 @@ def parse():
                          "run_device(region=True)); each timed launch idles the queue ~9 us around it")
     ap.add_argument("--cpu-extra-seconds", type=float, default=3.0,
                     help="CPU-baseline sample budget of each of C1/C3/C5")
-    ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic_r04s2.json"))
+    ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic_r05p.json"))
     ap.add_argument("--share-device", action="store_true",
                     help="development: ranks share the visible GPUs round-robin (gloo barrier), to run "
                          "the N-rank path on a 1-GPU box")
@@ -361,7 +361,7 @@ def run_e2e(A, C, torch, batch, steps, zero_copy=False):
     return batch * steps / dt
 
 
-def run_c5(A, C, torch, steps, warmup, pool_mib, src_wh=(640, 480)):
+def run_c5(A, C, torch, steps, warmup, pool_mib, src_wh=(640, 480), kernel_timing=True):
     """C5 (BASELINE configs[4]): image + pixel mask drawn with ONE shared params set per record
     (aeon provider_base::provide, src/provider.cpp:109-119): joint crop/flip, bilinear image
     -> 512x512x3 f32 CHW, NEAREST mask -> 512x512x1 u8, batch 128, device-resident sources."""
@@ -413,6 +413,13 @@ def run_c5(A, C, torch, steps, warmup, pool_mib, src_wh=(640, 480)):
         step(s)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    res = {"value": batch * steps / dt, "unit": "images/s (image+mask pairs)", "batch": batch,
+           "ms_per_step": dt / steps * 1e3, "source": f"{w}x{h} u8 HWC image + {w}x{h} u8 mask",
+           "what": "image 512x512x3 f32 CHW (bilinear) + mask 512x512 u8 (nearest), shared params, one "
+                   "aeon_hip_augment_pair_batch call per batch"}
+    if not kernel_timing:
+        ctx.close()
+        return res
     # kernel durations: the same steps again with every launch timed (the events cost GPU time
     # between launches, so the rate above is taken without them)
     ctx.kernel_times()
@@ -423,11 +430,8 @@ def run_c5(A, C, torch, steps, warmup, pool_mib, src_wh=(640, 480)):
     k_ms, k_bytes, k_n = ctx.kernel_times()["augment"]
     ctx.set_timing(False)
     ctx.close()
-    return {"value": batch * steps / dt, "unit": "images/s (image+mask pairs)", "batch": batch,
-            "ms_per_step": dt / steps * 1e3, "source": f"{w}x{h} u8 HWC image + {w}x{h} u8 mask",
-            "kernels_ms_per_step": k_ms / steps, "kernels_gbs": k_bytes / (k_ms * 1e-3) / 1e9 if k_ms else 0,
-            "what": "image 512x512x3 f32 CHW (bilinear) + mask 512x512 u8 (nearest), shared params, one "
-                    "aeon_hip_augment_pair_batch call per batch"}
+    res.update(kernels_ms_per_step=k_ms / steps, kernels_gbs=k_bytes / (k_ms * 1e-3) / 1e9 if k_ms else 0)
+    return res
 
 
 def pool_threads():

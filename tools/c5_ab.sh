@@ -12,6 +12,6 @@ for round in 1 2; do
     [ "$spec" != "$name" ] && envs="${spec#*:}"
     ( IFS=','; for kv in $envs; do export "$kv"; done
       timeout -k 10 120 python tools/c5_run.py 50 > "gpurun_out/c5_$name.json" ) || exit 1
-    python -c "import json;d=json.load(open('gpurun_out/c5_$name.json'));print('$name', round(d['ms_per_step']*1e3,1), round(d['kernels_ms_per_step']*1e3,1))"
+    python -c "import json;d=json.load(open('gpurun_out/c5_$name.json'));print('$name', round(d['ms_per_step']*1e3,1), round(d.get('kernels_ms_per_step',0)*1e3,1))"
   done
 done

@@ -1,4 +1,5 @@
-"""Run bench.py's C5 side workload alone (for rocprofv3 per-kernel stats): python tools/c5_run.py [steps]."""
+"""Run bench.py's C5 side workload alone (for rocprofv3 per-kernel stats): python tools/c5_run.py [steps]
+(C5_NO_TIMING=1: the untimed run only, for kernel traces of the real schedule)."""
 import json
 import os
 import sys
@@ -11,4 +12,4 @@ import bench  # noqa: E402
 from aeon_amd import configs as C  # noqa: E402
 
 steps = int(sys.argv[1]) if len(sys.argv) > 1 else 50
-print(json.dumps(bench.run_c5(A, C, torch, steps, 10, 400)))
+print(json.dumps(bench.run_c5(A, C, torch, steps, 10, 400, kernel_timing=os.environ.get("C5_NO_TIMING") != "1")))
