@@ -946,6 +946,7 @@ struct JpegState {
     std::vector<Arena>           arenas;
     struct Set {
         hipEvent_t done    = nullptr;
+        hipEvent_t copied  = nullptr; // the set's H2D (on `copy`) is done: the call's kernels may start
         bool       pending = false;
         uint8_t*   pinned  = nullptr;
         size_t     pinned_cap = 0;
@@ -956,7 +957,10 @@ struct JpegState {
         uint8_t*   work    = nullptr; // GPU-decoded files: block records, dense coefficients, subsequence scratch
         size_t     work_cap = 0;
     } sets[2];
-    int        next = 0;
+    int         next = 0;
+    hipStream_t copy = nullptr; // the H2D of a call's staging, so that it overlaps the previous call's
+                                // kernels (AEON_HIP_JPEG_COPY_STREAM=0: on the call's stream)
+    bool        use_copy = true;
     bool       gpu_huff = true; // false: every file through the host entropy decoder
     int        huff_lanes = kHuffLanes; // jpeg_huff workgroup size (AEON_HIP_JPEG_HUFF_LANES=256 / 1024: A/B)
     std::mutex mu;
@@ -986,6 +990,7 @@ JpegState* jpeg_state_create(thread_pool* shared, bool gpu_huff)
 {
     auto* s = new JpegState();
     s->gpu_huff = gpu_huff;
+    if (const char* e = std::getenv("AEON_HIP_JPEG_COPY_STREAM")) s->use_copy = std::atoi(e) != 0;
     if (const char* e = std::getenv("AEON_HIP_JPEG_HUFF_LANES")) {
         const int l   = std::atoi(e);
         s->huff_lanes = l == 256 || l == 512 || l == 1024 ? l : kHuffLanes;
@@ -1008,11 +1013,13 @@ void jpeg_state_destroy(JpegState* s)
     for (auto& st : s->sets) {
         if (st.pending) (void)hipEventSynchronize(st.done);
         if (st.done) (void)hipEventDestroy(st.done);
+        if (st.copied) (void)hipEventDestroy(st.copied);
         if (st.pinned) (void)hipHostFree(st.pinned);
         if (st.dev) (void)hipFree(st.dev);
         if (st.planes) (void)hipFree(st.planes);
         if (st.work) (void)hipFree(st.work);
     }
+    if (s->copy) (void)hipStreamDestroy(s->copy);
     delete s;
 }
 
@@ -1168,7 +1175,15 @@ void jpeg_decode_batch(JpegState* S, int n, const void* const* data, const size_
     S->pool->run((int)S->arenas.size(), [&](int w) {
         if (S->arenas[w].used) std::memcpy(st.pinned + arena_off[w], S->arenas[w].host.data(), S->arenas[w].used);
     });
-    hip_ok(hipMemcpyAsync(st.dev, st.pinned, total, hipMemcpyHostToDevice, stream), "hipMemcpyAsync");
+    if (S->use_copy) { // (the set's previous kernels are done: st.done above)
+        if (!S->copy) hip_ok(hipStreamCreateWithFlags(&S->copy, hipStreamNonBlocking), "hipStreamCreate");
+        if (!st.copied) hip_ok(hipEventCreateWithFlags(&st.copied, hipEventDisableTiming), "hipEventCreate");
+        hip_ok(hipMemcpyAsync(st.dev, st.pinned, total, hipMemcpyHostToDevice, S->copy), "hipMemcpyAsync");
+        hip_ok(hipEventRecord(st.copied, S->copy), "hipEventRecord");
+        hip_ok(hipStreamWaitEvent(stream, st.copied, 0), "hipStreamWaitEvent");
+    } else {
+        hip_ok(hipMemcpyAsync(st.dev, st.pinned, total, hipMemcpyHostToDevice, stream), "hipMemcpyAsync");
+    }
     if (n_gpu) hip_ok(hipMemsetAsync(st.work, 0, rec_bytes, stream), "hipMemsetAsync");
     if (start) hip_ok(hipEventRecord(start, stream), "hipEventRecord");
     if (n_gpu)

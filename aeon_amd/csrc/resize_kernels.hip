@@ -15,14 +15,21 @@
 //    else saturate_cast<uchar>(sum * (1.f / area))); otherwise resizeArea_ over computeResizeAreaTab:
 //    float sums in table order, horizontal then vertical.
 // A workgroup takes one tile (rows [y0, y0 + TR) x columns [x0, x0 + CW) of a record's window): the
-// column and row taps go to LDS, then the horizontal pass of every source row the tile's rows touch
-// (each staged source row read from global memory once per tile, int or float sums in LDS), then
-// the vertical pass writes the tile.
+// column and row taps go to LDS, the source rows and columns the tile touches are staged in LDS (read
+// from global memory once per tile), then the horizontal pass (int or float sums in LDS), then the
+// vertical pass writes the tile.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cfloat>
 
 #include "aug_job.hpp"
+
+// (development: AEON_RG_SKIP bits drop the horizontal pass (1), the vertical pass / stores (2) or the
+// staging (4) -- wrong outputs, phase timing only)
+#ifndef AEON_RG_SKIP
+#define AEON_RG_SKIP 0
+#endif
 
 namespace aeon_hip {
 
@@ -30,6 +37,13 @@ namespace {
 
 __device__ __forceinline__ int sat_u8(int v) { return min(max(v, 0), 255); }
 __device__ __forceinline__ int sat_s16(int v) { return min(max(v, -32768), 32767); }
+// 24-bit signed multiply-add, full rate (|operands| < 2^23)
+__device__ __forceinline__ int mad_i24(int a, int b, int c)
+{
+    int r;
+    asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
 __device__ __forceinline__ int coef_q(float c) { return sat_s16((int)__builtin_rintf(c * 2048)); }
 
 __device__ __forceinline__ void interpolate_cubic(float x, float* c)
@@ -63,7 +77,8 @@ __device__ __forceinline__ int src_px(const ResizeJob& J, int u, int v, int c)
         u += J.shift_x, v += J.shift_y;
         if (u < 0 || v < 0 || u >= J.crop_w || v >= J.crop_h) return 0;
     }
-    return ((const uint8_t*)J.src_ptr)[(size_t)(J.crop_y + v) * J.src_stride + (size_t)(J.crop_x + u) * J.cn + c];
+    return ((const __attribute__((address_space(1))) uint8_t*)J.src_ptr)[(size_t)(J.crop_y + v) * J.src_stride +
+                                                                        (size_t)(J.crop_x + u) * J.cn + c];
 }
 
 // K-tap filters: destination column dx -> (clamped sx, K coefficients), cv::resize's set-up
@@ -130,9 +145,13 @@ __device__ __forceinline__ void area_taps(int ssize, double scale, int d, int* t
 
 } // namespace
 
-// grid (tiles, jobs); LDS: xt[CW][xs] | yt[TR][xs] | H[NR][CW][cn] words
+// grid (tiles, jobs); LDS: xt[CW][xs] | yt[TR][xs] | H[NR][CW * cn] words | S[NR][SW] bytes.
+// S holds the tile's source rows [r_lo, r_hi] x columns [u_lo, u_hi] as src_px gives them (add_padding's
+// zero border applied while staging), so both passes read LDS only: the horizontal pass one (row,
+// column) per lane with the column's taps in registers, the vertical pass 4 consecutive output bytes
+// per lane (one dword store) -- an element's H word is row * CW * cn + its byte index in the row.
 __global__ __launch_bounds__(256) void resize_generic(const ResizeJob* __restrict__ jobs, const uint8_t* __restrict__ table,
-                                                      int TR, int CW, int NR, int xs, int amax, int32_t* error)
+                                                      int TR, int CW, int NR, int xs, int amax, int SW, int32_t* error)
 {
     extern __shared__ int lds_w[];
     const ResizeJob J = jobs[blockIdx.y];
@@ -141,7 +160,9 @@ __global__ __launch_bounds__(256) void resize_generic(const ResizeJob* __restric
     const int ty = blockIdx.x / J.tiles_x, tx = blockIdx.x - ty * J.tiles_x;
     const int x0 = tx * CW, y0 = ty * TR;
     const int nx = min(CW, J.win_w - x0), ny = min(TR, J.win_h - y0);
-    uint8_t*  out = (uint8_t*)J.out_ptr;
+    // global (not flat) pointers: a flat store counts on the LDS counter too, so the next LDS read's
+    // wait would also wait for the store to reach memory
+    const auto out = (__attribute__((address_space(1))) uint8_t*)J.out_ptr;
 
     if (J.method == GR_AREA_FAST) { // resizeAreaFast_: integer box, no staging
         const bool  fast2 = J.isx == 2 && J.isy == 2 && (cn == 1 || cn == 3 || cn == 4);
@@ -160,9 +181,11 @@ __global__ __launch_bounds__(256) void resize_generic(const ResizeJob* __restric
 
     const bool area = J.method == GR_AREA;
     const int  K = ksize_of(J.method), k2 = K / 2;
+    const int  rowH = CW * cn; // H words per staged row
     int*       xt = lds_w;
     int*       yt = xt + CW * xs;
     int*       H  = yt + TR * xs;
+    uint8_t*   S  = (uint8_t*)(H + NR * rowH);
     // taps of the tile's columns and rows
     for (int i = tid; i < nx; i += nt) {
         int* t = xt + i * xs;
@@ -183,74 +206,426 @@ __global__ __launch_bounds__(256) void resize_generic(const ResizeJob* __restric
         } else row_taps(J, J.win_y + y0 + r, t);
     }
     __syncthreads();
-    // the source rows the tile touches (row taps are monotone)
+    // the source rows and columns the tile touches (taps are monotone)
     const int* tf = yt;
     const int* tl = yt + (ny - 1) * xs;
     const int  r_lo = area ? tf[0] : min(max(tf[0] - k2 + 1, 0), J.crop_h - 1);
     const int  r_hi = area ? tl[0] + tl[1] - 1 : min(max(tl[0] + k2, 0), J.crop_h - 1);
     const int  nr   = r_hi - r_lo + 1;
-    if (nr > NR) {
+    const int* cf   = xt;
+    const int* cl   = xt + (nx - 1) * xs;
+    const int  u_lo = area ? cf[0] : min(max(cf[0] - k2 + 1, 0), J.crop_w - 1);
+    const int  u_hi = area ? cl[0] + cl[1] - 1 : min(max(cl[0] + k2, 0), J.crop_w - 1);
+    const int  sb   = (u_hi - u_lo + 1) * cn; // staged bytes per row
+    const bool staged = SW > 0; // (0: the host found no room for the staging -- large downscales)
+    if (nr > NR || (staged && sb > SW)) {
         if (tid == 0) atomicOr(error, 128);
         return;
     }
-    // horizontal pass: H[r][i][c] (int sums, or float bits for INTER_AREA)
-    for (int q = tid; q < nr * nx; q += nt) {
-        const int  r = q / nx, i = q - r * nx, v = r_lo + r;
-        const int* t = xt + i * xs;
-        for (int c = 0; c < cn; c++) {
+    // staging: S[r][(u - u_lo) * cn + c] = src_px(u, r_lo + r, c), 4 bytes per lane and step; (row,
+    // chunk) advanced incrementally (no divisions per step).  A staged byte b of row v is the source
+    // byte (u_lo + shift_x) * cn + b of that row's crop, zero outside it when padded.
+    if (staged && !(AEON_RG_SKIP & 4)) {
+        const uint8_t* src  = (const uint8_t*)J.src_ptr + (size_t)J.crop_x * cn;
+        const int      nch  = (sb + 3) >> 2, total = nr * nch;
+        const int      dr   = nt / nch, dc = nt - dr * nch;
+        const int      sx0  = (u_lo + (J.padded ? J.shift_x : 0)) * cn, rowb = J.crop_w * cn;
+        int            r = tid / nch, ch = tid - r * nch;
+        // kBatch steps' loads issued before their LDS writes (one memory latency per batch, not per step)
+        constexpr int kBatch = 8;
+        for (int q0 = tid; q0 < total; q0 += kBatch * nt) {
+            uint32_t w[kBatch];
+            int      at[kBatch];
+#pragma unroll
+            for (int u = 0; u < kBatch; u++) {
+                w[u] = 0, at[u] = -1;
+                {
+                    // unconditional loads from clamped (valid) addresses, zeroed after: no branch
+                    // around a load, so the batch's loads stay in flight together
+                    const bool qv  = q0 + u * nt < total;
+                    const int  rr  = min(r, nr - 1);
+                    const int  v   = r_lo + rr + (J.padded ? J.shift_y : 0);
+                    const bool vin = qv && (!J.padded || (v >= 0 && v < J.crop_h));
+                    const auto row = (const __attribute__((address_space(1))) uint8_t*)(
+                        src + (size_t)(J.crop_y + min(max(v, 0), J.crop_h - 1)) * J.src_stride);
+#pragma unroll
+                    for (int k = 0; k < 4; k++) {
+                        const int      b  = ch * 4 + k;
+                        const int      bo = sx0 + b;
+                        const bool     ok = b < sb && vin && (!J.padded || (bo >= 0 && bo < rowb));
+                        const uint32_t x  = row[min(max(bo, 0), rowb - 1)];
+                        w[u] |= (ok ? x : 0u) << (8 * k);
+                    }
+                    at[u] = qv ? rr * SW + ch * 4 : -1;
+                }
+                r += dr, ch += dc;
+                if (ch >= nch) ch -= nch, r++;
+            }
+#pragma unroll
+            for (int u = 0; u < kBatch; u++)
+                if (at[u] >= 0) *(uint32_t*)(S + at[u]) = w[u];
+        }
+    }
+    __syncthreads();
+    // horizontal pass: H[r][i * cn + c] (int sums, or float bits for INTER_AREA); lane -> column i,
+    // rows r, r + nt / nx, ... (its column's taps loaded once)
+    {
+        const int per = max(nt / nx, 1);
+        const int i = tid % nx, r0 = tid / nx;
+        if (r0 < per && tid < per * nx && !(AEON_RG_SKIP & 1)) {
+            const int* t = xt + i * xs;
             if (area) {
-                float b = 0.f;
-                for (int e = 0; e < t[1]; e++) b = b + (float)src_px(J, t[0] + e, v, c) * __int_as_float(t[2 + e]);
-                H[(r * CW + i) * cn + c] = __float_as_int(b);
+                const int n = t[1], u0 = t[0] - u_lo;
+                for (int r = r0; r < nr; r += per) {
+                    const uint8_t* row = S + r * SW;
+                    for (int c = 0; c < cn; c++) {
+                        float b = 0.f;
+                        for (int e = 0; e < n; e++)
+                            b = b + (float)(staged ? row[(u0 + e) * cn + c] : src_px(J, t[0] + e, r_lo + r, c)) *
+                                        __int_as_float(t[2 + e]);
+                        H[r * rowH + i * cn + c] = __float_as_int(b);
+                    }
+                }
+            } else if (!staged) {
+                for (int r = r0; r < nr; r += per)
+                    for (int c = 0; c < cn; c++) {
+                        int acc = 0;
+                        for (int j = 0; j < K; j++)
+                            acc += src_px(J, min(max(t[0] - k2 + 1 + j, 0), J.crop_w - 1), r_lo + r, c) * t[1 + j];
+                        H[r * rowH + i * cn + c] = acc;
+                    }
             } else {
-                int acc = 0;
-                for (int j = 0; j < K; j++) acc += src_px(J, min(max(t[0] - k2 + 1 + j, 0), J.crop_w - 1), v, c) * t[1 + j];
-                H[(r * CW + i) * cn + c] = acc;
+                int off[8], cf8[8];
+#pragma unroll
+                for (int j = 0; j < 8; j++) {
+                    off[j] = j < K ? (min(max(t[0] - k2 + 1 + j, 0), J.crop_w - 1) - u_lo) * cn : 0;
+                    cf8[j] = j < K ? t[1 + j] : 0;
+                }
+                for (int r = r0; r < nr; r += per) {
+                    const uint8_t* row = S + r * SW;
+                    for (int c = 0; c < cn; c++) {
+                        int acc = 0;
+                        if (K == 4) {
+#pragma unroll
+                            for (int j = 0; j < 4; j++) acc += (int)row[off[j] + c] * cf8[j];
+                        } else {
+                            for (int j = 0; j < K; j++) acc += (int)row[off[j] + c] * cf8[j];
+                        }
+                        H[r * rowH + i * cn + c] = acc;
+                    }
+                }
             }
         }
     }
     __syncthreads();
-    // vertical pass
-    const int W  = J.dst_w * cn;
-    const int xv = simd_end(K, W);
-    for (int q = tid; q < ny * nx * cn; q += nt) {
-        const int  r = q / (nx * cn), e = q - r * nx * cn, i = e / cn, c = e - i * cn;
+    // vertical pass: 4 consecutive bytes of an output row per lane
+    const int W   = J.dst_w * cn;
+    const int xv  = simd_end(K, W);
+    const int nb  = nx * cn;          // output bytes of a tile row
+    const int nq  = (nb + 3) >> 2;    // dword groups per tile row
+    const int xb0 = (J.win_x + x0) * cn; // the tile's first element in the full destination row
+    for (int q = tid; q < ny * nq && !(AEON_RG_SKIP & 2); q += nt) {
+        const int  r = q / nq, e0 = (q - r * nq) * 4;
         const int* t = yt + r * xs;
-        int        v;
-        if (area) {
-            float sum = 0.f;
-            for (int k = 0; k < t[1]; k++)
-                sum = sum + __int_as_float(t[2 + k]) * __int_as_float(H[((t[0] + k - r_lo) * CW + i) * cn + c]);
-            v = sat_u8((int)__builtin_rintf(sum));
-        } else {
-            const int x = (J.win_x + x0 + i) * cn + c; // element of the full destination row
-            auto      h = [&](int k) { return H[((min(max(t[0] - k2 + 1 + k, 0), J.crop_h - 1) - r_lo) * CW + i) * cn + c]; };
-            if (x < xv && K == 2) { // VResizeLinearVec_32s8u
-                const int m = sat_s16(((sat_s16(h(0) >> 4) * t[1]) >> 16) + ((sat_s16(h(1) >> 4) * t[2]) >> 16));
-                v           = sat_u8(sat_s16(m + 2) >> 2);
-            } else if (x < xv && K == 4) { // VResizeCubicVec_32s8u, SSE's order of operations
-                const float sc = 1.f / (2048 * 2048);
-                float       s  = (float)h(0) * ((float)t[1] * sc) + (float)h(1) * ((float)t[2] * sc);
-                s              = s + (float)h(2) * ((float)t[3] * sc);
-                s              = s + (float)h(3) * ((float)t[4] * sc);
-                v              = sat_u8(sat_s16((int)__builtin_rintf(s)));
-            } else { // FixedPtCast<int, uchar, 22>, int32 sums wrapping
-                uint32_t acc = 0;
-                for (int k = 0; k < K; k++) acc += (uint32_t)h(k) * (uint32_t)t[1 + k];
-                v = sat_u8((int32_t)(acc + (1u << 21)) >> 22);
+        uint32_t   word = 0;
+        int        vals[4];
+#pragma unroll
+        for (int k4 = 0; k4 < 4; k4++) {
+            const int e = min(e0 + k4, nb - 1);
+            int       v;
+            if (area) {
+                float sum = 0.f;
+                for (int k = 0; k < t[1]; k++) sum = sum + __int_as_float(t[2 + k]) * __int_as_float(H[(t[0] + k - r_lo) * rowH + e]);
+                v = sat_u8((int)__builtin_rintf(sum));
+            } else {
+                const int x = xb0 + e; // element of the full destination row
+                auto      h = [&](int k) { return H[(min(max(t[0] - k2 + 1 + k, 0), J.crop_h - 1) - r_lo) * rowH + e]; };
+                if (x < xv && K == 2) { // VResizeLinearVec_32s8u
+                    const int m = sat_s16(((sat_s16(h(0) >> 4) * t[1]) >> 16) + ((sat_s16(h(1) >> 4) * t[2]) >> 16));
+                    v           = sat_u8(sat_s16(m + 2) >> 2);
+                } else if (x < xv && K == 4) { // VResizeCubicVec_32s8u, SSE's order of operations
+                    const float sc = 1.f / (2048 * 2048);
+                    float       s  = (float)h(0) * ((float)t[1] * sc) + (float)h(1) * ((float)t[2] * sc);
+                    s              = s + (float)h(2) * ((float)t[3] * sc);
+                    s              = s + (float)h(3) * ((float)t[4] * sc);
+                    v              = sat_u8(sat_s16((int)__builtin_rintf(s)));
+                } else { // FixedPtCast<int, uchar, 22>, int32 sums wrapping
+                    uint32_t acc = 0;
+                    for (int k = 0; k < K; k++) acc += (uint32_t)h(k) * (uint32_t)t[1 + k];
+                    v = sat_u8((int32_t)(acc + (1u << 21)) >> 22);
+                }
             }
+            vals[k4] = v;
+            word |= (uint32_t)v << (8 * k4);
         }
-        out[((size_t)(y0 + r) * J.win_w + x0 + i) * cn + c] = (uint8_t)v;
+        const auto dst = out + ((size_t)(y0 + r) * J.win_w + x0) * cn + e0;
+        if (e0 + 4 <= nb && ((uintptr_t)dst & 3) == 0) {
+            *(__attribute__((address_space(1))) uint32_t*)dst = word;
+        } else {
+            for (int k4 = 0; k4 < 4 && e0 + k4 < nb; k4++) dst[k4] = (uint8_t)vals[k4];
+        }
     }
 }
 
-hipError_t launch_resize_generic(const ResizeJob* jobs, const uint8_t* table, int n_jobs, int max_tiles, int TR, int CW,
-                                 int NR, int xs, int amax, int cn_max, int32_t* error, hipStream_t stream)
+// The separable fixed-K methods (CUBIC K = 4, LANCZOS4 K = 8, INTER_AREA's bilinear emulation K = 2),
+// one workgroup per band of TR output rows x CW columns: the band's source rows staged in LDS as above,
+// then each lane owns 4 consecutive output bytes of the band's rows and walks the rows in order,
+// keeping the K horizontal sums of its 4 elements it last used in registers (a new source row's sums
+// are computed only when the row window moves onto it; the window position is uniform over the
+// workgroup, so those branches are too).  No horizontal-sum array in LDS: the workgroup needs only the
+// staged bytes and the taps, so several bands share a CU and their latencies overlap.  Same
+// arithmetic as resize_generic, element for element.
+template <int K>
+__global__ __launch_bounds__(256) void resize_sep(const ResizeJob* __restrict__ jobs, const uint8_t* __restrict__ table, int TR,
+                                                  int CW, int NR, int SW, int32_t* error)
+{
+    extern __shared__ int lds_w[];
+    const ResizeJob J = jobs[blockIdx.y];
+    if ((int)blockIdx.x >= J.tiles) return;
+    constexpr int k2 = K / 2, xs = 1 + K;
+    const int     tid = threadIdx.x, nt = blockDim.x, cn = J.cn;
+    const int     ty = blockIdx.x / J.tiles_x, tx = blockIdx.x - ty * J.tiles_x;
+    const int     x0 = tx * CW, y0 = ty * TR;
+    const int     nx = min(CW, J.win_w - x0), ny = min(TR, J.win_h - y0);
+    const auto    out = (__attribute__((address_space(1))) uint8_t*)J.out_ptr;
+    int*          xt  = lds_w;
+    int*          yt  = xt + CW * xs;
+    uint8_t*      S   = (uint8_t*)lds_w + ((CW + TR) * xs * 4 + 15) / 16 * 16; // (16-aligned rows)
+    for (int i = tid; i < nx; i += nt) {
+        int* t = xt + i * xs;
+        if (K == 8) {
+            const GrTap g = ((const GrTap*)(table + J.coef_x))[x0 + i];
+            t[0]          = g.s;
+            for (int k = 0; k < 8; k++) t[1 + k] = g.c[k];
+        } else {
+            col_taps(J, J.win_x + x0 + i, t);
+        }
+    }
+    for (int r = tid; r < ny; r += nt) {
+        int* t = yt + r * xs;
+        if (K == 8) {
+            const GrTap g = ((const GrTap*)(table + J.coef_y))[y0 + r];
+            t[0]          = g.s;
+            for (int k = 0; k < 8; k++) t[1 + k] = g.c[k];
+        } else {
+            row_taps(J, J.win_y + y0 + r, t);
+        }
+    }
+    __syncthreads();
+    const int r_lo = min(max(yt[0] - k2 + 1, 0), J.crop_h - 1);
+    const int r_hi = min(max(yt[(ny - 1) * xs] + k2, 0), J.crop_h - 1);
+    const int nr   = r_hi - r_lo + 1;
+    const int u_lo = min(max(xt[0] - k2 + 1, 0), J.crop_w - 1);
+    const int u_hi = min(max(xt[(nx - 1) * xs] + k2, 0), J.crop_w - 1);
+    const int sb   = (u_hi - u_lo + 1) * cn;
+    if (nr > NR || (J.padded ? sb : ((sb + 30) >> 4) * 16) > SW) {
+        if (tid == 0) atomicOr(error, 128);
+        return;
+    }
+    // Non-padded jobs: each staged row is the 16-byte-aligned blocks covering its bytes (one
+    // dwordx4 load per block; a 16-byte-aligned block holding one byte of the row never leaves that
+    // byte's page, so the over-read is always mapped), the row's first byte at S[r * SW + its
+    // address & 15].  Padded jobs: byte by byte, the zero border applied (as resize_generic's).
+    const uint64_t rowa0 = J.src_ptr + (uint64_t)J.crop_y * J.src_stride + (uint64_t)(J.crop_x + u_lo) * cn;
+    if (AEON_RG_SKIP & 4) {
+    } else if (!J.padded) {
+        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+        const int     nblk = (sb + 15 + 15) >> 4; // blocks of the worst-aligned row
+        const int     total = nr * nblk;
+        constexpr int kBatch = 4;
+        for (int q0 = tid; q0 < total; q0 += kBatch * nt) {
+            u32x4 w[kBatch];
+            int   at[kBatch];
+#pragma unroll
+            for (int u = 0; u < kBatch; u++) {
+                const int      q  = min(q0 + u * nt, total - 1);
+                const int      r  = q / nblk, b = q - r * nblk;
+                const uint64_t a  = rowa0 + (uint64_t)(r_lo + r) * J.src_stride;
+                const uint64_t a0 = a & ~(uint64_t)15;
+                const int      bl = (int)((((a + sb - 1) & ~(uint64_t)15) - a0) >> 4); // the row's last block
+                w[u]  = *(const __attribute__((address_space(1))) u32x4*)(a0 + (uint64_t)min(b, bl) * 16);
+                at[u] = q0 + u * nt < total && b <= bl ? r * SW + b * 16 : -1;
+            }
+#pragma unroll
+            for (int u = 0; u < kBatch; u++)
+                if (at[u] >= 0) *(u32x4*)(S + at[u]) = w[u];
+        }
+    } else { // staging (as resize_generic's)
+        const uint8_t* src = (const uint8_t*)J.src_ptr + (size_t)J.crop_x * cn;
+        const int      nch = (sb + 3) >> 2, total = nr * nch;
+        const int      dr = nt / nch, dc = nt - dr * nch;
+        const int      sx0 = (u_lo + (J.padded ? J.shift_x : 0)) * cn, rowb = J.crop_w * cn;
+        int            r = tid / nch, ch = tid - r * nch;
+        constexpr int  kBatch = 8;
+        for (int q0 = tid; q0 < total; q0 += kBatch * nt) {
+            uint32_t w[kBatch];
+            int      at[kBatch];
+#pragma unroll
+            for (int u = 0; u < kBatch; u++) {
+                const bool qv  = q0 + u * nt < total;
+                const int  rr  = min(r, nr - 1);
+                const int  v   = r_lo + rr + (J.padded ? J.shift_y : 0);
+                const bool vin = qv && (!J.padded || (v >= 0 && v < J.crop_h));
+                const auto row = (const __attribute__((address_space(1))) uint8_t*)(
+                    src + (size_t)(J.crop_y + min(max(v, 0), J.crop_h - 1)) * J.src_stride);
+                w[u] = 0;
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const int      b  = ch * 4 + k;
+                    const int      bo = sx0 + b;
+                    const bool     ok = b < sb && vin && (!J.padded || (bo >= 0 && bo < rowb));
+                    const uint32_t x  = row[min(max(bo, 0), rowb - 1)];
+                    w[u] |= (ok ? x : 0u) << (8 * k);
+                }
+                at[u] = qv ? rr * SW + ch * 4 : -1;
+                r += dr, ch += dc;
+                if (ch >= nch) ch -= nch, r++;
+            }
+#pragma unroll
+            for (int u = 0; u < kBatch; u++)
+                if (at[u] >= 0) *(uint32_t*)(S + at[u]) = w[u];
+        }
+    }
+    __syncthreads();
+    const int nb = nx * cn, e0 = tid * 4;
+    if (e0 >= nb) return; // (no barrier below)
+    // the lane's 4 elements: staged-byte offsets of their K column taps, and the coefficients
+    int off[4][K], cf[4][K];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const int  e = min(e0 + q, nb - 1), i = e / cn, c = e - i * cn;
+        const int* t = xt + i * xs;
+#pragma unroll
+        for (int j = 0; j < K; j++) {
+            off[q][j] = (min(max(t[0] - k2 + 1 + j, 0), J.crop_w - 1) - u_lo) * cn + c;
+            cf[q][j]  = t[1 + j];
+        }
+    }
+    const int W = J.dst_w * cn, xv = simd_end(K, W), xb = (J.win_x + x0) * cn + e0;
+    // The window: hw[j][q] = horizontal sum of staged row wrow[j] for element q, as float (exact:
+    // |sum| < 2^24).  The row indices are workgroup-uniform (scalar registers), so the window's reuse
+    // tests are scalar branches; a row not in the window is summed from its staged bytes.
+    typedef float f32x2 __attribute__((ext_vector_type(2)));
+    float hw[K][4];
+    int   wrow[K];
+#pragma unroll
+    for (int j = 0; j < K; j++) {
+        wrow[j] = -1;
+#pragma unroll
+        for (int q = 0; q < 4; q++) hw[j][q] = 0.f;
+    }
+    const int shift0 = J.padded ? 0 : (int)(rowa0 & 15), sstep = J.padded ? 0 : (int)(J.src_stride & 15);
+    for (int r = 0; r < ny; r++) {
+        const int* t  = yt + r * xs;
+        const int  sy = __builtin_amdgcn_readfirstlane(t[0]);
+        int        rows[K];
+#pragma unroll
+        for (int j = 0; j < K; j++) rows[j] = min(max(sy - k2 + 1 + j, 0), J.crop_h - 1) - r_lo;
+        float nh[K][4];
+#pragma unroll
+        for (int j = 0; j < K; j++) {
+            bool found = false;
+#pragma unroll
+            for (int m = 0; m < K; m++)
+                if (!found && wrow[m] == rows[j]) {
+#pragma unroll
+                    for (int q = 0; q < 4; q++) nh[j][q] = hw[m][q];
+                    found = true;
+                }
+            if (!found) {
+                if (AEON_RG_SKIP & 1) {
+#pragma unroll
+                    for (int q = 0; q < 4; q++) nh[j][q] = (float)(rows[j] + q);
+                } else {
+                    // (the row's first byte sits at its address & 15 in its staged blocks)
+                    const uint8_t* row = S + rows[j] * SW + ((shift0 + (r_lo + rows[j]) * sstep) & 15);
+#pragma unroll
+                    for (int q = 0; q < 4; q++) {
+                        int acc = 0;
+#pragma unroll
+                        for (int jj = 0; jj < K; jj++) acc = mad_i24((int)row[off[q][jj]], cf[q][jj], acc);
+                        nh[j][q] = (float)acc;
+                    }
+                }
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < K; j++) {
+            wrow[j] = rows[j];
+#pragma unroll
+            for (int q = 0; q < 4; q++) hw[j][q] = nh[j][q];
+        }
+        int coef[K];
+#pragma unroll
+        for (int j = 0; j < K; j++) coef[j] = __builtin_amdgcn_readfirstlane(t[1 + j]);
+        uint32_t word = 0;
+        if (K == 4) { // VResizeCubicVec_32s8u, SSE's order of operations, two elements per packed op
+            const float sc = 1.f / (2048 * 2048);
+            const float c0 = (float)coef[0] * sc, c1 = (float)coef[1] * sc, c2 = (float)coef[2] * sc, c3 = (float)coef[3] * sc;
+#pragma unroll
+            for (int p2 = 0; p2 < 2; p2++) {
+                const int qa = 2 * p2, qb = qa + 1;
+                f32x2     sm = (f32x2){hw[0][qa], hw[0][qb]} * (f32x2){c0, c0} + (f32x2){hw[1][qa], hw[1][qb]} * (f32x2){c1, c1};
+                sm           = sm + (f32x2){hw[2][qa], hw[2][qb]} * (f32x2){c2, c2};
+                sm           = sm + (f32x2){hw[3][qa], hw[3][qb]} * (f32x2){c3, c3};
+                // saturate_cast<uchar>(saturate_cast<short>(cvRound(s))): round half to even, clamp to
+                // [0, 255], in one v_cvt_pk_u8_f32 per element
+                word = __builtin_amdgcn_cvt_pk_u8_f32(sm.x, (uint32_t)qa, word);
+                word = __builtin_amdgcn_cvt_pk_u8_f32(sm.y, (uint32_t)qb, word);
+            }
+        }
+        if (K != 4 || xb + 3 >= xv) { // the other forms, and elements on the scalar tail
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const int x = xb + q;
+                int       v;
+                if (K == 4 && x < xv) continue;
+                if (K == 2 && x < xv) { // VResizeLinearVec_32s8u
+                    const int m = sat_s16(((sat_s16((int)hw[0][q] >> 4) * coef[0]) >> 16) +
+                                          ((sat_s16((int)hw[1][q] >> 4) * coef[1]) >> 16));
+                    v           = sat_u8(sat_s16(m + 2) >> 2);
+                } else { // FixedPtCast<int, uchar, 22>, int32 sums wrapping
+                    uint32_t acc = 0;
+#pragma unroll
+                    for (int j = 0; j < K; j++) acc += (uint32_t)(int)hw[j][q] * (uint32_t)coef[j];
+                    v = sat_u8((int32_t)(acc + (1u << 21)) >> 22);
+                }
+                word = (word & ~(0xffu << (8 * q))) | ((uint32_t)v << (8 * q));
+            }
+        }
+        const auto dst = out + ((size_t)(y0 + r) * J.win_w + x0) * cn + e0;
+        if ((AEON_RG_SKIP & 2) && word != 0x12345678u) {
+        } else if (e0 + 4 <= nb && ((uintptr_t)dst & 3) == 0) {
+            *(__attribute__((address_space(1))) uint32_t*)dst = word;
+        } else {
+            for (int q = 0; q < 4 && e0 + q < nb; q++) dst[q] = (uint8_t)(word >> (8 * q));
+        }
+    }
+}
+
+hipError_t launch_resize_sep(int K, const ResizeJob* jobs, const uint8_t* table, int n_jobs, int max_tiles, int TR, int CW,
+                             int NR, int SW, int cn, int32_t* error, hipStream_t stream)
 {
     if (n_jobs <= 0) return hipSuccess;
-    const size_t lds = ((size_t)CW * xs + (size_t)TR * xs + (size_t)NR * CW * cn_max) * 4;
+    const size_t lds     = ((size_t)(CW + TR) * (1 + K) * 4 + 15) / 16 * 16 + (size_t)NR * SW;
+    const int    threads = std::min(256, ((CW * cn + 3) / 4 + 63) / 64 * 64);
+    const dim3   grid((unsigned)max_tiles, (unsigned)n_jobs);
+    switch (K) {
+    case 2: hipLaunchKernelGGL(resize_sep<2>, grid, dim3(threads), lds, stream, jobs, table, TR, CW, NR, SW, error); break;
+    case 4: hipLaunchKernelGGL(resize_sep<4>, grid, dim3(threads), lds, stream, jobs, table, TR, CW, NR, SW, error); break;
+    case 8: hipLaunchKernelGGL(resize_sep<8>, grid, dim3(threads), lds, stream, jobs, table, TR, CW, NR, SW, error); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_resize_generic(const ResizeJob* jobs, const uint8_t* table, int n_jobs, int max_tiles, int TR, int CW,
+                                 int NR, int xs, int amax, int cn_max, int SW, int32_t* error, hipStream_t stream)
+{
+    if (n_jobs <= 0) return hipSuccess;
+    const size_t lds = ((size_t)CW * xs + (size_t)TR * xs + (size_t)NR * CW * cn_max) * 4 + (size_t)NR * SW;
     hipLaunchKernelGGL(resize_generic, dim3((unsigned)max_tiles, (unsigned)n_jobs), dim3(256), lds, stream, jobs, table, TR,
-                       CW, NR, xs, amax, error);
+                       CW, NR, xs, amax, SW, error);
     return hipGetLastError();
 }
 

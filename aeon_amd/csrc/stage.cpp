@@ -47,7 +47,9 @@ hipError_t launch_contrast_records(bool fast, bool split, const LaunchArgs& a, c
                                    hipEvent_t start, hipEvent_t stop);
 hipError_t contrast_records_lds_limit(int bytes);
 hipError_t launch_resize_generic(const ResizeJob* jobs, const uint8_t* table, int n_jobs, int max_tiles, int TR, int CW,
-                                 int NR, int xs, int amax, int cn_max, int32_t* error, hipStream_t stream);
+                                 int NR, int xs, int amax, int cn_max, int SW, int32_t* error, hipStream_t stream);
+hipError_t launch_resize_sep(int K, const ResizeJob* jobs, const uint8_t* table, int n_jobs, int max_tiles, int TR, int CW,
+                             int NR, int SW, int cn, int32_t* error, hipStream_t stream);
 void       jpeg_decode_batch(JpegState* S, int n, const void* const* data, const size_t* sizes,
                              const aeon_img_desc* descs, void* dst_base, int32_t* error, hipStream_t stream,
                              hipEvent_t start, hipEvent_t stop);
@@ -452,7 +454,8 @@ struct GrPlan {
     std::vector<ResizeJob> jobs;
     std::vector<GrTap>     taps;
     size_t                 off = 0, taps_off = 0; // byte offsets in the call's table
-    int TR = 16, CW = 128, NR = 1, xs = 3, amax = 1, cn_max = 1, max_tiles = 0;
+    int TR = 16, CW = 128, NR = 1, xs = 3, amax = 1, cn_max = 1, max_tiles = 0, SW = 4;
+    int sep = 0; // K of resize_sep when every job is one fixed-K method and its band fits (else 0: resize_generic)
     double bytes = 0; // algorithmic: the source region read once + the window written
 
     size_t n_taps = 0; // Lanczos4 taps reserved by add(), computed by fill_taps()
@@ -490,6 +493,19 @@ struct GrPlan {
         }
         return nr;
     }
+    // staged source bytes per row a tile of `cw` output columns needs at most (a multiple of 4)
+    int bytes_for(int cw) const
+    {
+        int sw = 4;
+        for (const ResizeJob& R : jobs) {
+            const int K = R.method == GR_CUBIC ? 4 : (R.method == GR_LANCZOS4 ? 8 : 2);
+            int cols = 1;
+            if (R.method == GR_AREA) cols = (int)std::ceil(cw * R.scale_x) + 4;
+            else if (R.method != GR_AREA_FAST) cols = (int)std::ceil((cw - 1) * R.scale_x) + K + 2;
+            sw = std::max(sw, (std::min(cols, R.crop_w) * R.cn + 3) / 4 * 4);
+        }
+        return sw;
+    }
     void finalize()
     {
         if (jobs.empty()) return;
@@ -504,11 +520,35 @@ struct GrPlan {
         xs = std::max(1 + K, 2 + amax);
         CW = std::min(128, ww);
         TR = 16;
-        auto lds = [&] { return ((size_t)CW * xs + (size_t)TR * xs + (size_t)rows_for(TR) * CW * cn_max) * 4; };
+        // with the source rows staged in LDS (SW > 0) when they fit at 16 x 128 tiles, else without
+        bool staged = true;
+        auto lds    = [&] {
+            return ((size_t)CW * xs + (size_t)TR * xs + (size_t)rows_for(TR) * CW * cn_max) * 4 +
+                   (staged ? (size_t)rows_for(TR) * bytes_for(CW) : 0);
+        };
+        staged = lds() <= kGenericLds;
         while (lds() > kGenericLds && TR > 1) TR--;
         while (lds() > kGenericLds && CW > 8) CW /= 2;
         if (lds() > kGenericLds) fail(AEON_HIP_EUNSUPPORTED, "resize scale too large for the generic resize's LDS tiles");
         NR        = rows_for(TR);
+        SW        = staged ? bytes_for(CW) : 0;
+        // resize_sep: bands of up to 32 rows x the window's width (at most 256 lanes of 4 bytes)
+        sep = 0;
+        {
+            const int m0 = jobs[0].method;
+            bool      one = m0 == GR_CUBIC || m0 == GR_LANCZOS4 || m0 == GR_LINEAR_AREA;
+            for (const ResizeJob& R : jobs) one = one && R.method == m0 && R.cn == cn_max;
+            if (one) {
+                const int sk = m0 == GR_CUBIC ? 4 : m0 == GR_LANCZOS4 ? 8 : 2;
+                static const int tr0 = std::getenv("AEON_HIP_SEP_TR") ? std::atoi(std::getenv("AEON_HIP_SEP_TR")) : 32;
+                int       cw = std::min(ww, 1024 / cn_max), tr = std::max(4, std::min(64, tr0));
+                // staged rows: whole 16-byte blocks (resize_sep), hence up to 30 bytes more per row
+                auto sw = [&] { return (bytes_for(cw) + 30 + 15) / 16 * 16; };
+                auto l  = [&] { return ((size_t)(cw + tr) * (1 + sk) * 4 + 15) / 16 * 16 + (size_t)rows_for(tr) * sw(); };
+                while (l() > kSepLds && tr > 4) tr /= 2;
+                if (l() <= kSepLds) sep = sk, TR = tr, CW = cw, NR = rows_for(tr), SW = sw();
+            }
+        }
         max_tiles = 0;
         bytes     = 0;
         for (ResizeJob& R : jobs) {
@@ -520,6 +560,7 @@ struct GrPlan {
         }
     }
     static constexpr size_t kGenericLds = 64 * 1024;
+    static constexpr size_t kSepLds     = 40 * 1024; // (four bands per CU)
 };
 
 // A resize of the (cropped, padded) region of J's source to its window, into scratch at `off`.
@@ -1634,8 +1675,12 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
         KernelTimer t{};
         if (timed) t = take_timer(ctx, KM_RAW, g.bytes);
         if (timed) HIP_OK(hipEventRecord(t.start, stream));
-        HIP_OK(launch_resize_generic((const ResizeJob*)(table + g.off), table, (int)g.jobs.size(), g.max_tiles, g.TR, g.CW,
-                                     g.NR, g.xs, g.amax, g.cn_max, ctx->d_error, stream));
+        if (g.sep)
+            HIP_OK(launch_resize_sep(g.sep, (const ResizeJob*)(table + g.off), table, (int)g.jobs.size(), g.max_tiles, g.TR,
+                                     g.CW, g.NR, g.SW, g.cn_max, ctx->d_error, stream));
+        else
+            HIP_OK(launch_resize_generic((const ResizeJob*)(table + g.off), table, (int)g.jobs.size(), g.max_tiles, g.TR,
+                                         g.CW, g.NR, g.xs, g.amax, g.cn_max, g.SW, ctx->d_error, stream));
         if (timed) {
             HIP_OK(hipEventRecord(t.stop, stream));
             ctx->timers.push_back(t);
