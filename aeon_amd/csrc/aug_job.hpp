@@ -117,7 +117,8 @@ struct alignas(16) ResizeJob {
     int32_t  coef_x, coef_y;                 // GR_LANCZOS4: host-built taps, byte offsets in the call's table
     int32_t  tiles_x, tiles;                 // column bands of the window, tiles in all
     int32_t  src_scratch, out_scratch;       // host bookkeeping: offsets into the slot scratch until relocated
-    int32_t  pad_[2];
+    int32_t  final_out, flip;                // final_out: out_ptr is the loader's item (flip, standardize LUT,
+    int32_t  out_pitch, out_plane;           // f32 planes or HWC at these strides), no copy pass after this one
 };
 // GR_LANCZOS4 taps per destination column / row as the host builds them (interpolateLanczos4 with
 // the C library's sin / cos, as OpenCV): first source index, then 8 fixed-point coefficients.

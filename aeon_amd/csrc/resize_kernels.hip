@@ -145,13 +145,65 @@ __device__ __forceinline__ void area_taps(int ssize, double scale, int d, int* t
 
 } // namespace
 
-// grid (tiles, jobs); LDS: xt[CW][xs] | yt[TR][xs] | H[NR][CW * cn] words | S[NR][SW] bytes.
+// The loader for a final_out job (stage.cpp plan_image: no photometric stage, f32 output): element e
+// of window row y (pixel e / cn, source channel e % cn) -> cv::flip, BGR->RGB, the standardize LUT (in
+// LDS, [source channel][value]), stored into the output item's plane (channel-major) or pixel.
+__device__ __forceinline__ void store_final(const ResizeJob& J, const float* lut, int bgr, int chm, int y, int x0, int e0,
+                                            int nb, uint32_t word)
+{
+    const auto o  = (__attribute__((address_space(1))) float*)J.out_ptr;
+    const int  cn = J.cn;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const int e = e0 + q;
+        if (e >= nb) break;
+        const int px = e / cn, c = e - px * cn;
+        const int x  = x0 + px;
+        const int ox = J.flip ? J.win_w - 1 - x : x;
+        const int oc = bgr ? 2 - c : c;
+        const int i  = chm ? oc * J.out_plane + y * J.out_pitch + ox : (y * J.out_pitch + ox) * cn + oc;
+        o[i]         = lut[c * 256 + ((word >> (8 * q)) & 0xff)];
+    }
+}
+
+// store_final for 4 consecutive pixels x, x + 1, ... (n of them valid) of source channel c: one float4
+// into the channel's plane when the 4 output elements are contiguous and 16-byte aligned (reversed
+// when flipped), element stores otherwise.
+__device__ __forceinline__ void store_planar(const ResizeJob& J, const float* lut, int bgr, int chm, int y, int x, int c, int n,
+                                             uint32_t word)
+{
+    typedef float f32x4 __attribute__((ext_vector_type(4)));
+    const auto o  = (__attribute__((address_space(1))) float*)J.out_ptr;
+    const int  cn = J.cn, oc = bgr ? 2 - c : c;
+    float      v[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) v[q] = lut[c * 256 + ((word >> (8 * q)) & 0xff)];
+    if (chm && n >= 4) {
+        const int  lo = J.flip ? J.win_w - 1 - (x + 3) : x; // the lowest of the 4 output columns
+        const int  i  = oc * J.out_plane + y * J.out_pitch + lo;
+        const auto p  = o + i;
+        if (((uintptr_t)p & 15) == 0) {
+            const f32x4 q4 = J.flip ? (f32x4){v[3], v[2], v[1], v[0]} : (f32x4){v[0], v[1], v[2], v[3]};
+            __builtin_nontemporal_store(q4, (__attribute__((address_space(1))) f32x4*)p);
+            return;
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        if (q >= n) break;
+        const int ox = J.flip ? J.win_w - 1 - (x + q) : x + q;
+        o[chm ? oc * J.out_plane + y * J.out_pitch + ox : (y * J.out_pitch + ox) * cn + oc] = v[q];
+    }
+}
+
+// grid (tiles, jobs); LDS: xt[CW][xs] | yt[TR][xs] | H[NR][CW * cn] words | S[NR][SW] bytes | LUT.
 // S holds the tile's source rows [r_lo, r_hi] x columns [u_lo, u_hi] as src_px gives them (add_padding's
 // zero border applied while staging), so both passes read LDS only: the horizontal pass one (row,
 // column) per lane with the column's taps in registers, the vertical pass 4 consecutive output bytes
 // per lane (one dword store) -- an element's H word is row * CW * cn + its byte index in the row.
 __global__ __launch_bounds__(256) void resize_generic(const ResizeJob* __restrict__ jobs, const uint8_t* __restrict__ table,
-                                                      int TR, int CW, int NR, int xs, int amax, int SW, int32_t* error)
+                                                      int TR, int CW, int NR, int xs, int amax, int SW, const float* lutg,
+                                                      int bgr, int chm, int32_t* error)
 {
     extern __shared__ int lds_w[];
     const ResizeJob J = jobs[blockIdx.y];
@@ -186,6 +238,9 @@ __global__ __launch_bounds__(256) void resize_generic(const ResizeJob* __restric
     int*       yt = xt + CW * xs;
     int*       H  = yt + TR * xs;
     uint8_t*   S  = (uint8_t*)(H + NR * rowH);
+    float*     lut = (float*)(S + NR * SW); // (final_out jobs)
+    if (J.final_out)
+        for (int i = tid; i < 768; i += nt) lut[i] = lutg[i];
     // taps of the tile's columns and rows
     for (int i = tid; i < nx; i += nt) {
         int* t = xt + i * xs;
@@ -358,6 +413,10 @@ __global__ __launch_bounds__(256) void resize_generic(const ResizeJob* __restric
             vals[k4] = v;
             word |= (uint32_t)v << (8 * k4);
         }
+        if (J.final_out) {
+            store_final(J, lut, bgr, chm, y0 + r, x0, e0, nb, word);
+            continue;
+        }
         const auto dst = out + ((size_t)(y0 + r) * J.win_w + x0) * cn + e0;
         if (e0 + 4 <= nb && ((uintptr_t)dst & 3) == 0) {
             *(__attribute__((address_space(1))) uint32_t*)dst = word;
@@ -377,7 +436,7 @@ __global__ __launch_bounds__(256) void resize_generic(const ResizeJob* __restric
 // arithmetic as resize_generic, element for element.
 template <int K>
 __global__ __launch_bounds__(256) void resize_sep(const ResizeJob* __restrict__ jobs, const uint8_t* __restrict__ table, int TR,
-                                                  int CW, int NR, int SW, int32_t* error)
+                                                  int CW, int NR, int SW, const float* lutg, int bgr, int chm, int32_t* error)
 {
     extern __shared__ int lds_w[];
     const ResizeJob J = jobs[blockIdx.y];
@@ -391,6 +450,9 @@ __global__ __launch_bounds__(256) void resize_sep(const ResizeJob* __restrict__ 
     int*          xt  = lds_w;
     int*          yt  = xt + CW * xs;
     uint8_t*      S   = (uint8_t*)lds_w + ((CW + TR) * xs * 4 + 15) / 16 * 16; // (16-aligned rows)
+    float*        lut = (float*)(S + NR * SW);                                 // (final_out jobs)
+    if (J.final_out)
+        for (int i = tid; i < 768; i += nt) lut[i] = lutg[i];
     for (int i = tid; i < nx; i += nt) {
         int* t = xt + i * xs;
         if (K == 8) {
@@ -487,13 +549,25 @@ __global__ __launch_bounds__(256) void resize_sep(const ResizeJob* __restrict__ 
         }
     }
     __syncthreads();
+    // The lane's 4 elements: 4 consecutive bytes of the window row (a u8 window: one dword store),
+    // or, for a final_out job, 4 consecutive pixels of one channel (one float4 store into its plane).
     const int nb = nx * cn, e0 = tid * 4;
-    if (e0 >= nb) return; // (no barrier below)
-    // the lane's 4 elements: staged-byte offsets of their K column taps, and the coefficients
+    const int gpr = (nx + 3) >> 2, lc = tid / gpr, px0 = (tid - lc * gpr) * 4;
+    const bool planar = J.final_out != 0;
+    if (planar ? lc >= cn : e0 >= nb) return; // (no barrier below; the LUT was published by the staging barrier)
+    int px[4], ch[4], xe[4]; // pixel in the tile, channel, element of the full destination row
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const int e = min(e0 + q, nb - 1);
+        px[q]       = planar ? min(px0 + q, nx - 1) : e / cn;
+        ch[q]       = planar ? lc : e - (e / cn) * cn;
+        xe[q]       = (J.win_x + x0 + px[q]) * cn + ch[q];
+    }
+    // staged-byte offsets of their K column taps, and the coefficients
     int off[4][K], cf[4][K];
 #pragma unroll
     for (int q = 0; q < 4; q++) {
-        const int  e = min(e0 + q, nb - 1), i = e / cn, c = e - i * cn;
+        const int  i = px[q], c = ch[q];
         const int* t = xt + i * xs;
 #pragma unroll
         for (int j = 0; j < K; j++) {
@@ -501,7 +575,7 @@ __global__ __launch_bounds__(256) void resize_sep(const ResizeJob* __restrict__ 
             cf[q][j]  = t[1 + j];
         }
     }
-    const int W = J.dst_w * cn, xv = simd_end(K, W), xb = (J.win_x + x0) * cn + e0;
+    const int W = J.dst_w * cn, xv = simd_end(K, W), xmax = max(max(xe[0], xe[1]), max(xe[2], xe[3]));
     // The window: hw[j][q] = horizontal sum of staged row wrow[j] for element q, as float (exact:
     // |sum| < 2^24).  The row indices are workgroup-uniform (scalar registers), so the window's reuse
     // tests are scalar branches; a row not in the window is summed from its staged bytes.
@@ -574,10 +648,10 @@ __global__ __launch_bounds__(256) void resize_sep(const ResizeJob* __restrict__ 
                 word = __builtin_amdgcn_cvt_pk_u8_f32(sm.y, (uint32_t)qb, word);
             }
         }
-        if (K != 4 || xb + 3 >= xv) { // the other forms, and elements on the scalar tail
+        if (K != 4 || xmax >= xv) { // the other forms, and elements on the scalar tail
 #pragma unroll
             for (int q = 0; q < 4; q++) {
-                const int x = xb + q;
+                const int x = xe[q];
                 int       v;
                 if (K == 4 && x < xv) continue;
                 if (K == 2 && x < xv) { // VResizeLinearVec_32s8u
@@ -593,6 +667,10 @@ __global__ __launch_bounds__(256) void resize_sep(const ResizeJob* __restrict__ 
                 word = (word & ~(0xffu << (8 * q))) | ((uint32_t)v << (8 * q));
             }
         }
+        if (planar) {
+            if (!(AEON_RG_SKIP & 2) || word == 0x12345678u) store_planar(J, lut, bgr, chm, y0 + r, x0 + px0, lc, nx - px0, word);
+            continue;
+        }
         const auto dst = out + ((size_t)(y0 + r) * J.win_w + x0) * cn + e0;
         if ((AEON_RG_SKIP & 2) && word != 0x12345678u) {
         } else if (e0 + 4 <= nb && ((uintptr_t)dst & 3) == 0) {
@@ -604,28 +682,29 @@ __global__ __launch_bounds__(256) void resize_sep(const ResizeJob* __restrict__ 
 }
 
 hipError_t launch_resize_sep(int K, const ResizeJob* jobs, const uint8_t* table, int n_jobs, int max_tiles, int TR, int CW,
-                             int NR, int SW, int cn, int32_t* error, hipStream_t stream)
+                             int NR, int SW, int cn, const float* lut, int bgr, int chm, int32_t* error, hipStream_t stream)
 {
     if (n_jobs <= 0) return hipSuccess;
-    const size_t lds     = ((size_t)(CW + TR) * (1 + K) * 4 + 15) / 16 * 16 + (size_t)NR * SW;
-    const int    threads = std::min(256, ((CW * cn + 3) / 4 + 63) / 64 * 64);
+    const size_t lds     = ((size_t)(CW + TR) * (1 + K) * 4 + 15) / 16 * 16 + (size_t)NR * SW + (lut ? 768 * 4 : 0);
+    const int    threads = std::min(256, (std::max((CW * cn + 3) / 4, cn * ((CW + 3) / 4)) + 63) / 64 * 64);
     const dim3   grid((unsigned)max_tiles, (unsigned)n_jobs);
     switch (K) {
-    case 2: hipLaunchKernelGGL(resize_sep<2>, grid, dim3(threads), lds, stream, jobs, table, TR, CW, NR, SW, error); break;
-    case 4: hipLaunchKernelGGL(resize_sep<4>, grid, dim3(threads), lds, stream, jobs, table, TR, CW, NR, SW, error); break;
-    case 8: hipLaunchKernelGGL(resize_sep<8>, grid, dim3(threads), lds, stream, jobs, table, TR, CW, NR, SW, error); break;
+    case 2: hipLaunchKernelGGL(resize_sep<2>, grid, dim3(threads), lds, stream, jobs, table, TR, CW, NR, SW, lut, bgr, chm, error); break;
+    case 4: hipLaunchKernelGGL(resize_sep<4>, grid, dim3(threads), lds, stream, jobs, table, TR, CW, NR, SW, lut, bgr, chm, error); break;
+    case 8: hipLaunchKernelGGL(resize_sep<8>, grid, dim3(threads), lds, stream, jobs, table, TR, CW, NR, SW, lut, bgr, chm, error); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
 }
 
 hipError_t launch_resize_generic(const ResizeJob* jobs, const uint8_t* table, int n_jobs, int max_tiles, int TR, int CW,
-                                 int NR, int xs, int amax, int cn_max, int SW, int32_t* error, hipStream_t stream)
+                                 int NR, int xs, int amax, int cn_max, int SW, const float* lut, int bgr, int chm,
+                                 int32_t* error, hipStream_t stream)
 {
     if (n_jobs <= 0) return hipSuccess;
-    const size_t lds = ((size_t)CW * xs + (size_t)TR * xs + (size_t)NR * CW * cn_max) * 4 + (size_t)NR * SW;
+    const size_t lds = ((size_t)CW * xs + (size_t)TR * xs + (size_t)NR * CW * cn_max) * 4 + (size_t)NR * SW + (lut ? 768 * 4 : 0);
     hipLaunchKernelGGL(resize_generic, dim3((unsigned)max_tiles, (unsigned)n_jobs), dim3(256), lds, stream, jobs, table, TR,
-                       CW, NR, xs, amax, SW, error);
+                       CW, NR, xs, amax, SW, lut, bgr, chm, error);
     return hipGetLastError();
 }
 

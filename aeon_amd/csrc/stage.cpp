@@ -47,9 +47,10 @@ hipError_t launch_contrast_records(bool fast, bool split, const LaunchArgs& a, c
                                    hipEvent_t start, hipEvent_t stop);
 hipError_t contrast_records_lds_limit(int bytes);
 hipError_t launch_resize_generic(const ResizeJob* jobs, const uint8_t* table, int n_jobs, int max_tiles, int TR, int CW,
-                                 int NR, int xs, int amax, int cn_max, int SW, int32_t* error, hipStream_t stream);
+                                 int NR, int xs, int amax, int cn_max, int SW, const float* lut, int bgr, int chm,
+                                 int32_t* error, hipStream_t stream);
 hipError_t launch_resize_sep(int K, const ResizeJob* jobs, const uint8_t* table, int n_jobs, int max_tiles, int TR, int CW,
-                             int NR, int SW, int cn, int32_t* error, hipStream_t stream);
+                             int NR, int SW, int cn, const float* lut, int bgr, int chm, int32_t* error, hipStream_t stream);
 void       jpeg_decode_batch(JpegState* S, int n, const void* const* data, const size_t* sizes,
                              const aeon_img_desc* descs, void* dst_base, int32_t* error, hipStream_t stream,
                              hipEvent_t start, hipEvent_t stop);
@@ -456,6 +457,7 @@ struct GrPlan {
     size_t                 off = 0, taps_off = 0; // byte offsets in the call's table
     int TR = 16, CW = 128, NR = 1, xs = 3, amax = 1, cn_max = 1, max_tiles = 0, SW = 4;
     int sep = 0; // K of resize_sep when every job is one fixed-K method and its band fits (else 0: resize_generic)
+    bool any_final = false; // some job writes the loader's output itself (its LUT in the launch's LDS)
     double bytes = 0; // algorithmic: the source region read once + the window written
 
     size_t n_taps = 0; // Lanczos4 taps reserved by add(), computed by fill_taps()
@@ -509,6 +511,9 @@ struct GrPlan {
     void finalize()
     {
         if (jobs.empty()) return;
+        any_final = false;
+        for (const ResizeJob& R : jobs) any_final = any_final || R.final_out;
+        const size_t lut_lds = any_final ? 768 * 4 : 0;
         int K = 2, ww = 1;
         for (const ResizeJob& R : jobs) {
             K = std::max(K, R.method == GR_CUBIC ? 4 : (R.method == GR_LANCZOS4 ? 8 : 2));
@@ -524,7 +529,7 @@ struct GrPlan {
         bool staged = true;
         auto lds    = [&] {
             return ((size_t)CW * xs + (size_t)TR * xs + (size_t)rows_for(TR) * CW * cn_max) * 4 +
-                   (staged ? (size_t)rows_for(TR) * bytes_for(CW) : 0);
+                   (staged ? (size_t)rows_for(TR) * bytes_for(CW) : 0) + lut_lds;
         };
         staged = lds() <= kGenericLds;
         while (lds() > kGenericLds && TR > 1) TR--;
@@ -544,7 +549,9 @@ struct GrPlan {
                 int       cw = std::min(ww, 1024 / cn_max), tr = std::max(4, std::min(64, tr0));
                 // staged rows: whole 16-byte blocks (resize_sep), hence up to 30 bytes more per row
                 auto sw = [&] { return (bytes_for(cw) + 30 + 15) / 16 * 16; };
-                auto l  = [&] { return ((size_t)(cw + tr) * (1 + sk) * 4 + 15) / 16 * 16 + (size_t)rows_for(tr) * sw(); };
+                auto l  = [&] {
+                    return ((size_t)(cw + tr) * (1 + sk) * 4 + 15) / 16 * 16 + (size_t)rows_for(tr) * sw() + lut_lds;
+                };
                 while (l() > kSepLds && tr > 4) tr /= 2;
                 if (l() <= kSepLds) sep = sk, TR = tr, CW = cw, NR = rows_for(tr), SW = sw();
             }
@@ -556,7 +563,7 @@ struct GrPlan {
             R.tiles   = R.tiles_x * ((R.win_h + TR - 1) / TR);
             max_tiles = std::max(max_tiles, R.tiles);
             bytes += (double)R.crop_w * R.crop_h * R.cn * ((double)R.win_w / R.dst_w) * ((double)R.win_h / R.dst_h) +
-                     (double)R.win_w * R.win_h * R.cn;
+                     (double)R.win_w * R.win_h * R.cn * (R.final_out ? 4 : 1);
         }
     }
     static constexpr size_t kGenericLds = 64 * 1024;
@@ -671,6 +678,17 @@ void plan_image(const aeon_img_desc& d, const void* src_base, const aeon_aug_par
     }
     int isx = 0, isy = 0;
     const int gm = is_mask ? -1 : generic_method(J.crop_w, J.crop_h, J.dst_w, J.dst_h, p.interp, cn, &isx, &isy);
+    if (gm >= 0 && gm != GR_AREA_FAST && J.photo == 0 && o.dtype == AEON_DTYPE_F32 && !o.fixed_aspect_ratio &&
+        (cn == 1 || cn == 3) && (o.channels == cn)) {
+        // no photometric stage and f32 output: the resize pass is the last one -- it flips,
+        // standardizes through the LUT and stores the loader's layout itself (no u8 window in scratch,
+        // no copy pass)
+        ResizeJob R = resize_job(J, gm, isx, isy);
+        R.out_ptr   = J.out_ptr;
+        R.final_out = 1, R.flip = J.flip, R.out_pitch = J.out_pitch, R.out_plane = J.out_plane;
+        gr_main.add(R);
+        return;
+    }
     if (gm >= 0) {
         // CUBIC / LANCZOS4 / INTER_AREA resize of the (padded) crop into scratch (resize_kernels.hip),
         // then the photometric stages, flip and the loader as a copy pass over it
@@ -1675,12 +1693,14 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
         KernelTimer t{};
         if (timed) t = take_timer(ctx, KM_RAW, g.bytes);
         if (timed) HIP_OK(hipEventRecord(t.start, stream));
+        const float* glut = g.any_final ? d_lut : nullptr;
+        const int    gbgr = o.bgr_to_rgb && o.channels == 3, gchm = o.channel_major;
         if (g.sep)
             HIP_OK(launch_resize_sep(g.sep, (const ResizeJob*)(table + g.off), table, (int)g.jobs.size(), g.max_tiles, g.TR,
-                                     g.CW, g.NR, g.SW, g.cn_max, ctx->d_error, stream));
+                                     g.CW, g.NR, g.SW, g.cn_max, glut, gbgr, gchm, ctx->d_error, stream));
         else
             HIP_OK(launch_resize_generic((const ResizeJob*)(table + g.off), table, (int)g.jobs.size(), g.max_tiles, g.TR,
-                                         g.CW, g.NR, g.xs, g.amax, g.cn_max, g.SW, ctx->d_error, stream));
+                                         g.CW, g.NR, g.xs, g.amax, g.cn_max, g.SW, glut, gbgr, gchm, ctx->d_error, stream));
         if (timed) {
             HIP_OK(hipEventRecord(t.stop, stream));
             ctx->timers.push_back(t);

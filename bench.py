@@ -860,16 +860,25 @@ def main():
             side(extra, "two_streams", two_streams)
         side(extra, "C5", lambda: run_c5(A, C, torch, max(20, args.steps), 3, args.pool_mib))
 
-        # aeon's other interpolation methods on the C2 workload: a generic resize pre-pass
-        # (OpenCV 2.4's resizeGeneric_ / resizeArea_) into scratch, then the tile kernel's copy pass
+        # aeon's other interpolation methods on the C2 workload: CUBIC / LANCZOS4 as resize_sep bands and
+        # AREA as resize_generic tiles, writing the loader's f32 CHW output themselves (no photometric
+        # stage in C2); the rate from an untimed run, each kernel kind's time, bytes and HBM fraction
+        # from a second run with every launch timed
         def interpolation():
             out = {}
             for m in ("CUBIC", "AREA", "LANCZOS4"):
-                em, ktm, _, _ = run_device(A, C, torch, "C2:" + m, batch, 20, 3, 0, 1, args.pool_mib, None, 1)
-                out[m] = {"value": batch * 20 / em, "unit": "images/s", "ms_per_step": em / 20 * 1e3,
-                          "kernels_us_per_step": {k: v[0] / 20 * 1e3 for k, v in ktm.items() if v[2]}}
-            out["what"] = ("C2 workload (batch 256) with interpolation_method set; every launch timed "
-                           "(events idle the queue between launches: rates are lower bounds)")
+                em, _, _, _ = run_device(A, C, torch, "C2:" + m, batch, 20, 3, 0, 1, args.pool_mib, None, 0)
+                _, ktm, _, _ = run_device(A, C, torch, "C2:" + m, batch, 20, 3, 0, 1, args.pool_mib, None, 1)
+                kinds = {}
+                for k, (ms, by, n) in ktm.items():
+                    if n and ms > 0:
+                        gbs = by / (ms * 1e-3) / 1e9
+                        kinds[k] = {"us_per_step": ms / 20 * 1e3, "algorithmic_bytes_per_step": by / 20,
+                                    "gbs": gbs, "roofline_frac": gbs / HBM_PEAK_GBS}
+                out[m] = {"value": batch * 20 / em, "unit": "images/s", "ms_per_step": em / 20 * 1e3, "kernels": kinds}
+            out["what"] = ("C2 workload (batch 256) with interpolation_method set: value from an untimed run; "
+                           "kernels: 'pre' = the resize pass (resize_sep / resize_generic, f32 CHW output), 'augment' = "
+                           "tile launches of records the resize pass does not take; every launch timed there")
             return out
         side(extra, "interpolation", interpolation)
         side(extra, "e2e_host_to_host", lambda: {
