@@ -10,6 +10,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <stdexcept>
@@ -1033,6 +1036,17 @@ void jpeg_decode_batch(JpegState* S, int n, const void* const* data, const size_
                        void* dst_base, int32_t* error, hipStream_t stream, hipEvent_t start, hipEvent_t stop)
 {
     std::lock_guard<std::mutex> lock(S->mu);
+    // (AEON_HIP_JPEG_PROFILE=1, development: host time per phase of each call on stderr)
+    static const bool prof = std::getenv("AEON_HIP_JPEG_PROFILE") && std::atoi(std::getenv("AEON_HIP_JPEG_PROFILE"));
+    using clk = std::chrono::steady_clock;
+    auto t0 = clk::now();
+    double tp[6] = {0};
+    auto mark = [&](int k) {
+        if (!prof) return;
+        const auto t = clk::now();
+        tp[k] = std::chrono::duration<double, std::micro>(t - t0).count();
+        t0 = t;
+    };
     for (auto& a : S->arenas) a.used = 0;
     std::vector<Frame>   frames(n);
     std::vector<int>     owner(n);
@@ -1060,6 +1074,7 @@ void jpeg_decode_batch(JpegState* S, int n, const void* const* data, const size_
             throw jpeg_error(e.code, std::string(e.what()) + " (record " + std::to_string(i) + ")");
         }
     });
+    mark(0);
     // device layout of the call: [images][GPU-decoded files][chunks][rows][arena 0][arena 1]...; the
     // work buffer (device only): [block records of the GPU-decoded files][their dense coefficients]
     // [their subsequence scratch]
@@ -1112,10 +1127,12 @@ void jpeg_decode_batch(JpegState* S, int n, const void* const* data, const size_
         arena_off[w] = total;
         total += (S->arenas[w].used + 255) & ~(size_t)255;
     }
+    mark(1);
     JpegState::Set& st = S->sets[S->next];
     S->next ^= 1;
     if (!st.done) hip_ok(hipEventCreateWithFlags(&st.done, hipEventDisableTiming), "hipEventCreate");
     if (st.pending) hip_ok(hipEventSynchronize(st.done), "hipEventSynchronize");
+    mark(2);
     st.pending = false;
     grow_buf(st.pinned, st.pinned_cap, total, true);
     grow_buf(st.dev, st.dev_cap, total, false);
@@ -1172,9 +1189,11 @@ void jpeg_decode_batch(JpegState* S, int n, const void* const* data, const size_
     }
     if (!chunks.empty()) std::memcpy(st.pinned + chk_off, chunks.data(), chunks.size() * sizeof(JpegChunk));
     if (!rows.empty()) std::memcpy(st.pinned + row_off, rows.data(), rows.size() * sizeof(JpegRows));
+    mark(3);
     S->pool->run((int)S->arenas.size(), [&](int w) {
         if (S->arenas[w].used) std::memcpy(st.pinned + arena_off[w], S->arenas[w].host.data(), S->arenas[w].used);
     });
+    mark(4);
     if (S->use_copy) { // (the set's previous kernels are done: st.done above)
         if (!S->copy) hip_ok(hipStreamCreateWithFlags(&S->copy, hipStreamNonBlocking), "hipStreamCreate");
         if (!st.copied) hip_ok(hipEventCreateWithFlags(&st.copied, hipEventDisableTiming), "hipEventCreate");
@@ -1195,6 +1214,10 @@ void jpeg_decode_batch(JpegState* S, int n, const void* const* data, const size_
     if (stop) hip_ok(hipEventRecord(stop, stream), "hipEventRecord");
     hip_ok(hipEventRecord(st.done, stream), "hipEventRecord");
     st.pending = true;
+    mark(5);
+    if (prof)
+        std::fprintf(stderr, "[jpeg stage] n=%d bytes=%zu us: pool %.0f layout %.0f set_wait %.0f fill %.0f arena_copy %.0f enqueue %.0f\n",
+                     n, total, tp[0], tp[1], tp[2], tp[3], tp[4], tp[5]);
 }
 
 // aeon_jpeg_info's body.
