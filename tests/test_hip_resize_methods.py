@@ -132,3 +132,29 @@ def test_resize_methods_mixed_batch(ctx):
                                    brightness=0.9 if i % 4 == 0 else 1.0))
     out = A.out_desc(item_stride=3 * 224 * 224 * 4, **F32)
     _assert_same(H.hip_records(ctx, imgs, params, out), H.oracle_records(imgs, params, out), "mixed")
+
+
+F32_HWC = dict(channels=3, channel_major=False, bgr_to_rgb=True, dtype="float32", mean=C.MEAN, stddev=C.STDDEV)
+
+
+@pytest.mark.parametrize("method", list(METHODS))
+@pytest.mark.parametrize("case", ["hwc", "gray", "padded", "odd_stride", "no_mean"])
+def test_resize_methods_final_output(ctx, method, case):
+    """Records with no photometric stage and f32 output: the resize pass writes the loader's layout
+    itself (ResizeJob.final_out -- flip, BGR->RGB, the standardize LUT, planes or pixels).  Covers the
+    HWC layout, one channel, add_padding's border, item strides that leave the planes' rows off 16-byte
+    alignment (element stores instead of float4), and no mean/stddev (the LUT is (float)x)."""
+    cn = 1 if case == "gray" else 3
+    imgs = [A.synthetic_image(40 + i, 211, 157, cn) for i in range(4)]
+    sizes = [(224, 224), (97, 61), (101, 45), (35, 160)]
+    pad = dict(padding=8, pad_off_x=3, pad_off_y=12) if case == "padded" else {}
+    params = [A.aug_params(crop_x=5 + i, crop_y=3, crop_w=180 - 7 * i, crop_h=140 - 5 * i, out_w=ow, out_h=oh,
+                           flip=i % 2, interp=METHODS[method], **pad) for i, (ow, oh) in enumerate(sizes)]
+    ok = dict(F32_HWC if case == "hwc" else F32)
+    if cn == 1:
+        ok.update(channels=1, bgr_to_rgb=False, mean=[0.5], stddev=[0.25])
+    if case == "no_mean":
+        ok.pop("mean"), ok.pop("stddev")
+    stride = 224 * 224 * cn * 4 + (36 if case == "odd_stride" else 0)
+    out = A.out_desc(item_stride=stride, **ok)
+    _assert_same(H.hip_records(ctx, imgs, params, out), H.oracle_records(imgs, params, out), f"{method} {case}")
