@@ -982,6 +982,14 @@ const uint8_t* publish_table(aeon_hip_ctx* ctx, Slot& s, size_t bytes)
     return s.vram;
 }
 
+// publish_table for a table the host wrote into s.vram itself: the fence and the read-back only.
+const uint8_t* publish_written(Slot& s, size_t bytes)
+{
+    std::atomic_thread_fence(std::memory_order_seq_cst);
+    (void)*(volatile const uint32_t*)(s.vram + ((bytes - 1) & ~(size_t)3));
+    return s.vram;
+}
+
 // Wait until no kernel of any ring slot can still be running.
 void drain_ring(aeon_hip_ctx* ctx)
 {
@@ -1289,22 +1297,28 @@ bool run_direct(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void
     // without photometric stages the tiles read only each job's hot half: the table holds just those
     // (half the bytes the host writes and publishes)
     const size_t stride = P.photo ? sizeof(AugJob) : (size_t)kJobHotBytes;
+    const size_t tbytes = (size_t)n * stride;
+    // the jobs go straight into the slot's HBM table when it has one (no pinned copy first), else
+    // into the pinned slot the tiles read over PCIe
+    const bool vram = ctx->vram_jobs && tbytes > 0 && tbytes <= kVramTableMax && tbytes <= s.vram_cap;
+    uint8_t*   dstt = vram ? s.vram : s.host;
     for (int i = 0; i < n; i++) {
         AugJob& J = jobs[i];
         J.tiles   = (J.win_h + P.tr - 1) / P.tr;
-        std::memcpy(s.host + i * stride, &J, stride);
+        std::memcpy(dstt + i * stride, &J, stride);
     }
     phase(4);
     const bool timed = ctx->timing && (ctx->timing_calls++ % ctx->timing_every) == ctx->timing_every - 1;
     if (o.fixed_aspect_ratio) // std::fill_n of each item's canvas, its whole byte size (etl_image.cpp:263)
         HIP_OK(hipMemset2DAsync(out_dev, o.item_stride, 0,
                                 (size_t)o.canvas_w * o.canvas_h * o.channels * out_elem_bytes(od.dtype), n, stream));
-    const uint8_t* vt = publish_table(ctx, s, (size_t)n * stride);
+    const uint8_t* vt = vram ? publish_written(s, tbytes) : nullptr;
     phase(5);
     LaunchArgs     a  = launch_args(ctx, s, vt ? vt : s.host_dev, P, n, o, d_lut, 1, ov.u8_map);
     a.job_stride      = (int)stride;
     a.jobs_host       = 1; // (read-through loads: pinned host memory, or the uncached HBM copy)
-    timed_launch(ctx, KM_FINAL, P, a, stream, launch_bytes(geo, KM_FINAL, out_elem_bytes(o.dtype)), timed);
+    // (the algorithmic bytes only for a timed launch: a pass over the records the call does not need)
+    timed_launch(ctx, KM_FINAL, P, a, stream, timed ? launch_bytes(geo, KM_FINAL, out_elem_bytes(o.dtype)) : 0, timed);
     phase(6);
     release_slot(ctx, slot, stream);
     phase(7);

@@ -235,9 +235,11 @@ class Workload:
         self.param_us = (time.perf_counter() - t0) / max(1, steps * batch) * 1e6
 
     def step(self, ctx, s, stream):
+        # (device addresses read once: aeon's host holds plain pointers, not torch tensors)
+        if not hasattr(self, "_ptrs"):
+            self._ptrs = (self.src.data_ptr(), [d.data_ptr() for d in self.dst])
         b = s % self.n_pool
-        ctx.augment_batch(self.descs[b], self.src.data_ptr(), self.params[s], self.out,
-                          self.dst[s & 1].data_ptr(), stream)
+        ctx.augment_batch(self.descs[b], self._ptrs[0], self.params[s], self.out, self._ptrs[1][s & 1], stream)
 
 
 def step_bytes(params):
