@@ -455,9 +455,16 @@ struct GrPlan {
     std::vector<ResizeJob> jobs;
     std::vector<GrTap>     taps;
     size_t                 off = 0, taps_off = 0; // byte offsets in the call's table
-    int TR = 16, CW = 128, NR = 1, xs = 3, amax = 1, cn_max = 1, max_tiles = 0, SW = 4;
-    int sep = 0; // K of resize_sep when every job is one fixed-K method and its band fits (else 0: resize_generic)
-    bool any_final = false; // some job writes the loader's output itself (its LUT in the launch's LDS)
+    // One launch per method class (finalize sorts the jobs so each class is contiguous): the
+    // fixed-K methods as resize_sep bands, the rest (INTER_AREA's float taps, integer boxes, jobs
+    // whose bands do not fit) as resize_generic tiles.
+    struct Sub {
+        int  first = 0, count = 0;
+        int  TR = 16, CW = 128, NR = 1, xs = 3, amax = 1, cn_max = 1, max_tiles = 0, SW = 4;
+        int  sep = 0;           // K of resize_sep, or 0: resize_generic
+        bool any_final = false; // some job writes the loader's output itself (its LUT in the launch's LDS)
+    };
+    std::vector<Sub> subs;
     double bytes = 0; // algorithmic: the source region read once + the window written
 
     size_t n_taps = 0; // Lanczos4 taps reserved by add(), computed by fill_taps()
@@ -484,86 +491,109 @@ struct GrPlan {
         if (pool && n_taps > 4096) pool->run((int)jobs.size(), one);
         else for (int i = 0; i < (int)jobs.size(); i++) one(i);
     }
-    // rows of H a tile of `tr` output rows needs at most
-    int rows_for(int tr) const
+    static int ksize(int m) { return m == GR_CUBIC ? 4 : (m == GR_LANCZOS4 ? 8 : 2); }
+    static int sep_k(int m) { return m == GR_CUBIC ? 4 : m == GR_LANCZOS4 ? 8 : m == GR_LINEAR_AREA ? 2 : 0; }
+    // rows of H a tile of `tr` output rows needs at most (jobs [f, f + n))
+    int rows_for(int f, int n, int tr) const
     {
         int nr = 1;
-        for (const ResizeJob& R : jobs) {
-            const int K = R.method == GR_CUBIC ? 4 : (R.method == GR_LANCZOS4 ? 8 : 2);
+        for (int i = f; i < f + n; i++) {
+            const ResizeJob& R = jobs[i];
             if (R.method == GR_AREA) nr = std::max(nr, (int)std::ceil(tr * R.scale_y) + 3);
-            else if (R.method != GR_AREA_FAST) nr = std::max(nr, (int)std::ceil((tr - 1) * R.scale_y) + K + 2);
+            else if (R.method != GR_AREA_FAST) nr = std::max(nr, (int)std::ceil((tr - 1) * R.scale_y) + ksize(R.method) + 2);
         }
         return nr;
     }
     // staged source bytes per row a tile of `cw` output columns needs at most (a multiple of 4)
-    int bytes_for(int cw) const
+    int bytes_for(int f, int n, int cw) const
     {
         int sw = 4;
-        for (const ResizeJob& R : jobs) {
-            const int K = R.method == GR_CUBIC ? 4 : (R.method == GR_LANCZOS4 ? 8 : 2);
-            int cols = 1;
+        for (int i = f; i < f + n; i++) {
+            const ResizeJob& R = jobs[i];
+            int              cols = 1;
             if (R.method == GR_AREA) cols = (int)std::ceil(cw * R.scale_x) + 4;
-            else if (R.method != GR_AREA_FAST) cols = (int)std::ceil((cw - 1) * R.scale_x) + K + 2;
+            else if (R.method != GR_AREA_FAST) cols = (int)std::ceil((cw - 1) * R.scale_x) + ksize(R.method) + 2;
             sw = std::max(sw, (std::min(cols, R.crop_w) * R.cn + 3) / 4 * 4);
         }
         return sw;
     }
-    void finalize()
+    // the launch shape of jobs [f, f + n): resize_sep when they are one fixed-K class of one channel
+    // count and a band fits, else resize_generic
+    Sub shape(int f, int n) const
     {
-        if (jobs.empty()) return;
-        any_final = false;
-        for (const ResizeJob& R : jobs) any_final = any_final || R.final_out;
-        const size_t lut_lds = any_final ? 768 * 4 : 0;
-        int K = 2, ww = 1;
-        for (const ResizeJob& R : jobs) {
-            K = std::max(K, R.method == GR_CUBIC ? 4 : (R.method == GR_LANCZOS4 ? 8 : 2));
-            if (R.method == GR_AREA)
-                amax = std::max(amax, (int)std::ceil(std::max(R.scale_x, R.scale_y)) + 3);
-            cn_max = std::max(cn_max, R.cn);
-            ww     = std::max(ww, R.win_w);
+        Sub u;
+        u.first = f, u.count = n;
+        for (int i = f; i < f + n; i++) u.any_final = u.any_final || jobs[i].final_out;
+        const size_t lut_lds = u.any_final ? 768 * 4 : 0;
+        int          K = 2, ww = 1;
+        for (int i = f; i < f + n; i++) {
+            const ResizeJob& R = jobs[i];
+            K = std::max(K, ksize(R.method));
+            if (R.method == GR_AREA) u.amax = std::max(u.amax, (int)std::ceil(std::max(R.scale_x, R.scale_y)) + 3);
+            u.cn_max = std::max(u.cn_max, R.cn);
+            ww       = std::max(ww, R.win_w);
         }
-        xs = std::max(1 + K, 2 + amax);
-        CW = std::min(128, ww);
-        TR = 16;
+        // resize_sep: bands of up to 32 rows x the window's width (at most 256 lanes of 4 bytes)
+        const int sk  = sep_k(jobs[f].method);
+        bool      one = sk != 0;
+        for (int i = f; i < f + n; i++) one = one && jobs[i].method == jobs[f].method && jobs[i].cn == u.cn_max;
+        if (one) {
+            static const int tr0 = std::getenv("AEON_HIP_SEP_TR") ? std::atoi(std::getenv("AEON_HIP_SEP_TR")) : 16;
+            int cw = std::min(ww, 1024 / u.cn_max), tr = std::max(4, std::min(64, tr0));
+            // staged rows: whole 16-byte blocks (resize_sep), hence up to 30 bytes more per row
+            auto sw = [&] { return (bytes_for(f, n, cw) + 30 + 15) / 16 * 16; };
+            auto l  = [&] {
+                return ((size_t)(cw + tr) * (1 + sk) * 4 + 15) / 16 * 16 + (size_t)rows_for(f, n, tr) * sw() + lut_lds;
+            };
+            while (l() > kSepLds && tr > 4) tr /= 2;
+            if (l() <= kSepLds) {
+                u.sep = sk, u.TR = tr, u.CW = cw, u.NR = rows_for(f, n, tr), u.SW = sw(), u.xs = 1 + sk;
+                return u;
+            }
+        }
+        u.xs = std::max(1 + K, 2 + u.amax);
+        u.CW = std::min(128, ww);
+        u.TR = 16;
         // with the source rows staged in LDS (SW > 0) when they fit at 16 x 128 tiles, else without
         bool staged = true;
         auto lds    = [&] {
-            return ((size_t)CW * xs + (size_t)TR * xs + (size_t)rows_for(TR) * CW * cn_max) * 4 +
-                   (staged ? (size_t)rows_for(TR) * bytes_for(CW) : 0) + lut_lds;
+            return ((size_t)u.CW * u.xs + (size_t)u.TR * u.xs + (size_t)rows_for(f, n, u.TR) * u.CW * u.cn_max) * 4 +
+                   (staged ? (size_t)rows_for(f, n, u.TR) * bytes_for(f, n, u.CW) : 0) + lut_lds;
         };
         staged = lds() <= kGenericLds;
-        while (lds() > kGenericLds && TR > 1) TR--;
-        while (lds() > kGenericLds && CW > 8) CW /= 2;
+        while (lds() > kGenericLds && u.TR > 1) u.TR--;
+        while (lds() > kGenericLds && u.CW > 8) u.CW /= 2;
         if (lds() > kGenericLds) fail(AEON_HIP_EUNSUPPORTED, "resize scale too large for the generic resize's LDS tiles");
-        NR        = rows_for(TR);
-        SW        = staged ? bytes_for(CW) : 0;
-        // resize_sep: bands of up to 32 rows x the window's width (at most 256 lanes of 4 bytes)
-        sep = 0;
-        {
-            const int m0 = jobs[0].method;
-            bool      one = m0 == GR_CUBIC || m0 == GR_LANCZOS4 || m0 == GR_LINEAR_AREA;
-            for (const ResizeJob& R : jobs) one = one && R.method == m0 && R.cn == cn_max;
-            if (one) {
-                const int sk = m0 == GR_CUBIC ? 4 : m0 == GR_LANCZOS4 ? 8 : 2;
-                static const int tr0 = std::getenv("AEON_HIP_SEP_TR") ? std::atoi(std::getenv("AEON_HIP_SEP_TR")) : 32;
-                int       cw = std::min(ww, 1024 / cn_max), tr = std::max(4, std::min(64, tr0));
-                // staged rows: whole 16-byte blocks (resize_sep), hence up to 30 bytes more per row
-                auto sw = [&] { return (bytes_for(cw) + 30 + 15) / 16 * 16; };
-                auto l  = [&] {
-                    return ((size_t)(cw + tr) * (1 + sk) * 4 + 15) / 16 * 16 + (size_t)rows_for(tr) * sw() + lut_lds;
-                };
-                while (l() > kSepLds && tr > 4) tr /= 2;
-                if (l() <= kSepLds) sep = sk, TR = tr, CW = cw, NR = rows_for(tr), SW = sw();
-            }
+        u.NR = rows_for(f, n, u.TR);
+        u.SW = staged ? bytes_for(f, n, u.CW) : 0;
+        return u;
+    }
+    void finalize()
+    {
+        subs.clear();
+        bytes = 0;
+        if (jobs.empty()) return;
+        // the classes contiguous: resize_sep's by K, then the generic methods
+        std::stable_sort(jobs.begin(), jobs.end(), [](const ResizeJob& a, const ResizeJob& b) {
+            const int ka = sep_k(a.method), kb = sep_k(b.method);
+            return (ka ? ka : 99) < (kb ? kb : 99);
+        });
+        for (int f = 0; f < (int)jobs.size();) {
+            int e = f + 1;
+            while (e < (int)jobs.size() && sep_k(jobs[e].method) == sep_k(jobs[f].method)) e++;
+            subs.push_back(shape(f, e - f));
+            f = e;
         }
-        max_tiles = 0;
-        bytes     = 0;
-        for (ResizeJob& R : jobs) {
-            R.tiles_x = (R.win_w + CW - 1) / CW;
-            R.tiles   = R.tiles_x * ((R.win_h + TR - 1) / TR);
-            max_tiles = std::max(max_tiles, R.tiles);
-            bytes += (double)R.crop_w * R.crop_h * R.cn * ((double)R.win_w / R.dst_w) * ((double)R.win_h / R.dst_h) +
-                     (double)R.win_w * R.win_h * R.cn * (R.final_out ? 4 : 1);
+        for (Sub& u : subs) {
+            u.max_tiles = 0;
+            for (int i = u.first; i < u.first + u.count; i++) {
+                ResizeJob& R = jobs[i];
+                R.tiles_x    = (R.win_w + u.CW - 1) / u.CW;
+                R.tiles      = R.tiles_x * ((R.win_h + u.TR - 1) / u.TR);
+                u.max_tiles  = std::max(u.max_tiles, R.tiles);
+                bytes += (double)R.crop_w * R.crop_h * R.cn * ((double)R.win_w / R.dst_w) * ((double)R.win_h / R.dst_h) +
+                         (double)R.win_w * R.win_h * R.cn * (R.final_out ? 4 : 1);
+            }
         }
     }
     static constexpr size_t kGenericLds = 64 * 1024;
@@ -1707,14 +1737,17 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
         KernelTimer t{};
         if (timed) t = take_timer(ctx, KM_RAW, g.bytes);
         if (timed) HIP_OK(hipEventRecord(t.start, stream));
-        const float* glut = g.any_final ? d_lut : nullptr;
-        const int    gbgr = o.bgr_to_rgb && o.channels == 3, gchm = o.channel_major;
-        if (g.sep)
-            HIP_OK(launch_resize_sep(g.sep, (const ResizeJob*)(table + g.off), table, (int)g.jobs.size(), g.max_tiles, g.TR,
-                                     g.CW, g.NR, g.SW, g.cn_max, glut, gbgr, gchm, ctx->d_error, stream));
-        else
-            HIP_OK(launch_resize_generic((const ResizeJob*)(table + g.off), table, (int)g.jobs.size(), g.max_tiles, g.TR,
-                                         g.CW, g.NR, g.xs, g.amax, g.cn_max, g.SW, glut, gbgr, gchm, ctx->d_error, stream));
+        const int gbgr = o.bgr_to_rgb && o.channels == 3, gchm = o.channel_major;
+        for (const GrPlan::Sub& u : g.subs) {
+            const ResizeJob* gj   = (const ResizeJob*)(table + g.off) + u.first;
+            const float*     glut = u.any_final ? d_lut : nullptr;
+            if (u.sep)
+                HIP_OK(launch_resize_sep(u.sep, gj, table, u.count, u.max_tiles, u.TR, u.CW, u.NR, u.SW, u.cn_max, glut, gbgr,
+                                         gchm, ctx->d_error, stream));
+            else
+                HIP_OK(launch_resize_generic(gj, table, u.count, u.max_tiles, u.TR, u.CW, u.NR, u.xs, u.amax, u.cn_max, u.SW,
+                                             glut, gbgr, gchm, ctx->d_error, stream));
+        }
         if (timed) {
             HIP_OK(hipEventRecord(t.stop, stream));
             ctx->timers.push_back(t);
