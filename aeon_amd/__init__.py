@@ -342,6 +342,20 @@ def out_desc(channels=3, channel_major=True, bgr_to_rgb=False, dtype="float32", 
 
 
 # ---- device stage --------------------------------------------------------------------------------
+class JpegFiles:
+    """Encoded files marshalled once for aeon_hip_decode_jpeg_batch (the pointer and size arrays; the
+    bytes objects are kept alive here)."""
+
+    def __init__(self, files):
+        self.bufs = [bytes(f) for f in files]
+        n = len(self.bufs)
+        self.ptrs = (ctypes.c_void_p * n)(*[ctypes.cast(ctypes.c_char_p(b), ctypes.c_void_p) for b in self.bufs])
+        self.sizes = (ctypes.c_size_t * n)(*[len(b) for b in self.bufs])
+
+    def __len__(self):
+        return len(self.bufs)
+
+
 class Context:
     """One per GPU (aeon_hip_ctx)."""
 
@@ -401,11 +415,10 @@ class Context:
 
     def decode_jpeg_batch(self, files, descs, dst_ptr, stream=0):
         """image::extractor::extract of JPEG files into device memory (aeon_hip_decode_jpeg_batch):
-        files = list of bytes, descs[i] = where record i goes (HWC, channels 3 = BGR / 1 = gray)."""
-        n = len(files)
-        bufs = [bytes(f) for f in files]
-        ptrs = (ctypes.c_void_p * n)(*[ctypes.cast(ctypes.c_char_p(b), ctypes.c_void_p) for b in bufs])
-        sizes = (ctypes.c_size_t * n)(*[len(b) for b in bufs])
+        files = list of bytes (or a JpegFiles, marshalled once), descs[i] = where record i goes (HWC,
+        channels 3 = BGR / 1 = gray)."""
+        jf = files if isinstance(files, JpegFiles) else JpegFiles(files)
+        n, ptrs, sizes = len(jf), jf.ptrs, jf.sizes
         d = descs if isinstance(descs, ctypes.Array) else (ImgDesc * n)(*descs)
         _check(lib().aeon_hip_decode_jpeg_batch(self._h, n, ptrs, sizes, d, ctypes.c_void_p(dst_ptr),
                                                 ctypes.c_void_p(stream or 0)))

@@ -210,8 +210,42 @@ struct Frame {
 };
 
 // The worker's growable output: block records then values per image (16-byte aligned pieces).
+// A growable byte buffer: pageable, or pinned (the decode call's per-set arenas, which the H2D copies
+// read directly).  Growing keeps the contents, as std::vector's resize does.
+struct HostBuf {
+    uint8_t* p      = nullptr;
+    size_t   n      = 0;
+    bool     pinned = false;
+    HostBuf()       = default;
+    HostBuf(const HostBuf&) = delete;
+    HostBuf& operator=(const HostBuf&) = delete;
+    HostBuf(HostBuf&& o) noexcept : p(o.p), n(o.n), pinned(o.pinned) { o.p = nullptr, o.n = 0; }
+    ~HostBuf() { release(); }
+    uint8_t* data() { return p; }
+    size_t   size() const { return n; }
+    void     release()
+    {
+        if (p) (void)(pinned ? hipHostFree(p) : (std::free(p), hipSuccess));
+        p = nullptr, n = 0;
+    }
+    void resize(size_t m)
+    {
+        if (m <= n) return;
+        uint8_t* q = nullptr;
+        if (pinned) {
+            if (hipHostMalloc((void**)&q, m, hipHostMallocDefault) != hipSuccess) q = nullptr;
+        } else {
+            q = (uint8_t*)std::malloc(m);
+        }
+        if (!q) throw jpeg_error(AEON_HIP_ERUNTIME, "JPEG arena allocation failed");
+        if (n) std::memcpy(q, p, n);
+        release();
+        p = q, n = m;
+    }
+};
+
 struct Arena {
-    std::vector<uint8_t> host; // pageable staging, copied into the set's pinned buffer
+    HostBuf              host; // staging the H2D reads (pinned in the decode call's sets)
     size_t               used = 0;
     std::vector<int16_t> coef; // progressive files: every block's 64 coefficients (zigzag order)
     std::vector<uint32_t> seg; // GPU-decoded files: segment starts while unstuffing
@@ -946,7 +980,6 @@ bool prepare_gpu(const uint8_t* d, size_t size, Frame& f, Arena& a, GpuScan& g, 
 struct JpegState {
     std::unique_ptr<thread_pool> own;
     thread_pool*                 pool = nullptr;
-    std::vector<Arena>           arenas;
     struct Set {
         hipEvent_t done    = nullptr;
         hipEvent_t copied  = nullptr; // the set's H2D (on `copy`) is done: the call's kernels may start
@@ -959,6 +992,7 @@ struct JpegState {
         size_t     planes_cap = 0;
         uint8_t*   work    = nullptr; // GPU-decoded files: block records, dense coefficients, subsequence scratch
         size_t     work_cap = 0;
+        std::vector<Arena> arenas;    // per pool worker, pinned: the H2D copies read them in place
     } sets[2];
     int         next = 0;
     hipStream_t copy = nullptr; // the H2D of a call's staging, so that it overlaps the previous call's
@@ -1006,7 +1040,10 @@ JpegState* jpeg_state_create(thread_pool* shared, bool gpu_huff)
         s->own.reset(new thread_pool(map));
         s->pool = s->own.get();
     }
-    s->arenas.resize(s->pool->size());
+    for (auto& st : s->sets) {
+        st.arenas.resize(s->pool->size());
+        for (auto& a : st.arenas) a.host.pinned = true;
+    }
     return s;
 }
 
@@ -1047,7 +1084,16 @@ void jpeg_decode_batch(JpegState* S, int n, const void* const* data, const size_
         tp[k] = std::chrono::duration<double, std::micro>(t - t0).count();
         t0 = t;
     };
-    for (auto& a : S->arenas) a.used = 0;
+    // the call's set (pinned staging, device buffers, the workers' pinned arenas): reused once the
+    // call that last used it is done with it
+    JpegState::Set& st = S->sets[S->next];
+    S->next ^= 1;
+    if (!st.done) hip_ok(hipEventCreateWithFlags(&st.done, hipEventDisableTiming), "hipEventCreate");
+    if (st.pending) hip_ok(hipEventSynchronize(st.done), "hipEventSynchronize");
+    st.pending = false;
+    mark(0);
+    std::vector<Arena>& arenas = st.arenas;
+    for (auto& a : arenas) a.used = 0;
     std::vector<Frame>   frames(n);
     std::vector<int>     owner(n);
     std::vector<size_t>  blk(3 * (size_t)n), val(n);
@@ -1059,11 +1105,11 @@ void jpeg_decode_batch(JpegState* S, int n, const void* const* data, const size_
             const aeon_img_desc& d = descs[i];
             if (d.channels != 1 && d.channels != 3) bad("decoded channels must be 1 or 3");
             const uint8_t* b = (const uint8_t*)data[i];
-            if (S->gpu_huff && prepare_gpu(b, sizes[i], frames[i], S->arenas[w], gs[i], S->huff_lanes)) {
+            if (S->gpu_huff && prepare_gpu(b, sizes[i], frames[i], arenas[w], gs[i], S->huff_lanes)) {
                 on_gpu[i] = 1;
             } else {
                 frames[i] = Frame();
-                decode_file(b, sizes[i], frames[i], S->arenas[w], &blk[3 * (size_t)i], &val[i], d.channels == 1);
+                decode_file(b, sizes[i], frames[i], arenas[w], &blk[3 * (size_t)i], &val[i], d.channels == 1);
             }
             owner[i] = w;
             if (frames[i].W != d.width || frames[i].H != d.height)
@@ -1074,7 +1120,7 @@ void jpeg_decode_batch(JpegState* S, int n, const void* const* data, const size_
             throw jpeg_error(e.code, std::string(e.what()) + " (record " + std::to_string(i) + ")");
         }
     });
-    mark(0);
+    mark(1);
     // device layout of the call: [images][GPU-decoded files][chunks][rows][arena 0][arena 1]...; the
     // work buffer (device only): [block records of the GPU-decoded files][their dense coefficients]
     // [their subsequence scratch]
@@ -1122,19 +1168,14 @@ void jpeg_decode_batch(JpegState* S, int n, const void* const* data, const size_
     const size_t chk_off   = huf_off + (((size_t)n_gpu * sizeof(JpegHuffFile) + 255) & ~(size_t)255);
     const size_t row_off   = chk_off + ((chunks.size() * sizeof(JpegChunk) + 255) & ~(size_t)255);
     size_t       total     = row_off + ((rows.size() * sizeof(JpegRows) + 255) & ~(size_t)255);
-    std::vector<size_t> arena_off(S->arenas.size());
-    for (size_t w = 0; w < S->arenas.size(); w++) {
+    const size_t head = total; // descriptors and lists: staged in st.pinned; the arenas go up from their own
+    std::vector<size_t> arena_off(arenas.size());
+    for (size_t w = 0; w < arenas.size(); w++) {
         arena_off[w] = total;
-        total += (S->arenas[w].used + 255) & ~(size_t)255;
+        total += (arenas[w].used + 255) & ~(size_t)255;
     }
-    mark(1);
-    JpegState::Set& st = S->sets[S->next];
-    S->next ^= 1;
-    if (!st.done) hip_ok(hipEventCreateWithFlags(&st.done, hipEventDisableTiming), "hipEventCreate");
-    if (st.pending) hip_ok(hipEventSynchronize(st.done), "hipEventSynchronize");
     mark(2);
-    st.pending = false;
-    grow_buf(st.pinned, st.pinned_cap, total, true);
+    grow_buf(st.pinned, st.pinned_cap, head, true);
     grow_buf(st.dev, st.dev_cap, total, false);
     grow_buf(st.planes, st.planes_cap, std::max<size_t>(plane_bytes, 256), false);
     const size_t coef_off = rec_bytes, sub_off = rec_bytes + coef_bytes;
@@ -1190,18 +1231,23 @@ void jpeg_decode_batch(JpegState* S, int n, const void* const* data, const size_
     if (!chunks.empty()) std::memcpy(st.pinned + chk_off, chunks.data(), chunks.size() * sizeof(JpegChunk));
     if (!rows.empty()) std::memcpy(st.pinned + row_off, rows.data(), rows.size() * sizeof(JpegRows));
     mark(3);
-    S->pool->run((int)S->arenas.size(), [&](int w) {
-        if (S->arenas[w].used) std::memcpy(st.pinned + arena_off[w], S->arenas[w].host.data(), S->arenas[w].used);
-    });
+    // (round 4 copied the arenas into st.pinned on the pool first: ~0.5 ms per 512 files)
+    auto h2d = [&](hipStream_t on) {
+        hip_ok(hipMemcpyAsync(st.dev, st.pinned, head, hipMemcpyHostToDevice, on), "hipMemcpyAsync");
+        for (size_t w = 0; w < arenas.size(); w++)
+            if (arenas[w].used)
+                hip_ok(hipMemcpyAsync(st.dev + arena_off[w], arenas[w].host.data(), arenas[w].used, hipMemcpyHostToDevice, on),
+                       "hipMemcpyAsync");
+    };
     mark(4);
     if (S->use_copy) { // (the set's previous kernels are done: st.done above)
         if (!S->copy) hip_ok(hipStreamCreateWithFlags(&S->copy, hipStreamNonBlocking), "hipStreamCreate");
         if (!st.copied) hip_ok(hipEventCreateWithFlags(&st.copied, hipEventDisableTiming), "hipEventCreate");
-        hip_ok(hipMemcpyAsync(st.dev, st.pinned, total, hipMemcpyHostToDevice, S->copy), "hipMemcpyAsync");
+        h2d(S->copy);
         hip_ok(hipEventRecord(st.copied, S->copy), "hipEventRecord");
         hip_ok(hipStreamWaitEvent(stream, st.copied, 0), "hipStreamWaitEvent");
     } else {
-        hip_ok(hipMemcpyAsync(st.dev, st.pinned, total, hipMemcpyHostToDevice, stream), "hipMemcpyAsync");
+        h2d(stream);
     }
     if (n_gpu) hip_ok(hipMemsetAsync(st.work, 0, rec_bytes, stream), "hipMemsetAsync");
     if (start) hip_ok(hipEventRecord(start, stream), "hipEventRecord");
@@ -1216,7 +1262,7 @@ void jpeg_decode_batch(JpegState* S, int n, const void* const* data, const size_
     st.pending = true;
     mark(5);
     if (prof)
-        std::fprintf(stderr, "[jpeg stage] n=%d bytes=%zu us: pool %.0f layout %.0f set_wait %.0f fill %.0f arena_copy %.0f enqueue %.0f\n",
+        std::fprintf(stderr, "[jpeg stage] n=%d bytes=%zu us: set_wait %.0f pool %.0f layout %.0f fill %.0f h2d_setup %.0f enqueue %.0f\n",
                      n, total, tp[0], tp[1], tp[2], tp[3], tp[4], tp[5]);
 }
 

@@ -625,7 +625,7 @@ def run_e2e_jpeg(A, C, torch, batch=512, windows=12, on_device=False):
     return batch * windows / dt
 
 
-def run_jpeg_stage(A, torch, batch=512, reps=10):
+def run_jpeg_stage(A, torch, batch=512, reps=20):
     """aeon_hip_decode_jpeg_batch alone (extract of a window of JPEG files into device memory): a
     512-record window (aeon's decode_size = 2 x batch 256), so the GPU Huffman decoder holds two files per
     CU."""
@@ -639,18 +639,20 @@ def run_jpeg_stage(A, torch, batch=512, reps=10):
     descs = (A.ImgDesc * batch)(*descs)
     dst = torch.empty(off, dtype=torch.uint8, device="cuda")
     stream = torch.cuda.Stream().cuda_stream  # (a stream of our own: see run_device)
-    ctx.decode_jpeg_batch(files, descs, dst.data_ptr(), stream)
+    jf = A.JpegFiles(files)  # (marshalled once: aeon's host hands over plain pointers)
+    for _ in range(2):  # warmup: both staging sets allocated (their first use grows pinned buffers)
+        ctx.decode_jpeg_batch(jf, descs, dst.data_ptr(), stream)
     ctx.synchronize(stream)
     t0 = time.perf_counter()
     for _ in range(reps):
-        ctx.decode_jpeg_batch(files, descs, dst.data_ptr(), stream)
+        ctx.decode_jpeg_batch(jf, descs, dst.data_ptr(), stream)
     ctx.synchronize(stream)
     dt = time.perf_counter() - t0
     # the GPU part alone: HIP events around the IDCT + colour launches of every call
     ctx.kernel_times()
     ctx.set_timing(1)
     for _ in range(reps):
-        ctx.decode_jpeg_batch(files, descs, dst.data_ptr(), stream)
+        ctx.decode_jpeg_batch(jf, descs, dst.data_ptr(), stream)
     ctx.synchronize(stream)
     k_ms, k_px, k_n = ctx.kernel_times()["jpeg"]
     ctx.set_timing(False)
