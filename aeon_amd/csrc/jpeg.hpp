@@ -14,6 +14,7 @@
 // runs on the GPU, which writes the decoded HWC records straight into the device source arena the
 // augmentation kernels read.
 #pragma once
+#include <stddef.h>
 #include <stdint.h>
 
 #include <stdexcept>
@@ -56,7 +57,10 @@ struct alignas(16) JpegImage {
     int32_t  hf[3], vf[3]; // hmax / hs, vmax / vs
     int32_t  pad2_;
     uint16_t q[3][64];  // quantisation table of each component, natural order
+    uint16_t pad3_[4];
+    uint16_t qz[3][64]; // the same in zigzag order (the dense path of jpeg_idct: 16-byte loads)
 };
+static_assert(offsetof(JpegImage, qz) % 16 == 0, "JpegImage.qz: 16-byte rows");
 
 // jdsample.c's upsampler of a component, chosen per file on the host.
 enum JpegUpsample : int32_t {
@@ -137,7 +141,7 @@ constexpr int kJpegCorruptBit = 256;
 constexpr int kJpegIdctLanes  = 256;                             // IDCT workgroup: 8 lanes per block
 constexpr int kJpegIdctUnroll = 4;                               // blocks per lane group
 constexpr int kJpegIdctBlocks = kJpegIdctLanes / 8 * kJpegIdctUnroll; // blocks per IDCT workgroup (chunk)
-constexpr int kJpegRowsPerWg = 8;   // output rows per colour workgroup (fewer when the staged rows outgrow LDS)
+constexpr int kJpegRowsPerWg = 32;  // output rows per colour workgroup (fewer when the staged rows outgrow LDS)
 constexpr int kJpegColorLds  = 160 * 1024; // most LDS a colour workgroup stages
 
 // jdsample.c's choice for a component (h / v expansion factors, dw samples per row): fancy

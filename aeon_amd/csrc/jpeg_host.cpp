@@ -1149,13 +1149,14 @@ void jpeg_decode_batch(JpegState* S, int n, const void* const* data, const size_
             const int nb = f.c[k].bw * f.c[k].bh;
             for (int b = 0; b < nb; b += kJpegIdctBlocks) chunks.push_back({i, k, b, std::min(kJpegIdctBlocks, nb - b)});
         }
-        // colour bands: as many rows as the staged plane rows of the band fit the LDS
+        // colour bands: as many rows as the staged plane rows of the band fit the LDS (16 bytes more per
+        // staged row: the 4:2:0 path's edge columns, jpeg_kernels.hip color_h2v2)
         int band = kJpegRowsPerWg, lds = 0;
         for (;; band /= 2) {
             lds = 0;
             for (int k = 0; k < nc; k++) {
                 const int hf = f.hmax / f.c[k].h, vf = f.vmax / f.c[k].v;
-                lds += jpeg_stage_rows(jpeg_upsample_mode(hf, vf, f.c[k].dw), vf, band) * f.c[k].bw * 8;
+                lds += jpeg_stage_rows(jpeg_upsample_mode(hf, vf, f.c[k].dw), vf, band) * (f.c[k].bw * 8 + 16);
             }
             if (lds <= kJpegColorLds || band == 1) break;
         }
@@ -1203,6 +1204,7 @@ void jpeg_decode_batch(JpegState* S, int n, const void* const* data, const size_
             J.hf[k] = f.hmax / f.c[k].h, J.vf[k] = f.vmax / f.c[k].v;
             J.up[k] = jpeg_upsample_mode(J.hf[k], J.vf[k], f.c[k].dw);
             std::memcpy(J.q[k], f.q[f.c[k].tq], sizeof(J.q[k]));
+            for (int z = 0; z < 64; z++) J.qz[k][z] = f.q[f.c[k].tq][kZigzagToNatural[z]];
         }
         J.values     = on_gpu[i] ? 0 : base + val[i];
         J.out        = (uint64_t)dst_base + descs[i].offset;

@@ -37,10 +37,12 @@ __constant__ uint8_t kZz[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 
                                 35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51,
                                 58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
 
+// range_limit[x & 1023] of jdmaster.c (prepare_range_limit_table, with the +CENTERJSAMPLE folded in):
+// the low 10 bits as a signed value s, then clamp(s + 128, 0, 255) -- v_bfe_i32 + v_med3_i32
 __device__ __forceinline__ uint32_t idct_limit(int x)
 {
-    const int i = x & 1023;
-    return i < 128 ? (uint32_t)(i + 128) : (i < 512 ? 255u : (i < 896 ? 0u : (uint32_t)(i - 896)));
+    const int s = __builtin_amdgcn_sbfe(x, 0, 10);
+    return (uint32_t)min(max(s + 128, 0), 255);
 }
 
 // One 1-D LL&M pass on 8 values (in[0..7] at stride 1), results descaled by `shift`.
@@ -76,19 +78,24 @@ __constant__ uint8_t kZzInv[64] = {0,  1,  5,  6,  14, 15, 27, 28, 2,  4,  7,  1
 
 // Eight lanes per block, the eight adjacent lanes of a wave, kJpegIdctUnroll blocks per lane group
 // (group g takes blocks g, g + G, ... so concurrent lanes still write neighbouring blocks): first
-// every block's descriptor, then every column gather -- lane j takes column j straight from the
-// sparse stream (coefficient at natural n = r*8 + j present iff its zigzag bit is set; its value
-// index = the set bits below it): no zero fill, no scatter, all loads in flight together -- then
-// per block pass 1 in registers, a transpose through the wave's own LDS region (no workgroup
-// barrier) and pass 2 on row j.  Slot stride 66 dwords: lane (g, j) of pass 1 writes bank
-// (2g + 8r + j) % 64 -- conflict-free per wave.
+// every block's descriptor, then every column gather, all loads in flight together.  A host-decoded
+// file (sparse stream): lane j takes column j straight from the stream (coefficient at natural
+// n = r*8 + j present iff its zigzag bit is set; its value index = the set bits below it).  A
+// GPU-decoded file (dense zigzag slots): lane j takes zigzag slots 8j .. 8j + 7 of the block as one
+// 16-byte load, dequantises them with the zigzag-ordered table (JpegImage.qz, one 16-byte load),
+// zeroes those whose mask bit is clear (the slots are not cleared between calls) and scatters them
+// to their natural positions in the block's LDS slot, from which it reads column j.  Then per block
+// pass 1 in registers, a transpose through the same slot (no workgroup barrier) and pass 2 on row j.
+// Slot stride 66 dwords: lane (g, j) reads / writes column j of row r at bank (8g + 2u + 8r + j) % 64
+// -- conflict-free per wave.
 constexpr int kSlot = 66;
 
 __global__ __launch_bounds__(kJpegIdctLanes) void jpeg_idct(const JpegImage* __restrict__ imgs,
                                                             const JpegChunk* __restrict__ chunks)
 {
     constexpr int G = kJpegIdctLanes / 8; // lane groups per workgroup
-    __shared__ int slot[G * kSlot];
+    constexpr int U = kJpegIdctUnroll;
+    __shared__ int slot[G * U * kSlot];
     const JpegChunk  C  = chunks[blockIdx.x];
     const JpegImage& I  = imgs[C.img];
     const int        k  = C.comp;
@@ -96,28 +103,45 @@ __global__ __launch_bounds__(kJpegIdctLanes) void jpeg_idct(const JpegImage* __r
     const gp<const JpegBlock> blocks = gaddr<const JpegBlock>(I.blocks[k]) + C.first;
     const gp<const int16_t>   vals   = gaddr<const int16_t>(I.values);
     const gp<const int16_t>   dense  = gaddr<const int16_t>(I.dvals[k]);
-    JpegBlock        B[kJpegIdctUnroll];
+    JpegBlock        B[U];
 #pragma unroll
-    for (int u = 0; u < kJpegIdctUnroll; u++) B[u] = blocks[min(g + u * G, C.count - 1)];
-    int qv[8];
-#pragma unroll
-    for (int r = 0; r < 8; r++) qv[r] = I.q[k][r * 8 + j];
-    // pass 1 inputs: column j of every block, dequantised (jidctint.c DEQUANTIZE = coef * quantval);
-    // a GPU-decoded file's coefficients sit at their zigzag slot of the block's 64
-    int col[kJpegIdctUnroll][8];
+    for (int u = 0; u < U; u++) B[u] = blocks[min(g + u * G, C.count - 1)];
+    int* const s0 = slot + g * U * kSlot; // the group's U block slots
+    // pass 1 inputs: column j of every block, dequantised (jidctint.c DEQUANTIZE = coef * quantval)
+    int col[U][8];
     if (dense) {
+        uint4 c4[U];
 #pragma unroll
-        for (int u = 0; u < kJpegIdctUnroll; u++) {
-            const gp<const int16_t> bv = dense + (size_t)(C.first + min(g + u * G, C.count - 1)) * 64;
+        for (int u = 0; u < U; u++)
+            c4[u] = *(gp<const uint4>)(dense + (size_t)(C.first + min(g + u * G, C.count - 1)) * 64 + 8 * j);
+        const uint4 q4 = *(gp<const uint4>)gaddr<const uint16_t>((uint64_t)&I.qz[k][8 * j]);
+        int nat[8];
 #pragma unroll
-            for (int r = 0; r < 8; r++) { // unconditional loads, the mask zeroes the stale slots
-                const int z = kZzInv[r * 8 + j];
-                col[u][r]   = ((int)bv[z] * qv[r]) & -(int)((B[u].mask >> z) & 1);
+        for (int e = 0; e < 8; e++) nat[e] = kZz[8 * j + e];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const uint32_t m8 = (uint32_t)(B[u].mask >> (8 * j)) & 0xffu;
+            const uint32_t cw[4] = {c4[u].x, c4[u].y, c4[u].z, c4[u].w}, qw[4] = {q4.x, q4.y, q4.z, q4.w};
+#pragma unroll
+            for (int e = 0; e < 8; e++) {
+                const int c = (int)(int16_t)(cw[e >> 1] >> (16 * (e & 1)));
+                const int q = (int)((qw[e >> 1] >> (16 * (e & 1))) & 0xffff);
+                s0[u * kSlot + nat[e]] = ((m8 >> e) & 1) ? c * q : 0;
             }
         }
-    } else {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
-        for (int u = 0; u < kJpegIdctUnroll; u++)
+        for (int u = 0; u < U; u++)
+#pragma unroll
+            for (int r = 0; r < 8; r++) col[u][r] = s0[u * kSlot + r * 8 + j];
+    } else {
+        int qv[8];
+#pragma unroll
+        for (int r = 0; r < 8; r++) qv[r] = I.q[k][r * 8 + j];
+#pragma unroll
+        for (int u = 0; u < U; u++)
 #pragma unroll
             for (int r = 0; r < 8; r++) {
                 const int z = kZzInv[r * 8 + j];
@@ -126,11 +150,11 @@ __global__ __launch_bounds__(kJpegIdctLanes) void jpeg_idct(const JpegImage* __r
                     col[u][r] = (int)vals[B[u].val_off + __builtin_popcountll(B[u].mask & ((1ull << z) - 1))] * qv[r];
             }
     }
-    int* s = slot + g * kSlot;
     const int bw = I.bw[k];
 #pragma unroll
-    for (int u = 0; u < kJpegIdctUnroll; u++) {
+    for (int u = 0; u < U; u++) {
         const int bi = g + u * G;
+        int* const s = s0 + u * kSlot;
         int       out[8], in[8];
         // pass 1: columns, descaled by CONST_BITS - PASS1_BITS
         llm8<11, false>(col[u], out);
@@ -249,24 +273,186 @@ __device__ __forceinline__ void color_rows(const JpegImage& I, const CompView* c
     }
 }
 
+// ---- 4:2:0 BGR fast path (luma full, both chroma h2v2_fancy_upsample) --------------------------
+// A lane owns 8 output columns x0 = 8q.. of an output row pair (2r, 2r + 1), which share chroma row
+// r: per chroma it takes columns i0 - 1 .. i0 + 4 (i0 = 4q) of rows r - 1, r, r + 1 as three aligned
+// dwords of the LDS-staged rows (each row staged with its edge columns replicated to columns -1 and
+// dw, which turns jdsample.c's edge cases (i == 0, i == dw - 1) into the general formula), forms
+// the column sums 3 * row r + neighbour row as packed 16-bit pairs, and the output pairs
+// (3 * colsum(i) + colsum(i -+ 1) + 8 / 7) >> 4 of h2v2_fancy_upsample the same way.  Luma comes
+// straight from the plane (8-byte loads).  Bit-exact with the general path: same integer formulas.
+typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
+constexpr int kH2v2Pad = 8; // staged chroma row: [8 bytes: col -1 at 7][pw bytes][8 bytes: col dw]
+
+__device__ __forceinline__ u16x2 as_u16x2(uint32_t v) { return __builtin_bit_cast(u16x2, v); }
+
+// One staged chroma row's bytes i0 - 1 .. i0 + 4 as 16-bit pairs: P0 (i0-1, i0), P1 (i0+1, i0+2),
+// P2 (i0+3, i0+4), Q0 (i0, i0+1), Q1 (i0+2, i0+3); `row` is 4-byte aligned at column i0 - 4.
+struct ChromaCols {
+    u16x2 p0, p1, p2, q0, q1;
+};
+__device__ __forceinline__ ChromaCols chroma_cols(const uint8_t* row)
+{
+    const uint32_t* w  = (const uint32_t*)row;
+    const uint32_t  d0 = w[0], d1 = w[1], d2 = w[2];
+    ChromaCols      c;
+    c.p0 = as_u16x2(__builtin_amdgcn_perm(d1, d0, 0x0c040c03u));
+    c.p1 = as_u16x2(__builtin_amdgcn_perm(d1, d1, 0x0c020c01u));
+    c.p2 = as_u16x2(__builtin_amdgcn_perm(d2, d1, 0x0c040c03u));
+    c.q0 = as_u16x2(__builtin_amdgcn_perm(d1, d1, 0x0c010c00u));
+    c.q1 = as_u16x2(__builtin_amdgcn_perm(d1, d1, 0x0c030c02u));
+    return c;
+}
+
+// h2v2_fancy_upsample of 8 output columns of one output row: e01 = (x0, x0 + 2), o01 = (x0 + 1,
+// x0 + 3), e23 = (x0 + 4, x0 + 6), o23 = (x0 + 5, x0 + 7); `t3` = 3 * row r, `nb` the neighbour row.
+struct ChromaOut {
+    u16x2 e01, o01, e23, o23;
+};
+__device__ __forceinline__ ChromaOut chroma_row(const ChromaCols& t3, const ChromaCols& nb)
+{
+    const u16x2 three = {3, 3}, r8 = {8, 8}, r7 = {7, 7}, four = {4, 4};
+    const u16x2 sp0 = t3.p0 + nb.p0, sp1 = t3.p1 + nb.p1, sp2 = t3.p2 + nb.p2;
+    const u16x2 sq0 = t3.q0 + nb.q0, sq1 = t3.q1 + nb.q1;
+    ChromaOut o;
+    o.e01 = (sq0 * three + sp0 + r8) >> four;
+    o.o01 = (sq0 * three + sp1 + r7) >> four;
+    o.e23 = (sq1 * three + sp1 + r8) >> four;
+    o.o23 = (sq1 * three + sp2 + r7) >> four;
+    return o;
+}
+
+// jdcolor.c ycc_rgb_convert of one pixel, packed B | G << 8 | R << 16
+__device__ __forceinline__ uint32_t ycc_bgr(int Y, int cb, int cr)
+{
+    cb -= 128, cr -= 128;
+    const int r  = Y + ((91881 * cr + 32768) >> 16);
+    const int g  = Y + ((-22554 * cb + 32768 + -46802 * cr) >> 16);
+    const int bl = Y + ((116130 * cb + 32768) >> 16);
+    return (uint32_t)min(max(bl, 0), 255) | (uint32_t)min(max(g, 0), 255) << 8 | (uint32_t)min(max(r, 0), 255) << 16;
+}
+
+// 8 BGR pixels of one output row to `o`: three 8-byte stores (aligned), six dwords, or bytes
+__device__ __forceinline__ void store_bgr8(gp<uint8_t> o, const uint32_t (&p)[8], int n)
+{
+    uint32_t d[6];
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+        d[3 * h + 0] = p[4 * h] | p[4 * h + 1] << 24;
+        d[3 * h + 1] = p[4 * h + 1] >> 8 | p[4 * h + 2] << 16;
+        d[3 * h + 2] = p[4 * h + 2] >> 16 | p[4 * h + 3] << 8;
+    }
+    const uintptr_t a = (uintptr_t)o;
+    if (n == 8 && (a & 7) == 0) {
+        const gp<uint2> d2 = (gp<uint2>)o;
+        d2[0] = make_uint2(d[0], d[1]), d2[1] = make_uint2(d[2], d[3]), d2[2] = make_uint2(d[4], d[5]);
+    } else if (n == 8 && (a & 3) == 0) {
+        const gp<uint32_t> d4 = (gp<uint32_t>)o;
+#pragma unroll
+        for (int e = 0; e < 6; e++) d4[e] = d[e];
+    } else {
+        for (int e = 0; e < 3 * n; e++) o[e] = (uint8_t)(d[e >> 2] >> (8 * (e & 3)));
+    }
+}
+
+__device__ __forceinline__ void color_h2v2(const JpegImage& I, const JpegRows& R, uint8_t* lds)
+{
+    const int y0 = R.y0, y1 = R.y0 + R.rows - 1;
+    // stage chroma rows [lo, hi] of both components, then replicate their edge columns
+    int lo[2], n[2], lp[2], off[2];
+    int o = 0;
+#pragma unroll
+    for (int c = 0; c < 2; c++) {
+        const int k = c + 1;
+        lo[c] = max((y0 >> 1) - 1, 0);
+        n[c]  = min((y1 >> 1) + 1, I.dh[k] - 1) - lo[c] + 1;
+        lp[c] = I.bw[k] * 8 + 2 * kH2v2Pad, off[c] = o;
+        const gp<const uint2> src = (gp<const uint2>)(gaddr<const uint8_t>(I.planes[k]) + (size_t)lo[c] * (I.bw[k] * 8));
+        const int per = I.bw[k]; // 8-byte words per row
+        for (int e = threadIdx.x; e < n[c] * per; e += blockDim.x) {
+            const int rr = e / per, w = e - rr * per;
+            *(uint2*)(lds + o + rr * lp[c] + kH2v2Pad + w * 8) = src[e];
+        }
+        o += n[c] * lp[c];
+    }
+    __syncthreads();
+    if (threadIdx.x < n[0] + n[1]) {
+        const bool c1 = threadIdx.x >= n[0]; // (selects, not an index: the arrays stay in registers)
+        const int  rr = threadIdx.x - (c1 ? n[0] : 0);
+        uint8_t*   row = lds + (c1 ? off[1] + rr * lp[1] : rr * lp[0]) + kH2v2Pad;
+        const int  dw  = c1 ? I.dw[2] : I.dw[1];
+        row[-1] = row[0], row[dw] = row[dw - 1];
+    }
+    __syncthreads();
+
+    const int W = I.W, H = I.H, groups = (W + 7) >> 3, pairs = (R.rows + 1) >> 1;
+    const int pw0 = I.bw[0] * 8, dh1 = I.dh[1], dh2 = I.dh[2];
+    const gp<const uint8_t> Yp  = gaddr<const uint8_t>(I.planes[0]);
+    const gp<uint8_t>       out = gaddr<uint8_t>(I.out);
+    const float rcp = 1.0f / (float)groups;
+    for (int it = threadIdx.x; it < groups * pairs; it += blockDim.x) {
+        const int pr = (int)(((float)it + 0.5f) * rcp), q = it - pr * groups;
+        const int y = y0 + 2 * pr, x0 = q * 8, i0 = q * 4, r = y >> 1;
+        const int yb = min(y + 1, H - 1);
+        const uint2 ya = *(gp<const uint2>)(Yp + (size_t)y * pw0 + x0);
+        const uint2 yv = *(gp<const uint2>)(Yp + (size_t)yb * pw0 + x0);
+        ChromaOut ce[2], co[2]; // [chroma]: output row y (even), y + 1 (odd)
+#pragma unroll
+        for (int c = 0; c < 2; c++) {
+            const int      dh   = c ? dh2 : dh1;
+            const uint8_t* base = lds + off[c] + kH2v2Pad - 4 + i0;
+            const ChromaCols m  = chroma_cols(base + (max(r - 1, 0) - lo[c]) * lp[c]);
+            const ChromaCols t  = chroma_cols(base + (r - lo[c]) * lp[c]);
+            const ChromaCols p  = chroma_cols(base + (min(r + 1, dh - 1) - lo[c]) * lp[c]);
+            const u16x2      three = {3, 3};
+            const ChromaCols t3 = {t.p0 * three, t.p1 * three, t.p2 * three, t.q0 * three, t.q1 * three};
+            ce[c] = chroma_row(t3, m);
+            co[c] = chroma_row(t3, p);
+        }
+        const int nx = min(8, W - x0);
+#pragma unroll
+        for (int v = 0; v < 2; v++) {
+            if (v == 1 && y + 1 >= H) continue;
+            const uint2 yy = v ? yv : ya;
+            const ChromaOut& cb = v ? co[0] : ce[0];
+            const ChromaOut& cr = v ? co[1] : ce[1];
+            const u16x2 bq[4] = {cb.e01, cb.o01, cb.e23, cb.o23}, rq[4] = {cr.e01, cr.o01, cr.e23, cr.o23};
+            uint32_t px[8];
+#pragma unroll
+            for (int e = 0; e < 8; e++) {
+                // pixel e: even e -> e01/e23, odd -> o01/o23; pair half = (e >> 1) & 1
+                const int      s  = (e >> 2) * 2 + (e & 1), h = (e >> 1) & 1;
+                const uint32_t yw = e < 4 ? yy.x : yy.y;
+                px[e] = ycc_bgr((int)((yw >> (8 * (e & 3))) & 0xff), (int)bq[s][h], (int)rq[s][h]);
+            }
+            store_bgr8(out + (size_t)(y + v) * I.out_stride + (size_t)x0 * 3, px, nx);
+        }
+    }
+}
+
 // A workgroup per band of output rows: the plane rows the band's upsampling reads are copied into
 // LDS with coalesced 8-byte loads (jpeg_stage_rows bounds them), then color_rows.
 __global__ __launch_bounds__(256) void jpeg_color(const JpegImage* __restrict__ imgs, const JpegRows* __restrict__ rows)
 {
-    extern __shared__ uint8_t lds_b[];
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds_b[];
     const JpegRows   R  = rows[blockIdx.x];
     const JpegImage& I  = imgs[R.img];
+    if (I.ncomp == 3 && I.out_cn == 3 && I.up[0] == UP_FULL && I.up[1] == UP_H2V2 && I.up[2] == UP_H2V2 &&
+        (R.y0 & 1) == 0) {
+        color_h2v2(I, R, lds_b);
+        return;
+    }
     const int        nc = I.out_cn == 1 ? 1 : I.ncomp;
     const int        y1 = R.y0 + R.rows - 1;
     CompView         cv[3];
     int              off = 0;
 #pragma unroll
     for (int k = 0; k < 3; k++) {
-        if (k >= nc) break;
         CompView& c = cv[k];
         int       hi;
         comp_rows(I, k, R.y0, y1, c, hi);
         c.P = lds_b + off;
+        if (k >= nc) continue;
         // stage plane rows [lo, hi]: whole rows of pw bytes (a multiple of 8) are contiguous
         const gp<const uint2> src = (gp<const uint2>)(gaddr<const uint8_t>(I.planes[k]) + (size_t)c.lo * c.pw);
         uint2*       dst = (uint2*)(lds_b + off);
