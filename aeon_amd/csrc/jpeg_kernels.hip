@@ -84,10 +84,10 @@ __constant__ uint8_t kZzInv[64] = {0,  1,  5,  6,  14, 15, 27, 28, 2,  4,  7,  1
 // GPU-decoded file (dense zigzag slots): lane j takes zigzag slots 8j .. 8j + 7 of the block as one
 // 16-byte load, dequantises them with the zigzag-ordered table (JpegImage.qz, one 16-byte load),
 // zeroes those whose mask bit is clear (the slots are not cleared between calls) and scatters them
-// to their natural positions in the block's LDS slot, from which it reads column j.  Then per block
-// pass 1 in registers, a transpose through the same slot (no workgroup barrier) and pass 2 on row j.
-// Slot stride 66 dwords: lane (g, j) reads / writes column j of row r at bank (8g + 2u + 8r + j) % 64
-// -- conflict-free per wave.
+// to their natural positions in the group's LDS slot, from which it reads column j (block by
+// block).  Then per block pass 1 in registers, a transpose through the same slot (wave barriers
+// only) and pass 2 on row j.  Slot stride 66 dwords: lane (g, j) reads / writes column j of row r at
+// bank (2g + 8r + j) % 64 -- conflict-free per wave.
 constexpr int kSlot = 66;
 
 __global__ __launch_bounds__(kJpegIdctLanes) void jpeg_idct(const JpegImage* __restrict__ imgs,
@@ -95,7 +95,7 @@ __global__ __launch_bounds__(kJpegIdctLanes) void jpeg_idct(const JpegImage* __r
 {
     constexpr int G = kJpegIdctLanes / 8; // lane groups per workgroup
     constexpr int U = kJpegIdctUnroll;
-    __shared__ int slot[G * U * kSlot];
+    __shared__ int slot[G * kSlot];
     const JpegChunk  C  = chunks[blockIdx.x];
     const JpegImage& I  = imgs[C.img];
     const int        k  = C.comp;
@@ -106,7 +106,7 @@ __global__ __launch_bounds__(kJpegIdctLanes) void jpeg_idct(const JpegImage* __r
     JpegBlock        B[U];
 #pragma unroll
     for (int u = 0; u < U; u++) B[u] = blocks[min(g + u * G, C.count - 1)];
-    int* const s0 = slot + g * U * kSlot; // the group's U block slots
+    int* const s0 = slot + g * kSlot; // the group's block slot
     // pass 1 inputs: column j of every block, dequantised (jidctint.c DEQUANTIZE = coef * quantval)
     int col[U][8];
     if (dense) {
@@ -122,20 +122,23 @@ __global__ __launch_bounds__(kJpegIdctLanes) void jpeg_idct(const JpegImage* __r
         for (int u = 0; u < U; u++) {
             const uint32_t m8 = (uint32_t)(B[u].mask >> (8 * j)) & 0xffu;
             const uint32_t cw[4] = {c4[u].x, c4[u].y, c4[u].z, c4[u].w}, qw[4] = {q4.x, q4.y, q4.z, q4.w};
+            if (u) { // the previous block's column reads are done
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            }
 #pragma unroll
             for (int e = 0; e < 8; e++) {
                 const int c = (int)(int16_t)(cw[e >> 1] >> (16 * (e & 1)));
                 const int q = (int)((qw[e >> 1] >> (16 * (e & 1))) & 0xffff);
-                s0[u * kSlot + nat[e]] = ((m8 >> e) & 1) ? c * q : 0;
+                s0[nat[e]] = ((m8 >> e) & 1) ? c * q : 0;
             }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+            for (int r = 0; r < 8; r++) col[u][r] = s0[r * 8 + j];
         }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-        for (int u = 0; u < U; u++)
-#pragma unroll
-            for (int r = 0; r < 8; r++) col[u][r] = s0[u * kSlot + r * 8 + j];
     } else {
         int qv[8];
 #pragma unroll
@@ -150,11 +153,12 @@ __global__ __launch_bounds__(kJpegIdctLanes) void jpeg_idct(const JpegImage* __r
                     col[u][r] = (int)vals[B[u].val_off + __builtin_popcountll(B[u].mask & ((1ull << z) - 1))] * qv[r];
             }
     }
-    const int bw = I.bw[k];
+    int* const  s   = s0;
+    const int   bw  = I.bw[k];
+    const float rbw = 1.0f / (float)bw;
 #pragma unroll
     for (int u = 0; u < U; u++) {
         const int bi = g + u * G;
-        int* const s = s0 + u * kSlot;
         int       out[8], in[8];
         // pass 1: columns, descaled by CONST_BITS - PASS1_BITS
         llm8<11, false>(col[u], out);
@@ -172,7 +176,9 @@ __global__ __launch_bounds__(kJpegIdctLanes) void jpeg_idct(const JpegImage* __r
         llm8<18, true>(in, out);
         if (bi < C.count) {
             const int b  = C.first + bi;
-            const int bx = b % bw, by = b / bw;
+            // b / bw through a float reciprocal: exact while bw < 512 ((b + 0.5) / bw stays 0.5 / bw from
+            // an integer, far above the float error at these sizes)
+            const int by = bw < 512 ? (int)(((float)b + 0.5f) * rbw) : b / bw, bx = b - by * bw;
             const gp<uint8_t> o = gaddr<uint8_t>(I.planes[k]) + (size_t)(by * 8 + j) * (bw * 8) + bx * 8;
             const uint32_t lo = idct_limit(out[0]) | idct_limit(out[1]) << 8 | idct_limit(out[2]) << 16 |
                                 idct_limit(out[3]) << 24;
@@ -389,13 +395,22 @@ __device__ __forceinline__ void color_h2v2(const JpegImage& I, const JpegRows& R
     const int pw0 = I.bw[0] * 8, dh1 = I.dh[1], dh2 = I.dh[2];
     const gp<const uint8_t> Yp  = gaddr<const uint8_t>(I.planes[0]);
     const gp<uint8_t>       out = gaddr<uint8_t>(I.out);
-    const float rcp = 1.0f / (float)groups;
-    for (int it = threadIdx.x; it < groups * pairs; it += blockDim.x) {
+    const float rcp   = 1.0f / (float)groups;
+    const int   total = groups * pairs;
+    // the luma of the lane's next item is loaded before this one is computed
+    auto luma = [&](int it, uint2& a, uint2& b) {
+        const int pr = (int)(((float)it + 0.5f) * rcp), q = it - pr * groups;
+        const int y = y0 + 2 * pr, x0 = q * 8;
+        a = *(gp<const uint2>)(Yp + (size_t)y * pw0 + x0);
+        b = *(gp<const uint2>)(Yp + (size_t)min(y + 1, H - 1) * pw0 + x0);
+    };
+    uint2 na = make_uint2(0, 0), nb = make_uint2(0, 0);
+    if (threadIdx.x < total) luma(threadIdx.x, na, nb);
+    for (int it = threadIdx.x; it < total; it += blockDim.x) {
+        const uint2 ya = na, yv = nb;
+        if (it + (int)blockDim.x < total) luma(it + blockDim.x, na, nb);
         const int pr = (int)(((float)it + 0.5f) * rcp), q = it - pr * groups;
         const int y = y0 + 2 * pr, x0 = q * 8, i0 = q * 4, r = y >> 1;
-        const int yb = min(y + 1, H - 1);
-        const uint2 ya = *(gp<const uint2>)(Yp + (size_t)y * pw0 + x0);
-        const uint2 yv = *(gp<const uint2>)(Yp + (size_t)yb * pw0 + x0);
         ChromaOut ce[2], co[2]; // [chroma]: output row y (even), y + 1 (odd)
 #pragma unroll
         for (int c = 0; c < 2; c++) {
