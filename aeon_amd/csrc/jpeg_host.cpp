@@ -1126,6 +1126,11 @@ void jpeg_decode_batch(JpegState* S, int n, const void* const* data, const size_
     // [their subsequence scratch]
     std::vector<JpegChunk> chunks;
     std::vector<JpegRows>  rows;
+    // colour band height: kJpegRowsPerWg, or AEON_HIP_JPEG_BAND (tests: 1, 2, ... rows per workgroup
+    // take the colour kernels' band-edge cases)
+    int band_max = kJpegRowsPerWg;
+    if (const char* e = std::getenv("AEON_HIP_JPEG_BAND"))
+        if (std::atoi(e) >= 1) band_max = std::min(std::atoi(e), 64);
     size_t                 plane_bytes = 0;
     std::vector<size_t>    plane_off(3 * (size_t)n, 0);
     int                    color_lds = 0, n_gpu = 0;
@@ -1151,7 +1156,7 @@ void jpeg_decode_batch(JpegState* S, int n, const void* const* data, const size_
         }
         // colour bands: as many rows as the staged plane rows of the band fit the LDS (16 bytes more per
         // staged row: the 4:2:0 path's edge columns, jpeg_kernels.hip color_h2v2)
-        int band = kJpegRowsPerWg, lds = 0;
+        int band = band_max, lds = 0;
         for (;; band /= 2) {
             lds = 0;
             for (int k = 0; k < nc; k++) {

@@ -427,7 +427,7 @@ __device__ __forceinline__ void color_h2v2(const JpegImage& I, const JpegRows& R
         const int nx = min(8, W - x0);
 #pragma unroll
         for (int v = 0; v < 2; v++) {
-            if (v == 1 && y + 1 >= H) continue;
+            if (v == 1 && y + 1 > y1) continue; // (the band's last row, or the image's)
             const uint2 yy = v ? yv : ya;
             const ChromaOut& cb = v ? co[0] : ce[0];
             const ChromaOut& cr = v ? co[1] : ce[1];

@@ -131,6 +131,19 @@ def test_gpu_jpeg_batch_matches_golden(ctx, oracle, channels):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("band", [1, 2, 3, 8])
+def test_gpu_jpeg_colour_bands(ctx, band, monkeypatch):
+    """The colour pass with short bands of output rows per workgroup (AEON_HIP_JPEG_BAND; the default
+    is 32): odd band starts take the general path, even ones the 4:2:0 row-pair path with a band
+    that ends on an odd row -- every fixture still matches its golden digest."""
+    monkeypatch.setenv("AEON_HIP_JPEG_BAND", str(band))
+    files = [_jpg(n) for n in NAMES]
+    res = _decode_gpu(ctx, files, 3)
+    for name, r in zip(NAMES, res):
+        assert np.array_equal(_sha(r), FX[name + ".bgr"]), (name, band)
+
+
+@pytest.mark.gpu
 def test_gpu_jpeg_large_batch_repeatable(ctx, oracle):
     """A decode window of 300 JPEGs (the two aeon fixtures cycled with the synthetic ones):
     bit-exact against the oracle and identical on a rerun."""
