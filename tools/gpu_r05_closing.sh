@@ -1,11 +1,12 @@
 #!/bin/bash
-# Round-5 closing profile set (profiles/r05g): GPU tests, smoke, the driver's bench command, rocprofv3 kernel
+# Round-5 closing profile set (profiles/r05g, profiles/r05h: CLOSE_TAG): GPU tests, smoke, the driver's bench command, rocprofv3 kernel
 # stats of the C2 contract run, C3 (one-launch record kernel), C5, the JPEG stage and the C2 workload
 # with CUBIC / AREA / LANCZOS4, then PMC passes + HBM traffic for C2 / C3 / C5.
 set -o pipefail
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
-cd "$R"; mkdir -p gpurun_out/r05g; export TMPDIR=/tmp
-O="$R/gpurun_out/r05g"
+T="${CLOSE_TAG:-r05g}" # output set: gpurun_out/$T (copied to profiles/$T)
+cd "$R"; mkdir -p gpurun_out/$T; export TMPDIR=/tmp
+O="$R/gpurun_out/$T"
 if [ -z "$SKIP_TESTS" ]; then
   timeout -k 10 900 python -u -m pytest tests -m gpu -q --maxfail=5 --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { tail -20 $O/pytest_gpu.log; exit 1; }
   tail -1 $O/pytest_gpu.log
@@ -34,6 +35,6 @@ cd "$R"
 [ -n "$SKIP_PMC" ] && exit 0
 for cfg in C2 C3 C5; do
   tools/gpu_pmc.sh $cfg > $O/pmc_$cfg.txt 2>&1 || { echo "pmc $cfg failed"; tail $O/pmc_$cfg.txt; exit 1; }
-  python tools/pmc_summary.py gpurun_out/pmc/$cfg $cfg $O/traffic_r05g.json > $O/pmc_${cfg}_summary.txt || exit 1
+  python tools/pmc_summary.py gpurun_out/pmc/$cfg $cfg $O/traffic_$T.json > $O/pmc_${cfg}_summary.txt || exit 1
 done
 echo "pmc ok"
