@@ -126,6 +126,15 @@ struct GrTap {
     int32_t s;
     int16_t c[8];
 };
+// What the host computes per GR_LANCZOS4 destination column / row: the source anchor s and fraction f
+// (cv::resize's), and sin / cos of y0 = -(f + 3) * pi / 4 from the C library, as OpenCV's
+// interpolateLanczos4 takes them (imgwarp.cpp); the device finishes the eight coefficients
+// (lanczos4_taps, resize_kernels.hip) in the same IEEE operations, so the taps are the host's bit for bit.
+struct LzIn {
+    double  s0, c0;
+    float   f;
+    int32_t s;
+};
 
 // Per-launch uniform arguments.
 struct LaunchArgs {

@@ -470,19 +470,24 @@ void thread_pool::worker(int index)
             fn   = m_fn;
             n    = m_n;
         }
-        for (;;) { // dynamic task distribution (thread_pool.hpp:155-162)
-            int i = m_next.fetch_add(1);
-            if (i >= n) break;
+        // dynamic task distribution (thread_pool.hpp:155-162), the task counter tagged with the run's
+        // generation: a worker that wakes after its run completed (the caller has returned, fn is
+        // gone) takes nothing, whatever run the counter belongs to by then
+        uint64_t st = m_state.load();
+        for (;;) {
+            if ((uint32_t)(st >> 32) != (uint32_t)seen || (int)(uint32_t)st >= n) break;
+            if (!m_state.compare_exchange_weak(st, st + 1)) continue;
             try {
-                (*fn)(i, index);
+                (*fn)((int)(uint32_t)st, index);
             } catch (...) {
                 std::lock_guard<std::mutex> l(m_mu);
                 if (!m_error) m_error = std::current_exception();
             }
-        }
-        {
-            std::lock_guard<std::mutex> l(m_mu);
-            if (--m_active == 0) m_done_cv.notify_all();
+            if (m_done.fetch_add(1) + 1 == n) {
+                std::lock_guard<std::mutex> l(m_mu);
+                m_done_cv.notify_all();
+            }
+            st = m_state.load();
         }
     }
 }
@@ -494,18 +499,21 @@ void thread_pool::run(int n, const std::function<void(int)>& fn)
 
 void thread_pool::run_indexed(int n, const std::function<void(int, int)>& fn)
 {
+    // aeon's run() waits for every worker to check in (thread_pool.hpp:103-116); this one waits for the
+    // n tasks: a pinned worker whose CPU another process holds no longer stalls the run until it is
+    // scheduled (milliseconds on a shared host) when the others have done its share
     {
         std::lock_guard<std::mutex> l(m_mu);
-        m_fn     = &fn;
-        m_n      = n;
-        m_active = m_nthreads;
-        m_error  = nullptr;
-        m_next   = 0;
+        m_fn    = &fn;
+        m_n     = n;
+        m_error = nullptr;
+        m_done  = 0;
         m_generation++;
+        m_state = (uint64_t)(uint32_t)m_generation << 32;
     }
     m_cv.notify_all();
     std::unique_lock<std::mutex> l(m_mu);
-    m_done_cv.wait(l, [&] { return m_active == 0; });
+    m_done_cv.wait(l, [&] { return m_done.load() >= n; });
     if (m_error) std::rethrow_exception(m_error); // thread_pool.hpp:113-115
 }
 

@@ -183,9 +183,10 @@ private:
     std::mutex                           m_mu;
     std::condition_variable              m_cv, m_done_cv;
     const std::function<void(int, int)>* m_fn = nullptr;
-    int                            m_n = 0, m_active = 0;
+    int                            m_n = 0;
+    std::atomic<int>               m_done{0}; // tasks of the current run completed
     long                           m_generation = 0;
-    std::atomic<int>               m_next{0};
+    std::atomic<uint64_t>          m_state{0}; // (generation << 32) | next task: a task is taken only in its own run
     std::exception_ptr             m_error;
     bool                           m_stop = false;
 };

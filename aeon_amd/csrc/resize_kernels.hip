@@ -681,6 +681,49 @@ __global__ __launch_bounds__(256) void resize_sep(const ResizeJob* __restrict__ 
     }
 }
 
+// The device half of interpolateLanczos4 (OpenCV 2.4.9 imgwarp.cpp; the host half: lanczos4_inputs,
+// stage.cpp): per destination column / row the eight coefficients from the fraction f and the host's
+// sin / cos of y0 -- the same IEEE float and double operations in the same order (no contraction:
+// -ffp-contract=off; correctly rounded divisions) -- normalised to sum 1 in float, then the 11-bit
+// fixed point of the taps.
+__global__ __launch_bounds__(256) void lanczos4_taps(const LzIn* __restrict__ in, GrTap* __restrict__ out, int n)
+{
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const LzIn L = in[i];
+    const double s45 = 0.70710678118654752440084436210485;
+    const double cs0[8] = {1, -s45, 0, s45, -1, s45, 0, -s45}, cs1[8] = {0, -s45, 1, -s45, 0, s45, -1, s45};
+    const double kPi = 3.1415926535897932384626433832795;
+    float c[8];
+    if (L.f < FLT_EPSILON) {
+#pragma unroll
+        for (int k = 0; k < 8; k++) c[k] = k == 3 ? 1.f : 0.f;
+    } else {
+        float sum = 0;
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const double y = -(L.f + 3 - k) * kPi * 0.25;
+            c[k]           = (float)((cs0[k] * L.s0 + cs1[k] * L.c0) / (y * y));
+            sum += c[k];
+        }
+        sum = __fdiv_rn(1.f, sum);
+#pragma unroll
+        for (int k = 0; k < 8; k++) c[k] *= sum;
+    }
+    GrTap t;
+    t.s = L.s;
+#pragma unroll
+    for (int k = 0; k < 8; k++) t.c[k] = (int16_t)min(max((int)rintf(c[k] * 2048.f), -32768), 32767);
+    out[i] = t;
+}
+
+hipError_t launch_lanczos4_taps(const LzIn* in, GrTap* out, int n, hipStream_t stream)
+{
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(lanczos4_taps, dim3((n + 255) / 256), dim3(256), 0, stream, in, out, n);
+    return hipGetLastError();
+}
+
 hipError_t launch_resize_sep(int K, const ResizeJob* jobs, const uint8_t* table, int n_jobs, int max_tiles, int TR, int CW,
                              int NR, int SW, int cn, const float* lut, int bgr, int chm, int32_t* error, hipStream_t stream)
 {

@@ -49,6 +49,7 @@ hipError_t contrast_records_lds_limit(int bytes);
 hipError_t launch_resize_generic(const ResizeJob* jobs, const uint8_t* table, int n_jobs, int max_tiles, int TR, int CW,
                                  int NR, int xs, int amax, int cn_max, int SW, const float* lut, int bgr, int chm,
                                  int32_t* error, hipStream_t stream);
+hipError_t launch_lanczos4_taps(const LzIn* in, GrTap* out, int n, hipStream_t stream);
 hipError_t launch_resize_sep(int K, const ResizeJob* jobs, const uint8_t* table, int n_jobs, int max_tiles, int TR, int CW,
                              int NR, int SW, int cn, const float* lut, int bgr, int chm, int32_t* error, hipStream_t stream);
 void       jpeg_decode_batch(JpegState* S, int n, const void* const* data, const size_t* sizes,
@@ -408,44 +409,26 @@ int generic_method(int sw, int sh, int dw, int dh, int interp, int cn, int* isx,
     return GR_AREA;
 }
 
-// interpolateLanczos4 (OpenCV 2.4.9 imgwarp.cpp), double sin / cos of the C library as OpenCV's.
-void lanczos4_coeffs(float x, float* c)
+// The host half of interpolateLanczos4 (OpenCV 2.4.9 imgwarp.cpp) for destinations [d0, d0 + n) of an
+// ssize -> dsize axis (x: the anchor clamped as cv::resize does for columns; y: raw, the rows clipped
+// per tap on use): the anchor, the fraction and the double sin / cos of the C library as OpenCV's --
+// the one part a device could not reproduce bit for bit.  The coefficients are finished on the device
+// (lanczos4_taps, resize_kernels.hip).
+void lanczos4_inputs(int ssize, double scale, int d0, int n, bool clamp, LzIn* out)
 {
-    static const double s45 = 0.70710678118654752440084436210485;
-    static const double cs[][2] = {{1, 0}, {-s45, -s45}, {0, 1}, {s45, -s45}, {-1, 0}, {s45, s45}, {0, -1}, {-s45, s45}};
     const double kPi = 3.1415926535897932384626433832795;
-    if (x < FLT_EPSILON) {
-        for (int i = 0; i < 8; i++) c[i] = 0;
-        c[3] = 1;
-        return;
-    }
-    float        sum = 0;
-    const double y0 = -(x + 3) * kPi * 0.25, s0 = std::sin(y0), c0 = std::cos(y0);
-    for (int i = 0; i < 8; i++) {
-        const double y = -(x + 3 - i) * kPi * 0.25;
-        c[i]           = (float)((cs[i][0] * s0 + cs[i][1] * c0) / (y * y));
-        sum += c[i];
-    }
-    sum = 1.f / sum;
-    for (int i = 0; i < 8; i++) c[i] *= sum;
-}
-
-// Lanczos4 taps of destinations [d0, d0 + n) of an ssize -> dsize axis (x: the anchor clamped as
-// cv::resize does for columns; y: raw, the rows clipped per tap on use), into out[0 .. n).
-void lanczos4_taps(int ssize, double scale, int d0, int n, bool clamp, GrTap* out)
-{
     for (int d = d0; d < d0 + n; d++) {
         float f = (float)((d + 0.5) * scale - 0.5);
         int   s = (int)std::floor(f);
         f -= (float)s;
         if (clamp && s < 0) f = 0, s = 0;
         if (clamp && s >= ssize - 1) f = 0, s = ssize - 1;
-        float c[8];
-        lanczos4_coeffs(f, c);
-        GrTap t{};
-        t.s = s;
-        for (int k = 0; k < 8; k++) t.c[k] = (int16_t)std::min(std::max((int)std::rint(c[k] * 2048.f), -32768), 32767);
-        out[d - d0] = t;
+        LzIn L{0.0, 0.0, f, s};
+        if (!(f < FLT_EPSILON)) {
+            const double y0 = -(f + 3) * kPi * 0.25;
+            L.s0 = std::sin(y0), L.c0 = std::cos(y0);
+        }
+        out[d - d0] = L;
     }
 }
 
@@ -453,8 +436,7 @@ void lanczos4_taps(int ssize, double scale, int d0, int n, bool clamp, GrTap* ou
 // shares (rows x columns of a tile sized so the taps and the horizontal sums fit 64 KiB of LDS).
 struct GrPlan {
     std::vector<ResizeJob> jobs;
-    std::vector<GrTap>     taps;
-    size_t                 off = 0, taps_off = 0; // byte offsets in the call's table
+    size_t                 off = 0, lz_off = 0, taps_off = 0; // byte offsets in the call's table
     // One launch per method class (finalize sorts the jobs so each class is contiguous): the
     // fixed-K methods as resize_sep bands, the rest (INTER_AREA's float taps, integer boxes, jobs
     // whose bands do not fit) as resize_generic tiles.
@@ -467,7 +449,7 @@ struct GrPlan {
     std::vector<Sub> subs;
     double bytes = 0; // algorithmic: the source region read once + the window written
 
-    size_t n_taps = 0; // Lanczos4 taps reserved by add(), computed by fill_taps()
+    size_t n_taps = 0; // Lanczos4 taps reserved by add(), their inputs computed by fill_taps()
 
     void add(ResizeJob R)
     {
@@ -477,16 +459,20 @@ struct GrPlan {
         }
         jobs.push_back(R);
     }
-    // The Lanczos4 tap tables (a sin and a cos per destination column and row: ~18 us of libm per
-    // 224x224 record), on `pool` when there are enough jobs to pay for it.
-    void fill_taps(thread_pool* pool)
+    // The Lanczos4 tap inputs (a sin and a cos per destination column and row), on `pool` when there
+    // are enough jobs to pay for it; the device turns them into the taps (the whole taps computed here
+    // cost ~75 us per 224x224 record of libm, divisions and rounding: ~1.1 ms per 256-record call on
+    // 14 threads, and the LANCZOS4 step was host-bound).
+    // They go straight into the call's pinned table (`lz`: n_taps entries; a per-call vector of ~2.8 MB
+    // and its copy into the table cost page faults under 14 writers and ~0.1 ms of memcpy).
+    void fill_taps(thread_pool* pool, LzIn* lz) const
     {
-        taps.resize(n_taps);
         auto one = [&](int i) {
             const ResizeJob& R = jobs[i];
             if (R.method != GR_LANCZOS4) return;
-            lanczos4_taps(R.crop_w, R.scale_x, R.win_x, R.win_w, true, taps.data() + R.coef_x / sizeof(GrTap));
-            lanczos4_taps(R.crop_h, R.scale_y, R.win_y, R.win_h, false, taps.data() + R.coef_y / sizeof(GrTap));
+            // (coef_x / coef_y: byte offsets of the device-built taps, taps_off onwards)
+            lanczos4_inputs(R.crop_w, R.scale_x, R.win_x, R.win_w, true, lz + (R.coef_x - taps_off) / sizeof(GrTap));
+            lanczos4_inputs(R.crop_h, R.scale_y, R.win_y, R.win_h, false, lz + (R.coef_y - taps_off) / sizeof(GrTap));
         };
         if (pool && n_taps > 4096) pool->run((int)jobs.size(), one);
         else for (int i = 0; i < (int)jobs.size(); i++) one(i);
@@ -1039,9 +1025,12 @@ void ensure_ring(aeon_hip_ctx* ctx, size_t table, size_t partials, size_t shifts
     table = std::max<size_t>(table, 16);
     if (table <= ctx->table_cap && partials <= ctx->partials_cap && shifts <= ctx->shifts_cap) return;
     drain_ring(ctx);
-    const size_t tc = table > ctx->table_cap ? std::max(table, ctx->table_cap * 2) : ctx->table_cap;
-    const size_t pc = partials > ctx->partials_cap ? std::max(partials, ctx->partials_cap * 2) : ctx->partials_cap;
-    const size_t sc = shifts > ctx->shifts_cap ? std::max(shifts, ctx->shifts_cap * 2) : ctx->shifts_cap;
+    // (a quarter over the first need: a call's tables vary with its records' crops, and a later call
+    // needing a few bytes more would otherwise reallocate every slot inside a loader's steady state --
+    // ~10-20 ms of pinned and device allocations, seen as one-off stalls of the LANCZOS4 step)
+    const size_t tc = table > ctx->table_cap ? std::max(table + table / 4, ctx->table_cap * 2) : ctx->table_cap;
+    const size_t pc = partials > ctx->partials_cap ? std::max(partials + partials / 4, ctx->partials_cap * 2) : ctx->partials_cap;
+    const size_t sc = shifts > ctx->shifts_cap ? std::max(shifts + shifts / 4, ctx->shifts_cap * 2) : ctx->shifts_cap;
     for (Slot& q : ctx->slots) {
         grow(q.host, q.host_cap, tc, true);
         HIP_OK(hipHostGetDevicePointer((void**)&q.host_dev, q.host, 0));
@@ -1551,15 +1540,12 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
     for (GrPlan* g : {&gr_short, &gr_main}) { // jobs, then their Lanczos taps (offsets made absolute)
         if (g->jobs.empty()) continue;
         if (g->n_taps > 4096 && !ctx->plan_pool) ctx->plan_pool.reset(new thread_pool(thread_affinity_map("")));
-        g->fill_taps(ctx->plan_pool.get());
         g->finalize();
         blob        = (blob + 15) & ~(size_t)15;
         g->off      = blob;
         blob += g->jobs.size() * sizeof(ResizeJob);
-        g->taps_off = blob;
-        blob += g->taps.size() * sizeof(GrTap);
-        for (ResizeJob& R : g->jobs)
-            if (R.method == GR_LANCZOS4) R.coef_x += (int32_t)g->taps_off, R.coef_y += (int32_t)g->taps_off;
+        g->lz_off = blob;
+        blob += g->n_taps * sizeof(LzIn);
     }
     blob = (blob + 15) & ~(size_t)15;
     int              exp_max_px = 0;
@@ -1610,6 +1596,15 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
                     if (J.stats_slot >= 0) J.stats_tiles = slot_tiles[J.stats_slot];
         }
     const size_t partial_words = std::max<size_t>(4, pass1_all.jobs.size() * partial_stride * 4);
+    // the Lanczos4 taps the device builds: after everything the host writes (not uploaded)
+    size_t table_cap = (blob + 15) & ~(size_t)15;
+    for (GrPlan* g : {&gr_short, &gr_main}) {
+        if (g->n_taps == 0) continue;
+        g->taps_off = table_cap;
+        table_cap += ((g->n_taps * sizeof(GrTap)) + 15) & ~(size_t)15;
+        for (ResizeJob& R : g->jobs)
+            if (R.method == GR_LANCZOS4) R.coef_x += (int32_t)g->taps_off, R.coef_y += (int32_t)g->taps_off;
+    }
 
     phase(2);
     int   slot;
@@ -1618,8 +1613,8 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
     const float* d_lut = resident_lut(ctx, od, ov.u8_map);
     // job tables, contrast sums and shifts: one capacity for every slot of the ring (a call never
     // allocates unless it needs more than any call before it); scratch per slot, on demand
-    ensure_ring(ctx, blob, partial_words * 4, std::max<size_t>(1, pass1_all.jobs.size()) * 4 * sizeof(double));
-    if (scratch_bytes > 0) grow(s.scratch, s.scratch_cap, scratch_bytes, false);
+    ensure_ring(ctx, table_cap, partial_words * 4, std::max<size_t>(1, pass1_all.jobs.size()) * 4 * sizeof(double));
+    if (scratch_bytes > s.scratch_cap) grow(s.scratch, s.scratch_cap, scratch_bytes + scratch_bytes / 4, false); // (slack as ensure_ring)
     for (RotJob& R : rot) R.out_ptr += (uint64_t)s.scratch;
     for (Mask16Job& M : m16)
         if (M.src_scratch) M.src_ptr += (uint64_t)s.scratch;
@@ -1635,7 +1630,7 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
             if (R.out_scratch) R.out_ptr += (uint64_t)s.scratch;
         }
         std::memcpy(s.host + g->off, g->jobs.data(), g->jobs.size() * sizeof(ResizeJob));
-        if (!g->taps.empty()) std::memcpy(s.host + g->taps_off, g->taps.data(), g->taps.size() * sizeof(GrTap));
+        if (g->n_taps) g->fill_taps(ctx->plan_pool.get(), (LzIn*)(s.host + g->lz_off));
     }
     if (!rot.empty()) std::memcpy(s.host + rot_off, rot.data(), rot.size() * sizeof(RotJob));
     if (!m16.empty()) std::memcpy(s.host + m16_off, m16.data(), m16.size() * sizeof(Mask16Job));
@@ -1660,7 +1655,7 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
         for (LaunchPlan& P : *v) mask_only = mask_only && P.jobs.empty();
     // the tables in HBM written by the host (no upload launch) unless a LANCZOS4 tap table is among
     // them (read per output pixel: the cached device copy)
-    const bool     vram_ok = gr_short.taps.empty() && gr_main.taps.empty();
+    const bool     vram_ok = gr_short.n_taps == 0 && gr_main.n_taps == 0;
     const uint8_t* vt      = vram_ok ? publish_table(ctx, s, blob) : nullptr;
     const uint8_t* table   = vt ? vt : mask_only ? s.host_dev : s.dev;
     // timing events on one call in timing_every (each event pair costs GPU time between launches)
@@ -1684,6 +1679,10 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
     } else {
         HIP_OK(launch_upload_table(s.host_dev, s.dev, blob, stream));
     }
+    for (GrPlan* g : {&gr_short, &gr_main}) // the Lanczos4 taps from their host-computed inputs
+        if (g->n_taps)
+            HIP_OK(launch_lanczos4_taps((const LzIn*)(table + g->lz_off), (GrTap*)(table + g->taps_off), (int)g->n_taps,
+                                        stream));
     phase(5);
 
     auto args = [&](const LaunchPlan& L) {
