@@ -158,3 +158,16 @@ def test_resize_methods_final_output(ctx, method, case):
     stride = 224 * 224 * cn * 4 + (36 if case == "odd_stride" else 0)
     out = A.out_desc(item_stride=stride, **ok)
     _assert_same(H.hip_records(ctx, imgs, params, out), H.oracle_records(imgs, params, out), f"{method} {case}")
+
+
+def test_resize_lanczos4_taps_c2_batch(ctx):
+    """LANCZOS4's taps are finished on the GPU from the host's libm sin / cos (stage.cpp
+    lanczos4_inputs -> resize_kernels.hip lanczos4_taps): a C2 batch of 64 random crops (as many
+    distinct fractions per axis as output columns and rows) equals the oracle, whose taps are the
+    host's from end to end."""
+    aug = dict(C.C2_AUG, interpolation_method="LANCZOS4")
+    imgs = [A.synthetic_image(60 + i, 256, 256, 3) for i in range(64)]
+    params = H.draw_params(aug, [(256, 256)] * 64, 224, 224, seed=29)
+    assert all(p.interp == A.INTERP_LANCZOS4 for p in params)
+    out = A.out_desc(item_stride=3 * 224 * 224 * 4, **F32)
+    _assert_same(H.hip_records(ctx, imgs, params, out), H.oracle_records(imgs, params, out), "LANCZOS4 C2")
