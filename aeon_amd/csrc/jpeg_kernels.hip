@@ -1,12 +1,15 @@
 // jpeg_kernels.hip -- GPU half of the JPEG decode stage (see jpeg.hpp), bit-exact with libjpeg's
 // defaults as cv::imdecode runs them under aeon's image::extractor::extract (etl_image.cpp:83-99).
 //
-// jpeg_idct: eight lanes per 8x8 block.  They scatter the block's non-zero coefficients (zigzag
-// mask + values), dequantised, into its LDS slot (a mask byte each), then run jidctint.c's
-// jpeg_idct_islow (LL&M, CONST_BITS 13, PASS1_BITS 2; the post-IDCT range limit of jdmaster.c,
-// x & 1023 wrap) -- integer multiply-adds only -- a column each, then a row each, and each lane
-// writes its output row of the block into the component plane (one 8-byte store).
-// jpeg_color: one lane per 4 output pixels of each of kJpegRowsPerWg rows: each component sampled
+// jpeg_idct: eight lanes per 8x8 block.  They gather the block's non-zero coefficients (the sparse
+// stream of a host-decoded file, or the dense zigzag slots of a GPU-decoded one through an LDS
+// scatter), dequantised, then run jidctint.c's jpeg_idct_islow (LL&M, CONST_BITS 13, PASS1_BITS 2;
+// the post-IDCT range limit of jdmaster.c, x & 1023 wrap) -- integer multiply-adds only -- a column
+// each, then a row each, and each lane writes its output row of the block into the component plane
+// (one 8-byte store).
+// jpeg_color: a workgroup per band of up to kJpegRowsPerWg output rows.  4:2:0 files with BGR output
+// take color_h2v2 (8 columns of a row pair per lane, packed 16-bit upsampling); the others one lane
+// per 4 output pixels of the band: each component sampled
 // through jdsample.c's upsampler (h2v1 / h1v2 / h2v2 fancy triangle filters, context rows
 // replicated at the edges as jdmainct.c does; box replication for the other ratios and for
 // components narrower than 3 samples), then jdcolor.c ycc_rgb_convert (16-bit fixed point) and the
