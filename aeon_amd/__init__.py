@@ -85,6 +85,17 @@ class EncodedElem(ctypes.Structure):
                 ("height", ctypes.c_int32), ("channels", ctypes.c_int32), ("stride", ctypes.c_int32)]
 
 
+class EncodedRecords:
+    """Records marshalled once (Decoder.encoded): their aeon_encoded_elem array and the Python objects
+    whose memory it points at."""
+
+    def __init__(self, n, elems, keep):
+        self.n, self.elems, self.keep = n, elems, keep
+
+    def __len__(self):
+        return self.n
+
+
 class AeonHipError(RuntimeError):
     def __init__(self, code, msg):
         super().__init__(f"aeon_hip error {code}: {msg}")
@@ -572,8 +583,17 @@ class Decoder:
         except Exception:
             pass
 
+    def encoded(self, records):
+        """The records marshalled once into their aeon_encoded_elem array (EncodedRecords), for windows
+        submitted again and again: aeon's host hands the decoder plain pointers, so a benchmark that
+        rebuilds ctypes structures per record per window (~2-5 us each) would time Python instead."""
+        elems, keep = self._encoded(records)
+        return EncodedRecords(len(records), elems, keep)
+
     def _encoded(self, records):
         """aeon_encoded_elem array for records whose elements are JPEG bytes or HWC uint8 arrays."""
+        if isinstance(records, EncodedRecords):
+            return records.elems, records.keep
         n, ne = len(records), len(self.outputs)
         keep = []
         elems = (EncodedElem * (n * ne))()
@@ -631,7 +651,9 @@ class Decoder:
 
     def submit(self, records, output_ptrs, on_device=False):
         """Double-buffered window (aeon_decoder_submit): output_ptrs[k] = address of n items of
-        output k (pinned host memory, or device memory with on_device); complete after wait()."""
+        output k (pinned host memory, or device memory with on_device); complete after wait().
+        records: a list of tuples, or an EncodedRecords from encoded() (kept alive by the caller
+        until the window's wait())."""
         n, ne = len(records), len(self.outputs)
         elems, keep = self._encoded(records)
         ptrs = (ctypes.c_void_p * ne)(*output_ptrs)

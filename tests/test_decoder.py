@@ -142,8 +142,8 @@ def test_decoder_encoded_and_decoded_elements_mix():
 
 def test_decoder_submit_wait_double_buffered():
     """aeon_decoder_submit / wait: two windows in flight on the decoder's streams (async_manager's
-    two containers) give exactly the synchronous decode's outputs, window by window; a third submit
-    before a wait is refused."""
+    two containers) give exactly the synchronous decode's outputs, window by window (windows 1 and 3
+    as records marshalled once, Decoder.encoded); a third submit before a wait is refused."""
     import torch
     files = _jpeg_files()
     files = [f for f in files if min(A.jpeg_info(f)[:2]) >= 8]
@@ -152,6 +152,7 @@ def test_decoder_submit_wait_double_buffered():
     sync = A.Decoder(cfg)
     want = [sync.decode(win)[0] for win in windows]
     d = A.Decoder(cfg)
+    windows = [d.encoded(win) if w % 2 else win for w, win in enumerate(windows)]
     item = 3 * 224 * 224 * 4
     bufs = [torch.empty(len(files) * item, dtype=torch.uint8).pin_memory() for _ in range(2)]
     got = []
