@@ -596,7 +596,7 @@ def jpeg_files(batch):
     return [files[i % 2] for i in range(batch)]
 
 
-def run_e2e_jpeg(A, C, torch, batch=512, windows=12, on_device=False):
+def run_e2e_jpeg(A, C, torch, batch=512, windows=30, on_device=False):
     """The product's whole decode stage from encoded records, double-buffered (aeon_decoder_submit /
     wait over two windows): JPEG entropy decode on the host pool, sparse coefficients H2D, GPU IDCT
     + colour into the source arena, C2 augmentation, and (host outputs) D2H into pinned buffers."""
