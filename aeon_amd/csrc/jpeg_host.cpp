@@ -1235,6 +1235,12 @@ void jpeg_decode_batch(JpegState* S, int n, const void* const* data, const size_
         H.data_words = g.data_words;
         if (g.data_words * 4 <= stage_cap) huff_stage = std::max(huff_stage, g.data_words * 4);
     }
+    // The Huffman workgroups in order of entropy-coded size, largest first: dispatched in order, one
+    // per CU per pass, workgroups i and i + 256 of a 512-file window share a CU, so each CU pairs a
+    // long decode with a short one (in file order an alternating window put two large files on every
+    // CU of half the XCDs).  Each descriptor carries its own outputs: the order changes nothing else.
+    std::stable_sort((JpegHuffFile*)(st.pinned + huf_off), hf,
+                     [](const JpegHuffFile& x, const JpegHuffFile& y) { return x.data_words > y.data_words; });
     if (!chunks.empty()) std::memcpy(st.pinned + chk_off, chunks.data(), chunks.size() * sizeof(JpegChunk));
     if (!rows.empty()) std::memcpy(st.pinned + row_off, rows.data(), rows.size() * sizeof(JpegRows));
     mark(3);
