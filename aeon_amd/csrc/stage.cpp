@@ -829,6 +829,7 @@ struct aeon_hip_ctx {
     bool                 jpeg_gpu_huff = true; // AEON_HIP_JPEG_HUFF=host: every JPEG through the host entropy decoder
     std::vector<JobGeom> geoms;              // reused per call
     std::vector<AugJob>  direct_jobs;        // (run_direct) the call's jobs before they go into the slot
+    std::vector<int>     direct_order;       // (run_direct) their table order: largest crop first
     JpegState*           jpeg = nullptr;     // JPEG decode stage (pool, staging ring), on first use
     thread_pool*         host_pool = nullptr; // the owning decoder's pool (ctx_share_pool), for the JPEG stage
     std::unique_ptr<thread_pool> plan_pool;        // the context's own, made for the first call with many Lanczos4 taps
@@ -1321,8 +1322,17 @@ bool run_direct(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void
     // into the pinned slot the tiles read over PCIe
     const bool vram = ctx->vram_jobs && tbytes > 0 && tbytes <= kVramTableMax && tbytes <= s.vram_cap;
     uint8_t*   dstt = vram ? s.vram : s.host;
+    // largest crop first: the first round's workgroups take the first jobs' tiles and the dynamic tail
+    // hands out the rest in table order, so the cheapest tiles come last and the launch's tail is
+    // theirs (each job carries its own source and output: the order changes nothing else)
+    std::vector<int>& order = ctx->direct_order;
+    order.resize(n);
+    for (int i = 0; i < n; i++) order[i] = i;
+    std::stable_sort(order.begin(), order.end(), [&](int x, int y) {
+        return (int64_t)geo[x].crop_w * geo[x].crop_h > (int64_t)geo[y].crop_w * geo[y].crop_h;
+    });
     for (int i = 0; i < n; i++) {
-        AugJob& J = jobs[i];
+        AugJob& J = jobs[order[i]];
         J.tiles   = (J.win_h + P.tr - 1) / P.tr;
         std::memcpy(dstt + i * stride, &J, stride);
     }
