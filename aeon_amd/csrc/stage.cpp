@@ -1325,12 +1325,19 @@ bool run_direct(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void
     // largest crop first: the first round's workgroups take the first jobs' tiles and the dynamic tail
     // hands out the rest in table order, so the cheapest tiles come last and the launch's tail is
     // theirs (each job carries its own source and output: the order changes nothing else)
+    // (a counting sort into 32 area classes: two passes, ~1 us for 256 records, where a comparison sort
+    // cost the host several)
     std::vector<int>& order = ctx->direct_order;
     order.resize(n);
-    for (int i = 0; i < n; i++) order[i] = i;
-    std::stable_sort(order.begin(), order.end(), [&](int x, int y) {
-        return (int64_t)geo[x].crop_w * geo[x].crop_h > (int64_t)geo[y].crop_w * geo[y].crop_h;
-    });
+    {
+        int64_t amax = 1;
+        for (int i = 0; i < n; i++) amax = std::max(amax, (int64_t)geo[i].crop_w * geo[i].crop_h);
+        int  cnt[33] = {0};
+        auto cls     = [&](int i) { return 31 - (int)((int64_t)geo[i].crop_w * geo[i].crop_h * 31 / amax); };
+        for (int i = 0; i < n; i++) cnt[cls(i) + 1]++;
+        for (int c = 0; c < 32; c++) cnt[c + 1] += cnt[c];
+        for (int i = 0; i < n; i++) order[cnt[cls(i)]++] = i;
+    }
     for (int i = 0; i < n; i++) {
         AugJob& J = jobs[order[i]];
         J.tiles   = (J.win_h + P.tr - 1) / P.tr;
