@@ -1191,6 +1191,24 @@ void jpeg_decode_batch(JpegState* S, int n, const void* const* data, const size_
     JpegHuffFile*  hf   = (JpegHuffFile*)(st.pinned + huf_off);
     int            huff_stage = 0; // LDS for the largest GPU-decoded file's data that fits the cap
     const int      stage_cap  = n_gpu ? jpeg_huff_stage_cap(S->huff_lanes) : 0;
+    // The Huffman workgroups in order of entropy-coded size, largest first: dispatched in order, one
+    // per CU per pass, workgroups i and i + 256 of a 512-file window share a CU, so each CU pairs a
+    // long decode with a short one (in file order an alternating window put two large files on every
+    // CU of half the XCDs).  Each descriptor carries its own outputs: the order changes nothing else.
+    // A counting sort into 64 size classes gives each file its descriptor slot (hpos).
+    std::vector<int> hpos(n, -1);
+    {
+        int64_t maxw = 1;
+        for (int i = 0; i < n; i++)
+            if (on_gpu[i]) maxw = std::max<int64_t>(maxw, gs[i].data_words);
+        int  cnt[65] = {0};
+        auto cls     = [&](int i) { return 63 - (int)((int64_t)gs[i].data_words * 63 / maxw); };
+        for (int i = 0; i < n; i++)
+            if (on_gpu[i]) cnt[cls(i) + 1]++;
+        for (int c = 0; c < 64; c++) cnt[c + 1] += cnt[c];
+        for (int i = 0; i < n; i++)
+            if (on_gpu[i]) hpos[i] = cnt[cls(i)]++;
+    }
     for (int i = 0; i < n; i++) {
         const Frame& f = frames[i];
         JpegImage&   J = imgs[i];
@@ -1217,7 +1235,7 @@ void jpeg_decode_batch(JpegState* S, int n, const void* const* data, const size_
         J.hmax       = f.hmax, J.vmax = f.vmax;
         if (!on_gpu[i]) continue;
         const GpuScan& g = gs[i];
-        JpegHuffFile&  H = *hf++;
+        JpegHuffFile&  H = hf[hpos[i]];
         std::memset(&H, 0, sizeof(H));
         H.data    = base + g.data;
         H.segs    = base + g.segs;
@@ -1235,12 +1253,6 @@ void jpeg_decode_batch(JpegState* S, int n, const void* const* data, const size_
         H.data_words = g.data_words;
         if (g.data_words * 4 <= stage_cap) huff_stage = std::max(huff_stage, g.data_words * 4);
     }
-    // The Huffman workgroups in order of entropy-coded size, largest first: dispatched in order, one
-    // per CU per pass, workgroups i and i + 256 of a 512-file window share a CU, so each CU pairs a
-    // long decode with a short one (in file order an alternating window put two large files on every
-    // CU of half the XCDs).  Each descriptor carries its own outputs: the order changes nothing else.
-    std::stable_sort((JpegHuffFile*)(st.pinned + huf_off), hf,
-                     [](const JpegHuffFile& x, const JpegHuffFile& y) { return x.data_words > y.data_words; });
     if (!chunks.empty()) std::memcpy(st.pinned + chk_off, chunks.data(), chunks.size() * sizeof(JpegChunk));
     if (!rows.empty()) std::memcpy(st.pinned + row_off, rows.data(), rows.size() * sizeof(JpegRows));
     mark(3);
