@@ -238,6 +238,36 @@ AEON_HD inline LdsLayout lds_layout(int max_win_w, int rows_per_tile, int stage_
     return L;
 }
 
+// ---- split_kernels.hip: the single-pass tile kernel with staging helper waves ----------------------
+// LDS carve of augment_split (bytes, 16-aligned regions): the LUT at offset 0 (lut_at), then per
+// staging buffer b its column taps, row taps and tile info, a ring of three jobs, two staging buffers.
+struct SplitLds {
+    int lut, xt, yt, job, info, stage, stage_bytes, xt_bytes, total;
+};
+constexpr int kSplitTRMax  = 64; // output rows per tile, at most (row-tap table size)
+constexpr int kSplitJobs   = 3;  // job ring slots
+AEON_HD inline SplitLds split_lds_layout(int win_w, int stage_bytes)
+{
+    SplitLds L;
+    int      o = 0;
+    L.lut = o; o += 3 * 256 * 4;                         // standardize LUT (source channel order)
+    L.xt_bytes = ((win_w * 8 + 15) / 16) * 16;
+    L.xt  = o; o += 2 * L.xt_bytes;                      // column taps + weights, per buffer
+    L.yt  = o; o += 2 * kSplitTRMax * 16;                // row taps + weights, per buffer
+    L.job = o; o += kSplitJobs * (int)sizeof(AugJob);    // the jobs of three consecutive tiles
+    L.info = o; o += 2 * 64;                             // per buffer: its tile (ok, job slot, y0, rows)
+    L.stage_bytes = stage_bytes;
+    L.stage = o; o += 2 * stage_bytes;                   // two staging buffers
+    L.total = o;
+    return L;
+}
+struct SplitArgs {
+    int nwc;   // compute waves (the first nwc * 64 lanes); the rest of the workgroup stages
+    int nph;   // row phases of the compute lanes (nph * win_w / 4 <= nwc * 64)
+    int rpl;   // output rows per compute lane per tile: rows_per_tile = nph * rpl
+    int win_w; // the launch's common window width (a multiple of 4)
+};
+
 // ---- record_kernels.hip: contrast records in one launch (the post-hue record in registers) ------
 constexpr int kRecPhasesMax = 32;                  // row phases (lanes per column group), at most
 constexpr int kRecRows   = 14;                     // rows per lane held in registers (win_h <= 224)

@@ -554,6 +554,9 @@ __global__ __launch_bounds__(256) void resize_sep(const ResizeJob* __restrict__ 
     const int nb = nx * cn, e0 = tid * 4;
     const int gpr = (nx + 3) >> 2, lc = tid / gpr, px0 = (tid - lc * gpr) * 4;
     const bool planar = J.final_out != 0;
+    // (the host sizes bands so that every element has a lane; a band that outgrew the workgroup would
+    // leave outputs unwritten: reported, never silent)
+    if (tid == 0 && (planar ? cn * gpr : (nb + 3) >> 2) > nt) atomicOr(error, 512);
     if (planar ? lc >= cn : e0 >= nb) return; // (no barrier below; the LUT was published by the staging barrier)
     int px[4], ch[4], xe[4]; // pixel in the tile, channel, element of the full destination row
 #pragma unroll

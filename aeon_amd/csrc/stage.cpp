@@ -12,9 +12,6 @@
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
-#include <csetjmp>
-#include <csignal>
-#include <signal.h>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -46,6 +43,9 @@ hipError_t launch_upload_table(const void* host_dev, void* dst, size_t bytes, hi
 hipError_t launch_contrast_records(bool fast, bool split, const LaunchArgs& a, const RecArgs& r, int grid, hipStream_t stream,
                                    hipEvent_t start, hipEvent_t stop);
 hipError_t contrast_records_lds_limit(int bytes);
+hipError_t launch_split(bool tail, const LaunchArgs& a, const SplitArgs& s, int grid, hipStream_t stream, hipEvent_t start,
+                        hipEvent_t stop);
+hipError_t split_lds_limit(int bytes);
 hipError_t launch_resize_generic(const ResizeJob* jobs, const uint8_t* table, int n_jobs, int max_tiles, int TR, int CW,
                                  int NR, int xs, int amax, int cn_max, int SW, const float* lut, int bgr, int chm,
                                  int32_t* error, hipStream_t stream);
@@ -87,7 +87,8 @@ std::string device_error_text(int err)
                 {32, "dynamic-tail counter left over by an earlier launch"},
                 {64, "rotation source box exceeds the launch's LDS"},
                 {128, "generic resize footprint exceeds the launch's LDS"},
-                {256, "JPEG entropy-coded data corrupt or truncated (GPU Huffman decoder)"}};
+                {256, "JPEG entropy-coded data corrupt or truncated (GPU Huffman decoder)"},
+                {512, "separable resize band wider than its workgroup"}};
     std::string s;
     for (const auto& b : bits)
         if (err & b.bit) s += (s.empty() ? "" : "; ") + std::string(b.what);
@@ -525,7 +526,9 @@ struct GrPlan {
         for (int i = f; i < f + n; i++) one = one && jobs[i].method == jobs[f].method && jobs[i].cn == u.cn_max;
         if (one) {
             static const int tr0 = std::getenv("AEON_HIP_SEP_TR") ? std::atoi(std::getenv("AEON_HIP_SEP_TR")) : 16;
-            int cw = std::min(ww, 1024 / u.cn_max), tr = std::max(4, std::min(64, tr0));
+            // a band's lanes (at most 256): 4 bytes of a u8 window row each, or 4 pixels of one channel of a
+            // final_out job each -- cn * ceil(cw / 4) lanes, so 340 columns for 3 channels, not 341
+            int cw = std::min({ww, 1024 / u.cn_max, 4 * (256 / u.cn_max)}), tr = std::max(4, std::min(64, tr0));
             // staged rows: whole 16-byte blocks (resize_sep), hence up to 30 bytes more per row
             auto sw = [&] { return (bytes_for(f, n, cw) + 30 + 15) / 16 * 16; };
             auto l  = [&] {
@@ -806,7 +809,12 @@ struct KernelTimer {
 
 struct aeon_hip_ctx {
     int        device = 0;
-    int32_t*   d_error = nullptr;
+    int32_t*   d_error = nullptr; // kErrWords device error words: [0] the null stream's (and overflow),
+                                  // [i] the i-th stream's (stream_error)
+    static constexpr int kErrWords = 64;
+    hipStream_t err_stream[kErrWords] = {};
+    std::mutex  err_mu;
+    int32_t*    call_error = nullptr; // the word of the call in progress (run_batch, under mu)
     uint32_t*  d_tail  = nullptr; // per ring slot: dynamic-tail tile counters (zero between launches)
     int32_t*   d_hsv   = nullptr;
     // staging ring: a slot (job table, scratch) is reused only after the kernels that read it
@@ -823,6 +831,9 @@ struct aeon_hip_ctx {
     bool                 records = true; // AEON_HIP_RECORDS=0: contrast calls through the two-launch path
     int                  rec_helpers = 2; // AEON_HIP_REC_HELPERS: staging-only waves of the record kernel
     int                  rec_phases  = 0; // AEON_HIP_REC_PHASES (development): row phases of the record kernel
+    bool                 split = true;      // AEON_HIP_SPLIT=0: direct non-photometric calls through augment_tiles
+    int                  split_helpers = 2; // AEON_HIP_SPLIT_HELPERS: staging waves of augment_split
+    int                  split_rpl = 2;     // AEON_HIP_SPLIT_RPL: output rows per compute lane per tile
     bool                 fuse_masks = false; // AEON_HIP_FUSE_MASKS=1: a pair call's masks inside the image launch
     bool                 vram_jobs = false; // job tables written by the host into device memory (large-BAR GPUs;
                                             // AEON_HIP_VRAM_JOBS=0: pinned host tables)
@@ -893,34 +904,36 @@ void close_slots(aeon_hip_ctx* ctx);
 // Device memory the host writes directly (a large-BAR GPU maps all of it): uncached, so every GPU read
 // of it -- a kernel's job fetch -- goes to HBM and never meets a stale cache line of the slot's
 // previous call.
-// One guarded host write + read-back through p: false when it faults (SIGSEGV / SIGBUS, caught for the
-// duration of the probe only, the previous handlers restored) or reads back something else.
-thread_local sigjmp_buf* t_probe_jmp = nullptr;
-void probe_fault(int sig, siginfo_t*, void*)
+// The host may write through p when the page holding it is mapped read-write into this process (on a
+// large-BAR GPU the driver maps host-visible VRAM at the allocation's own address; a restricted or
+// virtualised BAR can allocate device memory without mapping it for the CPU, and the runtime reports no
+// host pointer for device memory either way).  Checked in /proc/self/maps -- no signal handlers, nothing
+// process-wide touched, safe next to other threads -- then one write + read-back through p.
+bool host_mapped_rw(const void* p, size_t bytes)
 {
-    if (t_probe_jmp) siglongjmp(*t_probe_jmp, 1);
-    std::signal(sig, SIG_DFL); // another thread's fault inside the probe window: the default action
+    std::FILE* f = std::fopen("/proc/self/maps", "r");
+    if (!f) return false;
+    const unsigned long a  = (unsigned long)(uintptr_t)p;
+    bool                ok = false;
+    char                line[512];
+    while (std::fgets(line, sizeof line, f)) {
+        unsigned long lo = 0, hi = 0;
+        char          perms[8] = {0};
+        if (std::sscanf(line, "%lx-%lx %7s", &lo, &hi, perms) != 3) continue;
+        if (a >= lo && a < hi) {
+            ok = a + bytes <= hi && perms[0] == 'r' && perms[1] == 'w';
+            break;
+        }
+    }
+    std::fclose(f);
+    return ok;
 }
 bool host_can_write(void* p)
 {
-    struct sigaction sa{}, old_segv{}, old_bus{};
-    sa.sa_sigaction = probe_fault;
-    sa.sa_flags     = SA_SIGINFO;
-    sigemptyset(&sa.sa_mask);
-    sigaction(SIGSEGV, &sa, &old_segv);
-    sigaction(SIGBUS, &sa, &old_bus);
-    sigjmp_buf jb;
-    volatile bool ok = false;
-    t_probe_jmp = &jb;
-    if (sigsetjmp(jb, 1) == 0) {
-        volatile uint32_t* q = (volatile uint32_t*)p;
-        q[0]                 = 0xA5C3E1F7u;
-        ok                   = q[0] == 0xA5C3E1F7u;
-    }
-    t_probe_jmp = nullptr;
-    sigaction(SIGSEGV, &old_segv, nullptr);
-    sigaction(SIGBUS, &old_bus, nullptr);
-    return ok;
+    if (!host_mapped_rw(p, sizeof(uint32_t))) return false;
+    volatile uint32_t* q = (volatile uint32_t*)p;
+    q[0]                 = 0xA5C3E1F7u;
+    return q[0] == 0xA5C3E1F7u;
 }
 
 // The uncached HBM tables are never handed back to the driver: a context's tables go into a process-wide
@@ -968,11 +981,13 @@ bool grow_vram(int device, uint8_t*& p, size_t& cap, size_t need) // false: no t
         p = nullptr;
         return false;
     }
-    // the host writes these tables through p itself: only when a guarded probe write + read-back
-    // through p works (a restricted BAR or a virtualised GPU can allocate it without mapping it for the
+    // the host writes these tables through p itself: only when p's page is mapped read-write for the
+    // host and a write + read-back through p works (a restricted BAR or a virtualised GPU can allocate it without mapping it for the
     // CPU; the runtime reports no host pointer for device memory either way) -- the pinned paths then
     if (!host_can_write(p)) {
         (void)hipGetLastError();
+        if (std::getenv("AEON_HIP_HOST_PROFILE"))
+            std::fprintf(stderr, "[aeon_hip] uncached HBM block not host-writable: pinned job tables\n");
         std::lock_guard<std::mutex> lock(g_vram_pool_mu);
         g_vram_unused.push_back(p); // (not freed either: see above)
         p = nullptr;
@@ -1203,6 +1218,27 @@ OutView out_view(const aeon_out_desc& o)
     return v;
 }
 
+// The device error word of the calls on `stream`: each stream its own (so that aeon_hip_synchronize of
+// one stream -- a decode window -- never reads or clears a bit another stream's kernels set meanwhile),
+// the null stream and streams beyond the table's size share word 0.  A stream keeps its word until
+// aeon_hip_synchronize has read it.
+int32_t* stream_error(aeon_hip_ctx* ctx, hipStream_t stream, bool release = false)
+{
+    if (!stream) return ctx->d_error;
+    std::lock_guard<std::mutex> lock(ctx->err_mu);
+    int free_i = 0;
+    for (int i = 1; i < aeon_hip_ctx::kErrWords; i++) {
+        if (ctx->err_stream[i] == stream) {
+            if (release) ctx->err_stream[i] = nullptr;
+            return ctx->d_error + i;
+        }
+        if (!free_i && !ctx->err_stream[i]) free_i = i;
+    }
+    if (release || !free_i) return ctx->d_error;
+    ctx->err_stream[free_i] = stream;
+    return ctx->d_error + free_i;
+}
+
 LaunchArgs launch_args(aeon_hip_ctx* ctx, const Slot& s, const uint8_t* table, const LaunchPlan& L, int n_jobs,
                        const aeon_out_desc& o, const float* d_lut, int partial_stride, bool u8_map = false)
 {
@@ -1223,7 +1259,7 @@ LaunchArgs launch_args(aeon_hip_ctx* ctx, const Slot& s, const uint8_t* table, c
     a.partials       = s.partials;
     a.shifts         = s.shifts;
     a.partial_stride = partial_stride;
-    a.error          = ctx->d_error;
+    a.error          = ctx->call_error;
 #ifdef AEON_HIP_TRACE
     a.trace = ctx->trace; // development builds only (tools/build_variants.sh trace)
 #endif
@@ -1248,6 +1284,44 @@ LaunchArgs launch_args(aeon_hip_ctx* ctx, const Slot& s, const uint8_t* table, c
     a.threads       = L.threads;
     a.has_rtab      = L.rtab;
     return a;
+}
+
+// augment_split's shape for a direct call's records (all 3-channel, INTER_LINEAR, one window width W,
+// W % 4 == 0): nwc compute waves of nph row phases x W/4 column groups plus ctx->split_helpers staging
+// waves in one workgroup of <= 1,024 lanes, rows_per_tile = nph * rpl, two staging buffers.  The LDS
+// request is held above half a CU's 160 KB so that the grid's n_cu workgroups land one per CU.  False:
+// no such shape (the caller keeps augment_tiles).
+bool plan_split(const aeon_hip_ctx* ctx, const std::vector<JobGeom>& geo, LaunchPlan& P, SplitArgs& sa)
+{
+    if (geo.empty()) return false;
+    const int W = geo[0].win_w;
+    if (W <= 0 || (W & 3) != 0) return false;
+    for (const JobGeom& g : geo)
+        if (g.cn != 3 || g.win_w != W || g.mode != RESIZE_LINEAR) return false;
+    const int gpr = W / 4, nh = ctx->split_helpers;
+    int       nph = 0, nwc = 0;
+    for (int p = 32; p >= 1; p--) {
+        const int w = (p * gpr + 63) / 64;
+        if (w + nh <= 16) {
+            nph = p, nwc = w;
+            break;
+        }
+    }
+    if (nph == 0) return false;
+    const int rpl = std::max(1, std::min(ctx->split_rpl, kSplitTRMax / nph));
+    const int tr  = nph * rpl;
+    long      by  = 0;
+    for (const JobGeom& g : geo) by = std::max(by, stage_bytes_for(3, stage_rows_for(g, tr), stage_cols(g)));
+    by             = (by + 1023) / 1024 * 1024;
+    const int lds  = split_lds_layout(W, (int)by).total;
+    if (lds > kMaxLds) return false;
+    P.tr          = tr;
+    P.stage_bytes = (int)by;
+    P.max_win_w   = W;
+    P.threads     = (nwc + nh) * 64;
+    P.lds         = std::max(lds, kMaxLds / 2 + 1024);
+    sa.nwc = nwc, sa.nph = nph, sa.rpl = rpl, sa.win_w = W;
+    return true;
 }
 
 // Direct call (the common case: C2, C5's image, every record transformed straight from its source in
@@ -1301,6 +1375,11 @@ bool run_direct(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void
     P.vec_ok = vec_ok;
     P.rtab   = P.photo && o.dtype == AEON_DTYPE_F32;
     P.shape(geo);
+    // non-photometric INTER_LINEAR into float32 CHW planes, one window width: augment_split (staging on
+    // helper waves, split_kernels.hip)
+    SplitArgs  sa{};
+    const bool split = ctx->split && !P.photo && P.rm == RESIZE_LINEAR && o.dtype == AEON_DTYPE_F32 && o.channel_major &&
+                       vec_ok && !ov.u8_map && !o.fixed_aspect_ratio && plan_split(ctx, geo, P, sa);
     P.max_tiles = (max_h + P.tr - 1) / P.tr;
     // every tile reads its job over PCIe: past ~512 KB of such reads per launch the multi-pass path's
     // device table wins (C5's image launch, 4,096 tiles of 256 B: 98 vs 90 us of kernels per step;
@@ -1354,7 +1433,16 @@ bool run_direct(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void
     a.job_stride      = (int)stride;
     a.jobs_host       = 1; // (read-through loads: pinned host memory, or the uncached HBM copy)
     // (the algorithmic bytes only for a timed launch: a pass over the records the call does not need)
-    timed_launch(ctx, KM_FINAL, P, a, stream, timed ? launch_bytes(geo, KM_FINAL, out_elem_bytes(o.dtype)) : 0, timed);
+    const double lbytes = timed ? launch_bytes(geo, KM_FINAL, out_elem_bytes(o.dtype)) : 0;
+    if (split) {
+        KernelTimer t{};
+        if (timed) t = take_timer(ctx, KM_FINAL, lbytes);
+        const int grid = std::min(a.total_tiles, ctx->n_cu); // one workgroup per CU (the LDS request holds it)
+        HIP_OK(launch_split(P.tail, a, sa, grid, stream, timed ? t.start : nullptr, timed ? t.stop : nullptr));
+        if (timed) ctx->timers.push_back(t);
+    } else {
+        timed_launch(ctx, KM_FINAL, P, a, stream, lbytes, timed);
+    }
     phase(6);
     release_slot(ctx, slot, stream);
     phase(7);
@@ -1430,7 +1518,7 @@ bool run_records(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const voi
     a.job_bytes   = (int)sizeof(AugJob);
     a.lut         = d_lut;
     a.hsv_tables  = ctx->d_hsv;
-    a.error       = ctx->d_error;
+    a.error       = ctx->call_error;
     a.stage_bytes = (int)stage;
     a.max_win_w   = W;
     a.out_dtype   = AEON_DTYPE_F32;
@@ -1497,6 +1585,7 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
     hipStream_t stream = (hipStream_t)stream_;
 
     std::lock_guard<std::mutex> lock(ctx->mu);
+    ctx->call_error = stream_error(ctx, stream);
     using clk = std::chrono::steady_clock;
     auto t_prev = clk::now();
     auto phase  = [&](int k) {
@@ -1710,7 +1799,7 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
         HIP_OK(hipMemset2DAsync(out_dev, o.item_stride, 0,
                                 (size_t)o.canvas_w * o.canvas_h * o.channels * out_elem_bytes(od.dtype), n, stream));
     if (!rot.empty()) // image::rotate pre-pass first: the gather and tile passes read its output
-        HIP_OK(launch_rotate((const RotJob*)(table + rot_off), (int)rot.size(), rot_max_tiles, rot_words, rot_cn, ctx->d_error,
+        HIP_OK(launch_rotate((const RotJob*)(table + rot_off), (int)rot.size(), rot_max_tiles, rot_words, rot_cn, ctx->call_error,
                              stream));
     if (!exp.empty()) // then image::expand (etl_image.cpp:155-159)
         HIP_OK(launch_expand((const ExpandJob*)(table + exp_off), (int)exp.size(), exp_max_px, stream));
@@ -1759,10 +1848,10 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
             const float*     glut = u.any_final ? d_lut : nullptr;
             if (u.sep)
                 HIP_OK(launch_resize_sep(u.sep, gj, table, u.count, u.max_tiles, u.TR, u.CW, u.NR, u.SW, u.cn_max, glut, gbgr,
-                                         gchm, ctx->d_error, stream));
+                                         gchm, ctx->call_error, stream));
             else
                 HIP_OK(launch_resize_generic(gj, table, u.count, u.max_tiles, u.TR, u.CW, u.NR, u.xs, u.amax, u.cn_max, u.SW,
-                                             glut, gbgr, gchm, ctx->d_error, stream));
+                                             glut, gbgr, gchm, ctx->call_error, stream));
         }
         if (timed) {
             HIP_OK(hipEventRecord(t.stop, stream));
@@ -1851,8 +1940,9 @@ int aeon_hip_ctx_create(int device, aeon_hip_ctx** out)
             HIP_OK(hipSetDevice(device));
             HIP_OK(set_kernel_lds_limit(kMaxLds));
             HIP_OK(contrast_records_lds_limit(kMaxLds));
-            HIP_OK(hipMalloc((void**)&c->d_error, sizeof(int32_t)));
-            HIP_OK(hipMemset(c->d_error, 0, sizeof(int32_t)));
+            HIP_OK(split_lds_limit(kMaxLds));
+            HIP_OK(hipMalloc((void**)&c->d_error, sizeof(int32_t) * aeon_hip_ctx::kErrWords));
+            HIP_OK(hipMemset(c->d_error, 0, sizeof(int32_t) * aeon_hip_ctx::kErrWords));
             // per slot: the dynamic-tail counter, then (kSlots on) the mask-block counter of pair calls
             HIP_OK(hipMalloc((void**)&c->d_tail, 2 * aeon_hip_ctx::kSlots * sizeof(uint32_t)));
             HIP_OK(hipMemset(c->d_tail, 0, 2 * aeon_hip_ctx::kSlots * sizeof(uint32_t)));
@@ -1910,6 +2000,9 @@ int aeon_hip_ctx_create(int device, aeon_hip_ctx** out)
             if (const char* e = std::getenv("AEON_HIP_RECORDS")) c->records = std::atoi(e) != 0;
             if (const char* e = std::getenv("AEON_HIP_REC_HELPERS")) c->rec_helpers = std::max(0, std::min(4, std::atoi(e)));
             if (const char* e = std::getenv("AEON_HIP_REC_PHASES")) c->rec_phases = std::atoi(e);
+            if (const char* e = std::getenv("AEON_HIP_SPLIT")) c->split = std::atoi(e) != 0;
+            if (const char* e = std::getenv("AEON_HIP_SPLIT_HELPERS")) c->split_helpers = std::max(1, std::min(4, std::atoi(e)));
+            if (const char* e = std::getenv("AEON_HIP_SPLIT_RPL")) c->split_rpl = std::max(1, std::min(4, std::atoi(e)));
             if (const char* e = std::getenv("AEON_HIP_JPEG_HUFF")) c->jpeg_gpu_huff = std::strcmp(e, "host") != 0;
             if (const char* e = std::getenv("AEON_HIP_FUSE_MASKS")) c->fuse_masks = std::atoi(e) != 0;
 #ifdef AEON_HIP_TRACE
@@ -2070,10 +2163,15 @@ int aeon_hip_synchronize(aeon_hip_ctx* ctx, void* stream)
         if (const int rc = aeon_hip_release_stream(ctx, stream)) return rc;
         HIP_OK(hipSetDevice(ctx->device));
         HIP_OK(hipStreamSynchronize((hipStream_t)stream));
-        int32_t err = 0;
-        HIP_OK(hipMemcpy(&err, ctx->d_error, sizeof(err), hipMemcpyDeviceToHost));
+        // this stream's word (its calls' kernels are done): read and cleared on the stream itself, the
+        // word then handed back (a stream that is reused gets a word again at its next call)
+        int32_t* word = stream_error(ctx, (hipStream_t)stream);
+        int32_t  err  = 0;
+        HIP_OK(hipMemcpyAsync(&err, word, sizeof(err), hipMemcpyDeviceToHost, (hipStream_t)stream));
+        if (err != 0) HIP_OK(hipMemsetAsync(word, 0, sizeof(int32_t), (hipStream_t)stream));
+        HIP_OK(hipStreamSynchronize((hipStream_t)stream));
+        (void)stream_error(ctx, (hipStream_t)stream, true);
         if (err != 0) {
-            HIP_OK(hipMemset(ctx->d_error, 0, sizeof(int32_t)));
             fail(AEON_HIP_EDEVICE, "device error word " + std::to_string(err) + " (" + device_error_text(err) + ")");
         }
         return 0;
@@ -2266,7 +2364,7 @@ int aeon_hip_decode_jpeg_batch(aeon_hip_ctx* ctx, int n, const void* const* data
                 t = take_timer(ctx, kTimerJpeg, px);
             }
         }
-        jpeg_decode_batch(ctx->jpeg, n, data, sizes, descs, dst_base, ctx->d_error, (hipStream_t)stream,
+        jpeg_decode_batch(ctx->jpeg, n, data, sizes, descs, dst_base, stream_error(ctx, (hipStream_t)stream), (hipStream_t)stream,
                           timed ? t.start : nullptr,
                           timed ? t.stop : nullptr);
         if (timed) {

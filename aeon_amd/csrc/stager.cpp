@@ -29,6 +29,7 @@
 #include <mutex>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -126,6 +127,7 @@ struct aeon_hip_stager {
     int           cur = 0; // the window stages go to
     uint64_t      gens = 0;
     std::vector<hipEvent_t> spare_events;
+    std::atomic<int>        waiters{0}; // aeon_hip_stager_wait(NULL, ...) calls inside this stager (destroy waits)
 };
 
 namespace {
@@ -133,8 +135,14 @@ namespace {
 // Batch buffers of launched windows -> their stager, for aeon_hip_stager_wait(NULL, buffer) (the
 // consumer, batch_iterator_fbm::filler, knows the buffers but not the providers).  Lock order: a
 // stager's mu may be held when g_reg_mu is taken, never the reverse.
-std::mutex                                   g_reg_mu;
-std::unordered_map<void*, aeon_hip_stager*> g_pending;
+// An entry is (stager, window generation): a buffer address that appears in both windows keeps the
+// newer window's entry, and retiring the older window erases only its own.
+struct Pending {
+    aeon_hip_stager* s;
+    uint64_t         gen;
+};
+std::mutex                        g_reg_mu;
+std::unordered_map<void*, Pending> g_pending;
 
 template <typename F>
 int stager_guarded(F&& f)
@@ -169,7 +177,7 @@ void reset_window(aeon_hip_stager* s, Window& w)
         std::lock_guard<std::mutex> r(g_reg_mu);
         for (auto& b : w.batches) {
             auto it = g_pending.find(b->out);
-            if (it != g_pending.end() && it->second == s) g_pending.erase(it);
+            if (it != g_pending.end() && it->second.s == s && it->second.gen == w.gen) g_pending.erase(it);
         }
     }
     for (auto& b : w.batches)
@@ -304,7 +312,7 @@ void launch_window(aeon_hip_stager* s, Window& w)
     w.gen      = ++s->gens;
     w.unwaited = (int)w.batches.size();
     std::lock_guard<std::mutex> r(g_reg_mu);
-    for (auto& b : w.batches) g_pending[b->out] = s;
+    for (auto& b : w.batches) g_pending[b->out] = Pending{s, w.gen};
 }
 
 // Launch the staging window if batch_out belongs to it (the first post_process of a window); mark
@@ -408,6 +416,14 @@ int aeon_hip_stager_create(aeon_hip_ctx* ctx, int kind, const aeon_out_desc* out
 int aeon_hip_stager_destroy(aeon_hip_stager* s)
 {
     if (!s) return 0;
+    {
+        // no new consumer wait can find this stager once its buffers are unregistered; the ones already
+        // inside it finish first
+        std::lock_guard<std::mutex> r(g_reg_mu);
+        for (auto it = g_pending.begin(); it != g_pending.end();)
+            it = it->second.s == s ? g_pending.erase(it) : std::next(it);
+    }
+    while (s->waiters.load(std::memory_order_acquire) != 0) std::this_thread::yield();
     (void)hipSetDevice(s->device);
     {
         std::lock_guard<std::mutex> l(s->mu);
@@ -488,10 +504,22 @@ int aeon_hip_stager_wait(aeon_hip_stager* s, void* batch_out)
     return stager_guarded([&] {
         if (!batch_out) fail(AEON_HIP_EINVAL, "null argument");
         if (!s) { // the consumer's form: whichever stager launched this buffer, if any
-            std::lock_guard<std::mutex> r(g_reg_mu);
-            auto it = g_pending.find(batch_out);
-            if (it == g_pending.end()) return;
-            s = it->second;
+            {
+                // the stager is pinned (waiters) under the registry lock, which its destroy takes to
+                // unregister: it cannot go away between the lookup and the wait
+                std::lock_guard<std::mutex> r(g_reg_mu);
+                auto it = g_pending.find(batch_out);
+                if (it == g_pending.end()) return;
+                s = it->second.s;
+                s->waiters.fetch_add(1, std::memory_order_acq_rel);
+            }
+            struct Unpin {
+                aeon_hip_stager* s;
+                ~Unpin() { s->waiters.fetch_sub(1, std::memory_order_acq_rel); }
+            } unpin{s};
+            bool found = false;
+            wait_batch(s, batch_out, found);
+            return;
         }
         bool found = false;
         wait_batch(s, batch_out, found);

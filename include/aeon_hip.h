@@ -191,8 +191,9 @@ int aeon_jpeg_host_stage(const void* data, size_t size, int* gpu_entropy, int64_
 int aeon_hip_decode_jpeg_batch(aeon_hip_ctx* ctx, int n, const void* const* data, const size_t* sizes,
                                const aeon_img_desc* descs, void* dst_base, void* stream);
 
-/* Wait for `stream` and check the device error word of ctx: AEON_HIP_EDEVICE (the word cleared) when a
- * kernel flagged an inconsistency -- an LDS footprint the host sized too small, a dynamic-tail counter
+/* Wait for `stream` and check the device error word of the calls made on it (each stream has its own
+ * word, so a window's check never reads or clears what another stream's kernels set):
+ * AEON_HIP_EDEVICE (the word cleared) when a kernel flagged an inconsistency -- an LDS footprint the host sized too small, a dynamic-tail counter
  * not reset by an earlier launch, a rotation source box over its LDS.  None is expected. */
 int aeon_hip_synchronize(aeon_hip_ctx* ctx, void* stream);
 

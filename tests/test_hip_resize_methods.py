@@ -71,6 +71,10 @@ CASES = [
     ("resize_short_then_resize", (500, 375), dict(crop_x=20, crop_y=4, crop_w=300, crop_h=250, out_w=160,
                                                   out_h=128, resize_short_size=300, flip=1), U8_HWC),
     ("rotated", (300, 240), dict(crop_x=20, crop_y=10, crop_w=250, crop_h=200, out_w=160, out_h=120, angle=30), F32),
+    # f32 outputs of 341+ columns near 1:1: a 3-channel final_out band needs 3 * ceil(cw / 4) lanes, so
+    # its column band must stop at 340 (round-5 advisor: columns 336-340 of channel 2 went unwritten)
+    ("wide_f32_384", (400, 300), dict(crop_x=5, crop_y=3, crop_w=390, crop_h=160, out_w=384, out_h=40, flip=1), F32),
+    ("wide_f32_512", (520, 200), dict(crop_x=2, crop_y=1, crop_w=515, crop_h=64, out_w=512, out_h=64), F32),
 ]
 
 

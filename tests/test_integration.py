@@ -34,7 +34,9 @@ pytestmark = pytest.mark.gpu
 
 class Buffer:
     """One buffer_fixed_size_elements of a batch (src/buffer_batch.hpp:154-188): pageable numpy,
-    pinned host (aeon's "pinned" loader option) or device memory."""
+    pinned host (aeon's "pinned" loader option: buffer_fixed_size_elements::allocate's HAS_GPU branch,
+    src/buffer_batch.cpp:150-186, as INTEGRATION.md edit 5 rewrites it -- aeon_hip_host_alloc /
+    aeon_hip_host_free) or device memory."""
 
     def __init__(self, nbytes, where):
         import torch
@@ -377,3 +379,21 @@ def test_stager_launch_wait_errors():
     finally:
         st.close()
         ctx.close()
+
+
+def test_aeon_path_cpp_native_sequence():
+    """tools/aeon_path_cpp.cpp (INTEGRATION.md edits 1-5 in C++ against the C ABI alone): a short run of
+    each form -- pinned (edit 5: zero-copy stores) and pageable batch buffers, launch-only post_process with
+    the consumer's waits, and flushing post_process -- completes and reports its rate.  (Its outputs are the
+    stager's, which the tests above check bit for bit through the same entry points.)"""
+    import json
+    import os
+    import subprocess
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "aeon_amd", "aeon_path_cpp")
+    assert os.path.exists(exe), "aeon_amd/aeon_path_cpp not built (make -C aeon_amd/csrc)"
+    for buffers in ("pinned", "pageable"):
+        for mode in ("overlap", "flush"):
+            r = subprocess.run([exe, "C2", buffers, mode, "2", "1"], capture_output=True, text=True, timeout=120)
+            assert r.returncode == 0, r.stderr
+            line = json.loads(r.stdout.strip().splitlines()[-1])
+            assert line["buffers"] == buffers and line["value"] > 0, line
