@@ -186,6 +186,7 @@ def lib():
                                                P(ctypes.c_int64), P(ctypes.c_int64)]
         L.aeon_hip_last_error.restype = ctypes.c_char_p
         L.aeon_hip_version.restype = ctypes.c_char_p
+        L.aeon_hip_debug_uncached_blocks.argtypes = [P(ctypes.c_uint64), ctypes.c_int, P(ctypes.c_int)]
         _lib = L
     return _lib
 
@@ -194,6 +195,16 @@ def _check(rc):
     if rc != 0:
         raise AeonHipError(rc, lib().aeon_hip_last_error().decode())
     return rc
+
+
+def uncached_blocks():
+    """[(lo, hi)] device address ranges of every uncached job-table block of this process (diagnostics:
+    aeon_hip_debug_uncached_blocks)."""
+    n = ctypes.c_int()
+    _check(lib().aeon_hip_debug_uncached_blocks(None, 0, ctypes.byref(n)))
+    buf = (ctypes.c_uint64 * (2 * max(n.value, 1)))()
+    _check(lib().aeon_hip_debug_uncached_blocks(buf, n.value, ctypes.byref(n)))
+    return [(buf[2 * i], buf[2 * i + 1]) for i in range(n.value)]
 
 
 def exported_symbols():

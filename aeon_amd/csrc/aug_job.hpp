@@ -240,24 +240,29 @@ AEON_HD inline LdsLayout lds_layout(int max_win_w, int rows_per_tile, int stage_
 
 // ---- split_kernels.hip: the single-pass tile kernel with staging helper waves ----------------------
 // LDS carve of augment_split (bytes, 16-aligned regions): the LUT at offset 0 (lut_at), then per
-// staging buffer b its column taps, row taps and tile info, a ring of three jobs, two staging buffers.
+// staging buffer b its column taps, row taps and tile info, a ring of jobs, the staging buffers.  Three
+// buffers: the compute waves work on tile k while tile k + 1 is unpacked and tile k + 2's loads are in
+// flight (a tile's LDS-DMA then has a whole tile's time to land).
+constexpr int kSplitBufs   = 3;  // staging buffers
+constexpr int kSplitTRMax  = 64; // output rows per tile, at most (row-tap table size)
+constexpr int kSplitJobs   = 6;  // job ring slots: tiles k (compute), k + 1 (unpack), k + 2 (issue), k + 3 (geometry),
+                                 // k + 4 (landed), k + 5 (fetched)
+constexpr int kSplitGeo    = 4;  // tile geometry slots: tiles k, k + 1, k + 2, k + 3
 struct SplitLds {
     int lut, xt, yt, job, info, stage, stage_bytes, xt_bytes, total;
 };
-constexpr int kSplitTRMax  = 64; // output rows per tile, at most (row-tap table size)
-constexpr int kSplitJobs   = 3;  // job ring slots
 AEON_HD inline SplitLds split_lds_layout(int win_w, int stage_bytes)
 {
     SplitLds L;
     int      o = 0;
     L.lut = o; o += 3 * 256 * 4;                         // standardize LUT (source channel order)
     L.xt_bytes = ((win_w * 8 + 15) / 16) * 16;
-    L.xt  = o; o += 2 * L.xt_bytes;                      // column taps + weights, per buffer
-    L.yt  = o; o += 2 * kSplitTRMax * 16;                // row taps + weights, per buffer
-    L.job = o; o += kSplitJobs * (int)sizeof(AugJob);    // the jobs of three consecutive tiles
-    L.info = o; o += 2 * 64;                             // per buffer: its tile (ok, job slot, y0, rows)
+    L.xt  = o; o += kSplitBufs * L.xt_bytes;             // column taps + weights, per buffer
+    L.yt  = o; o += kSplitBufs * kSplitTRMax * 16;       // row taps + weights, per buffer
+    L.job = o; o += kSplitJobs * (int)sizeof(AugJob);    // the jobs of six consecutive tiles
+    L.info = o; o += kSplitGeo * 64;                     // per tile of the ring: its geometry (split_kernels.hip)
     L.stage_bytes = stage_bytes;
-    L.stage = o; o += 2 * stage_bytes;                   // two staging buffers
+    L.stage = o; o += kSplitBufs * stage_bytes;          // the staging buffers
     L.total = o;
     return L;
 }
@@ -266,6 +271,7 @@ struct SplitArgs {
     int nph;   // row phases of the compute lanes (nph * win_w / 4 <= nwc * 64)
     int rpl;   // output rows per compute lane per tile: rows_per_tile = nph * rpl
     int win_w; // the launch's common window width (a multiple of 4)
+    int occ;   // workgroups per CU (1 or 2: the kernel's register budget; host only)
 };
 
 // ---- record_kernels.hip: contrast records in one launch (the post-hue record in registers) ------

@@ -76,6 +76,34 @@ __device__ __forceinline__ T job_get(const JobRef& J, int off)
         return __builtin_bit_cast(T, (uint32_t)__builtin_amdgcn_readfirstlane(lds_ld(J.lds + off)));
     }
 }
+// The hot half of a job (kJobHotBytes: every field a non-photometric tile reads) loaded from its LDS
+// copy at once -- eight 16-byte LDS reads, one wait -- into scalar registers: JF on it is a register
+// read, where JF on a JobRef is an LDS round trip per field (each one waited for before the next; in
+// augment_split's per-tile staging those waits were most of its 1.8 us).
+struct JobS {
+    uint32_t w[kJobHotBytes / 4];
+};
+__device__ __forceinline__ JobS job_load(int lds)
+{
+    u32x4 v[kJobHotBytes / 16];
+#pragma unroll
+    for (int i = 0; i < kJobHotBytes / 16; i++) v[i] = *lds_ptr<const u32x4>(lds + 16 * i);
+    JobS J;
+#pragma unroll
+    for (int i = 0; i < kJobHotBytes / 16; i++)
+#pragma unroll
+        for (int k = 0; k < 4; k++) J.w[4 * i + k] = __builtin_amdgcn_readfirstlane(v[i][k]);
+    return J;
+}
+template <typename T>
+__device__ __forceinline__ T job_get(const JobS& J, int off)
+{
+    if constexpr (sizeof(T) == 8) {
+        return __builtin_bit_cast(T, (uint64_t)J.w[off >> 2] | ((uint64_t)J.w[(off >> 2) + 1] << 32));
+    } else {
+        return __builtin_bit_cast(T, J.w[off >> 2]);
+    }
+}
 #define JF(J, field) job_get<decltype(AugJob::field)>(J, (int)__builtin_offsetof(AugJob, field))
 #define JFA(J, field, i)                                                                                     \
     job_get<__remove_extent(decltype(AugJob::field))>(J, (int)__builtin_offsetof(AugJob, field) +           \
@@ -413,17 +441,20 @@ __device__ __forceinline__ int stage_need(const StageGeom& G, int cn)
 
 // byte offset in the source buffer of staged pixel (row j, column u); negative above/left of a
 // padded crop
-__device__ __forceinline__ int src_off(const JobRef& J, const StageGeom& G, int j, int u)
+template <typename JR>
+__device__ __forceinline__ int src_off(const JR& J, const StageGeom& G, int j, int u)
 {
     return (JF(J, crop_y) + G.v_lo + JF(J, shift_y) + j) * JF(J, src_stride) + (JF(J, crop_x) + G.u_lo + JF(J, shift_x) + u) * JF(J, cn);
 }
 
 // Units (BGR groups or gray pixels) per staged row.
-__device__ __forceinline__ int stage_units_per_row(const JobRef& J, const StageGeom& G) { return JF(J, cn) == 3 ? G.ng : G.pitch; }
+template <typename JR>
+__device__ __forceinline__ int stage_units_per_row(const JR& J, const StageGeom& G) { return JF(J, cn) == 3 ? G.ng : G.pitch; }
 
 // (1) This wave's share of the tile's LDS-DMA loads: instructions wave, wave + nw, ...; unit q of
 // the tile (row q / upr) lands in slot q.
-__device__ __forceinline__ void stage_issue(const JobRef& J, const StageGeom& G, int buf, int wave, int nw)
+template <typename JR>
+__device__ __forceinline__ void stage_issue(const JR& J, const StageGeom& G, int buf, int wave, int nw)
 {
     const int   lane = threadIdx.x & 63;
     const int   cn   = JF(J, cn);
@@ -454,7 +485,8 @@ __device__ __forceinline__ u32x4 unpack_bgr(u32x4 w) // 12 bytes BGR BGR BGR BGR
     return (u32x4){w.x & 0xffffffu, __builtin_amdgcn_perm(w.y, w.x, 0x0C050403u),
                    __builtin_amdgcn_perm(w.z, w.y, 0x0C040302u), w.z >> 8};
 }
-__device__ __forceinline__ void stage_unpack(const JobRef& J, const StageGeom& G, int buf, int wave, int nw)
+template <typename JR>
+__device__ __forceinline__ void stage_unpack(const JR& J, const StageGeom& G, int buf, int wave, int nw)
 {
     const int  lane      = threadIdx.x & 63;
     const int  cn        = JF(J, cn);
@@ -622,6 +654,32 @@ __device__ __forceinline__ void resize_px(i32x4 ytr, int col, uint32_t wx, int s
         const uint32_t p00 = lds_ld(a0);
 #pragma unroll
         for (int c = 0; c < 3; c++) s[c] = byte_of(p00, c) << (SCALED ? 2 : 0);
+    }
+}
+
+// resize_px<RESIZE_LINEAR, true> for a lane's 4 pixels of a row with all 16 staged words read first: the
+// reads are in flight together (one LDS wait per row instead of one per pixel).
+__device__ __forceinline__ void resize4_linear_scaled(i32x4 ytr, const int (&col)[4], const uint32_t (&wx)[4], int (&s)[4][3])
+{
+    uint32_t p[4][4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const int a0 = ytr.x + col[q], a1 = ytr.y + col[q];
+        p[q][0] = lds_ld(a0), p[q][1] = lds_ld(a0 + 4), p[q][2] = lds_ld(a1), p[q][3] = lds_ld(a1 + 4);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const u16x2 w = __builtin_bit_cast(u16x2, wx[q]);
+#pragma unroll
+        for (int c = 0; c < 3; c++) {
+            const uint32_t sel = (uint32_t)c | (0x0Cu << 8) | ((4u + c) << 16) | (0x0Cu << 24);
+            const uint32_t H0  = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, __builtin_amdgcn_perm(p[q][1], p[q][0], sel)), w, 0u, false);
+            const uint32_t H1  = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, __builtin_amdgcn_perm(p[q][3], p[q][2], sel)), w, 0u, false);
+            const uint32_t t0  = (uint32_t)__mul24((int)(H0 >> 4), ytr.z) + (2u << 16);
+            const uint32_t t1  = (uint32_t)__mul24((int)(H1 >> 4), ytr.w);
+            s[q][c]            = (int)((t0 >> 16) + (t1 >> 16));
+        }
     }
 }
 

@@ -43,9 +43,10 @@ hipError_t launch_upload_table(const void* host_dev, void* dst, size_t bytes, hi
 hipError_t launch_contrast_records(bool fast, bool split, const LaunchArgs& a, const RecArgs& r, int grid, hipStream_t stream,
                                    hipEvent_t start, hipEvent_t stop);
 hipError_t contrast_records_lds_limit(int bytes);
-hipError_t launch_split(bool tail, const LaunchArgs& a, const SplitArgs& s, int grid, hipStream_t stream, hipEvent_t start,
-                        hipEvent_t stop);
+hipError_t launch_split(bool tail, int occ, const LaunchArgs& a, const SplitArgs& s, int grid, hipStream_t stream,
+                        hipEvent_t start, hipEvent_t stop);
 hipError_t split_lds_limit(int bytes);
+hipError_t split_occupancy(bool tail, int occ, const LaunchArgs& a, int* blocks);
 hipError_t launch_resize_generic(const ResizeJob* jobs, const uint8_t* table, int n_jobs, int max_tiles, int TR, int CW,
                                  int NR, int xs, int amax, int cn_max, int SW, const float* lut, int bgr, int chm,
                                  int32_t* error, hipStream_t stream);
@@ -204,12 +205,14 @@ struct LaunchPlan {
     bool                vec_ok = true;
     bool                has_hue = false, has_contrast = false;
     bool                rtab    = false; // final f32 launch with contrast / lighting: per-record LDS table
+    bool                split   = false; // launched as augment_split (shape set by plan_split)
+    SplitArgs           sa{};
 
-    // launch shape for this->jobs, and each job's tile count
+    // launch shape for this->jobs (unless plan_split set it), and each job's tile count
     void finalize()
     {
         if (jobs.empty()) return;
-        shape(jobs);
+        if (!split) shape(jobs);
         max_tiles = 0;
         for (AugJob& J : jobs) {
             J.tiles   = (J.win_h + tr - 1) / tr;
@@ -831,9 +834,11 @@ struct aeon_hip_ctx {
     bool                 records = true; // AEON_HIP_RECORDS=0: contrast calls through the two-launch path
     int                  rec_helpers = 2; // AEON_HIP_REC_HELPERS: staging-only waves of the record kernel
     int                  rec_phases  = 0; // AEON_HIP_REC_PHASES (development): row phases of the record kernel
-    bool                 split = true;      // AEON_HIP_SPLIT=0: direct non-photometric calls through augment_tiles
+    bool                 split = false;     // AEON_HIP_SPLIT=1: non-photometric INTER_LINEAR f32 launches through
+                                            // augment_split (measured slower than augment_tiles)
     int                  split_helpers = 2; // AEON_HIP_SPLIT_HELPERS: staging waves of augment_split
     int                  split_rpl = 2;     // AEON_HIP_SPLIT_RPL: output rows per compute lane per tile
+    int                  split_occ = 1;     // AEON_HIP_SPLIT_OCC: augment_split workgroups per CU (1 or 2)
     bool                 fuse_masks = false; // AEON_HIP_FUSE_MASKS=1: a pair call's masks inside the image launch
     bool                 vram_jobs = false; // job tables written by the host into device memory (large-BAR GPUs;
                                             // AEON_HIP_VRAM_JOBS=0: pinned host tables)
@@ -945,6 +950,7 @@ bool host_can_write(void* p)
 std::mutex                               g_vram_pool_mu;
 std::vector<std::pair<uint8_t*, size_t>> g_vram_pool;   // released tables, still allocated and mapped
 std::vector<uint8_t*>                    g_vram_unused; // blocks whose probe failed (kept, never used)
+std::vector<std::pair<uint8_t*, size_t>> g_vram_all;    // every uncached block of the process (diagnostics)
 void free_vram(uint8_t*& p, size_t& cap)
 {
     if (p) {
@@ -980,6 +986,10 @@ bool grow_vram(int device, uint8_t*& p, size_t& cap, size_t need) // false: no t
         (void)hipGetLastError();
         p = nullptr;
         return false;
+    }
+    {
+        std::lock_guard<std::mutex> lock(g_vram_pool_mu);
+        g_vram_all.emplace_back(p, n);
     }
     // the host writes these tables through p itself: only when p's page is mapped read-write for the
     // host and a write + read-back through p works (a restricted BAR or a virtualised GPU can allocate it without mapping it for the
@@ -1291,12 +1301,13 @@ LaunchArgs launch_args(aeon_hip_ctx* ctx, const Slot& s, const uint8_t* table, c
 // waves in one workgroup of <= 1,024 lanes, rows_per_tile = nph * rpl, two staging buffers.  The LDS
 // request is held above half a CU's 160 KB so that the grid's n_cu workgroups land one per CU.  False:
 // no such shape (the caller keeps augment_tiles).
-bool plan_split(const aeon_hip_ctx* ctx, const std::vector<JobGeom>& geo, LaunchPlan& P, SplitArgs& sa)
+template <typename J_>
+bool plan_split(const aeon_hip_ctx* ctx, const std::vector<J_>& geo, LaunchPlan& P, SplitArgs& sa)
 {
     if (geo.empty()) return false;
     const int W = geo[0].win_w;
     if (W <= 0 || (W & 3) != 0) return false;
-    for (const JobGeom& g : geo)
+    for (const J_& g : geo)
         if (g.cn != 3 || g.win_w != W || g.mode != RESIZE_LINEAR) return false;
     const int gpr = W / 4, nh = ctx->split_helpers;
     int       nph = 0, nwc = 0;
@@ -1311,16 +1322,17 @@ bool plan_split(const aeon_hip_ctx* ctx, const std::vector<JobGeom>& geo, Launch
     const int rpl = std::max(1, std::min(ctx->split_rpl, kSplitTRMax / nph));
     const int tr  = nph * rpl;
     long      by  = 0;
-    for (const JobGeom& g : geo) by = std::max(by, stage_bytes_for(3, stage_rows_for(g, tr), stage_cols(g)));
+    for (const J_& g : geo) by = std::max(by, stage_bytes_for(3, stage_rows_for(g, tr), stage_cols(g)));
     by             = (by + 1023) / 1024 * 1024;
     const int lds  = split_lds_layout(W, (int)by).total;
+    const int occ  = ctx->split_occ == 2 && !P.tail && lds <= kMaxLds / 2 ? 2 : 1; // (the TAIL form spills at 64 VGPRs)
     if (lds > kMaxLds) return false;
     P.tr          = tr;
     P.stage_bytes = (int)by;
     P.max_win_w   = W;
     P.threads     = (nwc + nh) * 64;
-    P.lds         = std::max(lds, kMaxLds / 2 + 1024);
-    sa.nwc = nwc, sa.nph = nph, sa.rpl = rpl, sa.win_w = W;
+    P.lds         = occ == 2 ? lds : std::max(lds, kMaxLds / 2 + 1024);
+    sa.nwc = nwc, sa.nph = nph, sa.rpl = rpl, sa.win_w = W, sa.occ = occ;
     return true;
 }
 
@@ -1374,12 +1386,12 @@ bool run_direct(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void
     P.photo  = (key & 1) != 0;
     P.vec_ok = vec_ok;
     P.rtab   = P.photo && o.dtype == AEON_DTYPE_F32;
-    P.shape(geo);
     // non-photometric INTER_LINEAR into float32 CHW planes, one window width: augment_split (staging on
-    // helper waves, split_kernels.hip)
+    // helper waves, split_kernels.hip); else augment_tiles' shape
     SplitArgs  sa{};
     const bool split = ctx->split && !P.photo && P.rm == RESIZE_LINEAR && o.dtype == AEON_DTYPE_F32 && o.channel_major &&
                        vec_ok && !ov.u8_map && !o.fixed_aspect_ratio && plan_split(ctx, geo, P, sa);
+    if (!split) P.shape(geo);
     P.max_tiles = (max_h + P.tr - 1) / P.tr;
     // every tile reads its job over PCIe: past ~512 KB of such reads per launch the multi-pass path's
     // device table wins (C5's image launch, 4,096 tiles of 256 B: 98 vs 90 us of kernels per step;
@@ -1437,8 +1449,8 @@ bool run_direct(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void
     if (split) {
         KernelTimer t{};
         if (timed) t = take_timer(ctx, KM_FINAL, lbytes);
-        const int grid = std::min(a.total_tiles, ctx->n_cu); // one workgroup per CU (the LDS request holds it)
-        HIP_OK(launch_split(P.tail, a, sa, grid, stream, timed ? t.start : nullptr, timed ? t.stop : nullptr));
+        const int grid = std::min(a.total_tiles, sa.occ * ctx->n_cu); // sa.occ workgroups per CU (the LDS request holds it)
+        HIP_OK(launch_split(P.tail, sa.occ, a, sa, grid, stream, timed ? t.start : nullptr, timed ? t.stop : nullptr));
         if (timed) ctx->timers.push_back(t);
     } else {
         timed_launch(ctx, KM_FINAL, P, a, stream, lbytes, timed);
@@ -1689,6 +1701,10 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
             if (P.jobs.empty()) continue;
             P.vec_ok = main_all.vec_ok;
             P.rtab   = v == &main && P.photo && o.dtype == AEON_DTYPE_F32;
+            // final non-photometric INTER_LINEAR float32 CHW launches (C5's images): augment_split
+            P.split = v == &main && ctx->split && !P.photo && P.rm == RESIZE_LINEAR && o.dtype == AEON_DTYPE_F32 &&
+                      o.channel_major && P.vec_ok && !ov.u8_map && !o.fixed_aspect_ratio && !(ms && ctx->fuse_masks) &&
+                      plan_split(ctx, P.jobs, P, P.sa);
             P.finalize();
             P.blob_off = blob;
             blob += P.jobs.size() * sizeof(AugJob);
@@ -1818,7 +1834,7 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
         const int srows = std::min(mask16_rows(m16_max_w, m16_max_seg), AEON_HIP_FUSED_MASK_ROWS);
         bool in_main = false;
         for (LaunchPlan& P : main) in_main |= fused == &P;
-        if (groups == 1 && in_main && srows >= 1 && !fused->has_contrast) {
+        if (groups == 1 && in_main && srows >= 1 && !fused->has_contrast && !fused->split) {
             const int pitch = mask16_pitch(m16_max_seg);
             const int slots = std::max(1, std::min(m16_max_slots, srows));
             const int base  = lds_layout(fused->max_win_w, fused->tr, fused->stage_bytes, fused->photo && fused->has_hue,
@@ -1879,7 +1895,15 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
             a.lds_bytes = fused_masks.lds_bytes;
             bytes += m16_bytes;
         }
-        timed_launch(ctx, KM_FINAL, P, a, stream, bytes, timed);
+        if (P.split) {
+            KernelTimer t{};
+            if (timed) t = take_timer(ctx, KM_FINAL, bytes);
+            HIP_OK(launch_split(P.tail, P.sa.occ, a, P.sa, std::min(a.total_tiles, P.sa.occ * ctx->n_cu), stream,
+                                timed ? t.start : nullptr, timed ? t.stop : nullptr));
+            if (timed) ctx->timers.push_back(t);
+        } else {
+            timed_launch(ctx, KM_FINAL, P, a, stream, bytes, timed);
+        }
     }
     phase(6);
     release_slot(ctx, slot, stream);
@@ -2003,6 +2027,7 @@ int aeon_hip_ctx_create(int device, aeon_hip_ctx** out)
             if (const char* e = std::getenv("AEON_HIP_SPLIT")) c->split = std::atoi(e) != 0;
             if (const char* e = std::getenv("AEON_HIP_SPLIT_HELPERS")) c->split_helpers = std::max(1, std::min(4, std::atoi(e)));
             if (const char* e = std::getenv("AEON_HIP_SPLIT_RPL")) c->split_rpl = std::max(1, std::min(4, std::atoi(e)));
+            if (const char* e = std::getenv("AEON_HIP_SPLIT_OCC")) c->split_occ = std::max(1, std::min(2, std::atoi(e)));
             if (const char* e = std::getenv("AEON_HIP_JPEG_HUFF")) c->jpeg_gpu_huff = std::strcmp(e, "host") != 0;
             if (const char* e = std::getenv("AEON_HIP_FUSE_MASKS")) c->fuse_masks = std::atoi(e) != 0;
 #ifdef AEON_HIP_TRACE
@@ -2420,6 +2445,20 @@ int aeon_hip_host_free(void* p)
 }
 
 const char* aeon_hip_last_error(void) { return g_err.c_str(); }
+int aeon_hip_debug_uncached_blocks(uint64_t* ranges, int cap, int* n)
+{
+    return guarded([&] {
+        if (!n || (cap > 0 && !ranges)) fail(AEON_HIP_EINVAL, "null argument");
+        std::lock_guard<std::mutex> lock(g_vram_pool_mu);
+        *n = (int)g_vram_all.size();
+        for (int i = 0; i < cap && i < *n; i++) {
+            ranges[2 * i]     = (uint64_t)(uintptr_t)g_vram_all[i].first;
+            ranges[2 * i + 1] = (uint64_t)(uintptr_t)g_vram_all[i].first + g_vram_all[i].second;
+        }
+        return 0;
+    });
+}
+
 const char* aeon_hip_version(void) { return "aeon-hip 0.1 (gfx950)"; }
 
 } // extern "C"

@@ -837,11 +837,17 @@ def main():
     if world > 1 and not args.no_extra:
         # C4 (BASELINE configs[3]): the full augment_image workload at per-GPU batch 1024 on every
         # rank, each its own node slice and seed; global batch 1024 * N
+        # (the rate from an untimed run -- an event pair around a launch idles the queue around it --
+        # the kernel duration from a second, short run that times every launch, as the C3 extra does)
         st4 = max(5, args.steps // 5)
-        e4, kt4, _, _ = run_device(A, C, torch, "C3", 1024, st4, 2, rank, world, args.pool_mib, dist)
+        e4, _, _, _ = run_device(A, C, torch, "C3", 1024, st4, 2, rank, world, args.pool_mib, dist, 0)
+        _, kt4, _, _ = run_device(A, C, torch, "C3", 1024, 4, 1, rank, world, args.pool_mib, dist, 1)
+        m4, b4, n4 = kt4["augment"]
         extra["C4"] = {"value": 1024 * st4 * world / e4, "unit": "images/s", "batch_per_gpu": 1024,
                        "global_batch": 1024 * world, "steps": st4, "ms_per_step": e4 / st4 * 1e3,
-                       "what": "C3 workload on every rank (node slice + seed 1 + node_id), max over ranks"}
+                       "augment_kernel_avg_launch_ms": m4 / max(n4, 1),
+                       "what": "C3 workload on every rank (node slice + seed 1 + node_id), max over ranks; "
+                               "rate untimed, kernel time from a second run timing every launch"}
     if rank == 0 and world == 1 and not args.no_extra:
         if args.config == "C2":
             # rate untimed (an event pair between a step's launches costs ~10 us of GPU time there),

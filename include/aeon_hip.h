@@ -388,6 +388,11 @@ const char* aeon_hip_stager_last_error(void);
 int aeon_hip_host_alloc(size_t bytes, void** out);
 int aeon_hip_host_free(void* p);
 
+/* Diagnostics: the device address ranges [lo, hi) of every uncached job-table block this process
+ * allocated (stage.cpp grow_vram; they are pooled, never freed: DESIGN.md §8), up to cap pairs into
+ * ranges; *n = how many there are.  Lets a test that finds lost writes say whether they lie inside one. */
+int aeon_hip_debug_uncached_blocks(uint64_t* ranges, int cap, int* n);
+
 const char* aeon_hip_last_error(void);
 const char* aeon_hip_version(void);
 

@@ -113,8 +113,9 @@ def hip_canvases(ctx, images, params, out, mask=False):
     return [host[i * out.item_stride: i * out.item_stride + nb].reshape(shape).copy() for i in range(n)]
 
 
-def hip_records(ctx, images, params, out, mask=False, dtype=None):
-    """Run records through the HIP stage on cuda:0; returns one array per record."""
+def hip_records(ctx, images, params, out, mask=False, dtype=None, info=None):
+    """Run records through the HIP stage on cuda:0; returns one array per record.  info (a dict): gets
+    the device output buffer's address ('dst_ptr') for failure reports."""
     import torch
     arena, descs = A.pack_images(images)
     src = torch.from_numpy(arena).to("cuda") if arena.size else torch.zeros(16, dtype=torch.uint8, device="cuda")
@@ -124,6 +125,8 @@ def hip_records(ctx, images, params, out, mask=False, dtype=None):
     fn = ctx.mask_batch if mask else ctx.augment_batch
     fn(descs, src.data_ptr(), params, out, dst.data_ptr(), stream)
     ctx.synchronize(stream)
+    if info is not None:
+        info["dst_ptr"] = dst.data_ptr()
     host = dst.cpu().numpy()
     res = []
     for i, p in enumerate(params):
@@ -145,3 +148,21 @@ def draw_params(aug, sizes, out_w, out_h, seed=1):
         st = states[i:i + 1].copy()
         res.append(f.make_params(st, w, h, out_w, out_h))
     return res
+
+
+def lost_lines_report(dst_ptr, item_stride, index, got, want):
+    """Where a device output differs from the oracle: the 128-byte lines' device addresses and whether
+    each lies inside one of the process's uncached job-table blocks (A.uncached_blocks), with the
+    blocks' ranges -- the evidence the lost-line fault of DESIGN.md §8 needs."""
+    g = np.ascontiguousarray(got).view(np.uint8).reshape(-1)
+    w = np.ascontiguousarray(want).view(np.uint8).reshape(-1)
+    off = np.nonzero(g != w)[0]
+    if not off.size:
+        return "no difference"
+    base = dst_ptr + index * item_stride
+    lines = sorted({(base + int(o)) & ~127 for o in off})
+    blocks = A.uncached_blocks()
+    inside = [ln for ln in lines if any(lo <= ln < hi for lo, hi in blocks)]
+    return (f"record {index}: {off.size} bytes differ in {len(lines)} lines of 128 B at device "
+            f"{hex(lines[0])}..{hex(lines[-1])} (buffer {hex(dst_ptr)}); {len(inside)} of them inside an uncached "
+            f"job-table block; blocks: {[(hex(lo), hex(hi)) for lo, hi in blocks]}")

@@ -285,13 +285,15 @@ def test_decoder_after_contexts_come_and_go():
         ctx = A.Context(0)
         imgs = [A.synthetic_image(900 + 8 * k + i, 300, 280, 3) for i in range(8)]
         ps = [f.make_params(eng, 300, 280, 224, 224) for _ in imgs]
-        got = H.hip_records(ctx, imgs, ps, od)
+        info = {}
+        got = H.hip_records(ctx, imgs, ps, od, info=info)
         ctx.close()
-        for g, r in zip(got, H.oracle_records(imgs, ps, od)):
-            assert np.array_equal(g, r), k
+        for i, (g, r) in enumerate(zip(got, H.oracle_records(imgs, ps, od))):
+            assert np.array_equal(g, r), (k, H.lost_lines_report(info["dst_ptr"], od.item_stride, i, g, r))
     cfg = dict(batch_size=4, random_seed=9, batch_major=False, etl=[C.IMAGE_224], augmentation=[C.C3_AUG])
     recs = _records(8, seed=4)
     for _ in range(2):
         (out,) = A.Decoder(cfg).decode(recs)
         (pin,) = _decode_pinned(A.Decoder(cfg), recs)
-        assert np.array_equal(out.view(np.uint8), pin.view(np.uint8)), _diff_report(out, pin)
+        assert np.array_equal(out.view(np.uint8), pin.view(np.uint8)), (
+            _diff_report(out, pin), "uncached blocks: " + str([(hex(lo), hex(hi)) for lo, hi in A.uncached_blocks()]))

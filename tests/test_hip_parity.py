@@ -701,3 +701,29 @@ def test_spec_bs_hue_primary_colours_and_greys(ctx):
     imgs = [img] * len(params)
     out = A.out_desc(**MEAN_OUT)
     _assert_same(H.hip_records(ctx, imgs, params, out), H.oracle_records(imgs, params, out), "spec primaries")
+
+
+@pytest.mark.parametrize("occ", ["1", "2"])
+def test_split_kernel_opt_in(occ, monkeypatch):
+    """augment_split (split_kernels.hip; AEON_HIP_SPLIT=1 -- measured slower than augment_tiles, DESIGN §4,
+    kept opt-in): the C2 batch, both goldens' configuration (flip, non-multiple-of-4 crop) and the C5 image
+    launch through the planner path, bit-exact against the oracle, with one and with two workgroups per CU."""
+    monkeypatch.setenv("AEON_HIP_SPLIT", "1")
+    monkeypatch.setenv("AEON_HIP_SPLIT_OCC", occ)
+    monkeypatch.setenv("AEON_HIP_SPLIT_RPL", "1" if occ == "2" else "2")
+    c = A.Context(0)
+    try:
+        n = 256
+        imgs = _synthetic(n)
+        params = H.draw_params(C.C2_AUG, [(256, 256)] * n, 224, 224, seed=3)
+        out = A.out_desc(**MEAN_OUT)
+        _assert_same(H.hip_records(c, imgs, params, out), H.oracle_records(imgs, params, out), "split C2")
+        p = [A.aug_params(crop_x=50, crop_y=50, crop_w=171, crop_h=201, out_w=224, out_h=224, flip=f) for f in (0, 1)]
+        two = _synthetic(2)
+        _assert_same(H.hip_records(c, two, p, out), H.oracle_records(two, p, out), "split flip / odd crop")
+        imgs5 = [A.synthetic_image(i, 640, 480, 3) for i in range(16)]
+        params5 = H.draw_params(C.C5_AUG, [(640, 480)] * 16, 512, 512, seed=2)
+        iout = C.out_desc_for(C.IMAGE_512, C.C5_AUG)
+        _assert_same(H.hip_records(c, imgs5, params5, iout), H.oracle_records(imgs5, params5, iout), "split C5 images")
+    finally:
+        c.close()

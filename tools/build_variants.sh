@@ -6,5 +6,5 @@ R="$(cd "$(dirname "$0")/.." && pwd)"
 mkdir -p "$R/aeon_amd/variants"
 for spec in "$@"; do
   name="${spec%%=*}"; defs="${spec#*=}"
-  make -s -C "$R/aeon_amd/csrc" OUT="$R/aeon_amd/variants/$name.so" BUILD="$R/aeon_amd/csrc/build_$name" KDEFS="$defs" -j4
+  make -s -C "$R/aeon_amd/csrc" OUT="$R/aeon_amd/variants/$name.so" BUILD="$R/aeon_amd/csrc/build_$name" KDEFS="$defs" -j4 "$R/aeon_amd/variants/$name.so"
 done
