@@ -67,7 +67,8 @@ struct RecTile {
 };
 
 // staged-source geometry of tile `band` (rows band*32 ...) of the record whose job is J
-__device__ __forceinline__ RecTile rec_tile(const JobRef& J, int band, int TR, int H, int stage_bytes, int32_t* error)
+template <typename JR>
+__device__ __forceinline__ RecTile rec_tile(const JR& J, int band, int TR, int H, int stage_bytes, int32_t* error)
 {
     RecTile f;
     f.ok    = false;
@@ -93,7 +94,8 @@ __device__ __forceinline__ RecTile rec_tile(const JobRef& J, int band, int TR, i
 }
 
 // row taps of tile f into the table at yt (staged rows in the buffer at `stage`)
-__device__ __forceinline__ void rec_row_taps(const JobRef& J, const RecTile& f, int yt, int stage, int i0, int step)
+template <typename JR>
+__device__ __forceinline__ void rec_row_taps(const JR& J, const RecTile& f, int yt, int stage, int i0, int step)
 {
     for (int r = i0; r < f.nrows; r += step) {
         const YTap y = ycoef<RESIZE_LINEAR>(JF(J, win_y) + f.y0 + r, JF(J, scale_y), JF(J, crop_h));
@@ -573,7 +575,10 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) void 
         // stall -- their staging then ends after the compute waves' rows.
         __builtin_amdgcn_s_setprio(AEON_REC_HELPER_PRIO);
         int cur_idx = 0; // (trace builds: the entry the staging stamps go to)
-        const auto stage_tile = [&](const JobRef& J, int band, int buf) {
+        // (the job's hot half in scalar registers at once: an LDS round trip per field, each waited for,
+        // made the helpers' staging the tile's critical path)
+        const auto stage_tile = [&](const JobRef& JR, int band, int buf) {
+            const JobS    J = job_load(JR.lds);
             const RecTile f = rec_tile(J, band, TR, H, L.stage_bytes, a.error);
             if (f.ok) {
                 const int sb = L.stage + buf * L.stage_bytes;
