@@ -91,6 +91,7 @@ struct Batch {
     int        first = 0;     // its first record in the window's launch order
     int        n     = 0;     // records staged (idx 0..n-1)
     hipEvent_t done  = nullptr;
+    bool       d2h   = false; // pageable batch: its wait copies it out of the window's device outputs
     bool       launched = false; // a flush / launch named this batch buffer
     bool       waited   = false; // a flush / wait returned (or is returning) its completion
 };
@@ -112,6 +113,7 @@ struct Window {
     size_t                              dev_src_cap = 0;
     uint8_t*                            dev_out = nullptr;
     size_t                              dev_out_cap = 0;
+    std::atomic<int>                    copying{0}; // waits copying a pageable batch out of dev_out
 };
 
 } // namespace
@@ -199,6 +201,15 @@ Window& staging_window(aeon_hip_stager* s)
     if (w.state == Window::LAUNCHED) {
         hip_ok(hipSetDevice(s->device), "hipSetDevice");
         hip_ok(hipEventSynchronize(w.done), "hipEventSynchronize");
+        // its pageable batches nobody waited for: their D2H now, so they are complete when this returns
+        for (auto& b : w.batches)
+            if (b->d2h && !b->waited) {
+                b->waited = true;
+                hip_ok(hipMemcpy(b->out, w.dev_out + (size_t)b->first * s->out.item_stride, (size_t)b->n * s->out.item_stride,
+                                 hipMemcpyDeviceToHost),
+                       "hipMemcpy");
+            }
+        while (w.copying.load(std::memory_order_acquire) != 0) std::this_thread::yield();
         reset_window(s, w);
     }
     return w;
@@ -248,11 +259,6 @@ void launch_window(aeon_hip_stager* s, Window& w)
         c.base = total;
         total += c.used;
     }
-    grow(w.dev_src, w.dev_src_cap, std::max<size_t>(total, 16));
-    for (const Chunk& c : w.chunks)
-        if (c.used)
-            hip_ok(hipMemcpyAsync(w.dev_src + c.base, c.host, c.used, hipMemcpyHostToDevice, w.stream),
-                   "hipMemcpyAsync");
     std::vector<aeon_img_desc>   descs;
     std::vector<aeon_aug_params> params;
     std::vector<void*>           views;
@@ -274,17 +280,42 @@ void launch_window(aeon_hip_stager* s, Window& w)
         views.push_back(v);
         all_mapped = all_mapped && v;
     }
+    // The window's sources: read by the kernels straight from its pinned chunk over PCIe when the outputs
+    // go to pinned host buffers too and the window fits one chunk -- no H2D ahead of the kernels (the
+    // runtime may run that copy as a blit kernel, which then cannot overlap the previous window's
+    // persistent grid: C2 60 K vs ~80 K records/s, tools/aeon_path_cpp.cpp) -- else one H2D per chunk into
+    // the window's device arena.
+    const bool on_device = (s->kind & AEON_STAGER_DEVICE_OUT) != 0;
+    bool       all_out_mapped = !on_device;
+    for (auto& bp : w.batches) all_out_mapped = all_out_mapped && mapped_view(bp->out);
+    int         used_chunks = 0;
+    const Chunk* used = nullptr; // (its base is 0: the chunks before it hold nothing)
+    for (const Chunk& c : w.chunks)
+        if (c.used) used_chunks++, used = used ? used : &c;
+    static const bool src_copy = [] {
+        const char* e = std::getenv("AEON_HIP_STAGER_SRC_COPY");
+        return e && std::atoi(e) != 0;
+    }();
+    const uint8_t* src_base = nullptr;
+    if (all_out_mapped && used_chunks == 1 && !src_copy) src_base = (const uint8_t*)mapped_view(used->host);
+    if (!src_base) {
+        grow(w.dev_src, w.dev_src_cap, std::max<size_t>(total, 16));
+        for (const Chunk& c : w.chunks)
+            if (c.used)
+                hip_ok(hipMemcpyAsync(w.dev_src + c.base, c.host, c.used, hipMemcpyHostToDevice, w.stream),
+                       "hipMemcpyAsync");
+        src_base = w.dev_src;
+    }
     const size_t item = s->out.item_stride;
     auto run = [&](int first, int n, void* dst) {
         if (n == 0) return;
         if ((s->kind & ~AEON_STAGER_DEVICE_OUT) == AEON_STAGER_MASK)
-            abi_ok(aeon_hip_mask_batch(s->ctx, n, descs.data() + first, w.dev_src, params.data() + first, &s->out,
+            abi_ok(aeon_hip_mask_batch(s->ctx, n, descs.data() + first, src_base, params.data() + first, &s->out,
                                        dst, w.stream));
         else
-            abi_ok(aeon_hip_augment_batch(s->ctx, n, descs.data() + first, w.dev_src, params.data() + first, &s->out,
+            abi_ok(aeon_hip_augment_batch(s->ctx, n, descs.data() + first, src_base, params.data() + first, &s->out,
                                           dst, w.stream));
     };
-    const bool on_device = (s->kind & AEON_STAGER_DEVICE_OUT) != 0;
     if (on_device || all_mapped) {
         // outputs the kernels can store into directly (device batch buffers, or pinned host ones over
         // PCIe): one launch per batch, queued back to back
@@ -294,17 +325,17 @@ void launch_window(aeon_hip_stager* s, Window& w)
             hip_ok(hipEventRecord(b.done, w.stream), "hipEventRecord");
         }
     } else {
-        // pageable host batches: the whole window in ONE launch into device memory, then a D2H into
-        // each batch buffer
+        // pageable host batches: the whole window in ONE launch into device memory; each batch's D2H is
+        // made by its wait (the consumer's thread): a copy into pageable memory holds the calling thread
+        // until the data is out (the runtime stages it), and on the decode thread that made the
+        // launch-only post_process wait for the window's kernels (overlap measured below flush)
         grow(w.dev_out, w.dev_out_cap, std::max<size_t>(descs.size() * item, 16));
         run(0, (int)descs.size(), w.dev_out);
+        hip_ok(hipEventRecord(w.batches.front()->done, w.stream), "hipEventRecord");
         for (auto& bp : w.batches) {
             Batch& b = *bp;
-            if (b.n)
-                hip_ok(hipMemcpyAsync(b.out, w.dev_out + (size_t)b.first * item, (size_t)b.n * item,
-                                      hipMemcpyDeviceToHost, w.stream),
-                       "hipMemcpyAsync");
-            hip_ok(hipEventRecord(b.done, w.stream), "hipEventRecord");
+            if (&b != w.batches.front().get()) hip_ok(hipEventRecord(b.done, w.stream), "hipEventRecord");
+            b.d2h = b.n > 0;
         }
     }
     hip_ok(hipEventRecord(w.done, w.stream), "hipEventRecord");
@@ -357,6 +388,9 @@ void wait_batch(aeon_hip_stager* s, void* batch_out, bool& found)
     Window*     wp  = nullptr;
     uint64_t    gen = 0;
     bool        last = false;
+    void*       copy_dst = nullptr; // pageable batch: its D2H, made here
+    const void* copy_src = nullptr;
+    size_t      copy_bytes = 0;
     {
         std::lock_guard<std::mutex> l(s->mu);
         for (Window& w : s->win) {
@@ -367,6 +401,12 @@ void wait_batch(aeon_hip_stager* s, void* batch_out, bool& found)
                     ev        = b->done;
                     wp = &w, gen = w.gen, wdone = w.done, wstream = w.stream;
                     last = --w.unwaited == 0;
+                    if (b->d2h) {
+                        w.copying.fetch_add(1, std::memory_order_acq_rel);
+                        copy_dst   = b->out;
+                        copy_src   = w.dev_out + (size_t)b->first * s->out.item_stride;
+                        copy_bytes = (size_t)b->n * s->out.item_stride;
+                    }
                     break;
                 }
         }
@@ -375,7 +415,14 @@ void wait_batch(aeon_hip_stager* s, void* batch_out, bool& found)
     if (!found) return;
     hip_ok(hipSetDevice(s->device), "hipSetDevice");
     hip_ok(hipEventSynchronize(ev), "hipEventSynchronize");
+    // (the window's device outputs stay until its last wait has returned: reset_window runs after it)
+    if (copy_bytes) {
+        const hipError_t e = hipMemcpy(copy_dst, copy_src, copy_bytes, hipMemcpyDeviceToHost);
+        wp->copying.fetch_sub(1, std::memory_order_acq_rel);
+        hip_ok(e, "hipMemcpy");
+    }
     if (!last) return;
+    while (wp->copying.load(std::memory_order_acquire) != 0) std::this_thread::yield(); // (other batches' copies)
     // the window is complete: surface a device error word, then free it for the window after next
     hip_ok(hipEventSynchronize(wdone), "hipEventSynchronize");
     const int rc = aeon_hip_synchronize(s->ctx, wstream);

@@ -578,6 +578,38 @@ def run_aeon_path(A, C, torch, cfg="C2", overlap=True, windows=8, warmup=2):
             "ms_per_window": dt / windows * 1e3}
 
 
+def run_aeon_path_cpp(windows=24, warmup=4, reps=2):
+    """aeon's decode stage with the stager, call for call, as a C++ program against the C ABI
+    (tools/aeon_path_cpp.cpp, built as aeon_amd/aeon_path_cpp; INTEGRATION.md edits 1-5): aeon's pinned pool of
+    thread_affinity_map workers running provide() (make_params from each record's slot engine +
+    aeon_hip_stager_stage of a decoded host record) over aeon's decode_size window, post_process() per batch,
+    a consumer thread waiting per buffer over two alternating containers.  Per config, batch buffers pageable
+    or pinned ("pinned": true -> aeon_hip_host_alloc, the kernels store into them), post_process launch-only
+    with the consumer's wait ('overlap') or flushing; each run `reps` times (the host's load swings these
+    PCIe/host-bound rates), all values kept, best first."""
+    import subprocess
+    exe = os.path.join(ROOT, "aeon_amd", "aeon_path_cpp")
+    res = {}
+    for cfg in ("C2", "C1"):
+        for buffers in ("pinned", "pageable"):
+            for mode in ("overlap", "flush"):
+                vals = []
+                for _ in range(reps):
+                    r = subprocess.run([exe, cfg, buffers, mode, str(windows), str(warmup)], capture_output=True,
+                                       text=True, timeout=180)
+                    if r.returncode != 0:
+                        raise RuntimeError(f"aeon_path_cpp {cfg} {buffers} {mode}: {r.stderr.strip()[-300:]}")
+                    vals.append(json.loads(r.stdout.strip().splitlines()[-1]))
+                vals.sort(key=lambda d: -d["value"])
+                res.setdefault(cfg, {}).setdefault(buffers, {})[mode] = {
+                    "value": vals[0]["value"], "runs": [round(v["value"]) for v in vals], "unit": "images/s",
+                    "batch": vals[0]["batch"], "decode_size": vals[0]["decode_size"],
+                    "pool_threads": vals[0]["pool_threads"]}
+    res["what"] = ("tools/aeon_path_cpp.cpp: aeon's decode stage in C++ (loader.cpp:158-176 pool and decode_size, "
+                   "batch_decoder::filler's provide + post_process, batch_iterator_fbm::filler's wait, two containers)")
+    return res
+
+
 def side(extra, key, fn):
     """One side run of the bench line (rank 0's extras): a failure is recorded in the line under its
     key instead of losing the line."""
@@ -906,18 +938,7 @@ def main():
                     "batch (zero-copy over PCIe, no D2H)"})
         side(extra, "C1", lambda: {"decoder": run_c1_decoder(A, C, torch)})
 
-        def aeon_path():
-            r = {}
-            for cfg in ("C1", "C2"):
-                r[cfg] = {"overlap": run_aeon_path(A, C, torch, cfg, True),
-                          "flush": run_aeon_path(A, C, torch, cfg, False)}
-            r["what"] = ("aeon's decode stage emulated call for call through the stager (INTEGRATION.md edits 1-4): "
-                         "provide() on 8 pool threads (make_params + stage of decoded host records), post_process() "
-                         "per batch, a consumer taking batches out of two alternating containers; 'overlap': "
-                         "launch-only post_process + consumer-side wait, 'flush': post_process waits; pageable "
-                         "batch buffers (D2H)")
-            return r
-        side(extra, "aeon_path", aeon_path)
+        side(extra, "aeon_path_cpp", run_aeon_path_cpp)
         side(extra, "e2e_jpeg_decoder", lambda: {
             "host_outputs": {"value": run_e2e_jpeg(A, C, torch, on_device=False), "unit": "images/s"},
             "device_outputs": {"value": run_e2e_jpeg(A, C, torch, on_device=True), "unit": "images/s"},
