@@ -647,7 +647,14 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) void 
     for (int i = 0; i < kRecWords; i++) rec[i] = 0;
     uint64_t b_out = 0;
     int      par   = 0;
+    // the lane's first output row and its index in a plane: every row's y and index are these plus a
+    // uniform multiple of nph (computed per row).  Made opaque at each record so that the compiler does
+    // not hoist the 14 per-row indices of the unrolled tile loop out of the record loop -- held across
+    // it they spilled, and each scratch reload's vmcnt(0) drained the B stores in flight.
+    int        lrow = lph, lidx = lph * W + ox0;
+    const int  rstep = nph * W;
     for (int k = 0; k <= K; k++) {
+        asm volatile("" : "+v"(lrow), "+v"(lidx));
         const bool   hasA = k < K, hasB = k > 0;
         const JobRef JA{slot(k)};
         RecA         R{};
@@ -679,20 +686,20 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) void 
 #pragma unroll
             for (int u = 0; u < kRecTileRows; u++) {
                 const int j = t * kRecTileRows + u;
-                const int y = lph + nph * j;
+                const int y = lrow + nph * j, yi = lidx + rstep * j; // (yi = y * W + ox0)
                 uint32_t* hw = rec + rb + 3 * u;
                 nwv[3 * u] = nwv[3 * u + 1] = nwv[3 * u + 2] = 0;
                 if (FAST && AEON_REC_FUSED && fok) { // (uniform) A and B interleaved
                     const bool  va  = active && y < H;
                     const i32x4 ytr = lds_ptr<const i32x4>(L.yt + par * kRecTRMax * 16)[min(y - t * TR, TR - 1)];
-                    const u32x3 q   = rec_row_fast(R, L, ytr, va, s0, s1, s2, orsrc, plane, hasB && va ? y * W + ox0 : -1,
+                    const u32x3 q   = rec_row_fast(R, L, ytr, va, s0, s1, s2, orsrc, plane, hasB && va ? yi : -1,
                                                    bgr, hw[0], hw[1], hw[2]);
                     hw[0] = q.x, hw[1] = q.y, hw[2] = q.z; // (B has read them)
                     nwv[3 * u] = q.x, nwv[3 * u + 1] = q.y, nwv[3 * u + 2] = q.z;
                     continue;
                 }
                 if (hasB && __builtin_amdgcn_ballot_w64(active && y < H) != 0) {
-                    if (active && y < H) rec_store(L, orsrc, plane, y * W + ox0, bgr, hw[0], hw[1], hw[2]);
+                    if (active && y < H) rec_store(L, orsrc, plane, yi, bgr, hw[0], hw[1], hw[2]);
                 }
                 if constexpr (!(FAST && AEON_REC_FUSED)) {
                     if (fok && active && y < H) {
