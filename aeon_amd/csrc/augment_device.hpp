@@ -659,7 +659,8 @@ __device__ __forceinline__ void resize_px(i32x4 ytr, int col, uint32_t wx, int s
 
 // resize_px<RESIZE_LINEAR, true> for a lane's 4 pixels of a row with all 16 staged words read first: the
 // reads are in flight together (one LDS wait per row instead of one per pixel).
-__device__ __forceinline__ void resize4_linear_scaled(i32x4 ytr, const int (&col)[4], const uint32_t (&wx)[4], int (&s)[4][3])
+template <bool SCALED = true>
+__device__ __forceinline__ void resize4_linear(i32x4 ytr, const int (&col)[4], const uint32_t (&wx)[4], int (&s)[4][3])
 {
     uint32_t p[4][4];
 #pragma unroll
@@ -679,8 +680,13 @@ __device__ __forceinline__ void resize4_linear_scaled(i32x4 ytr, const int (&col
             const uint32_t t0  = (uint32_t)__mul24((int)(H0 >> 4), ytr.z) + (2u << 16);
             const uint32_t t1  = (uint32_t)__mul24((int)(H1 >> 4), ytr.w);
             s[q][c]            = (int)((t0 >> 16) + (t1 >> 16));
+            if (!SCALED) s[q][c] >>= 2;
         }
     }
+}
+__device__ __forceinline__ void resize4_linear_scaled(i32x4 ytr, const int (&col)[4], const uint32_t (&wx)[4], int (&s)[4][3])
+{
+    resize4_linear<true>(ytr, col, wx, s);
 }
 
 // Elements of OpenCV's scalar row tail (e >= xv) use FixedPtCast<int, uchar, 22> instead.

@@ -37,6 +37,9 @@
 #ifndef AEON_REC_UNROLL // split kernel: the compute waves' tile loop unrolled (no register rotation)
 #define AEON_REC_UNROLL 1
 #endif
+#ifndef AEON_REC_HOIST // FAST form: a row's 16 tap words read together (resize4_linear)
+#define AEON_REC_HOIST 1
+#endif
 #ifndef AEON_REC_FUSED // FAST form: A and B of a row interleaved (rec_row_fast); 0 = B's row, then A's
 #define AEON_REC_FUSED 1
 #endif
@@ -259,8 +262,12 @@ __device__ __forceinline__ u32x3 rec_row_fast(const RecA& R, const RecLds& L, i3
     float b[4] = {T(0, w0, 0), T(0, w0, 3), T(0, w1, 2), T(0, w2, 1)};
     __builtin_amdgcn_sched_barrier(0);
     int val[4][3];
+#if AEON_REC_HOIST
+    resize4_linear<false>(ytr, R.col, R.wx, val); // (the 16 staged words in flight together)
+#else
 #pragma unroll
     for (int k = 0; k < 4; k++) resize_px<RESIZE_LINEAR, false>(ytr, R.col[k], R.wx[k], val[k]);
+#endif
     __builtin_amdgcn_sched_barrier(0);
     store_f32x4(orsrc, off(bgr ? 2 : 0), b[0], b[1], b[2], b[3]);
     float g[4] = {T(1, w0, 1), T(1, w1, 0), T(1, w1, 3), T(1, w2, 2)};
