@@ -22,6 +22,7 @@
 
 #include <algorithm>
 #include <cfloat>
+#include <type_traits>
 
 #include "aug_job.hpp"
 
@@ -30,6 +31,9 @@
 #ifndef AEON_RG_SKIP
 #define AEON_RG_SKIP 0
 #endif
+#ifndef AEON_SEP_SCHED // resize_sep: a row's taps read together up to this K (K = 8's 32 loads in flight: 150+ VGPRs)
+#define AEON_SEP_SCHED 4
+#endif
 
 namespace aeon_hip {
 
@@ -37,13 +41,10 @@ namespace {
 
 __device__ __forceinline__ int sat_u8(int v) { return min(max(v, 0), 255); }
 __device__ __forceinline__ int sat_s16(int v) { return min(max(v, -32768), 32767); }
-// 24-bit signed multiply-add, full rate (|operands| < 2^23)
-__device__ __forceinline__ int mad_i24(int a, int b, int c)
-{
-    int r;
-    asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-    return r;
-}
+// 24-bit signed multiply-add, full rate (|operands| < 2^23; the sum wraps).  (Not inline asm: the
+// compiler schedules no load across an asm statement, so each element's LDS reads waited for the previous
+// element's multiply-adds.)
+__device__ __forceinline__ int mad_i24(int a, int b, int c) { return (int)((uint32_t)__mul24(a, b) + (uint32_t)c); }
 __device__ __forceinline__ int coef_q(float c) { return sat_s16((int)__builtin_rintf(c * 2048)); }
 
 __device__ __forceinline__ void interpolate_cubic(float x, float* c)
@@ -434,7 +435,31 @@ __global__ __launch_bounds__(256) void resize_generic(const ResizeJob* __restric
 // workgroup, so those branches are too).  No horizontal-sum array in LDS: the workgroup needs only the
 // staged bytes and the taps, so several bands share a CU and their latencies overlap.  Same
 // arithmetic as resize_generic, element for element.
-template <int K>
+// Each staged row sits kSepPadL bytes into its SW-byte slot: room for the replicated left border (at
+// most K/2 - 1 pixels), as the slot's end has room for the right one (at most K/2), so every tap of an
+// element is its first tap's staged byte + j * cn -- no per-tap clamp (cv::resize's border replicate).
+constexpr int kSepPadL = 16;
+
+// f(integral_constant<int, d>) for a workgroup-uniform d in 1..K (0: nothing)
+template <int K, typename F>
+__device__ __forceinline__ void sep_shift(int d, F&& f)
+{
+    if (d == 1) return f(std::integral_constant<int, 1>{});
+    if (d == 2) return f(std::integral_constant<int, 2>{});
+    if constexpr (K > 2) {
+        if (d == 3) return f(std::integral_constant<int, 3>{});
+        if (d == 4) return f(std::integral_constant<int, 4>{});
+    }
+    if constexpr (K > 4) {
+        if (d == 5) return f(std::integral_constant<int, 5>{});
+        if (d == 6) return f(std::integral_constant<int, 6>{});
+        if (d == 7) return f(std::integral_constant<int, 7>{});
+        if (d == 8) return f(std::integral_constant<int, 8>{});
+    }
+}
+
+// CN: the jobs' channel count when it is 3 (the taps' LDS offsets immediates), else 0 (J.cn)
+template <int K, int CN>
 __global__ __launch_bounds__(256) void resize_sep(const ResizeJob* __restrict__ jobs, const uint8_t* __restrict__ table, int TR,
                                                   int CW, int NR, int SW, const float* lutg, int bgr, int chm, int32_t* error)
 {
@@ -442,7 +467,7 @@ __global__ __launch_bounds__(256) void resize_sep(const ResizeJob* __restrict__ 
     const ResizeJob J = jobs[blockIdx.y];
     if ((int)blockIdx.x >= J.tiles) return;
     constexpr int k2 = K / 2, xs = 1 + K;
-    const int     tid = threadIdx.x, nt = blockDim.x, cn = J.cn;
+    const int     tid = threadIdx.x, nt = blockDim.x, cn = CN ? CN : J.cn;
     const int     ty = blockIdx.x / J.tiles_x, tx = blockIdx.x - ty * J.tiles_x;
     const int     x0 = tx * CW, y0 = ty * TR;
     const int     nx = min(CW, J.win_w - x0), ny = min(TR, J.win_h - y0);
@@ -480,7 +505,7 @@ __global__ __launch_bounds__(256) void resize_sep(const ResizeJob* __restrict__ 
     const int u_lo = min(max(xt[0] - k2 + 1, 0), J.crop_w - 1);
     const int u_hi = min(max(xt[(nx - 1) * xs] + k2, 0), J.crop_w - 1);
     const int sb   = (u_hi - u_lo + 1) * cn;
-    if (nr > NR || (J.padded ? sb : ((sb + 30) >> 4) * 16) > SW) {
+    if (nr > NR || (J.padded ? sb : ((sb + 30) >> 4) * 16) + kSepPadL + 16 > SW || (CN && J.cn != CN)) {
         if (tid == 0) atomicOr(error, 128);
         return;
     }
@@ -506,7 +531,7 @@ __global__ __launch_bounds__(256) void resize_sep(const ResizeJob* __restrict__ 
                 const uint64_t a0 = a & ~(uint64_t)15;
                 const int      bl = (int)((((a + sb - 1) & ~(uint64_t)15) - a0) >> 4); // the row's last block
                 w[u]  = *(const __attribute__((address_space(1))) u32x4*)(a0 + (uint64_t)min(b, bl) * 16);
-                at[u] = q0 + u * nt < total && b <= bl ? r * SW + b * 16 : -1;
+                at[u] = q0 + u * nt < total && b <= bl ? r * SW + kSepPadL + b * 16 : -1;
             }
 #pragma unroll
             for (int u = 0; u < kBatch; u++)
@@ -539,7 +564,7 @@ __global__ __launch_bounds__(256) void resize_sep(const ResizeJob* __restrict__ 
                     const uint32_t x  = row[min(max(bo, 0), rowb - 1)];
                     w[u] |= (ok ? x : 0u) << (8 * k);
                 }
-                at[u] = qv ? rr * SW + ch * 4 : -1;
+                at[u] = qv ? rr * SW + kSepPadL + ch * 4 : -1;
                 r += dr, ch += dc;
                 if (ch >= nch) ch -= nch, r++;
             }
@@ -549,6 +574,22 @@ __global__ __launch_bounds__(256) void resize_sep(const ResizeJob* __restrict__ 
         }
     }
     __syncthreads();
+    // staged row rr's first byte (column u_lo)
+    const int  shift0 = J.padded ? 0 : (int)(rowa0 & 15), sstep = J.padded ? 0 : (int)(J.src_stride & 15);
+    const auto srow   = [&](int rr) { return S + rr * SW + kSepPadL + ((shift0 + (r_lo + rr) * sstep) & 15); };
+    // The replicated border: taps left of column 0 read column 0, right of crop_w - 1 read crop_w - 1
+    // (the anchors are clamped into the crop, so at most K/2 - 1 and K/2 columns).
+    const int padl = max(0, -(xt[0] - k2 + 1)), padr = max(0, xt[(nx - 1) * xs] + k2 - (J.crop_w - 1));
+    if (padl + padr > 0) { // (uniform; u_lo = 0 when padl, u_hi = crop_w - 1 when padr)
+        const int per = (padl + padr) * cn;
+        for (int i = tid; i < nr * per; i += nt) {
+            const int rr = i / per, k = i - rr * per, p = k / cn, c = k - p * cn;
+            uint8_t*  row = srow(rr);
+            if (p < padl) row[-(p + 1) * cn + c] = row[c];
+            else row[(J.crop_w - u_lo + (p - padl)) * cn + c] = row[(J.crop_w - 1 - u_lo) * cn + c];
+        }
+        __syncthreads();
+    }
     // The lane's 4 elements: 4 consecutive bytes of the window row (a u8 window: one dword store),
     // or, for a final_out job, 4 consecutive pixels of one channel (one float4 store into its plane).
     const int nb = nx * cn, e0 = tid * 4;
@@ -566,77 +607,74 @@ __global__ __launch_bounds__(256) void resize_sep(const ResizeJob* __restrict__ 
         ch[q]       = planar ? lc : e - (e / cn) * cn;
         xe[q]       = (J.win_x + x0 + px[q]) * cn + ch[q];
     }
-    // staged-byte offsets of their K column taps, and the coefficients
-    int off[4][K], cf[4][K];
+    // element q's first tap in a staged row (its taps: + j * cn), and the coefficients
+    int ob[4], cf[4][K];
 #pragma unroll
     for (int q = 0; q < 4; q++) {
         const int  i = px[q], c = ch[q];
         const int* t = xt + i * xs;
+        ob[q]        = (t[0] - k2 + 1 - u_lo) * cn + c;
 #pragma unroll
-        for (int j = 0; j < K; j++) {
-            off[q][j] = (min(max(t[0] - k2 + 1 + j, 0), J.crop_w - 1) - u_lo) * cn + c;
-            cf[q][j]  = t[1 + j];
-        }
+        for (int j = 0; j < K; j++) cf[q][j] = t[1 + j];
     }
     const int W = J.dst_w * cn, xv = simd_end(K, W), xmax = max(max(xe[0], xe[1]), max(xe[2], xe[3]));
-    // The window: hw[j][q] = horizontal sum of staged row wrow[j] for element q, as float (exact:
-    // |sum| < 2^24).  The row indices are workgroup-uniform (scalar registers), so the window's reuse
-    // tests are scalar branches; a row not in the window is summed from its staged bytes.
+    // The window: hw[j][q] = horizontal sum of source row clamp(sy - K/2 + 1 + j) for element q (float
+    // for the cubic vector form, exact: |sum| < 2^24; int otherwise).  The rows follow sy, which grows
+    // with the output row, so a step of d rows keeps hw[d..K) as hw[0..K - d) and sums the d new rows:
+    // d is workgroup-uniform (a scalar switch, register indices constant in every case).
     typedef float f32x2 __attribute__((ext_vector_type(2)));
-    float hw[K][4];
-    int   wrow[K];
+    using HT = typename std::conditional<K == 4, float, int>::type;
+    HT  hw[K][4] = {};
+    int wsy      = 0;
+    const auto hsum = [&](int j, int sy) {
+        const int      rr  = min(max(sy - k2 + 1 + j, 0), J.crop_h - 1) - r_lo;
+        const uint8_t* row = srow(rr);
+        // the row's taps read together, then the sums (the compiler would otherwise wait for each
+        // element's reads before issuing the next element's) -- up to K = AEON_SEP_SCHED
+        if constexpr (K <= AEON_SEP_SCHED) {
+            int b[4][K];
 #pragma unroll
-    for (int j = 0; j < K; j++) {
-        wrow[j] = -1;
+            for (int q = 0; q < 4; q++)
 #pragma unroll
-        for (int q = 0; q < 4; q++) hw[j][q] = 0.f;
-    }
-    const int shift0 = J.padded ? 0 : (int)(rowa0 & 15), sstep = J.padded ? 0 : (int)(J.src_stride & 15);
+                for (int jj = 0; jj < K; jj++) b[q][jj] = row[ob[q] + jj * cn];
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                int acc = 0;
+#pragma unroll
+                for (int jj = 0; jj < K; jj++) acc = mad_i24(b[q][jj], cf[q][jj], acc);
+                hw[j][q] = (HT)((AEON_RG_SKIP & 1) ? rr + q : acc);
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const uint8_t* e   = row + ob[q];
+                int            acc = 0;
+#pragma unroll
+                for (int jj = 0; jj < K; jj++) acc = mad_i24((int)e[jj * cn], cf[q][jj], acc);
+                hw[j][q] = (HT)((AEON_RG_SKIP & 1) ? rr + q : acc);
+            }
+        }
+    };
     for (int r = 0; r < ny; r++) {
         const int* t  = yt + r * xs;
         const int  sy = __builtin_amdgcn_readfirstlane(t[0]);
-        int        rows[K];
+        const int  d  = (r == 0 || sy < wsy || sy - wsy > K) ? K : sy - wsy;
+        wsy           = sy;
+        sep_shift<K>(d, [&](auto D) {
+            constexpr int dd = decltype(D)::value;
 #pragma unroll
-        for (int j = 0; j < K; j++) rows[j] = min(max(sy - k2 + 1 + j, 0), J.crop_h - 1) - r_lo;
-        float nh[K][4];
+            for (int j = 0; j + dd < K; j++)
 #pragma unroll
-        for (int j = 0; j < K; j++) {
-            bool found = false;
+                for (int q = 0; q < 4; q++) hw[j][q] = hw[j + dd][q];
 #pragma unroll
-            for (int m = 0; m < K; m++)
-                if (!found && wrow[m] == rows[j]) {
-#pragma unroll
-                    for (int q = 0; q < 4; q++) nh[j][q] = hw[m][q];
-                    found = true;
-                }
-            if (!found) {
-                if (AEON_RG_SKIP & 1) {
-#pragma unroll
-                    for (int q = 0; q < 4; q++) nh[j][q] = (float)(rows[j] + q);
-                } else {
-                    // (the row's first byte sits at its address & 15 in its staged blocks)
-                    const uint8_t* row = S + rows[j] * SW + ((shift0 + (r_lo + rows[j]) * sstep) & 15);
-#pragma unroll
-                    for (int q = 0; q < 4; q++) {
-                        int acc = 0;
-#pragma unroll
-                        for (int jj = 0; jj < K; jj++) acc = mad_i24((int)row[off[q][jj]], cf[q][jj], acc);
-                        nh[j][q] = (float)acc;
-                    }
-                }
-            }
-        }
-#pragma unroll
-        for (int j = 0; j < K; j++) {
-            wrow[j] = rows[j];
-#pragma unroll
-            for (int q = 0; q < 4; q++) hw[j][q] = nh[j][q];
-        }
+            for (int j = K - dd; j < K; j++) hsum(j, sy);
+        });
         int coef[K];
 #pragma unroll
         for (int j = 0; j < K; j++) coef[j] = __builtin_amdgcn_readfirstlane(t[1 + j]);
         uint32_t word = 0;
-        if (K == 4) { // VResizeCubicVec_32s8u, SSE's order of operations, two elements per packed op
+        if constexpr (K == 4) { // VResizeCubicVec_32s8u, SSE's order of operations, two elements per packed op
             const float sc = 1.f / (2048 * 2048);
             const float c0 = (float)coef[0] * sc, c1 = (float)coef[1] * sc, c2 = (float)coef[2] * sc, c3 = (float)coef[3] * sc;
 #pragma unroll
@@ -663,8 +701,13 @@ __global__ __launch_bounds__(256) void resize_sep(const ResizeJob* __restrict__ 
                     v           = sat_u8(sat_s16(m + 2) >> 2);
                 } else { // FixedPtCast<int, uchar, 22>, int32 sums wrapping
                     uint32_t acc = 0;
+                    if constexpr (K == 4) {
 #pragma unroll
-                    for (int j = 0; j < K; j++) acc += (uint32_t)(int)hw[j][q] * (uint32_t)coef[j];
+                        for (int j = 0; j < K; j++) acc += (uint32_t)(int)hw[j][q] * (uint32_t)coef[j];
+                    } else { // (|hw|, |coef| < 2^23: the 24-bit product's low 32 bits are the wrapping product)
+#pragma unroll
+                        for (int j = 0; j < K; j++) acc = (uint32_t)mad_i24((int)hw[j][q], coef[j], (int)acc);
+                    }
                     v = sat_u8((int32_t)(acc + (1u << 21)) >> 22);
                 }
                 word = (word & ~(0xffu << (8 * q))) | ((uint32_t)v << (8 * q));
@@ -734,12 +777,16 @@ hipError_t launch_resize_sep(int K, const ResizeJob* jobs, const uint8_t* table,
     const size_t lds     = ((size_t)(CW + TR) * (1 + K) * 4 + 15) / 16 * 16 + (size_t)NR * SW + (lut ? 768 * 4 : 0);
     const int    threads = std::min(256, (std::max((CW * cn + 3) / 4, cn * ((CW + 3) / 4)) + 63) / 64 * 64);
     const dim3   grid((unsigned)max_tiles, (unsigned)n_jobs);
+    const bool c3 = cn == 3; // (every job of a resize_sep launch has the launch's channel count)
+    typedef void (*SepFn)(const ResizeJob*, const uint8_t*, int, int, int, int, const float*, int, int, int32_t*);
+    SepFn fn = nullptr;
     switch (K) {
-    case 2: hipLaunchKernelGGL(resize_sep<2>, grid, dim3(threads), lds, stream, jobs, table, TR, CW, NR, SW, lut, bgr, chm, error); break;
-    case 4: hipLaunchKernelGGL(resize_sep<4>, grid, dim3(threads), lds, stream, jobs, table, TR, CW, NR, SW, lut, bgr, chm, error); break;
-    case 8: hipLaunchKernelGGL(resize_sep<8>, grid, dim3(threads), lds, stream, jobs, table, TR, CW, NR, SW, lut, bgr, chm, error); break;
+    case 2: fn = c3 ? resize_sep<2, 3> : resize_sep<2, 0>; break;
+    case 4: fn = c3 ? resize_sep<4, 3> : resize_sep<4, 0>; break;
+    case 8: fn = c3 ? resize_sep<8, 3> : resize_sep<8, 0>; break;
     default: return hipErrorInvalidValue;
     }
+    hipLaunchKernelGGL(fn, grid, dim3(threads), lds, stream, jobs, table, TR, CW, NR, SW, lut, bgr, chm, error);
     return hipGetLastError();
 }
 

@@ -248,7 +248,9 @@ struct LaunchPlan {
         // (the next tile's loads in flight during the current tile's compute) at two rows per
         // lane: 42 vs 45 us (C2), 152/291 vs 186/370 us (C3 pass 2 / pass 1) -- the second
         // buffer costs occupancy and halves the rows per tile (rejected).
-        const int tr_cap = std::min(64, std::max(1, 4 * nph));
+        // (development: AEON_HIP_TILE_ROWS caps the rows per tile instead)
+        static const int tr_env = std::getenv("AEON_HIP_TILE_ROWS") ? std::atoi(std::getenv("AEON_HIP_TILE_ROWS")) : 0;
+        const int        tr_cap = std::min(64, std::max(1, tr_env > 0 ? tr_env : 4 * nph));
         int       budget = kStageBudget;
         bool hue = false, contrast = false;
         for (const J_& J : jobs) {
@@ -429,8 +431,24 @@ void lanczos4_inputs(int ssize, double scale, int d0, int n, bool clamp, LzIn* o
         if (clamp && s >= ssize - 1) f = 0, s = ssize - 1;
         LzIn L{0.0, 0.0, f, s};
         if (!(f < FLT_EPSILON)) {
-            const double y0 = -(f + 3) * kPi * 0.25;
-            L.s0 = std::sin(y0), L.c0 = std::cos(y0);
+            // sin / cos of a function of the float f alone: memoised per thread.  A batch's fractions are
+            // few (integer crop sizes over a common output size: multiples of 1 / (2 * size), rounded to
+            // float), so a 256-record LANCZOS4 call computes a few thousand pairs instead of 115 K (the
+            // host side was the C2:LANCZOS4 step's bound).  Same libm calls on the same doubles: the
+            // same bits.
+            struct Entry {
+                uint32_t key; // float bits + 1 (0: empty)
+                double   s, c;
+            };
+            static thread_local std::vector<Entry> memo(1 << 14);
+            uint32_t bits;
+            std::memcpy(&bits, &f, 4);
+            Entry& e = memo[(bits * 2654435761u) >> 18];
+            if (e.key != bits + 1) {
+                const double y0 = -(f + 3) * kPi * 0.25;
+                e               = Entry{bits + 1, std::sin(y0), std::cos(y0)};
+            }
+            L.s0 = e.s, L.c0 = e.c;
         }
         out[d - d0] = L;
     }
@@ -532,8 +550,9 @@ struct GrPlan {
             // a band's lanes (at most 256): 4 bytes of a u8 window row each, or 4 pixels of one channel of a
             // final_out job each -- cn * ceil(cw / 4) lanes, so 340 columns for 3 channels, not 341
             int cw = std::min({ww, 1024 / u.cn_max, 4 * (256 / u.cn_max)}), tr = std::max(4, std::min(64, tr0));
-            // staged rows: whole 16-byte blocks (resize_sep), hence up to 30 bytes more per row
-            auto sw = [&] { return (bytes_for(f, n, cw) + 30 + 15) / 16 * 16; };
+            // staged rows: whole 16-byte blocks (resize_sep), hence up to 30 bytes more per row, and 32
+            // bytes of room for the replicated borders (resize_kernels.hip kSepPadL)
+            auto sw = [&] { return (bytes_for(f, n, cw) + 30 + 15) / 16 * 16 + 32; };
             auto l  = [&] {
                 return ((size_t)(cw + tr) * (1 + sk) * 4 + 15) / 16 * 16 + (size_t)rows_for(f, n, tr) * sw() + lut_lds;
             };

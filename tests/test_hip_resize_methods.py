@@ -164,14 +164,20 @@ def test_resize_methods_final_output(ctx, method, case):
     _assert_same(H.hip_records(ctx, imgs, params, out), H.oracle_records(imgs, params, out), f"{method} {case}")
 
 
-def test_resize_lanczos4_taps_c2_batch(ctx):
-    """LANCZOS4's taps are finished on the GPU from the host's libm sin / cos (stage.cpp
-    lanczos4_inputs -> resize_kernels.hip lanczos4_taps): a C2 batch of 64 random crops (as many
-    distinct fractions per axis as output columns and rows) equals the oracle, whose taps are the
-    host's from end to end."""
-    aug = dict(C.C2_AUG, interpolation_method="LANCZOS4")
+@pytest.mark.parametrize("method", list(METHODS))
+def test_resize_c2_batch(ctx, method):
+    """A C2 batch of 64 random crops with the method set.  LANCZOS4: its taps are finished on the GPU
+    from the host's libm sin / cos (stage.cpp lanczos4_inputs -> resize_kernels.hip lanczos4_taps), as
+    many distinct fractions per axis as output columns and rows, against the oracle's taps computed on
+    the host from end to end.  AREA: the batch holds both method classes (resizeArea_ records on
+    resize_generic, upscaled axes on resize_sep<2>), launched concurrently on the slot's side stream and
+    the call's stream."""
+    aug = dict(C.C2_AUG, interpolation_method=method)
     imgs = [A.synthetic_image(60 + i, 256, 256, 3) for i in range(64)]
     params = H.draw_params(aug, [(256, 256)] * 64, 224, 224, seed=29)
-    assert all(p.interp == A.INTERP_LANCZOS4 for p in params)
+    assert all(p.interp == METHODS[method] for p in params)
+    if method == "AREA":
+        down = [p.crop_w >= 224 and p.crop_h >= 224 for p in params]
+        assert any(down) and not all(down), "the batch should mix resizeArea_ and bilinear-emulation records"
     out = A.out_desc(item_stride=3 * 224 * 224 * 4, **F32)
-    _assert_same(H.hip_records(ctx, imgs, params, out), H.oracle_records(imgs, params, out), "LANCZOS4 C2")
+    _assert_same(H.hip_records(ctx, imgs, params, out), H.oracle_records(imgs, params, out), f"{method} C2")
