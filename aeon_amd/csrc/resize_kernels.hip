@@ -458,15 +458,19 @@ __device__ __forceinline__ void sep_shift(int d, F&& f)
     }
 }
 
-// CN: the jobs' channel count when it is 3 (the taps' LDS offsets immediates), else 0 (J.cn)
-template <int K, int CN>
+// CN: the jobs' channel count when it is 3 (the taps' LDS offsets immediates), else 0 (J.cn).
+// AREA: resizeArea_ (both axes downscaled, non-integer): K = the most taps of a destination index
+// (computeResizeAreaTab's entries, area_taps), float weights zero-padded to K -- exact, as every
+// product is >= +0 and adding +0 changes no sum -- horizontal sums from 0 in tap order, the vertical sum
+// beta0 * h0 + beta1 * h1 + ..., cvRound: ResizeArea_Invoker's arithmetic, element for element.
+template <int K, int CN, bool AREA = false>
 __global__ __launch_bounds__(256) void resize_sep(const ResizeJob* __restrict__ jobs, const uint8_t* __restrict__ table, int TR,
                                                   int CW, int NR, int SW, const float* lutg, int bgr, int chm, int32_t* error)
 {
     extern __shared__ int lds_w[];
     const ResizeJob J = jobs[blockIdx.y];
     if ((int)blockIdx.x >= J.tiles) return;
-    constexpr int k2 = K / 2, xs = 1 + K;
+    constexpr int k2 = AREA ? 1 : K / 2, xs = (AREA ? 2 : 1) + K; // (area: t[0] first index, t[1] taps, weights)
     const int     tid = threadIdx.x, nt = blockDim.x, cn = CN ? CN : J.cn;
     const int     ty = blockIdx.x / J.tiles_x, tx = blockIdx.x - ty * J.tiles_x;
     const int     x0 = tx * CW, y0 = ty * TR;
@@ -480,7 +484,9 @@ __global__ __launch_bounds__(256) void resize_sep(const ResizeJob* __restrict__ 
         for (int i = tid; i < 768; i += nt) lut[i] = lutg[i];
     for (int i = tid; i < nx; i += nt) {
         int* t = xt + i * xs;
-        if (K == 8) {
+        if (AREA) {
+            area_taps(J.crop_w, J.scale_x, J.win_x + x0 + i, t, K, error);
+        } else if (K == 8) {
             const GrTap g = ((const GrTap*)(table + J.coef_x))[x0 + i];
             t[0]          = g.s;
             for (int k = 0; k < 8; k++) t[1 + k] = g.c[k];
@@ -490,7 +496,9 @@ __global__ __launch_bounds__(256) void resize_sep(const ResizeJob* __restrict__ 
     }
     for (int r = tid; r < ny; r += nt) {
         int* t = yt + r * xs;
-        if (K == 8) {
+        if (AREA) {
+            area_taps(J.crop_h, J.scale_y, J.win_y + y0 + r, t, K, error);
+        } else if (K == 8) {
             const GrTap g = ((const GrTap*)(table + J.coef_y))[y0 + r];
             t[0]          = g.s;
             for (int k = 0; k < 8; k++) t[1 + k] = g.c[k];
@@ -499,11 +507,11 @@ __global__ __launch_bounds__(256) void resize_sep(const ResizeJob* __restrict__ 
         }
     }
     __syncthreads();
-    const int r_lo = min(max(yt[0] - k2 + 1, 0), J.crop_h - 1);
-    const int r_hi = min(max(yt[(ny - 1) * xs] + k2, 0), J.crop_h - 1);
+    const int r_lo = AREA ? yt[0] : min(max(yt[0] - k2 + 1, 0), J.crop_h - 1);
+    const int r_hi = AREA ? yt[(ny - 1) * xs] + yt[(ny - 1) * xs + 1] - 1 : min(max(yt[(ny - 1) * xs] + k2, 0), J.crop_h - 1);
     const int nr   = r_hi - r_lo + 1;
-    const int u_lo = min(max(xt[0] - k2 + 1, 0), J.crop_w - 1);
-    const int u_hi = min(max(xt[(nx - 1) * xs] + k2, 0), J.crop_w - 1);
+    const int u_lo = AREA ? xt[0] : min(max(xt[0] - k2 + 1, 0), J.crop_w - 1);
+    const int u_hi = AREA ? xt[(nx - 1) * xs] + xt[(nx - 1) * xs + 1] - 1 : min(max(xt[(nx - 1) * xs] + k2, 0), J.crop_w - 1);
     const int sb   = (u_hi - u_lo + 1) * cn;
     if (nr > NR || (J.padded ? sb : ((sb + 30) >> 4) * 16) + kSepPadL + 16 > SW || (CN && J.cn != CN)) {
         if (tid == 0) atomicOr(error, 128);
@@ -579,7 +587,8 @@ __global__ __launch_bounds__(256) void resize_sep(const ResizeJob* __restrict__ 
     const auto srow   = [&](int rr) { return S + rr * SW + kSepPadL + ((shift0 + (r_lo + rr) * sstep) & 15); };
     // The replicated border: taps left of column 0 read column 0, right of crop_w - 1 read crop_w - 1
     // (the anchors are clamped into the crop, so at most K/2 - 1 and K/2 columns).
-    const int padl = max(0, -(xt[0] - k2 + 1)), padr = max(0, xt[(nx - 1) * xs] + k2 - (J.crop_w - 1));
+    // (INTER_AREA's taps stay inside the crop: its zero-weight padding taps read whatever follows)
+    const int padl = AREA ? 0 : max(0, -(xt[0] - k2 + 1)), padr = AREA ? 0 : max(0, xt[(nx - 1) * xs] + k2 - (J.crop_w - 1));
     if (padl + padr > 0) { // (uniform; u_lo = 0 when padl, u_hi = crop_w - 1 when padr)
         const int per = (padl + padr) * cn;
         for (int i = tid; i < nr * per; i += nt) {
@@ -615,7 +624,7 @@ __global__ __launch_bounds__(256) void resize_sep(const ResizeJob* __restrict__ 
         const int* t = xt + i * xs;
         ob[q]        = (t[0] - k2 + 1 - u_lo) * cn + c;
 #pragma unroll
-        for (int j = 0; j < K; j++) cf[q][j] = t[1 + j];
+        for (int j = 0; j < K; j++) cf[q][j] = AREA ? (j < t[1] ? t[2 + j] : 0) : t[1 + j]; // (area: float bits; +0.f)
     }
     const int W = J.dst_w * cn, xv = simd_end(K, W), xmax = max(max(xe[0], xe[1]), max(xe[2], xe[3]));
     // The window: hw[j][q] = horizontal sum of source row clamp(sy - K/2 + 1 + j) for element q (float
@@ -623,12 +632,29 @@ __global__ __launch_bounds__(256) void resize_sep(const ResizeJob* __restrict__ 
     // with the output row, so a step of d rows keeps hw[d..K) as hw[0..K - d) and sums the d new rows:
     // d is workgroup-uniform (a scalar switch, register indices constant in every case).
     typedef float f32x2 __attribute__((ext_vector_type(2)));
-    using HT = typename std::conditional<K == 4, float, int>::type;
+    using HT = typename std::conditional<K == 4 || AREA, float, int>::type;
     HT  hw[K][4] = {};
     int wsy      = 0;
     const auto hsum = [&](int j, int sy) {
-        const int      rr  = min(max(sy - k2 + 1 + j, 0), J.crop_h - 1) - r_lo;
+        // (area: rows past the tile's last are its last, weighted 0)
+        const int      rr  = AREA ? min(sy + j - r_lo, nr - 1) : min(max(sy - k2 + 1 + j, 0), J.crop_h - 1) - r_lo;
         const uint8_t* row = srow(rr);
+        if constexpr (AREA) { // buf[dx] += S[sx] * alpha from 0, in tap order
+            int b[4][K];
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+#pragma unroll
+                for (int jj = 0; jj < K; jj++) b[q][jj] = row[ob[q] + jj * cn];
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                float acc = 0.f;
+#pragma unroll
+                for (int jj = 0; jj < K; jj++) acc = acc + (float)b[q][jj] * __int_as_float(cf[q][jj]);
+                hw[j][q] = acc;
+            }
+            return;
+        }
         // the row's taps read together, then the sums (the compiler would otherwise wait for each
         // element's reads before issuing the next element's) -- up to K = AEON_SEP_SCHED
         if constexpr (K <= AEON_SEP_SCHED) {
@@ -670,11 +696,12 @@ __global__ __launch_bounds__(256) void resize_sep(const ResizeJob* __restrict__ 
 #pragma unroll
             for (int j = K - dd; j < K; j++) hsum(j, sy);
         });
-        int coef[K];
+        int coef[K] = {};
+        if constexpr (!AREA)
 #pragma unroll
-        for (int j = 0; j < K; j++) coef[j] = __builtin_amdgcn_readfirstlane(t[1 + j]);
+            for (int j = 0; j < K; j++) coef[j] = __builtin_amdgcn_readfirstlane(t[1 + j]);
         uint32_t word = 0;
-        if constexpr (K == 4) { // VResizeCubicVec_32s8u, SSE's order of operations, two elements per packed op
+        if constexpr (K == 4 && !AREA) { // VResizeCubicVec_32s8u, SSE's order of operations, two elements per packed op
             const float sc = 1.f / (2048 * 2048);
             const float c0 = (float)coef[0] * sc, c1 = (float)coef[1] * sc, c2 = (float)coef[2] * sc, c3 = (float)coef[3] * sc;
 #pragma unroll
@@ -689,7 +716,19 @@ __global__ __launch_bounds__(256) void resize_sep(const ResizeJob* __restrict__ 
                 word = __builtin_amdgcn_cvt_pk_u8_f32(sm.y, (uint32_t)qb, word);
             }
         }
-        if (K != 4 || xmax >= xv) { // the other forms, and elements on the scalar tail
+        if constexpr (AREA) { // sum = beta0 * h0, sum += beta_k * h_k; saturate_cast<uchar>(cvRound)
+            const int n = __builtin_amdgcn_readfirstlane(t[1]);
+            float     beta[K];
+#pragma unroll
+            for (int j = 0; j < K; j++) beta[j] = j < n ? __int_as_float(__builtin_amdgcn_readfirstlane(t[2 + j])) : 0.f;
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                float sum = beta[0] * hw[0][q];
+#pragma unroll
+                for (int j = 1; j < K; j++) sum = sum + beta[j] * hw[j][q];
+                word |= (uint32_t)sat_u8((int)__builtin_rintf(sum)) << (8 * q);
+            }
+        } else if (K != 4 || xmax >= xv) { // the other forms, and elements on the scalar tail
 #pragma unroll
             for (int q = 0; q < 4; q++) {
                 const int x = xe[q];
@@ -770,17 +809,21 @@ hipError_t launch_lanczos4_taps(const LzIn* in, GrTap* out, int n, hipStream_t s
     return hipGetLastError();
 }
 
-hipError_t launch_resize_sep(int K, const ResizeJob* jobs, const uint8_t* table, int n_jobs, int max_tiles, int TR, int CW,
-                             int NR, int SW, int cn, const float* lut, int bgr, int chm, int32_t* error, hipStream_t stream)
+hipError_t launch_resize_sep(int K, bool area, const ResizeJob* jobs, const uint8_t* table, int n_jobs, int max_tiles, int TR,
+                             int CW, int NR, int SW, int cn, const float* lut, int bgr, int chm, int32_t* error, hipStream_t stream)
 {
     if (n_jobs <= 0) return hipSuccess;
-    const size_t lds     = ((size_t)(CW + TR) * (1 + K) * 4 + 15) / 16 * 16 + (size_t)NR * SW + (lut ? 768 * 4 : 0);
+    const size_t lds = ((size_t)(CW + TR) * ((area ? 2 : 1) + K) * 4 + 15) / 16 * 16 + (size_t)NR * SW + (lut ? 768 * 4 : 0);
     const int    threads = std::min(256, (std::max((CW * cn + 3) / 4, cn * ((CW + 3) / 4)) + 63) / 64 * 64);
     const dim3   grid((unsigned)max_tiles, (unsigned)n_jobs);
     const bool c3 = cn == 3; // (every job of a resize_sep launch has the launch's channel count)
     typedef void (*SepFn)(const ResizeJob*, const uint8_t*, int, int, int, int, const float*, int, int, int32_t*);
     SepFn fn = nullptr;
-    switch (K) {
+    if (area) {
+        if (K == 4) fn = c3 ? resize_sep<4, 3, true> : resize_sep<4, 0, true>;
+        else if (K == 8) fn = c3 ? resize_sep<8, 3, true> : resize_sep<8, 0, true>;
+        else return hipErrorInvalidValue;
+    } else switch (K) {
     case 2: fn = c3 ? resize_sep<2, 3> : resize_sep<2, 0>; break;
     case 4: fn = c3 ? resize_sep<4, 3> : resize_sep<4, 0>; break;
     case 8: fn = c3 ? resize_sep<8, 3> : resize_sep<8, 0>; break;

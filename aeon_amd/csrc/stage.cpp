@@ -51,7 +51,7 @@ hipError_t launch_resize_generic(const ResizeJob* jobs, const uint8_t* table, in
                                  int NR, int xs, int amax, int cn_max, int SW, const float* lut, int bgr, int chm,
                                  int32_t* error, hipStream_t stream);
 hipError_t launch_lanczos4_taps(const LzIn* in, GrTap* out, int n, hipStream_t stream);
-hipError_t launch_resize_sep(int K, const ResizeJob* jobs, const uint8_t* table, int n_jobs, int max_tiles, int TR, int CW,
+hipError_t launch_resize_sep(int K, bool area, const ResizeJob* jobs, const uint8_t* table, int n_jobs, int max_tiles, int TR, int CW,
                              int NR, int SW, int cn, const float* lut, int bgr, int chm, int32_t* error, hipStream_t stream);
 void       jpeg_decode_batch(JpegState* S, int n, const void* const* data, const size_t* sizes,
                              const aeon_img_desc* descs, void* dst_base, int32_t* error, hipStream_t stream,
@@ -466,6 +466,7 @@ struct GrPlan {
         int  first = 0, count = 0;
         int  TR = 16, CW = 128, NR = 1, xs = 3, amax = 1, cn_max = 1, max_tiles = 0, SW = 4;
         int  sep = 0;           // K of resize_sep, or 0: resize_generic
+        bool area = false;      // resize_sep's INTER_AREA form (resizeArea_ jobs, sep = their most taps)
         bool any_final = false; // some job writes the loader's output itself (its LUT in the launch's LDS)
     };
     std::vector<Sub> subs;
@@ -501,6 +502,8 @@ struct GrPlan {
     }
     static int ksize(int m) { return m == GR_CUBIC ? 4 : (m == GR_LANCZOS4 ? 8 : 2); }
     static int sep_k(int m) { return m == GR_CUBIC ? 4 : m == GR_LANCZOS4 ? 8 : m == GR_LINEAR_AREA ? 2 : 0; }
+    // launch classes: the fixed-K methods by K, resizeArea_ jobs, the rest
+    static int cls(int m) { return sep_k(m) ? sep_k(m) : m == GR_AREA ? 50 : 99; }
     // rows of H a tile of `tr` output rows needs at most (jobs [f, f + n))
     int rows_for(int f, int n, int tr) const
     {
@@ -541,8 +544,18 @@ struct GrPlan {
             u.cn_max = std::max(u.cn_max, R.cn);
             ww       = std::max(ww, R.win_w);
         }
-        // resize_sep: bands of up to 32 rows x the window's width (at most 256 lanes of 4 bytes)
-        const int sk  = sep_k(jobs[f].method);
+        // resize_sep: bands of up to 32 rows x the window's width (at most 256 lanes of 4 bytes); resizeArea_
+        // jobs as its INTER_AREA form, K = their most taps per destination index (floor(scale) + 2)
+        int               ka      = 0;
+        static const bool no_area = std::getenv("AEON_HIP_AREA_SEP") && std::atoi(std::getenv("AEON_HIP_AREA_SEP")) == 0;
+        if (jobs[f].method == GR_AREA && !no_area) { // (development: AEON_HIP_AREA_SEP=0, resize_generic)
+            double smax = 1;
+            for (int i = f; i < f + n; i++) smax = std::max({smax, jobs[i].scale_x, jobs[i].scale_y});
+            const int taps = (int)std::floor(smax) + 2;
+            ka             = taps <= 4 ? 4 : taps <= 8 ? 8 : 0;
+        }
+        const int sk  = ka ? ka : sep_k(jobs[f].method);
+        const int xs  = (ka ? 2 : 1) + sk;
         bool      one = sk != 0;
         for (int i = f; i < f + n; i++) one = one && jobs[i].method == jobs[f].method && jobs[i].cn == u.cn_max;
         if (one) {
@@ -554,11 +567,11 @@ struct GrPlan {
             // bytes of room for the replicated borders (resize_kernels.hip kSepPadL)
             auto sw = [&] { return (bytes_for(f, n, cw) + 30 + 15) / 16 * 16 + 32; };
             auto l  = [&] {
-                return ((size_t)(cw + tr) * (1 + sk) * 4 + 15) / 16 * 16 + (size_t)rows_for(f, n, tr) * sw() + lut_lds;
+                return ((size_t)(cw + tr) * xs * 4 + 15) / 16 * 16 + (size_t)rows_for(f, n, tr) * sw() + lut_lds;
             };
             while (l() > kSepLds && tr > 4) tr /= 2;
             if (l() <= kSepLds) {
-                u.sep = sk, u.TR = tr, u.CW = cw, u.NR = rows_for(f, n, tr), u.SW = sw(), u.xs = 1 + sk;
+                u.sep = sk, u.area = ka != 0, u.TR = tr, u.CW = cw, u.NR = rows_for(f, n, tr), u.SW = sw(), u.xs = xs;
                 return u;
             }
         }
@@ -584,14 +597,11 @@ struct GrPlan {
         subs.clear();
         bytes = 0;
         if (jobs.empty()) return;
-        // the classes contiguous: resize_sep's by K, then the generic methods
-        std::stable_sort(jobs.begin(), jobs.end(), [](const ResizeJob& a, const ResizeJob& b) {
-            const int ka = sep_k(a.method), kb = sep_k(b.method);
-            return (ka ? ka : 99) < (kb ? kb : 99);
-        });
+        // the classes contiguous: resize_sep's by K, resizeArea_'s, then the other generic methods
+        std::stable_sort(jobs.begin(), jobs.end(), [](const ResizeJob& a, const ResizeJob& b) { return cls(a.method) < cls(b.method); });
         for (int f = 0; f < (int)jobs.size();) {
             int e = f + 1;
-            while (e < (int)jobs.size() && sep_k(jobs[e].method) == sep_k(jobs[f].method)) e++;
+            while (e < (int)jobs.size() && cls(jobs[e].method) == cls(jobs[f].method)) e++;
             subs.push_back(shape(f, e - f));
             f = e;
         }
@@ -1882,7 +1892,7 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
             const ResizeJob* gj   = (const ResizeJob*)(table + g.off) + u.first;
             const float*     glut = u.any_final ? d_lut : nullptr;
             if (u.sep)
-                HIP_OK(launch_resize_sep(u.sep, gj, table, u.count, u.max_tiles, u.TR, u.CW, u.NR, u.SW, u.cn_max, glut, gbgr,
+                HIP_OK(launch_resize_sep(u.sep, u.area, gj, table, u.count, u.max_tiles, u.TR, u.CW, u.NR, u.SW, u.cn_max, glut, gbgr,
                                          gchm, ctx->call_error, stream));
             else
                 HIP_OK(launch_resize_generic(gj, table, u.count, u.max_tiles, u.TR, u.CW, u.NR, u.xs, u.amax, u.cn_max, u.SW,
