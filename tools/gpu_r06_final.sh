@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-6 closing profile set (profiles/r06f): GPU tests, smoke, the driver's bench command, rocprofv3 kernel
 # stats of the C2 contract run, C3 (one-launch record kernel), C5, the JPEG stage and the C2 workload
-# with CUBIC / AREA / LANCZOS4, then PMC passes + HBM traffic for C2 / C3 / C5.
+# with CUBIC / AREA / LANCZOS4, then PMC passes + HBM traffic for C2 / C3 / C5 and the three resize methods.
 set -o pipefail
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd "$R"; mkdir -p gpurun_out/r06f; export TMPDIR=/tmp
@@ -34,7 +34,7 @@ bash tools/c5_ab.sh pair > $O/c5_steps.txt 2>&1 || exit 1
 fi
 cd "$R"
 [ -n "$SKIP_PMC" ] && exit 0
-for cfg in C2 C3 C5; do
+for cfg in C2 C3 C5 C2:CUBIC C2:AREA C2:LANCZOS4; do
   tools/gpu_pmc.sh $cfg > $O/pmc_$cfg.txt 2>&1 || { echo "pmc $cfg failed"; tail $O/pmc_$cfg.txt; exit 1; }
   python tools/pmc_summary.py gpurun_out/pmc/$cfg $cfg $O/traffic_r06f.json > $O/pmc_${cfg}_summary.txt || exit 1
 done

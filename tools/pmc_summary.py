@@ -31,7 +31,8 @@ if __name__ == "__main__":
             print(f"    {c:28s} {v:16.1f}")
     if len(sys.argv) > 3:
         cfg, out = sys.argv[2], sys.argv[3]
-        main = [k for k in s if "augment_tiles<0," in k or "augment_tilesILi0E" in k or "contrast_records" in k]
+        main = [k for k in s if any(m in k for m in ("augment_tiles<0,", "augment_tilesILi0E", "contrast_records",
+                                                      "resize_sep", "resize_generic", "nearest_staged"))]
         tot = {}
         for k in main:
             cs = s[k]
