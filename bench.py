@@ -890,8 +890,12 @@ def main():
                 _, kt3, _, _ = run_device(A, C, torch, "C3", 1024, 6, 2, 0, 1, args.pool_mib, None, 1)
                 m3, b3, n3 = kt3["augment"]
                 s3 = kt3["stats"]
+                # consecutive batches alternating over two streams (aeon_decoder's two windows): a CU
+                # that finishes its last record starts the next launch's first while the others drain
+                e32, _, _, _ = run_device(A, C, torch, "C3", 1024, st3, 3, 0, 1, args.pool_mib, None, 0, 2)
                 return {"value": 1024 * st3 / e3, "unit": "images/s", "batch": 1024,
                         "ms_per_step": e3 / st3 * 1e3,
+                        "two_streams": {"value": 1024 * st3 / e32, "ms_per_step": e32 / st3 * 1e3},
                         "augment_kernel_avg_launch_ms": m3 / max(n3, 1),
                         "stats_kernel_avg_launch_ms": s3[0] / max(s3[2], 1),
                         "augment_kernel_gbs": b3 / (m3 * 1e-3) / 1e9 if m3 else 0}
@@ -908,8 +912,8 @@ def main():
             side(extra, "two_streams", two_streams)
         side(extra, "C5", lambda: run_c5(A, C, torch, max(20, args.steps), 3, args.pool_mib))
 
-        # aeon's other interpolation methods on the C2 workload: CUBIC / LANCZOS4 as resize_sep bands and
-        # AREA as resize_generic tiles, writing the loader's f32 CHW output themselves (no photometric
+        # aeon's other interpolation methods on the C2 workload: CUBIC / LANCZOS4 / AREA as resize_sep bands
+        # (AREA: its resizeArea_ form and the bilinear emulation), writing the loader's f32 CHW output themselves (no photometric
         # stage in C2); the rate from an untimed run, each kernel kind's time, bytes and HBM fraction
         # from a second run with every launch timed
         def interpolation():
@@ -925,7 +929,7 @@ def main():
                                     "gbs": gbs, "roofline_frac": gbs / HBM_PEAK_GBS}
                 out[m] = {"value": batch * 20 / em, "unit": "images/s", "ms_per_step": em / 20 * 1e3, "kernels": kinds}
             out["what"] = ("C2 workload (batch 256) with interpolation_method set: value from an untimed run; "
-                           "kernels: 'pre' = the resize pass (resize_sep / resize_generic, f32 CHW output), 'augment' = "
+                           "kernels: 'pre' = the resize pass (resize_sep bands, f32 CHW output), 'augment' = "
                            "tile launches of records the resize pass does not take; every launch timed there")
             return out
         side(extra, "interpolation", interpolation)
