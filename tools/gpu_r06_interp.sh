@@ -7,12 +7,12 @@ OUT=gpurun_out/r06; mkdir -p $OUT; T=${1:-x}
 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_hip_resize_methods.py > $OUT/pytest_interp_$T.log 2>&1
 rc=$?; tail -1 $OUT/pytest_interp_$T.log; [ $rc -eq 0 ] || exit $rc
 for round in 1 2; do
-  for v in new noarea prev; do
+  for v in ${VARIANTS:-new noarea prev}; do
     unset AEON_HIP_LIB AEON_HIP_AREA_SEP
-    [ $v = prev ] && export AEON_HIP_LIB=aeon_amd/variants/prev.so
+    [ $v != new ] && [ -f aeon_amd/variants/$v.so ] && export AEON_HIP_LIB=aeon_amd/variants/$v.so
     [ $v = noarea ] && export AEON_HIP_AREA_SEP=0
     echo "== $v" | tee -a $OUT/interp_$T.txt
-    timeout -k 10 200 python tools/interp_steps.py 20 CUBIC,AREA,LANCZOS4 2>&1 | grep -v amdgpu.ids | tee -a $OUT/interp_$T.txt || exit 1
+    timeout -k 10 200 python tools/interp_steps.py 20 ${METHODS:-CUBIC,AREA,LANCZOS4} 2>&1 | grep -v amdgpu.ids | tee -a $OUT/interp_$T.txt || exit 1
   done
 done
 unset AEON_HIP_LIB AEON_HIP_AREA_SEP
