@@ -21,7 +21,10 @@ import bench  # noqa: E402
 from aeon_amd import configs as C  # noqa: E402
 
 torch.cuda.set_device(0)
-bench.run_device(A, C, torch, sys.argv[1] if len(sys.argv) > 1 else "C2", 256, 3, 1, 0, 1, 400, None)
+# TRACE_ISOLATED=1: the traced launch alone (one timed step after a synchronize), else the last of three
+# back-to-back launches
+iso = os.environ.get("TRACE_ISOLATED") == "1"
+bench.run_device(A, C, torch, sys.argv[1] if len(sys.argv) > 1 else "C2", 256, 1 if iso else 3, 2 if iso else 1, 0, 1, 400, None)
 torch.cuda.synchronize()
 t = tr.cpu().numpy().view(np.uint32).reshape(8192, 16, 16).astype(np.int64)
 used = np.nonzero(t[:, 0, 15])[0]
@@ -56,6 +59,8 @@ print("realtime: entry us p0/p50/p90/max %.2f %.2f %.2f %.2f" % (ent_us.min(), n
 print("realtime: exit  us p10/p50/p90/max %.2f %.2f %.2f %.2f" % (np.percentile(ext_us, 10), np.median(ext_us), np.percentile(ext_us, 90), ext_us.max()))
 print("s_memtime ticks per us (median over workgroups): %.0f" % np.median(life_ticks / np.maximum(life_us, 1e-3)))
 wid = used[ok]
+print("entry us p50 by blockIdx eighth: " + " ".join("%.2f" % np.median(ent_us[(wid * 8 // 768) == k]) for k in range(8)))
+print("entries per us:", [int(((ent_us >= b) & (ent_us < b + 1)).sum()) for b in range(int(np.ceil(ent_us.max())) + 1)])
 for xcd in range(8):
     s = wid % 8 == xcd
     print("realtime xcd %d: exit p10/p50/p90/max %.2f %.2f %.2f %.2f" % (xcd, np.percentile(ext_us[s], 10), np.median(ext_us[s]),
