@@ -14,6 +14,7 @@
 #include <mutex>
 #include <stdexcept>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/aeon_hip.h"
@@ -473,12 +474,45 @@ struct GrPlan {
     double bytes = 0; // algorithmic: the source region read once + the window written
 
     size_t n_taps = 0; // Lanczos4 taps reserved by add(), their inputs computed by fill_taps()
+    // One tap array per distinct axis (source size, scale, first destination index, count, column clamp):
+    // a batch of random crops over one output size repeats them (C2: ~76 crop widths, ~76 heights for 512
+    // axes of 256 records), and equal inputs give equal taps.
+    struct LzAxis {
+        int      ssize, d0, n, clamp;
+        uint64_t scale_bits;
+        bool     operator==(const LzAxis& o) const
+        {
+            return ssize == o.ssize && d0 == o.d0 && n == o.n && clamp == o.clamp && scale_bits == o.scale_bits;
+        }
+    };
+    struct LzAxisHash {
+        size_t operator()(const LzAxis& a) const
+        {
+            uint64_t h = a.scale_bits * 0x9E3779B97F4A7C15ull;
+            for (int v : {a.ssize, a.d0, a.n, a.clamp}) h = (h ^ (uint32_t)v) * 0x100000001B3ull;
+            return (size_t)h;
+        }
+    };
+    std::unordered_map<LzAxis, size_t, LzAxisHash> lz_index; // axis -> its first tap
+    std::vector<std::pair<LzAxis, size_t>>          lz_axes;  // (axis, first tap), in reservation order
+    int32_t axis_taps(int ssize, double scale, int d0, int n, bool clamp)
+    {
+        LzAxis a{ssize, d0, n, clamp ? 1 : 0, 0};
+        std::memcpy(&a.scale_bits, &scale, 8);
+        auto it = lz_index.find(a);
+        if (it == lz_index.end()) {
+            it = lz_index.emplace(a, n_taps).first;
+            lz_axes.emplace_back(a, n_taps);
+            n_taps += n;
+        }
+        return (int32_t)(it->second * sizeof(GrTap));
+    }
 
     void add(ResizeJob R)
     {
         if (R.method == GR_LANCZOS4) { // byte offsets, relative until the table is laid out
-            R.coef_x = (int32_t)(n_taps * sizeof(GrTap)), n_taps += R.win_w;
-            R.coef_y = (int32_t)(n_taps * sizeof(GrTap)), n_taps += R.win_h;
+            R.coef_x = axis_taps(R.crop_w, R.scale_x, R.win_x, R.win_w, true);
+            R.coef_y = axis_taps(R.crop_h, R.scale_y, R.win_y, R.win_h, false);
         }
         jobs.push_back(R);
     }
@@ -491,14 +525,13 @@ struct GrPlan {
     void fill_taps(thread_pool* pool, LzIn* lz) const
     {
         auto one = [&](int i) {
-            const ResizeJob& R = jobs[i];
-            if (R.method != GR_LANCZOS4) return;
-            // (coef_x / coef_y: byte offsets of the device-built taps, taps_off onwards)
-            lanczos4_inputs(R.crop_w, R.scale_x, R.win_x, R.win_w, true, lz + (R.coef_x - taps_off) / sizeof(GrTap));
-            lanczos4_inputs(R.crop_h, R.scale_y, R.win_y, R.win_h, false, lz + (R.coef_y - taps_off) / sizeof(GrTap));
+            const LzAxis& a = lz_axes[i].first;
+            double        scale;
+            std::memcpy(&scale, &a.scale_bits, 8);
+            lanczos4_inputs(a.ssize, scale, a.d0, a.n, a.clamp != 0, lz + lz_axes[i].second);
         };
-        if (pool && n_taps > 4096) pool->run((int)jobs.size(), one);
-        else for (int i = 0; i < (int)jobs.size(); i++) one(i);
+        if (pool && n_taps > 4096) pool->run((int)lz_axes.size(), one);
+        else for (int i = 0; i < (int)lz_axes.size(); i++) one(i);
     }
     static int ksize(int m) { return m == GR_CUBIC ? 4 : (m == GR_LANCZOS4 ? 8 : 2); }
     static int sep_k(int m) { return m == GR_CUBIC ? 4 : m == GR_LANCZOS4 ? 8 : m == GR_LINEAR_AREA ? 2 : 0; }
