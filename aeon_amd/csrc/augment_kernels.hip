@@ -24,6 +24,10 @@ namespace aeon_hip {
 
 enum OutForm : int { OF_F32_CHW_VEC = 0, OF_GENERIC = 1 };
 
+#ifndef AEON_HIP_INFO_JOBS // 1: a tile's geometry derived from the job's hot half in SGPRs (0: per-field LDS reads)
+#define AEON_HIP_INFO_JOBS 1
+#endif
+
 // ---- the band kernel -----------------------------------------------------------------------
 // A launch covers n_jobs x max_tiles tiles: tile t = band (t % max_tiles) of job (t / max_tiles),
 // a band being TR consecutive output rows of the job's window.  Workgroups are persistent (the
@@ -68,7 +72,14 @@ struct Bands {
         f.job  = t / a.max_tiles;
         f.band = t - f.job * a.max_tiles;
         f.jl   = jl;
+        // (the job's hot half read at once into scalar registers: the derivation below is on the critical
+        // path of the first tile and of every dynamic-tail tile, and each field's LDS round trip was
+        // waited for before the next)
+#if AEON_HIP_INFO_JOBS
+        const JobS J = job_load(jl);
+#else
         const JobRef J = jref(f);
+#endif
         if (f.band >= JF(J, tiles)) return f;
         if (KM == KM_STATS && JF(J, stats_slot) < 0) return f;
         const int TR = a.rows_per_tile;
