@@ -919,7 +919,8 @@ def main():
         def interpolation():
             out = {}
             for m in ("CUBIC", "AREA", "LANCZOS4"):
-                em, _, _, _ = run_device(A, C, torch, "C2:" + m, batch, 20, 3, 0, 1, args.pool_mib, None, 0)
+                # (10 warmup calls: LANCZOS4's per-thread sin / cos memo warms over the plan pool's threads)
+                em, _, _, _ = run_device(A, C, torch, "C2:" + m, batch, 20, 10, 0, 1, args.pool_mib, None, 0)
                 _, ktm, _, _ = run_device(A, C, torch, "C2:" + m, batch, 20, 3, 0, 1, args.pool_mib, None, 1)
                 kinds = {}
                 for k, (ms, by, n) in ktm.items():
