@@ -75,6 +75,12 @@ CASES = [
     # its column band must stop at 340 (round-5 advisor: columns 336-340 of channel 2 went unwritten)
     ("wide_f32_384", (400, 300), dict(crop_x=5, crop_y=3, crop_w=390, crop_h=160, out_w=384, out_h=40, flip=1), F32),
     ("wide_f32_512", (520, 200), dict(crop_x=2, crop_y=1, crop_w=515, crop_h=64, out_w=512, out_h=64), F32),
+    # resizeArea_ as resize_sep's INTER_AREA form (round 6): K = floor(max scale) + 2 taps -- just under 3
+    # (K = 4), just under 7 (K = 8, zero-padded taps reading past the row), just above 7 (resize_generic)
+    ("area_k4_edge", (320, 320), dict(crop_x=7, crop_y=3, crop_w=299, crop_h=298, out_w=100, out_h=100, flip=1), F32),
+    ("area_k8_edge", (720, 520), dict(crop_x=5, crop_y=9, crop_w=690, crop_h=483, out_w=100, out_h=70), U8_HWC),
+    ("area_k8_f32", (720, 520), dict(crop_x=0, crop_y=0, crop_w=689, crop_h=481, out_w=100, out_h=70, flip=1), F32),
+    ("area_over_k8", (760, 560), dict(crop_x=3, crop_y=2, crop_w=710, crop_h=500, out_w=100, out_h=70), U8_HWC),
 ]
 
 
