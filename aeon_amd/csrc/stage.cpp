@@ -655,6 +655,13 @@ struct GrPlan {
 };
 
 // A resize of the (cropped, padded) region of J's source to its window, into scratch at `off`.
+// (development: AEON_HIP_IDENTITY_SEP=0 keeps identity resizes on the tile kernel)
+bool no_identity_sep()
+{
+    static const bool v = std::getenv("AEON_HIP_IDENTITY_SEP") && std::atoi(std::getenv("AEON_HIP_IDENTITY_SEP")) == 0;
+    return v;
+}
+
 ResizeJob resize_job(const AugJob& J, int method, int isx, int isy)
 {
     ResizeJob R{};
@@ -760,10 +767,19 @@ void plan_image(const aeon_img_desc& d, const void* src_base, const aeon_aug_par
         J.crop_x = 0, J.crop_y = 0;
         J.src_scratch = 1; // relocated to the slot's scratch by the caller
     }
-    int isx = 0, isy = 0;
-    const int gm = is_mask ? -1 : generic_method(J.crop_w, J.crop_h, J.dst_w, J.dst_h, p.interp, cn, &isx, &isy);
-    if (gm >= 0 && gm != GR_AREA_FAST && J.photo == 0 && o.dtype == AEON_DTYPE_F32 && !o.fixed_aspect_ratio &&
-        (cn == 1 || cn == 3) && (o.channels == cn)) {
+    int       isx = 0, isy = 0;
+    int       gm  = is_mask ? -1 : generic_method(J.crop_w, J.crop_h, J.dst_w, J.dst_h, p.interp, cn, &isx, &isy);
+    const bool final_ok = J.photo == 0 && o.dtype == AEON_DTYPE_F32 && !o.fixed_aspect_ratio && (cn == 1 || cn == 3) &&
+                          o.channels == cn;
+    // An identity resize (cv::resize copies) of a CUBIC / LANCZOS4 / INTER_AREA call with no photometric
+    // stage and f32 output: through the call's resize class with identity taps -- (0, 2048, 0, 0), the
+    // fraction-0 Lanczos row, the bilinear emulation's (2048, 0), each reproducing the byte exactly -- so
+    // the call launches no tile kernel for its few uncropped records (an 8.5 us launch per C2:<method>
+    // step: one tile's latency).
+    if (gm < 0 && !is_mask && final_ok && J.crop_w == J.dst_w && J.crop_h == J.dst_h &&
+        (p.interp == AEON_INTERP_CUBIC || p.interp == AEON_INTERP_LANCZOS4 || p.interp == AEON_INTERP_AREA) && !no_identity_sep())
+        gm = p.interp == AEON_INTERP_CUBIC ? GR_CUBIC : p.interp == AEON_INTERP_LANCZOS4 ? GR_LANCZOS4 : GR_LINEAR_AREA;
+    if (gm >= 0 && gm != GR_AREA_FAST && final_ok) {
         // no photometric stage and f32 output: the resize pass is the last one -- it flips,
         // standardizes through the LUT and stores the loader's layout itself (no u8 window in scratch,
         // no copy pass)

@@ -40,6 +40,7 @@ def _assert_same(hip, ref, what):
 
 F32 = dict(channels=3, channel_major=True, bgr_to_rgb=True, dtype="float32", mean=C.MEAN, stddev=C.STDDEV)
 U8_HWC = dict(channels=3, channel_major=False, dtype="uint8")
+F32_HWC = dict(channels=3, channel_major=False, bgr_to_rgb=True, dtype="float32", mean=C.MEAN, stddev=C.STDDEV)
 
 CASES = [
     # (name, src (w, h), params kwargs, out kwargs)
@@ -81,6 +82,12 @@ CASES = [
     ("area_k8_edge", (720, 520), dict(crop_x=5, crop_y=9, crop_w=690, crop_h=483, out_w=100, out_h=70), U8_HWC),
     ("area_k8_f32", (720, 520), dict(crop_x=0, crop_y=0, crop_w=689, crop_h=481, out_w=100, out_h=70, flip=1), F32),
     ("area_over_k8", (760, 560), dict(crop_x=3, crop_y=2, crop_w=710, crop_h=500, out_w=100, out_h=70), U8_HWC),
+    # identity resizes with f32 output and no photometric stage: through the call's resize class with
+    # identity taps (round 6), planes and pixels, flipped, and over add_padding's zero border
+    ("identity_f32", (256, 256), dict(crop_x=16, crop_y=9, crop_w=224, crop_h=224, out_w=224, out_h=224, flip=1), F32),
+    ("identity_hwc", (300, 200), dict(crop_x=3, crop_y=5, crop_w=221, crop_h=150, out_w=221, out_h=150), F32_HWC),
+    ("identity_padded", (40, 30), dict(crop_x=0, crop_y=0, crop_w=40, crop_h=30, out_w=40, out_h=30, padding=6,
+                                       pad_off_x=2, pad_off_y=9, flip=1), F32),
 ]
 
 
@@ -142,9 +149,6 @@ def test_resize_methods_mixed_batch(ctx):
                                    brightness=0.9 if i % 4 == 0 else 1.0))
     out = A.out_desc(item_stride=3 * 224 * 224 * 4, **F32)
     _assert_same(H.hip_records(ctx, imgs, params, out), H.oracle_records(imgs, params, out), "mixed")
-
-
-F32_HWC = dict(channels=3, channel_major=False, bgr_to_rgb=True, dtype="float32", mean=C.MEAN, stddev=C.STDDEV)
 
 
 @pytest.mark.parametrize("method", list(METHODS))
