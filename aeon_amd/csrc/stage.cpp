@@ -473,7 +473,8 @@ struct GrPlan {
     std::vector<Sub> subs;
     double bytes = 0; // algorithmic: the source region read once + the window written
 
-    size_t n_taps = 0; // Lanczos4 taps reserved by add(), their inputs computed by fill_taps()
+    size_t n_taps = 0;     // Lanczos4 taps reserved by add(), their inputs computed by fill_taps()
+    size_t n_taps_max = 0; // ... and what the jobs would need with no axis shared (the ring's sizing bound)
     // One tap array per distinct axis (source size, scale, first destination index, count, column clamp):
     // a batch of random crops over one output size repeats them (C2: ~76 crop widths, ~76 heights for 512
     // axes of 256 records), and equal inputs give equal taps.
@@ -511,6 +512,7 @@ struct GrPlan {
     void add(ResizeJob R)
     {
         if (R.method == GR_LANCZOS4) { // byte offsets, relative until the table is laid out
+            n_taps_max += (size_t)R.win_w + R.win_h;
             R.coef_x = axis_taps(R.crop_w, R.scale_x, R.win_x, R.win_w, true);
             R.coef_y = axis_taps(R.crop_h, R.scale_y, R.win_y, R.win_h, false);
         }
@@ -1813,7 +1815,12 @@ int run_batch(aeon_hip_ctx* ctx, int n, const aeon_img_desc* descs, const void* 
     const float* d_lut = resident_lut(ctx, od, ov.u8_map);
     // job tables, contrast sums and shifts: one capacity for every slot of the ring (a call never
     // allocates unless it needs more than any call before it); scratch per slot, on demand
-    ensure_ring(ctx, table_cap, partial_words * 4, std::max<size_t>(1, pass1_all.jobs.size()) * 4 * sizeof(double));
+    // (sized for the Lanczos4 taps with no axis shared: the shared count varies from call to call, and a
+    // ring growth inside a loader's steady state costs ~10-20 ms of allocations)
+    size_t ring_need = table_cap;
+    for (GrPlan* g : {&gr_short, &gr_main})
+        ring_need += (g->n_taps_max - g->n_taps) * (sizeof(LzIn) + sizeof(GrTap)) + 32;
+    ensure_ring(ctx, ring_need, partial_words * 4, std::max<size_t>(1, pass1_all.jobs.size()) * 4 * sizeof(double));
     if (scratch_bytes > s.scratch_cap) grow(s.scratch, s.scratch_cap, scratch_bytes + scratch_bytes / 4, false); // (slack as ensure_ring)
     for (RotJob& R : rot) R.out_ptr += (uint64_t)s.scratch;
     for (Mask16Job& M : m16)
