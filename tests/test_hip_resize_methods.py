@@ -191,3 +191,17 @@ def test_resize_c2_batch(ctx, method):
         assert any(down) and not all(down), "the batch should mix resizeArea_ and bilinear-emulation records"
     out = A.out_desc(item_stride=3 * 224 * 224 * 4, **F32)
     _assert_same(H.hip_records(ctx, imgs, params, out), H.oracle_records(imgs, params, out), f"{method} C2")
+
+
+@pytest.mark.parametrize("method", list(METHODS))
+def test_resize_shared_axes(ctx, method):
+    """Records sharing crop sizes (LANCZOS4: one tap array per distinct axis, stage.cpp GrPlan::axis_taps)
+    at different crop positions, flips and source images, mixed with a record of another size and an
+    identity record, equal the oracle record by record."""
+    imgs = [A.synthetic_image(80 + i, 300, 260, 3) for i in range(9)]
+    geo = [(0, 0, 250, 200), (30, 40, 250, 200), (49, 59, 250, 200), (7, 3, 250, 180), (10, 12, 224, 224),
+           (3, 3, 250, 200), (50, 60, 250, 200), (11, 5, 190, 230), (2, 9, 250, 200)]
+    params = [A.aug_params(crop_x=x, crop_y=y, crop_w=w, crop_h=h, out_w=224, out_h=224, flip=i % 2,
+                           interp=METHODS[method]) for i, (x, y, w, h) in enumerate(geo)]
+    out = A.out_desc(item_stride=3 * 224 * 224 * 4, **F32)
+    _assert_same(H.hip_records(ctx, imgs, params, out), H.oracle_records(imgs, params, out), f"{method} shared axes")
